@@ -1,0 +1,257 @@
+"""Caller-side data formats: SHA padding, bit arrays, limb chunking, synthetic
+passports and packing of circuit inputs into the flat Fr buffer the C-ABI takes.
+
+Mirrors the input preparation of test/process_passport.js (padding :11-91,
+bigintToArrayString :125-135, getFakeIdenData :628-657, writeToJson :659-672).
+Synthetic workloads follow SURVEY.md §8d (configs 2-4, seeds 0x2-0x4).
+"""
+import hashlib
+
+import numpy as np
+
+from .field import P, SplitMix64, poseidon
+
+# ----------------------------------------------------------- process_passport.js
+def sha_pad(msg: bytes, block_bits=512) -> bytes:
+    """padding() test/process_passport.js:11-91 (0x80, zeros, big-endian bit length)."""
+    bs = block_bits // 8
+    lsz = 8 if block_bits == 512 else 16
+    padlen = (bs - ((len(msg) + 1 + lsz) % bs)) % bs
+    return msg + b"\x80" + b"\x00" * padlen + (8 * len(msg)).to_bytes(lsz, "big")
+
+
+def bits_msb_first(data: bytes):
+    """bytes -> list of 0/1, MSB first per byte (process_passport.js:702-713)."""
+    return np.unpackbits(np.frombuffer(data, dtype=np.uint8)).astype(np.uint8)
+
+
+def chunk_limbs(x: int, n=64, k=32):
+    """bigintToArrayString(n, k, x) process_passport.js:125-135 (little-endian limbs)."""
+    m = (1 << n) - 1
+    return [(x >> (n * i)) & m for i in range(k)]
+
+
+# ------------------------------------------------------------------ RSA (synthetic)
+_SMALL_PRIMES = [p for p in range(3, 2000) if all(p % q for q in range(2, int(p ** 0.5) + 1))]
+
+
+def _is_probable_prime(n, rng):
+    for q in _SMALL_PRIMES:
+        if n % q == 0:
+            return n == q
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for _ in range(16):
+        a = 2 + rng.below(n - 3)
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _gen_prime(bits, rng):
+    while True:
+        c = rng.bits(bits) | (3 << (bits - 2)) | 1
+        if _is_probable_prime(c, rng):
+            return c
+
+
+class RsaKey:
+    def __init__(self, bits, rng, e=65537):
+        while True:
+            p = _gen_prime(bits // 2, rng)
+            q = _gen_prime(bits // 2, rng)
+            if p == q:
+                continue
+            n = p * q
+            phi = (p - 1) * (q - 1)
+            if n.bit_length() != bits or phi % e == 0:
+                continue
+            break
+        self.n, self.e, self.p, self.q = n, e, p, q
+        self.d = pow(e, -1, phi)
+        self.dp, self.dq, self.qinv = self.d % (p - 1), self.d % (q - 1), pow(q, -1, p)
+        self.bits = bits
+
+    def sign_raw(self, m):
+        s1 = pow(m, self.dp, self.p)
+        s2 = pow(m, self.dq, self.q)
+        h = (self.qinv * (s1 - s2)) % self.p
+        return s2 + h * self.q
+
+
+_DIGESTINFO_SHA256 = bytes.fromhex("3031300d060960864801650304020105000420")
+
+
+def pkcs1v15_sha256_sign(key: RsaKey, msg: bytes) -> int:
+    h = hashlib.sha256(msg).digest()
+    k = key.bits // 8
+    t = _DIGESTINFO_SHA256 + h
+    em = b"\x00\x01" + b"\xff" * (k - len(t) - 3) + b"\x00" + t
+    return key.sign_raw(int.from_bytes(em, "big"))
+
+
+# ------------------------------------------------------------- synthetic passports
+CANONICAL = dict(sig=1, dg_hash=256, doc=3, ec_blocks=4, ec_shift=600, dg1_shift=248, aa=1,
+                 dg15_shift=1496, dg15_blocks=3, aa_shift=256)  # hardhat.config.ts:30
+
+_MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789<"
+_DG15_PREFIX = bytes.fromhex("6f81a230819f300d06092a864886f70d010101050003818d00308189028181")
+
+
+def _mrz_dg1(rng):
+    body = bytes(_MRZ[rng.below(len(_MRZ))] for _ in range(88))
+    return bytes.fromhex("615b5f1f58") + body  # TD3 DG1: 93 bytes
+
+
+def _dg15_rsa1024(rng):
+    mod = bytearray(rng.bytes(128))
+    mod[0] |= 0x80
+    # 32-byte DER prefix puts the modulus at bit 256 = AA_SHIFT (identity.circom:34)
+    return _DG15_PREFIX + b"\x00" + bytes(mod) + bytes.fromhex("0203010001")
+
+
+class PassportGen:
+    """Synthetic passports for the canonical instance."""
+
+    def __init__(self, seed=3, n_keys=64, key_bits=2048, params=None):
+        self.rng = SplitMix64(seed)
+        self.params = dict(CANONICAL if params is None else params)
+        self.keys = [RsaKey(key_bits, self.rng) for _ in range(n_keys)]
+        self._pkhash = {}
+
+    def pk_hash(self, key):
+        """RSA pubkey hash = Poseidon5 of 5 x 192-bit limb triples (passportVerificationBuilder.circom:182-191)."""
+        h = self._pkhash.get(key.n)
+        if h is None:
+            a = chunk_limbs(key.n, 64, 15)
+            h = poseidon([(a[3 * i] << 128) + (a[3 * i + 1] << 64) + a[3 * i + 2] for i in range(5)])
+            self._pkhash[key.n] = h
+        return h
+
+    def passport(self, i, smt_depth=0):
+        """Returns dict of raw fields for passport i (bytes + ints)."""
+        pr = self.params
+        rng = self.rng
+        key = self.keys[i % len(self.keys)]
+        dg1 = _mrz_dg1(rng)
+        dg15 = _dg15_rsa1024(rng)
+        ec_len = 219 + rng.below(pr["ec_blocks"] * 64 - 9 - 219 + 1)
+        ec = bytearray(rng.bytes(ec_len))
+        h1, h15 = hashlib.sha256(dg1).digest(), hashlib.sha256(dg15).digest()
+        d1 = pr["dg1_shift"] // 8
+        ec[d1 - 7:d1] = bytes.fromhex("30250201010420")
+        ec[d1:d1 + 32] = h1
+        d15 = pr["dg15_shift"] // 8
+        ec[d15 - 7:d15] = bytes.fromhex("302502010f0420")
+        ec[d15:d15 + 32] = h15
+        ec = bytes(ec)
+        sa_shift = pr["ec_shift"] // 8
+        sa_len = sa_shift + 32 + rng.below(119 - (sa_shift + 32) + 1)
+        sa = bytearray(rng.bytes(sa_len))
+        sa[sa_shift - 2:sa_shift] = b"\x04\x20"
+        sa[sa_shift:sa_shift + 32] = hashlib.sha256(ec).digest()
+        sa = bytes(sa)
+        sig = pkcs1v15_sha256_sign(key, sa)
+        sk = int.from_bytes(hashlib.sha256(ec).digest()[:31], "big")  # getFakeIdenData :630
+        pkh = self.pk_hash(key)
+        siblings = [0] * 80
+        if smt_depth:
+            for k in range(smt_depth):
+                v = 0
+                while v == 0:
+                    v = rng.fr()
+                siblings[k] = v
+            root = None  # computed by the caller (config 4); not enforced by the circuit
+        else:
+            root = poseidon([pkh, pkh, 1])  # getFakeIdenData :654
+        return dict(dg1=dg1, dg15=dg15, ec=ec, sa=sa, sig=sig, n=key.n, sk=sk, root=root,
+                    siblings=siblings, pk_hash=pkh)
+
+
+def passport_json(pp, params=CANONICAL):
+    """The reference's input JSON (writeToJson, process_passport.js:659-672)."""
+    K = 64 if params["sig"] == 2 else 32
+
+    def bits(b, nbits):
+        arr = bits_msb_first(sha_pad(b, 512))
+        assert len(arr) == nbits, (len(arr), nbits)
+        return [str(int(x)) for x in arr]
+
+    return {
+        "dg1": bits(pp["dg1"], 1024),
+        "dg15": bits(pp["dg15"], params["dg15_blocks"] * 512),
+        "signedAttributes": bits(pp["sa"], 1024),
+        "encapsulatedContent": bits(pp["ec"], params["ec_blocks"] * 512),
+        "pubkey": [str(x) for x in chunk_limbs(pp["n"], 64, K)],
+        "signature": [str(x) for x in chunk_limbs(pp["sig"], 64, K)],
+        "skIdentity": hex(pp["sk"]),
+        "slaveMerkleRoot": hex(pp["root"] or 0),
+        "slaveMerkleInclusionBranches": [str(x) for x in pp["siblings"]],
+    }
+
+
+def pack_register_inputs(pp, params=CANONICAL, out=None):
+    """Flat input buffer in witness order: slaveMerkleRoot, encapsulatedContent, dg1, dg15,
+    signedAttributes, signature, pubkey, slaveMerkleInclusionBranches, skIdentity
+    (registerIdentityBuilder.circom:143-152, public input first). -> (nIn, 32) uint8."""
+    K = 64 if params["sig"] == 2 else 32
+    ecL, d15L = params["ec_blocks"] * 512, params["dg15_blocks"] * 512
+    n_in = 1 + ecL + 1024 + d15L + 1024 + 2 * K + 80 + 1
+    buf = out if out is not None else np.zeros((n_in, 32), dtype=np.uint8)
+    buf[:] = 0
+    o = 0
+
+    def put_int(v):
+        nonlocal o
+        buf[o] = np.frombuffer(int(v % P).to_bytes(32, "little"), dtype=np.uint8)
+        o += 1
+
+    def put_bits(b, nbits):
+        nonlocal o
+        arr = bits_msb_first(sha_pad(b, 512))
+        if len(arr) != nbits:
+            raise ValueError("padded length %d != %d bits" % (len(arr), nbits))
+        buf[o:o + nbits, 0] = arr
+        o += nbits
+
+    def put_u64s(vals):
+        nonlocal o
+        for v in vals:
+            buf[o, :8] = np.frombuffer(int(v).to_bytes(8, "little"), dtype=np.uint8)
+            o += 1
+
+    put_int(pp["root"] or 0)
+    put_bits(pp["ec"], ecL)
+    put_bits(pp["dg1"], 1024)
+    put_bits(pp["dg15"], d15L)
+    put_bits(pp["sa"], 1024)
+    put_u64s(chunk_limbs(pp["sig"], 64, K))
+    put_u64s(chunk_limbs(pp["n"], 64, K))
+    for s in pp["siblings"]:
+        put_int(s)
+    put_int(pp["sk"])
+    assert o == n_in
+    return buf
+
+
+def sha256_config2_batch(batch, seed=2, blocks=6):
+    """Config 2: messages of L in [312,375] bytes, padded to 6 blocks; -> (msgs, (batch, 3072, 32) uint8)."""
+    rng = SplitMix64(seed)
+    lo, hi = 64 * (blocks - 1) - 8, 64 * blocks - 9
+    out = np.zeros((batch, 512 * blocks, 32), dtype=np.uint8)
+    msgs = []
+    for b in range(batch):
+        L = lo + rng.below(hi - lo + 1)
+        m = rng.bytes(L)
+        msgs.append(m)
+        out[b, :, 0] = bits_msb_first(sha_pad(m, 512))
+    return msgs, out

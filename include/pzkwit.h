@@ -1,0 +1,135 @@
+/* pzkwit.h — C-ABI of the MI355X batched witness generator (libpzkwit.so).
+ *
+ * Drop-in boundary for the witness-calculation surface of the reference:
+ *   - circom's generated witness calculator, used by circom_tester
+ *     (test/automatisationTest.js:37-51: wasm_tester -> circuit.calculateWitness(input, true))
+ *     and by generate_witness.js (circuits/scripts/gen-witness.sh:25 -> calculateWTNSBin);
+ *   - the per-input serial loop of test/automatisationTest.js:24, replaced by one batched call.
+ * The JS binding (passport-zk-circuits_amd/js, Node N-API) and the Python binding
+ * (passport-zk-circuits_amd/pzkwit) sit on top of these entry points; INTEGRATION.md shows
+ * the bindings a maintainer adds.
+ *
+ * Conventions: plain pointers and sizes; every function returns 0 on success or a negative
+ * PZK_E_* code, with a message in pzk_last_error() (thread-local). Caller owns all input and
+ * output buffers; the instance owns its device scratch. One in-flight call per instance.
+ * Field elements are 32 bytes, little-endian, NORMAL form (< p), as in a .wtns file.
+ */
+#ifndef PZKWIT_H
+#define PZKWIT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* circuit families (the `component main` the instance evaluates) */
+enum {
+  PZK_CIRCUIT_REGISTER = 0, /* RegisterIdentityBuilder(...)  registerIdentityBuilder.circom:41 */
+  PZK_CIRCUIT_POSEIDON = 1, /* PoseidonHash(n)               poseidon.circom:214 (config 1) */
+  PZK_CIRCUIT_SHA256 = 2    /* Sha256HashChunks(blocks)      sha256HashChunks.circom:8 (config 2) */
+};
+
+/* Template parameters of RegisterIdentityBuilder (registerIdentityBuilder.circom:41-52),
+ * verbatim, plus the circuit family and its size argument for the standalone circuits. */
+typedef struct pzk_params {
+  int32_t circuit;            /* PZK_CIRCUIT_* */
+  int32_t size_arg;           /* n for POSEIDON, blocks for SHA256; ignored for REGISTER */
+  int32_t signature_type;     /* SIGNATURE_TYPE (1 = RSA-2048/SHA-256/65537, 2 = RSA-4096) */
+  int32_t dg_hash_type;       /* DG_HASH_TYPE (256) */
+  int32_t document_type;      /* DOCUMENT_TYPE (1 = TD1, 3 = TD3) */
+  int32_t ec_block_number;    /* EC_BLOCK_NUMBER */
+  int32_t ec_shift;           /* EC_SHIFT (bits) */
+  int32_t dg1_shift;          /* DG1_SHIFT (bits) */
+  int32_t aa_signature_algo;  /* AA_SIGNATURE_ALGO (0 = none, 1 = RSA-1024) */
+  int32_t dg15_shift;         /* DG15_SHIFT (bits) */
+  int32_t dg15_block_number;  /* DG15_BLOCK_NUMBER */
+  int32_t aa_shift;           /* AA_SHIFT (bits) */
+} pzk_params;
+
+typedef struct pzk_info {
+  uint64_t witness_size;   /* number of field elements per witness (wtns section 2 / 32) */
+  uint64_t n_inputs;       /* number of input signals (flat input buffer length / 32) */
+  uint32_t n_outputs;      /* main outputs (witness[1 .. n_outputs]) */
+  uint32_t n_public_inputs;/* public inputs, right after the outputs */
+  uint32_t n_input_groups; /* named input signals (see pzk_instance_input) */
+  uint32_t reserved;
+} pzk_info;
+
+typedef struct pzk_exec {
+  int32_t device;   /* HIP device ordinal */
+  int32_t flags;    /* PZK_EXEC_* */
+  void* stream;     /* hipStream_t to launch on (NULL = the instance's own stream) */
+} pzk_exec;
+
+enum { PZK_EXEC_SYNC = 1 /* synchronise the stream before returning */ };
+
+/* lane status codes: 0 = OK, else the first failing `===` site (reference file:line) */
+enum {
+  PZK_ST_OK = 0,
+  PZK_ST_NUM2BITS = 1,    /* bitify.circom:26 */
+  PZK_ST_ALIAS = 2,       /* aliascheck.circom:14 */
+  PZK_ST_ISZERO = 3,      /* comparators.circom:20 */
+  PZK_ST_LASTBIT = 4,     /* int/arithmetic.circom:169-170 */
+  PZK_ST_LASTNBITS = 5,   /* int/arithmetic.circom:203 */
+  PZK_ST_BITS2 = 6,       /* sha2Common.circom:65-68 */
+  PZK_ST_FLOW = 7,        /* passportVerificationBuilder.circom:155 */
+  PZK_ST_RSA_HASH = 8,    /* rsa.circom:48 */
+  PZK_ST_RSA_PREFIX = 9,  /* rsa.circom:53-54 */
+  PZK_ST_RSA_PAD = 10,    /* rsa.circom:57-71 */
+  PZK_ST_BIGMOD_GT = 11,  /* bigInt.circom:245 */
+  PZK_ST_BIGISZERO = 12,  /* bigIntComparators.circom:128 */
+  PZK_ST_SMT_LAST = 13,   /* SMTVerifier.circom:54 */
+  PZK_ST_BJJ_ADD = 14,    /* babyjubjub/curve.circom:98,102 */
+  PZK_ST_INPUT_RANGE = 64 /* an input outside the domain the GPU path evaluates (e.g. a non-bit
+                             SHA input, a limb >= 2^64); see DESIGN.md §5 */
+};
+
+enum {
+  PZK_E_ARG = -1,       /* invalid argument */
+  PZK_E_PARAMS = -2,    /* unsupported template parameters */
+  PZK_E_HIP = -3,       /* HIP runtime error */
+  PZK_E_NOMEM = -4,     /* device allocation failed */
+  PZK_E_DATA = -5,      /* Poseidon parameter file missing/corrupt */
+  PZK_E_NODEVICE = -6   /* no HIP device: the library never falls back to a CPU path */
+};
+
+typedef struct pzk_instance pzk_instance;
+
+/* Replaces: circom compile + WitnessCalculator builder(wasm) — witness_calculator.js builder(). */
+int pzk_instance_create(const pzk_params* params, pzk_instance** out);
+void pzk_instance_destroy(pzk_instance* inst);
+
+/* Replaces: wc.witnessSize / wc.n32 / wc.prime fields and getInputSignalSize(fnv(name)). */
+int pzk_instance_info(const pzk_instance* inst, pzk_info* info);
+/* i-th named input signal, in flat-input order: name, element offset and length. */
+int pzk_instance_input(const pzk_instance* inst, uint32_t i, const char** name, uint64_t* offset,
+                       uint64_t* length);
+
+/* The 76-byte .wtns header (wtns v2, 2 sections, n8 = 32, prime, witnessSize) that
+ * calculateWTNSBin prepends. */
+int pzk_wtns_header(const pzk_instance* inst, uint8_t header[76]);
+
+/* Batched witness calculation on device buffers (inputs resident in HBM).
+ *   d_inputs : batch x n_inputs x 32 B (normal form), device pointer
+ *   d_wtns   : batch x witness_size x 32 B elements, row stride wtns_stride bytes (>= 32*witness_size,
+ *              multiple of 16), device pointer
+ *   d_status : batch x int32 lane status (PZK_ST_*), device pointer (may be NULL)
+ * Replaces: for (input of inputs) await wc.calculateWitness(input) (automatisationTest.js:24-50). */
+int pzk_witness_batch(pzk_instance* inst, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns,
+                      size_t wtns_stride, int32_t* d_status, const pzk_exec* exec);
+
+/* Host-buffer convenience (copies in/out; used by the single-input calculateWitness path). */
+int pzk_witness_batch_host(pzk_instance* inst, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
+                           int32_t* h_status, const pzk_exec* exec);
+
+/* Reason for the last failure on this thread. */
+const char* pzk_last_error(void);
+
+/* Library version string. */
+const char* pzk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

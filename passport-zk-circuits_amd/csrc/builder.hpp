@@ -1,0 +1,42 @@
+// Host-side layout builder: walks the template tree of an instance (at region granularity)
+// and produces the region table, the per-kernel work lists, the SHA jobs, the Poseidon task
+// DAG and the value-store map. Pure host C++.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/pzkwit.h"
+#include "kernels.hpp"
+#include "layout.hpp"
+
+namespace pzk {
+
+struct InputGroup {
+  std::string name;
+  uint64_t offset, length;
+};
+
+struct Layout {
+  uint64_t wit_size = 0, n_inputs = 0;
+  uint32_t n_outputs = 0, n_public = 0;
+  std::vector<InputGroup> inputs;
+  std::vector<Region> regions;
+  std::vector<Work> work_sha, work_pos, work_gen;
+  std::vector<ShaJob> sha;
+  uint32_t sha_core_words = 0;
+  std::vector<PosTask> pos;            // sorted by level, then t
+  std::vector<uint32_t> pos_level_start;
+  uint32_t pos_core_elems = 0;
+  int max_t = 2;
+  uint32_t n_values = 0;
+  std::vector<ValueLoad> loads;
+};
+
+bool build_layout(const pzk_params& p, Layout& L, std::string& why);
+
+// chunk size of one emit workgroup (signals)
+constexpr uint32_t EMIT_CHUNK = 4096;
+
+}  // namespace pzk

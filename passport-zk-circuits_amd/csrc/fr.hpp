@@ -1,0 +1,174 @@
+// BN254 scalar field Fr on gfx950: 8 x 32-bit limbs, Montgomery form (R = 2^256).
+//
+// The witness is exported in NORMAL form (the .wtns contract); values
+// that are Fr products are carried in Montgomery form inside the core kernels and
+// converted once, in the emit kernels, right before the 32-byte store.
+//
+// Multiplication is CIOS with the "no final carry" shortcut that is valid because the
+// top word of p (0x30644e72) is < (2^32-1)/2 - 1: each step is one v_mad_u64_u32
+// (32x32 + 64 -> 64) per limb product. p < 2^254 also lets additions skip the
+// 257th bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pzk {
+
+struct fr { uint32_t v[8]; };
+
+constexpr uint32_t P_[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                                 0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+// R^2 mod p
+constexpr uint32_t R2_[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                                  0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+// R mod p (Montgomery one)
+constexpr uint32_t R1_[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                                  0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+constexpr uint32_t PINV = 0xefffffffu;  // -p^-1 mod 2^32
+
+__device__ __forceinline__ fr fr_zero() { fr r; for (int i = 0; i < 8; i++) r.v[i] = 0; return r; }
+__device__ __forceinline__ fr fr_u64(uint64_t x) {
+  fr r = fr_zero(); r.v[0] = (uint32_t)x; r.v[1] = (uint32_t)(x >> 32); return r;
+}
+__device__ __forceinline__ fr fr_const(const uint32_t (&c)[8]) { fr r; for (int i = 0; i < 8; i++) r.v[i] = c[i]; return r; }
+__device__ __forceinline__ fr fr_mont_one() { return fr_const(R1_); }
+
+__device__ __forceinline__ bool fr_is_zero(const fr& a) {
+  uint32_t o = 0; for (int i = 0; i < 8; i++) o |= a.v[i]; return o == 0;
+}
+__device__ __forceinline__ bool fr_eq(const fr& a, const fr& b) {
+  uint32_t o = 0; for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i]; return o == 0;
+}
+
+// r = a - p if a >= p (a < 2p)
+__device__ __forceinline__ fr fr_reduce_once(const fr& a) {
+  fr t; uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a.v[i] - P_[i] - br;
+    t.v[i] = (uint32_t)d; br = (d >> 32) & 1;
+  }
+  return br ? a : t;
+}
+
+__device__ __forceinline__ fr fr_add(const fr& a, const fr& b) {
+  fr r; uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)a.v[i] + b.v[i] + c; r.v[i] = (uint32_t)s; c = s >> 32; }
+  return fr_reduce_once(r);
+}
+
+__device__ __forceinline__ fr fr_sub(const fr& a, const fr& b) {
+  fr r; uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t d = (uint64_t)a.v[i] - b.v[i] - br; r.v[i] = (uint32_t)d; br = (d >> 32) & 1; }
+  if (br) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)r.v[i] + P_[i] + c; r.v[i] = (uint32_t)s; c = s >> 32; }
+  }
+  return r;
+}
+
+__device__ __forceinline__ fr fr_neg(const fr& a) { return fr_sub(fr_zero(), a); }
+
+// Montgomery product a*b*2^-256 mod p
+__device__ __forceinline__ fr fr_mul(const fr& a, const fr& b) {
+  uint32_t t[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a.v[0] * b.v[i] + t[0];
+    uint32_t C = (uint32_t)(s >> 32);
+    uint32_t t0 = (uint32_t)s;
+    uint32_t m = t0 * PINV;
+    uint64_t s2 = (uint64_t)m * P_[0] + t0;
+    uint32_t C2 = (uint32_t)(s2 >> 32);
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      s = (uint64_t)a.v[j] * b.v[i] + t[j] + C;
+      C = (uint32_t)(s >> 32);
+      s2 = (uint64_t)m * P_[j] + (uint32_t)s + C2;
+      C2 = (uint32_t)(s2 >> 32);
+      t[j - 1] = (uint32_t)s2;
+    }
+    t[7] = C + C2;
+  }
+  fr r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = t[j];
+  return fr_reduce_once(r);
+}
+
+__device__ __forceinline__ fr fr_sqr(const fr& a) { return fr_mul(a, a); }
+__device__ __forceinline__ fr fr_to_mont(const fr& a) { return fr_mul(a, fr_const(R2_)); }
+__device__ __forceinline__ fr fr_from_mont(const fr& a) { fr one = fr_zero(); one.v[0] = 1; return fr_mul(a, one); }
+
+// a^(p-2) in Montgomery form; inverse of 0 is 0 (IsZero semantics, comparators.circom:17)
+__device__ __forceinline__ fr fr_inv(const fr& a) {
+  // exponent p-2, scanned MSB->LSB with a 4-bit fixed window (wave-uniform control flow)
+  constexpr uint32_t E[8] = {0xefffffffu, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                             0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  fr tbl[16];
+  tbl[0] = fr_mont_one();
+  tbl[1] = a;
+#pragma unroll
+  for (int i = 2; i < 16; i++) tbl[i] = fr_mul(tbl[i - 1], a);
+  fr r = fr_mont_one();
+  bool started = false;
+  for (int w = 63; w >= 0; w--) {
+    uint32_t nib = (E[w >> 3] >> ((w & 7) * 4)) & 15u;
+    if (started) { r = fr_sqr(r); r = fr_sqr(r); r = fr_sqr(r); r = fr_sqr(r); }
+    if (nib) {
+      // select tbl[nib] without dynamic indexing into a register array
+      fr s = tbl[0];
+#pragma unroll
+      for (int q = 1; q < 16; q++) if ((uint32_t)q == nib) s = tbl[q];
+      r = started ? fr_mul(r, s) : s;
+      started = true;
+    }
+  }
+  return r;
+}
+
+// Batch inversion (Montgomery's trick) over n values in a caller-provided array.
+// x[i] := x[i]^-1 (0 stays 0); scratch must hold n elements.
+template <typename Acc>
+__device__ __forceinline__ void fr_batch_inv(Acc x, Acc scratch, int n) {
+  fr acc = fr_mont_one();
+  for (int i = 0; i < n; i++) {
+    fr xi = x(i);
+    scratch(i) = acc;
+    if (!fr_is_zero(xi)) acc = fr_mul(acc, xi);
+  }
+  fr inv = fr_inv(acc);
+  for (int i = n - 1; i >= 0; i--) {
+    fr xi = x(i);
+    if (!fr_is_zero(xi)) {
+      fr r = fr_mul(inv, scratch(i));
+      inv = fr_mul(inv, xi);
+      x(i) = r;
+    }
+  }
+}
+
+// 32-byte normal-form store of a small non-negative integer
+__device__ __forceinline__ void store_u64(uint8_t* dst, uint64_t v) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+  d[1] = make_uint4(0u, 0u, 0u, 0u);
+}
+__device__ __forceinline__ void store_fr(uint8_t* dst, const fr& a) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+__device__ __forceinline__ fr load_fr(const uint8_t* src) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4 a = s[0], b = s[1];
+  fr r; r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w; r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+}  // namespace pzk

@@ -1,0 +1,213 @@
+// Device kernels of the witness generator (unity build: every device header is included
+// here; the host runtime in runtime.cpp launches them through the launch_* wrappers).
+#include <hip/hip_runtime.h>
+
+#include "poseidon.hpp"
+#include "sha.hpp"
+#include "kernels.hpp"
+
+namespace pzk {
+
+constexpr int EMIT_THREADS = 256;
+
+// ------------------------------------------------------------------- value loads
+// value-store slot <- input element (normal form -> Montgomery)
+__global__ void k_load_values(const ValueLoad* loads, int n_loads, const uint8_t* inputs, uint64_t n_inputs,
+                              fr* values, uint32_t batch) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  int l = blockIdx.y;
+  if (w >= batch || l >= n_loads) return;
+  ValueLoad ld = loads[l];
+  fr x = load_fr(inputs + 32ull * ((uint64_t)w * n_inputs + ld.in_off));
+  values[(size_t)ld.slot * batch + w] = fr_to_mont(x);
+}
+
+// ------------------------------------------------------------------- SHA core
+__global__ void k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs, uint64_t n_inputs,
+                           uint32_t* sha_core, uint32_t core_words, int32_t* status, uint32_t batch) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  int j = blockIdx.y;
+  if (w >= batch || j >= n_jobs) return;
+  sha_core_lane(inputs + 32ull * (uint64_t)w * n_inputs, jobs[j], sha_core + (size_t)w * core_words,
+                status ? status + w : nullptr);
+}
+
+// ------------------------------------------------------------------- Poseidon core
+template <int T>
+__global__ void k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= vs.batch) return;
+  const PosTask& task = tasks[blockIdx.y];
+  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
+}
+
+// ------------------------------------------------------------------- emit: SHA regions
+__device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t* H /* (B+1)*8 in LDS */,
+                                                const uint8_t* in_row, uint32_t s, bool& is_copy, uint64_t& src) {
+  const int B = R.a[1];
+  const uint32_t inLen = 512u * B;
+  is_copy = false;
+  if (R.a[3]) {  // ShaHashChunks wrapper: out[256] | in[512B]
+    if (s < 256) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
+    s -= 256;
+    if (s < inLen) { is_copy = true; src = (uint64_t)R.a[2] + s; return 0; }
+    s -= inLen;
+  }
+  if (s < 256) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
+  s -= 256;
+  if (s < inLen) { is_copy = true; src = (uint64_t)R.a[2] + s; return 0; }
+  s -= inLen;
+  if (s < 256u * (B + 1)) { uint32_t m = s >> 8, j = (s >> 5) & 7, i = s & 31; return (H[m * 8 + j] >> i) & 1; }
+  s -= 256u * (B + 1);
+  return (SHA_IV[s >> 5] >> (s & 31)) & 1;
+}
+
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
+                                                          const uint32_t* sha_core, uint8_t* wtns, size_t stride) {
+  __shared__ uint32_t core[SHA_BLOCK_CORE + 8 * 17];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const ShaJob job = L.sha[R.a[0]];
+  const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
+  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  if (R.kind == RK_SHA_BLOCK) {
+    const uint32_t* bc = wc + R.a[1] * SHA_BLOCK_CORE;
+    for (int i = threadIdx.x; i < SHA_BLOCK_CORE; i += blockDim.x) core[i] = bc[i];
+    __syncthreads();
+    ShaBlk B{core};
+    for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) store_u64(out + 32ull * q, sha_block_sig(B, wk.start + q));
+  } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)
+    const int Bn = R.a[1];
+    for (int i = threadIdx.x; i < 8 * (Bn + 1); i += blockDim.x) {
+      int m = i >> 3, j = i & 7;
+      core[i] = m < Bn ? wc[m * SHA_BLOCK_CORE + j] : wc[Bn * SHA_BLOCK_CORE + j];
+    }
+    __syncthreads();
+    const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+    for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+      bool cp; uint64_t src = 0;
+      uint64_t v = sha_own_sig(R, core, in_row, wk.start + q, cp, src);
+      if (cp) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(in_row + 32ull * src);
+        uint4* d4 = reinterpret_cast<uint4*>(out + 32ull * q);
+        d4[0] = s4[0]; d4[1] = s4[1];
+      } else {
+        store_u64(out + 32ull * q, v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------- emit: Poseidon
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
+                                                          const fr* pos_core, uint8_t* wtns, size_t stride) {
+  extern __shared__ fr lds[];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const PosTask task = L.pos[R.a[0]];
+  const int n = task.n, t = n + 1;
+  PosLds P;
+  pos_lds_carve(P, lds, t);
+  for (int i = 0; i < n; i++) P.inputs[i] = vs.at(task.in_slot[i], w);
+  P.hash = vs.at(task.out_slot, w);
+  pos_lds_fill(P, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off);
+  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x)
+    store_fr(out + 32ull * q, fr_from_mont(pos_block_sig(P, n, wk.start + q)));
+}
+
+// ------------------------------------------------------------------- emit: generic
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, const uint8_t* inputs,
+                                                          ValueStore vs, uint8_t* wtns, size_t stride) {
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint32_t s = wk.start + q;
+    uint4* d4 = reinterpret_cast<uint4*>(out + 32ull * q);
+    switch (R.kind) {
+      case RK_ONE: store_u64(out + 32ull * q, 1); break;
+      case RK_INCOPY: {
+        const uint4* s4 = reinterpret_cast<const uint4*>(in_row + 32ull * ((uint64_t)R.a[0] + s));
+        d4[0] = s4[0]; d4[1] = s4[1];
+        break;
+      }
+      case RK_VALUE: store_fr(out + 32ull * q, fr_from_mont(vs.at(R.a[0] + (int)s, w))); break;
+      default: break;
+    }
+  }
+}
+
+// ------------------------------------------------------------------- launchers
+#define HIP_TRY(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inputs, uint64_t n_inputs, fr* values,
+                              uint32_t batch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 g((batch + 63) / 64, n);
+  hipLaunchKernelGGL(k_load_values, g, dim3(64), 0, st, loads, n, inputs, n_inputs, values, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* sha_core, int32_t* status,
+                           uint32_t batch, hipStream_t st) {
+  if (L.n_sha == 0) return hipSuccess;
+  dim3 g((batch + 63) / 64, L.n_sha);
+  hipLaunchKernelGGL(k_sha_core, g, dim3(64), 0, st, L.sha, (int)L.n_sha, inputs, L.n_inputs, sha_core,
+                     L.sha_core_words, status, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
+                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, hipStream_t st) {
+  // group consecutive tasks of equal t into one launch (blockIdx.y = task)
+  uint32_t i = 0;
+  while (i < count) {
+    int t = h_tasks[first + i].n + 1;
+    uint32_t j = i;
+    while (j < count && h_tasks[first + j].n + 1 == t) j++;
+    dim3 g((vs.batch + 63) / 64, j - i);
+    const PosTask* tp = d_tasks + first + i;
+    switch (t) {
+      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      default: return hipErrorInvalidValue;
+    }
+    HIP_TRY(hipGetLastError());
+    i = j;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_emit_sha(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
+                           const uint32_t* sha_core, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_emit_sha, dim3(n_work, batch), dim3(EMIT_THREADS), 0, st, L, work, inputs, sha_core, wtns,
+                     stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, ValueStore vs,
+                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch, int max_t, hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  size_t lds = sizeof(fr) * (size_t)pos_lds_elems(max_t);
+  hipLaunchKernelGGL(k_emit_pos, dim3(n_work, batch), dim3(EMIT_THREADS), lds, st, L, work, K, vs, pos_core, wtns,
+                     stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit_gen(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
+                           ValueStore vs, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_emit_gen, dim3(n_work, batch), dim3(EMIT_THREADS), 0, st, L, work, inputs, vs, wtns, stride);
+  return hipGetLastError();
+}
+
+}  // namespace pzk

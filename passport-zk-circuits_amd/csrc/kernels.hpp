@@ -1,0 +1,32 @@
+// Launch wrappers shared between kernels.hip (device code) and runtime.cpp (host runtime).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fr.hpp"
+#include "layout.hpp"
+
+namespace pzk {
+
+struct ValueLoad {
+  int32_t slot;    // value-store slot
+  int32_t in_off;  // input element offset
+};
+
+struct PosConsts;
+struct ValueStore;
+
+hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inputs, uint64_t n_inputs, fr* values,
+                              uint32_t batch, hipStream_t st);
+hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* sha_core, int32_t* status,
+                           uint32_t batch, hipStream_t st);
+hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
+                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, hipStream_t st);
+hipError_t launch_emit_sha(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
+                           const uint32_t* sha_core, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st);
+hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, ValueStore vs,
+                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch, int max_t, hipStream_t st);
+hipError_t launch_emit_gen(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
+                           ValueStore vs, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st);
+
+}  // namespace pzk

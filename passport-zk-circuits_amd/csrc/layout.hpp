@@ -1,0 +1,110 @@
+// Instance layout: where every template instance's signals live in the witness, and the
+// work lists the kernels run over. Built once per instance on the host (layout.cpp),
+// uploaded to the device, shared by every batch.
+//
+// Witness numbering: witness[0] = 1, then the main component; each
+// component instance is one contiguous block = its own signals (outputs, inputs,
+// intermediates, each in declaration order) followed by its subcomponents' blocks in
+// creation order. The layout is data-driven: a region table, not hard-coded offsets.
+#pragma once
+#include <stdint.h>
+
+namespace pzk {
+
+// lane status codes (mirror include/pzkwit.h PZK_ST_*)
+constexpr int32_t ST_NUM2BITS = 1, ST_ALIAS = 2, ST_ISZERO = 3, ST_FLOW = 7, ST_RSA_HASH = 8,
+                  ST_RSA_PREFIX = 9, ST_RSA_PAD = 10, ST_BIGMOD_GT = 11, ST_BIGISZERO = 12,
+                  ST_SMT_LAST = 13, ST_INPUT_RANGE = 64;
+
+// ---- emit regions: a contiguous run of witness signals with one closed-form generator
+enum RegionKind : uint32_t {
+  RK_ONE = 0,        // witness[0] = 1
+  RK_INCOPY = 1,     // a0 = input element offset: w[off+i] = in[a0+i]
+  RK_SHA_OWN = 2,    // ShaHashChunks wrapper (a3) + Sha256HashChunks own signals + iv;
+                     //   a0 = sha slot, a1 = blocks, a2 = input element offset of the bits, a3 = wrapper
+  RK_SHA_BLOCK = 3,  // Sha2_224_256Shedule + Sha2_224_256Rounds(64) of one block; a0 = sha slot, a1 = block
+  RK_POSEIDON = 4,   // PoseidonHash(n) block; a0 = poseidon task, a1 = n
+  RK_MODMUL = 5,     // BigMultModP(64,K,K,K); a0 = modmul index
+  RK_VALUE = 6,      // w[off+i] = value-store slot a0+i (normal-form conversion)
+  RK_BITS2NUM = 7,   // Bits2Num(L) over bits taken from a bit source; a0 = L, a1 = bit source id,
+                     //   a2 = first bit, a3 = stride(+1/-1), a4 = alias-check flag
+  RK_NUM2BITS = 8,   // Num2Bits(L) of a value-store slot; a0 = L, a1 = slot
+  RK_MISC = 9,       // small irregular templates, a0 = sub-kind (see kernels)
+  RK_COUNT
+};
+
+struct Region {
+  uint64_t off;   // witness element offset
+  uint32_t len;   // number of signals
+  uint32_t kind;  // RegionKind
+  int32_t a[6];
+};
+
+// one workgroup's slice of a region
+struct Work {
+  uint32_t region;
+  uint32_t start;
+  uint32_t count;
+  uint32_t pad;
+};
+
+// SHA hasher job: one (witness, hasher) lane of the SHA core kernel
+struct ShaJob {
+  int32_t in_off;   // input element offset of the first message bit
+  int32_t blocks;   // number of 512-bit blocks
+  int32_t core_off; // u32 offset of this hasher's core inside the per-witness SHA core
+  int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
+};
+
+// per block core: Hin[8] W[64] A[1..64] E[1..64]; per hasher: blocks*200 + Hout[8]
+constexpr int SHA_BLOCK_CORE = 200;
+
+// Poseidon task: one permutation PoseidonHash(n) per (witness, task) lane
+struct PosTask {
+  int32_t n;          // inputs (t = n + 1)
+  int32_t in_slot[5]; // value-store slots (Montgomery) of the inputs
+  int32_t out_slot;   // value-store slot for the hash
+  int32_t core_off;   // Fr offset of this task's round states inside the per-witness Poseidon core
+  int32_t level;      // dependency level (launch wave)
+  int32_t pad;
+};
+
+constexpr int POS_MAX_T = 6;
+__host__ __device__ inline int pos_nrp(int t) {
+  return t == 2 ? 56 : t == 3 ? 57 : t == 4 ? 56 : t == 5 ? 60 : 60;
+}
+// round states kept per permutation: X0..X3, Y0..Y_RP, Z1..Z3 (t each)
+__host__ __device__ inline int pos_core_len(int t) { return (pos_nrp(t) + 8) * t; }
+// signals of PoseidonEx(n,1)
+__host__ __device__ inline uint32_t pos_ex_size(int n) {
+  int t = n + 1, RP = pos_nrp(t);
+  return (uint32_t)((2 + n) + 8 * (2 * t) + 8 * t * 4 + 7 * (2 * t + 2 * t * t) + RP * (4 + 4 * t) + (3 * t + 1));
+}
+__host__ __device__ inline uint32_t pos_hash_size(int n) { return 1 + n + pos_ex_size(n); }
+
+// Poseidon parameters on device: per t, offsets (in Fr) into one constant array, Montgomery form
+struct PosParamIndex {
+  int32_t nrp[POS_MAX_T + 1];
+  int32_t c_off[POS_MAX_T + 1];
+  int32_t m_off[POS_MAX_T + 1];
+  int32_t p_off[POS_MAX_T + 1];
+  int32_t s_off[POS_MAX_T + 1];
+};
+
+// everything the kernels need about an instance (device copy lives in Instance)
+struct DevLayout {
+  uint64_t wit_size;      // elements per witness
+  uint64_t n_inputs;      // elements per input row
+  uint32_t n_regions, n_work;
+  uint32_t n_sha, sha_core_words;   // SHA jobs; u32 words of SHA core per witness
+  uint32_t n_pos, pos_core_elems;   // Poseidon tasks; Fr per witness of Poseidon core
+  uint32_t n_values;                // value-store slots per witness (Fr, Montgomery)
+  uint32_t n_pos_levels;
+  const Region* regions;
+  const Work* work;
+  const ShaJob* sha;
+  const PosTask* pos;
+  const uint32_t* pos_level_start;  // tasks sorted by level: [start_l, start_{l+1})
+};
+
+}  // namespace pzk

@@ -1,0 +1,146 @@
+"""ctypes binding of libpzkwit.so (include/pzkwit.h).
+
+The library is the only compute path: there is no CPU fallback. Loading fails loudly
+when the shared object is missing, and instance creation fails when no HIP device is
+visible (PZK_E_NODEVICE).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libpzkwit.so")
+
+PZK_CIRCUIT_REGISTER, PZK_CIRCUIT_POSEIDON, PZK_CIRCUIT_SHA256 = 0, 1, 2
+PZK_EXEC_SYNC = 1
+
+# C-ABI entry points declared in include/pzkwit.h (checked by tests/test_capi.py)
+EXPORTS = ("pzk_instance_create", "pzk_instance_destroy", "pzk_instance_info", "pzk_instance_input",
+           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_last_error", "pzk_version")
+
+STATUS_NAMES = {
+    0: "OK", 1: "Num2Bits (bitify.circom:26)", 2: "AliasCheck (aliascheck.circom:14)",
+    3: "IsZero (comparators.circom:20)", 4: "GetLastBitUnsecure (arithmetic.circom:169)",
+    5: "GetLastNBits (arithmetic.circom:203)", 6: "Bits2 (sha2Common.circom:65)",
+    7: "PassportVerificationBuilder (passportVerificationBuilder.circom:155)",
+    8: "RsaVerifyPkcs1v15 (rsa.circom:48)", 9: "RsaVerifyPkcs1v15 (rsa.circom:53)",
+    10: "RsaVerifyPkcs1v15 (rsa.circom:57)", 11: "BigMultModP (bigInt.circom:245)",
+    12: "BigIntIsZero (bigIntComparators.circom:128)", 13: "SMTLevIns (SMTVerifier.circom:54)",
+    14: "BabyjubjubAdd (babyjubjub/curve.circom:98)", 64: "input out of range",
+}
+
+
+class PzkParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "circuit", "size_arg", "signature_type", "dg_hash_type", "document_type", "ec_block_number",
+        "ec_shift", "dg1_shift", "aa_signature_algo", "dg15_shift", "dg15_block_number", "aa_shift")]
+
+
+class PzkInfo(ctypes.Structure):
+    _fields_ = [("witness_size", ctypes.c_uint64), ("n_inputs", ctypes.c_uint64), ("n_outputs", ctypes.c_uint32),
+                ("n_public_inputs", ctypes.c_uint32), ("n_input_groups", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class PzkExec(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_int32), ("stream", ctypes.c_void_p)]
+
+
+class PzkError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PzkError("libpzkwit.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        L.pzk_instance_create.argtypes = [ctypes.POINTER(PzkParams), ctypes.POINTER(ctypes.c_void_p)]
+        L.pzk_instance_destroy.argtypes = [ctypes.c_void_p]
+        L.pzk_instance_destroy.restype = None
+        L.pzk_instance_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(PzkInfo)]
+        L.pzk_instance_input.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.pzk_wtns_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.pzk_witness_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(PzkExec)]
+        L.pzk_witness_batch_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.POINTER(PzkExec)]
+        L.pzk_last_error.restype = ctypes.c_char_p
+        L.pzk_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise PzkError("pzkwit error %d: %s" % (rc, lib().pzk_last_error().decode()))
+
+
+class Instance:
+    """One compiled circuit instance (the analogue of circom's compiled WASM module)."""
+
+    def __init__(self, circuit=PZK_CIRCUIT_REGISTER, size_arg=0, params=None):
+        L = lib()
+        p = PzkParams(circuit=circuit, size_arg=size_arg)
+        if params:
+            m = dict(sig="signature_type", dg_hash="dg_hash_type", doc="document_type",
+                     ec_blocks="ec_block_number", ec_shift="ec_shift", dg1_shift="dg1_shift",
+                     aa="aa_signature_algo", dg15_shift="dg15_shift", dg15_blocks="dg15_block_number",
+                     aa_shift="aa_shift")
+            for k, v in params.items():
+                setattr(p, m.get(k, k), int(v))
+        h = ctypes.c_void_p()
+        _check(L.pzk_instance_create(ctypes.byref(p), ctypes.byref(h)))
+        self._h = h
+        info = PzkInfo()
+        _check(L.pzk_instance_info(h, ctypes.byref(info)))
+        self.witness_size = int(info.witness_size)
+        self.n_inputs = int(info.n_inputs)
+        self.n_outputs = int(info.n_outputs)
+        self.n_public_inputs = int(info.n_public_inputs)
+        self.input_groups = []
+        for i in range(info.n_input_groups):
+            nm, off, ln = ctypes.c_char_p(), ctypes.c_uint64(), ctypes.c_uint64()
+            _check(L.pzk_instance_input(h, i, ctypes.byref(nm), ctypes.byref(off), ctypes.byref(ln)))
+            self.input_groups.append((nm.value.decode(), int(off.value), int(ln.value)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pzk_instance_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def wtns_header(self):
+        h = (ctypes.c_uint8 * 76)()
+        _check(lib().pzk_wtns_header(self._h, h))
+        return bytes(h)
+
+    def witness_batch_device(self, d_inputs, batch, d_wtns, stride, d_status=None, stream=None, device=0, sync=False):
+        ex = PzkExec(device=device, flags=PZK_EXEC_SYNC if sync else 0, stream=stream)
+        _check(lib().pzk_witness_batch(self._h, ctypes.c_void_p(d_inputs), batch, ctypes.c_void_p(d_wtns), stride,
+                                       ctypes.c_void_p(d_status) if d_status else None, ctypes.byref(ex)))
+
+    def witness_batch_host(self, inputs):
+        """inputs: (batch, n_inputs, 32) uint8 -> (witness (batch, W, 32) uint8, status (batch,) int32)."""
+        a = np.ascontiguousarray(inputs, dtype=np.uint8)
+        if a.ndim == 2:
+            a = a[None]
+        b = a.shape[0]
+        assert a.shape[1:] == (self.n_inputs, 32), a.shape
+        out = np.empty((b, self.witness_size, 32), dtype=np.uint8)
+        st = np.zeros(b, dtype=np.int32)
+        ex = PzkExec(device=0, flags=0, stream=None)
+        _check(lib().pzk_witness_batch_host(self._h, a.ctypes.data, b, out.ctypes.data, st.ctypes.data,
+                                            ctypes.byref(ex)))
+        return out, st

@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py — RegisterIdentityBuilder witnesses/s on MI355X (BASELINE.json metric).
+
+python bench.py --gpus N --steps K --warmup W [--workload register|sha256]
+
+One step = one pass of the hot path over one batch of synthetic passports per GPU
+(batch 4096 of the canonical instance RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256),
+SURVEY.md §8d config 3), inputs already resident in HBM when the timed region starts.
+A full --O0 witness is ~72 MB, so a 4096 batch (~295 GB) does not fit one GPU's 288 GB:
+each step runs it as sub-batches into a reused output slab (every witness is fully
+written). N > 1 shards the batch (weak scaling, no data-path collective).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "passport-zk-circuits_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------------- inputs
+def _gen_slice(args):
+    seed, lo, hi, n_keys = args
+    from pzkwit import inputs as I
+    g = I.PassportGen.shared(seed, n_keys)
+    out = np.zeros((hi - lo, g.n_inputs, 32), dtype=np.uint8)
+    for k, i in enumerate(range(lo, hi)):
+        I.pack_register_inputs(g.passport_at(i), g.params, out=out[k])
+    return lo, out
+
+
+def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None):
+    from concurrent.futures import ProcessPoolExecutor
+    from pzkwit import inputs as I
+    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    I.PassportGen.shared(seed, n_keys)  # keys generated once (parallel inside)
+    step = (batch + workers * 4 - 1) // (workers * 4)
+    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys) for lo in range(0, batch, step)]
+    n_in = I.PassportGen.shared(seed, n_keys).n_inputs
+    buf = np.zeros((batch, n_in, 32), dtype=np.uint8)
+    if workers == 1:
+        res = map(_gen_slice, jobs)
+    else:
+        ex = ProcessPoolExecutor(workers)
+        res = ex.map(_gen_slice, jobs)
+    for lo, arr in res:
+        buf[lo - first: lo - first + len(arr)] = arr
+    return buf
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_work(args):
+    kind, rows = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from pzkwit import inputs as I
+    if kind == "register":
+        prm = pyoracle.register_params(**I.CANONICAL)
+        nin, nw = pyoracle.register_sizes(prm)
+        w = np.zeros((nw, 32), dtype=np.uint8)
+        for r in rows:
+            pyoracle.register_witness(prm, r, out=w)
+    else:
+        for r in rows:
+            pyoracle.sha256_witness(r, 6)
+    return len(rows)
+
+
+def cpu_baseline(kind, sample_rows, procs):
+    """The CPU restatement (oracle/, kind "port") on a bounded sample, one witness per process."""
+    from concurrent.futures import ProcessPoolExecutor
+    chunks = [(kind, sample_rows[i::procs]) for i in range(procs)]
+    with ProcessPoolExecutor(procs) as ex:
+        list(ex.map(_cpu_work, [(kind, sample_rows[:1])] * procs))  # warm (lib load)
+        t0 = time.perf_counter()
+        n = sum(ex.map(_cpu_work, chunks))
+        dt = time.perf_counter() - t0
+    return n / dt, dt
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["register", "sha256"], default="register")
+    ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
+    ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
+    ap.add_argument("--cpu-sample", type=int, default=None)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from pzkwit import native, inputs as I
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    if args.workload == "register":
+        batch = args.batch or 4096
+        inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.CANONICAL)
+        t0 = time.time()
+        host_in = make_register_inputs(batch, rank * batch)
+        log("inputs: %d passports generated in %.1fs" % (batch, time.time() - t0))
+        metric = "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline"
+        workload = "RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports (config 3)"
+    else:
+        batch = args.batch or 1024
+        inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
+        _, host_in = I.sha256_config2_batch(batch, seed=2 + rank, blocks=6)
+        metric = "Sha256HashChunks(6) witnesses/sec, batch=1024 (config 2)"
+        workload = "Sha256HashChunks(6) synthetic 312-375 B messages (config 2)"
+
+    W, NIN = inst.witness_size, inst.n_inputs
+    stride = 32 * W
+    free, total = torch.cuda.mem_get_info(dev)
+    sub = args.sub or max(1, min(batch, int((free * 0.85 - host_in.nbytes) // stride)))
+    sub = min(sub, batch)
+    log("witness_size=%d (%.1f MB), batch=%d, sub-batch=%d, slab %.1f GB" % (W, stride / 1e6, batch, sub,
+                                                                             sub * stride / 1e9))
+    d_in = torch.from_numpy(host_in.reshape(-1)).to(dev)
+    del host_in
+    d_out = torch.empty(sub * stride, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(batch, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(timing):
+        for lo in range(0, batch, sub):
+            n = min(sub, batch - lo)
+            inst.witness_batch_device(d_in.data_ptr() + lo * NIN * 32, n, d_out.data_ptr(), stride,
+                                      d_st.data_ptr() + 4 * lo, stream=stream.cuda_stream, device=local,
+                                      timing=timing)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    bad = int((d_st != 0).sum().item())
+    inst.timing(reset=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        bt = torch.tensor([bad], device=dev, dtype=torch.int64)
+        dist.all_reduce(bt)
+        bad = int(bt.item())
+    total_w = batch * world * args.steps
+    value = total_w / dt
+
+    # roofline of the dominant kernel (HIP events on the launch stream, inside the timed region)
+    tm = inst.timing()
+    info = {n: (k, b) for n, k, b in inst.phase_info()}
+    dom = max((p for p in tm if tm[p][1] > 0), key=lambda p: tm[p][0])
+    ms_total, launches = tm[dom]
+    avg_ms = ms_total / launches
+    bytes_per_launch = info[dom][1] * sub
+    achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
+    phases = {p: {"ms_per_launch": round(tm[p][0] / max(tm[p][1], 1), 4), "launches": tm[p][1],
+                  "kernel": info[p][0], "alg_bytes_per_witness": info[p][1]} for p in tm if tm[p][1]}
+
+    out = {
+        "metric": metric, "value": round(value, 2), "unit": "witnesses/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic", "config": {"workload": workload, "batch_per_gpu": batch, "sub_batch": sub,
+                                        "witness_elements": W, "witness_bytes": stride, "layout": "O0 (all signals)",
+                                        "parallelism": "shard%d" % world, "invalid_lanes": bad},
+        "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_ms, 4)},
+        "phases": phases,
+    }
+    if rank == 0 and not args.no_cpu:
+        procs = max(1, min(16, os.cpu_count() or 1))
+        if args.workload == "register":
+            ns = args.cpu_sample or 16 * procs
+            rows = make_register_inputs(ns, 10 ** 6, workers=procs)
+        else:
+            ns = args.cpu_sample or 64 * procs
+            _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)
+        v, cdt = cpu_baseline(args.workload, list(rows), procs)
+        out["cpu_baseline"] = {"value": round(v, 2), "unit": "witnesses/s", "cores": procs, "kind": "port",
+                               "sample": "%d witnesses of the same workload on %d processes (%.1fs wall)" % (
+                                   ns, procs, cdt)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

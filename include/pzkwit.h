@@ -62,7 +62,10 @@ typedef struct pzk_exec {
   void* stream;     /* hipStream_t to launch on (NULL = the instance's own stream) */
 } pzk_exec;
 
-enum { PZK_EXEC_SYNC = 1 /* synchronise the stream before returning */ };
+enum {
+  PZK_EXEC_SYNC = 1,   /* synchronise the stream before returning */
+  PZK_EXEC_TIMING = 2  /* bracket every kernel phase with HIP events on the launch stream */
+};
 
 /* lane status codes: 0 = OK, else the first failing `===` site (reference file:line) */
 enum {
@@ -100,6 +103,11 @@ typedef struct pzk_instance pzk_instance;
 int pzk_instance_create(const pzk_params* params, pzk_instance** out);
 void pzk_instance_destroy(pzk_instance* inst);
 
+/* Host-only layout queries (no device needed): witness/input sizes of an instance and its
+ * emit-region table (offset, length, kind). Used by the CPU test suite. */
+int pzk_layout_query(const pzk_params* params, pzk_info* info, uint32_t* n_regions);
+int pzk_layout_region(const pzk_params* params, uint32_t i, uint64_t* off, uint32_t* len, uint32_t* kind);
+
 /* Replaces: wc.witnessSize / wc.n32 / wc.prime fields and getInputSignalSize(fnv(name)). */
 int pzk_instance_info(const pzk_instance* inst, pzk_info* info);
 /* i-th named input signal, in flat-input order: name, element offset and length. */
@@ -122,6 +130,16 @@ int pzk_witness_batch(pzk_instance* inst, const uint8_t* d_inputs, size_t batch,
 /* Host-buffer convenience (copies in/out; used by the single-input calculateWitness path). */
 int pzk_witness_batch_host(pzk_instance* inst, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
                            int32_t* h_status, const pzk_exec* exec);
+
+/* Per-phase kernel time accumulated (ms) by calls made with PZK_EXEC_TIMING, and the number of
+ * launches of each phase. On input *count is the capacity of the arrays; on output the number of
+ * phases. Synchronises on the recorded events. reset != 0 clears the accumulators afterwards. */
+int pzk_timing(pzk_instance* inst, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset);
+
+/* Static description of a kernel phase: name, kernel symbol, and its ALGORITHMIC HBM bytes per
+ * witness (each element written once + the unique bytes it must read). Used for roofline math. */
+int pzk_phase_info(const pzk_instance* inst, uint32_t phase, const char** name, const char** kernel,
+                   uint64_t* bytes_per_witness);
 
 /* Reason for the last failure on this thread. */
 const char* pzk_last_error(void);

@@ -608,7 +608,8 @@ static void run_addzero(ctx_t *c, size_t b) {
     W(R + 2) = W(z1); W(R + 3) = W(L); W(R + 4) = W(b + 4 + i);
     run_switcher(c, R);
   }
-  W(b) = W(sw); W(b + 1) = W(sw + 12);
+  /* out[c] <== switcherRight[c].out[0] (curve.circom:56-57); blocks are L0, R0, L1, R1 */
+  W(b) = W(sw + 6); W(b + 1) = W(sw + 18);
 }
 /* BabyjubjubBase8Multiplication curve.circom:143-171:
  * out[2] | scalar | getBase8, num2Bits(254), adders[0], (adders[i], doublers[i-1]) i=1..253 */

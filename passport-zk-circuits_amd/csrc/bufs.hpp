@@ -1,0 +1,24 @@
+// Per-batch device pointers handed to every emit kernel.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fr.hpp"
+#include "poseidon.hpp"
+
+namespace pzk {
+
+struct Bufs {
+  const uint8_t* inputs;
+  const uint32_t* sha_core;
+  const uint64_t* rsa_core;
+  const fr* pos_core;
+  const fr* bjj_core;
+  const fr* smt_core;
+  ValueStore vs;
+  uint8_t* wtns;
+  size_t stride;
+  int32_t* status;
+};
+
+}  // namespace pzk

@@ -23,7 +23,7 @@ struct Layout {
   uint32_t n_outputs = 0, n_public = 0;
   std::vector<InputGroup> inputs;
   std::vector<Region> regions;
-  std::vector<Work> work_sha, work_pos, work_gen;
+  std::vector<Work> work[E_COUNT];  // per emit kernel
   std::vector<ShaJob> sha;
   uint32_t sha_core_words = 0;
   std::vector<PosTask> pos;            // sorted by level, then t
@@ -32,6 +32,12 @@ struct Layout {
   int max_t = 2;
   uint32_t n_values = 0;
   std::vector<ValueLoad> loads;
+  // RegisterIdentityBuilder only
+  bool is_register = false;
+  RegInfo reg{};
+  pzk_params params{};
+  std::vector<int> out_slots;
+  uint32_t rsa_core_words = 0, bjj_core_fr = 0, smt_core_fr = 0;
 };
 
 bool build_layout(const pzk_params& p, Layout& L, std::string& why);

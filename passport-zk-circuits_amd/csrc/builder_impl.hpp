@@ -1,0 +1,101 @@
+// Builder shared by the layout translation units (builder.cpp, builder_register.cpp).
+#pragma once
+#include <algorithm>
+
+#include "builder.hpp"
+
+namespace pzk {
+
+constexpr uint32_t SHA_BLOCK_LEN = 150762;  // Sha2_224_256Shedule (36,048) + Sha2_224_256Rounds(64) (114,714)
+
+struct Builder {
+  Layout& L;
+  uint64_t cur = 0;
+  explicit Builder(Layout& l) : L(l) {}
+
+  int value() { return (int)L.n_values++; }
+
+  uint32_t region(uint32_t kind, uint64_t len, std::initializer_list<int32_t> a = {}) {
+    Region r{};
+    r.off = cur;
+    r.len = (uint32_t)len;
+    r.kind = kind;
+    int i = 0;
+    for (int32_t x : a) r.a[i++] = x;
+    L.regions.push_back(r);
+    cur += len;
+    return (uint32_t)L.regions.size() - 1;
+  }
+
+  int sha_job(int in_off, int blocks) {
+    ShaJob j{};
+    j.in_off = in_off;
+    j.blocks = blocks;
+    j.core_off = (int)L.sha_core_words;
+    j.digest_slot = -1;
+    L.sha_core_words += blocks * SHA_BLOCK_CORE + 8;
+    L.sha.push_back(j);
+    return (int)L.sha.size() - 1;
+  }
+
+  // Sha256HashChunks(B) (sha256HashChunks.circom:8-48), optionally inside ShaHashChunks(B,256)
+  // (hash.circom:32-68): own/wrapper signals as one RK_SHA_OWN region, then (sch, rds) per block.
+  int sha256(int in_off, int blocks, bool wrapper) {
+    int job = sha_job(in_off, blocks);
+    uint64_t own = (wrapper ? 256 + 512ull * blocks : 0) + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
+    region(RK_SHA_OWN, own, {job, blocks, in_off, wrapper ? 1 : 0});
+    for (int m = 0; m < blocks; m++) region(RK_SHA_BLOCK, SHA_BLOCK_LEN, {job, m});
+    return job;
+  }
+
+  // PoseidonHash(n) (poseidon.circom:214-226) as one RK_POSEIDON region; returns output slot
+  int poseidon(int n, const std::vector<int>& in_slots, int level, int out_slot = -1) {
+    PosTask t{};
+    t.n = n;
+    int i = 0;
+    for (int s : in_slots) t.in_slot[i++] = s;
+    t.out_slot = out_slot >= 0 ? out_slot : value();
+    t.core_off = (int)L.pos_core_elems;
+    t.level = level;
+    t.smt_level = -1;
+    L.pos_core_elems += pos_core_len(n + 1);
+    L.max_t = std::max(L.max_t, n + 1);
+    L.pos.push_back(t);
+    region(RK_POSEIDON, pos_hash_size(n), {(int32_t)L.pos.size() - 1, n});
+    return t.out_slot;
+  }
+
+  void finalize() {
+    L.wit_size = cur;
+    // Poseidon tasks: launch order = (level, t); remap region references
+    std::vector<int> order(L.pos.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      if (L.pos[a].level != L.pos[b].level) return L.pos[a].level < L.pos[b].level;
+      return L.pos[a].n < L.pos[b].n;
+    });
+    std::vector<int> inv(order.size());
+    std::vector<PosTask> sorted;
+    for (size_t i = 0; i < order.size(); i++) { inv[order[i]] = (int)i; sorted.push_back(L.pos[order[i]]); }
+    L.pos = sorted;
+    int max_level = -1;
+    for (auto& t : L.pos) max_level = std::max(max_level, t.level);
+    L.pos_level_start.assign(1, 0);
+    for (int lv = 0; lv <= max_level; lv++) {
+      uint32_t e = L.pos_level_start.back();
+      while (e < L.pos.size() && L.pos[e].level == lv) e++;
+      L.pos_level_start.push_back(e);
+    }
+    for (uint32_t ri = 0; ri < L.regions.size(); ri++) {
+      Region& r = L.regions[ri];
+      if (r.kind == RK_POSEIDON) r.a[0] = inv[r.a[0]];
+      int e = emitter_of(r.kind);
+      std::vector<Work>* wl = &L.work[e];
+      uint32_t chunk = emitter_whole(e) ? r.len : EMIT_CHUNK;
+      for (uint32_t s = 0; s < r.len; s += chunk) wl->push_back(Work{ri, s, std::min(chunk, r.len - s), 0});
+    }
+  }
+};
+
+
+}  // namespace pzk

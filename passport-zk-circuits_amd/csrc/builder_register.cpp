@@ -1,12 +1,228 @@
-// RegisterIdentityBuilder layout (registerIdentityBuilder.circom:41-196) — see builder.hpp.
-#include "builder.hpp"
+// RegisterIdentityBuilder layout (registerIdentityBuilder.circom:41-196).
+//
+// Walks the component tree in creation order and emits one region per contiguous run of
+// signals that shares a closed-form generator. Sizes are re-derived here from the
+// templates (cited inline); the CPU oracle derives them independently and the parity tests
+// compare every element.
+#include "builder_impl.hpp"
 
 namespace pzk {
 
+namespace {
+
+// sizes of small templates (own signals + subcomponents)
+constexpr uint32_t SZ_ISEQUAL = 6;        // IsEqual: out | in[2] | IsZero(out, in, inv)
+constexpr uint32_t SZ_SWITCHER = 6;       // Switcher: out[2] | bool, in[2] | aux
+uint32_t sz_num2bits(int L) { return 2 * L + 1 + (L == 254 ? 254 + 383 + 271 : 0); }  // + AliasCheck
+uint32_t sz_bits2num(int L) { return 2 * L + 1 + (L == 254 ? 254 + 383 + 271 : 0); }
+
+int log_ceil(int n) { int i = 0; while (n) { n >>= 1; i++; } return i; }
+int get_a_coeff(int a) { return a == 8 ? 70 : a == 16 ? 211 : a == 32 ? 640 : a == 64 ? 1940 : a == 128 ? 5881 : 1 << 30; }
+uint32_t sz_karatsuba(int N) { return N == 1 ? 4 : 4 * N + 3 * sz_karatsuba(N / 2); }
+uint32_t sz_bmneq(int G, int L) { return (G + L - 1) + G + L + G * L + (G + L - 1) * L; }
+
+}  // namespace
+
+// BigMultModP(64,K,K,K) block size (bigInt.circom:206-272)
+uint32_t modmul_size(int K) {
+  int BASE = 2 * K, DIV = K + 1, MAX = 128 + log_ceil(K + DIV - 1);
+  bool kara = (K & (K - 1)) == 0 && K >= 8 && get_a_coeff(K) <= K * K;
+  uint32_t bmo = (BASE - 1) + 2 * K + (kara ? sz_karatsuba(K) : sz_bmneq(K, K));
+  uint32_t bgt = 1 + 2 * K + (1 + 2 * K + K + K * ((3 + sz_num2bits(65)) + SZ_ISEQUAL));
+  uint32_t bisz = (BASE - 1) + (BASE - 2) + (BASE - 2) * sz_num2bits(MAX + 3 - 64);
+  return DIV + K + 3 * K + bmo + K * sz_num2bits(64) + bgt + sz_bmneq(DIV, K) + bisz;
+}
+
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
-  (void)p; (void)L;
-  why = "RegisterIdentityBuilder layout: not built in this library version";
-  return false;
+  if (p.signature_type != 1 && p.signature_type != 2) {
+    why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) + " not built yet (RSA PKCS#1 v1.5 types 1 and 2 are)";
+    return false;
+  }
+  if (p.dg_hash_type != 256) { why = "DG_HASH_TYPE must be 256 (SHA-256 chunks)"; return false; }
+  if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
+  if (p.aa_signature_algo != 0 && p.aa_signature_algo != 1) { why = "AA_SIGNATURE_ALGO must be 0 or 1"; return false; }
+  const int K = p.signature_type == 2 ? 64 : 32;
+  const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
+  const bool aa = p.aa_signature_algo != 0;
+  if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
+  const int dg15shift = aa ? p.dg15_shift : 256;
+  if (p.dg1_shift < 0 || p.dg1_shift + 256 > ecLen || dg15shift < 24 || dg15shift + 256 > ecLen ||
+      p.ec_shift < 0 || p.ec_shift + 256 > 1024 || (aa && p.aa_shift + 1024 > d15Len)) {
+    why = "shift parameters address bits outside the inputs";
+    return false;
+  }
+  const int chunk = p.document_type == 1 ? 190 : 186;
+
+  Builder b(L);
+  // flat inputs in witness order (public first): root, ec, dg1, dg15, sa, signature, pubkey, branches, sk
+  const int IN_ROOT = 0, IN_EC = 1, IN_DG1 = IN_EC + ecLen, IN_DG15 = IN_DG1 + 1024, IN_SA = IN_DG15 + d15Len,
+            IN_SIG = IN_SA + 1024, IN_PK = IN_SIG + K, IN_BR = IN_PK + K, IN_SK = IN_BR + 80;
+  L.n_inputs = IN_SK + 1;
+  L.n_outputs = 4;
+  L.n_public = 1;
+  L.inputs = {{"slaveMerkleRoot", (uint64_t)IN_ROOT, 1},   {"encapsulatedContent", (uint64_t)IN_EC, (uint64_t)ecLen},
+              {"dg1", (uint64_t)IN_DG1, 1024},             {"dg15", (uint64_t)IN_DG15, (uint64_t)d15Len},
+              {"signedAttributes", (uint64_t)IN_SA, 1024},  {"signature", (uint64_t)IN_SIG, (uint64_t)K},
+              {"pubkey", (uint64_t)IN_PK, (uint64_t)K},     {"slaveMerkleInclusionBranches", (uint64_t)IN_BR, 80},
+              {"skIdentity", (uint64_t)IN_SK, 1}};
+  L.is_register = true;
+  L.params = p;
+  L.reg.K = K;
+  L.reg.in_pk = IN_PK;
+  L.reg.in_sig = IN_SIG;
+  L.reg.in_br = IN_BR;
+  L.reg.in_root = IN_ROOT;
+  L.reg.in_dg1 = IN_DG1;
+  L.reg.in_dg15 = IN_DG15;
+  L.reg.aa = aa ? 1 : 0;
+  L.reg.aa_shift = p.aa_shift;
+
+  // ---- value-store slots that feed Poseidon tasks (filled by k_prep / core kernels)
+  const int V_ONE = b.value();        // Montgomery 1 (SMTHash1 in[2])
+  const int V_SK = b.value();
+  int V_PK[5], V_AA[5], V_DG1[4];
+  for (int i = 0; i < 5; i++) V_PK[i] = b.value();
+  for (int i = 0; i < 5; i++) V_AA[i] = b.value();
+  for (int i = 0; i < 4; i++) V_DG1[i] = b.value();
+  const int V_SANUM = b.value();
+  const int V_BJJ_X = b.value(), V_BJJ_Y = b.value();
+  int V_L[80], V_R[80];
+  for (int i = 0; i < 80; i++) { V_L[i] = b.value(); V_R[i] = b.value(); }
+  L.loads.push_back(ValueLoad{V_SK, IN_SK});
+  L.reg.v_one = V_ONE; L.reg.v_sk = V_SK; L.reg.v_pk = V_PK[0]; L.reg.v_aa = V_AA[0]; L.reg.v_dg1 = V_DG1[0];
+  L.reg.v_sanum = V_SANUM; L.reg.v_bjj = V_BJJ_X; L.reg.v_smt_lr = V_L[0];
+  L.reg.dg1_chunk = chunk;
+
+  // Poseidon tasks are created where their components are created (creation order = layout
+  // order); region() records the block. Levels encode the data dependencies:
+  //   0: pk hash, sk hash, AA hash, passportHash, pkIdentity hash (after BJJ core)
+  //   1: SMT leaf (needs pk hash), dg1Commitment (needs sk hash)
+  //   2: SMT level hashes (need the leaf / key bits)
+
+  // =========================== main: [1 | outputs(4) | inputs] =========================
+  b.region(RK_ONE, 1);
+  const uint32_t r_out = b.region(RK_VALUE, 4, {-1});  // outputs patched below (4 slots, non-contiguous)
+  b.region(RK_INCOPY, L.n_inputs, {0});
+
+  // =========================== PassportVerificationBuilder ============================
+  // own: passportHash | inputs (ec, dg1, dg15, sa, sig, pk, branches, root) | dg1Hash, dg15Hash, ecHash, saHash,
+  //      pubkeyHash, tempModulus[5]
+  const uint32_t r_pvb_out = b.region(RK_VALUE, 1, {-1});
+  b.region(RK_INCOPY, IN_SK - IN_EC, {IN_EC});
+  b.region(RK_INCOPY, 1, {IN_ROOT});
+  // SHA jobs are created when the hashers are created; their digests are referenced earlier,
+  // so reserve the job ids first (creation order dg1, dg15, ec, sa).
+  const int J_DG1 = b.sha_job(IN_DG1, 2);
+  const int J_DG15 = aa ? b.sha_job(IN_DG15, d15B) : -1;
+  const int J_EC = b.sha_job(IN_EC, ecB);
+  const int J_SA = b.sha_job(IN_SA, 2);
+  L.reg.j_dg1 = J_DG1; L.reg.j_dg15 = J_DG15; L.reg.j_ec = J_EC; L.reg.j_sa = J_SA;
+  b.region(RK_DIGEST, 256, {J_DG1});
+  if (aa) b.region(RK_DIGEST, 256, {J_DG15});
+  else b.region(RK_VALUE, 256, {-2});  // dg15Hash <== 0 (zeros)
+  b.region(RK_DIGEST, 256, {J_EC});
+  b.region(RK_DIGEST, 256, {J_SA});
+  const uint32_t r_pkhash = b.region(RK_VALUE, 1, {-1});
+  b.region(RK_TEMPMOD, 5, {IN_PK});
+  auto sha_blocks = [&](int job, int in_off, int blocks) {
+    uint64_t own = 256 + 512ull * blocks + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
+    b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1});
+    for (int m = 0; m < blocks; m++) b.region(RK_SHA_BLOCK, 150762, {job, m});
+  };
+  sha_blocks(J_DG1, IN_DG1, 2);
+  if (aa) sha_blocks(J_DG15, IN_DG15, d15B);
+  sha_blocks(J_EC, IN_EC, ecB);
+  sha_blocks(J_SA, IN_SA, 2);
+  // PassportVerificationFlow(ecLen, 256, 256, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA)
+  b.region(RK_FLOW, 1 + 256 + 256 + ecLen + 256 + 1024 + 776 + 776 * SZ_ISEQUAL,
+           {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, aa ? 1 : 0});
+  // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15
+  b.region(RK_INCOPY, K, {IN_PK});
+  b.region(RK_INCOPY, K, {IN_SIG});
+  b.region(RK_DIGEST, 256, {J_SA});
+  //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
+  b.region(RK_INCOPY, K, {IN_SIG});
+  b.region(RK_INCOPY, K, {IN_PK});
+  b.region(RK_DIGEST, 256, {J_SA});
+  b.region(RK_HCHUNK, 4, {J_SA});
+  //   PowerMod(64,K,65537): out[K] | base[K], modulus[K] | muls[16], resultMuls[1]
+  b.region(RK_RSA_OUT, K);
+  b.region(RK_INCOPY, K, {IN_SIG});
+  b.region(RK_INCOPY, K, {IN_PK});
+  const uint32_t mm = modmul_size(K);
+  L.reg.modmul_size = mm;
+  // exp_to_bits(65537) = [16, 2, 0, 16]: muls[i] = muls[i-1]^2 (muls[0] = base^2); resultMuls[0] = base * muls[15]
+  L.reg.n_modmul = 17;
+  L.rsa_core_words = 17 * MM_CORE_WORDS(K);
+  L.bjj_core_fr = BJJ_CORE_FR;
+  L.smt_core_fr = SMT_CORE_FR;
+  for (int i = 0; i < 17; i++) b.region(RK_MODMUL, mm, {i, IN_PK});
+  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
+  b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
+  // signedAttributesNum = Bits2Num(252)(saHash[0..251])
+  b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, 0, 1, J_SA});
+  // pubkeyHasherRsa = PoseidonHash(5)
+  const int S_PKH = b.poseidon(5, {V_PK[0], V_PK[1], V_PK[2], V_PK[3], V_PK[4]}, 0);
+  // ---- SMTVerifier(80): isVerified | root, leaf, key, siblings[80] | value
+  //      | hash1New, n2bNew, smtLevIns, sm[80], levels[79..0], isEqual
+  b.region(RK_SMT_OWN, 1 + 3 + 80 + 1, {IN_ROOT, IN_BR});
+  b.region(RK_SMTHASH, 3, {-1});
+  const int S_LEAF = b.poseidon(3, {S_PKH, S_PKH, V_ONE}, 1);
+  b.region(RK_NUM2BITS, sz_num2bits(254), {254, 0, S_PKH});
+  b.region(RK_LEVINS, 80 + 80 + 79 + 80 * 3, {IN_BR});
+  b.region(RK_SM, 80 * 4);
+  int S_H[80];
+  for (int i = 0; i < 80; i++) S_H[i] = b.value();  // level hashes: contiguous slots
+  for (int i = 79; i >= 0; i--) {
+    b.region(RK_SMT_LEVEL, 8, {i, IN_BR});
+    b.region(RK_SMTHASH, 3, {i});
+    b.poseidon(2, {V_L[i], V_R[i]}, 2, S_H[i]);
+    L.pos.back().smt_level = i;
+    b.region(RK_SWITCHER, SZ_SWITCHER, {i, IN_BR});
+  }
+  b.region(RK_ISEQ_ROOT, SZ_ISEQUAL, {IN_ROOT});
+  L.reg.v_pkhash = S_PKH; L.reg.v_leaf = S_LEAF; L.reg.v_smt_h = S_H[0];
+  for (int i = 1; i < 80; i++)
+    if (S_H[i] != S_H[0] + i) { why = "internal: SMT hash slots not contiguous"; return false; }
+  // signedAttributesHashHasher = PoseidonHash(1)(signedAttributesNum)
+  const int S_PASS = b.poseidon(1, {V_SANUM}, 0);
+
+  // =========================== RegisterIdentity ============================
+  // own: dg15PubKeyHash, dg1Commitment, pkIdentityHash | dg1[1024], dg15[d15Len], skIdentity
+  const uint32_t r_rid_out = b.region(RK_VALUE, 3, {-1});
+  b.region(RK_INCOPY, 1024, {IN_DG1});
+  if (d15Len) b.region(RK_INCOPY, d15Len, {IN_DG15});
+  b.region(RK_INCOPY, 1, {IN_SK});
+  int S_AA = -1;
+  if (aa) {
+    for (int j = 0; j < 4; j++) b.region(RK_BITS2NUM, sz_bits2num(200), {200, 0, IN_DG15 + p.aa_shift + j * 200 + 199, -1});
+    b.region(RK_BITS2NUM, sz_bits2num(224), {224, 0, IN_DG15 + p.aa_shift + 800 + 223, -1});
+    S_AA = b.poseidon(5, {V_AA[0], V_AA[1], V_AA[2], V_AA[3], V_AA[4]}, 0);
+  }
+  // dg1Hasher is created before dg1Chunking[i] (identity.circom:89-92); its 5th input is P1(sk)
+  const size_t dg1_task = L.pos.size();
+  const int S_DG1C = b.poseidon(5, {V_DG1[0], V_DG1[1], V_DG1[2], V_DG1[3], -1}, 1);
+  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(chunk), {chunk, 0, IN_DG1 + i * chunk, 1});
+  const int S_SKH = b.poseidon(1, {V_SK}, 0);
+  L.pos[dg1_task].in_slot[4] = S_SKH;
+  // BabyjubjubBase8Multiplication: out[2] | scalar | getBase8, num2Bits(254), adders/doublers
+  b.region(RK_BJJ_OWN, 3 + 2);
+  b.region(RK_NUM2BITS, sz_num2bits(254), {254, 0, V_SK});
+  b.region(RK_BJJ_STEPS, 46 + 253 * 60);
+  const int S_PKID = b.poseidon(2, {V_BJJ_X, V_BJJ_Y}, 0);
+
+  // outputs: main [dg15PubKeyHash, passportHash, dg1Commitment, pkIdentityHash]
+  L.out_slots = {aa ? S_AA : -2, S_PASS, S_DG1C, S_PKID};
+  auto set_value = [&](uint32_t r, std::vector<int> slots) {
+    L.regions[r].a[0] = -3;  // explicit list
+    for (size_t i = 0; i < slots.size(); i++) L.regions[r].a[1 + i] = slots[i];
+  };
+  set_value(r_out, {aa ? S_AA : -2, S_PASS, S_DG1C, S_PKID});
+  set_value(r_pvb_out, {S_PASS});
+  set_value(r_pkhash, {S_PKH});
+  set_value(r_rid_out, {aa ? S_AA : -2, S_DG1C, S_PKID});
+  b.finalize();
+  return true;
 }
 
 }  // namespace pzk

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include "poseidon.hpp"
+#include "regcore.hpp"
+#include "regemit.hpp"
 #include "sha.hpp"
 #include "kernels.hpp"
 
@@ -33,17 +35,24 @@ __global__ void k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs
 }
 
 // ------------------------------------------------------------------- Poseidon core
+// wave = 64 witnesses of one task. SMT level tasks below the insertion level depend on the
+// chain and are left to k_smt_chain.
 template <int T>
-__global__ void k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems) {
+__global__ void k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems,
+                           const fr* smt_core, uint32_t smt_core_fr) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
   const PosTask& task = tasks[blockIdx.y];
+  if (task.smt_level >= 0) {
+    int j = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
+    if (task.smt_level < j) return;
+  }
   pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
 }
 
 // ------------------------------------------------------------------- emit: SHA regions
-__device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t* H /* (B+1)*8 in LDS */,
-                                                const uint8_t* in_row, uint32_t s, bool& is_copy, uint64_t& src) {
+__device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t* H /* (B+1)*8 in LDS */, uint32_t s,
+                                                bool& is_copy, uint64_t& src) {
   const int B = R.a[1];
   const uint32_t inLen = 512u * B;
   is_copy = false;
@@ -87,14 +96,9 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
     for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
       bool cp; uint64_t src = 0;
-      uint64_t v = sha_own_sig(R, core, in_row, wk.start + q, cp, src);
-      if (cp) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(in_row + 32ull * src);
-        uint4* d4 = reinterpret_cast<uint4*>(out + 32ull * q);
-        d4[0] = s4[0]; d4[1] = s4[1];
-      } else {
-        store_u64(out + 32ull * q, v);
-      }
+      uint64_t v = sha_own_sig(R, core, wk.start + q, cp, src);
+      if (cp) copy_el(out + 32ull * q, in_row + 32ull * src);
+      else store_u64(out + 32ull * q, v);
     }
   }
 }
@@ -118,28 +122,13 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
     store_fr(out + 32ull * q, fr_from_mont(pos_block_sig(P, n, wk.start + q)));
 }
 
-// ------------------------------------------------------------------- emit: generic
-__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, const uint8_t* inputs,
-                                                          ValueStore vs, uint8_t* wtns, size_t stride) {
+// ------------------------------------------------------------------- emit: generic small regions
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
-  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
-  const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
-    uint32_t s = wk.start + q;
-    uint4* d4 = reinterpret_cast<uint4*>(out + 32ull * q);
-    switch (R.kind) {
-      case RK_ONE: store_u64(out + 32ull * q, 1); break;
-      case RK_INCOPY: {
-        const uint4* s4 = reinterpret_cast<const uint4*>(in_row + 32ull * ((uint64_t)R.a[0] + s));
-        d4[0] = s4[0]; d4[1] = s4[1];
-        break;
-      }
-      case RK_VALUE: store_fr(out + 32ull * q, fr_from_mont(vs.at(R.a[0] + (int)s, w))); break;
-      default: break;
-    }
-  }
+  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) emit_small(L, B, R, w, wk.start + q, out + 32ull * q);
 }
 
 // ------------------------------------------------------------------- launchers
@@ -163,7 +152,8 @@ hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* 
 }
 
 hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
-                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, hipStream_t st) {
+                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, const fr* smt_core,
+                           uint32_t smt_core_fr, hipStream_t st) {
   // group consecutive tasks of equal t into one launch (blockIdx.y = task)
   uint32_t i = 0;
   while (i < count) {
@@ -173,11 +163,11 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
     dim3 g((vs.batch + 63) / 64, j - i);
     const PosTask* tp = d_tasks + first + i;
     switch (t) {
-      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
-      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
-      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
-      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
-      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems); break;
+      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
       default: return hipErrorInvalidValue;
     }
     HIP_TRY(hipGetLastError());
@@ -186,27 +176,69 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
   return hipSuccess;
 }
 
-hipError_t launch_emit_sha(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
-                           const uint32_t* sha_core, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st) {
-  if (n_work == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_emit_sha, dim3(n_work, batch), dim3(EMIT_THREADS), 0, st, L, work, inputs, sha_core, wtns,
-                     stride);
+hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
+                       int32_t* status, hipStream_t st) {
+  hipLaunchKernelGGL(k_prep, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, vs, status);
   return hipGetLastError();
 }
 
-hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, ValueStore vs,
-                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch, int max_t, hipStream_t st) {
-  if (n_work == 0) return hipSuccess;
-  size_t lds = sizeof(fr) * (size_t)pos_lds_elems(max_t);
-  hipLaunchKernelGGL(k_emit_pos, dim3(n_work, batch), dim3(EMIT_THREADS), lds, st, L, work, K, vs, pos_core, wtns,
-                     stride);
+hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
+                           uint32_t batch, hipStream_t st) {
+  if (L.reg.K == 32) {
+    constexpr int NL = 64;
+    size_t lds = sizeof(uint64_t) * rsa_lds_words<32>() * NL;
+    HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<32, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_rsa_core<32, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, status,
+                       batch);
+  } else {
+    constexpr int NL = 32;
+    size_t lds = sizeof(uint64_t) * rsa_lds_words<64>() * NL;
+    HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<64, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_rsa_core<64, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, status,
+                       batch);
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_emit_gen(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
-                           ValueStore vs, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st) {
+hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, fr* bjj_core, fr* scratch, hipStream_t st) {
+  hipLaunchKernelGGL(k_bjj_core, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, vs, bjj_core, scratch, vs.batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_smt_prep, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, inputs, vs, smt_core, status, vs.batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
+                            ValueStore vs, fr* pos_core, fr* smt_core, hipStream_t st) {
+  hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
+                     smt_core, vs.batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,
+                       const Bufs& B, uint32_t batch, int max_t, hipStream_t st) {
   if (n_work == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_emit_gen, dim3(n_work, batch), dim3(EMIT_THREADS), 0, st, L, work, inputs, vs, wtns, stride);
+  dim3 g(n_work, batch), blk(EMIT_THREADS);
+  switch (emitter) {
+    case E_GEN: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
+    case E_SHA: hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride); break;
+    case E_POS: {
+      size_t lds = sizeof(fr) * (size_t)pos_lds_elems(max_t);
+      hipLaunchKernelGGL(k_emit_pos, g, blk, lds, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride);
+      break;
+    }
+    case E_BITS: hipLaunchKernelGGL(k_emit_bits, g, blk, 0, st, L, work, B); break;
+    case E_FLOW: hipLaunchKernelGGL(k_emit_flow, g, blk, 0, st, L, work, B); break;
+    case E_MM:
+      if (L.reg.K == 32) hipLaunchKernelGGL(k_emit_mm<32>, g, blk, 0, st, L, work, B);
+      else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
+      break;
+    case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -15,18 +15,25 @@ struct ValueLoad {
 
 struct PosConsts;
 struct ValueStore;
+struct Bufs;
 
 hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inputs, uint64_t n_inputs, fr* values,
                               uint32_t batch, hipStream_t st);
 hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* sha_core, int32_t* status,
                            uint32_t batch, hipStream_t st);
 hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
-                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, hipStream_t st);
-hipError_t launch_emit_sha(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
-                           const uint32_t* sha_core, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st);
-hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, ValueStore vs,
-                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch, int max_t, hipStream_t st);
-hipError_t launch_emit_gen(const DevLayout& L, const Work* work, uint32_t n_work, const uint8_t* inputs,
-                           ValueStore vs, uint8_t* wtns, size_t stride, uint32_t batch, hipStream_t st);
+                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, const fr* smt_core,
+                           uint32_t smt_core_fr, hipStream_t st);
+hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
+                       int32_t* status, hipStream_t st);
+hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
+                           uint32_t batch, hipStream_t st);
+hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, fr* bjj_core, fr* scratch, hipStream_t st);
+hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
+                           hipStream_t st);
+hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
+                            ValueStore vs, fr* pos_core, fr* smt_core, hipStream_t st);
+hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,
+                       const Bufs& B, uint32_t batch, int max_t, hipStream_t st);
 
 }  // namespace pzk

@@ -29,15 +29,46 @@ enum RegionKind : uint32_t {
   RK_BITS2NUM = 7,   // Bits2Num(L) over bits taken from a bit source; a0 = L, a1 = bit source id,
                      //   a2 = first bit, a3 = stride(+1/-1), a4 = alias-check flag
   RK_NUM2BITS = 8,   // Num2Bits(L) of a value-store slot; a0 = L, a1 = slot
-  RK_MISC = 9,       // small irregular templates, a0 = sub-kind (see kernels)
+  RK_DIGEST = 9,     // 256 digest bits (MSB first) of SHA job a0
+  RK_TEMPMOD = 10,   // tempModulus[5] = pk[3i]*2^128 + pk[3i+1]*2^64; a0 = pubkey input offset
+  RK_FLOW = 11,      // PassportVerificationFlow (passportVerificationFlow.circom:6-109), whole block
+  RK_HCHUNK = 12,    // RsaVerifyPkcs1v15.hashed_chunks[4]; a0 = SHA job
+  RK_RSA_OUT = 13,   // PowerMod.out[K] = EM limbs (RSA core)
+  RK_SMT_OWN = 14,   // SMTVerifier own signals
+  RK_SMTHASH = 15,   // SMTHash1/2 own (out, key/L, value/R); a0 = level (-1 = hash1New)
+  RK_LEVINS = 16,    // SMTLevIns(80) block
+  RK_SM = 17,        // sm[80] SMTVerifierSM blocks
+  RK_SMT_LEVEL = 18, // SMTVerifierLevel own signals; a0 = level
+  RK_SWITCHER = 19,  // Switcher of SMT level a0
+  RK_ISEQ_ROOT = 20, // SMTVerifier.isEqual block
+  RK_BJJ_OWN = 21,   // BabyjubjubBase8Multiplication own (out[2], scalar) + GetBabyjubjubBase8
+  RK_BJJ_STEPS = 22, // adders[0], (adders[i], doublers[i-1]) i = 1..253
+  RK_SIG_OWN = 23,   // VerifySignature / RsaVerifyPkcs1v15 / PowerMod input copies (a0 = sub-kind)
   RK_COUNT
 };
 
+// emit kernels (one work list each)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_COUNT };
+__host__ __device__ inline int emitter_of(uint32_t kind) {
+  switch (kind) {
+    case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
+    case RK_POSEIDON: return E_POS;
+    case RK_BITS2NUM: case RK_NUM2BITS: return E_BITS;
+    case RK_FLOW: return E_FLOW;
+    case RK_MODMUL: return E_MM;
+    case RK_BJJ_STEPS: return E_BJJ;
+    default: return E_GEN;
+  }
+}
+// regions whose emit workgroup needs the whole region (LDS pre-pass over all of it)
+__host__ __device__ inline bool emitter_whole(int e) { return e == E_POS || e == E_BITS || e == E_FLOW; }
+
+constexpr int REGION_ARGS = 10;
 struct Region {
   uint64_t off;   // witness element offset
   uint32_t len;   // number of signals
   uint32_t kind;  // RegionKind
-  int32_t a[6];
+  int32_t a[REGION_ARGS];
 };
 
 // one workgroup's slice of a region
@@ -66,8 +97,27 @@ struct PosTask {
   int32_t out_slot;   // value-store slot for the hash
   int32_t core_off;   // Fr offset of this task's round states inside the per-witness Poseidon core
   int32_t level;      // dependency level (launch wave)
-  int32_t pad;
+  int32_t smt_level;  // >= 0: SMTVerifierLevel hash of that level (skipped where it depends on the chain)
 };
+
+// RegisterIdentityBuilder instance facts the kernels need (value-store slots, input offsets)
+struct RegInfo {
+  int32_t K;                       // RSA limbs (32 or 64)
+  int32_t in_pk, in_sig, in_br, in_root;
+  int32_t j_dg1, j_dg15, j_ec, j_sa; // SHA jobs
+  int32_t v_one, v_sk, v_pk, v_aa, v_dg1, v_sanum, v_bjj, v_smt_lr;  // slots (v_pk/v_aa/v_dg1: first of 5/5/4)
+  int32_t v_pkhash, v_leaf, v_smt_h;  // Poseidon outputs (v_smt_h: first of 80 level hashes)
+  int32_t dg1_chunk, aa_shift, in_dg1, in_dg15, aa;
+  int32_t n_modmul;
+  uint32_t modmul_size;
+};
+
+// per-witness core sizes of the register-circuit kernels
+constexpr int MM_CORE_WORDS(int K) { return 12 * K - 3; }  // x[K] y[K] q[K+1] r[K] inv[K](4 words) carry[2K-2](2 words)
+constexpr int BJJ_STEPS = 254;
+constexpr int BJJ_CORE_FR = 5 * BJJ_STEPS;                  // per step: Dx, Dy, Ax, Ay, inv(Dx)   (Montgomery)
+constexpr int SMT_LEVELS = 80;
+constexpr int SMT_CORE_FR = 3 * SMT_LEVELS + 2;             // inv(sibling), root, flags per level; j; inv(root-root0)
 
 constexpr int POS_MAX_T = 6;
 __host__ __device__ inline int pos_nrp(int t) {
@@ -105,6 +155,9 @@ struct DevLayout {
   const ShaJob* sha;
   const PosTask* pos;
   const uint32_t* pos_level_start;  // tasks sorted by level: [start_l, start_{l+1})
+  RegInfo reg;
+  uint32_t rsa_core_words;          // u64 per witness
+  uint32_t bjj_core_fr, smt_core_fr;
 };
 
 }  // namespace pzk

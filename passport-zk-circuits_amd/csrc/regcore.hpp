@@ -1,0 +1,518 @@
+// Core (sequential, per-witness) kernels of the RegisterIdentityBuilder path.
+//
+// Each computes the compact per-witness state from which the emit kernels regenerate
+// every signal in closed form:
+//   * k_prep      — Poseidon inputs that are linear/bit functions of the inputs and digests
+//   * k_rsa_core  — PowerMod(64,K,65537) (bigInt.circom:280-340): per BigMultModP the operands,
+//                   the exact quotient/remainder (any exact long division yields the unique
+//                   result that long_div, bigIntFunc.circom:190-232, must produce for a passing
+//                   witness), the K IsEqual inverses (one batched Fermat inversion per modmul) and
+//                   the 2K-2 signed BigIntIsZero carries. Per-lane 64-bit limb arrays live in LDS.
+//   * k_bjj_core  — BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171) as an
+//                   extended-coordinate ladder (no inversion on the critical path) followed by
+//                   ONE batched inversion that yields every affine point and IsZero inverse.
+//   * k_smt_prep / k_smt_chain — SMTVerifier(80) (SMTVerifier.circom:109-176): level hashes
+//                   whose child is 0 (every level at or above the insertion level) are
+//                   independent Poseidon tasks; only the levels below run sequentially.
+#pragma once
+#include "fr.hpp"
+#include "layout.hpp"
+#include "poseidon.hpp"
+#include "sha.hpp"
+
+namespace pzk {
+
+// ----------------------------------------------------------------------------- helpers
+__device__ __forceinline__ bool in_is_u64(const uint8_t* e) {
+  const uint4* q = reinterpret_cast<const uint4*>(e);
+  uint4 a = q[0], b = q[1];
+  return (a.z | a.w | b.x | b.y | b.z | b.w) == 0;
+}
+__device__ __forceinline__ uint64_t in_u64(const uint8_t* e) { return *reinterpret_cast<const uint64_t*>(e); }
+__device__ __forceinline__ uint32_t in_bit(const uint8_t* row, int idx, bool& bad) {
+  const uint4* q = reinterpret_cast<const uint4*>(row + 32ull * idx);
+  uint4 a = q[0], b = q[1];
+  bad |= (a.x > 1u) | ((a.y | a.z | a.w | b.x | b.y | b.z | b.w) != 0u);
+  return a.x & 1u;
+}
+__device__ __forceinline__ void set_status(int32_t* st, int32_t code) {
+  if (st) atomicCAS(st, 0, code);
+}
+// integer from bits (bit k of the number = get(k)), L <= 254
+template <typename F>
+__device__ __forceinline__ fr bits_to_fr(int L, F get) {
+  fr r = fr_zero();
+  for (int j = 0; j < L; j++) r.v[j >> 5] |= get(j) << (j & 31);
+  return r;
+}
+// signed 128-bit (lo, hi two's complement) -> normal-form Fr (negative x -> p - |x|)
+__device__ __forceinline__ fr fr_from_i128(uint64_t lo, uint64_t hi) {
+  bool neg = (int64_t)hi < 0;
+  if (neg) { lo = ~lo + 1; hi = ~hi + (lo == 0); }
+  fr m = fr_zero();
+  m.v[0] = (uint32_t)lo; m.v[1] = (uint32_t)(lo >> 32); m.v[2] = (uint32_t)hi; m.v[3] = (uint32_t)(hi >> 32);
+  return neg ? fr_sub(fr_zero(), m) : m;
+}
+
+// ============================================================================ k_prep
+// lane = witness. Runs after k_sha_core (needs the SA digest).
+__global__ void k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= vs.batch) return;
+  const RegInfo& R = L.reg;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  bool bad = false;
+  vs.at(R.v_one, w) = fr_mont_one();
+  // pubkeyHasherRsa inputs: tempModulus[i] + pk[3i+2] = pk[3i]*2^128 + pk[3i+1]*2^64 + pk[3i+2]
+  // (passportVerificationBuilder.circom:182-191), in field arithmetic
+  fr two64 = fr_zero(); two64.v[2] = 1;
+  fr two128 = fr_zero(); two128.v[4] = 1;
+  two64 = fr_to_mont(two64); two128 = fr_to_mont(two128);
+  for (int i = 0; i < 5; i++) {
+    fr a = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i)));
+    fr b = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 1)));
+    fr c = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 2)));
+    vs.at(R.v_pk + i, w) = fr_add(fr_add(fr_mul(a, two128), fr_mul(b, two64)), c);
+  }
+  // AA key chunks: Bits2Num(200) x4 + Bits2Num(224), in[L-1-i] = dg15[AA_SHIFT + 200 j + i] (identity.circom:31-45)
+  if (R.aa) {
+    for (int j = 0; j < 5; j++) {
+      int Lb = j < 4 ? 200 : 224, base = R.in_dg15 + R.aa_shift + j * 200;
+      fr v = bits_to_fr(Lb, [&](int k) { return in_bit(row, base + Lb - 1 - k, bad); });
+      vs.at(R.v_aa + j, w) = fr_to_mont(v);
+    }
+  }
+  // dg1 chunks: Bits2Num(186|190), in[j] = dg1[i*chunk + j] (identity.circom:95-101)
+  for (int i = 0; i < 4; i++) {
+    int base = R.in_dg1 + i * R.dg1_chunk;
+    fr v = bits_to_fr(R.dg1_chunk, [&](int k) { return in_bit(row, base + k, bad); });
+    vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
+  }
+  // signedAttributesNum = Bits2Num(252)(saHash[0..251]) (passportVerificationBuilder.circom:165-172)
+  const ShaJob job = L.sha[R.j_sa];
+  const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
+  fr sn = bits_to_fr(252, [&](int k) { return (H[k >> 5] >> (31 - (k & 31))) & 1u; });
+  vs.at(R.v_sanum, w) = fr_to_mont(sn);
+  if (bad) set_status(status ? status + w : nullptr, ST_INPUT_RANGE);
+}
+
+// ============================================================================ RSA core
+// Software 128/64 -> 64 division (Hacker's Delight divlu), requires u1 < v and v normalised.
+__device__ __forceinline__ uint64_t divlu(uint64_t u1, uint64_t u0, uint64_t v, uint64_t* rem) {
+  const uint64_t b = 1ull << 32;
+  uint64_t vn1 = v >> 32, vn0 = v & 0xffffffffull;
+  uint64_t un1 = u0 >> 32, un0 = u0 & 0xffffffffull;
+  uint64_t q1 = u1 / vn1, rhat = u1 - q1 * vn1;
+  while (q1 >= b || q1 * vn0 > b * rhat + un1) { q1--; rhat += vn1; if (rhat >= b) break; }
+  uint64_t un21 = u1 * b + un1 - q1 * v;
+  uint64_t q0 = un21 / vn1;
+  rhat = un21 - q0 * vn1;
+  while (q0 >= b || q0 * vn0 > b * rhat + un0) { q0--; rhat += vn1; if (rhat >= b) break; }
+  *rem = un21 * b + un0 - q0 * v;
+  return q1 * b + q0;
+}
+
+// 192-bit unsigned accumulator
+struct U192 {
+  uint64_t a0 = 0, a1 = 0, a2 = 0;
+  __device__ __forceinline__ void mac(uint64_t x, uint64_t y) {
+    uint64_t lo = x * y, hi = __umul64hi(x, y);
+    uint64_t s = a0 + lo; uint64_t c = s < lo; a0 = s;
+    uint64_t t = a1 + hi; uint64_t c2 = t < hi; uint64_t t2 = t + c; c2 += t2 < t; a1 = t2;
+    a2 += c2;
+  }
+};
+
+// per-lane LDS arrays, [index][lane] so a wave's accesses hit consecutive banks
+template <int NL>
+struct LaneArr {
+  uint64_t* base;
+  int lane;
+  __device__ __forceinline__ uint64_t& operator[](int i) const { return base[i * NL + lane]; }
+};
+
+template <int K>
+__host__ __device__ constexpr int rsa_lds_words() { return 7 * K + 2; }
+
+// RSA core for one witness lane (K limbs; NL lanes share the workgroup's LDS)
+template <int K, int NL>
+__device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core, int32_t* status, uint64_t* lds,
+                         int lane) {
+  LaneArr<NL> n{lds, lane}, x{lds + K * NL, lane}, y{lds + 2 * K * NL, lane}, u{lds + 3 * K * NL, lane},
+      q{lds + (5 * K + 1) * NL, lane}, vn{lds + (6 * K + 2) * NL, lane};
+  bool bad = false, badz = false;
+  for (int i = 0; i < K; i++) {
+    const uint8_t* e = row + 32ull * (L.reg.in_pk + i);
+    bad |= !in_is_u64(e);
+    n[i] = in_u64(e);
+  }
+  int nb = K;
+  while (nb > 1 && n[nb - 1] == 0) nb--;
+  const int s = __builtin_clzll(n[nb - 1] | 1ull);
+  for (int i = nb - 1; i > 0; i--) vn[i] = (n[i] << s) | (s ? n[i - 1] >> (64 - s) : 0ull);
+  vn[0] = n[0] << s;
+  constexpr int MMW = MM_CORE_WORDS(K);
+  for (int k = 0; k < 17; k++) {
+    uint64_t* mc = core + (size_t)k * MMW;
+    // operands (exp_to_bits(65537) = [16,2,0,16]): muls[k] = muls[k-1].mod^2 with muls[0] = base^2;
+    // resultMuls[0] = base * muls[15].mod (bigInt.circom:299-327)
+    for (int i = 0; i < K; i++) {
+      uint64_t xi;
+      if (k == 0 || k == 16) {
+        const uint8_t* e = row + 32ull * (L.reg.in_sig + i);
+        bad |= !in_is_u64(e);
+        xi = in_u64(e);
+      } else {
+        xi = core[(size_t)(k - 1) * MMW + 3 * K + 1 + i];
+      }
+      uint64_t yi = k == 16 ? core[(size_t)15 * MMW + 3 * K + 1 + i] : xi;
+      x[i] = xi; y[i] = yi;
+      mc[i] = xi; mc[K + i] = yi;
+    }
+    // exact product as 2K words
+    {
+      uint64_t c0 = 0, c1 = 0;
+      for (int i = 0; i < 2 * K; i++) {
+        U192 acc; acc.a0 = c0; acc.a1 = c1;
+        int lo = i < K ? 0 : i - K + 1, hi = i < K ? i : K - 1;
+        for (int j = lo; j <= hi; j++) acc.mac(x[j], y[i - j]);
+        u[i] = acc.a0; c0 = acc.a1; c1 = acc.a2;
+      }
+    }
+    // normalise into 2K+1 words
+    u[2 * K] = s ? u[2 * K - 1] >> (64 - s) : 0ull;
+    if (s) {
+      for (int i = 2 * K - 1; i > 0; i--) u[i] = (u[i] << s) | (u[i - 1] >> (64 - s));
+      u[0] = u[0] << s;
+    }
+    for (int j = 0; j <= K; j++) q[j] = 0;
+    const uint64_t vtop = vn[nb - 1], vsec = nb > 1 ? vn[nb - 2] : 0ull;
+    for (int j = 2 * K - nb; j >= 0; j--) {
+      uint64_t ujn = u[j + nb], ujn1 = u[j + nb - 1];
+      uint64_t qhat, rhat;
+      bool rhat_ovf = false;
+      if (ujn >= vtop) {
+        qhat = ~0ull;
+        rhat = ujn1 + vtop;
+        rhat_ovf = rhat < ujn1;
+      } else {
+        qhat = divlu(ujn, ujn1, vtop, &rhat);
+      }
+      if (nb > 1) {
+        for (int it = 0; it < 2 && !rhat_ovf; it++) {
+          uint64_t plo = qhat * vsec, phi = __umul64hi(qhat, vsec);
+          uint64_t u2 = u[j + nb - 2];
+          if (phi > rhat || (phi == rhat && plo > u2)) {
+            qhat--;
+            uint64_t r2 = rhat + vtop;
+            rhat_ovf = r2 < rhat;
+            rhat = r2;
+          } else {
+            break;
+          }
+        }
+      }
+      uint64_t borrow = 0, carry = 0;
+      for (int i = 0; i < nb; i++) {
+        uint64_t plo = qhat * vn[i], phi = __umul64hi(qhat, vn[i]);
+        plo += carry; phi += plo < carry; carry = phi;
+        uint64_t t = u[i + j];
+        uint64_t d = t - plo; uint64_t b1 = t < plo;
+        uint64_t d2 = d - borrow; uint64_t b2 = d < borrow;
+        u[i + j] = d2; borrow = b1 + b2;
+      }
+      uint64_t t = u[j + nb];
+      uint64_t d = t - carry; uint64_t b1 = t < carry;
+      uint64_t d2 = d - borrow; uint64_t b2 = d < borrow;
+      u[j + nb] = d2;
+      if (b1 + b2) {  // add back
+        qhat--;
+        uint64_t cy = 0;
+        for (int i = 0; i < nb; i++) {
+          uint64_t a = u[i + j], vb = vn[i];
+          uint64_t sm = a + vb; uint64_t ca = sm < a; uint64_t sm2 = sm + cy; uint64_t cb = sm2 < sm;
+          u[i + j] = sm2; cy = ca + cb;
+        }
+        u[j + nb] += cy;
+      }
+      q[j] = qhat;
+    }
+    uint64_t* qo = mc + 2 * K;      // q[K+1]
+    uint64_t* ro = mc + 3 * K + 1;  // r[K]
+    for (int i = 0; i <= K; i++) qo[i] = q[i];
+    for (int i = 0; i < K; i++) {
+      uint64_t r = 0;
+      if (i < nb) r = s ? (u[i] >> s) | (u[i + 1] << (64 - s)) : u[i];
+      ro[i] = r;
+    }
+    // IsEqual inverses of (r_i - n_i) (BigLessEqThan, bigIntComparators.circom:50-75) — one batched inversion
+    uint64_t* iv = mc + 4 * K + 1;  // K x 4 words, normal form
+    {
+      fr acc = fr_mont_one();
+      for (int i = 0; i < K; i++) {
+        uint64_t a = ro[i], b = n[i];
+        fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
+        d = fr_to_mont(d);
+        store_fr(reinterpret_cast<uint8_t*>(iv + 4 * i), acc);  // prefix product (exclusive)
+        if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+      }
+      fr inv = fr_inv(acc);
+      for (int i = K - 1; i >= 0; i--) {
+        uint64_t a = ro[i], b = n[i];
+        fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
+        d = fr_to_mont(d);
+        fr r = fr_zero();
+        if (!fr_is_zero(d)) {
+          r = fr_mul(inv, load_fr(reinterpret_cast<uint8_t*>(iv + 4 * i)));
+          inv = fr_mul(inv, d);
+        }
+        store_fr(reinterpret_cast<uint8_t*>(iv + 4 * i), fr_from_mont(r));
+      }
+    }
+    // BigIntIsZero carries (bigIntComparators.circom:105-129): c_i = (d_i + c_{i-1}) / 2^64 exactly,
+    // d_i = conv(x,y)_i - conv(q,n)_i - r_i   (signed, 256-bit two's complement)
+    uint64_t* cr = mc + 8 * K + 1;  // (2K-2) x (lo, hi)
+    {
+      uint64_t clo = 0, chi = 0;  // signed 128 carry
+      for (int i = 0; i < 2 * K - 1; i++) {
+        U192 a, b;
+        int lo = i < K ? 0 : i - K + 1, hi = i < K ? i : K - 1;
+        for (int j = lo; j <= hi; j++) a.mac(x[j], y[i - j]);
+        int lo2 = i < K ? 0 : i - K + 1, hi2 = i < K + 1 ? i : K;
+        for (int j = lo2; j <= hi2 && j <= K; j++) if (i - j < K) b.mac(q[j], n[i - j]);
+        // s = a - b - r_i + c (256-bit)
+        uint64_t s0, s1, s2, s3, br;
+        s0 = a.a0 - b.a0; br = a.a0 < b.a0;
+        uint64_t t1 = a.a1 - b.a1; uint64_t br1 = a.a1 < b.a1; s1 = t1 - br; br1 += t1 < br; br = br1;
+        uint64_t t2 = a.a2 - b.a2; uint64_t br2 = a.a2 < b.a2; s2 = t2 - br; br2 += t2 < br; br = br2;
+        s3 = 0 - br;
+        uint64_t rr = i < K ? ro[i] : 0ull;
+        uint64_t u0 = s0 - rr; uint64_t bb = s0 < rr; s0 = u0;
+        uint64_t u1 = s1 - bb; bb = s1 < bb; s1 = u1;
+        uint64_t u2 = s2 - bb; bb = s2 < bb; s2 = u2; s3 -= bb;
+        uint64_t csx = (int64_t)chi < 0 ? ~0ull : 0ull;  // sign extension of the carry
+        uint64_t v0 = s0 + clo; uint64_t cc = v0 < s0;
+        uint64_t v1 = s1 + chi; uint64_t cc1 = v1 < s1; uint64_t v1b = v1 + cc; cc1 += v1b < v1;
+        uint64_t v2 = s2 + csx; uint64_t cc2 = v2 < s2; uint64_t v2b = v2 + cc1; cc2 += v2b < v2;
+        uint64_t v3 = s3 + csx + cc2;
+        if (i < 2 * K - 2) {
+          badz |= v0 != 0;  // exact division by 2^64
+          clo = v1b; chi = v2b;
+          badz |= !((v3 == 0 && (int64_t)v2b >= 0) || (v3 == ~0ull && (int64_t)v2b < 0));
+          cr[2 * i] = clo; cr[2 * i + 1] = chi;
+        } else {
+          badz |= (v0 | v1b | v2b | v3) != 0;  // in[last] + carry[last-1] === 0
+        }
+      }
+    }
+  }
+  if (bad) set_status(status, ST_INPUT_RANGE);
+  if (badz) set_status(status, ST_BIGISZERO);
+}
+
+template <int K, int NL>
+__global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
+                                                 uint32_t batch) {
+  extern __shared__ uint64_t lds_rsa[];
+  uint32_t w = blockIdx.x * NL + threadIdx.x;
+  if (w >= batch) return;
+  rsa_lane<K, NL>(L, inputs + 32ull * (uint64_t)w * L.n_inputs, rsa_core + (size_t)w * L.rsa_core_words,
+                  status ? status + w : nullptr, lds_rsa, threadIdx.x);
+}
+
+// ============================================================================ BabyJubJub core
+// twisted Edwards a x^2 + y^2 = 1 + d x^2 y^2, a = 168700, d = 168696 (babyjubjub/curve.circom:62-70)
+struct ExtPt { fr X, Y, Z, T; };
+
+__device__ __forceinline__ ExtPt bjj_dbl(const ExtPt& P, const fr& A) {  // dbl-2008-hwcd
+  fr a = fr_sqr(P.X), b = fr_sqr(P.Y), c = fr_sqr(P.Z);
+  c = fr_add(c, c);
+  fr d = fr_mul(A, a);
+  fr xy = fr_add(P.X, P.Y);
+  fr e = fr_sub(fr_sub(fr_sqr(xy), a), b);
+  fr g = fr_add(d, b), f = fr_sub(g, c), h = fr_sub(d, b);
+  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+}
+__device__ __forceinline__ ExtPt bjj_add_affine(const ExtPt& P, const fr& x2, const fr& y2, const fr& t2d, const fr& A) {
+  // add-2008-hwcd with Z2 = 1, t2d = d * x2 * y2
+  fr a = fr_mul(P.X, x2), b = fr_mul(P.Y, y2), c = fr_mul(P.T, t2d), d = P.Z;
+  fr e = fr_sub(fr_sub(fr_mul(fr_add(P.X, P.Y), fr_add(x2, y2)), a), b);
+  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, fr_mul(A, a));
+  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+}
+
+// Base8 (babyjubjub/get.circom:9-10), normal form; 1/Base8.x (IsZero of adders' in2)
+constexpr uint32_t BJJ_B8X[8] = {0xbb957051u, 0x2893f3f6u, 0x0534e0b6u, 0x2ab8d801u,
+                                 0x9d6277c1u, 0x4eacb2e0u, 0xd63e739bu, 0x0bb77a6au};
+constexpr uint32_t BJJ_B8Y[8] = {0x872d7d8bu, 0x4b3c257au, 0xb9e13377u, 0xfce0051fu,
+                                 0xd16bf9edu, 0x25572e1cu, 0xf7a0b249u, 0x25797203u};
+constexpr uint32_t BJJ_INV_B8X[8] = {0x7bc45854u, 0x42cd5135u, 0x5936d873u, 0x5dc5f319u,
+                                     0x40d1c783u, 0x40e2c828u, 0xcaabb2bdu, 0x0b1a7dddu};
+constexpr uint64_t BJJ_A = 168700, BJJ_D = 168696;
+
+struct BjjConsts {
+  fr A, D, B8x, B8y, B8t_d;  // Montgomery
+  __device__ __forceinline__ void init() {
+    A = fr_to_mont(fr_u64(BJJ_A)); D = fr_to_mont(fr_u64(BJJ_D));
+    B8x = fr_to_mont(fr_const(BJJ_B8X)); B8y = fr_to_mont(fr_const(BJJ_B8Y));
+    B8t_d = fr_mul(fr_mul(D, B8x), B8y);
+  }
+};
+
+// scratch: SoA [elem][witness] with 3 * 2 * 254 (X, Y, Z of D_i and A_i) + 3 * 254 prefix products
+__global__ void k_bjj_core(DevLayout L, ValueStore vs, fr* bjj_core, fr* scratch, uint32_t batch) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  BjjConsts C;
+  C.init();
+  const int NS = BJJ_STEPS;
+  auto S = [&](int e) -> fr& { return scratch[(size_t)e * batch + w]; };
+  // projective coords of D_i (elems 0..3NS) and A_i (3NS..6NS): [X, Y, Z] per step
+  fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
+  bool have = false;  // A_{i-1} is a real point (not the (0,0) sentinel)
+  ExtPt A;
+  for (int i = 0; i < NS; i++) {
+    int bit = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
+    ExtPt D;
+    bool haveD = false;
+    if (i > 0 && have) { D = bjj_dbl(A, C.A); haveD = true; }
+    if (haveD) { S(3 * i) = D.X; S(3 * i + 1) = D.Y; S(3 * i + 2) = D.Z; }
+    else { S(3 * i) = fr_zero(); S(3 * i + 1) = fr_zero(); S(3 * i + 2) = fr_zero(); }
+    if (bit) {
+      if (haveD) A = bjj_add_affine(D, C.B8x, C.B8y, C.B8t_d, C.A);
+      else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = fr_mul(C.B8x, C.B8y); }
+      have = true;
+    } else {
+      if (haveD) A = D;
+      have = haveD;
+    }
+    if (have) { S(3 * NS + 3 * i) = A.X; S(3 * NS + 3 * i + 1) = A.Y; S(3 * NS + 3 * i + 2) = A.Z; }
+    else { S(3 * NS + 3 * i) = fr_zero(); S(3 * NS + 3 * i + 1) = fr_zero(); S(3 * NS + 3 * i + 2) = fr_zero(); }
+  }
+  // batch inversion of Z(D_i), Z(A_i), X(D_i): index list q -> element
+  auto elem = [&](int qi) -> fr {
+    int st = qi / 3, kind = qi - 3 * st;
+    return kind == 0 ? S(3 * st + 2) : kind == 1 ? S(3 * NS + 3 * st + 2) : S(3 * st);
+  };
+  const int NQ = 3 * NS;
+  const int PRE = 6 * NS;
+  fr acc = fr_mont_one();
+  for (int qi = 0; qi < NQ; qi++) {
+    fr e = elem(qi);
+    S(PRE + qi) = acc;
+    if (!fr_is_zero(e)) acc = fr_mul(acc, e);
+  }
+  fr inv = fr_inv(acc);
+  fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
+  for (int qi = NQ - 1; qi >= 0; qi--) {
+    fr e = elem(qi);
+    fr r = fr_zero();
+    if (!fr_is_zero(e)) { r = fr_mul(inv, S(PRE + qi)); inv = fr_mul(inv, e); }
+    int st = qi / 3, kind = qi - 3 * st;
+    fr* o = out + 5 * st;  // Dx, Dy, Ax, Ay, inv(Dx)
+    if (kind == 0) { o[0] = fr_mul(S(3 * st), r); o[1] = fr_mul(S(3 * st + 1), r); }
+    else if (kind == 1) { o[2] = fr_mul(S(3 * NS + 3 * st), r); o[3] = fr_mul(S(3 * NS + 3 * st + 1), r); }
+    else { o[4] = fr_mul(S(3 * st + 2), r); }  // 1/x = Z / X
+  }
+  vs.at(L.reg.v_bjj, w) = out[5 * (NS - 1) + 2];
+  vs.at(L.reg.v_bjj + 1, w) = out[5 * (NS - 1) + 3];
+}
+
+// ============================================================================ SMT
+// flags per level (u32 in the SMT core): bit0 levIns, bit1 done, bit2 st_top, bit3 st_inew, bit4 lrbit, bit5 isZero
+// SMT core (Fr): [inv(sibling) normal][80] [root Montgomery][80] [flags][80] [j, inv(root_in - root_0)]
+__global__ void k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
+                           uint32_t batch) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  const RegInfo& R = L.reg;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  fr* core = smt_core + (size_t)w * L.smt_core_fr;
+  uint32_t* flags = reinterpret_cast<uint32_t*>(core + 2 * SMT_LEVELS);
+  fr key = fr_from_mont(vs.at(R.v_pkhash, w));
+  int iz[SMT_LEVELS];
+  // inverses of the siblings (SMTLevIns isZero, SMTVerifier.circom:47-50), batched
+  fr acc = fr_mont_one();
+  for (int i = 0; i < SMT_LEVELS; i++) {
+    fr s = load_fr(row + 32ull * (R.in_br + i));
+    iz[i] = fr_is_zero(s);
+    core[i] = acc;
+    if (!iz[i]) acc = fr_mul(acc, fr_to_mont(s));
+  }
+  fr inv = fr_inv(acc);
+  for (int i = SMT_LEVELS - 1; i >= 0; i--) {
+    fr r = fr_zero();
+    if (!iz[i]) {
+      fr sm = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
+      r = fr_mul(inv, core[i]);
+      inv = fr_mul(inv, sm);
+    }
+    core[i] = fr_from_mont(r);
+  }
+  if (!iz[SMT_LEVELS - 1]) set_status(status ? status + w : nullptr, ST_SMT_LAST);
+  // SMTLevIns (SMTVerifier.circom:39-65)
+  int lev[SMT_LEVELS], done[SMT_LEVELS];
+  lev[SMT_LEVELS - 1] = 1 - iz[SMT_LEVELS - 2];
+  done[SMT_LEVELS - 2] = lev[SMT_LEVELS - 1];
+  done[SMT_LEVELS - 1] = 0;
+  for (int i = SMT_LEVELS - 2; i > 0; i--) {
+    lev[i] = (1 - done[i]) * (1 - iz[i - 1]);
+    done[i - 1] = lev[i] + done[i];
+  }
+  lev[0] = 1 - done[0];
+  // SMTVerifierSM chain and the insertion level j
+  int prev_top = 1, j = SMT_LEVELS;
+  for (int i = 0; i < SMT_LEVELS; i++) {
+    int st_inew = prev_top * lev[i], st_top = prev_top - st_inew;
+    if (st_inew) j = i;
+    int lr = (key.v[i >> 5] >> (i & 31)) & 1;
+    flags[i] = (uint32_t)(lev[i] & 1) | ((uint32_t)(done[i] & 1) << 1) | ((uint32_t)(st_top & 1) << 2) |
+               ((uint32_t)(st_inew & 1) << 3) | ((uint32_t)lr << 4) | ((uint32_t)iz[i] << 5);
+    prev_top = st_top;
+  }
+  reinterpret_cast<uint32_t*>(core + 3 * SMT_LEVELS)[0] = (uint32_t)j;
+  // level hashes whose child is 0 (i >= j): inputs known now
+  for (int i = (j < SMT_LEVELS ? j : 0); i < SMT_LEVELS; i++) {
+    fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
+    int lr = (flags[i] >> 4) & 1;
+    vs.at(R.v_smt_lr + 2 * i, w) = lr ? sib : fr_zero();
+    vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? fr_zero() : sib;
+  }
+}
+
+// sequential part: levels j-1 .. 0, then all roots and the isEqual inverse
+__global__ void k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs, ValueStore vs,
+                            fr* pos_core, fr* smt_core, uint32_t batch) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  const RegInfo& R = L.reg;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  fr* core = smt_core + (size_t)w * L.smt_core_fr;
+  const uint32_t* flags = reinterpret_cast<const uint32_t*>(core + 2 * SMT_LEVELS);
+  int j = (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0];
+  fr leaf = vs.at(R.v_leaf, w);
+  fr child = leaf;  // root_j = leaf
+  for (int i = (j < SMT_LEVELS ? j : SMT_LEVELS) - 1; i >= 0; i--) {
+    fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
+    int lr = (flags[i] >> 4) & 1;
+    vs.at(R.v_smt_lr + 2 * i, w) = lr ? sib : child;
+    vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? child : sib;
+    pos_core_lane<3>(K, L.pos[level_task[i]], vs, w, pos_core + (size_t)w * L.pos_core_elems);
+    child = vs.at(R.v_smt_h + i, w);  // root_i = H_i (st_top = 1 below the insertion level)
+  }
+  // roots of every level: root_i = st_top_i * H_i + st_inew_i * leaf (SMTVerifier.circom:104-106)
+  fr* roots = core + SMT_LEVELS;
+  for (int i = 0; i < SMT_LEVELS; i++) {
+    uint32_t f = flags[i];
+    fr r = fr_zero();
+    if (f & 4) r = vs.at(R.v_smt_h + i, w);
+    if (f & 8) r = fr_add(r, leaf);
+    roots[i] = r;
+  }
+  // isEqual(root_0, root): inverse of root - root_0
+  fr rin = fr_to_mont(load_fr(row + 32ull * R.in_root));
+  fr dlt = fr_sub(rin, roots[0]);
+  core[3 * SMT_LEVELS + 1] = fr_inv(dlt);
+}
+
+}  // namespace pzk

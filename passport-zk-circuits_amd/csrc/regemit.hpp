@@ -1,0 +1,641 @@
+// Emit (signal-parallel) generators of the RegisterIdentityBuilder regions.
+//
+// Every function maps a region-local signal index to its value in closed form from the
+// per-witness cores (regcore.hpp, sha.hpp, poseidon.hpp) — no sequential dependency, so
+// consecutive lanes store consecutive 32-byte witness elements.
+#pragma once
+#include "bufs.hpp"
+#include "fr.hpp"
+#include "layout.hpp"
+#include "poseidon.hpp"
+#include "regcore.hpp"
+#include "sha.hpp"
+
+namespace pzk {
+
+
+// ------------------------------------------------------------------ 256-bit helpers
+struct W256 { uint32_t v[8]; };
+__device__ __forceinline__ W256 w_zero() { W256 r; for (int i = 0; i < 8; i++) r.v[i] = 0; return r; }
+__device__ __forceinline__ W256 w_u64(uint64_t x) { W256 r = w_zero(); r.v[0] = (uint32_t)x; r.v[1] = (uint32_t)(x >> 32); return r; }
+__device__ __forceinline__ W256 w_mask(const W256& a, int nbits) {  // a mod 2^nbits
+  W256 r = a;
+  for (int i = 0; i < 8; i++) {
+    int lo = 32 * i;
+    if (nbits <= lo) r.v[i] = 0;
+    else if (nbits < lo + 32) r.v[i] &= (1u << (nbits - lo)) - 1u;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t w_bit(const W256& a, int i) { return (a.v[i >> 5] >> (i & 31)) & 1u; }
+__device__ __forceinline__ void store_w(uint8_t* dst, const W256& a) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+__device__ __forceinline__ W256 w_from_fr(const fr& a) { W256 r; for (int i = 0; i < 8; i++) r.v[i] = a.v[i]; return r; }
+__device__ __forceinline__ fr fr_from_w(const W256& a) { fr r; for (int i = 0; i < 8; i++) r.v[i] = a.v[i]; return r; }
+__device__ __forceinline__ void copy_el(uint8_t* dst, const uint8_t* src) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  d4[0] = s4[0]; d4[1] = s4[1];
+}
+__device__ __forceinline__ const uint32_t* sha_hout(const DevLayout& L, const Bufs& B, uint32_t w, int job) {
+  const ShaJob& J = L.sha[job];
+  return B.sha_core + (size_t)w * L.sha_core_words + J.core_off + J.blocks * SHA_BLOCK_CORE;
+}
+__device__ __forceinline__ uint32_t digest_bit(const uint32_t* H, int i) { return (H[i >> 5] >> (31 - (i & 31))) & 1u; }
+
+// ------------------------------------------------------------------ generic small regions
+// returns true and writes the element; the value source is per kind
+__device__ __forceinline__ void emit_small(const DevLayout& L, const Bufs& B, const Region& R, uint32_t w, uint32_t s,
+                                           uint8_t* dst) {
+  const RegInfo& G = L.reg;
+  const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
+  const fr* smt = B.smt_core + (size_t)w * L.smt_core_fr;
+  const uint32_t* flags = reinterpret_cast<const uint32_t*>(smt + 2 * SMT_LEVELS);
+  auto V = [&](int slot) { return fr_from_mont(B.vs.at(slot, w)); };
+  switch (R.kind) {
+    case RK_ONE: store_u64(dst, 1); return;
+    case RK_INCOPY: copy_el(dst, row + 32ull * ((uint64_t)R.a[0] + s)); return;
+    case RK_VALUE: {
+      int slot = R.a[0] >= 0 ? R.a[0] + (int)s : R.a[0] == -2 ? -2 : R.a[1 + s];
+      if (slot < 0) store_u64(dst, 0);
+      else store_fr(dst, V(slot));
+      return;
+    }
+    case RK_DIGEST: store_u64(dst, digest_bit(sha_hout(L, B, w, R.a[0]), (int)s)); return;
+    case RK_TEMPMOD: {
+      const uint8_t* a = row + 32ull * (R.a[0] + 3 * s);
+      const uint8_t* b = row + 32ull * (R.a[0] + 3 * s + 1);
+      if (in_is_u64(a) && in_is_u64(b)) {
+        uint64_t la = in_u64(a), lb = in_u64(b);
+        W256 r = w_zero();
+        r.v[2] = (uint32_t)lb; r.v[3] = (uint32_t)(lb >> 32); r.v[4] = (uint32_t)la; r.v[5] = (uint32_t)(la >> 32);
+        store_w(dst, r);
+      } else {
+        fr t64 = fr_zero(); t64.v[2] = 1;
+        fr t128 = fr_zero(); t128.v[4] = 1;
+        fr v = fr_add(fr_mul(fr_to_mont(load_fr(a)), fr_to_mont(t128)), fr_mul(fr_to_mont(load_fr(b)), fr_to_mont(t64)));
+        store_fr(dst, fr_from_mont(v));
+      }
+      return;
+    }
+    case RK_HCHUNK: {
+      const uint32_t* H = sha_hout(L, B, w, R.a[0]);
+      int wd = 3 - (int)s;
+      store_u64(dst, ((uint64_t)H[2 * wd] << 32) | H[2 * wd + 1]);
+      return;
+    }
+    case RK_RSA_OUT: {
+      const uint64_t* mc = B.rsa_core + (size_t)w * L.rsa_core_words + (size_t)(G.n_modmul - 1) * MM_CORE_WORDS(G.K);
+      store_u64(dst, mc[3 * G.K + 1 + s]);
+      return;
+    }
+    case RK_SMT_OWN: {  // isVerified | root, leaf, key, siblings[80] | value
+      if (s == 0) {
+        fr r0 = fr_from_mont(smt[SMT_LEVELS]);
+        store_u64(dst, fr_eq(r0, load_fr(row + 32ull * R.a[0])) ? 1 : 0);
+      } else if (s == 1) copy_el(dst, row + 32ull * R.a[0]);
+      else if (s == 2 || s == 3 || s == 84) store_fr(dst, V(G.v_pkhash));
+      else copy_el(dst, row + 32ull * (R.a[1] + s - 4));
+      return;
+    }
+    case RK_SMTHASH: {
+      int lv = R.a[0];
+      if (lv < 0) store_fr(dst, s == 0 ? V(G.v_leaf) : V(G.v_pkhash));
+      else store_fr(dst, s == 0 ? V(G.v_smt_h + lv) : V(G.v_smt_lr + 2 * lv + (int)s - 1));
+      return;
+    }
+    case RK_LEVINS: {  // levIns[80] | siblings[80] | done[79] | isZero[80] (out, in, inv)
+      if (s < 80) { store_u64(dst, flags[s] & 1); return; }
+      if (s < 160) { copy_el(dst, row + 32ull * (R.a[0] + s - 80)); return; }
+      if (s < 239) { store_u64(dst, (flags[s - 160] >> 1) & 1); return; }
+      uint32_t i = (s - 239) / 3, k = (s - 239) % 3;
+      if (k == 0) store_u64(dst, (flags[i] >> 5) & 1);
+      else if (k == 1) copy_el(dst, row + 32ull * (R.a[0] + i));
+      else store_fr(dst, smt[i]);
+      return;
+    }
+    case RK_SM: {  // st_top, st_inew | levIns, prev_top
+      uint32_t i = s >> 2, k = s & 3;
+      uint32_t v = k == 0 ? (flags[i] >> 2) & 1 : k == 1 ? (flags[i] >> 3) & 1 : k == 2 ? flags[i] & 1
+                                                                              : (i == 0 ? 1u : (flags[i - 1] >> 2) & 1);
+      store_u64(dst, v);
+      return;
+    }
+    case RK_SMT_LEVEL: {  // root | st_top, st_inew, sibling, new1leaf, lrbit, child | fromProof
+      int i = R.a[0];
+      uint32_t f = flags[i];
+      switch (s) {
+        case 0: store_fr(dst, fr_from_mont(smt[SMT_LEVELS + i])); break;
+        case 1: store_u64(dst, (f >> 2) & 1); break;
+        case 2: store_u64(dst, (f >> 3) & 1); break;
+        case 3: copy_el(dst, row + 32ull * (R.a[1] + i)); break;
+        case 4: store_fr(dst, V(G.v_leaf)); break;
+        case 5: store_u64(dst, (f >> 4) & 1); break;
+        case 6: store_fr(dst, i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1])); break;
+        default: store_fr(dst, (f & 4) ? V(G.v_smt_h + i) : fr_zero()); break;
+      }
+      return;
+    }
+    case RK_SWITCHER: {  // out[2] | bool, in[2] | aux
+      int i = R.a[0];
+      uint32_t lr = (flags[i] >> 4) & 1;
+      if (s < 2) { store_fr(dst, V(G.v_smt_lr + 2 * i + (int)s)); return; }
+      if (s == 2) { store_u64(dst, lr); return; }
+      fr child = i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1]);
+      fr sib = load_fr(row + 32ull * (R.a[1] + i));
+      if (s == 3) store_fr(dst, child);
+      else if (s == 4) copy_el(dst, row + 32ull * (R.a[1] + i));
+      else store_fr(dst, lr ? fr_sub(sib, child) : fr_zero());
+      return;
+    }
+    case RK_ISEQ_ROOT: {  // out | in[2] | IsZero(out, in, inv)
+      fr r0 = fr_from_mont(smt[SMT_LEVELS]);
+      fr rin = load_fr(row + 32ull * R.a[0]);
+      uint32_t eq = fr_eq(r0, rin);
+      if (s == 0 || s == 3) store_u64(dst, eq);
+      else if (s == 1) store_fr(dst, r0);
+      else if (s == 2) copy_el(dst, row + 32ull * R.a[0]);
+      else if (s == 4) store_fr(dst, fr_sub(rin, r0));
+      else store_fr(dst, fr_from_mont(smt[3 * SMT_LEVELS + 1]));
+      return;
+    }
+    case RK_BJJ_OWN: {  // out[2] | scalar | base8[2]
+      const fr* bc = B.bjj_core + (size_t)w * L.bjj_core_fr + 5 * (BJJ_STEPS - 1);
+      if (s < 2) store_fr(dst, fr_from_mont(bc[2 + s]));
+      else if (s == 2) store_fr(dst, V(G.v_sk));
+      else {
+        W256 r; for (int i = 0; i < 8; i++) r.v[i] = s == 3 ? BJJ_B8X[i] : BJJ_B8Y[i];
+        store_w(dst, r);
+      }
+      return;
+    }
+    default: store_u64(dst, 0); return;
+  }
+}
+
+// ------------------------------------------------------------------ Bits2Num / Num2Bits (+ AliasCheck)
+// one workgroup per (region, witness): the L-bit value is assembled in LDS first.
+__device__ __forceinline__ void u192_add(uint64_t* a, uint64_t lo, uint64_t hi) {
+  uint64_t s = a[0] + lo; uint64_t c = s < lo; a[0] = s;
+  uint64_t t = a[1] + hi; uint64_t c2 = t < hi; uint64_t t2 = t + c; c2 += t2 < t; a[1] = t2; a[2] += c2;
+}
+
+// CompConstant(p-1) part i (compconstant.circom:28-46): a = 2^i, b = 2^128 - 2^i
+__device__ __forceinline__ void alias_part(const W256& bits, int i, uint64_t& lo, uint64_t& hi) {
+  fr pm1 = fr_const(P_); pm1.v[0] -= 1;
+  uint32_t cl = (pm1.v[(2 * i) >> 5] >> ((2 * i) & 31)) & 1, cm = (pm1.v[(2 * i + 1) >> 5] >> ((2 * i + 1) & 31)) & 1;
+  uint32_t sl = w_bit(bits, 2 * i), sm = w_bit(bits, 2 * i + 1);
+  // which of {0, a, b}
+  int sel;
+  if (!cm && !cl) sel = (sm | sl) ? 2 : 0;
+  else if (!cm && cl) sel = sm ? 2 : (sl ? 0 : 1);
+  else if (cm && !cl) sel = sm ? (sl ? 2 : 0) : 1;
+  else sel = (sm & sl) ? 0 : 1;
+  uint64_t alo = i < 64 ? (1ull << i) : 0, ahi = i >= 64 ? (1ull << (i - 64)) : 0;
+  if (sel == 0) { lo = 0; hi = 0; }
+  else if (sel == 1) { lo = alo; hi = ahi; }
+  else { lo = 0 - alo; hi = ~0ull - ahi + (alo == 0 ? 1 : 0); if (alo == 0) hi = 0 - ahi; }
+}
+
+__device__ __forceinline__ W256 u192_w(const uint64_t* a) {
+  W256 r = w_zero();
+  for (int i = 0; i < 3; i++) { r.v[2 * i] = (uint32_t)a[i]; r.v[2 * i + 1] = (uint32_t)(a[i] >> 32); }
+  return r;
+}
+
+// AliasCheck block (908 signals) over bits of V; sout precomputed
+__device__ __forceinline__ W256 alias_sig(const W256& V, const uint64_t* sout, uint32_t s) {
+  if (s < 254) return w_u64(w_bit(V, s));                   // AliasCheck.in
+  s -= 254;
+  W256 so = u192_w(sout);
+  if (s == 0) return w_u64(w_bit(so, 127));                 // CompConstant.out
+  if (s < 255) return w_u64(w_bit(V, s - 1));               // CompConstant.in
+  if (s < 382) { uint64_t lo, hi; alias_part(V, s - 255, lo, hi); W256 r = w_zero();
+    r.v[0] = (uint32_t)lo; r.v[1] = (uint32_t)(lo >> 32); r.v[2] = (uint32_t)hi; r.v[3] = (uint32_t)(hi >> 32); return r; }
+  if (s == 382) return so;                                  // sout
+  s -= 383;                                                 // Num2Bits(135)(sout)
+  if (s < 135) return w_u64(w_bit(so, s));
+  if (s == 135) return so;
+  return w_mask(so, (int)s - 135);
+}
+
+__global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work, Bufs B) {
+  __shared__ uint32_t val[8];
+  __shared__ uint64_t sout[3];
+  __shared__ fr inval;
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const int Lb = R.a[0];
+  const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
+  if (threadIdx.x < 8) val[threadIdx.x] = 0;
+  if (threadIdx.x < 3) sout[threadIdx.x] = 0;
+  __syncthreads();
+  const bool b2n = R.kind == RK_BITS2NUM;
+  const uint32_t* H = (b2n && R.a[1] == 1) ? sha_hout(L, B, w, R.a[4]) : nullptr;
+  auto src_bit = [&](int j) -> uint32_t {
+    int idx = R.a[2] + R.a[3] * j;
+    if (R.a[1] == 1) return digest_bit(H, idx);
+    return *(row + 32ull * idx) & 1u;
+  };
+  if (b2n) {
+    for (int j = threadIdx.x; j < Lb; j += blockDim.x)
+      if (src_bit(j)) atomicOr(&val[j >> 5], 1u << (j & 31));
+  } else if (threadIdx.x == 0) {
+    fr v;
+    if (R.a[1] == 0) v = fr_from_mont(B.vs.at(R.a[2], w));
+    else v = fr_u64(B.rsa_core[(size_t)w * L.rsa_core_words + (size_t)(L.reg.n_modmul - 1) * MM_CORE_WORDS(L.reg.K) +
+                               3 * L.reg.K + 1 + R.a[2]]);
+    inval = v;
+    for (int i = 0; i < 8; i++) val[i] = v.v[i];
+    // bits beyond L are ignored by Num2Bits' outputs; in === sum is checked against the full value
+    W256 vv; for (int i = 0; i < 8; i++) vv.v[i] = v.v[i];
+    W256 m = w_mask(vv, Lb);
+    bool ok = true; for (int i = 0; i < 8; i++) ok &= m.v[i] == vv.v[i];
+    if (!ok && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_NUM2BITS);
+  }
+  __syncthreads();
+  W256 V; for (int i = 0; i < 8; i++) V.v[i] = val[i];
+  if (Lb == 254) {
+    if (threadIdx.x == 0) {
+      uint64_t acc[3] = {0, 0, 0};
+      for (int i = 0; i < 127; i++) { uint64_t lo, hi; alias_part(V, i, lo, hi); u192_add(acc, lo, hi); }
+      sout[0] = acc[0]; sout[1] = acc[1]; sout[2] = acc[2];
+      W256 so = u192_w(acc);
+      if (w_bit(so, 127) && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_ALIAS);
+    }
+    __syncthreads();
+  }
+  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint32_t s = wk.start + q;
+    uint8_t* dst = out + 32ull * q;
+    if (s > 2u * Lb) { store_w(dst, alias_sig(V, sout, s - 2 * Lb - 1)); continue; }
+    if (b2n) {
+      if (s == 0) store_w(dst, V);
+      else if (s <= (uint32_t)Lb) {
+        int idx = R.a[2] + R.a[3] * (int)(s - 1);
+        if (R.a[1] == 1) store_u64(dst, digest_bit(H, idx));
+        else copy_el(dst, row + 32ull * idx);
+      } else store_w(dst, w_mask(V, (int)(s - Lb)));
+    } else {
+      if (s < (uint32_t)Lb) store_u64(dst, w_bit(V, s));
+      else if (s == (uint32_t)Lb) store_fr(dst, inval);
+      else store_w(dst, w_mask(V, (int)(s - Lb)));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ PassportVerificationFlow
+__global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work, Bufs B) {
+  __shared__ uint8_t eq[776], chain[776];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const int jd1 = R.a[0], jd15 = R.a[1], jec = R.a[2], jsa = R.a[3], in_ec = R.a[4], in_sa = R.a[5];
+  const int d1s = R.a[6], d15s = R.a[7], ecs = R.a[8], V = R.a[9];
+  const int ecLen = 512 * L.sha[jec].blocks;
+  const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
+  const uint32_t* H1 = sha_hout(L, B, w, jd1);
+  const uint32_t* H15 = jd15 >= 0 ? sha_hout(L, B, w, jd15) : nullptr;
+  const uint32_t* HE = sha_hout(L, B, w, jec);
+  auto ebit = [&](int i) -> uint32_t { return *(row + 32ull * (in_ec + i)) & 1u; };
+  auto sbit = [&](int i) -> uint32_t { return *(row + 32ull * (in_sa + i)) & 1u; };
+  auto pair = [&](int k, uint32_t& a, uint32_t& b) {  // IsEqual k: in[0], in[1]
+    int g = k >> 8, i = k & 255;
+    if (g == 0) { a = digest_bit(H1, i); b = ebit(d1s + i); }
+    else if (g == 1) { a = H15 ? digest_bit(H15, i) * V : 0; b = ebit(d15s + i) * V; }
+    else if (g == 2) { a = digest_bit(HE, i); b = sbit(ecs + i); }
+    else { a = (i >= 4 ? 1u : 0u) * V; b = ebit(d15s - 24 + i) * V; }  // 0x0F prefix, MSB first
+  };
+  for (int k = threadIdx.x; k < 776; k += blockDim.x) { uint32_t a, b; pair(k, a, b); eq[k] = a == b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint8_t c = 1;
+    for (int k = 0; k < 776; k++) { c &= eq[k]; chain[k] = c; }
+    if (!c && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_FLOW);
+  }
+  __syncthreads();
+  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  const uint32_t o_d1 = 1, o_d15 = 257, o_ec = 513, o_eh = o_ec + ecLen, o_sa = o_eh + 256, o_v = o_sa + 1024,
+                 o_eq = o_v + 776;
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint32_t s = wk.start + q;
+    uint8_t* dst = out + 32ull * q;
+    if (s == 0) store_u64(dst, chain[775]);
+    else if (s < o_d15) store_u64(dst, digest_bit(H1, s - o_d1));
+    else if (s < o_ec) store_u64(dst, H15 ? digest_bit(H15, s - o_d15) : 0);
+    else if (s < o_eh) copy_el(dst, row + 32ull * (in_ec + s - o_ec));
+    else if (s < o_sa) store_u64(dst, digest_bit(HE, s - o_eh));
+    else if (s < o_v) copy_el(dst, row + 32ull * (in_sa + s - o_sa));
+    else if (s < o_eq) store_u64(dst, chain[s - o_v]);
+    else {
+      uint32_t k = (s - o_eq) / 6, t = (s - o_eq) % 6;
+      uint32_t a, b; pair(k, a, b);
+      // IsEqual: out | in[0], in[1] | IsZero: out, in = in[1]-in[0], inv
+      if (t == 0 || t == 3) store_u64(dst, a == b);
+      else if (t == 1) store_u64(dst, a);
+      else if (t == 2) store_u64(dst, b);
+      else {
+        int d = (int)b - (int)a;  // in {-1, 0, 1}; inverse of +-1 is itself
+        if (d >= 0) store_u64(dst, (uint64_t)d);
+        else store_fr(dst, fr_sub(fr_zero(), fr_u64(1)));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ BigMultModP
+struct MMCore {
+  int K;
+  const uint64_t *x, *y, *q, *r, *n, *inv, *cr;  // LDS
+  __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
+};
+
+// value of Karatsuba node input j under offset mask O: sum of limbs a[j + o], o in O (<= 2^70)
+__device__ __forceinline__ void kara_in(const uint64_t* a, uint64_t O, int j, uint64_t& lo, uint64_t& hi) {
+  lo = 0; hi = 0;
+  while (O) { int o = __builtin_ctzll(O); O &= O - 1; uint64_t v = a[j + o]; lo += v; hi += lo < v; }
+}
+// U192 += (alo + ahi 2^64) * (blo + bhi 2^64), ahi, bhi < 2^8
+__device__ __forceinline__ void mac2(U192& acc, uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi) {
+  acc.mac(alo, blo);
+  uint64_t m1 = alo * bhi, m1h = __umul64hi(alo, bhi), m2 = blo * ahi, m2h = __umul64hi(blo, ahi);
+  uint64_t s = acc.a1 + m1; uint64_t c = s < m1; uint64_t s2 = s + m2; c += s2 < s; acc.a1 = s2;
+  acc.a2 += m1h + m2h + c + ahi * bhi;
+}
+__device__ __forceinline__ W256 u192w(const U192& a) {
+  W256 r = w_zero();
+  r.v[0] = (uint32_t)a.a0; r.v[1] = (uint32_t)(a.a0 >> 32); r.v[2] = (uint32_t)a.a1; r.v[3] = (uint32_t)(a.a1 >> 32);
+  r.v[4] = (uint32_t)a.a2; r.v[5] = (uint32_t)(a.a2 >> 32);
+  return r;
+}
+__host__ __device__ inline uint32_t kara_size(int N) { return N == 1 ? 4 : 4 * N + 3 * kara_size(N / 2); }
+
+// Karatsuba subtree signal (bigIntHelpers.circom:11-53)
+__device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
+  uint64_t O = 1;  // offsets set (bit o = offset o)
+  for (;;) {
+    if (s < (uint32_t)(2 * N)) {
+      if (s == (uint32_t)(2 * N - 1)) return w_zero();  // top coefficient (K(1).out[1] never assigned)
+      U192 acc;
+      int lo = s < (uint32_t)N ? 0 : (int)s - N + 1, hi = s < (uint32_t)N ? (int)s : N - 1;
+      for (int u = lo; u <= hi; u++) {
+        uint64_t al, ah, bl, bh;
+        kara_in(C.x, O, u, al, ah);
+        kara_in(C.y, O, (int)s - u, bl, bh);
+        mac2(acc, al, ah, bl, bh);
+      }
+      return u192w(acc);
+    }
+    if (s < (uint32_t)(4 * N)) {
+      const uint64_t* a = s < (uint32_t)(3 * N) ? C.x : C.y;
+      uint64_t lo, hi;
+      kara_in(a, O, (int)(s - (s < (uint32_t)(3 * N) ? 2 * N : 3 * N)), lo, hi);
+      W256 r = w_zero(); r.v[0] = (uint32_t)lo; r.v[1] = (uint32_t)(lo >> 32); r.v[2] = (uint32_t)hi;
+      return r;
+    }
+    s -= 4 * N;
+    int h = N / 2;
+    uint32_t cs = kara_size(h), c = s / cs;
+    s -= c * cs;
+    if (c == 1) O <<= h;
+    else if (c == 2) O |= O << h;
+    N = h;
+  }
+}
+
+// signed 256-bit (two's complement in W256) -> normal-form field element
+__device__ __forceinline__ W256 w_signed_to_fr(const W256& a) {
+  if (!(a.v[7] >> 31)) return a;
+  W256 m; uint64_t c = 1;
+  for (int i = 0; i < 8; i++) { uint64_t t = (uint64_t)(~a.v[i]) + c; m.v[i] = (uint32_t)t; c = t >> 32; }
+  return w_from_fr(fr_sub(fr_zero(), fr_from_w(m)));
+}
+__device__ __forceinline__ W256 w_sub(const W256& a, const W256& b) {
+  W256 r; uint64_t br = 0;
+  for (int i = 0; i < 8; i++) { uint64_t d = (uint64_t)a.v[i] - b.v[i] - br; r.v[i] = (uint32_t)d; br = (d >> 32) & 1; }
+  return r;
+}
+
+// BigMultModP(64,K,K,K) block signal s (bigInt.circom:206-272)
+__device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
+  const int K = C.K, DIV = K + 1;
+  // own: div[DIV] | mod[K] | in1[K], in2[K], modulus[K]
+  if (s < (uint32_t)DIV) return w_u64(C.q[s]);
+  s -= DIV;
+  if (s < (uint32_t)K) return w_u64(C.r[s]);
+  s -= K;
+  if (s < (uint32_t)(3 * K)) { int g = s / K, i = s - g * K; return w_u64(g == 0 ? C.x[i] : g == 1 ? C.y[i] : C.n[i]); }
+  s -= 3 * K;
+  // mult = BigMultOverflow: out[2K-1] | in1, in2 | karatsuba
+  if (s < (uint32_t)(2 * K - 1)) return kara_sig(C, K, s);
+  s -= 2 * K - 1;
+  if (s < (uint32_t)(2 * K)) return w_u64(s < (uint32_t)K ? C.x[s] : C.y[s - K]);
+  s -= 2 * K;
+  uint32_t ks = kara_size(K);
+  if (s < ks) return kara_sig(C, K, s);
+  s -= ks;
+  // modChecks[K]: Num2Bits(64)(mod_i): out[64] | in | sum[64]
+  if (s < (uint32_t)(129 * K)) {
+    uint32_t i = s / 129, t = s - 129 * i;
+    uint64_t v = C.r[i];
+    if (t < 64) return w_u64((v >> t) & 1);
+    if (t == 64) return w_u64(v);
+    return w_u64(v & mask_lo((int)t - 64));
+  }
+  s -= 129 * K;
+  // greaterThan: out | in[0]=modulus, in[1]=mod | lessEqThan: out | in | result[K] | (lessThan(64), isEqual) x K
+  auto le_result = [&](int upto) -> uint32_t {
+    uint32_t res = 0;
+    for (int i = 0; i <= upto; i++) {
+      uint32_t lt = C.n[i] < C.r[i], e = C.n[i] == C.r[i];
+      res = i == 0 ? lt + e : lt + e * res;
+    }
+    return res;
+  };
+  if (s == 0) return w_u64(1 - le_result(K - 1));
+  if (s < (uint32_t)(1 + 2 * K)) { s -= 1; return w_u64(s < (uint32_t)K ? C.n[s] : C.r[s - K]); }
+  s -= 1 + 2 * K;
+  if (s == 0) return w_u64(le_result(K - 1));
+  if (s < (uint32_t)(1 + 2 * K)) { s -= 1; return w_u64(s < (uint32_t)K ? C.n[s] : C.r[s - K]); }
+  s -= 1 + 2 * K;
+  if (s < (uint32_t)K) return w_u64(le_result((int)s));
+  s -= K;
+  if (s < (uint32_t)(140 * K)) {
+    uint32_t i = s / 140, t = s - 140 * i;
+    uint64_t a = C.n[i], b = C.r[i];
+    if (t < 134) {  // LessThan(64): out | in[2] | Num2Bits(65)(a + 2^64 - b)
+      // v = a + 2^64 - b (65-bit)
+      uint64_t vlo = a - b; uint32_t vhi = a >= b ? 1u : 0u;
+      if (t == 0) return w_u64(1 - vhi);
+      if (t == 1) return w_u64(a);
+      if (t == 2) return w_u64(b);
+      t -= 3;
+      W256 v = w_zero(); v.v[0] = (uint32_t)vlo; v.v[1] = (uint32_t)(vlo >> 32); v.v[2] = vhi;
+      if (t < 65) return w_u64(w_bit(v, t));
+      if (t == 65) return v;
+      return w_mask(v, (int)t - 65);
+    }
+    t -= 134;  // IsEqual: out | in[2] | IsZero(out, in, inv)
+    if (t == 0 || t == 3) return w_u64(a == b);
+    if (t == 1) return w_u64(a);
+    if (t == 2) return w_u64(b);
+    if (t == 4) return a <= b ? w_u64(b - a) : w_from_fr(fr_sub(fr_zero(), fr_u64(a - b)));
+    W256 r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)(C.inv[4 * i + (k >> 1)] >> (32 * (k & 1)));
+    return r;
+  }
+  s -= 140 * K;
+  // mult2 = BigMultNonEqualOverflow(DIV, K): out[2K] | in1 = q, in2 = n | tmpMults[DIV][K] | tmpResult[2K][K]
+  auto conv_qn = [&](int i) -> U192 {
+    U192 acc;
+    for (int j = i < K ? 0 : i - K + 1; j <= i && j <= K; j++) acc.mac(C.q[j], C.n[i - j]);
+    return acc;
+  };
+  if (s < (uint32_t)(2 * K)) return u192w(conv_qn(s));
+  s -= 2 * K;
+  if (s < (uint32_t)(2 * K + 1)) return w_u64(s < (uint32_t)DIV ? C.q[s] : C.n[s - DIV]);
+  s -= 2 * K + 1;
+  if (s < (uint32_t)(DIV * K)) {
+    uint32_t i = s / K, j = s - i * K;
+    U192 acc; acc.mac(C.q[i], C.n[j]);
+    return u192w(acc);
+  }
+  s -= DIV * K;
+  if (s < (uint32_t)(2 * K * K)) {
+    int i = s / K, j = s - i * K;
+    U192 acc;
+    if (i < K) {
+      if (j > i) return w_zero();
+      for (int t = 0; t <= j; t++) acc.mac(C.q[i - t], C.n[t]);
+    } else if (i < DIV) {
+      for (int t = 0; t <= j; t++) acc.mac(C.q[i - t], C.n[t]);
+    } else {
+      if (j >= DIV + K - 1 - i) return w_zero();
+      for (int t = 0; t <= j; t++) acc.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
+    }
+    return u192w(acc);
+  }
+  s -= 2 * K * K;
+  // isZero = BigIntIsZero(64, MAX, 2K-1): in[2K-1] | carry[2K-2] | carryRangeChecks[2K-2]
+  if (s < (uint32_t)(2 * K - 1)) {
+    int i = s;
+    U192 a;
+    for (int j = i < K ? 0 : i - K + 1; j <= i && j < K; j++) a.mac(C.x[j], C.y[i - j]);
+    W256 d = w_sub(u192w(a), u192w(conv_qn(i)));
+    if (i < K) d = w_sub(d, w_u64(C.r[i]));
+    return w_signed_to_fr(d);
+  }
+  s -= 2 * K - 1;
+  if (s < (uint32_t)(2 * K - 2)) return w_from_fr(fr_from_i128(C.cr[2 * s], C.cr[2 * s + 1]));
+  s -= 2 * K - 2;
+  const int MAXB = 128 + (K == 32 ? 7 : 8);  // 2*64 + log_ceil(2K)
+  const int RL = MAXB + 3 - 64;              // Num2Bits width of the carry range checks
+  uint32_t per = 2 * RL + 1, i = s / per, t = s - per * i;
+  // value = carry + 2^(RL-1) (non-negative, < 2^RL for a passing witness)
+  uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1];
+  uint64_t add_hi = 1ull << (RL - 1 - 64);
+  uint64_t vhi = hi + add_hi;
+  W256 v = w_zero();
+  v.v[0] = (uint32_t)lo; v.v[1] = (uint32_t)(lo >> 32); v.v[2] = (uint32_t)vhi; v.v[3] = (uint32_t)(vhi >> 32);
+  if (t < (uint32_t)RL) return w_u64(w_bit(v, t));
+  if (t == (uint32_t)RL) return v;
+  return w_mask(v, (int)t - RL);
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
+  __shared__ uint64_t lds[MM_CORE_WORDS(K) + K];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const uint64_t* mc = B.rsa_core + (size_t)w * L.rsa_core_words + (size_t)R.a[0] * MM_CORE_WORDS(K);
+  const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
+  for (int i = threadIdx.x; i < MM_CORE_WORDS(K); i += blockDim.x) lds[i] = mc[i];
+  for (int i = threadIdx.x; i < K; i += blockDim.x) lds[MM_CORE_WORDS(K) + i] = in_u64(row + 32ull * (R.a[1] + i));
+  __syncthreads();
+  MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1};
+  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) store_w(out + 32ull * q, mm_sig(C, wk.start + q));
+}
+
+// ------------------------------------------------------------------ BabyJubJub steps
+__global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  BjjConsts C;
+  C.init();
+  const fr* core = B.bjj_core + (size_t)w * L.bjj_core_fr;
+  fr sk = fr_from_mont(B.vs.at(L.reg.v_sk, w));
+  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint32_t s = wk.start + q;
+    int i; uint32_t t; bool dbl;
+    if (s < 46) { i = 0; t = s; dbl = false; }
+    else { uint32_t s2 = s - 46; i = 1 + s2 / 60; t = s2 % 60; dbl = t >= 46; if (dbl) t -= 46; }
+    fr res;
+    if (dbl) {
+      // doublers[i-1]: out[2] = D_i | in[2] = A_{i-1} | adder: out, in1, in2, beta, gamma, delta, tau
+      const fr* Pp = core + 5 * (i - 1);
+      fr x = Pp[2], y = Pp[3];
+      const fr* Pc = core + 5 * i;
+      if (t < 2) res = Pc[t];
+      else if (t < 4) res = t == 2 ? x : y;
+      else {
+        uint32_t u = t - 4;
+        if (u < 2) res = Pc[u];
+        else if (u < 6) res = (u & 1) ? y : x;  // in1, in2 = (x, y)
+        else if (u == 6 || u == 7) res = fr_mul(x, y);
+        else if (u == 8) res = fr_mul(fr_sub(y, fr_mul(C.A, x)), fr_add(x, y));
+        else { fr b = fr_mul(x, y); res = fr_mul(b, b); }
+      }
+    } else {
+      const fr* P = core + 5 * i;
+      int bit = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
+      fr x1 = i == 0 ? fr_zero() : P[0], y1 = i == 0 ? fr_zero() : P[1];
+      fr x2 = bit ? C.B8x : fr_zero(), y2 = bit ? C.B8y : fr_zero();
+      bool z1 = fr_is_zero(x1), z2 = !bit;
+      fr ox = P[2], oy = P[3];
+      fr rawx = (!z1 && !z2) ? ox : fr_zero(), rawy = (!z1 && !z2) ? oy : fr_zero();
+      if (t < 2) res = t == 0 ? ox : oy;
+      else if (t < 4) res = t == 2 ? x1 : y1;
+      else if (t < 6) res = t == 4 ? x2 : y2;
+      else if (t < 9) { uint32_t u = t - 6; res = u == 0 ? (z1 ? fr_mont_one() : fr_zero()) : u == 1 ? x1 : (i == 0 ? fr_zero() : P[4]); }
+      else if (t < 12) {
+        uint32_t u = t - 9;
+        res = u == 0 ? (z2 ? fr_mont_one() : fr_zero()) : u == 1 ? x2 : (bit ? fr_to_mont(fr_const(BJJ_INV_B8X)) : fr_zero());
+      } else if (t < 22) {  // adder: out[2] | in1[2], in2[2] | beta, gamma, delta, tau
+        uint32_t u = t - 12;
+        if (u < 2) res = u == 0 ? rawx : rawy;
+        else if (u < 4) res = u == 2 ? x1 : y1;
+        else if (u < 6) res = u == 4 ? x2 : y2;
+        else if (u == 6) res = fr_mul(x1, y2);
+        else if (u == 7) res = fr_mul(y1, x2);
+        else if (u == 8) res = fr_mul(fr_sub(y1, fr_mul(C.A, x1)), fr_add(x2, y2));
+        else res = fr_mul(fr_mul(x1, y2), fr_mul(y1, x2));
+      } else {  // switchers L0, R0, L1, R1: out[2] | bool, in[2] | aux
+        uint32_t u = t - 22, sw = u / 6, k = u % 6;
+        int c = sw >> 1;
+        fr raw = c == 0 ? rawx : rawy, in1c = c == 0 ? x1 : y1, in2c = c == 0 ? x2 : y2;
+        fr bl = z2 ? fr_mont_one() : fr_zero();
+        fr l0 = z2 ? in1c : raw, l1 = z2 ? raw : in1c;
+        if ((sw & 1) == 0) {
+          fr vals[6] = {l0, l1, bl, raw, in1c, z2 ? fr_sub(in1c, raw) : fr_zero()};
+          res = vals[k];
+        } else {
+          fr br = z1 ? fr_mont_one() : fr_zero();
+          fr r0 = z1 ? in2c : l0, r1 = z1 ? l0 : in2c;
+          fr vals[6] = {r0, r1, br, l0, in2c, z1 ? fr_sub(in2c, l0) : fr_zero()};
+          res = vals[k];
+        }
+      }
+    }
+    store_fr(out + 32ull * q, fr_from_mont(res));
+  }
+}
+
+}  // namespace pzk

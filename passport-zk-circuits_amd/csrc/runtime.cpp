@@ -11,6 +11,7 @@
 #include "../../include/pzkwit.h"
 #include "builder.hpp"
 #include "kernels.hpp"
+#include "bufs.hpp"
 #include "poseidon.hpp"
 
 using namespace pzk;
@@ -23,17 +24,75 @@ static int fail(int code, const std::string& msg) { g_err = msg; return code; }
     if (e_ != hipSuccess) return fail(PZK_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
+// kernel phases, timed with HIP events on the launch stream when PZK_EXEC_TIMING is set
+enum Phase {
+  PH_LOAD, PH_SHA_CORE, PH_PREP, PH_RSA_CORE, PH_BJJ_CORE, PH_POS_CORE, PH_SMT,
+  PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_COUNT
+};
+static const char* PHASE_NAMES[PH_COUNT] = {"load_values", "sha_core", "prep",     "rsa_core",  "bjj_core",
+                                            "pos_core",    "smt",      "emit_gen", "emit_sha",  "emit_pos",
+                                            "emit_bits",   "emit_flow", "emit_mm", "emit_bjj"};
+static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k_prep",      "k_rsa_core",
+                                              "k_bjj_core",    "k_pos_core",  "k_smt_prep+k_smt_chain",
+                                              "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
+                                              "k_emit_flow",   "k_emit_mm",   "k_emit_bjj"};
+static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
+                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ};
+
+struct Timing {
+  static constexpr int RING = 8;
+  hipEvent_t ev[RING][PH_COUNT][2] = {};
+  bool used[RING][PH_COUNT] = {};
+  bool pending[RING] = {};
+  int head = 0;
+  double ms[PH_COUNT] = {};
+  uint64_t n[PH_COUNT] = {};
+  void collect(int slot) {
+    if (!pending[slot]) return;
+    for (int p = 0; p < PH_COUNT; p++) {
+      if (!used[slot][p]) continue;
+      float t = 0;
+      (void)hipEventSynchronize(ev[slot][p][1]);
+      if (hipEventElapsedTime(&t, ev[slot][p][0], ev[slot][p][1]) == hipSuccess) { ms[p] += t; n[p]++; }
+      used[slot][p] = false;
+    }
+    pending[slot] = false;
+  }
+  void destroy() {
+    for (auto& a : ev)
+      for (auto& b : a)
+        for (auto& e : b)
+          if (e) (void)hipEventDestroy(e);
+  }
+};
+
+struct PhaseScope {
+  Timing* T; int slot, ph; hipStream_t st;
+  PhaseScope(Timing* t, int s, int p, hipStream_t stream) : T(t), slot(s), ph(p), st(stream) {
+    if (!T) return;
+    for (auto& e : T->ev[slot][ph]) if (!e) (void)hipEventCreate(&e);
+    (void)hipEventRecord(T->ev[slot][ph][0], st);
+  }
+  ~PhaseScope() {
+    if (!T) return;
+    (void)hipEventRecord(T->ev[slot][ph][1], st);
+    T->used[slot][ph] = true;
+  }
+};
+
 struct pzk_instance {
   pzk_params params;
-  Layout lay;            // host layout (builder.hpp)
+  Timing timing;
+  Layout lay;
   int device = 0;
   hipStream_t stream = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
-  Work *d_work_sha = nullptr, *d_work_pos = nullptr, *d_work_gen = nullptr;
+  Work* d_work[E_COUNT] = {};
   ShaJob* d_sha = nullptr;
   PosTask* d_pos = nullptr;
   ValueLoad* d_loads = nullptr;
+  int32_t* d_level_task = nullptr;
   fr* d_pos_consts = nullptr;
   PosParamIndex pix{};
   // per-batch scratch, grown on demand
@@ -41,6 +100,8 @@ struct pzk_instance {
   uint32_t* d_sha_core = nullptr;
   fr* d_pos_core = nullptr;
   fr* d_values = nullptr;
+  uint64_t* d_rsa_core = nullptr;
+  fr *d_bjj_core = nullptr, *d_bjj_scratch = nullptr, *d_smt_core = nullptr;
   // staging for the host-buffer path
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -59,6 +120,10 @@ struct pzk_instance {
     L.regions = d_regions;
     L.sha = d_sha;
     L.pos = d_pos;
+    L.reg = lay.reg;
+    L.rsa_core_words = lay.rsa_core_words;
+    L.bjj_core_fr = lay.bjj_core_fr;
+    L.smt_core_fr = lay.smt_core_fr;
     return L;
   }
 };
@@ -131,18 +196,31 @@ static int upload(T** dst, const std::vector<T>& v) {
   return 0;
 }
 
-static void free_all(pzk_instance* I) {
-  void* ptrs[] = {I->d_regions, I->d_work_sha, I->d_work_pos, I->d_work_gen, I->d_sha, I->d_pos, I->d_loads,
-                  I->d_pos_consts, I->d_sha_core, I->d_pos_core, I->d_values, I->d_in, I->d_out, I->d_status};
+static void free_scratch(pzk_instance* I) {
+  void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_bjj_core, I->d_bjj_scratch, I->d_smt_core};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr;
+  I->d_bjj_core = nullptr; I->d_bjj_scratch = nullptr; I->d_smt_core = nullptr;
+  I->cap = 0;
+}
+
+static void free_all(pzk_instance* I) {
+  free_scratch(I);
+  void* ptrs[] = {I->d_regions, I->d_sha, I->d_pos, I->d_loads, I->d_level_task, I->d_pos_consts,
+                  I->d_in, I->d_out, I->d_status};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto* p : I->d_work)
+    if (p) (void)hipFree(p);
   if (I->stream) (void)hipStreamDestroy(I->stream);
+  I->timing.destroy();
 }
 
 extern "C" {
 
 const char* pzk_last_error(void) { return g_err.c_str(); }
-const char* pzk_version(void) { return "pzkwit 0.1.0 (gfx950)"; }
+const char* pzk_version(void) { return "pzkwit 0.2.0 (gfx950)"; }
 
 int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   if (!params || !out) return fail(PZK_E_ARG, "null argument");
@@ -156,16 +234,47 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   HIPCHK(hipGetDevice(&I->device));
   int rc;
   if ((rc = load_poseidon(I)) != 0) { free_all(I); delete I; return rc; }
-  if ((rc = upload(&I->d_regions, I->lay.regions)) || (rc = upload(&I->d_work_sha, I->lay.work_sha)) ||
-      (rc = upload(&I->d_work_pos, I->lay.work_pos)) || (rc = upload(&I->d_work_gen, I->lay.work_gen)) ||
-      (rc = upload(&I->d_sha, I->lay.sha)) || (rc = upload(&I->d_pos, I->lay.pos)) ||
-      (rc = upload(&I->d_loads, I->lay.loads))) {
-    free_all(I); delete I; return rc;
-  }
+  std::vector<int32_t> level_task(SMT_LEVELS, -1);
+  for (size_t i = 0; i < I->lay.pos.size(); i++)
+    if (I->lay.pos[i].smt_level >= 0) level_task[I->lay.pos[i].smt_level] = (int32_t)i;
+  rc = upload(&I->d_regions, I->lay.regions);
+  for (int e = 0; e < E_COUNT && !rc; e++) rc = upload(&I->d_work[e], I->lay.work[e]);
+  if (!rc) rc = upload(&I->d_sha, I->lay.sha);
+  if (!rc) rc = upload(&I->d_pos, I->lay.pos);
+  if (!rc) rc = upload(&I->d_loads, I->lay.loads);
+  if (!rc && I->lay.is_register) rc = upload(&I->d_level_task, level_task);
+  if (rc) { free_all(I); delete I; return rc; }
   if (hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) != hipSuccess) {
     free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate failed");
   }
   *out = I;
+  return 0;
+}
+
+int pzk_layout_query(const pzk_params* params, pzk_info* info, uint32_t* n_regions) {
+  if (!params || !info) return fail(PZK_E_ARG, "null argument");
+  Layout L;
+  std::string why;
+  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
+  memset(info, 0, sizeof *info);
+  info->witness_size = L.wit_size;
+  info->n_inputs = L.n_inputs;
+  info->n_outputs = L.n_outputs;
+  info->n_public_inputs = L.n_public;
+  info->n_input_groups = (uint32_t)L.inputs.size();
+  if (n_regions) *n_regions = (uint32_t)L.regions.size();
+  return 0;
+}
+
+int pzk_layout_region(const pzk_params* params, uint32_t i, uint64_t* off, uint32_t* len, uint32_t* kind) {
+  if (!params) return fail(PZK_E_ARG, "null argument");
+  Layout L;
+  std::string why;
+  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
+  if (i >= L.regions.size()) return fail(PZK_E_ARG, "region index out of range");
+  if (off) *off = L.regions[i].off;
+  if (len) *len = L.regions[i].len;
+  if (kind) *kind = L.regions[i].kind;
   return 0;
 }
 
@@ -211,17 +320,22 @@ int pzk_wtns_header(const pzk_instance* I, uint8_t h[76]) {
 
 static int ensure_scratch(pzk_instance* I, size_t batch) {
   if (batch <= I->cap) return 0;
-  if (I->d_sha_core) (void)hipFree(I->d_sha_core);
-  if (I->d_pos_core) (void)hipFree(I->d_pos_core);
-  if (I->d_values) (void)hipFree(I->d_values);
-  I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr;
-  size_t sha = 4ull * I->lay.sha_core_words * batch, pos = 32ull * I->lay.pos_core_elems * batch,
-         val = 32ull * std::max<uint32_t>(I->lay.n_values, 1) * batch;
-  if ((sha && hipMalloc(&I->d_sha_core, sha) != hipSuccess) || (pos && hipMalloc(&I->d_pos_core, pos) != hipSuccess) ||
-      hipMalloc(&I->d_values, val) != hipSuccess) {
-    I->cap = 0;
-    return fail(PZK_E_NOMEM, "device scratch allocation failed");
-  }
+  free_scratch(I);
+  const Layout& L = I->lay;
+  struct { void** p; size_t bytes; } req[] = {
+      {(void**)&I->d_sha_core, 4ull * L.sha_core_words * batch},
+      {(void**)&I->d_pos_core, 32ull * L.pos_core_elems * batch},
+      {(void**)&I->d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
+      {(void**)&I->d_rsa_core, 8ull * L.rsa_core_words * batch},
+      {(void**)&I->d_bjj_core, 32ull * L.bjj_core_fr * batch},
+      {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * 9 * BJJ_STEPS * batch : 0},
+      {(void**)&I->d_smt_core, 32ull * L.smt_core_fr * batch},
+  };
+  for (auto& r : req)
+    if (r.bytes && hipMalloc(r.p, r.bytes) != hipSuccess) {
+      free_scratch(I);
+      return fail(PZK_E_NOMEM, "device scratch allocation failed");
+    }
   I->cap = batch;
   return 0;
 }
@@ -237,21 +351,51 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   if (rc) return rc;
   hipStream_t st = (exec && exec->stream) ? (hipStream_t)exec->stream : I->stream;
   const uint32_t B = (uint32_t)batch;
+  const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
   ValueStore vs{I->d_values, B};
   PosConsts K{I->d_pos_consts, I->pix};
-  if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
-  HIPCHK(launch_load_values(I->d_loads, (int)I->lay.loads.size(), d_inputs, I->lay.n_inputs, I->d_values, B, st));
-  HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st));
-  for (size_t l = 0; l + 1 < I->lay.pos_level_start.size(); l++) {
-    uint32_t a = I->lay.pos_level_start[l], b = I->lay.pos_level_start[l + 1];
-    HIPCHK(launch_pos_core(K, I->d_pos, I->lay.pos.data(), a, b - a, vs, I->d_pos_core, I->lay.pos_core_elems, st));
+  Bufs bufs{d_inputs, I->d_sha_core, I->d_rsa_core, I->d_pos_core, I->d_bjj_core, I->d_smt_core, vs, d_wtns, stride,
+            d_status};
+  Timing* T = nullptr;
+  int slot = 0;
+  if (exec && (exec->flags & PZK_EXEC_TIMING)) {
+    T = &I->timing;
+    slot = T->head;
+    T->collect(slot);
+    T->head = (T->head + 1) % Timing::RING;
+    T->pending[slot] = true;
   }
-  HIPCHK(launch_emit_gen(L, I->d_work_gen, (uint32_t)I->lay.work_gen.size(), d_inputs, vs, d_wtns, stride, B, st));
-  HIPCHK(launch_emit_sha(L, I->d_work_sha, (uint32_t)I->lay.work_sha.size(), d_inputs, I->d_sha_core, d_wtns, stride,
-                         B, st));
-  HIPCHK(launch_emit_pos(L, I->d_work_pos, (uint32_t)I->lay.work_pos.size(), K, vs, I->d_pos_core, d_wtns, stride, B,
-                         I->lay.max_t, st));
+  auto pos_levels = [&](int lo, int hi) -> int {
+    for (int l = lo; l < hi && l + 1 < (int)lay.pos_level_start.size(); l++) {
+      uint32_t a = lay.pos_level_start[l], b = lay.pos_level_start[l + 1];
+      HIPCHK(launch_pos_core(K, I->d_pos, lay.pos.data(), a, b - a, vs, I->d_pos_core, lay.pos_core_elems,
+                             I->d_smt_core, lay.smt_core_fr, st));
+    }
+    return 0;
+  };
+  if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
+  { PhaseScope ps(T, slot, PH_LOAD, st);
+    HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, I->d_values, B, st)); }
+  { PhaseScope ps(T, slot, PH_SHA_CORE, st);
+    HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
+  if (lay.is_register) {
+    { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
+    { PhaseScope ps(T, slot, PH_RSA_CORE, st); HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, st)); }
+    { PhaseScope ps(T, slot, PH_BJJ_CORE, st); HIPCHK(launch_bjj_core(L, vs, I->d_bjj_core, I->d_bjj_scratch, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st);
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, I->d_pos_core, I->d_smt_core, st)); }
+  } else {
+    PhaseScope ps(T, slot, PH_POS_CORE, st);
+    if ((rc = pos_levels(0, 1 << 20))) return rc;
+  }
+  for (int e = 0; e < E_COUNT; e++) {
+    PhaseScope ps(lay.work[e].empty() ? nullptr : T, slot, EMIT_PHASE[e], st);
+    HIPCHK(launch_emit(e, L, I->d_work[e], (uint32_t)lay.work[e].size(), K, bufs, B, lay.max_t, st));
+  }
   if (exec && (exec->flags & PZK_EXEC_SYNC)) HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
@@ -279,6 +423,53 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
   HIPCHK(hipMemcpyAsync(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost, st));
   if (h_status) HIPCHK(hipMemcpyAsync(h_status, I->d_status, 4 * batch, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int pzk_timing(pzk_instance* I, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset) {
+  if (!I || !count) return fail(PZK_E_ARG, "null argument");
+  for (int s = 0; s < Timing::RING; s++) I->timing.collect(s);
+  uint32_t n = std::min<uint32_t>(*count, PH_COUNT);
+  for (uint32_t p = 0; p < n; p++) {
+    if (names) names[p] = PHASE_NAMES[p];
+    if (ms) ms[p] = I->timing.ms[p];
+    if (launches) launches[p] = I->timing.n[p];
+  }
+  *count = PH_COUNT;
+  if (reset) {
+    memset(I->timing.ms, 0, sizeof I->timing.ms);
+    memset(I->timing.n, 0, sizeof I->timing.n);
+  }
+  return 0;
+}
+
+int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, const char** kernel,
+                   uint64_t* bytes_per_witness) {
+  if (!I || phase >= PH_COUNT) return fail(PZK_E_ARG, "bad phase");
+  if (name) *name = PHASE_NAMES[phase];
+  if (kernel) *kernel = PHASE_KERNELS[phase];
+  if (bytes_per_witness) {
+    // ALGORITHMIC HBM bytes per witness: every witness element the phase writes (32 B) + the
+    // unique bytes it must read (input elements copied, core state it expands)
+    const Layout& L = I->lay;
+    uint64_t b = 0;
+    for (const Region& r : L.regions) {
+      if (EMIT_PHASE[emitter_of(r.kind)] != (int)phase) continue;
+      b += 32ull * r.len;
+      if (r.kind == RK_SHA_OWN) b += 32ull * 512 * r.a[1] * (r.a[3] ? 2 : 1);  // message bits copied
+      if (r.kind == RK_SHA_BLOCK) b += 4ull * SHA_BLOCK_CORE;
+      if (r.kind == RK_INCOPY) b += 32ull * r.len;
+      if (r.kind == RK_POSEIDON) b += 32ull * pos_core_len(r.a[1] + 1);
+      if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);
+    }
+    if (phase == PH_SHA_CORE)
+      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * SHA_BLOCK_CORE + 8);
+    if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
+    if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
+    if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;
+    if (phase == PH_LOAD) b += 64ull * L.loads.size();
+    *bytes_per_witness = b;
+  }
   return 0;
 }
 

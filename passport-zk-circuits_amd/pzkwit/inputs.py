@@ -6,6 +6,7 @@ bigintToArrayString :125-135, getFakeIdenData :628-657, writeToJson :659-672).
 Synthetic workloads follow SURVEY.md §8d (configs 2-4, seeds 0x2-0x4).
 """
 import hashlib
+import os
 
 import numpy as np
 
@@ -119,14 +120,54 @@ def _dg15_rsa1024(rng):
     return _DG15_PREFIX + b"\x00" + bytes(mod) + bytes.fromhex("0203010001")
 
 
-class PassportGen:
-    """Synthetic passports for the canonical instance."""
+def _keygen(args):
+    seed, k, bits = args
+    return RsaKey(bits, SplitMix64((seed << 32) ^ (0x4B455900 + k)))
 
-    def __init__(self, seed=3, n_keys=64, key_bits=2048, params=None):
+
+class PassportGen:
+    """Synthetic passports for the canonical instance.
+
+    Signer key k and passport i each draw from their own SplitMix64 stream, so any index
+    range can be generated independently (sharded across ranks / worker processes)."""
+
+    _shared = {}
+
+    def __init__(self, seed=3, n_keys=64, key_bits=2048, params=None, workers=None):
+        self.seed = seed
         self.rng = SplitMix64(seed)
         self.params = dict(CANONICAL if params is None else params)
-        self.keys = [RsaKey(key_bits, self.rng) for _ in range(n_keys)]
+        jobs = [(seed, k, key_bits) for k in range(n_keys)]
+        workers = workers or min(16, os.cpu_count() or 1)
+        if n_keys >= 8 and workers > 1:
+            from concurrent.futures import ProcessPoolExecutor
+            with ProcessPoolExecutor(min(workers, n_keys)) as ex:
+                self.keys = list(ex.map(_keygen, jobs))
+        else:
+            self.keys = [_keygen(j) for j in jobs]
         self._pkhash = {}
+
+    @classmethod
+    def shared(cls, seed=3, n_keys=64):
+        key = (seed, n_keys)
+        if key not in cls._shared:
+            cls._shared[key] = cls(seed, n_keys)
+        return cls._shared[key]
+
+    @property
+    def n_inputs(self):
+        pr = self.params
+        K = 64 if pr["sig"] == 2 else 32
+        return 1 + pr["ec_blocks"] * 512 + 1024 + pr["dg15_blocks"] * 512 + 1024 + 2 * K + 80 + 1
+
+    def passport_at(self, i, smt_depth=0):
+        """Passport i from its own stream (independent of generation order)."""
+        saved = self.rng
+        self.rng = SplitMix64((self.seed << 40) ^ (0x50415353 + i))
+        try:
+            return self.passport(i, smt_depth)
+        finally:
+            self.rng = saved
 
     def pk_hash(self, key):
         """RSA pubkey hash = Poseidon5 of 5 x 192-bit limb triples (passportVerificationBuilder.circom:182-191)."""

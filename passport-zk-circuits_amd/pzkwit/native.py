@@ -17,7 +17,8 @@ PZK_EXEC_SYNC = 1
 
 # C-ABI entry points declared in include/pzkwit.h (checked by tests/test_capi.py)
 EXPORTS = ("pzk_instance_create", "pzk_instance_destroy", "pzk_instance_info", "pzk_instance_input",
-           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_last_error", "pzk_version")
+           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_timing", "pzk_phase_info", "pzk_last_error",
+           "pzk_version")
 
 STATUS_NAMES = {
     0: "OK", 1: "Num2Bits (bitify.circom:26)", 2: "AliasCheck (aliascheck.circom:14)",
@@ -51,6 +52,16 @@ class PzkError(RuntimeError):
     pass
 
 
+_PARAM_MAP = dict(sig="signature_type", dg_hash="dg_hash_type", doc="document_type", ec_blocks="ec_block_number",
+                  ec_shift="ec_shift", dg1_shift="dg1_shift", aa="aa_signature_algo", dg15_shift="dg15_shift",
+                  dg15_blocks="dg15_block_number", aa_shift="aa_shift")
+
+
+def param_fields(params):
+    """short names (inputs.CANONICAL) -> pzk_params field names"""
+    return {_PARAM_MAP.get(k, k): int(v) for k, v in params.items()}
+
+
 _lib = None
 
 
@@ -71,6 +82,14 @@ def lib():
                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(PzkExec)]
         L.pzk_witness_batch_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(PzkExec)]
+        L.pzk_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+        L.pzk_phase_info.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
+                                     ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64)]
+        L.pzk_layout_query.argtypes = [ctypes.POINTER(PzkParams), ctypes.POINTER(PzkInfo),
+                                       ctypes.POINTER(ctypes.c_uint32)]
+        L.pzk_layout_region.argtypes = [ctypes.POINTER(PzkParams), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.pzk_last_error.restype = ctypes.c_char_p
         L.pzk_version.restype = ctypes.c_char_p
         _lib = L
@@ -126,10 +145,31 @@ class Instance:
         _check(lib().pzk_wtns_header(self._h, h))
         return bytes(h)
 
-    def witness_batch_device(self, d_inputs, batch, d_wtns, stride, d_status=None, stream=None, device=0, sync=False):
-        ex = PzkExec(device=device, flags=PZK_EXEC_SYNC if sync else 0, stream=stream)
+    def witness_batch_device(self, d_inputs, batch, d_wtns, stride, d_status=None, stream=None, device=0, sync=False,
+                             timing=False):
+        ex = PzkExec(device=device, flags=(PZK_EXEC_SYNC if sync else 0) | (2 if timing else 0), stream=stream)
         _check(lib().pzk_witness_batch(self._h, ctypes.c_void_p(d_inputs), batch, ctypes.c_void_p(d_wtns), stride,
                                        ctypes.c_void_p(d_status) if d_status else None, ctypes.byref(ex)))
+
+    def timing(self, reset=False):
+        """{phase: (ms accumulated, launches)} from calls made with timing=True (HIP events)."""
+        cap = 32
+        names = (ctypes.c_char_p * cap)()
+        ms = (ctypes.c_double * cap)()
+        n = (ctypes.c_uint64 * cap)()
+        cnt = ctypes.c_uint32(cap)
+        _check(lib().pzk_timing(self._h, names, ms, n, ctypes.byref(cnt), 1 if reset else 0))
+        return {names[i].decode(): (ms[i], int(n[i])) for i in range(cnt.value)}
+
+    def phase_info(self):
+        """[(phase, kernel symbol, algorithmic bytes per witness)]"""
+        out = []
+        for p in range(32):
+            nm, kn, b = ctypes.c_char_p(), ctypes.c_char_p(), ctypes.c_uint64()
+            if lib().pzk_phase_info(self._h, p, ctypes.byref(nm), ctypes.byref(kn), ctypes.byref(b)) != 0:
+                break
+            out.append((nm.value.decode(), kn.value.decode(), int(b.value)))
+        return out
 
     def witness_batch_host(self, inputs):
         """inputs: (batch, n_inputs, 32) uint8 -> (witness (batch, W, 32) uint8, status (batch,) int32)."""

@@ -1,0 +1,102 @@
+"""GPU parity for RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) (SURVEY.md §8d
+configs 3 and 4): every witness element equals the CPU oracle's, the public outputs equal
+independently computed values, and lane status is OK."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from pzkwit import field, inputs as I, native
+
+pytestmark = pytest.mark.gpu
+
+KIND_NAMES = {0: "ONE", 1: "INCOPY", 2: "SHA_OWN", 3: "SHA_BLOCK", 4: "POSEIDON", 5: "MODMUL", 6: "VALUE",
+              7: "BITS2NUM", 8: "NUM2BITS", 9: "DIGEST", 10: "TEMPMOD", 11: "FLOW", 12: "HCHUNK", 13: "RSA_OUT",
+              14: "SMT_OWN", 15: "SMTHASH", 16: "LEVINS", 17: "SM", 18: "SMT_LEVEL", 19: "SWITCHER",
+              20: "ISEQ_ROOT", 21: "BJJ_OWN", 22: "BJJ_STEPS"}
+
+
+def region_table(params):
+    L = native.lib()
+    p = native.PzkParams(circuit=0)
+    for k, v in native.param_fields(params).items():
+        setattr(p, k, v)
+    info = native.PzkInfo()
+    n = ctypes.c_uint32()
+    L.pzk_layout_query(ctypes.byref(p), ctypes.byref(info), ctypes.byref(n))
+    out = []
+    for i in range(n.value):
+        off, ln, kd = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+        L.pzk_layout_region(ctypes.byref(p), i, ctypes.byref(off), ctypes.byref(ln), ctypes.byref(kd))
+        out.append((off.value, ln.value, kd.value))
+    return out
+
+
+def mismatch_report(ref, got, regions, limit=12):
+    bad = np.nonzero((ref != got).any(axis=1))[0]
+    if bad.size == 0:
+        return ""
+    lines = ["%d mismatching elements" % bad.size]
+    seen = {}
+    for idx in bad:
+        for ri, (off, ln, kd) in enumerate(regions):
+            if off <= idx < off + ln:
+                seen.setdefault(ri, []).append(int(idx - off))
+                break
+    for ri, locs in list(seen.items())[:limit]:
+        off, ln, kd = regions[ri]
+        e = off + locs[0]
+        lines.append("region %d %s off=%d len=%d: %d bad, first local %s ref=%s got=%s" % (
+            ri, KIND_NAMES.get(kd, kd), off, ln, len(locs), locs[:6],
+            int.from_bytes(ref[e].tobytes(), "little"), int.from_bytes(got[e].tobytes(), "little")))
+    return "\n".join(lines)
+
+
+@pytest.fixture(scope="module")
+def gen():
+    return I.PassportGen(seed=3, n_keys=4)
+
+
+def _check(oracle, params, batch_inputs):
+    inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params)
+    wit, st = inst.witness_batch_host(batch_inputs)
+    prm = oracle.register_params(**params)
+    regions = region_table(params)
+    reports = []
+    for b in range(batch_inputs.shape[0]):
+        rc, ref = oracle.register_witness(prm, batch_inputs[b])
+        assert rc == 0, "oracle check failed (site %d) on row %d" % (rc, b)
+        rep = mismatch_report(ref, wit[b], regions)
+        if rep:
+            reports.append("row %d: %s" % (b, rep))
+    assert not reports, "\n".join(reports)
+    assert (st == 0).all(), st
+    return wit
+
+
+def test_register_canonical_matches_oracle(oracle, gen):
+    rows = np.stack([I.pack_register_inputs(gen.passport_at(i)) for i in range(6)])
+    wit = _check(oracle, I.CANONICAL, rows)
+    # public outputs vs independent computation (process_passport.js / identity formulas)
+    pp = gen.passport_at(0)
+    sah = hashlib.sha256(pp["sa"]).digest()
+    hb = [(sah[i // 8] >> (7 - i % 8)) & 1 for i in range(256)]
+    n252 = sum(hb[i] << i for i in range(252))
+    assert int.from_bytes(wit[0, 2].tobytes(), "little") == field.poseidon([n252])
+    assert int.from_bytes(wit[0, 5].tobytes(), "little") == pp["root"]
+    # pkIdentityHash = Poseidon2(sk * Base8) (identity.circom:112-120), dg1Commitment (identity.circom:89-109)
+    from refmath import bjj_mul, dg1_commitment
+    x, y = bjj_mul(pp["sk"])
+    assert int.from_bytes(wit[0, 4].tobytes(), "little") == field.poseidon([x, y])
+    assert int.from_bytes(wit[0, 3].tobytes(), "little") == dg1_commitment(pp["dg1"], pp["sk"])
+
+
+def test_register_smt_depth_matches_oracle(oracle, gen):
+    """config 4 shape: siblings non-zero up to a random depth (sequential SMT chain on GPU)."""
+    rows = []
+    for i, depth in enumerate([1, 7, 40, 79]):
+        pp = gen.passport_at(100 + i, smt_depth=depth)
+        pp["root"] = field.SplitMix64(i).fr()
+        rows.append(I.pack_register_inputs(pp))
+    _check(oracle, I.CANONICAL, np.stack(rows))

@@ -134,8 +134,16 @@ def main():
     W, NIN = inst.witness_size, inst.n_inputs
     stride = 32 * W
     free, total = torch.cuda.mem_get_info(dev)
-    sub = args.sub or max(1, min(batch, int((free * 0.85 - host_in.nbytes) // stride)))
-    sub = min(sub, batch)
+    if args.sub:
+        sub = min(args.sub, batch)
+    else:
+        # largest slab that fits next to the inputs and the per-witness core scratch (~1 MB/witness),
+        # rounded down to an even split of the batch
+        fit = max(1, int((free * 0.85 - host_in.nbytes) // (stride + (1 << 20))))
+        parts = 1
+        while (batch + parts - 1) // parts > fit:
+            parts += 1
+        sub = (batch + parts - 1) // parts
     log("witness_size=%d (%.1f MB), batch=%d, sub-batch=%d, slab %.1f GB" % (W, stride / 1e6, batch, sub,
                                                                              sub * stride / 1e9))
     d_in = torch.from_numpy(host_in.reshape(-1)).to(dev)

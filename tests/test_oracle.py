@@ -1,0 +1,117 @@
+"""CPU: the oracle against the reference's golden vectors and independent restatements.
+
+* Poseidon: 1,207 KATs produced by the reference's own test/poseidon.js (tests/golden/).
+* SHA-256: Sha256HashChunks(6) digest signals vs hashlib on config-2 messages.
+* RegisterIdentityBuilder: public outputs vs independent Python formulas (tests/refmath.py),
+  every `===` satisfied, and BigMultModP div/mod vs the literal long_div restatement
+  (oracle/pyref_bigint.py, bigIntFunc.circom:190-333).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from pzkwit import field, inputs as I
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "poseidon_kats.json")
+
+
+def test_poseidon_oracle_matches_reference_kats(oracle):
+    d = json.load(open(GOLD))
+    assert len(d["cases"]) >= 1200
+    for c in d["cases"]:
+        assert oracle.poseidon([int(x) for x in c["in"]]) == int(c["out"]), c["in"]
+
+
+def test_poseidon_known_values(oracle):
+    # canonical circomlib values
+    assert oracle.poseidon([1, 2]) == 7853200120776062878684798364095072458815029376092732009249414926327459813530
+    assert oracle.poseidon([1]) == 18586133768512220936620570745912940619677854269274689475585506675881198879027
+
+
+def test_host_poseidon_matches_kats():
+    d = json.load(open(GOLD))
+    for c in d["cases"][:50] + d["cases"][1000:]:
+        assert field.poseidon([int(x) for x in c["in"]]) == int(c["out"])
+
+
+def test_sha256_oracle_digest(oracle):
+    msgs, batch = I.sha256_config2_batch(8, seed=2, blocks=6)
+    for m, row in zip(msgs, batch):
+        rc, w = oracle.sha256_witness(row, 6)
+        assert rc == 0
+        assert np.packbits(w[1:257, 0]).tobytes() == hashlib.sha256(m).digest()
+
+
+@pytest.fixture(scope="module")
+def passports():
+    g = I.PassportGen(seed=3, n_keys=2)
+    return [g.passport_at(i) for i in range(2)] + [g.passport_at(50, smt_depth=5)]
+
+
+def test_register_oracle_public_outputs(oracle, passports):
+    from refmath import aa_rsa_hash, bjj_mul, dg1_commitment
+    prm = oracle.register_params(**I.CANONICAL)
+    for pp in passports[:2]:
+        rc, w = oracle.register_witness(prm, I.pack_register_inputs(pp))
+        assert rc == 0
+        v = [oracle.from_elem(w[i]) for i in range(6)]
+        assert v[0] == 1
+        assert v[1] == aa_rsa_hash(pp["dg15"], 256)
+        sah = hashlib.sha256(pp["sa"]).digest()
+        hb = [(sah[i // 8] >> (7 - i % 8)) & 1 for i in range(256)]
+        assert v[2] == field.poseidon([sum(hb[i] << i for i in range(252))])
+        assert v[3] == dg1_commitment(pp["dg1"], pp["sk"])
+        assert v[4] == field.poseidon(list(bjj_mul(pp["sk"])))
+        assert v[5] == pp["root"]
+
+
+def test_register_oracle_rejects_bad_signature(oracle, passports):
+    pp = dict(passports[0])
+    pp["sig"] = pp["sig"] ^ 1
+    rc, _ = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
+    assert rc in (8, 9, 10)  # rsa.circom:48-71 checks
+
+
+def test_register_oracle_rejects_bad_flow(oracle, passports):
+    pp = dict(passports[0])
+    pp["dg1"] = bytes([pp["dg1"][0] ^ 1]) + pp["dg1"][1:]
+    rc, _ = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
+    assert rc == 7  # passportVerificationBuilder.circom:155
+
+
+def test_bigmultmodp_divmod_matches_literal_long_div(oracle, passports):
+    import pyref_bigint
+    from pzkwit import native
+    from test_capi import region_table
+    prm = oracle.register_params(**I.CANONICAL)
+    rc, w = oracle.register_witness(prm, I.pack_register_inputs(passports[0]))
+    assert rc == 0
+    mm = [r for r in region_table(I.CANONICAL) if r[2] == 5]
+    assert len(mm) == 17
+    K = 32
+    el = lambda i: oracle.from_elem(w[i])
+    for off, ln, _ in mm[:6] + mm[-2:]:
+        div = [el(off + i) for i in range(K + 1)]
+        mod = [el(off + K + 1 + i) for i in range(K)]
+        x = [el(off + 2 * K + 1 + i) for i in range(K)]
+        y = [el(off + 3 * K + 1 + i) for i in range(K)]
+        n = [el(off + 4 * K + 1 + i) for i in range(K)]
+        d2, m2 = pyref_bigint.big_mult_mod_p_divmod(x, y, n)
+        assert d2 == div and m2 == mod
+
+
+def test_smt_depth_inputs_satisfy_checks(oracle, passports):
+    pp = dict(passports[2])
+    pp["root"] = 12345
+    rc, w = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
+    assert rc == 0
+
+
+def test_smt_last_sibling_must_be_zero(oracle, passports):
+    pp = dict(passports[0])
+    pp["siblings"] = [0] * 79 + [7]
+    rc, _ = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
+    assert rc == 13  # SMTVerifier.circom:54

@@ -4,6 +4,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <array>
 #include <string>
 #include <vector>
 
@@ -24,6 +25,8 @@ struct Layout {
   std::vector<InputGroup> inputs;
   std::vector<Region> regions;
   std::vector<Work> work[E_COUNT];  // per emit kernel
+  std::vector<GenPiece> gen_pieces;  // pieces of the packed emitters' work items
+  std::vector<std::array<uint32_t, 3>> pos_emit_groups;  // (t, first work, works) of work[E_POS]
   std::vector<ShaJob> sha;
   uint32_t sha_core_words = 0;
   std::vector<PosTask> pos;            // sorted by level, then t

@@ -90,9 +90,48 @@ struct Builder {
       Region& r = L.regions[ri];
       if (r.kind == RK_POSEIDON) r.a[0] = inv[r.a[0]];
       int e = emitter_of(r.kind);
+      if (emitter_packed(e)) continue;
       std::vector<Work>* wl = &L.work[e];
+      if (r.kind == RK_BJJ_STEPS) {  // step-aligned: steps [k*S, (k+1)*S); step i starts at signal sig(i)
+        auto sig = [](uint32_t i) -> uint32_t { return i == 0 ? 0 : 46 + 60 * (i - 1); };
+        for (uint32_t i = 0; i < (uint32_t)BJJ_STEPS; i += BJJ_EMIT_STEPS) {
+          uint32_t a0 = sig(i), a1 = i + BJJ_EMIT_STEPS >= (uint32_t)BJJ_STEPS ? r.len : sig(i + BJJ_EMIT_STEPS);
+          wl->push_back(Work{ri, a0, a1 - a0, 0});
+        }
+        continue;
+      }
       uint32_t chunk = emitter_whole(e) ? r.len : EMIT_CHUNK;
       for (uint32_t s = 0; s < r.len; s += chunk) wl->push_back(Work{ri, s, std::min(chunk, r.len - s), 0});
+    }
+    // Poseidon emission: one launch per width t, each with the LDS its image needs
+    {
+      auto t_of = [&](const Work& w) { return L.pos[L.regions[w.region].a[0]].n + 1; };
+      std::vector<Work>& pw = L.work[E_POS];
+      std::stable_sort(pw.begin(), pw.end(), [&](const Work& x, const Work& y) { return t_of(x) < t_of(y); });
+      L.pos_emit_groups.clear();
+      for (uint32_t i = 0; i < pw.size(); i++) {
+        uint32_t t = (uint32_t)t_of(pw[i]);
+        if (L.pos_emit_groups.empty() || L.pos_emit_groups.back()[0] != t) L.pos_emit_groups.push_back({t, i, 0});
+        L.pos_emit_groups.back()[2]++;
+      }
+    }
+    // packed emitters: consecutive regions (witness order) share work items of <= GEN_PACK signals
+    for (int e = 0; e < E_COUNT; e++) {
+      if (!emitter_packed(e)) continue;
+      Work cur_w{0, 0, 0, 0};
+      auto flush = [&]() { if (cur_w.count) L.work[e].push_back(cur_w); cur_w = Work{(uint32_t)L.gen_pieces.size(), 0, 0, 0}; };
+      flush();
+      for (uint32_t ri = 0; ri < L.regions.size(); ri++) {
+        const Region& r = L.regions[ri];
+        if (emitter_of(r.kind) != e) continue;
+        for (uint32_t s = 0; s < r.len;) {
+          if (cur_w.count == GEN_PACK || cur_w.pad == GEN_MAX_PIECES) flush();
+          uint32_t take = std::min(r.len - s, GEN_PACK - cur_w.count);
+          L.gen_pieces.push_back(GenPiece{ri, s, cur_w.count, 0});
+          cur_w.count += take; cur_w.pad++; s += take;
+        }
+      }
+      flush();
     }
   }
 };

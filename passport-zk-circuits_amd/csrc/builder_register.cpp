@@ -209,7 +209,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   b.region(RK_BJJ_OWN, 3 + 2);
   b.region(RK_NUM2BITS, sz_num2bits(254), {254, 0, V_SK});
   b.region(RK_BJJ_STEPS, 46 + 253 * 60);
-  const int S_PKID = b.poseidon(2, {V_BJJ_X, V_BJJ_Y}, 0);
+  const int S_PKID = b.poseidon(2, {V_BJJ_X, V_BJJ_Y}, 3);  // level 3: after the BJJ core joins
 
   // outputs: main [dg15PubKeyHash, passportHash, dg1Commitment, pkIdentityHash]
   L.out_slots = {aa ? S_AA : -2, S_PASS, S_DG1C, S_PKID};

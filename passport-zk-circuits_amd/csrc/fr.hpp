@@ -171,4 +171,16 @@ __device__ __forceinline__ fr load_fr(const uint8_t* src) {
   return r;
 }
 
+// lane status: keep the smallest nonzero check code, so the value reported for a lane that fails
+// several checks does not depend on which kernel or stream reached it first
+__device__ __forceinline__ void lane_status(int32_t* st, int32_t code) {
+  if (!st) return;
+  int32_t old = *(volatile int32_t*)st;
+  while (old == 0 || old > code) {
+    int32_t seen = atomicCAS(st, old, code);
+    if (seen == old) return;
+    old = seen;
+  }
+}
+
 }  // namespace pzk

@@ -25,7 +25,7 @@ __global__ void k_load_values(const ValueLoad* loads, int n_loads, const uint8_t
 }
 
 // ------------------------------------------------------------------- SHA core
-__global__ void k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs, uint64_t n_inputs,
+__global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs, uint64_t n_inputs,
                            uint32_t* sha_core, uint32_t core_words, int32_t* status, uint32_t batch) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   int j = blockIdx.y;
@@ -38,7 +38,7 @@ __global__ void k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs
 // wave = 64 witnesses of one task. SMT level tasks below the insertion level depend on the
 // chain and are left to k_smt_chain.
 template <int T>
-__global__ void k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems,
+__global__ void __launch_bounds__(64, 1) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems,
                            const fr* smt_core, uint32_t smt_core_fr) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
@@ -114,21 +114,38 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   const int n = task.n, t = n + 1;
   PosLds P;
   pos_lds_carve(P, lds, t);
-  for (int i = 0; i < n; i++) P.inputs[i] = vs.at(task.in_slot[i], w);
-  P.hash = vs.at(task.out_slot, w);
+  if (threadIdx.x < (unsigned)n) P.inputs[threadIdx.x] = vs.at(task.in_slot[threadIdx.x], w);
+  if (threadIdx.x == 0) *P.hash = vs.at(task.out_slot, w);
   pos_lds_fill(P, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off);
   uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
   for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x)
-    store_fr(out + 32ull * q, fr_from_mont(pos_block_sig(P, n, wk.start + q)));
+    store_fr(out + 32ull * q, pos_block_sig(P, n, wk.start + q));
 }
 
 // ------------------------------------------------------------------- emit: generic small regions
+// A work item packs up to GEN_PACK signals from up to GEN_MAX_PIECES region slices (most generic
+// regions are a handful of signals: SMT levels, switchers, IsZero blocks). Thread q finds its
+// piece by binary search over the piece prefix sums staged in LDS.
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
+  __shared__ uint32_t cum[GEN_MAX_PIECES];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
-  const Region R = L.regions[wk.region];
-  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) emit_small(L, B, R, w, wk.start + q, out + 32ull * q);
+  const GenPiece* pc = L.gen_pieces + wk.region;
+  const uint32_t np = wk.pad;
+  for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cum[i] = pc[i].cum;
+  __syncthreads();
+  uint8_t* row = B.wtns + (size_t)w * B.stride;
+  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint32_t lo = 0, hi = np - 1;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi + 1) >> 1;
+      if (cum[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    const GenPiece p = pc[lo];
+    const Region& R = L.regions[p.region];
+    const uint32_t s = p.start + (q - cum[lo]);
+    emit_small(L, B, R, w, s, row + 32ull * (R.off + s));
+  }
 }
 
 // ------------------------------------------------------------------- launchers
@@ -223,7 +240,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   if (n_work == 0) return hipSuccess;
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (emitter) {
-    case E_GEN: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
+    case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
     case E_SHA: hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride); break;
     case E_POS: {
       size_t lds = sizeof(fr) * (size_t)pos_lds_elems(max_t);

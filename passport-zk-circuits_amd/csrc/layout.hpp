@@ -48,7 +48,8 @@ enum RegionKind : uint32_t {
 };
 
 // emit kernels (one work list each)
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_COUNT };
+// E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -57,11 +58,14 @@ __host__ __device__ inline int emitter_of(uint32_t kind) {
     case RK_FLOW: return E_FLOW;
     case RK_MODMUL: return E_MM;
     case RK_BJJ_STEPS: return E_BJJ;
+    case RK_RSA_OUT: return E_GENR;
     default: return E_GEN;
   }
 }
 // regions whose emit workgroup needs the whole region (LDS pre-pass over all of it)
 __host__ __device__ inline bool emitter_whole(int e) { return e == E_POS || e == E_BITS || e == E_FLOW; }
+// emitters whose work items pack many small regions (Work.region = first GenPiece, Work.pad = pieces)
+__host__ __device__ inline bool emitter_packed(int e) { return e == E_GEN || e == E_GENR; }
 
 constexpr int REGION_ARGS = 10;
 struct Region {
@@ -78,6 +82,15 @@ struct Work {
   uint32_t count;
   uint32_t pad;
 };
+// packed work: a run of region slices emitted by one workgroup; cum = signals before this piece
+struct GenPiece {
+  uint32_t region;
+  uint32_t start;
+  uint32_t cum;
+  uint32_t pad;
+};
+constexpr uint32_t GEN_PACK = 2048;        // signals per packed work item
+constexpr uint32_t GEN_MAX_PIECES = 256;   // pieces per packed work item
 
 // SHA hasher job: one (witness, hasher) lane of the SHA core kernel
 struct ShaJob {
@@ -115,6 +128,7 @@ struct RegInfo {
 // per-witness core sizes of the register-circuit kernels
 constexpr int MM_CORE_WORDS(int K) { return 12 * K - 3; }  // x[K] y[K] q[K+1] r[K] inv[K](4 words) carry[2K-2](2 words)
 constexpr int BJJ_STEPS = 254;
+constexpr int BJJ_EMIT_STEPS = 32;                           // ladder steps per k_emit_bjj work item
 constexpr int BJJ_CORE_FR = 5 * BJJ_STEPS;                  // per step: Dx, Dy, Ax, Ay, inv(Dx)   (Montgomery)
 constexpr int SMT_LEVELS = 80;
 constexpr int SMT_CORE_FR = 3 * SMT_LEVELS + 2;             // inv(sibling), root, flags per level; j; inv(root-root0)
@@ -152,6 +166,7 @@ struct DevLayout {
   uint32_t n_pos_levels;
   const Region* regions;
   const Work* work;
+  const GenPiece* gen_pieces;
   const ShaJob* sha;
   const PosTask* pos;
   const uint32_t* pos_level_start;  // tasks sorted by level: [start_l, start_{l+1})

@@ -120,18 +120,20 @@ struct PosLds {
   fr* part_in0;   // [RP]  p5 + C
   fr* part_prod;  // [RP][t]  S[..+i] * in_i
   fr* part_out;   // [RP][t]  mixS outputs (= Y_{r+1})
-  fr inputs[5];   // PoseidonHash inputs (Montgomery)
-  fr hash;
+  fr* inputs;     // [5] PoseidonHash inputs
+  fr* hash;       // [1]
+  fr* base;       // whole image: pos_lds_elems(t) elements
 };
 
 __host__ __device__ inline int pos_lds_elems(int t) {
   int RP = pos_nrp(t);
-  return 8 * t * 4 + 7 * t + 7 * t * t + t + (RP + 1) * t + 4 * RP + RP * t;
+  return 8 * t * 4 + 7 * t + 7 * t * t + t + (RP + 1) * t + 4 * RP + RP * t + 6;
 }
 
 __device__ __forceinline__ void pos_lds_carve(PosLds& L, fr* base, int t) {
   int RP = pos_nrp(t);
   L.t = t; L.RP = RP;
+  L.base = base;
   fr* p = base;
   L.full_in = p; p += 8 * t;
   L.full_p2 = p; p += 8 * t;
@@ -146,6 +148,8 @@ __device__ __forceinline__ void pos_lds_carve(PosLds& L, fr* base, int t) {
   L.part_p5 = p; p += RP;
   L.part_in0 = p; p += RP;
   L.part_prod = p; p += RP * t;
+  L.inputs = p; p += 5;
+  L.hash = p; p += 1;
   L.part_out = L.part_in + t;  // Y_{r+1}
 }
 
@@ -186,6 +190,10 @@ __device__ __forceinline__ void pos_lds_fill(PosLds& L, const PosConsts& K, cons
     L.part_prod[q] = fr_mul(K.S(t, (2 * t - 1) * r + i), in);
   }
   __syncthreads();
+  // the image is emitted in normal form: convert every element once here rather than every
+  // signal at store time (GetSumOfNElements sums are linear, so they are summed in normal form)
+  for (int q = tid, n = pos_lds_elems(t); q < n; q += nt) L.base[q] = fr_from_mont(L.base[q]);
+  __syncthreads();
 }
 
 // GetSumOfNElements(t) block over an LDS product row: out | in[t] | sum[t-1]
@@ -199,14 +207,14 @@ __device__ __forceinline__ fr pos_getsum(const fr* prod, int t, int j) {
   return prod[j - 1];
 }
 
-// value (Montgomery) of local signal s of the PoseidonHash(n) block
+// value (normal form, after pos_lds_fill) of local signal s of the PoseidonHash(n) block
 __device__ __forceinline__ fr pos_block_sig(const PosLds& L, int n, uint32_t s) {
   const int t = L.t, RP = L.RP;
-  if (s == 0) return L.hash;
+  if (s == 0) return *L.hash;
   if (s <= (uint32_t)n) return L.inputs[s - 1];
   s -= 1 + n;
   // PoseidonEx own: out | in[n] | initialState
-  if (s == 0) return L.hash;
+  if (s == 0) return *L.hash;
   if (s <= (uint32_t)n) return L.inputs[s - 1];
   if (s == (uint32_t)n + 1) return fr_zero();
   s -= 2 + n;
@@ -273,7 +281,7 @@ __device__ __forceinline__ fr pos_block_sig(const PosLds& L, int n, uint32_t s) 
   if (s < SIG) return sigma_sig(7, s);
   s -= SIG;
   // mixLast: out | in[t] | sum (2t)
-  if (s == 0) return L.hash;
+  if (s == 0) return *L.hash;
   if (s <= (uint32_t)t) return L.full_p5[7 * t + s - 1];
   return pos_getsum(L.last_prod, t, s - 1 - t);
 }

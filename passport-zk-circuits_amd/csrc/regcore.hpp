@@ -36,7 +36,7 @@ __device__ __forceinline__ uint32_t in_bit(const uint8_t* row, int idx, bool& ba
   return a.x & 1u;
 }
 __device__ __forceinline__ void set_status(int32_t* st, int32_t code) {
-  if (st) atomicCAS(st, 0, code);
+  lane_status(st, code);
 }
 // integer from bits (bit k of the number = get(k)), L <= 254
 template <typename F>
@@ -56,7 +56,7 @@ __device__ __forceinline__ fr fr_from_i128(uint64_t lo, uint64_t hi) {
 
 // ============================================================================ k_prep
 // lane = witness. Runs after k_sha_core (needs the SA digest).
-__global__ void k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
+__global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
   const RegInfo& R = L.reg;
@@ -360,7 +360,7 @@ struct BjjConsts {
 };
 
 // scratch: SoA [elem][witness] with 3 * 2 * 254 (X, Y, Z of D_i and A_i) + 3 * 254 prefix products
-__global__ void k_bjj_core(DevLayout L, ValueStore vs, fr* bjj_core, fr* scratch, uint32_t batch) {
+__global__ void __launch_bounds__(64, 1) k_bjj_core(DevLayout L, ValueStore vs, fr* bjj_core, fr* scratch, uint32_t batch) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
   BjjConsts C;
@@ -421,7 +421,7 @@ __global__ void k_bjj_core(DevLayout L, ValueStore vs, fr* bjj_core, fr* scratch
 // ============================================================================ SMT
 // flags per level (u32 in the SMT core): bit0 levIns, bit1 done, bit2 st_top, bit3 st_inew, bit4 lrbit, bit5 isZero
 // SMT core (Fr): [inv(sibling) normal][80] [root Montgomery][80] [flags][80] [j, inv(root_in - root_0)]
-__global__ void k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
+__global__ void __launch_bounds__(64, 1) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            uint32_t batch) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
@@ -481,7 +481,7 @@ __global__ void k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr
 }
 
 // sequential part: levels j-1 .. 0, then all roots and the isEqual inverse
-__global__ void k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs, ValueStore vs,
+__global__ void __launch_bounds__(64, 1) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs, ValueStore vs,
                             fr* pos_core, fr* smt_core, uint32_t batch) {
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;

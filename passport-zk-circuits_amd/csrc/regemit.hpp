@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
     W256 vv; for (int i = 0; i < 8; i++) vv.v[i] = v.v[i];
     W256 m = w_mask(vv, Lb);
     bool ok = true; for (int i = 0; i < 8; i++) ok &= m.v[i] == vv.v[i];
-    if (!ok && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_NUM2BITS);
+    if (!ok && B.status) lane_status(B.status + w, ST_NUM2BITS);
   }
   __syncthreads();
   W256 V; for (int i = 0; i < 8; i++) V.v[i] = val[i];
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
       for (int i = 0; i < 127; i++) { uint64_t lo, hi; alias_part(V, i, lo, hi); u192_add(acc, lo, hi); }
       sout[0] = acc[0]; sout[1] = acc[1]; sout[2] = acc[2];
       W256 so = u192_w(acc);
-      if (w_bit(so, 127) && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_ALIAS);
+      if (w_bit(so, 127) && B.status) lane_status(B.status + w, ST_ALIAS);
     }
     __syncthreads();
   }
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
   if (threadIdx.x == 0) {
     uint8_t c = 1;
     for (int k = 0; k < 776; k++) { c &= eq[k]; chain[k] = c; }
-    if (!c && B.status) atomicCAS(B.status + w, 0, (int32_t)ST_FLOW);
+    if (!c && B.status) lane_status(B.status + w, ST_FLOW);
   }
   __syncthreads();
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
@@ -373,7 +373,13 @@ __device__ __forceinline__ W256 u192w(const U192& a) {
   r.v[4] = (uint32_t)a.a2; r.v[5] = (uint32_t)(a.a2 >> 32);
   return r;
 }
-__host__ __device__ inline uint32_t kara_size(int N) { return N == 1 ? 4 : 4 * N + 3 * kara_size(N / 2); }
+// KaratsubaOverflow(N) block size S(N) = 4N + 3 S(N/2), S(1) = 4 (closed table, no recursion)
+__host__ __device__ inline uint32_t kara_size(int N) {
+  switch (N) {
+    case 1: return 4; case 2: return 20; case 4: return 76; case 8: return 260; case 16: return 844;
+    case 32: return 2660; case 64: return 8236; default: return 0;
+  }
+}
 
 // Karatsuba subtree signal (bigIntHelpers.circom:11-53)
 __device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
@@ -563,78 +569,127 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps
+// Two stages. (1) Per ladder step, the twelve distinct field values its 60 signals are drawn
+// from (coordinates, the adder's/doubler's products, the IsZero inverse) are computed once, in
+// normal form, into an LDS record: one thread per (step, value). (2) Every signal is then a
+// select from the record (plus at most one subtraction, which needs no Montgomery form).
+// Work items are step-aligned (BJJ_EMIT_STEPS steps each, builder_impl.hpp).
+enum BjjRec { BR_X1, BR_Y1, BR_OX, BR_OY, BR_INV, BR_X1Y2, BR_Y1X2, BR_DELTA, BR_TAU, BR_XYD, BR_DELTAD, BR_TAUD, BR_N };
+
+__device__ __forceinline__ uint32_t bjj_step_of(uint32_t s) { return s < 46 ? 0 : 1 + (s - 46) / 60; }
+__device__ __forceinline__ uint32_t bjj_sig_of(uint32_t i) { return i == 0 ? 0 : 46 + 60 * (i - 1); }
+
 __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
+  __shared__ fr rec[(BJJ_EMIT_STEPS + 1) * BR_N];
+  __shared__ uint32_t bits[BJJ_EMIT_STEPS + 1];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
-  BjjConsts C;
-  C.init();
   const fr* core = B.bjj_core + (size_t)w * L.bjj_core_fr;
-  fr sk = fr_from_mont(B.vs.at(L.reg.v_sk, w));
+  const uint32_t i0 = bjj_step_of(wk.start), i1 = bjj_step_of(wk.start + wk.count - 1) + 1;
+  const int base = i0 == 0 ? 0 : (int)i0 - 1;  // local record 0 = step base (predecessor of i0 when i0 > 0)
+  const int nrec = (int)i1 - base;
+  {
+    fr skm = B.vs.at(L.reg.v_sk, w);
+    fr sk = fr_from_mont(skm);
+    for (int j = threadIdx.x; j < nrec; j += blockDim.x) {
+      int i = base + j;
+      bits[j] = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < nrec * BR_N; q += blockDim.x) {
+    const int j = q / BR_N, v = q - j * BR_N, i = base + j;
+    const fr* P = core + 5 * i;
+    fr r;
+    if (v >= BR_XYD) {  // doubler of step i (doublers[i-1]) over A_{i-1}
+      if (i == 0) r = fr_zero();
+      else {
+        fr xp = P[-3], yp = P[-2];  // core + 5(i-1) + 2, + 3
+        fr xy = fr_mul(xp, yp);
+        if (v == BR_XYD) r = xy;
+        else if (v == BR_DELTAD) r = fr_mul(fr_sub(yp, fr_mul(fr_to_mont(fr_u64(BJJ_A)), xp)), fr_add(xp, yp));
+        else r = fr_sqr(xy);
+      }
+    } else if (v == BR_OX || v == BR_OY) {
+      r = P[v];
+    } else {
+      const bool bit = bits[j];
+      fr x1 = i == 0 ? fr_zero() : P[0], y1 = i == 0 ? fr_zero() : P[1];
+      fr x2 = bit ? fr_to_mont(fr_const(BJJ_B8X)) : fr_zero(), y2 = bit ? fr_to_mont(fr_const(BJJ_B8Y)) : fr_zero();
+      switch (v) {
+        case BR_X1: r = x1; break;
+        case BR_Y1: r = y1; break;
+        case BR_INV: r = i == 0 ? fr_zero() : P[4]; break;
+        case BR_X1Y2: r = fr_mul(x1, y2); break;
+        case BR_Y1X2: r = fr_mul(y1, x2); break;
+        case BR_DELTA: r = fr_mul(fr_sub(y1, fr_mul(fr_to_mont(fr_u64(BJJ_A)), x1)), fr_add(x2, y2)); break;
+        default: r = fr_mul(fr_mul(x1, y2), fr_mul(y1, x2)); break;
+      }
+    }
+    rec[q] = fr_from_mont(r);
+  }
+  __syncthreads();
+  const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
-    uint32_t s = wk.start + q;
-    int i; uint32_t t; bool dbl;
-    if (s < 46) { i = 0; t = s; dbl = false; }
-    else { uint32_t s2 = s - 46; i = 1 + s2 / 60; t = s2 % 60; dbl = t >= 46; if (dbl) t -= 46; }
+    const uint32_t s = wk.start + q, i = bjj_step_of(s), t = s - bjj_sig_of(i);
+    const int j = (int)i - base;
+    const fr* rc = rec + j * BR_N;
     fr res;
-    if (dbl) {
-      // doublers[i-1]: out[2] = D_i | in[2] = A_{i-1} | adder: out, in1, in2, beta, gamma, delta, tau
-      const fr* Pp = core + 5 * (i - 1);
-      fr x = Pp[2], y = Pp[3];
-      const fr* Pc = core + 5 * i;
-      if (t < 2) res = Pc[t];
-      else if (t < 4) res = t == 2 ? x : y;
-      else {
-        uint32_t u = t - 4;
-        if (u < 2) res = Pc[u];
-        else if (u < 6) res = (u & 1) ? y : x;  // in1, in2 = (x, y)
-        else if (u == 6 || u == 7) res = fr_mul(x, y);
-        else if (u == 8) res = fr_mul(fr_sub(y, fr_mul(C.A, x)), fr_add(x, y));
-        else { fr b = fr_mul(x, y); res = fr_mul(b, b); }
-      }
+    if (t >= 46) {  // doublers[i-1]: out[2] = D_i | in[2] = A_{i-1} | adder out, in1, in2, beta, gamma, delta, tau
+      const fr* rp = rc - BR_N;
+      uint32_t u = t - 46;
+      if (u < 2) res = rc[BR_X1 + u];
+      else if (u < 4) res = rp[BR_OX + u - 2];
+      else if (u < 6) res = rc[BR_X1 + u - 4];
+      else if (u < 10) res = rp[BR_OX + (u & 1)];
+      else if (u < 12) res = rc[BR_XYD];
+      else res = rc[u == 12 ? BR_DELTAD : BR_TAUD];
     } else {
-      const fr* P = core + 5 * i;
-      int bit = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
-      fr x1 = i == 0 ? fr_zero() : P[0], y1 = i == 0 ? fr_zero() : P[1];
-      fr x2 = bit ? C.B8x : fr_zero(), y2 = bit ? C.B8y : fr_zero();
-      bool z1 = fr_is_zero(x1), z2 = !bit;
-      fr ox = P[2], oy = P[3];
-      fr rawx = (!z1 && !z2) ? ox : fr_zero(), rawy = (!z1 && !z2) ? oy : fr_zero();
-      if (t < 2) res = t == 0 ? ox : oy;
+      const bool bit = bits[j];
+      const fr x1 = rc[BR_X1], y1 = rc[BR_Y1];
+      const fr x2 = bit ? B8x : fr_zero(), y2 = bit ? B8y : fr_zero();
+      const bool z1 = fr_is_zero(x1), z2 = !bit;
+      const fr rawx = (!z1 && !z2) ? rc[BR_OX] : fr_zero(), rawy = (!z1 && !z2) ? rc[BR_OY] : fr_zero();
+      if (t < 2) res = rc[BR_OX + t];
       else if (t < 4) res = t == 2 ? x1 : y1;
       else if (t < 6) res = t == 4 ? x2 : y2;
-      else if (t < 9) { uint32_t u = t - 6; res = u == 0 ? (z1 ? fr_mont_one() : fr_zero()) : u == 1 ? x1 : (i == 0 ? fr_zero() : P[4]); }
-      else if (t < 12) {
-        uint32_t u = t - 9;
-        res = u == 0 ? (z2 ? fr_mont_one() : fr_zero()) : u == 1 ? x2 : (bit ? fr_to_mont(fr_const(BJJ_INV_B8X)) : fr_zero());
-      } else if (t < 22) {  // adder: out[2] | in1[2], in2[2] | beta, gamma, delta, tau
+      else if (t < 9) res = t == 6 ? (z1 ? one : fr_zero()) : t == 7 ? x1 : rc[BR_INV];
+      else if (t < 12) res = t == 9 ? (z2 ? one : fr_zero()) : t == 10 ? x2 : (bit ? fr_const(BJJ_INV_B8X) : fr_zero());
+      else if (t < 22) {  // adder: out[2] | in1[2], in2[2] | beta, gamma, delta, tau
         uint32_t u = t - 12;
         if (u < 2) res = u == 0 ? rawx : rawy;
         else if (u < 4) res = u == 2 ? x1 : y1;
         else if (u < 6) res = u == 4 ? x2 : y2;
-        else if (u == 6) res = fr_mul(x1, y2);
-        else if (u == 7) res = fr_mul(y1, x2);
-        else if (u == 8) res = fr_mul(fr_sub(y1, fr_mul(C.A, x1)), fr_add(x2, y2));
-        else res = fr_mul(fr_mul(x1, y2), fr_mul(y1, x2));
+        else res = rc[BR_X1Y2 + (u - 6)];
       } else {  // switchers L0, R0, L1, R1: out[2] | bool, in[2] | aux
         uint32_t u = t - 22, sw = u / 6, k = u % 6;
-        int c = sw >> 1;
-        fr raw = c == 0 ? rawx : rawy, in1c = c == 0 ? x1 : y1, in2c = c == 0 ? x2 : y2;
-        fr bl = z2 ? fr_mont_one() : fr_zero();
-        fr l0 = z2 ? in1c : raw, l1 = z2 ? raw : in1c;
+        const bool cy = (sw >> 1) != 0;
+        const fr raw = cy ? rawy : rawx, in1c = cy ? y1 : x1, in2c = cy ? y2 : x2;
+        const fr l0 = z2 ? in1c : raw, l1 = z2 ? raw : in1c;
         if ((sw & 1) == 0) {
-          fr vals[6] = {l0, l1, bl, raw, in1c, z2 ? fr_sub(in1c, raw) : fr_zero()};
-          res = vals[k];
+          switch (k) {
+            case 0: res = l0; break;
+            case 1: res = l1; break;
+            case 2: res = z2 ? one : fr_zero(); break;
+            case 3: res = raw; break;
+            case 4: res = in1c; break;
+            default: res = z2 ? fr_sub(in1c, raw) : fr_zero(); break;
+          }
         } else {
-          fr br = z1 ? fr_mont_one() : fr_zero();
-          fr r0 = z1 ? in2c : l0, r1 = z1 ? l0 : in2c;
-          fr vals[6] = {r0, r1, br, l0, in2c, z1 ? fr_sub(in2c, l0) : fr_zero()};
-          res = vals[k];
+          switch (k) {
+            case 0: res = z1 ? in2c : l0; break;
+            case 1: res = z1 ? l0 : in2c; break;
+            case 2: res = z1 ? one : fr_zero(); break;
+            case 3: res = l0; break;
+            case 4: res = in2c; break;
+            default: res = z1 ? fr_sub(in2c, l0) : fr_zero(); break;
+          }
         }
       }
     }
-    store_fr(out + 32ull * q, fr_from_mont(res));
+    store_fr(out + 32ull * q, res);
   }
 }
 

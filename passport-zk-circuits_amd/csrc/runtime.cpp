@@ -37,12 +37,15 @@ static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k
                                               "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
                                               "k_emit_flow",   "k_emit_mm",   "k_emit_bjj"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
-                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ};
+                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN};
 
+// Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
+// levels before and after the SMT prep); its time is the sum of its brackets, each bracket
+// recorded on the stream the phase's kernels run on.
 struct Timing {
-  static constexpr int RING = 8;
-  hipEvent_t ev[RING][PH_COUNT][2] = {};
-  bool used[RING][PH_COUNT] = {};
+  static constexpr int RING = 8, OCC = 4;
+  hipEvent_t ev[RING][PH_COUNT][OCC][2] = {};
+  int used[RING][PH_COUNT] = {};
   bool pending[RING] = {};
   int head = 0;
   double ms[PH_COUNT] = {};
@@ -51,32 +54,39 @@ struct Timing {
     if (!pending[slot]) return;
     for (int p = 0; p < PH_COUNT; p++) {
       if (!used[slot][p]) continue;
-      float t = 0;
-      (void)hipEventSynchronize(ev[slot][p][1]);
-      if (hipEventElapsedTime(&t, ev[slot][p][0], ev[slot][p][1]) == hipSuccess) { ms[p] += t; n[p]++; }
-      used[slot][p] = false;
+      double sum = 0;
+      bool ok = true;
+      for (int k = 0; k < used[slot][p]; k++) {
+        float t = 0;
+        (void)hipEventSynchronize(ev[slot][p][k][1]);
+        if (hipEventElapsedTime(&t, ev[slot][p][k][0], ev[slot][p][k][1]) == hipSuccess) sum += t; else ok = false;
+      }
+      if (ok) { ms[p] += sum; n[p]++; }
+      used[slot][p] = 0;
     }
     pending[slot] = false;
   }
   void destroy() {
     for (auto& a : ev)
       for (auto& b : a)
-        for (auto& e : b)
-          if (e) (void)hipEventDestroy(e);
+        for (auto& c : b)
+          for (auto& e : c)
+            if (e) (void)hipEventDestroy(e);
   }
 };
 
 struct PhaseScope {
-  Timing* T; int slot, ph; hipStream_t st;
+  Timing* T; int slot, ph, k = -1; hipStream_t st;
   PhaseScope(Timing* t, int s, int p, hipStream_t stream) : T(t), slot(s), ph(p), st(stream) {
-    if (!T) return;
-    for (auto& e : T->ev[slot][ph]) if (!e) (void)hipEventCreate(&e);
-    (void)hipEventRecord(T->ev[slot][ph][0], st);
+    if (!T || T->used[slot][ph] >= Timing::OCC) return;
+    k = T->used[slot][ph];
+    for (auto& e : T->ev[slot][ph][k]) if (!e) (void)hipEventCreate(&e);
+    (void)hipEventRecord(T->ev[slot][ph][k][0], st);
   }
   ~PhaseScope() {
-    if (!T) return;
-    (void)hipEventRecord(T->ev[slot][ph][1], st);
-    T->used[slot][ph] = true;
+    if (k < 0) return;
+    (void)hipEventRecord(T->ev[slot][ph][k][1], st);
+    T->used[slot][ph] = k + 1;
   }
 };
 
@@ -86,9 +96,16 @@ struct pzk_instance {
   Layout lay;
   int device = 0;
   hipStream_t stream = nullptr;
+  // side streams of the register pipeline (RSA core + emission; BJJ core + SHA/BJJ emission).
+  // Three streams in all: with the null stream they fit the 4 hardware queues HIP maps
+  // streams onto by default, so no two of them share a queue.
+  hipStream_t s_rsa = nullptr, s_bjj = nullptr;
+  hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_j_rsa = nullptr,
+             ev_j_bjj = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
   Work* d_work[E_COUNT] = {};
+  GenPiece* d_gen_pieces = nullptr;
   ShaJob* d_sha = nullptr;
   PosTask* d_pos = nullptr;
   ValueLoad* d_loads = nullptr;
@@ -118,6 +135,7 @@ struct pzk_instance {
     L.n_values = lay.n_values;
     L.n_pos_levels = (uint32_t)lay.pos_level_start.size() - 1;
     L.regions = d_regions;
+    L.gen_pieces = d_gen_pieces;
     L.sha = d_sha;
     L.pos = d_pos;
     L.reg = lay.reg;
@@ -207,13 +225,16 @@ static void free_scratch(pzk_instance* I) {
 
 static void free_all(pzk_instance* I) {
   free_scratch(I);
-  void* ptrs[] = {I->d_regions, I->d_sha, I->d_pos, I->d_loads, I->d_level_task, I->d_pos_consts,
-                  I->d_in, I->d_out, I->d_status};
+  void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
+                  I->d_pos_consts, I->d_in, I->d_out, I->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  if (I->stream) (void)hipStreamDestroy(I->stream);
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_bjj})
+    if (s) (void)hipStreamDestroy(s);
+  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_j_rsa, I->ev_j_bjj})
+    if (e) (void)hipEventDestroy(e);
   I->timing.destroy();
 }
 
@@ -239,14 +260,18 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
     if (I->lay.pos[i].smt_level >= 0) level_task[I->lay.pos[i].smt_level] = (int32_t)i;
   rc = upload(&I->d_regions, I->lay.regions);
   for (int e = 0; e < E_COUNT && !rc; e++) rc = upload(&I->d_work[e], I->lay.work[e]);
+  if (!rc) rc = upload(&I->d_gen_pieces, I->lay.gen_pieces);
   if (!rc) rc = upload(&I->d_sha, I->lay.sha);
   if (!rc) rc = upload(&I->d_pos, I->lay.pos);
   if (!rc) rc = upload(&I->d_loads, I->lay.loads);
   if (!rc && I->lay.is_register) rc = upload(&I->d_level_task, level_task);
   if (rc) { free_all(I); delete I; return rc; }
-  if (hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) != hipSuccess) {
-    free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate failed");
-  }
+  bool ok = hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&I->s_rsa, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&I->s_bjj, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_j_rsa, &I->ev_j_bjj})
+    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
   *out = I;
   return 0;
 }
@@ -374,27 +399,61 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     }
     return 0;
   };
+  auto emit = [&](int e, hipStream_t s) -> int {
+    PhaseScope ps(lay.work[e].empty() ? nullptr : T, slot, EMIT_PHASE[e], s);
+    if (e == E_POS) {
+      for (const auto& g : lay.pos_emit_groups)
+        HIPCHK(launch_emit(e, L, I->d_work[e] + g[1], g[2], K, bufs, B, (int)g[0], s));
+    } else {
+      HIPCHK(launch_emit(e, L, I->d_work[e], (uint32_t)lay.work[e].size(), K, bufs, B, lay.max_t, s));
+    }
+    return 0;
+  };
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
     HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, I->d_values, B, st)); }
-  { PhaseScope ps(T, slot, PH_SHA_CORE, st);
-    HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
-  if (lay.is_register) {
+  if (!lay.is_register) {
+    { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
+    for (int e = 0; e < E_COUNT; e++)
+      if ((rc = emit(e, st))) return rc;
+  } else {
+    // Three streams (DESIGN.md "Schedule"). The RSA and BabyJubJub cores depend only on the
+    // inputs, so they start at once on their own streams and their emitters follow them there
+    // (the SHA emitter behind the BJJ core). The main stream runs the Poseidon/SMT dependency
+    // chain and the remaining emitters, then joins the side streams.
+    HIPCHK(hipEventRecord(I->ev_load, st));
+    HIPCHK(hipStreamWaitEvent(I->s_rsa, I->ev_load, 0));
+    HIPCHK(hipStreamWaitEvent(I->s_bjj, I->ev_load, 0));
+    { PhaseScope ps(T, slot, PH_RSA_CORE, I->s_rsa);
+      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, I->s_rsa)); }
+    HIPCHK(hipEventRecord(I->ev_rsa, I->s_rsa));
+    if ((rc = emit(E_MM, I->s_rsa))) return rc;
+    HIPCHK(hipEventRecord(I->ev_j_rsa, I->s_rsa));
+    { PhaseScope ps(T, slot, PH_BJJ_CORE, I->s_bjj);
+      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_core, I->d_bjj_scratch, I->s_bjj)); }
+    HIPCHK(hipEventRecord(I->ev_bjj, I->s_bjj));
+    { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
+    HIPCHK(hipEventRecord(I->ev_sha, st));
+    HIPCHK(hipStreamWaitEvent(I->s_bjj, I->ev_sha, 0));
+    if ((rc = emit(E_SHA, I->s_bjj))) return rc;
+    if ((rc = emit(E_BJJ, I->s_bjj))) return rc;
+    HIPCHK(hipEventRecord(I->ev_j_bjj, I->s_bjj));
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
-    { PhaseScope ps(T, slot, PH_RSA_CORE, st); HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, st)); }
-    { PhaseScope ps(T, slot, PH_BJJ_CORE, st); HIPCHK(launch_bjj_core(L, vs, I->d_bjj_core, I->d_bjj_scratch, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, I->d_pos_core, I->d_smt_core, st)); }
-  } else {
-    PhaseScope ps(T, slot, PH_POS_CORE, st);
-    if ((rc = pos_levels(0, 1 << 20))) return rc;
-  }
-  for (int e = 0; e < E_COUNT; e++) {
-    PhaseScope ps(lay.work[e].empty() ? nullptr : T, slot, EMIT_PHASE[e], st);
-    HIPCHK(launch_emit(e, L, I->d_work[e], (uint32_t)lay.work[e].size(), K, bufs, B, lay.max_t, st));
+    HIPCHK(hipStreamWaitEvent(st, I->ev_bjj, 0));
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
+    if ((rc = emit(E_GEN, st))) return rc;
+    if ((rc = emit(E_FLOW, st))) return rc;
+    if ((rc = emit(E_POS, st))) return rc;
+    HIPCHK(hipStreamWaitEvent(st, I->ev_rsa, 0));
+    if ((rc = emit(E_BITS, st))) return rc;
+    if ((rc = emit(E_GENR, st))) return rc;
+    for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));
   }
   if (exec && (exec->flags & PZK_EXEC_SYNC)) HIPCHK(hipStreamSynchronize(st));
   return 0;

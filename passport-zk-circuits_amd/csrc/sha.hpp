@@ -73,7 +73,7 @@ __device__ __forceinline__ void sha_core_lane(const uint8_t* in_row, const ShaJo
   uint32_t* hout = core + job.core_off + job.blocks * SHA_BLOCK_CORE;
 #pragma unroll
   for (int j = 0; j < 8; j++) hout[j] = H[j];
-  if (bad && status) atomicCAS(status, 0, (int32_t)ST_INPUT_RANGE);
+  if (bad) lane_status(status, ST_INPUT_RANGE);
 }
 
 // ------------------------------------------------------------ closed-form signals

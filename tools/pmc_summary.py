@@ -1,0 +1,48 @@
+"""Per-kernel PMC summary (last dispatch of each kernel) from rocprofv3 counter_collection CSVs.
+
+usage: pmc_summary.py DIR_PREFIX   (reads DIR_PREFIX_sq, _rd, _wr)
+FETCH_SIZE is doubled (gfx950 reports half the bytes of wide streaming reads; MI355X_MICROARCH.md
+HBM section); FETCH_SIZE / WRITE_SIZE are in KB."""
+import csv
+import os
+import sys
+from collections import defaultdict
+
+
+def load(path):
+    per = defaultdict(dict)  # (kernel, dispatch) -> counters
+    dur = {}
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pzk::", "")
+        key = (k, int(r["Dispatch_Id"]))
+        per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    agg = defaultdict(lambda: defaultdict(float))
+    n = defaultdict(int)
+    for (k, d), c in per.items():
+        n[k] += 1
+        for name, v in c.items():
+            agg[k][name] += v
+        agg[k]["ms"] += dur[(k, d)]
+    return {k: {name: v / n[k] for name, v in c.items()} for k, c in agg.items()}
+
+
+def main(prefix):
+    sq = load(prefix + "_sq/run_counter_collection.csv")
+    rd = load(prefix + "_rd/run_counter_collection.csv") if os.path.exists(prefix + "_rd") else {}
+    wr = load(prefix + "_wr/run_counter_collection.csv") if os.path.exists(prefix + "_wr") else {}
+    print(f"{'kernel':26s} {'ms':>7s} {'waves':>9s} {'valu/wave':>9s} {'salu/w':>7s} {'vmwr/w':>7s} "
+          f"{'lds/w':>6s} {'rd GB':>7s} {'wr GB':>7s} {'rd+wr GB/s':>10s}")
+    for k in sorted(sq, key=lambda k: -sq[k]["ms"]):
+        c = sq[k]
+        w = max(c.get("SQ_WAVES", 1), 1)
+        rgb = 2 * rd.get(k, {}).get("FETCH_SIZE", 0) * 1024 / 1e9
+        wgb = wr.get(k, {}).get("WRITE_SIZE", 0) * 1024 / 1e9
+        ms = wr.get(k, {}).get("ms", c["ms"])
+        print(f"{k:26s} {c['ms']:7.3f} {w:9.0f} {c.get('SQ_INSTS_VALU', 0) / w:9.0f} {c.get('SQ_INSTS_SALU', 0) / w:7.0f} "
+              f"{c.get('SQ_INSTS_VMEM_WR', 0) / w:7.1f} {c.get('SQ_INSTS_LDS', 0) / w:6.0f} {rgb:7.2f} {wgb:7.2f} "
+              f"{(rgb + wgb) / ms if ms else 0:10.1f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

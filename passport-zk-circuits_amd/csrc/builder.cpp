@@ -2,11 +2,103 @@
 // every offset here is re-derived independently of the CPU oracle, and the parity tests
 // compare the two layouts element by element.
 #include "builder_impl.hpp"
+#include "sha_prog.hpp"
 
 #include <algorithm>
 #include <map>
 
 namespace pzk {
+
+// Descriptors of the 150,762 signals of one SHA-256 block, in witness order (sha_prog.hpp).
+// Mirrors the template signal order of sha256Schedule.circom:11-72, sha256Rounds.circom:12-125
+// and sha256Compress.circom:11-96; the GPU tests check every emitted element against the oracle.
+void sha_program(std::vector<uint32_t>& P) {
+  P.clear();
+  P.reserve(SHA_BLOCK_SIGNALS_COUNT);
+  auto X = [&](int idx, int lo, int n) { P.push_back(sha_desc(idx, lo, n, SHA_D_EXTRACT)); };
+  auto M = [&](int idx, int lo, int n) { P.push_back(sha_desc(idx, lo, n, SHA_D_MASK)); };
+  auto bits32 = [&](int idx) { for (int i = 0; i < 32; i++) X(idx, i, 1); };
+  // GetSumOfNElements(32) of (1<<i)*bit_i(X): out | in[32] | sum[31]
+  auto getsum32 = [&](int idx) {
+    X(idx, 0, 64);
+    for (int j = 1; j <= 32; j++) M(idx, j - 1, 1);
+    for (int j = 33; j < 64; j++) M(idx, 0, j - 31);
+  };
+  // GetLastNBits(32) of V: div | out[32] | in | check[32] | GetLastBitUnsecure[32] (in, out, div)
+  auto lastnbits32 = [&](int idx) {
+    X(idx, 32, 64);
+    for (int j = 1; j <= 32; j++) X(idx, j - 1, 1);
+    X(idx, 0, 64);
+    for (int j = 34; j < 66; j++) M(idx, 0, j - 33);
+    for (int q = 0; q < 32; q++) { X(idx, q, 1); X(idx, q + 1, 64); X(idx, q, 64); }
+  };
+  // Bits2Num(32): out | in[32] | sum[32]
+  auto bits2num32 = [&](int idx) {
+    X(idx, 0, 64);
+    for (int j = 1; j <= 32; j++) X(idx, j - 1, 1);
+    for (int j = 33; j <= 64; j++) M(idx, 0, j - 32);
+  };
+  auto hin = [](int j) { return j < 4 ? sha_wt_a(-j) : sha_wt_e(4 - j); };
+  // ---- Sha2_224_256Shedule
+  for (int k = 0; k < 64; k++) X(SHA_WT_W + k, 0, 64);                 // outWords
+  for (int k = 0; k < 16; k++) bits32(SHA_WT_W + k);                   // chunkBits[16][32]
+  for (int k = 0; k < 64; k++) bits32(SHA_WT_W + k);                   // outBits[64][32]
+  for (int k = 0; k < 16; k++) getsum32(SHA_WT_W + k);                 // sumN[16]
+  for (int r = 0; r < 48; r++) {
+    const int b = SHA_WT_SCH + SHA_SCH_WORDS * r;
+    getsum32(b + SW_S0);
+    getsum32(b + SW_S1);
+    for (int i = 0; i < 32; i++) {  // s0Xor[i], s1Xor[i]: XOR3_v2 out | x, y, z | tmp
+      X(b + SW_S0, i, 1); X(b + SW_X7, i, 1); X(b + SW_Y18, i, 1); X(b + SW_Z3, i, 1); X(b + SW_T0, i, 1);
+      X(b + SW_S1, i, 1); X(b + SW_X17, i, 1); X(b + SW_Y19, i, 1); X(b + SW_Z10, i, 1); X(b + SW_T1, i, 1);
+    }
+    lastnbits32(b + SW_V);
+    bits2num32(SHA_WT_W + r + 16);
+  }
+  // ---- Sha2_224_256Rounds(64): own signals
+  for (int j = 0; j < 8; j++)
+    for (int i = 0; i < 32; i++) X(SHA_WT_FF32 + j, i, 1);          // outHash[8][32]
+  for (int k = 0; k < 64; k++) X(SHA_WT_W + k, 0, 64);                 // words
+  for (int j = 0; j < 8; j++) bits32(hin(j));                          // hashBits
+  for (int arr = 0; arr < 3; arr++)                                    // a, b, c [65][32]
+    for (int k = 0; k < 65; k++) bits32(sha_wt_a(k - arr));
+  for (int k = 0; k < 65; k++) X(sha_wt_a(k - 3), 0, 64);              // dd
+  for (int arr = 0; arr < 3; arr++)                                    // e, f, g [65][32]
+    for (int k = 0; k < 65; k++) bits32(sha_wt_e(k - arr));
+  for (int k = 0; k < 65; k++) X(sha_wt_e(k - 3), 0, 64);              // hh
+  for (int k = 0; k < 64; k++) X(SHA_WT_K + k, 0, 64);                 // ROUND_KEYS
+  for (int j = 0; j < 8; j++) X(hin(j), 0, 64);                        // hashWords
+  // subcomponents: round keys, sumDd, sumHh, sum[8], compress[64], modulo[8], sumA..sumG
+  for (int k = 0; k < 64; k++) X(SHA_WT_K + k, 0, 64);
+  getsum32(hin(3));
+  getsum32(hin(7));
+  for (int j = 0; j < 8; j++) getsum32(hin(j));
+  for (int k = 0; k < 64; k++) {
+    const int a = sha_wt_a(k), bb = sha_wt_a(k - 1), c = sha_wt_a(k - 2), d = sha_wt_a(k - 3);
+    const int e = sha_wt_e(k), f = sha_wt_e(k - 1), g = sha_wt_e(k - 2), h = sha_wt_e(k - 3);
+    const int cw = SHA_WT_CMP + SHA_CMP_WORDS * k;
+    // outputs: outA bits, a bits, b bits, c | outE bits, e bits, f bits, g
+    bits32(sha_wt_a(k + 1)); bits32(a); bits32(bb); X(c, 0, 64);
+    bits32(sha_wt_e(k + 1)); bits32(e); bits32(f); X(g, 0, 64);
+    // inputs: inp, key, a, b, c bits, d | e, f, g bits, h
+    X(SHA_WT_W + k, 0, 64); X(SHA_WT_K + k, 0, 64);
+    bits32(a); bits32(bb); bits32(c); X(d, 0, 64);
+    bits32(e); bits32(f); bits32(g); X(h, 0, 64);
+    bits32(cw + CW_CH);                                                // ch bits
+    X(cw + CW_OVE, 0, 64); X(cw + CW_OVA, 0, 64);
+    getsum32(c); getsum32(g); getsum32(cw + CW_S0); getsum32(cw + CW_S1); getsum32(cw + CW_MJ);
+    getsum32(cw + CW_CH);
+    for (int i = 0; i < 32; i++) {  // Bits2(a+b+c) | XOR3 Sigma0 | XOR3 Sigma1
+      X(cw + CW_XY, 2 * i, 1); X(cw + CW_XY, 2 * i + 1, 1); X(cw + CW_XY, 2 * i, 2);
+      X(cw + CW_S0, i, 1); X(cw + CW_R2, i, 1); X(cw + CW_R13, i, 1); X(cw + CW_R22, i, 1); X(cw + CW_T0, i, 1);
+      X(cw + CW_S1, i, 1); X(cw + CW_R6, i, 1); X(cw + CW_R11, i, 1); X(cw + CW_R25, i, 1); X(cw + CW_T1, i, 1);
+    }
+    lastnbits32(cw + CW_OVE);
+    lastnbits32(cw + CW_OVA);
+  }
+  for (int j = 0; j < 8; j++) lastnbits32(SHA_WT_FF64 + j);            // modulo[8]
+  for (int q = 0; q < 6; q++) getsum32(q < 3 ? sha_wt_a(64 - q) : sha_wt_e(64 - (q - 3)));  // sumA..sumG
+}
 
 namespace {
 
@@ -44,12 +136,18 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why);
 
 bool build_layout(const pzk_params& p, Layout& L, std::string& why) {
   L = Layout();
+  bool ok;
   switch (p.circuit) {
-    case PZK_CIRCUIT_POSEIDON: return build_poseidon(p, L, why);
-    case PZK_CIRCUIT_SHA256: return build_sha256(p, L, why);
-    case PZK_CIRCUIT_REGISTER: return build_register(p, L, why);
+    case PZK_CIRCUIT_POSEIDON: ok = build_poseidon(p, L, why); break;
+    case PZK_CIRCUIT_SHA256: ok = build_sha256(p, L, why); break;
+    case PZK_CIRCUIT_REGISTER: ok = build_register(p, L, why); break;
     default: why = "unknown circuit family"; return false;
   }
+  if (ok && !L.sha.empty()) {
+    sha_program(L.sha_prog);
+    if (L.sha_prog.size() != SHA_BLOCK_SIGNALS_COUNT) { why = "internal: SHA block program size"; return false; }
+  }
+  return ok;
 }
 
 }  // namespace pzk

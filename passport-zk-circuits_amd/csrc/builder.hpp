@@ -3,6 +3,8 @@
 // DAG and the value-store map. Pure host C++.
 #pragma once
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <array>
 #include <string>
@@ -26,6 +28,7 @@ struct Layout {
   std::vector<Region> regions;
   std::vector<Work> work[E_COUNT];  // per emit kernel
   std::vector<GenPiece> gen_pieces;  // pieces of the packed emitters' work items
+  std::vector<uint32_t> sha_prog;    // SHA block program: one descriptor per block signal (sha_prog.hpp)
   std::vector<std::array<uint32_t, 3>> pos_emit_groups;  // (t, first work, works) of work[E_POS]
   std::vector<ShaJob> sha;
   uint32_t sha_core_words = 0;
@@ -47,5 +50,12 @@ bool build_layout(const pzk_params& p, Layout& L, std::string& why);
 
 // chunk size of one emit workgroup (signals)
 constexpr uint32_t EMIT_CHUNK = 4096;
+// signals per work item of a chunked emitter (PZK_CHUNK_<e> overrides, for tuning runs)
+inline uint32_t emit_chunk(int e) {
+  char name[32];
+  snprintf(name, sizeof name, "PZK_CHUNK_%d", e);
+  const char* v = getenv(name);
+  return v ? (uint32_t)atoi(v) : EMIT_CHUNK;
+}
 
 }  // namespace pzk

@@ -100,7 +100,7 @@ struct Builder {
         }
         continue;
       }
-      uint32_t chunk = emitter_whole(e) ? r.len : EMIT_CHUNK;
+      uint32_t chunk = emitter_whole(e) ? r.len : emit_chunk(e);
       for (uint32_t s = 0; s < r.len; s += chunk) wl->push_back(Work{ri, s, std::min(chunk, r.len - s), 0});
     }
     // Poseidon emission: one launch per width t, each with the LDS its image needs

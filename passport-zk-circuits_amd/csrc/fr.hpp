@@ -153,6 +153,52 @@ __device__ __forceinline__ void fr_batch_inv(Acc x, Acc scratch, int n) {
   }
 }
 
+// ---- wave-contiguous element stores
+// Emitters produce one 32-byte element per lane. Stored directly that is 32 B per lane per
+// store pair; staged through LDS it becomes two 1 KiB fully contiguous wave stores of 16 B per
+// lane, which the MI355X write path sustains ~19 % faster (k_emit_sha measurement).
+struct El { uint4 lo, hi; };
+__device__ __forceinline__ El el_zero() { return El{make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)}; }
+__device__ __forceinline__ El el_u64(uint64_t v) {
+  return El{make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
+}
+__device__ __forceinline__ El el_fr(const fr& a) {
+  return El{make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]), make_uint4(a.v[4], a.v[5], a.v[6], a.v[7])};
+}
+__device__ __forceinline__ El el_load(const uint8_t* src) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  return El{s[0], s[1]};
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// All 64 lanes of the wave call this; lane l holds element l of the wave's run starting at
+// wave_out; only the first nvalid elements are stored. stage: 128 uint4 of LDS per wave.
+__device__ __forceinline__ void wave_store(uint8_t* wave_out, const El& e, uint32_t nvalid, uint4* stage) {
+  const uint32_t lane = threadIdx.x & 63;
+  stage[2 * lane] = e.lo;
+  stage[2 * lane + 1] = e.hi;
+  wave_sync();
+  const uint4 a = stage[lane], b = stage[64 + lane];
+  uint4* d = reinterpret_cast<uint4*>(wave_out);
+  if (lane < 2 * nvalid) d[lane] = a;
+  if (64 + lane < 2 * nvalid) d[64 + lane] = b;
+  wave_sync();
+}
+// for (q < count) out[q] = f(q), wave-contiguous; f(q) is evaluated only for q < count
+template <typename F>
+__device__ __forceinline__ void emit_run(uint8_t* out, uint32_t count, uint4* stage_block, F f) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint4* stage = stage_block + (threadIdx.x >> 6) * 128;
+  for (uint32_t q0 = threadIdx.x - lane; q0 < count; q0 += blockDim.x) {
+    const uint32_t q = q0 + lane;
+    const El e = q < count ? f(q) : el_zero();
+    wave_store(out + 32ull * q0, e, count - q0 < 64 ? count - q0 : 64, stage);
+  }
+}
+
 // 32-byte normal-form store of a small non-negative integer
 __device__ __forceinline__ void store_u64(uint8_t* dst, uint64_t v) {
   uint4* d = reinterpret_cast<uint4*>(dst);
@@ -170,6 +216,11 @@ __device__ __forceinline__ fr load_fr(const uint8_t* src) {
   fr r; r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w; r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
   return r;
 }
+
+// Core kernels are latency-bound chains with one wave per SIMD; they share CUs with the
+// bandwidth-bound emitters of other streams. Raising their wave priority makes the SIMD arbiter
+// issue their instructions first, so the chains are not starved by emitter waves.
+__device__ __forceinline__ void core_priority() { __builtin_amdgcn_s_setprio(3); }
 
 // lane status: keep the smallest nonzero check code, so the value reported for a lane that fails
 // several checks does not depend on which kernel or stream reached it first

@@ -1,11 +1,13 @@
 // Device kernels of the witness generator (unity build: every device header is included
 // here; the host runtime in runtime.cpp launches them through the launch_* wrappers).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "poseidon.hpp"
 #include "regcore.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
+#include "sha_prog.hpp"
 #include "kernels.hpp"
 
 namespace pzk {
@@ -27,6 +29,7 @@ __global__ void k_load_values(const ValueLoad* loads, int n_loads, const uint8_t
 // ------------------------------------------------------------------- SHA core
 __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs, uint64_t n_inputs,
                            uint32_t* sha_core, uint32_t core_words, int32_t* status, uint32_t batch) {
+  core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   int j = blockIdx.y;
   if (w >= batch || j >= n_jobs) return;
@@ -40,6 +43,7 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
 template <int T>
 __global__ void __launch_bounds__(64, 1) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems,
                            const fr* smt_core, uint32_t smt_core_fr) {
+  core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
   const PosTask& task = tasks[blockIdx.y];
@@ -74,6 +78,7 @@ __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t*
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
                                                           const uint32_t* sha_core, uint8_t* wtns, size_t stride) {
   __shared__ uint32_t core[SHA_BLOCK_CORE + 8 * 17];
+  __shared__ __attribute__((aligned(16))) uint64_t wt[SHA_WT_SIZE];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
@@ -81,11 +86,41 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
   const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
   uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
   if (R.kind == RK_SHA_BLOCK) {
+    // stage 1: the word-table entries this chunk's signals read (base words, feed-forward sums,
+    // and the derived words of the schedule / compress rounds the chunk overlaps)
     const uint32_t* bc = wc + R.a[1] * SHA_BLOCK_CORE;
     for (int i = threadIdx.x; i < SHA_BLOCK_CORE; i += blockDim.x) core[i] = bc[i];
     __syncthreads();
-    ShaBlk B{core};
-    for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) store_u64(out + 32ull * q, sha_block_sig(B, wk.start + q));
+    const ShaBlk Bk{core};
+    const uint32_t a = wk.start, b = wk.start + wk.count - 1;
+    auto rng = [](uint32_t lo_sig, uint32_t per, int nr, uint32_t x) {  // round index of signal x, clamped
+      return x < lo_sig ? 0 : (int)min((x - lo_sig) / per, (uint32_t)nr - 1);
+    };
+    const bool sch = a < SHA_SCH_ROUND0 + 48 * SHA_SCH_ROUND_SIGS && b >= SHA_SCH_ROUND0;
+    const bool cmp = a < SHA_RDS_CMP0 + 64 * SHA_CMP_SIGS && b >= SHA_RDS_CMP0;
+    const int r0 = sch ? rng(SHA_SCH_ROUND0, SHA_SCH_ROUND_SIGS, 48, a) : 0;
+    const int r1 = sch ? rng(SHA_SCH_ROUND0, SHA_SCH_ROUND_SIGS, 48, b) + 1 : 0;
+    const int k0 = cmp ? rng(SHA_RDS_CMP0, SHA_CMP_SIGS, 64, a) : 0;
+    const int k1 = cmp ? rng(SHA_RDS_CMP0, SHA_CMP_SIGS, 64, b) + 1 : 0;
+    const int n_base = SHA_WT_SCH, n_ff = 16, n_sch = (r1 - r0) * SHA_SCH_WORDS, n_cmp = (k1 - k0) * SHA_CMP_WORDS;
+    for (int v = threadIdx.x; v < n_base + n_ff + n_sch + n_cmp; v += blockDim.x) {
+      int e = v < n_base ? v
+            : v < n_base + n_ff ? SHA_WT_FF32 + (v - n_base)
+            : v < n_base + n_ff + n_sch ? SHA_WT_SCH + r0 * SHA_SCH_WORDS + (v - n_base - n_ff)
+                                        : SHA_WT_CMP + k0 * SHA_CMP_WORDS + (v - n_base - n_ff - n_sch);
+      wt[e] = sha_wt_entry(Bk, e);
+    }
+    __syncthreads();
+    // stage 2: one descriptor, one LDS word, one bit-field extract per element
+    // Two lanes per element (16 B each), so every wave store is 1 KiB contiguous: the element
+    // is cheap enough to evaluate twice, and this store shape writes ~19 % faster than 32 B per
+    // lane (emit_run stages through LDS for the emitters whose elements are expensive).
+    const uint32_t* prog = L.sha_prog + wk.start;
+    for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) {
+      const uint32_t d = prog[h >> 1];
+      const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d, wt[d & 2047]);
+      reinterpret_cast<uint4*>(out)[h] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+    }
   } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)
     const int Bn = R.a[1];
     for (int i = threadIdx.x; i < 8 * (Bn + 1); i += blockDim.x) {
@@ -94,12 +129,12 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     }
     __syncthreads();
     const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
-    for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+    uint4* stage = reinterpret_cast<uint4*>(wt);  // the word table is not used on this path
+    emit_run(out, wk.count, stage, [&](uint32_t q) {
       bool cp; uint64_t src = 0;
       uint64_t v = sha_own_sig(R, core, wk.start + q, cp, src);
-      if (cp) copy_el(out + 32ull * q, in_row + 32ull * src);
-      else store_u64(out + 32ull * q, v);
-    }
+      return cp ? el_load(in_row + 32ull * src) : el_u64(v);
+    });
   }
 }
 
@@ -118,8 +153,8 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   if (threadIdx.x == 0) *P.hash = vs.at(task.out_slot, w);
   pos_lds_fill(P, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off);
   uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x)
-    store_fr(out + 32ull * q, pos_block_sig(P, n, wk.start + q));
+  __shared__ uint4 stage[2 * EMIT_THREADS];
+  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_fr(pos_block_sig(P, n, wk.start + q)); });
 }
 
 // ------------------------------------------------------------------- emit: generic small regions
@@ -199,6 +234,14 @@ hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t
   return hipGetLastError();
 }
 
+hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core,
+                            const uint64_t* rsa_core, int32_t* status, uint32_t batch, hipStream_t st) {
+  if (!status) return hipSuccess;
+  hipLaunchKernelGGL(k_rsa_check, dim3((batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, rsa_core, status,
+                     batch);
+  return hipGetLastError();
+}
+
 hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
                            uint32_t batch, hipStream_t st) {
   if (L.reg.K == 32) {
@@ -217,8 +260,15 @@ hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, fr* bjj_core, fr* scratch, hipStream_t st) {
-  hipLaunchKernelGGL(k_bjj_core, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, vs, bjj_core, scratch, vs.batch);
+hipError_t launch_bjj_table(fr* table, hipStream_t st) {
+  hipLaunchKernelGGL(k_bjj_table, dim3(BJJ_TABLE_WINDOWS * 256 / 256), dim3(256), 0, st, table);
+  return hipGetLastError();
+}
+
+hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
+                           hipStream_t st) {
+  const uint32_t lanes = vs.batch * BJJ_SEGS;
+  hipLaunchKernelGGL(k_bjj_core, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
   return hipGetLastError();
 }
 

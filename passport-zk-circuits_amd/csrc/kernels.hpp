@@ -26,9 +26,13 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
                            uint32_t smt_core_fr, hipStream_t st);
 hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
                        int32_t* status, hipStream_t st);
+hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core,
+                            const uint64_t* rsa_core, int32_t* status, uint32_t batch, hipStream_t st);
 hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
                            uint32_t batch, hipStream_t st);
-hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, fr* bjj_core, fr* scratch, hipStream_t st);
+hipError_t launch_bjj_table(fr* table, hipStream_t st);
+hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
+                           hipStream_t st);
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st);
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,

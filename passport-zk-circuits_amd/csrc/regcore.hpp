@@ -57,6 +57,7 @@ __device__ __forceinline__ fr fr_from_i128(uint64_t lo, uint64_t hi) {
 // ============================================================================ k_prep
 // lane = witness. Runs after k_sha_core (needs the SA digest).
 __global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
+  core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
   const RegInfo& R = L.reg;
@@ -313,11 +314,52 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
 template <int K, int NL>
 __global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
                                                  uint32_t batch) {
+  core_priority();
   extern __shared__ uint64_t lds_rsa[];
   uint32_t w = blockIdx.x * NL + threadIdx.x;
   if (w >= batch) return;
   rsa_lane<K, NL>(L, inputs + 32ull * (uint64_t)w * L.n_inputs, rsa_core + (size_t)w * L.rsa_core_words,
                   status ? status + w : nullptr, lds_rsa, threadIdx.x);
+}
+
+// ============================================================================ RSA EM checks
+// RsaVerifyPkcs1v15 (rsa.circom:47-71) on EM = PowerMod.out (last BigMultModP remainder), and
+// BigMultModP's BigGreaterThan(modulus, mod) (bigInt.circom:241-245) for every multiplication.
+// One lane per witness; reads the RSA core, the SA digest (SHA core) and the pubkey input.
+constexpr uint64_t RSA_EM4 = 217300885422736416ull, RSA_EM5 = 938447882527703397ull;  // rsa.circom:53-54
+constexpr uint64_t RSA_EM6 = 0xFFFFFFFF00303130ull;  // num2bits_6: remainsBits (rsa.circom:59-62), ones (:65-67)
+
+__global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
+                                                  const uint64_t* rsa_core, int32_t* status, uint32_t batch) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch || !status) return;
+  const int K = L.reg.K;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  const uint64_t* core = rsa_core + (size_t)w * L.rsa_core_words;
+  const uint64_t* em = core + (size_t)(L.reg.n_modmul - 1) * MM_CORE_WORDS(K) + 3 * K + 1;
+  const ShaJob& J = L.sha[L.reg.j_sa];
+  const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + J.core_off + J.blocks * SHA_BLOCK_CORE;
+  bool hash_bad = false;
+  for (int i = 0; i < 4; i++) {  // hashed_chunks[i] = digest bits [64(3-i), 64(4-i)) as a number
+    const int wd = 3 - i;
+    hash_bad |= (((uint64_t)H[2 * wd] << 32) | H[2 * wd + 1]) != em[i];
+  }
+  bool pad_bad = em[6] != RSA_EM6;
+  for (int i = 7; i < K - 1; i++) pad_bad |= em[i] != ~0ull;
+  bool gt_bad = false;
+  for (int m = 0; m < L.reg.n_modmul; m++) {  // mod < modulus, limb-wise from the top
+    const uint64_t* r = core + (size_t)m * MM_CORE_WORDS(K) + 3 * K + 1;
+    int cmp = 0;
+    for (int i = K - 1; i >= 0 && cmp == 0; i--) {
+      uint64_t n = in_u64(row + 32ull * (L.reg.in_pk + i));
+      cmp = n > r[i] ? 1 : n < r[i] ? -1 : 0;
+    }
+    gt_bad |= cmp != 1;
+  }
+  if (hash_bad) lane_status(status + w, ST_RSA_HASH);
+  if (em[4] != RSA_EM4 || em[5] != RSA_EM5) lane_status(status + w, ST_RSA_PREFIX);
+  if (pad_bad) lane_status(status + w, ST_RSA_PAD);
+  if (gt_bad) lane_status(status + w, ST_BIGMOD_GT);
 }
 
 // ============================================================================ BabyJubJub core
@@ -359,25 +401,85 @@ struct BjjConsts {
   }
 };
 
-// scratch: SoA [elem][witness] with 3 * 2 * 254 (X, Y, Z of D_i and A_i) + 3 * 254 prefix products
-__global__ void __launch_bounds__(64, 1) k_bjj_core(DevLayout L, ValueStore vs, fr* bjj_core, fr* scratch, uint32_t batch) {
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= batch) return;
+// Fixed-base table for the segment start points: T[w][v] = v * 2^(8w) * Base8, w < 32, v < 256,
+// affine (x, y) and t2d = d*x*y, Montgomery form. Built once per instance (k_bjj_table).
+__device__ __forceinline__ ExtPt bjj_add(const ExtPt& P, const ExtPt& Q, const BjjConsts& C) {  // add-2008-hwcd
+  fr a = fr_mul(P.X, Q.X), b = fr_mul(P.Y, Q.Y), c = fr_mul(fr_mul(P.T, C.D), Q.T), d = fr_mul(P.Z, Q.Z);
+  fr e = fr_sub(fr_sub(fr_mul(fr_add(P.X, P.Y), fr_add(Q.X, Q.Y)), a), b);
+  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, fr_mul(C.A, a));
+  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+}
+
+__global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (w, v)
+  if (idx >= BJJ_TABLE_WINDOWS * 256) return;
+  const int wi = idx >> 8, v = idx & 255;
+  BjjConsts C;
+  C.init();
+  fr* out = table + 3 * (size_t)idx;
+  if (v == 0) { out[0] = fr_zero(); out[1] = fr_zero(); out[2] = fr_zero(); return; }
+  ExtPt base{C.B8x, C.B8y, fr_mont_one(), fr_mul(C.B8x, C.B8y)};
+  for (int k = 0; k < 8 * wi; k++) base = bjj_dbl(base, C.A);
+  ExtPt acc = base;  // v * base, MSB-first double-and-add from the top set bit
+  for (int bit = 30 - __clz(v); bit >= 0; bit--) {
+    acc = bjj_dbl(acc, C.A);
+    if ((v >> bit) & 1) acc = bjj_add(acc, base, C);
+  }
+  fr zi = fr_inv(acc.Z);
+  fr x = fr_mul(acc.X, zi), y = fr_mul(acc.Y, zi);
+  out[0] = x; out[1] = y; out[2] = fr_mul(fr_mul(C.D, x), y);
+}
+
+__device__ __forceinline__ fr fr_shfl(const fr& a, int src, int width) {
+  fr r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src, width);
+  return r;
+}
+
+// BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171): MSB-first double-and-add over
+// the 254 bits of sk with the (0,0) sentinel for "no point yet". The ladder is cut into BJJ_SEGS
+// segments of BJJ_SEG_LEN steps, one lane each (8 adjacent lanes = one witness): a segment
+// starts from A_{i0-1} = (sk >> (254 - i0)) * Base8, summed from the fixed-base table, so the
+// segments run in parallel. The affine outputs need 1/Z of every point (and 1/x of every D):
+// one batched inversion per witness, whose single Fr inversion is shared by the 8 lanes
+// through wave shuffles.
+// scratch: SoA [elem][lane], 9 * BJJ_SEG_LEN elements per lane (X,Y,Z of D and A, 3 prefixes)
+__global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, const fr* table, fr* bjj_core,
+                                                fr* scratch, uint32_t batch) {
+  core_priority();
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nlanes = batch * BJJ_SEGS;
+  const uint32_t w = tid / BJJ_SEGS;
+  const int seg = (int)(tid % BJJ_SEGS);
+  if (w >= batch) return;  // whole 8-lane groups only (64 % BJJ_SEGS == 0)
   BjjConsts C;
   C.init();
   const int NS = BJJ_STEPS;
-  auto S = [&](int e) -> fr& { return scratch[(size_t)e * batch + w]; };
-  // projective coords of D_i (elems 0..3NS) and A_i (3NS..6NS): [X, Y, Z] per step
-  fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
-  bool have = false;  // A_{i-1} is a real point (not the (0,0) sentinel)
+  const int i0 = seg * BJJ_SEG_LEN, i1 = i0 + BJJ_SEG_LEN < NS ? i0 + BJJ_SEG_LEN : NS, ns = i1 - i0;
+  auto S = [&](int e) -> fr& { return scratch[(size_t)e * nlanes + tid]; };
+  const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
+  auto sk_bit = [&](int k) -> uint32_t { return (sk.v[k >> 5] >> (k & 31)) & 1u; };  // bit k of sk
+  // segment start: A_{i0-1} = p * Base8, p = sk >> (254 - i0) (an i0-bit prefix)
+  bool have = false;
   ExtPt A;
-  for (int i = 0; i < NS; i++) {
-    int bit = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
+  for (int wi = 0; 8 * wi < i0; wi++) {
+    uint32_t v = 0;
+    for (int b = 0; b < 8 && 8 * wi + b < i0; b++) v |= sk_bit(254 - i0 + 8 * wi + b) << b;
+    if (!v) continue;
+    const fr* e = table + 3 * (size_t)(wi * 256 + v);
+    if (!have) { A = ExtPt{e[0], e[1], fr_mont_one(), fr_mul(e[0], e[1])}; have = true; }
+    else A = bjj_add_affine(A, e[0], e[1], e[2], C.A);
+  }
+  // projective coords of D_i (local elems 0..3ns) and A_i (3ns..6ns): [X, Y, Z] per step
+  for (int j = 0; j < ns; j++) {
+    const int i = i0 + j;
+    const uint32_t bit = sk_bit(253 - i);
     ExtPt D;
     bool haveD = false;
     if (i > 0 && have) { D = bjj_dbl(A, C.A); haveD = true; }
-    if (haveD) { S(3 * i) = D.X; S(3 * i + 1) = D.Y; S(3 * i + 2) = D.Z; }
-    else { S(3 * i) = fr_zero(); S(3 * i + 1) = fr_zero(); S(3 * i + 2) = fr_zero(); }
+    if (haveD) { S(3 * j) = D.X; S(3 * j + 1) = D.Y; S(3 * j + 2) = D.Z; }
+    else { S(3 * j) = fr_zero(); S(3 * j + 1) = fr_zero(); S(3 * j + 2) = fr_zero(); }
     if (bit) {
       if (haveD) A = bjj_add_affine(D, C.B8x, C.B8y, C.B8t_d, C.A);
       else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = fr_mul(C.B8x, C.B8y); }
@@ -386,36 +488,44 @@ __global__ void __launch_bounds__(64, 1) k_bjj_core(DevLayout L, ValueStore vs, 
       if (haveD) A = D;
       have = haveD;
     }
-    if (have) { S(3 * NS + 3 * i) = A.X; S(3 * NS + 3 * i + 1) = A.Y; S(3 * NS + 3 * i + 2) = A.Z; }
-    else { S(3 * NS + 3 * i) = fr_zero(); S(3 * NS + 3 * i + 1) = fr_zero(); S(3 * NS + 3 * i + 2) = fr_zero(); }
+    const int o = 3 * BJJ_SEG_LEN + 3 * j;
+    if (have) { S(o) = A.X; S(o + 1) = A.Y; S(o + 2) = A.Z; }
+    else { S(o) = fr_zero(); S(o + 1) = fr_zero(); S(o + 2) = fr_zero(); }
   }
-  // batch inversion of Z(D_i), Z(A_i), X(D_i): index list q -> element
+  // batched inversion of Z(D_i), Z(A_i), X(D_i) over the segment, then across the 8 lanes
   auto elem = [&](int qi) -> fr {
-    int st = qi / 3, kind = qi - 3 * st;
-    return kind == 0 ? S(3 * st + 2) : kind == 1 ? S(3 * NS + 3 * st + 2) : S(3 * st);
+    int j = qi / 3, kind = qi - 3 * j;
+    return kind == 0 ? S(3 * j + 2) : kind == 1 ? S(3 * BJJ_SEG_LEN + 3 * j + 2) : S(3 * j);
   };
-  const int NQ = 3 * NS;
-  const int PRE = 6 * NS;
+  const int NQ = 3 * ns, PRE = 6 * BJJ_SEG_LEN;
   fr acc = fr_mont_one();
   for (int qi = 0; qi < NQ; qi++) {
     fr e = elem(qi);
     S(PRE + qi) = acc;
     if (!fr_is_zero(e)) acc = fr_mul(acc, e);
   }
-  fr inv = fr_inv(acc);
+  fr others = fr_mont_one(), total = fr_mont_one();
+  for (int t = 0; t < BJJ_SEGS; t++) {
+    fr pt = fr_shfl(acc, t, BJJ_SEGS);
+    total = fr_mul(total, pt);
+    if (t != seg) others = fr_mul(others, pt);
+  }
+  fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
   fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
   for (int qi = NQ - 1; qi >= 0; qi--) {
     fr e = elem(qi);
     fr r = fr_zero();
     if (!fr_is_zero(e)) { r = fr_mul(inv, S(PRE + qi)); inv = fr_mul(inv, e); }
-    int st = qi / 3, kind = qi - 3 * st;
-    fr* o = out + 5 * st;  // Dx, Dy, Ax, Ay, inv(Dx)
-    if (kind == 0) { o[0] = fr_mul(S(3 * st), r); o[1] = fr_mul(S(3 * st + 1), r); }
-    else if (kind == 1) { o[2] = fr_mul(S(3 * NS + 3 * st), r); o[3] = fr_mul(S(3 * NS + 3 * st + 1), r); }
-    else { o[4] = fr_mul(S(3 * st + 2), r); }  // 1/x = Z / X
+    const int j = qi / 3, kind = qi - 3 * j;
+    fr* o = out + 5 * (i0 + j);  // Dx, Dy, Ax, Ay, inv(Dx)
+    if (kind == 0) { o[0] = fr_mul(S(3 * j), r); o[1] = fr_mul(S(3 * j + 1), r); }
+    else if (kind == 1) { o[2] = fr_mul(S(3 * BJJ_SEG_LEN + 3 * j), r); o[3] = fr_mul(S(3 * BJJ_SEG_LEN + 3 * j + 1), r); }
+    else { o[4] = fr_mul(S(3 * j + 2), r); }  // 1/x = Z / X
   }
-  vs.at(L.reg.v_bjj, w) = out[5 * (NS - 1) + 2];
-  vs.at(L.reg.v_bjj + 1, w) = out[5 * (NS - 1) + 3];
+  if (i1 == NS) {
+    vs.at(L.reg.v_bjj, w) = out[5 * (NS - 1) + 2];
+    vs.at(L.reg.v_bjj + 1, w) = out[5 * (NS - 1) + 3];
+  }
 }
 
 // ============================================================================ SMT
@@ -423,6 +533,7 @@ __global__ void __launch_bounds__(64, 1) k_bjj_core(DevLayout L, ValueStore vs, 
 // SMT core (Fr): [inv(sibling) normal][80] [root Montgomery][80] [flags][80] [j, inv(root_in - root_0)]
 __global__ void __launch_bounds__(64, 1) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            uint32_t batch) {
+  core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
   const RegInfo& R = L.reg;
@@ -483,6 +594,7 @@ __global__ void __launch_bounds__(64, 1) k_smt_prep(DevLayout L, const uint8_t* 
 // sequential part: levels j-1 .. 0, then all roots and the isEqual inverse
 __global__ void __launch_bounds__(64, 1) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs, ValueStore vs,
                             fr* pos_core, fr* smt_core, uint32_t batch) {
+  core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
   const RegInfo& R = L.reg;

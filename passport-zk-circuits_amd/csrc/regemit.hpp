@@ -33,6 +33,9 @@ __device__ __forceinline__ void store_w(uint8_t* dst, const W256& a) {
   d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
   d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
 }
+__device__ __forceinline__ El el_w(const W256& a) {
+  return El{make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]), make_uint4(a.v[4], a.v[5], a.v[6], a.v[7])};
+}
 __device__ __forceinline__ W256 w_from_fr(const fr& a) { W256 r; for (int i = 0; i < 8; i++) r.v[i] = a.v[i]; return r; }
 __device__ __forceinline__ fr fr_from_w(const W256& a) { fr r; for (int i = 0; i < 8; i++) r.v[i] = a.v[i]; return r; }
 __device__ __forceinline__ void copy_el(uint8_t* dst, const uint8_t* src) {
@@ -270,23 +273,22 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
     __syncthreads();
   }
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+  __shared__ uint4 stage[2 * 256];
+  emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     uint32_t s = wk.start + q;
-    uint8_t* dst = out + 32ull * q;
-    if (s > 2u * Lb) { store_w(dst, alias_sig(V, sout, s - 2 * Lb - 1)); continue; }
+    if (s > 2u * Lb) return el_w(alias_sig(V, sout, s - 2 * Lb - 1));
     if (b2n) {
-      if (s == 0) store_w(dst, V);
-      else if (s <= (uint32_t)Lb) {
+      if (s == 0) return el_w(V);
+      if (s <= (uint32_t)Lb) {
         int idx = R.a[2] + R.a[3] * (int)(s - 1);
-        if (R.a[1] == 1) store_u64(dst, digest_bit(H, idx));
-        else copy_el(dst, row + 32ull * idx);
-      } else store_w(dst, w_mask(V, (int)(s - Lb)));
-    } else {
-      if (s < (uint32_t)Lb) store_u64(dst, w_bit(V, s));
-      else if (s == (uint32_t)Lb) store_fr(dst, inval);
-      else store_w(dst, w_mask(V, (int)(s - Lb)));
+        return R.a[1] == 1 ? el_u64(digest_bit(H, idx)) : el_load(row + 32ull * idx);
+      }
+      return el_w(w_mask(V, (int)(s - Lb)));
     }
-  }
+    if (s < (uint32_t)Lb) return el_u64(w_bit(V, s));
+    if (s == (uint32_t)Lb) return el_fr(inval);
+    return el_w(w_mask(V, (int)(s - Lb)));
+  });
 }
 
 // ------------------------------------------------------------------ PassportVerificationFlow
@@ -322,30 +324,25 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   const uint32_t o_d1 = 1, o_d15 = 257, o_ec = 513, o_eh = o_ec + ecLen, o_sa = o_eh + 256, o_v = o_sa + 1024,
                  o_eq = o_v + 776;
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+  __shared__ uint4 stage[2 * 256];
+  emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     uint32_t s = wk.start + q;
-    uint8_t* dst = out + 32ull * q;
-    if (s == 0) store_u64(dst, chain[775]);
-    else if (s < o_d15) store_u64(dst, digest_bit(H1, s - o_d1));
-    else if (s < o_ec) store_u64(dst, H15 ? digest_bit(H15, s - o_d15) : 0);
-    else if (s < o_eh) copy_el(dst, row + 32ull * (in_ec + s - o_ec));
-    else if (s < o_sa) store_u64(dst, digest_bit(HE, s - o_eh));
-    else if (s < o_v) copy_el(dst, row + 32ull * (in_sa + s - o_sa));
-    else if (s < o_eq) store_u64(dst, chain[s - o_v]);
-    else {
-      uint32_t k = (s - o_eq) / 6, t = (s - o_eq) % 6;
-      uint32_t a, b; pair(k, a, b);
-      // IsEqual: out | in[0], in[1] | IsZero: out, in = in[1]-in[0], inv
-      if (t == 0 || t == 3) store_u64(dst, a == b);
-      else if (t == 1) store_u64(dst, a);
-      else if (t == 2) store_u64(dst, b);
-      else {
-        int d = (int)b - (int)a;  // in {-1, 0, 1}; inverse of +-1 is itself
-        if (d >= 0) store_u64(dst, (uint64_t)d);
-        else store_fr(dst, fr_sub(fr_zero(), fr_u64(1)));
-      }
-    }
-  }
+    if (s == 0) return el_u64(chain[775]);
+    if (s < o_d15) return el_u64(digest_bit(H1, s - o_d1));
+    if (s < o_ec) return el_u64(H15 ? digest_bit(H15, s - o_d15) : 0);
+    if (s < o_eh) return el_load(row + 32ull * (in_ec + s - o_ec));
+    if (s < o_sa) return el_u64(digest_bit(HE, s - o_eh));
+    if (s < o_v) return el_load(row + 32ull * (in_sa + s - o_sa));
+    if (s < o_eq) return el_u64(chain[s - o_v]);
+    uint32_t k = (s - o_eq) / 6, t = (s - o_eq) % 6;
+    uint32_t a, b; pair(k, a, b);
+    // IsEqual: out | in[0], in[1] | IsZero: out, in = in[1]-in[0], inv
+    if (t == 0 || t == 3) return el_u64(a == b);
+    if (t == 1) return el_u64(a);
+    if (t == 2) return el_u64(b);
+    int d = (int)b - (int)a;  // in {-1, 0, 1}; inverse of +-1 is itself
+    return d >= 0 ? el_u64((uint64_t)d) : el_fr(fr_sub(fr_zero(), fr_u64(1)));
+  });
 }
 
 // ------------------------------------------------------------------ BigMultModP
@@ -565,7 +562,8 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   __syncthreads();
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) store_w(out + 32ull * q, mm_sig(C, wk.start + q));
+  __shared__ uint4 stage[2 * 256];
+  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, wk.start + q)); });
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps
@@ -632,7 +630,8 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
   __syncthreads();
   const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
+  __shared__ uint4 stage[2 * 256];
+  emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     const uint32_t s = wk.start + q, i = bjj_step_of(s), t = s - bjj_sig_of(i);
     const int j = (int)i - base;
     const fr* rc = rec + j * BR_N;
@@ -689,8 +688,8 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
         }
       }
     }
-    store_fr(out + 32ull * q, res);
-  }
+    return el_fr(res);
+  });
 }
 
 }  // namespace pzk

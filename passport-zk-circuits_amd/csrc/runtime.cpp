@@ -96,21 +96,23 @@ struct pzk_instance {
   Layout lay;
   int device = 0;
   hipStream_t stream = nullptr;
-  // side streams of the register pipeline (RSA core + emission; BJJ core + SHA/BJJ emission).
+  // side streams of the register pipeline (RSA core + emission; SHA + BJJ emission).
   // Three streams in all: with the null stream they fit the 4 hardware queues HIP maps
   // streams onto by default, so no two of them share a queue.
-  hipStream_t s_rsa = nullptr, s_bjj = nullptr;
+  hipStream_t s_rsa = nullptr, s_sha = nullptr;
   hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_j_rsa = nullptr,
              ev_j_bjj = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
   Work* d_work[E_COUNT] = {};
   GenPiece* d_gen_pieces = nullptr;
+  uint32_t* d_sha_prog = nullptr;
   ShaJob* d_sha = nullptr;
   PosTask* d_pos = nullptr;
   ValueLoad* d_loads = nullptr;
   int32_t* d_level_task = nullptr;
   fr* d_pos_consts = nullptr;
+  fr* d_bjj_table = nullptr;  // fixed-base Base8 table (register circuit)
   PosParamIndex pix{};
   // per-batch scratch, grown on demand
   size_t cap = 0;
@@ -136,6 +138,7 @@ struct pzk_instance {
     L.n_pos_levels = (uint32_t)lay.pos_level_start.size() - 1;
     L.regions = d_regions;
     L.gen_pieces = d_gen_pieces;
+    L.sha_prog = d_sha_prog;
     L.sha = d_sha;
     L.pos = d_pos;
     L.reg = lay.reg;
@@ -225,13 +228,13 @@ static void free_scratch(pzk_instance* I) {
 
 static void free_all(pzk_instance* I) {
   free_scratch(I);
-  void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
-                  I->d_pos_consts, I->d_in, I->d_out, I->d_status};
+  void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
+                  I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_bjj})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha})
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_j_rsa, I->ev_j_bjj})
     if (e) (void)hipEventDestroy(e);
@@ -261,14 +264,20 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   rc = upload(&I->d_regions, I->lay.regions);
   for (int e = 0; e < E_COUNT && !rc; e++) rc = upload(&I->d_work[e], I->lay.work[e]);
   if (!rc) rc = upload(&I->d_gen_pieces, I->lay.gen_pieces);
+  if (!rc) rc = upload(&I->d_sha_prog, I->lay.sha_prog);
   if (!rc) rc = upload(&I->d_sha, I->lay.sha);
   if (!rc) rc = upload(&I->d_pos, I->lay.pos);
   if (!rc) rc = upload(&I->d_loads, I->lay.loads);
   if (!rc && I->lay.is_register) rc = upload(&I->d_level_task, level_task);
+  if (!rc && I->lay.is_register) {
+    if (hipMalloc(&I->d_bjj_table, sizeof(fr) * 3 * BJJ_TABLE_WINDOWS * 256) != hipSuccess ||
+        launch_bjj_table(I->d_bjj_table, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
+  }
   if (rc) { free_all(I); delete I; return rc; }
   bool ok = hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&I->s_rsa, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&I->s_bjj, hipStreamNonBlocking) == hipSuccess;
+            hipStreamCreateWithFlags(&I->s_sha, hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_j_rsa, &I->ev_j_bjj})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
@@ -353,7 +362,7 @@ static int ensure_scratch(pzk_instance* I, size_t batch) {
       {(void**)&I->d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
       {(void**)&I->d_rsa_core, 8ull * L.rsa_core_words * batch},
       {(void**)&I->d_bjj_core, 32ull * L.bjj_core_fr * batch},
-      {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * 9 * BJJ_STEPS * batch : 0},
+      {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&I->d_smt_core, 32ull * L.smt_core_fr * batch},
   };
   for (auto& r : req)
@@ -418,39 +427,43 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     for (int e = 0; e < E_COUNT; e++)
       if ((rc = emit(e, st))) return rc;
   } else {
-    // Three streams (DESIGN.md "Schedule"). The RSA and BabyJubJub cores depend only on the
-    // inputs, so they start at once on their own streams and their emitters follow them there
-    // (the SHA emitter behind the BJJ core). The main stream runs the Poseidon/SMT dependency
-    // chain and the remaining emitters, then joins the side streams.
+    // Three streams (DESIGN.md §4 "Schedule"). The RSA core depends only on the inputs, so it
+    // starts at once on its own stream, its emitter behind it; the SHA emitter (the bulk of the
+    // bytes) starts as soon as the SHA core is done; the main stream runs the Poseidon/SMT
+    // dependency chain, the BabyJubJub core and the remaining emitters, then joins.
+    // PZK_SERIAL=1 (profiling): every phase on the launch stream, so kernel times are standalone
+    static const bool serial = getenv("PZK_SERIAL") != nullptr;
+    hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha;
     HIPCHK(hipEventRecord(I->ev_load, st));
-    HIPCHK(hipStreamWaitEvent(I->s_rsa, I->ev_load, 0));
-    HIPCHK(hipStreamWaitEvent(I->s_bjj, I->ev_load, 0));
-    { PhaseScope ps(T, slot, PH_RSA_CORE, I->s_rsa);
-      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, I->s_rsa)); }
-    HIPCHK(hipEventRecord(I->ev_rsa, I->s_rsa));
-    if ((rc = emit(E_MM, I->s_rsa))) return rc;
-    HIPCHK(hipEventRecord(I->ev_j_rsa, I->s_rsa));
-    { PhaseScope ps(T, slot, PH_BJJ_CORE, I->s_bjj);
-      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_core, I->d_bjj_scratch, I->s_bjj)); }
-    HIPCHK(hipEventRecord(I->ev_bjj, I->s_bjj));
+    HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_load, 0));
+    { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
+      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, s_rsa)); }
+    HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+    if ((rc = emit(E_MM, s_rsa))) return rc;
+    HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
     { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
     HIPCHK(hipEventRecord(I->ev_sha, st));
-    HIPCHK(hipStreamWaitEvent(I->s_bjj, I->ev_sha, 0));
-    if ((rc = emit(E_SHA, I->s_bjj))) return rc;
-    if ((rc = emit(E_BJJ, I->s_bjj))) return rc;
-    HIPCHK(hipEventRecord(I->ev_j_bjj, I->s_bjj));
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
+    if ((rc = emit(E_SHA, s_sha))) return rc;
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, I->d_pos_core, I->d_smt_core, st)); }
-    HIPCHK(hipStreamWaitEvent(st, I->ev_bjj, 0));
+    { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
+      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, I->d_bjj_core, I->d_bjj_scratch, st)); }
+    HIPCHK(hipEventRecord(I->ev_bjj, st));
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
+    if ((rc = emit(E_BJJ, s_sha))) return rc;
+    HIPCHK(hipEventRecord(I->ev_j_bjj, s_sha));
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
     if ((rc = emit(E_GEN, st))) return rc;
     if ((rc = emit(E_FLOW, st))) return rc;
     if ((rc = emit(E_POS, st))) return rc;
     HIPCHK(hipStreamWaitEvent(st, I->ev_rsa, 0));
+    { PhaseScope ps(T, slot, PH_PREP, st);
+      HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st)); }
     if ((rc = emit(E_BITS, st))) return rc;
     if ((rc = emit(E_GENR, st))) return rc;
     for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));

@@ -10,6 +10,7 @@
 #pragma once
 #include "fr.hpp"
 #include "layout.hpp"
+#include "sha_prog.hpp"
 
 namespace pzk {
 
@@ -254,6 +255,68 @@ __device__ __forceinline__ uint64_t sha_rounds_sig(const ShaBlk& B, uint32_t s) 
   uint32_t q = s >> 6;  // sumA sumB sumC sumE sumF sumG
   uint32_t X = q < 3 ? B.A(64 - (int)q) : B.E(64 - (int)(q - 3));
   return sig_getsum32(X, s & 63);
+}
+
+// word-table entry e of a block (sha_prog.hpp layout)
+__device__ __forceinline__ uint64_t sha_spread(uint32_t x) {  // bit i -> bit 2i
+  uint64_t v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+__device__ __forceinline__ uint64_t sha_wt_entry(const ShaBlk& B, int e) {
+  if (e < 64) return B.W(e);
+  if (e < sha_wt_e(-3)) return B.A(e - 67);
+  if (e <= sha_wt_e(64)) return B.E(e - 135);
+  if (e < SHA_WT_K) return 0;  // unused slots
+  if (e < SHA_WT_SCH) return SHA_K[e - SHA_WT_K];
+  if (e < SHA_WT_CMP) {
+    const int r = (e - SHA_WT_SCH) / SHA_SCH_WORDS, q = (e - SHA_WT_SCH) - r * SHA_SCH_WORDS, m = r + 16;
+    const uint32_t wk = B.W(m - 15), wl = B.W(m - 2);
+    switch (q) {
+      case SW_X7: return rotr32(wk, 7);
+      case SW_Y18: return rotr32(wk, 18);
+      case SW_Z3: return wk >> 3;
+      case SW_T0: return rotr32(wk, 18) & (wk >> 3);
+      case SW_S0: return ssig0(wk);
+      case SW_X17: return rotr32(wl, 17);
+      case SW_Y19: return rotr32(wl, 19);
+      case SW_Z10: return wl >> 10;
+      case SW_T1: return rotr32(wl, 19) & (wl >> 10);
+      case SW_S1: return ssig1(wl);
+      default: return (uint64_t)ssig1(wl) + B.W(m - 7) + ssig0(wk) + B.W(m - 16);
+    }
+  }
+  if (e < SHA_WT_FF32) {
+    const int k = (e - SHA_WT_CMP) / SHA_CMP_WORDS, q = (e - SHA_WT_CMP) - k * SHA_CMP_WORDS;
+    const uint32_t a = B.A(k), b = B.A(k - 1), c = B.A(k - 2), d = B.A(k - 3);
+    const uint32_t ee = B.E(k), f = B.E(k - 1), g = B.E(k - 2), h = B.E(k - 3);
+    const uint32_t ch = (ee & f) ^ (~ee & g), mj = (a & b) ^ (a & c) ^ (b & c);
+    switch (q) {
+      case CW_CH: return ch;
+      case CW_S1: return bsig1(ee);
+      case CW_S0: return bsig0(a);
+      case CW_MJ: return mj;
+      case CW_OVE: return (uint64_t)d + h + bsig1(ee) + ch + SHA_K[k] + B.W(k);
+      case CW_OVA: return (uint64_t)h + bsig1(ee) + ch + SHA_K[k] + B.W(k) + bsig0(a) + mj;
+      case CW_R2: return rotr32(a, 2);
+      case CW_R13: return rotr32(a, 13);
+      case CW_R22: return rotr32(a, 22);
+      case CW_T0: return rotr32(a, 13) & rotr32(a, 22);
+      case CW_R6: return rotr32(ee, 6);
+      case CW_R11: return rotr32(ee, 11);
+      case CW_R25: return rotr32(ee, 25);
+      case CW_T1: return rotr32(ee, 11) & rotr32(ee, 25);
+      default: return sha_spread(a ^ b ^ c) | (sha_spread(mj) << 1);
+    }
+  }
+  const int j = (e - SHA_WT_FF32) & 7;
+  const uint32_t hj = j < 4 ? B.A(-j) : B.E(4 - j);
+  const uint32_t xj = j < 4 ? B.A(64 - j) : B.E(64 - (j - 4));
+  return e < SHA_WT_FF64 ? (uint64_t)(uint32_t)(hj + xj) : (uint64_t)hj + xj;
 }
 
 __device__ __forceinline__ uint64_t sha_block_sig(const ShaBlk& B, uint32_t s) {

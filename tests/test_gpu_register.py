@@ -100,3 +100,46 @@ def test_register_smt_depth_matches_oracle(oracle, gen):
         pp["root"] = field.SplitMix64(i).fr()
         rows.append(I.pack_register_inputs(pp))
     _check(oracle, I.CANONICAL, np.stack(rows))
+
+
+PARAM_VARIANTS = [
+    dict(I.CANONICAL, doc=1),                      # TD1 chunking (190-bit dg1 chunks)
+    dict(I.CANONICAL, aa=0),                       # no active authentication
+    dict(I.CANONICAL, ec_blocks=5, ec_shift=640),  # longer encapsulated content
+]
+
+
+@pytest.mark.parametrize("params", PARAM_VARIANTS, ids=["td1", "aa0", "ec5"])
+def test_register_param_variants_match_oracle(oracle, params):
+    g = I.PassportGen(seed=11, n_keys=2, params=params)
+    rows = np.stack([I.pack_register_inputs(g.passport_at(i, smt_depth=3 * i), params) for i in range(3)])
+    _check(oracle, params, rows)
+
+
+def test_register_rsa4096_matches_oracle(oracle):
+    """SIGNATURE_TYPE 2: RSA-4096, 64-limb BigMultModP (k_rsa_core<64>, k_emit_mm<64>)."""
+    params = dict(I.CANONICAL, sig=2)
+    g = I.PassportGen(seed=12, n_keys=1, key_bits=4096, params=params)
+    rows = np.stack([I.pack_register_inputs(g.passport_at(i), params) for i in range(2)])
+    _check(oracle, params, rows)
+
+
+def test_register_failing_checks_flag_lanes(oracle, gen):
+    """Lanes that violate a constraint get the check-site code of the oracle (single failures) and
+    do not disturb their neighbours; a multiply-failing lane reports a nonzero code."""
+    pps = [gen.passport_at(200 + i) for i in range(4)]
+    rows = np.stack([I.pack_register_inputs(p) for p in pps])
+    ecL = I.CANONICAL["ec_blocks"] * 512
+    rows[1, 1 + ecL + 10] ^= 1                         # one dg1 bit: dg1 hash != EC field -> flow (7)
+    rows[2, rows.shape[1] - 2] = 0                     # siblings[79] != 0 -> SMTVerifier.circom:54 (13)
+    rows[2, rows.shape[1] - 2, 0] = 5
+    sig0 = 1 + ecL + 1024 + I.CANONICAL["dg15_blocks"] * 512 + 1024
+    rows[3, sig0, 0] ^= 1                              # signature limb: EM checks fail (rsa.circom)
+    inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.CANONICAL)
+    _, st = inst.witness_batch_host(rows)
+    prm = oracle.register_params(**I.CANONICAL)
+    codes = [oracle.register_witness(prm, rows[b])[0] for b in range(4)]
+    assert st[0] == 0 and codes[0] == 0
+    assert st[1] == codes[1] == 7
+    assert st[2] == codes[2] == 13
+    assert codes[3] in (8, 9, 10) and st[3] in (8, 9, 10)

@@ -3,6 +3,7 @@
 // compare the two layouts element by element.
 #include "builder_impl.hpp"
 #include "sha_prog.hpp"
+#include "pos_prog.hpp"
 
 #include <algorithm>
 #include <map>
@@ -100,6 +101,53 @@ void sha_program(std::vector<uint32_t>& P) {
   for (int q = 0; q < 6; q++) getsum32(q < 3 ? sha_wt_a(64 - q) : sha_wt_e(64 - (q - 3)));  // sumA..sumG
 }
 
+// Descriptors of the signals of a PoseidonHash(t-1) block (pos_prog.hpp), in witness order:
+// PoseidonHash own (out, in[n]), PoseidonEx own (out, in[n], initialState), ark[0], then per
+// full round Sigma[t] (out, in, in2, in4), Ark (out[t], in[t]), Mix (out[t], in[t], t x GetSum),
+// per partial round SigmaP and MixS, finally Sigma[7] and MixLast (poseidon.circom:80-209).
+void pos_program(int t, std::vector<uint16_t>& P) {
+  const PosImg I(t);
+  const int n = t - 1, RP = I.rp;
+  P.clear();
+  auto C = [&](int idx) { P.push_back(pos_desc(idx, POS_D_COPY)); };
+  // GetSumOfNElements(t) over a prefix-sum row: out | in[t] | sum[t-1]
+  auto getsum = [&](int row) {
+    C(row + t - 1);
+    C(row);
+    for (int j = 1; j < t; j++) P.push_back(pos_desc(row + j, POS_D_DIFF));
+    for (int q = 1; q < t; q++) C(row + q);
+  };
+  C(I.hash);
+  for (int i = 0; i < n; i++) C(I.inp + i);
+  C(I.hash);
+  for (int i = 0; i < n; i++) C(I.inp + i);
+  C(I.zero);
+  for (int j = 0; j < t; j++) C(I.in + j);                   // ark[0].out
+  C(I.zero);                                                 // ark[0].in = initialState, inputs
+  for (int i = 0; i < n; i++) C(I.inp + i);
+  auto full_round = [&](int f) {
+    for (int j = 0; j < t; j++) { int i = f * t + j; C(I.p5 + i); C(I.in + i); C(I.p2 + i); C(I.p4 + i); }
+    for (int q = 0; q < t; q++) C(I.ark + f * t + q);        // ark[f+1].out
+    for (int q = 0; q < t; q++) C(I.p5 + f * t + q);         // ark[f+1].in
+    for (int q = 0; q < t; q++) C(f == 3 ? I.pin + q : I.in + (f + 1) * t + q);  // mix.out = next layer
+    for (int q = 0; q < t; q++) C(I.ark + f * t + q);        // mix.in
+    for (int i = 0; i < t; i++) getsum(I.fs + (f * t + i) * t);
+  };
+  for (int f = 0; f < 4; f++) full_round(f);
+  for (int r = 0; r < RP; r++) {
+    C(I.pp5 + r); C(I.pin + r * t); C(I.pp2 + r); C(I.pp4 + r);      // sigmaP
+    for (int q = 0; q < t; q++) C(I.pin + (r + 1) * t + q);          // mixS.out
+    C(I.pin0 + r);                                                   // mixS.in
+    for (int i = 1; i < t; i++) C(I.pin + r * t + i);
+    getsum(I.ps + r * t);
+  }
+  for (int f = 4; f < 7; f++) full_round(f);
+  for (int j = 0; j < t; j++) { int i = 7 * t + j; C(I.p5 + i); C(I.in + i); C(I.p2 + i); C(I.p4 + i); }
+  C(I.hash);                                                         // mixLast
+  for (int j = 0; j < t; j++) C(I.p5 + 7 * t + j);
+  getsum(I.ls);
+}
+
 namespace {
 
 bool build_poseidon(const pzk_params& p, Layout& L, std::string& why) {
@@ -142,6 +190,16 @@ bool build_layout(const pzk_params& p, Layout& L, std::string& why) {
     case PZK_CIRCUIT_SHA256: ok = build_sha256(p, L, why); break;
     case PZK_CIRCUIT_REGISTER: ok = build_register(p, L, why); break;
     default: why = "unknown circuit family"; return false;
+  }
+  if (ok && !L.pos.empty()) {
+    L.pos_prog.clear();
+    for (int t = 2; t <= POS_MAX_T; t++) {
+      std::vector<uint16_t> P;
+      pos_program(t, P);
+      if (P.size() != pos_hash_size(t - 1)) { why = "internal: Poseidon block program size"; return false; }
+      L.pos_prog_off[t] = (uint32_t)L.pos_prog.size();
+      L.pos_prog.insert(L.pos_prog.end(), P.begin(), P.end());
+    }
   }
   if (ok && !L.sha.empty()) {
     sha_program(L.sha_prog);

@@ -29,6 +29,8 @@ struct Layout {
   std::vector<Work> work[E_COUNT];  // per emit kernel
   std::vector<GenPiece> gen_pieces;  // pieces of the packed emitters' work items
   std::vector<uint32_t> sha_prog;    // SHA block program: one descriptor per block signal (sha_prog.hpp)
+  std::vector<uint16_t> pos_prog;    // Poseidon block programs, t = 2..6 (pos_prog.hpp)
+  uint32_t pos_prog_off[POS_MAX_T + 1] = {};
   std::vector<std::array<uint32_t, 3>> pos_emit_groups;  // (t, first work, works) of work[E_POS]
   std::vector<ShaJob> sha;
   uint32_t sha_core_words = 0;
@@ -55,7 +57,8 @@ inline uint32_t emit_chunk(int e) {
   char name[32];
   snprintf(name, sizeof name, "PZK_CHUNK_%d", e);
   const char* v = getenv(name);
-  return v ? (uint32_t)atoi(v) : EMIT_CHUNK;
+  if (v) return (uint32_t)atoi(v);
+  return e == E_MM ? (1u << 30) : EMIT_CHUNK;  // BigMultModP blocks: whole block per workgroup
 }
 
 }  // namespace pzk

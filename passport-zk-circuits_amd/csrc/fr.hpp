@@ -153,6 +153,26 @@ __device__ __forceinline__ void fr_batch_inv(Acc x, Acc scratch, int n) {
   }
 }
 
+// ---- cross-lane moves of a field element (ds_bpermute per limb)
+__device__ __forceinline__ fr fr_shfl(const fr& a, int src, int width) {
+  fr r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src, width);
+  return r;
+}
+__device__ __forceinline__ fr fr_shfl_up(const fr& a, unsigned d) {
+  fr r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl_up((int)a.v[k], d, 64);
+  return r;
+}
+__device__ __forceinline__ fr fr_shfl_down(const fr& a, unsigned d) {
+  fr r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, 64);
+  return r;
+}
+
 // ---- wave-contiguous element stores
 // Emitters produce one 32-byte element per lane. Stored directly that is 32 B per lane per
 // store pair; staged through LDS it becomes two 1 KiB fully contiguous wave stores of 16 B per

@@ -41,17 +41,20 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
 // wave = 64 witnesses of one task. SMT level tasks below the insertion level depend on the
 // chain and are left to k_smt_chain.
 template <int T>
-__global__ void __launch_bounds__(64, 1) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core, uint32_t core_elems,
-                           const fr* smt_core, uint32_t smt_core_fr) {
+__global__ void __launch_bounds__(256) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
+                                                  uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
   core_priority();
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= vs.batch) return;
+  constexpr int G = T <= 4 ? 4 : 8;
+  const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / G;  // (witness) of this lane group
+  const int j = threadIdx.x & (G - 1);
+  const uint32_t w = gid;
+  if (w >= vs.batch) return;  // whole groups (batch rows are group-aligned)
   const PosTask& task = tasks[blockIdx.y];
   if (task.smt_level >= 0) {
-    int j = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
-    if (task.smt_level < j) return;
+    int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
+    if (task.smt_level < jl) return;  // whole group: same witness
   }
-  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
+  pos_core_group<T, G>(K, task, vs, w, pos_core + (size_t)w * core_elems, j);
 }
 
 // ------------------------------------------------------------------- emit: SHA regions
@@ -139,22 +142,26 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
 }
 
 // ------------------------------------------------------------------- emit: Poseidon
+template <int T>
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
                                                           const fr* pos_core, uint8_t* wtns, size_t stride) {
-  extern __shared__ fr lds[];
+  constexpr PosImg I(T);
+  __shared__ fr img[I.size];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
   const PosTask task = L.pos[R.a[0]];
-  const int n = task.n, t = n + 1;
-  PosLds P;
-  pos_lds_carve(P, lds, t);
-  if (threadIdx.x < (unsigned)n) P.inputs[threadIdx.x] = vs.at(task.in_slot[threadIdx.x], w);
-  if (threadIdx.x == 0) *P.hash = vs.at(task.out_slot, w);
-  pos_lds_fill(P, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off);
-  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
-  __shared__ uint4 stage[2 * EMIT_THREADS];
-  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_fr(pos_block_sig(P, n, wk.start + q)); });
+  pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+  // two lanes per element (16 B each, 1 KiB contiguous per wave store); DIFF rows are the
+  // products of a GetSum row, recovered from its prefix sums
+  const uint16_t* prog = L.pos_prog + L.pos_prog_off[T] + wk.start;
+  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
+  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) {
+    const uint32_t d = prog[h >> 1], idx = d & 2047;
+    fr v = img[idx];
+    if (d >> 11) v = fr_sub(v, img[idx - 1]);
+    out[h] = (h & 1) ? make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]) : make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  }
 }
 
 // ------------------------------------------------------------------- emit: generic small regions
@@ -212,14 +219,15 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
     int t = h_tasks[first + i].n + 1;
     uint32_t j = i;
     while (j < count && h_tasks[first + j].n + 1 == t) j++;
-    dim3 g((vs.batch + 63) / 64, j - i);
+    const uint32_t G = t <= 4 ? 4 : 8;
+    dim3 g((vs.batch * G + 255) / 256, j - i);
     const PosTask* tp = d_tasks + first + i;
     switch (t) {
-      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
       default: return hipErrorInvalidValue;
     }
     HIP_TRY(hipGetLastError());
@@ -242,20 +250,24 @@ hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uin
   return hipGetLastError();
 }
 
-hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
-                           uint32_t batch, hipStream_t st) {
+hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
+                           int32_t* status, uint32_t batch, hipStream_t st) {
   if (L.reg.K == 32) {
     constexpr int NL = 64;
     size_t lds = sizeof(uint64_t) * rsa_lds_words<32>() * NL;
     HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<32, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_rsa_core<32, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, status,
-                       batch);
+    hipLaunchKernelGGL((k_rsa_core<32, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
+                       status, batch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_rsa_inv<32>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
   } else {
     constexpr int NL = 32;
     size_t lds = sizeof(uint64_t) * rsa_lds_words<64>() * NL;
     HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<64, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_rsa_core<64, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, status,
-                       batch);
+    hipLaunchKernelGGL((k_rsa_core<64, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
+                       status, batch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_rsa_inv<64>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
   }
   return hipGetLastError();
 }
@@ -292,11 +304,16 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
     case E_SHA: hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride); break;
-    case E_POS: {
-      size_t lds = sizeof(fr) * (size_t)pos_lds_elems(max_t);
-      hipLaunchKernelGGL(k_emit_pos, g, blk, lds, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride);
+    case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
+      switch (max_t) {
+        case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+        case 3: hipLaunchKernelGGL(k_emit_pos<3>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+        case 4: hipLaunchKernelGGL(k_emit_pos<4>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+        case 5: hipLaunchKernelGGL(k_emit_pos<5>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+        case 6: hipLaunchKernelGGL(k_emit_pos<6>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+        default: return hipErrorInvalidValue;
+      }
       break;
-    }
     case E_BITS: hipLaunchKernelGGL(k_emit_bits, g, blk, 0, st, L, work, B); break;
     case E_FLOW: hipLaunchKernelGGL(k_emit_flow, g, blk, 0, st, L, work, B); break;
     case E_MM:

@@ -28,8 +28,8 @@ hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t
                        int32_t* status, hipStream_t st);
 hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core,
                             const uint64_t* rsa_core, int32_t* status, uint32_t batch, hipStream_t st);
-hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
-                           uint32_t batch, hipStream_t st);
+hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
+                           int32_t* status, uint32_t batch, hipStream_t st);
 hipError_t launch_bjj_table(fr* table, hipStream_t st);
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st);

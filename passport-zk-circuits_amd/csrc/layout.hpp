@@ -171,6 +171,8 @@ struct DevLayout {
   const Work* work;
   const GenPiece* gen_pieces;
   const uint32_t* sha_prog;         // SHA block program (sha_prog.hpp)
+  const uint16_t* pos_prog;         // Poseidon block programs (pos_prog.hpp), at pos_prog_off[t]
+  uint32_t pos_prog_off[POS_MAX_T + 1];
   const ShaJob* sha;
   const PosTask* pos;
   const uint32_t* pos_level_start;  // tasks sorted by level: [start_l, start_{l+1})

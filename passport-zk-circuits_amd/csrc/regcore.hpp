@@ -135,12 +135,32 @@ struct LaneArr {
 template <int K>
 __host__ __device__ constexpr int rsa_lds_words() { return 7 * K + 2; }
 
-// RSA core for one witness lane (K limbs; NL lanes share the workgroup's LDS)
+// 128/64 -> 64 division by a normalised v with a precomputed reciprocal
+// vinv = floor((2^128 - 1) / v) - 2^64 (Moller & Granlund, "Improved division by invariant
+// integers", Alg. 4); requires u1 < v. Two multiplications instead of a software divide.
+__device__ __forceinline__ uint64_t div_preinv(uint64_t u1, uint64_t u0, uint64_t v, uint64_t vinv, uint64_t* rem) {
+  uint64_t q0 = vinv * u1, q1 = __umul64hi(vinv, u1);
+  uint64_t s0 = q0 + u0;
+  q1 += u1 + 1 + (s0 < q0);
+  q0 = s0;
+  uint64_t r = u0 - q1 * v;
+  if (r > q0) { q1--; r += v; }
+  if (r >= v) { q1++; r -= v; }
+  *rem = r;
+  return q1;
+}
+
+// RSA core for one witness lane: the 17 BigMultModP of PowerMod(65537) (bigInt.circom:206-272,
+// 280-340) — operands, quotient and remainder of the exact product (Knuth D with a
+// precomputed reciprocal of the divisor's top word), and the BigIntIsZero carries. The IsEqual
+// inverses are left to k_rsa_inv (one batched inversion per witness over all 17 x K of them).
+// LDS: per-lane arrays [index][lane]; colsum: the x*y column sums, SoA [(3 i + c)][witness].
 template <int K, int NL>
-__device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core, int32_t* status, uint64_t* lds,
-                         int lane) {
+__device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core, uint64_t* colsum, uint32_t cs_stride,
+                         int32_t* status, uint64_t* lds, int lane) {
   LaneArr<NL> n{lds, lane}, x{lds + K * NL, lane}, y{lds + 2 * K * NL, lane}, u{lds + 3 * K * NL, lane},
       q{lds + (5 * K + 1) * NL, lane}, vn{lds + (6 * K + 2) * NL, lane};
+  auto CS = [&](int i, int c) -> uint64_t& { return colsum[(size_t)(3 * i + c) * cs_stride]; };
   bool bad = false, badz = false;
   for (int i = 0; i < K; i++) {
     const uint8_t* e = row + 32ull * (L.reg.in_pk + i);
@@ -152,6 +172,9 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
   const int s = __builtin_clzll(n[nb - 1] | 1ull);
   for (int i = nb - 1; i > 0; i--) vn[i] = (n[i] << s) | (s ? n[i - 1] >> (64 - s) : 0ull);
   vn[0] = n[0] << s;
+  const uint64_t vtop = vn[nb - 1], vsec = nb > 1 ? vn[nb - 2] : 0ull;
+  uint64_t vinv_r;
+  const uint64_t vinv = vtop ? divlu(~vtop, ~0ull, vtop, &vinv_r) : 0ull;  // a zero modulus is flagged below
   constexpr int MMW = MM_CORE_WORDS(K);
   for (int k = 0; k < 17; k++) {
     uint64_t* mc = core + (size_t)k * MMW;
@@ -170,14 +193,17 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
       x[i] = xi; y[i] = yi;
       mc[i] = xi; mc[K + i] = yi;
     }
-    // exact product as 2K words
+    // exact product as 2K words; the raw column sums are kept for the carries
     {
       uint64_t c0 = 0, c1 = 0;
       for (int i = 0; i < 2 * K; i++) {
-        U192 acc; acc.a0 = c0; acc.a1 = c1;
+        U192 acc;
         int lo = i < K ? 0 : i - K + 1, hi = i < K ? i : K - 1;
         for (int j = lo; j <= hi; j++) acc.mac(x[j], y[i - j]);
-        u[i] = acc.a0; c0 = acc.a1; c1 = acc.a2;
+        if (i < 2 * K - 1) { CS(i, 0) = acc.a0; CS(i, 1) = acc.a1; CS(i, 2) = acc.a2; }
+        uint64_t t0 = acc.a0 + c0; uint64_t cc = t0 < c0;
+        uint64_t t1 = acc.a1 + c1; uint64_t cc1 = t1 < c1; uint64_t t1b = t1 + cc; cc1 += t1b < t1;
+        u[i] = t0; c0 = t1b; c1 = acc.a2 + cc1;
       }
     }
     // normalise into 2K+1 words
@@ -187,8 +213,7 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
       u[0] = u[0] << s;
     }
     for (int j = 0; j <= K; j++) q[j] = 0;
-    const uint64_t vtop = vn[nb - 1], vsec = nb > 1 ? vn[nb - 2] : 0ull;
-    for (int j = 2 * K - nb; j >= 0; j--) {
+    for (int j = 2 * K - nb; j >= 0 && vtop; j--) {
       uint64_t ujn = u[j + nb], ujn1 = u[j + nb - 1];
       uint64_t qhat, rhat;
       bool rhat_ovf = false;
@@ -197,7 +222,7 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
         rhat = ujn1 + vtop;
         rhat_ovf = rhat < ujn1;
       } else {
-        qhat = divlu(ujn, ujn1, vtop, &rhat);
+        qhat = div_preinv(ujn, ujn1, vtop, vinv, &rhat);
       }
       if (nb > 1) {
         for (int it = 0; it < 2 && !rhat_ovf; it++) {
@@ -246,30 +271,6 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
       if (i < nb) r = s ? (u[i] >> s) | (u[i + 1] << (64 - s)) : u[i];
       ro[i] = r;
     }
-    // IsEqual inverses of (r_i - n_i) (BigLessEqThan, bigIntComparators.circom:50-75) — one batched inversion
-    uint64_t* iv = mc + 4 * K + 1;  // K x 4 words, normal form
-    {
-      fr acc = fr_mont_one();
-      for (int i = 0; i < K; i++) {
-        uint64_t a = ro[i], b = n[i];
-        fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
-        d = fr_to_mont(d);
-        store_fr(reinterpret_cast<uint8_t*>(iv + 4 * i), acc);  // prefix product (exclusive)
-        if (!fr_is_zero(d)) acc = fr_mul(acc, d);
-      }
-      fr inv = fr_inv(acc);
-      for (int i = K - 1; i >= 0; i--) {
-        uint64_t a = ro[i], b = n[i];
-        fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
-        d = fr_to_mont(d);
-        fr r = fr_zero();
-        if (!fr_is_zero(d)) {
-          r = fr_mul(inv, load_fr(reinterpret_cast<uint8_t*>(iv + 4 * i)));
-          inv = fr_mul(inv, d);
-        }
-        store_fr(reinterpret_cast<uint8_t*>(iv + 4 * i), fr_from_mont(r));
-      }
-    }
     // BigIntIsZero carries (bigIntComparators.circom:105-129): c_i = (d_i + c_{i-1}) / 2^64 exactly,
     // d_i = conv(x,y)_i - conv(q,n)_i - r_i   (signed, 256-bit two's complement)
     uint64_t* cr = mc + 8 * K + 1;  // (2K-2) x (lo, hi)
@@ -277,8 +278,7 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
       uint64_t clo = 0, chi = 0;  // signed 128 carry
       for (int i = 0; i < 2 * K - 1; i++) {
         U192 a, b;
-        int lo = i < K ? 0 : i - K + 1, hi = i < K ? i : K - 1;
-        for (int j = lo; j <= hi; j++) a.mac(x[j], y[i - j]);
+        a.a0 = CS(i, 0); a.a1 = CS(i, 1); a.a2 = CS(i, 2);
         int lo2 = i < K ? 0 : i - K + 1, hi2 = i < K + 1 ? i : K;
         for (int j = lo2; j <= hi2 && j <= K; j++) if (i - j < K) b.mac(q[j], n[i - j]);
         // s = a - b - r_i + c (256-bit)
@@ -307,19 +307,70 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
       }
     }
   }
-  if (bad) set_status(status, ST_INPUT_RANGE);
+  if (bad || !vtop) set_status(status, ST_INPUT_RANGE);
   if (badz) set_status(status, ST_BIGISZERO);
 }
 
 template <int K, int NL>
-__global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
-                                                 uint32_t batch) {
+__global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
+                                                 int32_t* status, uint32_t batch) {
   core_priority();
   extern __shared__ uint64_t lds_rsa[];
   uint32_t w = blockIdx.x * NL + threadIdx.x;
   if (w >= batch) return;
-  rsa_lane<K, NL>(L, inputs + 32ull * (uint64_t)w * L.n_inputs, rsa_core + (size_t)w * L.rsa_core_words,
-                  status ? status + w : nullptr, lds_rsa, threadIdx.x);
+  rsa_lane<K, NL>(L, inputs + 32ull * (uint64_t)w * L.n_inputs, rsa_core + (size_t)w * L.rsa_core_words, colsum + w,
+                  batch, status ? status + w : nullptr, lds_rsa, threadIdx.x);
+}
+
+// IsEqual inverses of (r_i - n_i) for every limb of every BigMultModP (BigLessEqThan,
+// bigIntComparators.circom:50-75; IsZero.inv = 1/in or 0, comparators.circom:17): one wave per
+// witness, one batched inversion over the 17 x K differences. Lane l takes a contiguous run of
+// elements; the run products are combined across the wave with shuffles, so the single Fr
+// inversion is shared by the 64 lanes. Output: normal form, in each BigMultModP's inv slots.
+template <int K>
+__global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, uint32_t batch) {
+  core_priority();
+  const uint32_t w = blockIdx.x;
+  if (w >= batch) return;
+  const int lane = threadIdx.x;
+  constexpr int NE = 17 * K, PER = (NE + 63) / 64, MMW = MM_CORE_WORDS(K);
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  uint64_t* core = rsa_core + (size_t)w * L.rsa_core_words;
+  const int e0 = lane * PER, e1 = e0 + PER < NE ? e0 + PER : NE;
+  auto diff = [&](int e) -> fr {  // (r_i - n_i) in Montgomery form
+    const int k = e / K, i = e - k * K;
+    const uint64_t a = core[(size_t)k * MMW + 3 * K + 1 + i], b = in_u64(row + 32ull * (L.reg.in_pk + i));
+    fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
+    return fr_to_mont(d);
+  };
+  auto slot = [&](int e) -> uint8_t* {
+    const int k = e / K, i = e - k * K;
+    return reinterpret_cast<uint8_t*>(core + (size_t)k * MMW + 4 * K + 1 + 4 * i);
+  };
+  fr acc = fr_mont_one();
+  for (int e = e0; e < e1; e++) {
+    fr d = diff(e);
+    store_fr(slot(e), acc);  // exclusive prefix within the run
+    if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+  }
+  // exclusive prefix / suffix products of the run products across the wave (log-step scans)
+  fr incl = acc, sincl = acc;
+  for (int d = 1; d < 64; d <<= 1) {
+    fr a = fr_shfl_up(incl, d), b = fr_shfl_down(sincl, d);
+    if (lane >= d) incl = fr_mul(incl, a);
+    if (lane + d < 64) sincl = fr_mul(sincl, b);
+  }
+  fr pre = fr_shfl_up(incl, 1), suf = fr_shfl_down(sincl, 1);
+  if (lane == 0) pre = fr_mont_one();
+  if (lane == 63) suf = fr_mont_one();
+  const fr total = fr_shfl(incl, 63, 64);
+  fr inv = fr_mul(fr_mul(fr_inv(total), pre), suf);  // = 1 / (this run's product)
+  for (int e = e1 - 1; e >= e0; e--) {
+    fr d = diff(e);
+    fr r = fr_zero();
+    if (!fr_is_zero(d)) { r = fr_mul(inv, load_fr(slot(e))); inv = fr_mul(inv, d); }
+    store_fr(slot(e), fr_from_mont(r));
+  }
 }
 
 // ============================================================================ RSA EM checks
@@ -430,12 +481,6 @@ __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
   out[0] = x; out[1] = y; out[2] = fr_mul(fr_mul(C.D, x), y);
 }
 
-__device__ __forceinline__ fr fr_shfl(const fr& a, int src, int width) {
-  fr r;
-#pragma unroll
-  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src, width);
-  return r;
-}
 
 // BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171): MSB-first double-and-add over
 // the 254 bits of sk with the (0,0) sentinel for "no point yet". The ladder is cut into BJJ_SEGS

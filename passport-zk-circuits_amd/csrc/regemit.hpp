@@ -349,8 +349,22 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
 struct MMCore {
   int K;
   const uint64_t *x, *y, *q, *r, *n, *inv, *cr;  // LDS
+  const uint64_t *cxy, *cqn;                      // LDS: column sums of x*y (2K-1) and q*n (2K), 3 words each
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
 };
+__device__ __forceinline__ U192 u192_at(const uint64_t* a, int i) { U192 r; r.a0 = a[3 * i]; r.a1 = a[3 * i + 1]; r.a2 = a[3 * i + 2]; return r; }
+__device__ __forceinline__ void u192_addto(U192& a, const U192& b) {
+  uint64_t s0 = a.a0 + b.a0; uint64_t c = s0 < b.a0;
+  uint64_t s1 = a.a1 + b.a1; uint64_t c1 = s1 < b.a1; uint64_t s1b = s1 + c; c1 += s1b < s1;
+  a.a0 = s0; a.a1 = s1b; a.a2 += b.a2 + c1;
+}
+__device__ __forceinline__ U192 u192_shfl_up(const U192& v, unsigned d) {
+  U192 r;
+  r.a0 = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v.a0 >> 32), d, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)v.a0, d, 64);
+  r.a1 = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v.a1 >> 32), d, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)v.a1, d, 64);
+  r.a2 = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v.a2 >> 32), d, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)v.a2, d, 64);
+  return r;
+}
 
 // value of Karatsuba node input j under offset mask O: sum of limbs a[j + o], o in O (<= 2^70)
 __device__ __forceinline__ void kara_in(const uint64_t* a, uint64_t O, int j, uint64_t& lo, uint64_t& hi) {
@@ -384,6 +398,7 @@ __device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
   for (;;) {
     if (s < (uint32_t)(2 * N)) {
       if (s == (uint32_t)(2 * N - 1)) return w_zero();  // top coefficient (K(1).out[1] never assigned)
+      if (N == C.K) return u192w(u192_at(C.cxy, (int)s));  // root: the plain x*y convolution
       U192 acc;
       int lo = s < (uint32_t)N ? 0 : (int)s - N + 1, hi = s < (uint32_t)N ? (int)s : N - 1;
       for (int u = lo; u <= hi; u++) {
@@ -493,11 +508,7 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
   }
   s -= 140 * K;
   // mult2 = BigMultNonEqualOverflow(DIV, K): out[2K] | in1 = q, in2 = n | tmpMults[DIV][K] | tmpResult[2K][K]
-  auto conv_qn = [&](int i) -> U192 {
-    U192 acc;
-    for (int j = i < K ? 0 : i - K + 1; j <= i && j <= K; j++) acc.mac(C.q[j], C.n[i - j]);
-    return acc;
-  };
+  auto conv_qn = [&](int i) -> U192 { return u192_at(C.cqn, i); };
   if (s < (uint32_t)(2 * K)) return u192w(conv_qn(s));
   s -= 2 * K;
   if (s < (uint32_t)(2 * K + 1)) return w_u64(s < (uint32_t)DIV ? C.q[s] : C.n[s - DIV]);
@@ -509,26 +520,32 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
   }
   s -= DIV * K;
   if (s < (uint32_t)(2 * K * K)) {
-    int i = s / K, j = s - i * K;
-    U192 acc;
-    if (i < K) {
-      if (j > i) return w_zero();
-      for (int t = 0; t <= j; t++) acc.mac(C.q[i - t], C.n[t]);
-    } else if (i < DIV) {
-      for (int t = 0; t <= j; t++) acc.mac(C.q[i - t], C.n[t]);
-    } else {
-      if (j >= DIV + K - 1 - i) return w_zero();
-      for (int t = 0; t <= j; t++) acc.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
+    // tmpResult[i][j] = sum_{t<=j} term(i, t): a running sum along the row. Consecutive signals of
+    // a row sit in consecutive lanes, so each lane forms its own term and a segmented inclusive
+    // scan across the wave adds the earlier ones; the row's terms before this wave (if the row
+    // started in an earlier wave) are added by the wave's first lane.
+    const int i = s / K, j = s - i * K, lane = threadIdx.x & 63;
+    auto term = [&](int t) -> U192 {
+      U192 a;
+      if (i < DIV) { if (t <= i) a.mac(C.q[i - t], C.n[t]); }
+      else if (t < DIV + K - 1 - i) a.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
+      return a;
+    };
+    U192 v = term(j);
+    if (lane == 0)
+      for (int t = 0; t < j; t++) u192_addto(v, term(t));
+    for (unsigned d = 1; d < 64; d <<= 1) {
+      U192 o = u192_shfl_up(v, d);
+      if ((int)d <= j && (unsigned)lane >= d) u192_addto(v, o);
     }
-    return u192w(acc);
+    if (i < K ? j > i : (i >= DIV && j >= DIV + K - 1 - i)) return w_zero();
+    return u192w(v);
   }
   s -= 2 * K * K;
   // isZero = BigIntIsZero(64, MAX, 2K-1): in[2K-1] | carry[2K-2] | carryRangeChecks[2K-2]
   if (s < (uint32_t)(2 * K - 1)) {
     int i = s;
-    U192 a;
-    for (int j = i < K ? 0 : i - K + 1; j <= i && j < K; j++) a.mac(C.x[j], C.y[i - j]);
-    W256 d = w_sub(u192w(a), u192w(conv_qn(i)));
+    W256 d = w_sub(u192w(u192_at(C.cxy, i)), u192w(conv_qn(i)));
     if (i < K) d = w_sub(d, w_u64(C.r[i]));
     return w_signed_to_fr(d);
   }
@@ -551,7 +568,7 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
 
 template <int K>
 __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
-  __shared__ uint64_t lds[MM_CORE_WORDS(K) + K];
+  __shared__ uint64_t lds[MM_CORE_WORDS(K) + K + 3 * (4 * K - 1)];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
@@ -560,7 +577,23 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   for (int i = threadIdx.x; i < MM_CORE_WORDS(K); i += blockDim.x) lds[i] = mc[i];
   for (int i = threadIdx.x; i < K; i += blockDim.x) lds[MM_CORE_WORDS(K) + i] = in_u64(row + 32ull * (R.a[1] + i));
   __syncthreads();
-  MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1};
+  // column sums of x*y (2K-1) and q*n (2K), one thread per column
+  uint64_t* cxy = lds + MM_CORE_WORDS(K) + K;
+  uint64_t* cqn = cxy + 3 * (2 * K - 1);
+  for (int c = threadIdx.x; c < 4 * K - 1; c += blockDim.x) {
+    U192 acc;
+    if (c < 2 * K - 1) {
+      for (int j = c < K ? 0 : c - K + 1; j <= c && j < K; j++) acc.mac(lds[j], lds[K + (c - j)]);
+      cxy[3 * c] = acc.a0; cxy[3 * c + 1] = acc.a1; cxy[3 * c + 2] = acc.a2;
+    } else {
+      const int i = c - (2 * K - 1);
+      for (int j = i < K ? 0 : i - K + 1; j <= i && j <= K; j++) acc.mac(lds[2 * K + j], lds[MM_CORE_WORDS(K) + (i - j)]);
+      cqn[3 * i] = acc.a0; cqn[3 * i + 1] = acc.a1; cqn[3 * i + 2] = acc.a2;
+    }
+  }
+  __syncthreads();
+  MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
+           cxy, cqn};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, wk.start + q)); });

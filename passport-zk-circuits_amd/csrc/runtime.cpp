@@ -101,12 +101,13 @@ struct pzk_instance {
   // streams onto by default, so no two of them share a queue.
   hipStream_t s_rsa = nullptr, s_sha = nullptr;
   hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_j_rsa = nullptr,
-             ev_j_bjj = nullptr;
+             ev_j_bjj = nullptr, ev_entry = nullptr, ev_exit = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
   Work* d_work[E_COUNT] = {};
   GenPiece* d_gen_pieces = nullptr;
   uint32_t* d_sha_prog = nullptr;
+  uint16_t* d_pos_prog = nullptr;
   ShaJob* d_sha = nullptr;
   PosTask* d_pos = nullptr;
   ValueLoad* d_loads = nullptr;
@@ -120,6 +121,7 @@ struct pzk_instance {
   fr* d_pos_core = nullptr;
   fr* d_values = nullptr;
   uint64_t* d_rsa_core = nullptr;
+  uint64_t* d_rsa_colsum = nullptr;  // RSA x*y column sums, SoA [(3 i + c)][witness]
   fr *d_bjj_core = nullptr, *d_bjj_scratch = nullptr, *d_smt_core = nullptr;
   // staging for the host-buffer path
   size_t host_cap = 0;
@@ -139,6 +141,8 @@ struct pzk_instance {
     L.regions = d_regions;
     L.gen_pieces = d_gen_pieces;
     L.sha_prog = d_sha_prog;
+    L.pos_prog = d_pos_prog;
+    for (int t = 0; t <= POS_MAX_T; t++) L.pos_prog_off[t] = lay.pos_prog_off[t];
     L.sha = d_sha;
     L.pos = d_pos;
     L.reg = lay.reg;
@@ -218,17 +222,18 @@ static int upload(T** dst, const std::vector<T>& v) {
 }
 
 static void free_scratch(pzk_instance* I) {
-  void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_bjj_core, I->d_bjj_scratch, I->d_smt_core};
+  void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_rsa_colsum, I->d_bjj_core,
+                  I->d_bjj_scratch, I->d_smt_core};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr;
+  I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr; I->d_rsa_colsum = nullptr;
   I->d_bjj_core = nullptr; I->d_bjj_scratch = nullptr; I->d_smt_core = nullptr;
   I->cap = 0;
 }
 
 static void free_all(pzk_instance* I) {
   free_scratch(I);
-  void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
+  void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -236,7 +241,7 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha})
     if (s) (void)hipStreamDestroy(s);
-  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_j_rsa, I->ev_j_bjj})
+  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_j_rsa, I->ev_j_bjj, I->ev_entry, I->ev_exit})
     if (e) (void)hipEventDestroy(e);
   I->timing.destroy();
 }
@@ -265,6 +270,7 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   for (int e = 0; e < E_COUNT && !rc; e++) rc = upload(&I->d_work[e], I->lay.work[e]);
   if (!rc) rc = upload(&I->d_gen_pieces, I->lay.gen_pieces);
   if (!rc) rc = upload(&I->d_sha_prog, I->lay.sha_prog);
+  if (!rc) rc = upload(&I->d_pos_prog, I->lay.pos_prog);
   if (!rc) rc = upload(&I->d_sha, I->lay.sha);
   if (!rc) rc = upload(&I->d_pos, I->lay.pos);
   if (!rc) rc = upload(&I->d_loads, I->lay.loads);
@@ -275,10 +281,17 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
       rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
   }
   if (rc) { free_all(I); delete I; return rc; }
-  bool ok = hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&I->s_rsa, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&I->s_sha, hipStreamNonBlocking) == hipSuccess;
-  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_j_rsa, &I->ev_j_bjj})
+  // The dependency chains (main stream: Poseidon/SMT/BJJ cores; s_rsa: RSA core) get the
+  // highest queue priority, the bulk SHA emitter the lowest: when the chip is full of emitter
+  // workgroups, the dispatcher hands freed CU slots to the latency-bound chain kernels first.
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (getenv("PZK_NO_PRIO")) prio_hi = prio_lo;  // A/B switch for scheduling experiments
+  bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess;
+  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_j_rsa, &I->ev_j_bjj, &I->ev_entry,
+                        &I->ev_exit})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
   *out = I;
@@ -361,6 +374,7 @@ static int ensure_scratch(pzk_instance* I, size_t batch) {
       {(void**)&I->d_pos_core, 32ull * L.pos_core_elems * batch},
       {(void**)&I->d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
       {(void**)&I->d_rsa_core, 8ull * L.rsa_core_words * batch},
+      {(void**)&I->d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
       {(void**)&I->d_bjj_core, 32ull * L.bjj_core_fr * batch},
       {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&I->d_smt_core, 32ull * L.smt_core_fr * batch},
@@ -383,7 +397,13 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   if (exec && exec->device != I->device) HIPCHK(hipSetDevice(exec->device));
   int rc = ensure_scratch(I, batch);
   if (rc) return rc;
-  hipStream_t st = (exec && exec->stream) ? (hipStream_t)exec->stream : I->stream;
+  // all work runs on the instance's streams; a caller stream is joined at entry and exit
+  hipStream_t user = (exec && exec->stream) ? (hipStream_t)exec->stream : nullptr;
+  hipStream_t st = I->stream;
+  if (user) {
+    HIPCHK(hipEventRecord(I->ev_entry, user));
+    HIPCHK(hipStreamWaitEvent(st, I->ev_entry, 0));
+  }
   const uint32_t B = (uint32_t)batch;
   const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
@@ -428,23 +448,24 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
       if ((rc = emit(e, st))) return rc;
   } else {
     // Three streams (DESIGN.md §4 "Schedule"). The RSA core depends only on the inputs, so it
-    // starts at once on its own stream, its emitter behind it; the SHA emitter (the bulk of the
-    // bytes) starts as soon as the SHA core is done; the main stream runs the Poseidon/SMT
-    // dependency chain, the BabyJubJub core and the remaining emitters, then joins.
+    // starts at once on its own (high-priority) stream; the bulk emitters (SHA, then BigMultModP,
+    // then BabyJubJub) run on the low-priority stream as their cores finish; the main
+    // (high-priority) stream runs the Poseidon/SMT dependency chain, the BabyJubJub core and the
+    // remaining emitters, then joins.
     // PZK_SERIAL=1 (profiling): every phase on the launch stream, so kernel times are standalone
     static const bool serial = getenv("PZK_SERIAL") != nullptr;
     hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha;
     HIPCHK(hipEventRecord(I->ev_load, st));
     HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_load, 0));
     { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
-      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, d_status, B, s_rsa)); }
+      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
     HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
-    if ((rc = emit(E_MM, s_rsa))) return rc;
-    HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
     { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
     HIPCHK(hipEventRecord(I->ev_sha, st));
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_rsa, 0));
+    if ((rc = emit(E_MM, s_sha))) return rc;
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
@@ -466,9 +487,13 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
       HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st)); }
     if ((rc = emit(E_BITS, st))) return rc;
     if ((rc = emit(E_GENR, st))) return rc;
-    for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));
+    HIPCHK(hipStreamWaitEvent(st, I->ev_j_bjj, 0));
   }
-  if (exec && (exec->flags & PZK_EXEC_SYNC)) HIPCHK(hipStreamSynchronize(st));
+  if (user) {
+    HIPCHK(hipEventRecord(I->ev_exit, st));
+    HIPCHK(hipStreamWaitEvent(user, I->ev_exit, 0));
+  }
+  if (exec && (exec->flags & PZK_EXEC_SYNC)) HIPCHK(hipStreamSynchronize(user ? user : st));
   return 0;
 }
 

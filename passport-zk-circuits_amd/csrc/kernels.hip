@@ -40,6 +40,22 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
 // ------------------------------------------------------------------- Poseidon core
 // wave = 64 witnesses of one task. SMT level tasks below the insertion level depend on the
 // chain and are left to k_smt_chain.
+// lane per permutation: for launches with many tasks (the 80 SMT level hashes), where the
+// batch x tasks lanes already fill the chip and the cooperative form only adds shuffles
+template <int T>
+__global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
+                                                  uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
+  core_priority();
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= vs.batch) return;
+  const PosTask& task = tasks[blockIdx.y];
+  if (task.smt_level >= 0) {
+    int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
+    if (task.smt_level < jl) return;
+  }
+  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
+}
+
 template <int T>
 __global__ void __launch_bounds__(256) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
                                                   uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
@@ -219,9 +235,23 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
     int t = h_tasks[first + i].n + 1;
     uint32_t j = i;
     while (j < count && h_tasks[first + j].n + 1 == t) j++;
+    const PosTask* tp = d_tasks + first + i;
+    if (j - i >= 8) {  // many tasks: one lane per permutation
+      dim3 g1((vs.batch + 63) / 64, j - i);
+      switch (t) {
+        case 2: hipLaunchKernelGGL(k_pos_core1<2>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+        case 3: hipLaunchKernelGGL(k_pos_core1<3>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+        case 4: hipLaunchKernelGGL(k_pos_core1<4>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+        case 5: hipLaunchKernelGGL(k_pos_core1<5>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+        case 6: hipLaunchKernelGGL(k_pos_core1<6>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+        default: return hipErrorInvalidValue;
+      }
+      HIP_TRY(hipGetLastError());
+      i = j;
+      continue;
+    }
     const uint32_t G = t <= 4 ? 4 : 8;
     dim3 g((vs.batch * G + 255) / 256, j - i);
-    const PosTask* tp = d_tasks + first + i;
     switch (t) {
       case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
       case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;

@@ -17,7 +17,9 @@ namespace pzk {
 
 struct PosConsts {
   const fr* base;   // Montgomery-form constants
+  const fr* nbase;  // the same constants in normal form
   PosParamIndex ix;
+  __device__ __forceinline__ const fr& Cn(int t, int i) const { return nbase[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& C(int t, int i) const { return base[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& M(int t, int i, int j) const { return base[ix.m_off[t] + i * t + j]; }
   __device__ __forceinline__ const fr& Pm(int t, int i, int j) const { return base[ix.p_off[t] + i * t + j]; }
@@ -191,19 +193,22 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (q < 8 * t) {
       const int f = q / t, j = q - f * t;
       const int ci = f < 4 ? f * t + j : f == 4 ? 4 * t + RP * t + j : 4 * t + (RP + 1) * t + (f - 5) * t + j;
-      const fr x = core[ci], x2 = fr_sqr(x), x4 = fr_sqr(x2), x5 = fr_mul(x4, x);
-      img[I.in + q] = fr_from_mont(x); img[I.p2 + q] = fr_from_mont(x2);
-      img[I.p4 + q] = fr_from_mont(x4); img[I.p5 + q] = fr_from_mont(x5);
+      // mixed forms: mont_mul(aR, b) = ab, so normal-form powers come straight out of products
+      // with the Montgomery-form x and x^2 (3.4 products per S-box instead of 5.3)
+      const fr xm = core[ci], x2m = fr_sqr(xm), x2 = fr_from_mont(x2m), x4 = fr_mul(x2m, x2), x5 = fr_mul(x4, xm);
+      img[I.in + q] = fr_from_mont(xm); img[I.p2 + q] = x2;
+      img[I.p4 + q] = x4; img[I.p5 + q] = x5;
       if (f < 7) {
         const int cidx = f < 4 ? (f + 1) * t + j : 5 * t + RP + (f - 4) * t + j;
-        img[I.ark + q] = fr_from_mont(fr_add(x5, K.C(t, cidx)));
+        img[I.ark + q] = fr_add(x5, K.Cn(t, cidx));
       }
     } else if (q < NA) {
       const int r = q - 8 * t;
-      const fr x = core[4 * t + r * t], x2 = fr_sqr(x), x4 = fr_sqr(x2), x5 = fr_mul(x4, x);
-      img[I.pin + r * t] = fr_from_mont(x); img[I.pp2 + r] = fr_from_mont(x2);
-      img[I.pp4 + r] = fr_from_mont(x4); img[I.pp5 + r] = fr_from_mont(x5);
-      img[I.pin0 + r] = fr_from_mont(fr_add(x5, K.C(t, 5 * t + r)));
+      const fr xm = core[4 * t + r * t], x2m = fr_sqr(xm), x2 = fr_from_mont(x2m), x4 = fr_mul(x2m, x2),
+               x5 = fr_mul(x4, xm);
+      img[I.pin + r * t] = fr_from_mont(xm); img[I.pp2 + r] = x2;
+      img[I.pp4 + r] = x4; img[I.pp5 + r] = x5;
+      img[I.pin0 + r] = fr_add(x5, K.Cn(t, 5 * t + r));
     } else if (q < NA + NC) {
       const int c = q - NA;
       int r, i;

@@ -115,6 +115,7 @@ struct pzk_instance {
   fr* d_pos_consts = nullptr;
   fr* d_bjj_table = nullptr;  // fixed-base Base8 table (register circuit)
   PosParamIndex pix{};
+  int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
   // per-batch scratch, grown on demand
   size_t cap = 0;
   uint32_t* d_sha_core = nullptr;
@@ -205,8 +206,11 @@ static int load_poseidon(pzk_instance* I) {
     off += 32 * n_el;
   }
   int n = (int)(consts.size() / 32);
-  HIPCHK(hipMalloc(&I->d_pos_consts, consts.size()));
+  // two copies: Montgomery form (cores) and normal form (the emitters' round-constant adds)
+  HIPCHK(hipMalloc(&I->d_pos_consts, 2 * consts.size()));
   HIPCHK(hipMemcpy(I->d_pos_consts, consts.data(), consts.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(I->d_pos_consts + n, consts.data(), consts.size(), hipMemcpyHostToDevice));
+  I->pos_consts_n = n;
   hipLaunchKernelGGL(k_to_mont_inplace, dim3((n + 255) / 256), dim3(256), 0, 0, I->d_pos_consts, n);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
@@ -408,7 +412,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
   ValueStore vs{I->d_values, B};
-  PosConsts K{I->d_pos_consts, I->pix};
+  PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix};
   Bufs bufs{d_inputs, I->d_sha_core, I->d_rsa_core, I->d_pos_core, I->d_bjj_core, I->d_smt_core, vs, d_wtns, stride,
             d_status};
   Timing* T = nullptr;

@@ -5,6 +5,7 @@
 // templates (cited inline); the CPU oracle derives them independently and the parity tests
 // compare every element.
 #include "builder_impl.hpp"
+#include "mm_prog.hpp"
 
 namespace pzk {
 
@@ -151,6 +152,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   b.region(RK_INCOPY, K, {IN_PK});
   const uint32_t mm = modmul_size(K);
   L.reg.modmul_size = mm;
+  if (mm_section_start(K, MM_SECTIONS) != mm) { why = "internal: BigMultModP section sizes"; return false; }
   // exp_to_bits(65537) = [16, 2, 0, 16]: muls[i] = muls[i-1]^2 (muls[0] = base^2); resultMuls[0] = base * muls[15]
   L.reg.n_modmul = 17;
   L.rsa_core_words = 17 * MM_CORE_WORDS(K);

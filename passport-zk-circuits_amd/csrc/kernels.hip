@@ -166,11 +166,14 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
-  const PosTask task = L.pos[R.a[0]];
+  const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
+  // the block's descriptors go to LDS first: a global load inside the store loop would wait for
+  // every store in flight (gfx9 vmcnt counts stores too)
+  __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
+  for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
   pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
   // two lanes per element (16 B each, 1 KiB contiguous per wave store); DIFF rows are the
   // products of a GetSum row, recovered from its prefix sums
-  const uint16_t* prog = L.pos_prog + L.pos_prog_off[T] + wk.start;
   uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
   for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) {
     const uint32_t d = prog[h >> 1], idx = d & 2047;

@@ -148,6 +148,11 @@ __host__ __device__ inline uint32_t pos_ex_size(int n) {
   return (uint32_t)((2 + n) + 8 * (2 * t) + 8 * t * 4 + 7 * (2 * t + 2 * t * t) + RP * (4 + 4 * t) + (3 * t + 1));
 }
 __host__ __device__ inline uint32_t pos_hash_size(int n) { return 1 + n + pos_ex_size(n); }
+__host__ __device__ constexpr uint32_t pos_hash_size_c(int n) {
+  return 1 + n + (uint32_t)((2 + n) + 8 * (2 * (n + 1)) + 8 * (n + 1) * 4 + 7 * (2 * (n + 1) + 2 * (n + 1) * (n + 1)) +
+                            (n + 1 == 2 ? 56 : n + 1 == 3 ? 57 : n + 1 == 4 ? 56 : 60) * (4 + 4 * (n + 1)) +
+                            (3 * (n + 1) + 1));
+}
 
 // Poseidon parameters on device: per t, offsets (in Fr) into one constant array, Montgomery form
 struct PosParamIndex {

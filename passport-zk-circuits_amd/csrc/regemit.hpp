@@ -10,6 +10,7 @@
 #include "poseidon.hpp"
 #include "regcore.hpp"
 #include "sha.hpp"
+#include "mm_prog.hpp"
 
 namespace pzk {
 
@@ -20,6 +21,7 @@ __device__ __forceinline__ W256 w_zero() { W256 r; for (int i = 0; i < 8; i++) r
 __device__ __forceinline__ W256 w_u64(uint64_t x) { W256 r = w_zero(); r.v[0] = (uint32_t)x; r.v[1] = (uint32_t)(x >> 32); return r; }
 __device__ __forceinline__ W256 w_mask(const W256& a, int nbits) {  // a mod 2^nbits
   W256 r = a;
+#pragma unroll
   for (int i = 0; i < 8; i++) {
     int lo = 32 * i;
     if (nbits <= lo) r.v[i] = 0;
@@ -27,7 +29,16 @@ __device__ __forceinline__ W256 w_mask(const W256& a, int nbits) {  // a mod 2^n
   }
   return r;
 }
-__device__ __forceinline__ uint32_t w_bit(const W256& a, int i) { return (a.v[i >> 5] >> (i & 31)) & 1u; }
+// word k of a (select chain: a runtime index into a register array would go to scratch, and a
+// scratch load inside an emit loop waits for every store in flight)
+__device__ __forceinline__ uint32_t w_word(const W256& a, int k) {
+  // AND/OR with lane masks rather than selects, which LLVM folds back into a scratch lookup
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r |= a.v[i] & (0u - (uint32_t)(k == i));
+  return r;
+}
+__device__ __forceinline__ uint32_t w_bit(const W256& a, int i) { return (w_word(a, i >> 5) >> (i & 31)) & 1u; }
 __device__ __forceinline__ void store_w(uint8_t* dst, const W256& a) {
   uint4* d = reinterpret_cast<uint4*>(dst);
   d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
@@ -439,34 +450,11 @@ __device__ __forceinline__ W256 w_sub(const W256& a, const W256& b) {
   return r;
 }
 
-// BigMultModP(64,K,K,K) block signal s (bigInt.circom:206-272)
-__device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
+// BigMultModP(64,K,K,K) block signal (bigInt.circom:206-272), addressed by the block program
+// (mm_prog.hpp): section + index within the section, so the emitter does no range cascade.
+__device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
   const int K = C.K, DIV = K + 1;
-  // own: div[DIV] | mod[K] | in1[K], in2[K], modulus[K]
-  if (s < (uint32_t)DIV) return w_u64(C.q[s]);
-  s -= DIV;
-  if (s < (uint32_t)K) return w_u64(C.r[s]);
-  s -= K;
-  if (s < (uint32_t)(3 * K)) { int g = s / K, i = s - g * K; return w_u64(g == 0 ? C.x[i] : g == 1 ? C.y[i] : C.n[i]); }
-  s -= 3 * K;
-  // mult = BigMultOverflow: out[2K-1] | in1, in2 | karatsuba
-  if (s < (uint32_t)(2 * K - 1)) return kara_sig(C, K, s);
-  s -= 2 * K - 1;
-  if (s < (uint32_t)(2 * K)) return w_u64(s < (uint32_t)K ? C.x[s] : C.y[s - K]);
-  s -= 2 * K;
-  uint32_t ks = kara_size(K);
-  if (s < ks) return kara_sig(C, K, s);
-  s -= ks;
-  // modChecks[K]: Num2Bits(64)(mod_i): out[64] | in | sum[64]
-  if (s < (uint32_t)(129 * K)) {
-    uint32_t i = s / 129, t = s - 129 * i;
-    uint64_t v = C.r[i];
-    if (t < 64) return w_u64((v >> t) & 1);
-    if (t == 64) return w_u64(v);
-    return w_u64(v & mask_lo((int)t - 64));
-  }
-  s -= 129 * K;
-  // greaterThan: out | in[0]=modulus, in[1]=mod | lessEqThan: out | in | result[K] | (lessThan(64), isEqual) x K
+  const uint32_t s = d & 0xFFFFFFu;
   auto le_result = [&](int upto) -> uint32_t {
     uint32_t res = 0;
     for (int i = 0; i <= upto; i++) {
@@ -475,95 +463,92 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t s) {
     }
     return res;
   };
-  if (s == 0) return w_u64(1 - le_result(K - 1));
-  if (s < (uint32_t)(1 + 2 * K)) { s -= 1; return w_u64(s < (uint32_t)K ? C.n[s] : C.r[s - K]); }
-  s -= 1 + 2 * K;
-  if (s == 0) return w_u64(le_result(K - 1));
-  if (s < (uint32_t)(1 + 2 * K)) { s -= 1; return w_u64(s < (uint32_t)K ? C.n[s] : C.r[s - K]); }
-  s -= 1 + 2 * K;
-  if (s < (uint32_t)K) return w_u64(le_result((int)s));
-  s -= K;
-  if (s < (uint32_t)(140 * K)) {
-    uint32_t i = s / 140, t = s - 140 * i;
-    uint64_t a = C.n[i], b = C.r[i];
-    if (t < 134) {  // LessThan(64): out | in[2] | Num2Bits(65)(a + 2^64 - b)
-      // v = a + 2^64 - b (65-bit)
-      uint64_t vlo = a - b; uint32_t vhi = a >= b ? 1u : 0u;
-      if (t == 0) return w_u64(1 - vhi);
+  switch (d >> 24) {
+    case MM_Q: return w_u64(C.q[s]);                                   // div[DIV]
+    case MM_R: return w_u64(C.r[s]);                                   // mod[K]
+    case MM_XYN: { int g = s / K, i = s - g * K; return w_u64(g == 0 ? C.x[i] : g == 1 ? C.y[i] : C.n[i]); }
+    case MM_MOUT: return u192w(u192_at(C.cxy, (int)s));                // mult.out = x*y columns
+    case MM_MCOPY: return w_u64(s < (uint32_t)K ? C.x[s] : C.y[s - K]);
+    case MM_KARA: return kara_sig(C, K, s);
+    case MM_MODCHK: {  // Num2Bits(64)(mod_i): out[64] | in | sum[64]
+      uint32_t i = s / 129, t = s - 129 * i;
+      uint64_t v = C.r[i];
+      if (t < 64) return w_u64((v >> t) & 1);
+      if (t == 64) return w_u64(v);
+      return w_u64(v & mask_lo((int)t - 64));
+    }
+    case MM_GT0: return w_u64(1 - le_result(K - 1));                   // greaterThan.out
+    case MM_GTIN: case MM_LEIN: return w_u64(s < (uint32_t)K ? C.n[s] : C.r[s - K]);
+    case MM_LE0: return w_u64(le_result(K - 1));
+    case MM_LERES: return w_u64(le_result((int)s));
+    case MM_LT: {
+      uint32_t i = s / 140, t = s - 140 * i;
+      uint64_t a = C.n[i], b = C.r[i];
+      if (t < 134) {  // LessThan(64): out | in[2] | Num2Bits(65)(a + 2^64 - b)
+        uint64_t vlo = a - b; uint32_t vhi = a >= b ? 1u : 0u;
+        if (t == 0) return w_u64(1 - vhi);
+        if (t == 1) return w_u64(a);
+        if (t == 2) return w_u64(b);
+        t -= 3;
+        W256 v = w_zero(); v.v[0] = (uint32_t)vlo; v.v[1] = (uint32_t)(vlo >> 32); v.v[2] = vhi;
+        if (t < 65) return w_u64(w_bit(v, t));
+        if (t == 65) return v;
+        return w_mask(v, (int)t - 65);
+      }
+      t -= 134;  // IsEqual: out | in[2] | IsZero(out, in, inv)
+      if (t == 0 || t == 3) return w_u64(a == b);
       if (t == 1) return w_u64(a);
       if (t == 2) return w_u64(b);
-      t -= 3;
-      W256 v = w_zero(); v.v[0] = (uint32_t)vlo; v.v[1] = (uint32_t)(vlo >> 32); v.v[2] = vhi;
-      if (t < 65) return w_u64(w_bit(v, t));
-      if (t == 65) return v;
-      return w_mask(v, (int)t - 65);
+      if (t == 4) return a <= b ? w_u64(b - a) : w_from_fr(fr_sub(fr_zero(), fr_u64(a - b)));
+      W256 r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)(C.inv[4 * i + (k >> 1)] >> (32 * (k & 1)));
+      return r;
     }
-    t -= 134;  // IsEqual: out | in[2] | IsZero(out, in, inv)
-    if (t == 0 || t == 3) return w_u64(a == b);
-    if (t == 1) return w_u64(a);
-    if (t == 2) return w_u64(b);
-    if (t == 4) return a <= b ? w_u64(b - a) : w_from_fr(fr_sub(fr_zero(), fr_u64(a - b)));
-    W256 r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)(C.inv[4 * i + (k >> 1)] >> (32 * (k & 1)));
-    return r;
-  }
-  s -= 140 * K;
-  // mult2 = BigMultNonEqualOverflow(DIV, K): out[2K] | in1 = q, in2 = n | tmpMults[DIV][K] | tmpResult[2K][K]
-  auto conv_qn = [&](int i) -> U192 { return u192_at(C.cqn, i); };
-  if (s < (uint32_t)(2 * K)) return u192w(conv_qn(s));
-  s -= 2 * K;
-  if (s < (uint32_t)(2 * K + 1)) return w_u64(s < (uint32_t)DIV ? C.q[s] : C.n[s - DIV]);
-  s -= 2 * K + 1;
-  if (s < (uint32_t)(DIV * K)) {
-    uint32_t i = s / K, j = s - i * K;
-    U192 acc; acc.mac(C.q[i], C.n[j]);
-    return u192w(acc);
-  }
-  s -= DIV * K;
-  if (s < (uint32_t)(2 * K * K)) {
-    // tmpResult[i][j] = sum_{t<=j} term(i, t): a running sum along the row. Consecutive signals of
-    // a row sit in consecutive lanes, so each lane forms its own term and a segmented inclusive
-    // scan across the wave adds the earlier ones; the row's terms before this wave (if the row
-    // started in an earlier wave) are added by the wave's first lane.
-    const int i = s / K, j = s - i * K, lane = threadIdx.x & 63;
-    auto term = [&](int t) -> U192 {
-      U192 a;
-      if (i < DIV) { if (t <= i) a.mac(C.q[i - t], C.n[t]); }
-      else if (t < DIV + K - 1 - i) a.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
-      return a;
-    };
-    U192 v = term(j);
-    if (lane == 0)
-      for (int t = 0; t < j; t++) u192_addto(v, term(t));
-    for (unsigned d = 1; d < 64; d <<= 1) {
-      U192 o = u192_shfl_up(v, d);
-      if ((int)d <= j && (unsigned)lane >= d) u192_addto(v, o);
+    case MM_M2OUT: return u192w(u192_at(C.cqn, (int)s));               // mult2.out = q*n columns
+    case MM_M2IN: return w_u64(s < (uint32_t)DIV ? C.q[s] : C.n[s - DIV]);
+    case MM_TMPM: { uint32_t i = s / K, j = s - i * K; U192 acc; acc.mac(C.q[i], C.n[j]); return u192w(acc); }
+    case MM_TMPR: {
+      // tmpResult[i][j] = sum_{t<=j} term(i, t): a running sum along the row. Consecutive signals of
+      // a row sit in consecutive lanes, so each lane forms its own term and a segmented inclusive
+      // scan across the wave adds the earlier ones; the row's terms before this wave (if the row
+      // started in an earlier wave) are added by the wave's first lane.
+      const int i = s / K, j = s - i * K, lane = threadIdx.x & 63;
+      auto term = [&](int t) -> U192 {
+        U192 a;
+        if (i < DIV) { if (t <= i) a.mac(C.q[i - t], C.n[t]); }
+        else if (t < DIV + K - 1 - i) a.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
+        return a;
+      };
+      U192 v = term(j);
+      if (lane == 0)
+        for (int t = 0; t < j; t++) u192_addto(v, term(t));
+      for (unsigned dd = 1; dd < 64; dd <<= 1) {
+        U192 o = u192_shfl_up(v, dd);
+        if ((int)dd <= j && (unsigned)lane >= dd) u192_addto(v, o);
+      }
+      if (i < K ? j > i : (i >= DIV && j >= DIV + K - 1 - i)) return w_zero();
+      return u192w(v);
     }
-    if (i < K ? j > i : (i >= DIV && j >= DIV + K - 1 - i)) return w_zero();
-    return u192w(v);
+    case MM_ISZIN: {  // BigIntIsZero.in = x*y - q*n - r (signed)
+      const int i = s;
+      W256 dd = w_sub(u192w(u192_at(C.cxy, i)), u192w(u192_at(C.cqn, i)));
+      if (i < K) dd = w_sub(dd, w_u64(C.r[i]));
+      return w_signed_to_fr(dd);
+    }
+    case MM_CARRY: return w_from_fr(fr_from_i128(C.cr[2 * s], C.cr[2 * s + 1]));
+    default: {  // MM_RANGE: Num2Bits(RL)(carry + 2^(RL-1))
+      const int MAXB = 128 + (K == 32 ? 7 : 8);  // 2*64 + log_ceil(2K)
+      const int RL = MAXB + 3 - 64;
+      uint32_t per = 2 * RL + 1, i = s / per, t = s - per * i;
+      uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1];
+      uint64_t add_hi = 1ull << (RL - 1 - 64);
+      uint64_t vhi = hi + add_hi;
+      W256 v = w_zero();
+      v.v[0] = (uint32_t)lo; v.v[1] = (uint32_t)(lo >> 32); v.v[2] = (uint32_t)vhi; v.v[3] = (uint32_t)(vhi >> 32);
+      if (t < (uint32_t)RL) return w_u64(w_bit(v, t));
+      if (t == (uint32_t)RL) return v;
+      return w_mask(v, (int)t - RL);
+    }
   }
-  s -= 2 * K * K;
-  // isZero = BigIntIsZero(64, MAX, 2K-1): in[2K-1] | carry[2K-2] | carryRangeChecks[2K-2]
-  if (s < (uint32_t)(2 * K - 1)) {
-    int i = s;
-    W256 d = w_sub(u192w(u192_at(C.cxy, i)), u192w(conv_qn(i)));
-    if (i < K) d = w_sub(d, w_u64(C.r[i]));
-    return w_signed_to_fr(d);
-  }
-  s -= 2 * K - 1;
-  if (s < (uint32_t)(2 * K - 2)) return w_from_fr(fr_from_i128(C.cr[2 * s], C.cr[2 * s + 1]));
-  s -= 2 * K - 2;
-  const int MAXB = 128 + (K == 32 ? 7 : 8);  // 2*64 + log_ceil(2K)
-  const int RL = MAXB + 3 - 64;              // Num2Bits width of the carry range checks
-  uint32_t per = 2 * RL + 1, i = s / per, t = s - per * i;
-  // value = carry + 2^(RL-1) (non-negative, < 2^RL for a passing witness)
-  uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1];
-  uint64_t add_hi = 1ull << (RL - 1 - 64);
-  uint64_t vhi = hi + add_hi;
-  W256 v = w_zero();
-  v.v[0] = (uint32_t)lo; v.v[1] = (uint32_t)(lo >> 32); v.v[2] = (uint32_t)vhi; v.v[3] = (uint32_t)(vhi >> 32);
-  if (t < (uint32_t)RL) return w_u64(w_bit(v, t));
-  if (t == (uint32_t)RL) return v;
-  return w_mask(v, (int)t - RL);
 }
 
 template <int K>
@@ -596,7 +581,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
            cxy, cqn};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
-  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, wk.start + q)); });
+  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, mm_locate<K>(wk.start + q))); });
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps

@@ -452,8 +452,9 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
       if ((rc = emit(e, st))) return rc;
   } else {
     // Three streams (DESIGN.md §4 "Schedule"). The RSA core depends only on the inputs, so it
-    // starts at once on its own (high-priority) stream; the bulk emitters (SHA, then BigMultModP,
-    // then BabyJubJub) run on the low-priority stream as their cores finish; the main
+    // starts at once on its own (high-priority) stream with the VALU-heavy BigMultModP emitter
+    // behind it, which then overlaps the bandwidth-bound SHA emitter (low-priority stream, with
+    // the BabyJubJub emitter after it); the main
     // (high-priority) stream runs the Poseidon/SMT dependency chain, the BabyJubJub core and the
     // remaining emitters, then joins.
     // PZK_SERIAL=1 (profiling): every phase on the launch stream, so kernel times are standalone
@@ -464,12 +465,12 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
       HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
     HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+    if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
+    HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
     { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
     HIPCHK(hipEventRecord(I->ev_sha, st));
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
-    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_rsa, 0));
-    if ((rc = emit(E_MM, s_sha))) return rc;
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
@@ -491,7 +492,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
       HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st)); }
     if ((rc = emit(E_BITS, st))) return rc;
     if ((rc = emit(E_GENR, st))) return rc;
-    HIPCHK(hipStreamWaitEvent(st, I->ev_j_bjj, 0));
+    for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));
   }
   if (user) {
     HIPCHK(hipEventRecord(I->ev_exit, st));

@@ -224,29 +224,36 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
   }
   __syncthreads();
   constexpr int NF = 7 * t, NR = NF + 1 + RP;
-  for (int row = tid; row < NR; row += nt) {
-    fr acc = fr_zero();
-    if (row < NF) {  // full mix f, output i: Mat_f[j][i] * ark[f][j]
+  // products, one per thread: row r, term k (full mix f, output i: Mat_f[k][i] * ark[f][k];
+  // mixLast: M[k][0] * x5[7][k]; partial r: S[(2t-1)r + k] * in_k, in_0 = the S-box's Ark output)
+  for (int q = tid; q < NR * t; q += nt) {
+    const int row = q / t, k = q - row * t;
+    fr c, v;
+    int dst;
+    if (row < NF) {
       const int f = row / t, i = row - f * t;
-#pragma unroll
-      for (int j = 0; j < t; j++) {
-        acc = fr_add(acc, fr_mul(f == 3 ? K.Pm(t, j, i) : K.M(t, j, i), img[I.ark + f * t + j]));
-        img[I.fs + row * t + j] = acc;
-      }
-    } else if (row == NF) {  // mixLast: M[j][0] * x5[7][j]
-#pragma unroll
-      for (int j = 0; j < t; j++) {
-        acc = fr_add(acc, fr_mul(K.M(t, j, 0), img[I.p5 + 7 * t + j]));
-        img[I.ls + j] = acc;
-      }
-    } else {  // partial r: S[(2t-1)r + i] * in_i, in_0 = ark output of the S-box
+      c = f == 3 ? K.Pm(t, k, i) : K.M(t, k, i);
+      v = img[I.ark + f * t + k];
+      dst = I.fs + row * t + k;
+    } else if (row == NF) {
+      c = K.M(t, k, 0);
+      v = img[I.p5 + 7 * t + k];
+      dst = I.ls + k;
+    } else {
       const int r = row - NF - 1;
-#pragma unroll
-      for (int i = 0; i < t; i++) {
-        acc = fr_add(acc, fr_mul(K.S(t, (2 * t - 1) * r + i), i == 0 ? img[I.pin0 + r] : img[I.pin + r * t + i]));
-        img[I.ps + r * t + i] = acc;
-      }
+      c = K.S(t, (2 * t - 1) * r + k);
+      v = k == 0 ? img[I.pin0 + r] : img[I.pin + r * t + k];
+      dst = I.ps + r * t + k;
     }
+    img[dst] = fr_mul(c, v);
+  }
+  __syncthreads();
+  // prefix sums along each row
+  for (int row = tid; row < NR; row += nt) {
+    const int base = row < NF ? I.fs + row * t : row == NF ? I.ls : I.ps + (row - NF - 1) * t;
+    fr acc = img[base];
+#pragma unroll
+    for (int k = 1; k < t; k++) { acc = fr_add(acc, img[base + k]); img[base + k] = acc; }
   }
   __syncthreads();
 }

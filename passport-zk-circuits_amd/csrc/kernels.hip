@@ -196,17 +196,35 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
   for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cum[i] = pc[i].cum;
   __syncthreads();
   uint8_t* row = B.wtns + (size_t)w * B.stride;
-  for (uint32_t q = threadIdx.x; q < wk.count; q += blockDim.x) {
-    uint32_t lo = 0, hi = np - 1;
-    while (lo < hi) {
-      uint32_t mid = (lo + hi + 1) >> 1;
-      if (cum[mid] <= q) lo = mid; else hi = mid - 1;
+  // two passes: every load of the thread's elements first, then every store. A load issued after
+  // a store waits for that store (gfx9 vmcnt counts both), which under a saturated write path
+  // would serialise each element on the store latency.
+  constexpr int PER = GEN_PACK / EMIT_THREADS;
+  El val[PER];
+  uint64_t dst[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t q = threadIdx.x + k * EMIT_THREADS;
+    dst[k] = ~0ull;
+    if (q < wk.count) {
+      uint32_t lo = 0, hi = np - 1;
+      while (lo < hi) {
+        uint32_t mid = (lo + hi + 1) >> 1;
+        if (cum[mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      const GenPiece p = pc[lo];
+      const Region& R = L.regions[p.region];
+      const uint32_t s = p.start + (q - cum[lo]);
+      val[k] = emit_small(L, B, R, w, s);
+      dst[k] = R.off + s;
     }
-    const GenPiece p = pc[lo];
-    const Region& R = L.regions[p.region];
-    const uint32_t s = p.start + (q - cum[lo]);
-    emit_small(L, B, R, w, s, row + 32ull * (R.off + s));
   }
+#pragma unroll
+  for (int k = 0; k < PER; k++)
+    if (dst[k] != ~0ull) {
+      uint4* d = reinterpret_cast<uint4*>(row + 32ull * dst[k]);
+      d[0] = val[k].lo; d[1] = val[k].hi;
+    }
 }
 
 // ------------------------------------------------------------------- launchers

@@ -62,23 +62,21 @@ __device__ __forceinline__ uint32_t digest_bit(const uint32_t* H, int i) { retur
 
 // ------------------------------------------------------------------ generic small regions
 // returns true and writes the element; the value source is per kind
-__device__ __forceinline__ void emit_small(const DevLayout& L, const Bufs& B, const Region& R, uint32_t w, uint32_t s,
-                                           uint8_t* dst) {
+__device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, const Region& R, uint32_t w, uint32_t s) {
   const RegInfo& G = L.reg;
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   const fr* smt = B.smt_core + (size_t)w * L.smt_core_fr;
   const uint32_t* flags = reinterpret_cast<const uint32_t*>(smt + 2 * SMT_LEVELS);
   auto V = [&](int slot) { return fr_from_mont(B.vs.at(slot, w)); };
   switch (R.kind) {
-    case RK_ONE: store_u64(dst, 1); return;
-    case RK_INCOPY: copy_el(dst, row + 32ull * ((uint64_t)R.a[0] + s)); return;
+    case RK_ONE: return el_u64(1);
+    case RK_INCOPY: return el_load(row + 32ull * ((uint64_t)R.a[0] + s));
     case RK_VALUE: {
       int slot = R.a[0] >= 0 ? R.a[0] + (int)s : R.a[0] == -2 ? -2 : R.a[1 + s];
-      if (slot < 0) store_u64(dst, 0);
-      else store_fr(dst, V(slot));
-      return;
+      if (slot < 0) return el_u64(0);
+      else return el_fr(V(slot));
     }
-    case RK_DIGEST: store_u64(dst, digest_bit(sha_hout(L, B, w, R.a[0]), (int)s)); return;
+    case RK_DIGEST: return el_u64(digest_bit(sha_hout(L, B, w, R.a[0]), (int)s));
     case RK_TEMPMOD: {
       const uint8_t* a = row + 32ull * (R.a[0] + 3 * s);
       const uint8_t* b = row + 32ull * (R.a[0] + 3 * s + 1);
@@ -86,107 +84,96 @@ __device__ __forceinline__ void emit_small(const DevLayout& L, const Bufs& B, co
         uint64_t la = in_u64(a), lb = in_u64(b);
         W256 r = w_zero();
         r.v[2] = (uint32_t)lb; r.v[3] = (uint32_t)(lb >> 32); r.v[4] = (uint32_t)la; r.v[5] = (uint32_t)(la >> 32);
-        store_w(dst, r);
+        return el_w(r);
       } else {
         fr t64 = fr_zero(); t64.v[2] = 1;
         fr t128 = fr_zero(); t128.v[4] = 1;
         fr v = fr_add(fr_mul(fr_to_mont(load_fr(a)), fr_to_mont(t128)), fr_mul(fr_to_mont(load_fr(b)), fr_to_mont(t64)));
-        store_fr(dst, fr_from_mont(v));
+        return el_fr(fr_from_mont(v));
       }
-      return;
     }
     case RK_HCHUNK: {
       const uint32_t* H = sha_hout(L, B, w, R.a[0]);
       int wd = 3 - (int)s;
-      store_u64(dst, ((uint64_t)H[2 * wd] << 32) | H[2 * wd + 1]);
-      return;
+      return el_u64(((uint64_t)H[2 * wd] << 32) | H[2 * wd + 1]);
     }
     case RK_RSA_OUT: {
       const uint64_t* mc = B.rsa_core + (size_t)w * L.rsa_core_words + (size_t)(G.n_modmul - 1) * MM_CORE_WORDS(G.K);
-      store_u64(dst, mc[3 * G.K + 1 + s]);
-      return;
+      return el_u64(mc[3 * G.K + 1 + s]);
     }
     case RK_SMT_OWN: {  // isVerified | root, leaf, key, siblings[80] | value
       if (s == 0) {
         fr r0 = fr_from_mont(smt[SMT_LEVELS]);
-        store_u64(dst, fr_eq(r0, load_fr(row + 32ull * R.a[0])) ? 1 : 0);
-      } else if (s == 1) copy_el(dst, row + 32ull * R.a[0]);
-      else if (s == 2 || s == 3 || s == 84) store_fr(dst, V(G.v_pkhash));
-      else copy_el(dst, row + 32ull * (R.a[1] + s - 4));
-      return;
+        return el_u64(fr_eq(r0, load_fr(row + 32ull * R.a[0])) ? 1 : 0);
+      } else if (s == 1) return el_load(row + 32ull * R.a[0]);
+      else if (s == 2 || s == 3 || s == 84) return el_fr(V(G.v_pkhash));
+      else return el_load(row + 32ull * (R.a[1] + s - 4));
     }
     case RK_SMTHASH: {
       int lv = R.a[0];
-      if (lv < 0) store_fr(dst, s == 0 ? V(G.v_leaf) : V(G.v_pkhash));
-      else store_fr(dst, s == 0 ? V(G.v_smt_h + lv) : V(G.v_smt_lr + 2 * lv + (int)s - 1));
-      return;
+      if (lv < 0) return el_fr(s == 0 ? V(G.v_leaf) : V(G.v_pkhash));
+      else return el_fr(s == 0 ? V(G.v_smt_h + lv) : V(G.v_smt_lr + 2 * lv + (int)s - 1));
     }
     case RK_LEVINS: {  // levIns[80] | siblings[80] | done[79] | isZero[80] (out, in, inv)
-      if (s < 80) { store_u64(dst, flags[s] & 1); return; }
-      if (s < 160) { copy_el(dst, row + 32ull * (R.a[0] + s - 80)); return; }
-      if (s < 239) { store_u64(dst, (flags[s - 160] >> 1) & 1); return; }
+      if (s < 80) { return el_u64(flags[s] & 1); }
+      if (s < 160) { return el_load(row + 32ull * (R.a[0] + s - 80)); }
+      if (s < 239) { return el_u64((flags[s - 160] >> 1) & 1); }
       uint32_t i = (s - 239) / 3, k = (s - 239) % 3;
-      if (k == 0) store_u64(dst, (flags[i] >> 5) & 1);
-      else if (k == 1) copy_el(dst, row + 32ull * (R.a[0] + i));
-      else store_fr(dst, smt[i]);
-      return;
+      if (k == 0) return el_u64((flags[i] >> 5) & 1);
+      else if (k == 1) return el_load(row + 32ull * (R.a[0] + i));
+      else return el_fr(smt[i]);
     }
     case RK_SM: {  // st_top, st_inew | levIns, prev_top
       uint32_t i = s >> 2, k = s & 3;
       uint32_t v = k == 0 ? (flags[i] >> 2) & 1 : k == 1 ? (flags[i] >> 3) & 1 : k == 2 ? flags[i] & 1
                                                                               : (i == 0 ? 1u : (flags[i - 1] >> 2) & 1);
-      store_u64(dst, v);
-      return;
+      return el_u64(v);
     }
     case RK_SMT_LEVEL: {  // root | st_top, st_inew, sibling, new1leaf, lrbit, child | fromProof
       int i = R.a[0];
       uint32_t f = flags[i];
       switch (s) {
-        case 0: store_fr(dst, fr_from_mont(smt[SMT_LEVELS + i])); break;
-        case 1: store_u64(dst, (f >> 2) & 1); break;
-        case 2: store_u64(dst, (f >> 3) & 1); break;
-        case 3: copy_el(dst, row + 32ull * (R.a[1] + i)); break;
-        case 4: store_fr(dst, V(G.v_leaf)); break;
-        case 5: store_u64(dst, (f >> 4) & 1); break;
-        case 6: store_fr(dst, i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1])); break;
-        default: store_fr(dst, (f & 4) ? V(G.v_smt_h + i) : fr_zero()); break;
+        case 0: return el_fr(fr_from_mont(smt[SMT_LEVELS + i]));
+        case 1: return el_u64((f >> 2) & 1);
+        case 2: return el_u64((f >> 3) & 1);
+        case 3: return el_load(row + 32ull * (R.a[1] + i));
+        case 4: return el_fr(V(G.v_leaf));
+        case 5: return el_u64((f >> 4) & 1);
+        case 6: return el_fr(i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1]));
+        default: return el_fr((f & 4) ? V(G.v_smt_h + i) : fr_zero());
       }
-      return;
     }
     case RK_SWITCHER: {  // out[2] | bool, in[2] | aux
       int i = R.a[0];
       uint32_t lr = (flags[i] >> 4) & 1;
-      if (s < 2) { store_fr(dst, V(G.v_smt_lr + 2 * i + (int)s)); return; }
-      if (s == 2) { store_u64(dst, lr); return; }
+      if (s < 2) { return el_fr(V(G.v_smt_lr + 2 * i + (int)s)); }
+      if (s == 2) { return el_u64(lr); }
       fr child = i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1]);
       fr sib = load_fr(row + 32ull * (R.a[1] + i));
-      if (s == 3) store_fr(dst, child);
-      else if (s == 4) copy_el(dst, row + 32ull * (R.a[1] + i));
-      else store_fr(dst, lr ? fr_sub(sib, child) : fr_zero());
-      return;
+      if (s == 3) return el_fr(child);
+      else if (s == 4) return el_load(row + 32ull * (R.a[1] + i));
+      else return el_fr(lr ? fr_sub(sib, child) : fr_zero());
     }
     case RK_ISEQ_ROOT: {  // out | in[2] | IsZero(out, in, inv)
       fr r0 = fr_from_mont(smt[SMT_LEVELS]);
       fr rin = load_fr(row + 32ull * R.a[0]);
       uint32_t eq = fr_eq(r0, rin);
-      if (s == 0 || s == 3) store_u64(dst, eq);
-      else if (s == 1) store_fr(dst, r0);
-      else if (s == 2) copy_el(dst, row + 32ull * R.a[0]);
-      else if (s == 4) store_fr(dst, fr_sub(rin, r0));
-      else store_fr(dst, fr_from_mont(smt[3 * SMT_LEVELS + 1]));
-      return;
+      if (s == 0 || s == 3) return el_u64(eq);
+      else if (s == 1) return el_fr(r0);
+      else if (s == 2) return el_load(row + 32ull * R.a[0]);
+      else if (s == 4) return el_fr(fr_sub(rin, r0));
+      else return el_fr(fr_from_mont(smt[3 * SMT_LEVELS + 1]));
     }
     case RK_BJJ_OWN: {  // out[2] | scalar | base8[2]
       const fr* bc = B.bjj_core + (size_t)w * L.bjj_core_fr + 5 * (BJJ_STEPS - 1);
-      if (s < 2) store_fr(dst, fr_from_mont(bc[2 + s]));
-      else if (s == 2) store_fr(dst, V(G.v_sk));
+      if (s < 2) return el_fr(fr_from_mont(bc[2 + s]));
+      else if (s == 2) return el_fr(V(G.v_sk));
       else {
         W256 r; for (int i = 0; i < 8; i++) r.v[i] = s == 3 ? BJJ_B8X[i] : BJJ_B8Y[i];
-        store_w(dst, r);
+        return el_w(r);
       }
-      return;
     }
-    default: store_u64(dst, 0); return;
+    default: return el_u64(0);
   }
 }
 
@@ -429,7 +416,7 @@ __device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
     }
     s -= 4 * N;
     int h = N / 2;
-    uint32_t cs = kara_size(h), c = s / cs;
+    const uint32_t cs = kara_size(h), c = s >= cs ? (s >= 2 * cs ? 2u : 1u) : 0u;  // child 0, 1, 2
     s -= c * cs;
     if (c == 1) O <<= h;
     else if (c == 2) O |= O << h;

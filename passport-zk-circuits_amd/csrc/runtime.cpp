@@ -484,9 +484,9 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     if ((rc = emit(E_BJJ, s_sha))) return rc;
     HIPCHK(hipEventRecord(I->ev_j_bjj, s_sha));
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
+    if ((rc = emit(E_POS, st))) return rc;
     if ((rc = emit(E_GEN, st))) return rc;
     if ((rc = emit(E_FLOW, st))) return rc;
-    if ((rc = emit(E_POS, st))) return rc;
     HIPCHK(hipStreamWaitEvent(st, I->ev_rsa, 0));
     { PhaseScope ps(T, slot, PH_PREP, st);
       HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st)); }

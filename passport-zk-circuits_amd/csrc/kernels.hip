@@ -95,11 +95,14 @@ __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t*
 }
 
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
-                                                          const uint32_t* sha_core, uint8_t* wtns, size_t stride) {
+                                                          const uint32_t* sha_core, uint8_t* wtns, size_t stride,
+                                                          int wit_major) {
   __shared__ uint32_t core[SHA_BLOCK_CORE + 8 * 17];
   __shared__ __attribute__((aligned(16))) uint64_t wt[SHA_WT_SIZE];
-  const Work wk = work[blockIdx.x];
-  const uint32_t w = blockIdx.y;
+  // grid (witness, chunk): the blocks in flight together work on the same chunk of different
+  // witnesses, so they share its slice of the block program in L2
+  const Work wk = work[wit_major ? blockIdx.y : blockIdx.x];
+  const uint32_t w = wit_major ? blockIdx.x : blockIdx.y;
   const Region R = L.regions[wk.region];
   const ShaJob job = L.sha[R.a[0]];
   const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
@@ -354,7 +357,13 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
-    case E_SHA: hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride); break;
+    case E_SHA: {
+      static const int wm = getenv("PZK_SHA_GRID") ? atoi(getenv("PZK_SHA_GRID")) : 1;
+      if (wm) hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns,
+                                 B.stride, 1);
+      else hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride, 0);
+      break;
+    }
     case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
       switch (max_t) {
         case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;

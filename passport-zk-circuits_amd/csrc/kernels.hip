@@ -357,13 +357,9 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
-    case E_SHA: {
-      static const int wm = getenv("PZK_SHA_GRID") ? atoi(getenv("PZK_SHA_GRID")) : 1;
-      if (wm) hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns,
-                                 B.stride, 1);
-      else hipLaunchKernelGGL(k_emit_sha, g, blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride, 0);
+    case E_SHA:  // witness-major grid (see k_emit_sha)
+      hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride, 1);
       break;
-    }
     case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
       switch (max_t) {
         case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;

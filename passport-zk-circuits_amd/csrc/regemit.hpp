@@ -344,10 +344,18 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
 }
 
 // ------------------------------------------------------------------ BigMultModP
+// Karatsuba input table (K = 32): the in1/in2 values of every non-root KaratsubaOverflow node
+// (bigIntHelpers.circom:11-53), level by level; node m of level l holds in1[N_l] then in2[N_l],
+// N_l = K >> l. A value is a sum of up to 2^l limbs: lo 64 bits + a small high part. Level l
+// starts at value kt_base(l) = sum_{i<l} 3^i 2 N_i (i >= 1): 0, 96, 240, 456, 780; 1266 in all.
+constexpr int KT_K = 32, KT_LEVELS = 5, KT_VALUES = 1266;
+
 struct MMCore {
   int K;
   const uint64_t *x, *y, *q, *r, *n, *inv, *cr;  // LDS
   const uint64_t *cxy, *cqn;                      // LDS: column sums of x*y (2K-1) and q*n (2K), 3 words each
+  const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32; else null)
+  const uint8_t* kt_hi;
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
 };
 __device__ __forceinline__ U192 u192_at(const uint64_t* a, int i) { U192 r; r.a0 = a[3 * i]; r.a1 = a[3 * i + 1]; r.a2 = a[3 * i + 2]; return r; }
@@ -390,27 +398,37 @@ __host__ __device__ inline uint32_t kara_size(int N) {
   }
 }
 
-// Karatsuba subtree signal (bigIntHelpers.circom:11-53)
+// Karatsuba subtree signal (bigIntHelpers.circom:11-53). A node's out[] is the convolution of
+// its inputs: at the root that is the x*y column sums (LDS); below it, products of the node's
+// input values from the table (K = 32) or sums over the node's limb offsets (K = 64).
 __device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
   uint64_t O = 1;  // offsets set (bit o = offset o)
+  int lvl = 0, m = 0, p3 = 1, base = 0;  // level, node index in level, 3^lvl, table start of the level
   for (;;) {
+    const int tb = C.kt_lo && lvl > 0 ? base + m * 2 * N : -1;  // this node's table slice
     if (s < (uint32_t)(2 * N)) {
       if (s == (uint32_t)(2 * N - 1)) return w_zero();  // top coefficient (K(1).out[1] never assigned)
-      if (N == C.K) return u192w(u192_at(C.cxy, (int)s));  // root: the plain x*y convolution
+      if (lvl == 0) return u192w(u192_at(C.cxy, (int)s));
       U192 acc;
       int lo = s < (uint32_t)N ? 0 : (int)s - N + 1, hi = s < (uint32_t)N ? (int)s : N - 1;
       for (int u = lo; u <= hi; u++) {
         uint64_t al, ah, bl, bh;
-        kara_in(C.x, O, u, al, ah);
-        kara_in(C.y, O, (int)s - u, bl, bh);
+        if (tb >= 0) {
+          al = C.kt_lo[tb + u]; ah = C.kt_hi[tb + u];
+          bl = C.kt_lo[tb + N + (int)s - u]; bh = C.kt_hi[tb + N + (int)s - u];
+        } else {
+          kara_in(C.x, O, u, al, ah);
+          kara_in(C.y, O, (int)s - u, bl, bh);
+        }
         mac2(acc, al, ah, bl, bh);
       }
       return u192w(acc);
     }
     if (s < (uint32_t)(4 * N)) {
-      const uint64_t* a = s < (uint32_t)(3 * N) ? C.x : C.y;
+      const int k = (int)s - 2 * N;  // in1[0..N) then in2[0..N)
       uint64_t lo, hi;
-      kara_in(a, O, (int)(s - (s < (uint32_t)(3 * N) ? 2 * N : 3 * N)), lo, hi);
+      if (tb >= 0) { lo = C.kt_lo[tb + k]; hi = C.kt_hi[tb + k]; }
+      else kara_in(k < N ? C.x : C.y, O, k < N ? k : k - N, lo, hi);
       W256 r = w_zero(); r.v[0] = (uint32_t)lo; r.v[1] = (uint32_t)(lo >> 32); r.v[2] = (uint32_t)hi;
       return r;
     }
@@ -420,6 +438,10 @@ __device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
     s -= c * cs;
     if (c == 1) O <<= h;
     else if (c == 2) O |= O << h;
+    if (lvl > 0) base += p3 * 2 * N;
+    p3 *= 3;
+    m = 3 * m + (int)c;
+    lvl++;
     N = h;
   }
 }
@@ -564,8 +586,40 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
     }
   }
   __syncthreads();
+  // Karatsuba input table (K = 32), level by level: a child's operand is the parent's low half,
+  // high half, or their sum
+  constexpr int KTN = K == KT_K ? KT_VALUES : 1;
+  __shared__ uint64_t kt_lo[KTN];
+  __shared__ uint8_t kt_hi[KTN];
+  if (K == KT_K) {
+    int base = 0, pbase = 0, nodes = 3;
+    for (int l = 1; l <= KT_LEVELS; l++) {
+      const int N = K >> l, cnt = nodes * 2 * N;
+      for (int r = threadIdx.x; r < cnt; r += blockDim.x) {
+        const int m = r / (2 * N), k = r - m * 2 * N, op = k >= N, u = k - op * N, p = m / 3, c = m - 3 * p;
+        uint64_t alo, ahi, blo = 0, bhi = 0;
+        if (l == 1) {
+          const uint64_t* src = op ? lds + K : lds;  // x or y
+          alo = src[u]; ahi = 0; if (c != 0) { blo = src[u + N]; bhi = 0; }
+        } else {
+          const int pi = pbase + p * 4 * N + op * 2 * N + u;  // parent node: in1[2N] then in2[2N]
+          alo = kt_lo[pi]; ahi = kt_hi[pi];
+          if (c != 0) { blo = kt_lo[pi + N]; bhi = kt_hi[pi + N]; }
+        }
+        uint64_t lo, hi;
+        if (c == 0) { lo = alo; hi = ahi; }
+        else if (c == 1) { lo = blo; hi = bhi; }
+        else { lo = alo + blo; hi = ahi + bhi + (lo < alo); }
+        kt_lo[base + r] = lo; kt_hi[base + r] = (uint8_t)hi;
+      }
+      __syncthreads();
+      pbase = base;
+      base += cnt;
+      nodes *= 3;
+    }
+  }
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
-           cxy, cqn};
+           cxy, cqn, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, mm_locate<K>(wk.start + q))); });

@@ -290,7 +290,6 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   // workgroups, the dispatcher hands freed CU slots to the latency-bound chain kernels first.
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (getenv("PZK_NO_PRIO")) prio_hi = prio_lo;  // A/B switch for scheduling experiments
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess;

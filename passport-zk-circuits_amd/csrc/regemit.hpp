@@ -655,8 +655,10 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
     }
   }
   __syncthreads();
+  // value-major item order: the lanes of a wave compute the same record value for consecutive
+  // steps (one or two branches of the switch per wave instead of all twelve)
   for (int q = threadIdx.x; q < nrec * BR_N; q += blockDim.x) {
-    const int j = q / BR_N, v = q - j * BR_N, i = base + j;
+    const int v = q / nrec, j = q - v * nrec, i = base + j;
     const fr* P = core + 5 * i;
     fr r;
     if (v >= BR_XYD) {  // doubler of step i (doublers[i-1]) over A_{i-1}
@@ -684,7 +686,7 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
         default: r = fr_mul(fr_mul(x1, y2), fr_mul(y1, x2)); break;
       }
     }
-    rec[q] = fr_from_mont(r);
+    rec[j * BR_N + v] = fr_from_mont(r);
   }
   __syncthreads();
   const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);

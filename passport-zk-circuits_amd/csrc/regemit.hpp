@@ -622,7 +622,14 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
            cxy, cqn, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
-  emit_run(out, wk.count, stage, [&](uint32_t q) { return el_w(mm_sig(C, mm_locate<K>(wk.start + q))); });
+  // section by section: every wave works inside one section (uniform branch), and each section
+  // starts wave-aligned, so a tmpResult row never straddles the start of a wave (K = 32: two rows
+  // per wave; K = 64: one)
+  constexpr MMStarts S = mm_starts(K);
+  for (int sec = 0; sec < (int)MM_SECTIONS; sec++) {
+    const uint32_t a = S.v[sec], n = S.v[sec + 1] - a;
+    emit_run(out + 32ull * a, n, stage, [&](uint32_t q) { return el_w(mm_sig(C, ((uint32_t)sec << 24) | q)); });
+  }
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps

@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "build", "liboracle.so")
 POSEIDON_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "poseidon_t2_6.bin")
+P256_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "p256_gpow8.bin")
 
 P = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
@@ -51,6 +52,10 @@ def lib():
         rc = L.orc_load_poseidon(POSEIDON_BIN.encode())
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
+        L.orc_load_p256.argtypes = [ctypes.c_char_p]
+        rc = L.orc_load_p256(P256_BIN.encode())
+        if rc != 0:
+            raise RuntimeError("oracle: cannot load the P-256 generator table (%d)" % rc)
         _lib = L
     return _lib
 

@@ -51,6 +51,8 @@ enum {
   S_BIGISZERO = 12,      /* bigIntComparators.circom:128 */
   S_SMT_LAST = 13,       /* SMTVerifier.circom:54 */
   S_BJJ_ADD = 14,        /* babyjubjub/curve.circom:98,102 */
+  S_ECDSA_INV = 15,      /* bigInt.circom:364-368  in * inv mod n === 1 */
+  S_ECDSA_R = 16,        /* ecdsa.circom:81-83  x1 mod n === r */
 };
 
 /* ------------------------------------------------------------- fr helpers */
@@ -949,6 +951,8 @@ static void run_verifysig(ctx_t *c, size_t b, int K) {
   run_rsa(c, rsa, K, 65537);
 }
 
+#include "ecdsa_p256.inc.c"
+
 /* ======================================================== SMT (depth 80) */
 static size_t sz_smthash1(void) { return 3 + sz_poseidon(3); }
 static size_t sz_smthash2(void) { return 3 + sz_poseidon(2); }
@@ -1049,27 +1053,31 @@ static void run_flow(ctx_t *c, size_t b, int ecLen, int dg1s, int dg15s, int ecs
 
 /* ============================================ PassportVerificationBuilder */
 static int sig_chunks(int sig) { return sig == 2 ? 64 : 32; }
+/* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
+static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
 
 static size_t sz_pvb(const orc_params *P) {
-  int K = sig_chunks(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512;
-  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 256 * 4 + 1 + 5;
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, ec = P->sig >= 20;
+  /* own: ..., pubkeyHash, then tempModulus[5] (RSA, :184) or ecBitsX[256], ecBitsY[256] (ECDSA, :197-198) */
+  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 256 * 4 + 1 + (ec ? 512 : 5);
+  size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   return own + sz_shahash(2) + (P->aa ? sz_shahash(P->dg15_blocks) : 0) + sz_shahash(P->ec_blocks) + sz_shahash(2) +
-         sz_flow(ecLen) + sz_verifysig(K) + sz_bits2num(252) + sz_poseidon(5) + sz_smt(80) + sz_poseidon(1);
+         sz_flow(ecLen) + (ec ? sz_verifysig_ec() : sz_verifysig(K)) + sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
-  int K = sig_chunks(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512;
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, isec = P->sig >= 20;
   size_t ec = b + 1, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
          br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + 256, ecH = dg15H + 256, saH = ecH + 256,
          pkHash = saH + 256, tmpMod = pkHash + 1;
-  size_t p = tmpMod + 5;
+  size_t p = tmpMod + (isec ? 512 : 5);
   size_t hDg1 = p; p += sz_shahash(2);
   size_t hDg15 = 0; if (P->aa) { hDg15 = p; p += sz_shahash(P->dg15_blocks); }
   size_t hEc = p; p += sz_shahash(P->ec_blocks);
   size_t hSa = p; p += sz_shahash(2);
   size_t flow = p; p += sz_flow(ecLen);
-  size_t vs = p; p += sz_verifysig(K);
+  size_t vs = p; p += isec ? sz_verifysig_ec() : sz_verifysig(K);
   size_t saNum = p; p += sz_bits2num(252);
-  size_t pkH = p; p += sz_poseidon(5);
+  size_t pkH = p; p += isec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   size_t smt = p; p += sz_smt(80);
   size_t saHH = p;
   /* hashes */
@@ -1102,17 +1110,33 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   /* signature */
   for (int i = 0; i < K; i++) { W(vs + K + i) = W(sig + i); W(vs + i) = W(pk + i); }
   for (int i = 0; i < 256; i++) W(vs + 2 * K + i) = W(saH + i);
-  run_verifysig(c, vs, K);
+  if (isec) run_verifysig_ec(c, vs);
+  else run_verifysig(c, vs, K);
   /* passportHash bits */
   for (int i = 0; i < 252; i++) W(saNum + 1 + i) = W(saH + i);
   run_bits2num(c, saNum, 252);
-  /* RSA pubkey hash */
-  for (int i = 0; i < 5; i++) {
-    W(tmpMod + i) = fr_add(fr_mul(W(pk + 3 * i), POW2[128]), fr_mul(W(pk + 3 * i + 1), POW2[64]));
-    W(pkH + 1 + i) = fr_add(W(tmpMod + i), W(pk + 3 * i + 2));
+  if (!isec) { /* RSA pubkey hash (:182-191) */
+    for (int i = 0; i < 5; i++) {
+      W(tmpMod + i) = fr_add(fr_mul(W(pk + 3 * i), POW2[128]), fr_mul(W(pk + 3 * i + 1), POW2[64]));
+      W(pkH + 1 + i) = fr_add(W(tmpMod + i), W(pk + 3 * i + 2));
+    }
+    run_poseidon(c, pkH, 5);
+    W(pkHash) = W(pkH);
+  } else { /* ECDSA pubkey hash (:193-230): Poseidon2 of the low 248 bits of x and y */
+    size_t bx = tmpMod, by = bx + 256, n2b = pkH, per = sz_num2bits(64);
+    size_t xn = n2b + 8 * per, yn = xn + sz_bits2num(248), ph = yn + sz_bits2num(248);
+    for (int i = 0; i < 4; i++) {
+      size_t nx = n2b + (size_t)(2 * i) * per, ny = nx + per;
+      W(nx + 64) = W(pk + i); run_num2bits(c, nx, 64);
+      W(ny + 64) = W(pk + 4 + i); run_num2bits(c, ny, 64);
+      for (int j = 0; j < 64; j++) { W(bx + 255 - j - 64 * i) = W(nx + j); W(by + 255 - j - 64 * i) = W(ny + j); }
+    }
+    for (int i = 0; i < 248; i++) { W(xn + 1 + 247 - i) = W(bx + i + 8); W(yn + 1 + 247 - i) = W(by + i + 8); }
+    run_bits2num(c, xn, 248); run_bits2num(c, yn, 248);
+    W(ph + 1) = W(xn); W(ph + 2) = W(yn);
+    run_poseidon(c, ph, 2);
+    W(pkHash) = W(ph);
   }
-  run_poseidon(c, pkH, 5);
-  W(pkHash) = W(pkH);
   /* SMT */
   W(smt + 1) = W(root); W(smt + 2) = W(pkHash); W(smt + 3) = W(pkHash);
   for (int i = 0; i < 80; i++) W(smt + 4 + i) = W(br + i);
@@ -1183,12 +1207,12 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa == 0 || P->aa == 1) &&
+  return (P->sig == 1 || P->sig == 2 || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa == 0 || P->aa == 1) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 
 size_t orc_register_n_inputs(const orc_params *P) {
-  int K = sig_chunks(P->sig);
+  int K = sig_len(P->sig);
   return 1 + (size_t)P->ec_blocks * 512 + 1024 + (size_t)P->dg15_blocks * 512 + 1024 + 2 * K + 80 + 1;
 }
 size_t orc_register_witness_size(const orc_params *P) {
@@ -1207,7 +1231,7 @@ int orc_register_witness(const orc_params *P, const uint8_t *inputs, uint8_t *wi
   memset(wit, 0, nW * 32);
   W(0) = ONE();
   memcpy(&W(5), inputs, nIn * 32);
-  int K = sig_chunks(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512;
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512;
   size_t root = 5, ec = 6, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
          br = pk + K, sk = br + 80;
   size_t pvb = 5 + nIn, rid = pvb + sz_pvb(P);

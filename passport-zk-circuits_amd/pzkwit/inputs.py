@@ -100,6 +100,78 @@ def pkcs1v15_sha256_sign(key: RsaKey, msg: bytes) -> int:
     return key.sign_raw(int.from_bytes(em, "big"))
 
 
+# -------------------------------------------------------------- ECDSA P-256 (synthetic)
+# secp256r1 (signatureVerification.circom:177-182 passes its A, B, P as 4 x 64-bit limbs)
+P256_P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
+P256_A = P256_P - 3
+P256_N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+P256_G = (0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+          0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)
+
+
+def p256_add(p1, p2):
+    """Affine addition (None = point at infinity)."""
+    if p1 is None:
+        return p2
+    if p2 is None:
+        return p1
+    (x1, y1), (x2, y2) = p1, p2
+    if x1 == x2:
+        if (y1 + y2) % P256_P == 0:
+            return None
+        lam = (3 * x1 * x1 + P256_A) * pow(2 * y1, -1, P256_P) % P256_P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, P256_P) % P256_P
+    x3 = (lam * lam - x1 - x2) % P256_P
+    return x3, (lam * (x1 - x3) - y1) % P256_P
+
+
+def p256_mul(k, pt=P256_G):
+    r = None
+    for i in reversed(range(k.bit_length())):
+        r = p256_add(r, r)
+        if (k >> i) & 1:
+            r = p256_add(r, pt)
+    return r
+
+
+class EcKey:
+    """P-256 signer key (ECDSA, SIG 20)."""
+
+    def __init__(self, rng):
+        self.d = 1 + rng.below(P256_N - 1)
+        self.q = p256_mul(self.d)
+        self.n = self.q  # the "pubkey" of the passport dict: (x, y)
+
+    def sign(self, msg: bytes, rng):
+        """ECDSA-SHA256 (r, s); h = the digest as an integer, not reduced (ecdsa.circom:30-38)."""
+        h = int.from_bytes(hashlib.sha256(msg).digest(), "big")
+        while True:
+            k = 1 + rng.below(P256_N - 1)
+            r = p256_mul(k)[0] % P256_N
+            s = pow(k, -1, P256_N) * (h + r * self.d) % P256_N
+            if r and s:
+                return r, s
+
+
+def ecdsa_pk_hash(q):
+    """Poseidon2 of the low 248 bits of x and y (passportVerificationBuilder.circom:193-230)."""
+    m = (1 << 248) - 1
+    return poseidon([q[0] & m, q[1] & m])
+
+
+def sig_input_len(sig):
+    """signature / pubkey input lengths (registerIdentityBuilder.circom:131-140)."""
+    return 8 if sig >= 20 else 64 if sig == 2 else 32
+
+
+def sig_limbs(v, sig):
+    """RSA: integer -> K limbs; ECDSA: (a, b) -> 4 + 4 limbs (process_passport.js:125-135)."""
+    if sig >= 20:
+        return chunk_limbs(v[0], 64, 4) + chunk_limbs(v[1], 64, 4)
+    return chunk_limbs(v, 64, sig_input_len(sig))
+
+
 # ------------------------------------------------------------- synthetic passports
 CANONICAL = dict(sig=1, dg_hash=256, doc=3, ec_blocks=4, ec_shift=600, dg1_shift=248, aa=1,
                  dg15_shift=1496, dg15_blocks=3, aa_shift=256)  # hardhat.config.ts:30
@@ -122,7 +194,8 @@ def _dg15_rsa1024(rng):
 
 def _keygen(args):
     seed, k, bits = args
-    return RsaKey(bits, SplitMix64((seed << 32) ^ (0x4B455900 + k)))
+    rng = SplitMix64((seed << 32) ^ (0x4B455900 + k))
+    return EcKey(rng) if bits == "p256" else RsaKey(bits, rng)
 
 
 class PassportGen:
@@ -137,6 +210,10 @@ class PassportGen:
         self.seed = seed
         self.rng = SplitMix64(seed)
         self.params = dict(CANONICAL if params is None else params)
+        if self.params["sig"] >= 20:
+            key_bits = "p256"
+        elif self.params["sig"] == 2 and key_bits == 2048:
+            key_bits = 4096
         jobs = [(seed, k, key_bits) for k in range(n_keys)]
         workers = workers or min(16, os.cpu_count() or 1)
         if n_keys >= 8 and workers > 1:
@@ -157,7 +234,7 @@ class PassportGen:
     @property
     def n_inputs(self):
         pr = self.params
-        K = 64 if pr["sig"] == 2 else 32
+        K = sig_input_len(pr["sig"])
         return 1 + pr["ec_blocks"] * 512 + 1024 + pr["dg15_blocks"] * 512 + 1024 + 2 * K + 80 + 1
 
     def passport_at(self, i, smt_depth=0):
@@ -170,11 +247,15 @@ class PassportGen:
             self.rng = saved
 
     def pk_hash(self, key):
-        """RSA pubkey hash = Poseidon5 of 5 x 192-bit limb triples (passportVerificationBuilder.circom:182-191)."""
+        """RSA pubkey hash = Poseidon5 of 5 x 192-bit limb triples (passportVerificationBuilder.circom:182-191);
+        ECDSA: ecdsa_pk_hash."""
         h = self._pkhash.get(key.n)
         if h is None:
-            a = chunk_limbs(key.n, 64, 15)
-            h = poseidon([(a[3 * i] << 128) + (a[3 * i + 1] << 64) + a[3 * i + 2] for i in range(5)])
+            if isinstance(key, EcKey):
+                h = ecdsa_pk_hash(key.q)
+            else:
+                a = chunk_limbs(key.n, 64, 15)
+                h = poseidon([(a[3 * i] << 128) + (a[3 * i + 1] << 64) + a[3 * i + 2] for i in range(5)])
             self._pkhash[key.n] = h
         return h
 
@@ -201,7 +282,7 @@ class PassportGen:
         sa[sa_shift - 2:sa_shift] = b"\x04\x20"
         sa[sa_shift:sa_shift + 32] = hashlib.sha256(ec).digest()
         sa = bytes(sa)
-        sig = pkcs1v15_sha256_sign(key, sa)
+        sig = key.sign(sa, rng) if isinstance(key, EcKey) else pkcs1v15_sha256_sign(key, sa)
         sk = int.from_bytes(hashlib.sha256(ec).digest()[:31], "big")  # getFakeIdenData :630
         pkh = self.pk_hash(key)
         siblings = [0] * 80
@@ -220,7 +301,7 @@ class PassportGen:
 
 def passport_json(pp, params=CANONICAL):
     """The reference's input JSON (writeToJson, process_passport.js:659-672)."""
-    K = 64 if params["sig"] == 2 else 32
+    sg = params["sig"]
 
     def bits(b, nbits):
         arr = bits_msb_first(sha_pad(b, 512))
@@ -232,8 +313,8 @@ def passport_json(pp, params=CANONICAL):
         "dg15": bits(pp["dg15"], params["dg15_blocks"] * 512),
         "signedAttributes": bits(pp["sa"], 1024),
         "encapsulatedContent": bits(pp["ec"], params["ec_blocks"] * 512),
-        "pubkey": [str(x) for x in chunk_limbs(pp["n"], 64, K)],
-        "signature": [str(x) for x in chunk_limbs(pp["sig"], 64, K)],
+        "pubkey": [str(x) for x in sig_limbs(pp["n"], sg)],
+        "signature": [str(x) for x in sig_limbs(pp["sig"], sg)],
         "skIdentity": hex(pp["sk"]),
         "slaveMerkleRoot": hex(pp["root"] or 0),
         "slaveMerkleInclusionBranches": [str(x) for x in pp["siblings"]],
@@ -244,7 +325,7 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
     """Flat input buffer in witness order: slaveMerkleRoot, encapsulatedContent, dg1, dg15,
     signedAttributes, signature, pubkey, slaveMerkleInclusionBranches, skIdentity
     (registerIdentityBuilder.circom:143-152, public input first). -> (nIn, 32) uint8."""
-    K = 64 if params["sig"] == 2 else 32
+    K = sig_input_len(params["sig"])
     ecL, d15L = params["ec_blocks"] * 512, params["dg15_blocks"] * 512
     n_in = 1 + ecL + 1024 + d15L + 1024 + 2 * K + 80 + 1
     buf = out if out is not None else np.zeros((n_in, 32), dtype=np.uint8)
@@ -275,8 +356,8 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
     put_bits(pp["dg1"], 1024)
     put_bits(pp["dg15"], d15L)
     put_bits(pp["sa"], 1024)
-    put_u64s(chunk_limbs(pp["sig"], 64, K))
-    put_u64s(chunk_limbs(pp["n"], 64, K))
+    put_u64s(sig_limbs(pp["sig"], params["sig"]))
+    put_u64s(sig_limbs(pp["n"], params["sig"]))
     for s in pp["siblings"]:
         put_int(s)
     put_int(pp["sk"])

@@ -115,3 +115,70 @@ def test_smt_last_sibling_must_be_zero(oracle, passports):
     pp["siblings"] = [0] * 79 + [7]
     rc, _ = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
     assert rc == 13  # SMTVerifier.circom:54
+
+
+# ------------------------------------------------ ECDSA secp256r1 (SIGNATURE_TYPE 20)
+ECDSA = dict(I.CANONICAL, sig=20)
+
+
+@pytest.fixture(scope="module")
+def ec_passports():
+    g = I.PassportGen(seed=5, n_keys=2, params=ECDSA, workers=1)
+    return [g.passport_at(i) for i in range(3)]
+
+
+def _pk_hash_offset(params):
+    """PassportVerificationBuilder.pubkeyHash: after its passportHash, inputs (ec, dg1, dg15, sa,
+    signature, pubkey, branches, root) and dg1/dg15/ec/sa hashes (passportVerificationBuilder.circom:89-109)."""
+    nin = 1 + params["ec_blocks"] * 512 + 1024 + params["dg15_blocks"] * 512 + 1024 + 16 + 80 + 1
+    pvb = 5 + nin
+    return pvb + 1 + (nin - 1) + 4 * 256
+
+
+def test_p256_generator_table_is_pinned():
+    """data/p256_gpow8.bin (extracted from ec/powers/p256pows.circom) = j * 2^(8i) * G."""
+    t = np.fromfile(os.path.join(os.path.dirname(__file__), "..", "passport-zk-circuits_amd", "data",
+                                 "p256_gpow8.bin"), dtype="<u8").reshape(32, 256, 2, 4)
+    rng = np.random.default_rng(7)
+    for i, j in [(0, 1), (0, 255), (31, 1), (31, 255)] + [tuple(int(v) for v in x) for x in rng.integers([0, 1], [32, 256], (6, 2))]:
+        pt = I.p256_mul(j << (8 * i))
+        got = [sum(int(t[i, j, a, k]) << (64 * k) for k in range(4)) for a in range(2)]
+        assert got == list(pt), (i, j)
+    assert not t[:, 0].any()
+
+
+def test_ecdsa_oracle_verifies_and_public_outputs(oracle, ec_passports):
+    from refmath import aa_rsa_hash, bjj_mul, dg1_commitment
+    prm = oracle.register_params(**ECDSA)
+    nin, nw = oracle.register_sizes(prm)
+    assert nin == 5730
+    off = _pk_hash_offset(ECDSA)
+    for pp in ec_passports:
+        rc, w = oracle.register_witness(prm, I.pack_register_inputs(pp, ECDSA))
+        assert rc == 0
+        v = [oracle.from_elem(w[i]) for i in range(6)]
+        assert v[1] == aa_rsa_hash(pp["dg15"], 256)
+        sah = hashlib.sha256(pp["sa"]).digest()
+        hb = [(sah[i // 8] >> (7 - i % 8)) & 1 for i in range(256)]
+        assert v[2] == field.poseidon([sum(hb[i] << i for i in range(252))])
+        assert v[3] == dg1_commitment(pp["dg1"], pp["sk"])
+        assert v[4] == field.poseidon(list(bjj_mul(pp["sk"])))
+        assert oracle.from_elem(w[off]) == I.ecdsa_pk_hash(pp["n"]) == pp["pk_hash"]
+
+
+def test_ecdsa_oracle_rejects_bad_signature(oracle, ec_passports):
+    pp = dict(ec_passports[0])
+    r, s = pp["sig"]
+    pp["sig"] = (r, (s + 1) % I.P256_N)
+    rc, _ = oracle.register_witness(oracle.register_params(**ECDSA), I.pack_register_inputs(pp, ECDSA))
+    assert rc == 16  # ecdsa.circom:81-83  x1 mod n === r
+
+
+def test_ecdsa_oracle_rejects_off_curve_key(oracle, ec_passports):
+    pp = dict(ec_passports[0])
+    x, y = pp["n"]
+    pp["n"] = (x, (y + 1) % I.P256_P)
+    rc, _ = oracle.register_witness(oracle.register_params(**ECDSA), I.pack_register_inputs(pp, ECDSA))
+    # PointOnCurve of the first doubling: the non-exact carries of BigIntIsZero fail their
+    # Num2Bits range checks (bitify.circom:26) before the final `=== 0` (bigIntComparators.circom:128)
+    assert rc in (1, 12)

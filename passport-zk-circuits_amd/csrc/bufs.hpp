@@ -19,6 +19,11 @@ struct Bufs {
   uint8_t* wtns;
   size_t stride;
   int32_t* status;
+  // ECDSA (ec_common.hpp)
+  const uint64_t* ec_core;
+  const fr* ec_inv;       // IsEqual inverses, normal form
+  const uint8_t* ec_tab;  // value tables of the table ops
+  const fr* inv_small;    // 1/k mod p, k < 256, normal form
 };
 
 }  // namespace pzk

@@ -46,6 +46,13 @@ struct Layout {
   pzk_params params{};
   std::vector<int> out_slots;
   uint32_t rsa_core_words = 0, bjj_core_fr = 0, smt_core_fr = 0;
+  // ECDSA (SIGNATURE_TYPE 20)
+  bool is_ecdsa = false;
+  std::vector<uint32_t> ec_prog;      // per-type descriptor programs (ec_walk.hpp)
+  uint32_t ec_prog_off[3] = {}, ec_tab_n[3] = {};
+  std::vector<uint32_t> ec_tab_off;   // per table op
+  uint32_t ec_tab_entries = 0;
+  std::vector<int32_t> ec_ops[3];     // table ops per type (k_ec_table launches)
 };
 
 bool build_layout(const pzk_params& p, Layout& L, std::string& why);
@@ -58,7 +65,7 @@ inline uint32_t emit_chunk(int e) {
   snprintf(name, sizeof name, "PZK_CHUNK_%d", e);
   const char* v = getenv(name);
   if (v) return (uint32_t)atoi(v);
-  return e == E_MM ? (1u << 30) : EMIT_CHUNK;  // BigMultModP blocks: whole block per workgroup
+  return (e == E_MM || e == E_ECT) ? (1u << 30) : EMIT_CHUNK;  // whole block per workgroup
 }
 
 }  // namespace pzk

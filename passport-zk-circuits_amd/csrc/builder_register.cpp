@@ -24,6 +24,9 @@ uint32_t sz_bmneq(int G, int L) { return (G + L - 1) + G + L + G * L + (G + L - 
 
 }  // namespace
 
+bool ec_programs(Layout& L, std::string& why);
+void ec_verify_regions(Builder& b, int IN_PK, int IN_SIG, int J_SA);
+
 // BigMultModP(64,K,K,K) block size (bigInt.circom:206-272)
 uint32_t modmul_size(int K) {
   int BASE = 2 * K, DIV = K + 1, MAX = 128 + log_ceil(K + DIV - 1);
@@ -35,14 +38,16 @@ uint32_t modmul_size(int K) {
 }
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
-  if (p.signature_type != 1 && p.signature_type != 2) {
-    why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) + " not built yet (RSA PKCS#1 v1.5 types 1 and 2 are)";
+  if (p.signature_type != 1 && p.signature_type != 2 && p.signature_type != 20) {
+    why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
+          " not built yet (RSA PKCS#1 v1.5 types 1, 2 and ECDSA secp256r1 type 20 are)";
     return false;
   }
+  const bool ecdsa = p.signature_type == 20;
   if (p.dg_hash_type != 256) { why = "DG_HASH_TYPE must be 256 (SHA-256 chunks)"; return false; }
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
   if (p.aa_signature_algo != 0 && p.aa_signature_algo != 1) { why = "AA_SIGNATURE_ALGO must be 0 or 1"; return false; }
-  const int K = p.signature_type == 2 ? 64 : 32;
+  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : 32;  // signature / pubkey input length
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
@@ -77,6 +82,9 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   L.reg.in_dg15 = IN_DG15;
   L.reg.aa = aa ? 1 : 0;
   L.reg.aa_shift = p.aa_shift;
+  L.reg.ecdsa = ecdsa ? 1 : 0;
+  L.is_ecdsa = ecdsa;
+  if (ecdsa && !ec_programs(L, why)) return false;
 
   // ---- value-store slots that feed Poseidon tasks (filled by k_prep / core kernels)
   const int V_ONE = b.value();        // Montgomery 1 (SMTHash1 in[2])
@@ -90,6 +98,8 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   int V_L[80], V_R[80];
   for (int i = 0; i < 80; i++) { V_L[i] = b.value(); V_R[i] = b.value(); }
   L.loads.push_back(ValueLoad{V_SK, IN_SK});
+  const int V_PKX = b.value(), V_PKY = b.value();
+  L.reg.v_pkx = V_PKX; L.reg.v_pky = V_PKY;
   L.reg.v_one = V_ONE; L.reg.v_sk = V_SK; L.reg.v_pk = V_PK[0]; L.reg.v_aa = V_AA[0]; L.reg.v_dg1 = V_DG1[0];
   L.reg.v_sanum = V_SANUM; L.reg.v_bjj = V_BJJ_X; L.reg.v_smt_lr = V_L[0];
   L.reg.dg1_chunk = chunk;
@@ -124,7 +134,8 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   b.region(RK_DIGEST, 256, {J_EC});
   b.region(RK_DIGEST, 256, {J_SA});
   const uint32_t r_pkhash = b.region(RK_VALUE, 1, {-1});
-  b.region(RK_TEMPMOD, 5, {IN_PK});
+  if (ecdsa) b.region(RK_EC_PKBITS, 512, {IN_PK});  // ecBitsX[256], ecBitsY[256]
+  else b.region(RK_TEMPMOD, 5, {IN_PK});
   auto sha_blocks = [&](int job, int in_off, int blocks) {
     uint64_t own = 256 + 512ull * blocks + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
     b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1});
@@ -137,34 +148,51 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   // PassportVerificationFlow(ecLen, 256, 256, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA)
   b.region(RK_FLOW, 1 + 256 + 256 + ecLen + 256 + 1024 + 776 + 776 * SZ_ISEQUAL,
            {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, aa ? 1 : 0});
-  // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15
-  b.region(RK_INCOPY, K, {IN_PK});
-  b.region(RK_INCOPY, K, {IN_SIG});
-  b.region(RK_DIGEST, 256, {J_SA});
-  //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
-  b.region(RK_INCOPY, K, {IN_SIG});
-  b.region(RK_INCOPY, K, {IN_PK});
-  b.region(RK_DIGEST, 256, {J_SA});
-  b.region(RK_HCHUNK, 4, {J_SA});
-  //   PowerMod(64,K,65537): out[K] | base[K], modulus[K] | muls[16], resultMuls[1]
-  b.region(RK_RSA_OUT, K);
-  b.region(RK_INCOPY, K, {IN_SIG});
-  b.region(RK_INCOPY, K, {IN_PK});
-  const uint32_t mm = modmul_size(K);
-  L.reg.modmul_size = mm;
-  if (mm_section_start(K, MM_SECTIONS) != mm) { why = "internal: BigMultModP section sizes"; return false; }
-  // exp_to_bits(65537) = [16, 2, 0, 16]: muls[i] = muls[i-1]^2 (muls[0] = base^2); resultMuls[0] = base * muls[15]
-  L.reg.n_modmul = 17;
-  L.rsa_core_words = 17 * MM_CORE_WORDS(K);
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
-  for (int i = 0; i < 17; i++) b.region(RK_MODMUL, mm, {i, IN_PK});
-  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
-  b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
+  if (ecdsa) {
+    ec_verify_regions(b, IN_PK, IN_SIG, J_SA);
+  } else {
+    // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15
+    b.region(RK_INCOPY, K, {IN_PK});
+    b.region(RK_INCOPY, K, {IN_SIG});
+    b.region(RK_DIGEST, 256, {J_SA});
+    //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
+    b.region(RK_INCOPY, K, {IN_SIG});
+    b.region(RK_INCOPY, K, {IN_PK});
+    b.region(RK_DIGEST, 256, {J_SA});
+    b.region(RK_HCHUNK, 4, {J_SA});
+    //   PowerMod(64,K,65537): out[K] | base[K], modulus[K] | muls[16], resultMuls[1]
+    b.region(RK_RSA_OUT, K);
+    b.region(RK_INCOPY, K, {IN_SIG});
+    b.region(RK_INCOPY, K, {IN_PK});
+    const uint32_t mm = modmul_size(K);
+    L.reg.modmul_size = mm;
+    if (mm_section_start(K, MM_SECTIONS) != mm) { why = "internal: BigMultModP section sizes"; return false; }
+    // exp_to_bits(65537) = [16, 2, 0, 16]: muls[i] = muls[i-1]^2 (muls[0] = base^2); resultMuls[0] = base * muls[15]
+    L.reg.n_modmul = 17;
+    L.rsa_core_words = 17 * MM_CORE_WORDS(K);
+    for (int i = 0; i < 17; i++) b.region(RK_MODMUL, mm, {i, IN_PK});
+    for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
+    b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
+  }
   // signedAttributesNum = Bits2Num(252)(saHash[0..251])
   b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, 0, 1, J_SA});
-  // pubkeyHasherRsa = PoseidonHash(5)
-  const int S_PKH = b.poseidon(5, {V_PK[0], V_PK[1], V_PK[2], V_PK[3], V_PK[4]}, 0);
+  int S_PKH;
+  if (ecdsa) {
+    // num2bitsX[i], num2bitsY[i] (Num2Bits(64)), xToNum, yToNum (Bits2Num(248)), PoseidonHash(2)
+    // (passportVerificationBuilder.circom:193-230)
+    for (int i = 0; i < 4; i++) {
+      b.region(RK_EC_N2B, sz_num2bits(64), {1, IN_PK + i});
+      b.region(RK_EC_N2B, sz_num2bits(64), {1, IN_PK + 4 + i});
+    }
+    b.region(RK_EC_B2N248, sz_bits2num(248), {IN_PK});
+    b.region(RK_EC_B2N248, sz_bits2num(248), {IN_PK + 4});
+    S_PKH = b.poseidon(2, {V_PKX, V_PKY}, 0);
+  } else {
+    // pubkeyHasherRsa = PoseidonHash(5)
+    S_PKH = b.poseidon(5, {V_PK[0], V_PK[1], V_PK[2], V_PK[3], V_PK[4]}, 0);
+  }
   // ---- SMTVerifier(80): isVerified | root, leaf, key, siblings[80] | value
   //      | hash1New, n2bNew, smtLevIns, sm[80], levels[79..0], isEqual
   b.region(RK_SMT_OWN, 1 + 3 + 80 + 1, {IN_ROOT, IN_BR});

@@ -1,0 +1,105 @@
+// ECDSA secp256r1 (SIGNATURE_TYPE 20) path: constants, EC-op numbering and the per-witness
+// core layout shared by the host layout builder and the device kernels.
+//
+// verifyECDSABits (signatures/ecdsa.circom:18-87) evaluates 362 elliptic-curve point operations
+// per witness, every one a full template instance (EllipticCurveDouble / EllipticCurveAdd,
+// ec/curve.circom:281-345) whose PointOnCurve / PointOnTangent / PointOnLine sub-blocks hold
+// ~7-10 k signals. The path is split into
+//   * k_ec_core   — lane per witness: the scalars (s^-1, u1, u2 mod n) and the whole point chain in
+//                   Jacobian coordinates, then ONE batched inversion that yields every affine
+//                   point; writes an op RECORD (in1, in2, out) per point operation;
+//   * k_ec_table  — lane per (witness, op): the op's template walker (ec_walk.hpp) expands the
+//                   record into a VALUE TABLE (every distinct non-bit signal value, Fr normal form);
+//   * k_emit_ect  — workgroup per (witness, op): table -> LDS, then one u32 descriptor per signal
+//                   (COPY / BIT / MASK of a table entry), built once per op type on the host by the
+//                   same walker run symbolically.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pzk {
+
+// ---- curve constants, 64-bit limbs little-endian
+// A, B, P: signatureVerification.circom:179-182; order: ec/get.circom:155-156; dummy: get.circom:91-93
+#define PZK_EC_CONSTS                                                                                            \
+  constexpr uint64_t EC_A[4] = {18446744073709551612ull, 4294967295ull, 0ull, 18446744069414584321ull};        \
+  constexpr uint64_t EC_B[4] = {4309448131093880907ull, 7285987128567378166ull, 12964664127075681980ull,        \
+                                6540974713487397863ull};                                                        \
+  constexpr uint64_t EC_P[4] = {18446744073709551615ull, 4294967295ull, 0ull, 18446744069414584321ull};        \
+  constexpr uint64_t EC_N[4] = {17562291160714782033ull, 13611842547513532036ull, 18446744073709551615ull,      \
+                                18446744069414584320ull};                                                       \
+  constexpr uint64_t EC_D[8] = {4148137498610012746ull,  51237685452122967ull,   6555942389409504868ull,       \
+                                799804747332166731ull,   13395177781894339167ull, 1107697421929919296ull,      \
+                                6228258783500845564ull,  11862546499924939746ull};
+PZK_EC_CONSTS
+// constant limb i of curve constant id (RK_EC_CONST regions)
+enum { EC_K_A = 0, EC_K_B = 1, EC_K_P = 2, EC_K_ORDER = 3, EC_K_DUMMY = 4, EC_K_ONE = 5 };
+__host__ __device__ inline uint64_t ec_k(int id, int i) {
+  switch (id) {
+    case EC_K_A: return EC_A[i];
+    case EC_K_B: return EC_B[i];
+    case EC_K_P: return EC_P[i];
+    case EC_K_ORDER: return EC_N[i];
+    case EC_K_DUMMY: return EC_D[i];
+    default: return i == 0 ? 1 : 0;
+  }
+}
+
+// ---- EC point operations of one witness (fixed numbering, execution order of k_ec_core)
+constexpr int EC_OP_SD = 0;                                          // genmult getSecondDummy = 2 D (DBL)
+__host__ __device__ constexpr int ec_op_gm_add(int i) { return 1 + i; }            // genmult adders[i], i < 31
+__host__ __device__ constexpr int ec_op_pre(int i) { return 32 + (i - 2); }        // precompute out[i], i = 2..15
+__host__ __device__ constexpr int ec_op_sm_dbl(int d) { return 46 + (d / 4) * 5 + (d % 4); }  // doublers[d], d < 252
+__host__ __device__ constexpr int ec_op_sm_add(int a) { return 46 + a * 5 + 4; }   // scalarMult adders[a], a < 63
+constexpr int EC_OP_FINAL = 361;                                     // verifyECDSABits.add
+constexpr int EC_N_OPS = 362;
+__host__ __device__ constexpr bool ec_op_is_dbl(int op) {
+  return op == EC_OP_SD || (op >= 32 && op < 46 && (op - 32) % 2 == 0) || (op >= 46 && op < 361 && (op - 46) % 5 != 4);
+}
+// BigMultModP(64,4,4,4) instances (bigInt.circom:206-272): modInv.mult, mult, mult2, modOrder
+enum { EC_MM_INV = 0, EC_MM_U1 = 1, EC_MM_U2 = 2, EC_MM_XN = 3, EC_N_MM = 4 };
+
+// ---- per-witness EC core (u64 words)
+constexpr int ECC_SINV = 0, ECC_U1 = 4, ECC_U2 = 8, ECC_H = 12;
+constexpr int ECC_MM = 32;                      // [4] x (in1[4], in2[4])
+constexpr int ECC_GM_AP = 64;                   // genmult additionPoints[32][2][4]
+constexpr int ECC_GM_RP = ECC_GM_AP + 256;      // genmult resultingPoints[31][2][4]
+constexpr int ECC_PRE = ECC_GM_RP + 248;        // precompute out[16][2][4]
+constexpr int ECC_SM_AP = ECC_PRE + 128;        // scalarMult additionPoints[64][2][4]
+constexpr int ECC_SM_RP = ECC_SM_AP + 512;      // scalarMult resultingPoints[65][2][4]
+constexpr int ECC_REC = ECC_SM_RP + 520;        // op records: [362] x (in1[8], in2[8], out[8])
+constexpr int ECC_REC_WORDS = 24;
+constexpr int EC_CORE_WORDS = ECC_REC + EC_N_OPS * ECC_REC_WORDS;
+// IsEqual inverses (Fr normal form): genmult steps 4 per step (isFirst/SecondDummyLeft/Right),
+// scalarMult isZeroResult[64], isZeroAddition[1..63]
+constexpr int ECI_GM = 0, ECI_SM_ZR = 124, ECI_SM_ZA = 188, EC_N_INV = 251;
+// Jacobian scratch of k_ec_core per witness (u64): X, Y, Z per op + prefix products
+constexpr int EC_JAC_WORDS = EC_N_OPS * 16;
+
+// ---- table-block descriptor: op (3) | bit (9) | entry (20)
+enum : uint32_t { ECD_ZERO = 0, ECD_COPY = 1, ECD_BIT = 2, ECD_MASK = 3 };
+__host__ __device__ constexpr uint32_t ecd(uint32_t op, uint32_t idx, uint32_t bit = 0) {
+  return (op << 29) | (bit << 20) | idx;
+}
+enum EcType { ECT_DBL = 0, ECT_ADD = 1, ECT_MM = 2, ECT_N = 3 };
+
+// template sizes (ec/curve.circom; oracle/ecdsa_p256.inc.c derives them independently)
+__host__ __device__ constexpr uint32_t ec_n2b(int L) { return 2 * L + 1; }
+__host__ __device__ constexpr uint32_t ec_bmneq(int G, int L) { return (G + L - 1) + G + L + G * L + (G + L - 1) * L; }
+__host__ __device__ constexpr uint32_t ec_bmo(int G, int L) { return (G + L - 1) + G + L + ec_bmneq(G, L); }
+__host__ __device__ constexpr uint32_t ec_bisz(int MAX, int K) { return K + (K - 1) + (K - 1) * ec_n2b(MAX + 3 - 64); }
+__host__ __device__ constexpr uint32_t ec_bizmp(int MAX, int CN, int MCN) {
+  return CN + 4 + 1 + (MCN - 3) + (MCN - 3) * ec_n2b(64) + ec_bmo(MCN - 3, 4) + ec_bisz(MAX, MCN) + CN * 6;
+}
+constexpr uint32_t EC_SZ_PONCURVE = 8 + 3 * ec_bmo(4, 4) + ec_bmo(7, 4) + ec_bizmp(200, 10, 12);
+constexpr uint32_t EC_SZ_PONTANGENT = 16 + ec_bmo(4, 4) + 15 + 18 + 16 + ec_bmo(7, 4) + 9 + 12 + ec_bmo(4, 4) + ec_bizmp(200, 10, 13);
+constexpr uint32_t EC_SZ_PONLINE = 24 + 12 + 3 * 16 + 2 * ec_bmo(4, 4) + ec_bizmp(136, 7, 9);
+constexpr uint32_t EC_SZ_DBL = 16 + EC_SZ_PONTANGENT + EC_SZ_PONCURVE;
+constexpr uint32_t EC_SZ_ADD = 24 + EC_SZ_PONCURVE + EC_SZ_PONLINE;
+// BigMultModP(64,4,4,4): div[5], mod[4] | in1, in2, modulus | mult, modChecks[4], greaterThan, mult2, isZero
+constexpr uint32_t EC_SZ_BLET = 1 + 8 + 4 + 4 * ((3 + ec_n2b(65)) + 6);
+constexpr uint32_t EC_SZ_MM = 5 + 4 + 12 + ec_bmo(4, 4) + 4 * ec_n2b(64) + (1 + 8 + EC_SZ_BLET) + ec_bmneq(5, 4) + ec_bisz(132, 7);
+__host__ __device__ constexpr uint32_t ec_type_size(int t) { return t == ECT_DBL ? EC_SZ_DBL : t == ECT_ADD ? EC_SZ_ADD : EC_SZ_MM; }
+constexpr uint32_t EC_TABLE_MAX = 1024;   // table entries per op (checked by the host walker)
+
+}  // namespace pzk

@@ -1,0 +1,674 @@
+// ECDSA secp256r1 kernels (SIGNATURE_TYPE 20): k_ec_core, k_ec_table, k_emit_ect.
+// See ec_common.hpp for the split and the per-witness layouts.
+#pragma once
+#include "ec_common.hpp"
+#include "ec_walk.hpp"
+#include "fr.hpp"
+#include "layout.hpp"
+#include "regcore.hpp"
+
+namespace pzk {
+
+// ============================================================ signed 256-bit integers
+struct I256 { uint32_t w[8]; };
+__device__ __forceinline__ I256 i_u64(uint64_t x) {
+  I256 r; r.w[0] = (uint32_t)x; r.w[1] = (uint32_t)(x >> 32);
+#pragma unroll
+  for (int i = 2; i < 8; i++) r.w[i] = 0;
+  return r;
+}
+__device__ __forceinline__ I256 i_pow2(int k) {
+  I256 r = i_u64(0);
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = (k >> 5) == i ? (1u << (k & 31)) : 0u;
+  return r;
+}
+__device__ __forceinline__ I256 i_add(const I256& a, const I256& b) {
+  I256 r; uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)a.w[i] + b.w[i] + c; r.w[i] = (uint32_t)s; c = s >> 32; }
+  return r;
+}
+__device__ __forceinline__ I256 i_sub(const I256& a, const I256& b) {
+  I256 r; uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t d = (uint64_t)a.w[i] - b.w[i] - br; r.w[i] = (uint32_t)d; br = (d >> 32) & 1; }
+  return r;
+}
+__device__ __forceinline__ I256 i_neg(const I256& a) { return i_sub(i_u64(0), a); }
+__device__ __forceinline__ I256 i_mul(const I256& a, const I256& b) {  // low 256 bits (two's complement ring)
+  uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; i + j < 8; j++) {
+      uint64_t s = (uint64_t)a.w[i] * b.w[j] + t[i + j] + c;
+      t[i + j] = (uint32_t)s; c = (uint32_t)(s >> 32);
+    }
+  }
+  I256 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = t[i];
+  return r;
+}
+__device__ __forceinline__ bool i_is_neg(const I256& a) { return a.w[7] >> 31; }
+__device__ __forceinline__ bool i_is_zero(const I256& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.w[i];
+  return o == 0;
+}
+__device__ __forceinline__ I256 i_shr64(const I256& a) {  // arithmetic
+  I256 r; uint32_t s = i_is_neg(a) ? ~0u : 0u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = i + 2 < 8 ? a.w[i + 2] : s;
+  return r;
+}
+__device__ __forceinline__ uint32_t i_bit(const I256& a, int b) { return (a.w[b >> 5] >> (b & 31)) & 1u; }
+// v >= 0 and v < 2^L
+__device__ __forceinline__ bool i_fits(const I256& a, int L) {
+  if (i_is_neg(a)) return false;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int lo = 32 * i;
+    uint32_t m = L <= lo ? ~0u : L >= lo + 32 ? 0u : ~((1u << (L - lo)) - 1u);
+    ok &= (a.w[i] & m) == 0;
+  }
+  return ok;
+}
+// normal-form Fr of a signed integer |v| < p (negative v -> p + v)
+__device__ __forceinline__ I256 i_to_fr(const I256& a) {
+  if (!i_is_neg(a)) return a;
+  I256 p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) p.w[i] = P_[i];
+  return i_add(a, p);
+}
+__device__ __forceinline__ fr i_as_fr(const I256& a) { fr r; for (int i = 0; i < 8; i++) r.v[i] = a.w[i]; return r; }
+
+// ============================================================ multiprecision division (64-bit limbs)
+// floor(a / b), b = 4 limbs with b[3] != 0 (P-256 p and n); q[na-3], r[4]. Knuth D with the
+// 128/64 step of regcore.hpp (divlu). Same unique quotient/remainder long_div
+// (bigIntFunc.circom:190-232) produces.
+__device__ __forceinline__ void mp_divmod4(const uint64_t* a, int na, const uint64_t* b, uint64_t* q, uint64_t* r) {
+  const int s = __clzll((long long)b[3]);
+  uint64_t v[4], u[16];
+#pragma unroll
+  for (int i = 3; i > 0; i--) v[i] = (b[i] << s) | (s ? b[i - 1] >> (64 - s) : 0);
+  v[0] = b[0] << s;
+  u[na] = s ? a[na - 1] >> (64 - s) : 0;
+  for (int i = na - 1; i > 0; i--) u[i] = (a[i] << s) | (s ? a[i - 1] >> (64 - s) : 0);
+  u[0] = a[0] << s;
+  for (int j = na - 4; j >= 0; j--) {
+    uint64_t qhat, rhat;
+    bool big = false;
+    if (u[j + 4] >= v[3]) {
+      qhat = ~0ull;
+      rhat = u[j + 3] + v[3];
+      big = rhat < v[3];
+    } else {
+      qhat = divlu(u[j + 4], u[j + 3], v[3], &rhat);
+    }
+    while (!big) {
+      uint64_t ph = __umul64hi(qhat, v[2]), pl = qhat * v[2];
+      if (ph > rhat || (ph == rhat && pl > u[j + 2])) {
+        qhat--; rhat += v[3]; big = rhat < v[3];
+      } else break;
+    }
+    uint64_t carry = 0, borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint64_t pl = qhat * v[i], ph = __umul64hi(qhat, v[i]);
+      pl += carry; ph += pl < carry;
+      uint64_t t = u[i + j] - pl;
+      uint64_t b1 = u[i + j] < pl;
+      uint64_t t2 = t - borrow;
+      b1 += t < borrow;
+      u[i + j] = t2; borrow = b1; carry = ph;
+    }
+    uint64_t t = u[j + 4] - carry, b1 = u[j + 4] < carry;
+    uint64_t t2 = t - borrow; b1 += t < borrow;
+    u[j + 4] = t2;
+    if (b1) {  // add back
+      qhat--;
+      uint64_t c = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        uint64_t s1 = u[i + j] + v[i], c1 = s1 < v[i];
+        uint64_t s2 = s1 + c; c1 += s2 < c;
+        u[i + j] = s2; c = c1;
+      }
+      u[j + 4] += c;
+    }
+    q[j] = qhat;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = (u[i] >> s) | (s ? u[i + 1] << (64 - s) : 0);
+}
+
+// ============================================================ table context (device walker)
+struct EcTabCtx {
+  using V = I256;
+  uint4* tab;            // this op's table: 2 x uint4 per entry
+  uint32_t n;
+  const uint64_t* rp;    // op record
+  int32_t err;
+  __device__ void fail(int32_t code) { if (!err || code < err) err = code; }
+  __device__ void store(const V& v) {
+    I256 f = i_to_fr(v);
+    tab[2 * n] = make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]);
+    tab[2 * n + 1] = make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]);
+    n++;
+  }
+  __device__ V put(uint32_t, const V& v) { store(v); return v; }
+  __device__ V put_hidden(const V& v) { store(v); return v; }
+  __device__ void cp(uint32_t, const V&) {}
+  __device__ void bits(uint32_t, const V& v, int L) { if (!i_fits(v, L)) fail(ST_NUM2BITS); }  // bitify.circom:26
+  __device__ void masks(uint32_t, const V&, int) {}
+  __device__ V u64(uint64_t x) const { return i_u64(x); }
+  __device__ V pow2(int k) const { return i_pow2(k); }
+  __device__ V add(const V& a, const V& b) const { return i_add(a, b); }
+  __device__ V sub(const V& a, const V& b) const { return i_sub(a, b); }
+  __device__ V mul(const V& a, const V& b) const { return i_mul(a, b); }
+  __device__ V neg(const V& a) const { return i_neg(a); }
+  __device__ V sel(const V& c, const V& a, const V& b) const { return c.w[0] ? a : b; }
+  __device__ V is_zero(const V& a) const { return i_u64(i_is_zero(a) ? 1 : 0); }
+  __device__ V bit(const V& a, int b) const { return i_u64(i_bit(a, b)); }
+  // carry = (in + carry') / 2^64, field division (bigIntComparators.circom:119-122): exact for a passing witness
+  __device__ V shr64_exact(const V& t) {
+    if (t.w[0] | t.w[1]) fail(ST_BIGISZERO);
+    return i_shr64(t);
+  }
+  __device__ V inv_fr(const V& d) const {
+    fr x = fr_to_mont(i_as_fr(i_to_fr(d)));
+    fr y = fr_from_mont(fr_inv(x));
+    I256 r;
+    for (int i = 0; i < 8; i++) r.w[i] = y.v[i];
+    return r;
+  }
+  __device__ void check_zero(const V& v) { if (!i_is_zero(v)) fail(ST_BIGISZERO); }  // bigIntComparators.circom:128
+  __device__ void check_one(const V& v) {                                              // bigInt.circom:245
+    if (!i_is_zero(i_sub(v, i_u64(1)))) fail(ST_BIGMOD_GT);
+  }
+  // reduce_overflow_signed (bigIntFunc.circom:646-694) + long_div by P (:190-232): the signed sum
+  // S = sum in[i] 2^(64 i); sign = S >= 0; k = |S| / p (MCN - 3 digits)
+  __device__ void div_signed(const V* in, int CN, int MCN, V& sign, V* k) {
+    uint64_t acc[14];
+    for (int i = 0; i < 14; i++) acc[i] = 0;
+    for (int i = 0; i < CN; i++) {
+      const uint64_t ext = i_is_neg(in[i]) ? ~0ull : 0ull;
+      uint64_t c = 0;
+      for (int j = 0; i + j < 14; j++) {
+        uint64_t x = j < 4 ? ((uint64_t)in[i].w[2 * j + 1] << 32 | in[i].w[2 * j]) : ext;
+        uint64_t s1 = acc[i + j] + x, c1 = s1 < x;
+        uint64_t s2 = s1 + c; c1 += s2 < c;
+        acc[i + j] = s2; c = c1;
+      }
+    }
+    const bool pos = !(acc[13] >> 63);
+    if (!pos) {
+      uint64_t c = 1;
+      for (int i = 0; i < 14; i++) { uint64_t x = ~acc[i] + c; c = (c && x == 0) ? 1 : 0; acc[i] = x; }
+    }
+    uint64_t q[12], r[4];
+    mp_divmod4(acc, MCN, EC_P, q, r);
+    sign = i_u64(pos ? 1 : 0);
+    for (int i = 0; i < MCN - 3; i++) k[i] = i_u64(q[i]);
+  }
+  // reduce_overflow(64, 7, 8) (bigIntFunc.circom:570-588) + long_div by n
+  __device__ void divmod_n(const V* mo, V* q, V* r) {
+    uint64_t red[9];
+    for (int i = 0; i < 9; i++) red[i] = 0;
+    for (int i = 0; i < 7; i++) {
+      uint64_t c = 0;
+      for (int j = 0; j < 3 && i + j < 9; j++) {
+        uint64_t x = (uint64_t)mo[i].w[2 * j + 1] << 32 | mo[i].w[2 * j];
+        uint64_t s1 = red[i + j] + x, c1 = s1 < x;
+        uint64_t s2 = s1 + c; c1 += s2 < c;
+        red[i + j] = s2; c = c1;
+      }
+      for (int j = i + 3; j < 9 && c; j++) { red[j] += c; c = red[j] == 0; }
+    }
+    uint64_t qq[5], rr[4];
+    mp_divmod4(red, 8, EC_N, qq, rr);
+    for (int i = 0; i < 5; i++) q[i] = i_u64(qq[i]);
+    for (int i = 0; i < 4; i++) r[i] = i_u64(rr[i]);
+  }
+  __device__ V rec(int k) const { return i_u64(rp[k]); }
+};
+
+// ============================================================ P-256 Montgomery fields (p and n)
+struct e8 { uint32_t v[8]; };
+struct ModP {
+  static constexpr uint32_t m[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u,
+                                    0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
+  static constexpr uint32_t r2[8] = {0x00000003u, 0x00000000u, 0xffffffffu, 0xfffffffbu,
+                                     0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u};
+  static constexpr uint32_t r1[8] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu,
+                                     0xffffffffu, 0xffffffffu, 0xfffffffeu, 0x00000000u};
+  static constexpr uint32_t e[8] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0x00000000u,
+                                    0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
+  static constexpr uint32_t minv = 1u;
+};
+struct ModN {
+  static constexpr uint32_t m[8] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                    0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+  static constexpr uint32_t r2[8] = {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu,
+                                     0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u};
+  static constexpr uint32_t r1[8] = {0x039cdaafu, 0x0c46353du, 0x58e8617bu, 0x43190552u,
+                                     0x00000000u, 0x00000000u, 0xffffffffu, 0x00000000u};
+  static constexpr uint32_t e[8] = {0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                    0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+  static constexpr uint32_t minv = 0xee00bc4fu;
+};
+
+template <class M> __device__ __forceinline__ e8 m_const(const uint32_t (&c)[8]) { e8 r; for (int i = 0; i < 8; i++) r.v[i] = c[i]; return r; }
+// r = t - m if t >= m (t < 2m, t given with a carry word)
+template <class M> __device__ __forceinline__ e8 m_reduce(const uint32_t* t, uint32_t top) {
+  e8 d; uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t x = (uint64_t)t[i] - M::m[i] - br; d.v[i] = (uint32_t)x; br = (x >> 32) & 1; }
+  if (top || !br) return d;
+  e8 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  return r;
+}
+template <class M> __device__ __forceinline__ e8 m_mul(const e8& a, const e8& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t C = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) { uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + C; t[j] = (uint32_t)s; C = s >> 32; }
+    uint64_t s = (uint64_t)t[8] + C; t[8] = (uint32_t)s; t[9] = (uint32_t)(s >> 32);
+    const uint32_t m = t[0] * M::minv;
+    s = (uint64_t)m * M::m[0] + t[0]; C = s >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) { s = (uint64_t)m * M::m[j] + t[j] + C; t[j - 1] = (uint32_t)s; C = s >> 32; }
+    s = (uint64_t)t[8] + C; t[7] = (uint32_t)s; t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  return m_reduce<M>(t, t[8]);
+}
+template <class M> __device__ __forceinline__ e8 m_add(const e8& a, const e8& b) {
+  uint32_t t[8]; uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)a.v[i] + b.v[i] + c; t[i] = (uint32_t)s; c = s >> 32; }
+  return m_reduce<M>(t, (uint32_t)c);
+}
+template <class M> __device__ __forceinline__ e8 m_sub(const e8& a, const e8& b) {
+  e8 r; uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t d = (uint64_t)a.v[i] - b.v[i] - br; r.v[i] = (uint32_t)d; br = (d >> 32) & 1; }
+  if (br) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)r.v[i] + M::m[i] + c; r.v[i] = (uint32_t)s; c = s >> 32; }
+  }
+  return r;
+}
+template <class M> __device__ __forceinline__ e8 m_to(const e8& a) { return m_mul<M>(a, m_const<M>(M::r2)); }
+template <class M> __device__ __forceinline__ e8 m_from(const e8& a) { e8 one{}; for (int i = 0; i < 8; i++) one.v[i] = i == 0; return m_mul<M>(a, one); }
+template <class M> __device__ __forceinline__ bool m_is_zero(const e8& a) { uint32_t o = 0; for (int i = 0; i < 8; i++) o |= a.v[i]; return o == 0; }
+// a^(m-2) (Montgomery in/out), 4-bit fixed window; 0 -> 0 (mod_inv, bigIntFunc.circom:430-466)
+template <class M> __device__ e8 m_inv(const e8& a) {
+  e8 tbl[16];
+  tbl[0] = m_const<M>(M::r1);
+  tbl[1] = a;
+  for (int i = 2; i < 16; i++) tbl[i] = m_mul<M>(tbl[i - 1], a);
+  e8 r = tbl[0];
+  for (int w = 63; w >= 0; w--) {
+    if (w != 63) for (int k = 0; k < 4; k++) r = m_mul<M>(r, r);
+    const uint32_t nib = (M::e[w >> 3] >> ((w & 7) * 4)) & 15u;
+    e8 s = tbl[0];
+#pragma unroll
+    for (int q = 1; q < 16; q++) if ((uint32_t)q == nib) s = tbl[q];
+    if (nib) r = m_mul<M>(r, s);
+  }
+  return r;
+}
+__device__ __forceinline__ e8 e8_from_u64(const uint64_t* x) {
+  e8 r;
+  for (int i = 0; i < 4; i++) { r.v[2 * i] = (uint32_t)x[i]; r.v[2 * i + 1] = (uint32_t)(x[i] >> 32); }
+  return r;
+}
+__device__ __forceinline__ void e8_to_u64(const e8& a, uint64_t* x) {
+  for (int i = 0; i < 4; i++) x[i] = (uint64_t)a.v[2 * i + 1] << 32 | a.v[2 * i];
+}
+
+// Jacobian points (Montgomery mod p), a = -3 (P-256: A = p - 3)
+struct Jac { e8 x, y, z; };
+// dbl-2001-b
+__device__ Jac jac_dbl(const Jac& P) {
+  using M = ModP;
+  e8 delta = m_mul<M>(P.z, P.z), gamma = m_mul<M>(P.y, P.y), beta = m_mul<M>(P.x, gamma);
+  e8 t = m_mul<M>(m_sub<M>(P.x, delta), m_add<M>(P.x, delta));
+  e8 alpha = m_add<M>(m_add<M>(t, t), t);
+  e8 b4 = m_add<M>(beta, beta); b4 = m_add<M>(b4, b4);
+  Jac R;
+  R.x = m_sub<M>(m_mul<M>(alpha, alpha), m_add<M>(b4, b4));
+  e8 yz = m_add<M>(P.y, P.z);
+  R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), gamma), delta);
+  e8 g2 = m_mul<M>(gamma, gamma);
+  e8 g8 = m_add<M>(g2, g2); g8 = m_add<M>(g8, g8); g8 = m_add<M>(g8, g8);
+  R.y = m_sub<M>(m_mul<M>(alpha, m_sub<M>(b4, R.x)), g8);
+  return R;
+}
+// add-2007-bl (P != +-Q; H = 0 gives Z3 = 0, flagged by the caller)
+__device__ Jac jac_add(const Jac& P, const Jac& Q) {
+  using M = ModP;
+  e8 z1z1 = m_mul<M>(P.z, P.z), z2z2 = m_mul<M>(Q.z, Q.z);
+  e8 u1 = m_mul<M>(P.x, z2z2), u2 = m_mul<M>(Q.x, z1z1);
+  e8 s1 = m_mul<M>(m_mul<M>(P.y, Q.z), z2z2), s2 = m_mul<M>(m_mul<M>(Q.y, P.z), z1z1);
+  e8 h = m_sub<M>(u2, u1), h2 = m_add<M>(h, h);
+  e8 i = m_mul<M>(h2, h2), j = m_mul<M>(h, i);
+  e8 r = m_sub<M>(s2, s1); r = m_add<M>(r, r);
+  e8 v = m_mul<M>(u1, i);
+  Jac R;
+  R.x = m_sub<M>(m_sub<M>(m_mul<M>(r, r), j), m_add<M>(v, v));
+  e8 s1j = m_mul<M>(s1, j);
+  R.y = m_sub<M>(m_mul<M>(r, m_sub<M>(v, R.x)), m_add<M>(s1j, s1j));
+  e8 zz = m_add<M>(P.z, Q.z);
+  R.z = m_mul<M>(m_sub<M>(m_sub<M>(m_mul<M>(zz, zz), z1z1), z2z2), h);
+  return R;
+}
+
+// ============================================================ k_ec_core
+// handles of points: >= 0 op output; H_D dummy point; H_Q public key; <= -1000 fixed-base table entry
+constexpr int H_D = -1, H_Q = -2;
+__host__ __device__ constexpr int h_tab(int i, int j) { return -(1000 + i * 256 + j); }
+enum { PT_GM_AP, PT_GM_RP, PT_PRE, PT_SM_AP, PT_SM_RP };
+
+// The data flow of verifyECDSABits' two scalar multiplications (ec/curve.circom:356-494, 672-906):
+// calls on_op(op, in1, in2) for every point operation in op order and on_pt(kind, index, handle)
+// for every point the selection logic forwards (additionPoints / resultingPoints / precompute).
+// The isZero/isDummy decisions compare handles: a forwarded dummy is the dummy itself, and a
+// curve point equal in x[0] to a dummy by chance has probability ~2^-64.
+template <class OnOp, class OnPt>
+__device__ void ec_plan(const uint64_t* u1, const uint64_t* u2, OnOp on_op, OnPt on_pt) {
+  auto gm_ap = [&](int i) {
+    int b = (int)((u1[i >> 3] >> (8 * (i & 7))) & 255);
+    return b ? h_tab(i, b) : (i % 2 == 0 ? H_D : EC_OP_SD);
+  };
+  on_op(EC_OP_SD, H_D, 0);
+  for (int i = 0; i < 32; i++) on_pt(PT_GM_AP, i, gm_ap(i));
+  int left = gm_ap(0);
+  for (int i = 0; i < 31; i++) {
+    const int right = gm_ap(i + 1);
+    on_op(ec_op_gm_add(i), left, right);
+    const bool ld = left == H_D || left == EC_OP_SD, rd = right == H_D || right == EC_OP_SD;
+    const int rp = ld ? right : rd ? left : ec_op_gm_add(i);
+    on_pt(PT_GM_RP, i, rp);
+    left = rp;
+  }
+  const int gm_out = left;
+  auto pre = [](int i) { return i == 0 ? H_D : i == 1 ? H_Q : ec_op_pre(i); };
+  on_pt(PT_PRE, 0, H_D);
+  on_pt(PT_PRE, 1, H_Q);
+  for (int i = 2; i < 16; i++) {
+    if (i % 2 == 0) on_op(ec_op_pre(i), pre(i / 2), 0);
+    else on_op(ec_op_pre(i), H_Q, pre(i - 1));
+    on_pt(PT_PRE, i, ec_op_pre(i));
+  }
+  auto nib = [&](int w) { int b = 252 - 4 * w; return (int)((u2[b >> 6] >> (b & 63)) & 15); };
+  on_pt(PT_SM_RP, 0, H_D);
+  int rp = pre(nib(0));
+  on_pt(PT_SM_AP, 0, rp);
+  on_pt(PT_SM_RP, 1, rp);
+  for (int w = 1; w < 64; w++) {
+    const int ap = pre(nib(w));
+    on_pt(PT_SM_AP, w, ap);
+    const bool izr = rp == H_D, iza = ap == H_D;
+    for (int j = 0; j < 4; j++) {
+      const int op = ec_op_sm_dbl(4 * w - 4 + j);
+      on_op(op, j == 0 ? (izr ? H_D : rp) : op - 1, 0);
+    }
+    const int dl = ec_op_sm_dbl(4 * w - 1), ad = ec_op_sm_add(w - 1);
+    on_op(ad, dl, ap);
+    rp = izr ? ap : iza ? dl : ad;
+    on_pt(PT_SM_RP, w + 1, rp);
+  }
+  on_op(EC_OP_FINAL, gm_out, rp);
+}
+
+// Fr (BN254) of a - b for 64-bit a, b
+__device__ __forceinline__ fr fr_diff_u64(uint64_t a, uint64_t b) {
+  return a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
+}
+
+// lane = witness
+__global__ void __launch_bounds__(64) k_ec_core(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
+                                                uint64_t* ec_core, uint64_t* ec_jac, fr* ec_inv, int32_t* status,
+                                                uint32_t batch) {
+  core_priority();
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  const RegInfo& G = L.reg;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
+  int32_t* st = status ? status + w : nullptr;
+  bool bad = false;
+  uint64_t r[4], s[4], q[8], h[4];
+  for (int i = 0; i < 4; i++) {
+    const uint8_t* a = row + 32ull * (G.in_sig + i);
+    const uint8_t* b = row + 32ull * (G.in_sig + 4 + i);
+    bad |= !in_is_u64(a) || !in_is_u64(b);
+    r[i] = in_u64(a); s[i] = in_u64(b);
+  }
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* a = row + 32ull * (G.in_pk + i);
+    bad |= !in_is_u64(a);
+    q[i] = in_u64(a);
+  }
+  if (bad) set_status(st, ST_INPUT_RANGE);
+  {  // hashedChunked[j] (ecdsa.circom:30-38): 64-bit big-endian digest words, least significant first
+    const ShaJob job = L.sha[G.j_sa];
+    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
+    for (int j = 0; j < 4; j++) h[j] = ((uint64_t)H[2 * (3 - j)] << 32) | H[2 * (3 - j) + 1];
+  }
+  // ---- scalars mod n: sinv = s^-1 (BigModInv, bigInt.circom:344-368), u1 = sinv h, u2 = sinv r
+  using N = ModN;
+  auto red_n = [&](const uint64_t* x) {  // x mod n for x < 2^256 (< 2n)
+    e8 a = e8_from_u64(x);
+    return m_reduce<N>(a.v, 0);
+  };
+  const e8 sm = m_to<N>(red_n(s)), sinv_m = m_inv<N>(sm);
+  const e8 u1 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(h))));
+  const e8 u2 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(r))));
+  const e8 one_chk = m_from<N>(m_mul<N>(sm, sinv_m));
+  {
+    uint32_t o = one_chk.v[0] ^ 1u;
+    for (int i = 1; i < 8; i++) o |= one_chk.v[i];
+    if (o) set_status(st, ST_ECDSA_INV);  // bigInt.circom:364-368
+  }
+  uint64_t sinv[4], U1[4], U2[4];
+  e8_to_u64(m_from<N>(sinv_m), sinv);
+  e8_to_u64(u1, U1);
+  e8_to_u64(u2, U2);
+  for (int i = 0; i < 4; i++) {
+    C[ECC_SINV + i] = sinv[i]; C[ECC_U1 + i] = U1[i]; C[ECC_U2 + i] = U2[i]; C[ECC_H + i] = h[i];
+    C[ECC_MM + 8 * EC_MM_INV + i] = s[i];    C[ECC_MM + 8 * EC_MM_INV + 4 + i] = sinv[i];
+    C[ECC_MM + 8 * EC_MM_U1 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U1 + 4 + i] = h[i];
+    C[ECC_MM + 8 * EC_MM_U2 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U2 + 4 + i] = r[i];
+  }
+  // ---- point chain, Jacobian (phase 1)
+  auto aff_const = [&](int hd, uint64_t* xy) {
+    if (hd == H_D) { for (int i = 0; i < 8; i++) xy[i] = EC_D[i]; }
+    else if (hd == H_Q) { for (int i = 0; i < 8; i++) xy[i] = q[i]; }
+    else {
+      const int t = -hd - 1000;
+      const uint64_t* T = L.ec_gpow + (size_t)t * 8;
+      for (int i = 0; i < 8; i++) xy[i] = T[i];
+    }
+  };
+  auto get_jac = [&](int hd) {
+    Jac P;
+    if (hd >= 0) {
+      const uint64_t* s0 = J + 16 * hd;
+      P.x = e8_from_u64(s0); P.y = e8_from_u64(s0 + 4); P.z = e8_from_u64(s0 + 8);
+    } else {
+      uint64_t xy[8];
+      aff_const(hd, xy);
+      P.x = m_to<ModP>(e8_from_u64(xy)); P.y = m_to<ModP>(e8_from_u64(xy + 4)); P.z = m_const<ModP>(ModP::r1);
+    }
+    return P;
+  };
+  ec_plan(U1, U2,
+          [&](int op, int h1, int h2) {
+            Jac P = get_jac(h1);
+            Jac R = ec_op_is_dbl(op) ? jac_dbl(P) : jac_add(P, get_jac(h2));
+            uint64_t* d = J + 16 * op;
+            e8_to_u64(R.x, d); e8_to_u64(R.y, d + 4); e8_to_u64(R.z, d + 8);
+          },
+          [](int, int, int) {});
+  // ---- one batched inversion of every Z (phase 2), affine outputs into the op records
+  {
+    using M = ModP;
+    e8 acc = m_const<M>(M::r1);
+    bool degenerate = false;
+    for (int op = 0; op < EC_N_OPS; op++) {
+      uint64_t* d = J + 16 * op;
+      e8_to_u64(acc, d + 12);
+      e8 z = e8_from_u64(d + 8);
+      if (m_is_zero<M>(z)) degenerate = true;
+      else acc = m_mul<M>(acc, z);
+    }
+    if (degenerate) set_status(st, ST_BIGISZERO);  // dx = 0 or y = 0: the affine formulas divide by 0
+    e8 inv = m_inv<M>(acc);
+    for (int op = EC_N_OPS - 1; op >= 0; op--) {
+      uint64_t* d = J + 16 * op;
+      e8 z = e8_from_u64(d + 8);
+      uint64_t* o = C + ECC_REC + ECC_REC_WORDS * op + 16;
+      if (m_is_zero<M>(z)) { for (int i = 0; i < 8; i++) o[i] = 0; continue; }
+      e8 zi = m_mul<M>(inv, e8_from_u64(d + 12));
+      inv = m_mul<M>(inv, z);
+      e8 zi2 = m_mul<M>(zi, zi), zi3 = m_mul<M>(zi2, zi);
+      e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d), zi2)), o);
+      e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d + 4), zi3)), o + 4);
+    }
+  }
+  // ---- records' inputs and the forwarded points (phase 3)
+  auto aff = [&](int hd, uint64_t* xy) {
+    if (hd >= 0) { const uint64_t* o = C + ECC_REC + ECC_REC_WORDS * hd + 16; for (int i = 0; i < 8; i++) xy[i] = o[i]; }
+    else aff_const(hd, xy);
+  };
+  int gm_out = 0, sm_out = 0;
+  ec_plan(U1, U2,
+          [&](int op, int h1, int h2) {
+            uint64_t* rc = C + ECC_REC + ECC_REC_WORDS * op;
+            aff(h1, rc);
+            if (ec_op_is_dbl(op)) { for (int i = 0; i < 8; i++) rc[8 + i] = 0; }
+            else aff(h2, rc + 8);
+            if (op == EC_OP_FINAL) { gm_out = h1; sm_out = h2; }
+          },
+          [&](int kind, int i, int hd) {
+            int base = kind == PT_GM_AP ? ECC_GM_AP : kind == PT_GM_RP ? ECC_GM_RP : kind == PT_PRE ? ECC_PRE
+                     : kind == PT_SM_AP ? ECC_SM_AP : ECC_SM_RP;
+            aff(hd, C + base + 8 * i);
+          });
+  (void)gm_out; (void)sm_out;
+  // ---- x1 mod n === r (ecdsa.circom:81-83); modOrder record
+  {
+    const uint64_t* x1 = C + ECC_REC + ECC_REC_WORDS * EC_OP_FINAL + 16;
+    e8 xm = red_n(x1);
+    uint64_t xr[4];
+    e8_to_u64(xm, xr);
+    bool ok = true;
+    for (int i = 0; i < 4; i++) {
+      ok &= xr[i] == r[i];
+      C[ECC_MM + 8 * EC_MM_XN + i] = x1[i];
+      C[ECC_MM + 8 * EC_MM_XN + 4 + i] = i == 0 ? 1 : 0;
+    }
+    if (!ok) set_status(st, ST_ECDSA_R);
+  }
+  // ---- IsEqual inverses (phase 4): genmult dummy tests, scalarMult isZeroResult / isZeroAddition
+  {
+    fr* I = ec_inv + (size_t)w * EC_N_INV;
+    const uint64_t dx = EC_D[0], sdx = C[ECC_REC + ECC_REC_WORDS * EC_OP_SD + 16];
+    for (int i = 0; i < 31; i++) {
+      const uint64_t lx = i == 0 ? C[ECC_GM_AP] : C[ECC_GM_RP + 8 * (i - 1)], rx = C[ECC_GM_AP + 8 * (i + 1)];
+      I[ECI_GM + 4 * i + 0] = fr_to_mont(fr_diff_u64(lx, dx));
+      I[ECI_GM + 4 * i + 1] = fr_to_mont(fr_diff_u64(lx, sdx));
+      I[ECI_GM + 4 * i + 2] = fr_to_mont(fr_diff_u64(rx, dx));
+      I[ECI_GM + 4 * i + 3] = fr_to_mont(fr_diff_u64(rx, sdx));
+    }
+    for (int k = 0; k < 64; k++) I[ECI_SM_ZR + k] = fr_to_mont(fr_diff_u64(dx, C[ECC_SM_RP + 8 * k]));
+    for (int k = 1; k < 64; k++) I[ECI_SM_ZA + k - 1] = fr_to_mont(fr_diff_u64(dx, C[ECC_SM_AP + 8 * k]));
+    // Montgomery's trick over the 251 differences (0 stays 0: IsZero's inv, comparators.circom:17)
+    fr* pre = reinterpret_cast<fr*>(J);
+    fr acc = fr_mont_one();
+    for (int i = 0; i < EC_N_INV; i++) {
+      pre[i] = acc;
+      fr x = I[i];
+      if (!fr_is_zero(x)) acc = fr_mul(acc, x);
+    }
+    fr inv = fr_inv(acc);
+    for (int i = EC_N_INV - 1; i >= 0; i--) {
+      fr x = I[i];
+      if (fr_is_zero(x)) continue;
+      I[i] = fr_mul(inv, pre[i]);
+      inv = fr_mul(inv, x);
+    }
+    for (int i = 0; i < EC_N_INV; i++) I[i] = fr_from_mont(I[i]);
+  }
+}
+
+// ============================================================ k_ec_table: lane per (witness, op)
+template <int TYPE>
+__global__ void __launch_bounds__(64) k_ec_table(DevLayout L, const int32_t* ops, const uint64_t* ec_core, uint8_t* ec_tab,
+                                                 int32_t* status, uint32_t batch) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  const int t = ops[blockIdx.y];
+  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  const uint64_t* rec = t < EC_N_OPS ? C + ECC_REC + ECC_REC_WORDS * t : C + ECC_MM + 8 * (t - EC_N_OPS);
+  uint4* tab = reinterpret_cast<uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
+  EcTabCtx c{tab, 0, rec, 0};
+  EcWalk<EcTabCtx> walk(c);
+  walk.run(TYPE);
+  if (c.err && status) lane_status(status + w, c.err);
+}
+
+// ============================================================ k_emit_ect: table -> signals
+__device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_t half) {
+  const uint32_t op = d >> 29, bit = (d >> 20) & 511u, idx = d & 0xfffffu;
+  if (op == ECD_ZERO) return make_uint4(0u, 0u, 0u, 0u);
+  if (op == ECD_COPY) return tab[2 * idx + half];
+  if (op == ECD_BIT) {
+    if (half) return make_uint4(0u, 0u, 0u, 0u);
+    const uint4 q = tab[2 * idx + (bit >> 7)];
+    const uint32_t k = (bit >> 5) & 3u, wv = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+    return make_uint4((wv >> (bit & 31u)) & 1u, 0u, 0u, 0u);
+  }
+  // MASK: v & (2^(bit+1) - 1)
+  const uint4 q = tab[2 * idx + half];
+  const int nb = (int)bit + 1, lo = 128 * (int)half;
+  auto mw = [&](uint32_t x, int k) -> uint32_t {
+    const int b0 = lo + 32 * k;
+    return nb >= b0 + 32 ? x : nb <= b0 ? 0u : (x & ((1u << (nb - b0)) - 1u));
+  };
+  return make_uint4(mw(q.x, 0), mw(q.y, 1), mw(q.z, 2), mw(q.w, 3));
+}
+
+__global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
+                                                  size_t stride) {
+  __shared__ uint4 tab[2 * EC_TABLE_MAX];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const int t = R.a[0], type = R.a[1];
+  const uint32_t n = L.ec_tab_n[type];
+  const uint4* src = reinterpret_cast<const uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
+  for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
+  __syncthreads();
+  const uint32_t* prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
+  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
+  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = ect_value(tab, prog[h >> 1], h & 1);
+}
+
+}  // namespace pzk

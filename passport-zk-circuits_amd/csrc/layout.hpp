@@ -14,7 +14,7 @@ namespace pzk {
 // lane status codes (mirror include/pzkwit.h PZK_ST_*)
 constexpr int32_t ST_NUM2BITS = 1, ST_ALIAS = 2, ST_ISZERO = 3, ST_FLOW = 7, ST_RSA_HASH = 8,
                   ST_RSA_PREFIX = 9, ST_RSA_PAD = 10, ST_BIGMOD_GT = 11, ST_BIGISZERO = 12,
-                  ST_SMT_LAST = 13, ST_INPUT_RANGE = 64;
+                  ST_SMT_LAST = 13, ST_ECDSA_INV = 15, ST_ECDSA_R = 16, ST_INPUT_RANGE = 64;
 
 // ---- emit regions: a contiguous run of witness signals with one closed-form generator
 enum RegionKind : uint32_t {
@@ -44,12 +44,30 @@ enum RegionKind : uint32_t {
   RK_BJJ_OWN = 21,   // BabyjubjubBase8Multiplication own (out[2], scalar) + GetBabyjubjubBase8
   RK_BJJ_STEPS = 22, // adders[0], (adders[i], doublers[i-1]) i = 1..253
   RK_SIG_OWN = 23,   // VerifySignature / RsaVerifyPkcs1v15 / PowerMod input copies (a0 = sub-kind)
+  // ---- ECDSA secp256r1 (ec_common.hpp, ec_emit.hpp)
+  RK_ECT = 24,        // table block: a0 = table op (EC op, or EC_N_OPS + BigMultModP index), a1 = EcType
+  RK_EC_U64 = 25,     // w[off+i] = EC core word a0 + i
+  RK_EC_CONST = 26,   // curve constant a0 (ec_k ids)
+  RK_EC_GM_RCC = 27,  // generator mult resultCoordinateComputation[32][256][2][4]
+  RK_EC_GM_EQ = 28,   // generator mult equal[32][256] (IsEqual)
+  RK_EC_GM_SUM = 29,  // generator mult getSumOfNElements[32][2][4] (GetSum(256))
+  RK_EC_GM_STEP = 30, // generator mult step a0: 4 IsEqual dummy tests + 16 switchers
+  RK_EC_N2B = 31,     // Num2Bits(64): a0 = 0 EC core word a1 / 1 input element a1
+  RK_EC_B2N8 = 32,    // generator mult bits2num[32] (Bits2Num(8)) of the scalar at core word a0
+  RK_EC_SBITS = 33,   // scalarMult scalarBits[256] of the scalar at core word a0
+  RK_EC_SM_W0 = 34,   // scalarMult window a0: bits2Num(4) + isZeroResult
+  RK_EC_SM_DSW = 35,  // scalarMult window a0: doubleSwitcher[8]
+  RK_EC_SM_SEL = 36,  // scalarMult window a0: getSum[8] (GetSum(16)) + partsEqual[16]
+  RK_EC_SM_RSW = 37,  // scalarMult window a0: isZeroAddition + (resultSwitcherAddition, resultSwitcherDoubling)[8]
+  RK_EC_PKBITS = 38,  // PassportVerificationBuilder ecBitsX[256], ecBitsY[256] of pubkey input a0
+  RK_EC_B2N248 = 39,  // Bits2Num(248) of the 4-limb input at a0 (xToNum / yToNum)
   RK_COUNT
 };
 
 // emit kernels (one work list each)
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_COUNT };
+// E_ECT = ECDSA table blocks (k_emit_ect)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -59,7 +77,8 @@ __host__ __device__ inline int emitter_of(uint32_t kind) {
     case RK_MODMUL: return E_MM;
     case RK_BJJ_STEPS: return E_BJJ;
     case RK_RSA_OUT: return E_GENR;
-    default: return E_GEN;
+    case RK_ECT: return E_ECT;
+    default: return kind >= RK_EC_U64 && kind <= RK_EC_B2N248 ? E_GENR : E_GEN;
   }
 }
 // regions whose emit workgroup needs the whole region (LDS pre-pass over all of it)
@@ -123,6 +142,8 @@ struct RegInfo {
   int32_t dg1_chunk, aa_shift, in_dg1, in_dg15, aa;
   int32_t n_modmul;
   uint32_t modmul_size;
+  int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (secp256r1)
+  int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
 };
 
 // per-witness core sizes of the register-circuit kernels
@@ -184,6 +205,12 @@ struct DevLayout {
   RegInfo reg;
   uint32_t rsa_core_words;          // u64 per witness
   uint32_t bjj_core_fr, smt_core_fr;
+  // ECDSA (ec_common.hpp)
+  const uint64_t* ec_gpow;          // P-256 fixed-base table [32][256][2][4]
+  const uint32_t* ec_prog;          // table-block descriptor programs, at ec_prog_off[type]
+  uint32_t ec_prog_off[3], ec_tab_n[3];
+  const uint32_t* ec_tab_off;       // entry offset of table op t inside a witness's tables
+  uint32_t ec_tab_entries;          // table entries per witness
 };
 
 }  // namespace pzk

@@ -66,14 +66,29 @@ __global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inpu
   vs.at(R.v_one, w) = fr_mont_one();
   // pubkeyHasherRsa inputs: tempModulus[i] + pk[3i+2] = pk[3i]*2^128 + pk[3i+1]*2^64 + pk[3i+2]
   // (passportVerificationBuilder.circom:182-191), in field arithmetic
-  fr two64 = fr_zero(); two64.v[2] = 1;
-  fr two128 = fr_zero(); two128.v[4] = 1;
-  two64 = fr_to_mont(two64); two128 = fr_to_mont(two128);
-  for (int i = 0; i < 5; i++) {
-    fr a = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i)));
-    fr b = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 1)));
-    fr c = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 2)));
-    vs.at(R.v_pk + i, w) = fr_add(fr_add(fr_mul(a, two128), fr_mul(b, two64)), c);
+  if (R.ecdsa) {
+    // ECDSA: pubkeyHasher = Poseidon2(x mod 2^248, y mod 2^248) (passportVerificationBuilder.circom:193-230)
+    for (int a = 0; a < 2; a++) {
+      fr v = fr_zero();
+      for (int j = 0; j < 4; j++) {
+        const uint8_t* e = row + 32ull * (R.in_pk + 4 * a + j);
+        bad |= !in_is_u64(e);
+        uint64_t x = in_u64(e);
+        if (j == 3) x &= (1ull << 56) - 1;
+        v.v[2 * j] = (uint32_t)x; v.v[2 * j + 1] = (uint32_t)(x >> 32);
+      }
+      vs.at(a ? R.v_pky : R.v_pkx, w) = fr_to_mont(v);
+    }
+  } else {
+    fr two64 = fr_zero(); two64.v[2] = 1;
+    fr two128 = fr_zero(); two128.v[4] = 1;
+    two64 = fr_to_mont(two64); two128 = fr_to_mont(two128);
+    for (int i = 0; i < 5; i++) {
+      fr a = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i)));
+      fr b = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 1)));
+      fr c = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 2)));
+      vs.at(R.v_pk + i, w) = fr_add(fr_add(fr_mul(a, two128), fr_mul(b, two64)), c);
+    }
   }
   // AA key chunks: Bits2Num(200) x4 + Bits2Num(224), in[L-1-i] = dg15[AA_SHIFT + 200 j + i] (identity.circom:31-45)
   if (R.aa) {

@@ -11,6 +11,7 @@
 #include "regcore.hpp"
 #include "sha.hpp"
 #include "mm_prog.hpp"
+#include "ec_emit.hpp"
 
 namespace pzk {
 
@@ -173,7 +174,7 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
         return el_w(r);
       }
     }
-    default: return el_u64(0);
+    default: return ec_small(L, B, R, w, s);
   }
 }
 

@@ -12,6 +12,7 @@
 #include "builder.hpp"
 #include "kernels.hpp"
 #include "bufs.hpp"
+#include "ec_common.hpp"
 #include "poseidon.hpp"
 
 using namespace pzk;
@@ -27,17 +28,20 @@ static int fail(int code, const std::string& msg) { g_err = msg; return code; }
 // kernel phases, timed with HIP events on the launch stream when PZK_EXEC_TIMING is set
 enum Phase {
   PH_LOAD, PH_SHA_CORE, PH_PREP, PH_RSA_CORE, PH_BJJ_CORE, PH_POS_CORE, PH_SMT,
-  PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_COUNT
+  PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ,
+  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_COUNT
 };
 static const char* PHASE_NAMES[PH_COUNT] = {"load_values", "sha_core", "prep",     "rsa_core",  "bjj_core",
                                             "pos_core",    "smt",      "emit_gen", "emit_sha",  "emit_pos",
-                                            "emit_bits",   "emit_flow", "emit_mm", "emit_bjj"};
+                                            "emit_bits",   "emit_flow", "emit_mm", "emit_bjj",
+                                            "ec_core",     "ec_table",  "emit_ect"};
 static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k_prep",      "k_rsa_core",
                                               "k_bjj_core",    "k_pos_core",  "k_smt_prep+k_smt_chain",
                                               "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
-                                              "k_emit_flow",   "k_emit_mm",   "k_emit_bjj"};
+                                              "k_emit_flow",   "k_emit_mm",   "k_emit_bjj",
+                                              "k_ec_core",     "k_ec_table",  "k_emit_ect"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
-                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN};
+                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -114,6 +118,11 @@ struct pzk_instance {
   int32_t* d_level_task = nullptr;
   fr* d_pos_consts = nullptr;
   fr* d_bjj_table = nullptr;  // fixed-base Base8 table (register circuit)
+  // ECDSA (SIGNATURE_TYPE 20)
+  uint64_t* d_ec_gpow = nullptr;
+  uint32_t *d_ec_prog = nullptr, *d_ec_tab_off = nullptr;
+  int32_t* d_ec_ops[3] = {};
+  fr* d_inv_small = nullptr;
   PosParamIndex pix{};
   int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
   // per-batch scratch, grown on demand
@@ -124,6 +133,9 @@ struct pzk_instance {
   uint64_t* d_rsa_core = nullptr;
   uint64_t* d_rsa_colsum = nullptr;  // RSA x*y column sums, SoA [(3 i + c)][witness]
   fr *d_bjj_core = nullptr, *d_bjj_scratch = nullptr, *d_smt_core = nullptr;
+  uint64_t *d_ec_core = nullptr, *d_ec_jac = nullptr;
+  fr* d_ec_inv = nullptr;
+  uint8_t* d_ec_tab = nullptr;
   // staging for the host-buffer path
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -150,6 +162,11 @@ struct pzk_instance {
     L.rsa_core_words = lay.rsa_core_words;
     L.bjj_core_fr = lay.bjj_core_fr;
     L.smt_core_fr = lay.smt_core_fr;
+    L.ec_gpow = d_ec_gpow;
+    L.ec_prog = d_ec_prog;
+    for (int t = 0; t < 3; t++) { L.ec_prog_off[t] = lay.ec_prog_off[t]; L.ec_tab_n[t] = lay.ec_tab_n[t]; }
+    L.ec_tab_off = d_ec_tab_off;
+    L.ec_tab_entries = lay.ec_tab_entries;
     return L;
   }
 };
@@ -227,18 +244,20 @@ static int upload(T** dst, const std::vector<T>& v) {
 
 static void free_scratch(pzk_instance* I) {
   void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_rsa_colsum, I->d_bjj_core,
-                  I->d_bjj_scratch, I->d_smt_core};
+                  I->d_bjj_scratch, I->d_smt_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, I->d_ec_tab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr; I->d_rsa_colsum = nullptr;
   I->d_bjj_core = nullptr; I->d_bjj_scratch = nullptr; I->d_smt_core = nullptr;
+  I->d_ec_core = nullptr; I->d_ec_jac = nullptr; I->d_ec_inv = nullptr; I->d_ec_tab = nullptr;
   I->cap = 0;
 }
 
 static void free_all(pzk_instance* I) {
   free_scratch(I);
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
-                  I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status};
+                  I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
+                  I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
@@ -283,6 +302,21 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
     if (hipMalloc(&I->d_bjj_table, sizeof(fr) * 3 * BJJ_TABLE_WINDOWS * 256) != hipSuccess ||
         launch_bjj_table(I->d_bjj_table, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
       rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
+  }
+  if (!rc && I->lay.is_ecdsa) {
+    std::string path = data_dir() + "/p256_gpow8.bin";
+    std::vector<uint64_t> tab(32 * 256 * 8);
+    FILE* fp = fopen(path.c_str(), "rb");
+    size_t got = fp ? fread(tab.data(), 8, tab.size(), fp) : 0;
+    if (fp) fclose(fp);
+    if (got != tab.size()) rc = fail(PZK_E_DATA, "cannot read the P-256 generator table " + path);
+    if (!rc) rc = upload(&I->d_ec_gpow, tab);
+    if (!rc) rc = upload(&I->d_ec_prog, I->lay.ec_prog);
+    if (!rc) rc = upload(&I->d_ec_tab_off, I->lay.ec_tab_off);
+    for (int t = 0; t < 3 && !rc; t++) rc = upload(&I->d_ec_ops[t], I->lay.ec_ops[t]);
+    if (!rc && (hipMalloc(&I->d_inv_small, sizeof(fr) * 256) != hipSuccess ||
+                launch_inv_small(I->d_inv_small, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+      rc = fail(PZK_E_HIP, "ECDSA constant setup failed");
   }
   if (rc) { free_all(I); delete I; return rc; }
   // The dependency chains (main stream: Poseidon/SMT/BJJ cores; s_rsa: RSA core) get the
@@ -381,6 +415,10 @@ static int ensure_scratch(pzk_instance* I, size_t batch) {
       {(void**)&I->d_bjj_core, 32ull * L.bjj_core_fr * batch},
       {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&I->d_smt_core, 32ull * L.smt_core_fr * batch},
+      {(void**)&I->d_ec_core, L.is_ecdsa ? 8ull * EC_CORE_WORDS * batch : 0},
+      {(void**)&I->d_ec_jac, L.is_ecdsa ? 8ull * EC_JAC_WORDS * batch : 0},
+      {(void**)&I->d_ec_inv, L.is_ecdsa ? 32ull * EC_N_INV * batch : 0},
+      {(void**)&I->d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
   };
   for (auto& r : req)
     if (r.bytes && hipMalloc(r.p, r.bytes) != hipSuccess) {
@@ -413,7 +451,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   ValueStore vs{I->d_values, B};
   PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix};
   Bufs bufs{d_inputs, I->d_sha_core, I->d_rsa_core, I->d_pos_core, I->d_bjj_core, I->d_smt_core, vs, d_wtns, stride,
-            d_status};
+            d_status, I->d_ec_core, I->d_ec_inv, I->d_ec_tab, I->d_inv_small};
   Timing* T = nullptr;
   int slot = 0;
   if (exec && (exec->flags & PZK_EXEC_TIMING)) {
@@ -461,13 +499,28 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha;
     HIPCHK(hipEventRecord(I->ev_load, st));
     HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_load, 0));
-    { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
-      HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
-    HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
-    if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
-    HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+    if (!lay.is_ecdsa) {
+      { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
+        HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
+      HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+      if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
+      HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+    }
     { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
     HIPCHK(hipEventRecord(I->ev_sha, st));
+    if (lay.is_ecdsa) {
+      // ECDSA chain (needs the SA digest): EC core, value tables, table-block emission on s_rsa
+      HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_sha, 0));
+      { PhaseScope ps(T, slot, PH_EC_CORE, s_rsa);
+        HIPCHK(launch_ec_core(L, d_inputs, I->d_sha_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, d_status, B, s_rsa)); }
+      HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+      { PhaseScope ps(T, slot, PH_EC_TABLE, s_rsa);
+        for (int t = 0; t < 3; t++)
+          HIPCHK(launch_ec_table(L, t, I->d_ec_ops[t], (uint32_t)lay.ec_ops[t].size(), I->d_ec_core, I->d_ec_tab,
+                                 d_status, B, s_rsa)); }
+      if ((rc = emit(E_ECT, s_rsa))) return rc;
+      HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+    }
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
@@ -487,8 +540,10 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     if ((rc = emit(E_GEN, st))) return rc;
     if ((rc = emit(E_FLOW, st))) return rc;
     HIPCHK(hipStreamWaitEvent(st, I->ev_rsa, 0));
-    { PhaseScope ps(T, slot, PH_PREP, st);
-      HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st)); }
+    if (!lay.is_ecdsa) {
+      PhaseScope ps(T, slot, PH_PREP, st);
+      HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st));
+    }
     if ((rc = emit(E_BITS, st))) return rc;
     if ((rc = emit(E_GENR, st))) return rc;
     for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));

@@ -67,6 +67,8 @@ PARAM_SETS = [
     dict(I.CANONICAL, aa=0),                       # no active authentication
     dict(I.CANONICAL, ec_blocks=5, ec_shift=640),  # longer encapsulated content
     dict(I.CANONICAL, sig=2),                      # RSA-4096 (K = 64 limbs)
+    dict(I.CANONICAL, sig=20),                     # ECDSA secp256r1
+    dict(I.CANONICAL, sig=20, aa=0, doc=1),        # ECDSA, TD1, no AA
 ]
 
 
@@ -97,7 +99,7 @@ def test_small_circuit_layouts(oracle):
 
 
 def test_unsupported_params_rejected():
-    rc, _, _ = layout_sizes(dict(I.CANONICAL, sig=20))
+    rc, _, _ = layout_sizes(dict(I.CANONICAL, sig=21))  # brainpoolP256r1: not built yet
     assert rc == -2
     assert b"SIGNATURE_TYPE" in native.lib().pzk_last_error()
     rc, _, _ = layout_sizes(dict(I.CANONICAL, dg1_shift=2000))

@@ -33,23 +33,23 @@ def log(*a):
 
 # ----------------------------------------------------------------------------- inputs
 def _gen_slice(args):
-    seed, lo, hi, n_keys = args
+    seed, lo, hi, n_keys, sig = args
     from pzkwit import inputs as I
-    g = I.PassportGen.shared(seed, n_keys)
+    g = I.PassportGen.shared(seed, n_keys, sig)
     out = np.zeros((hi - lo, g.n_inputs, 32), dtype=np.uint8)
     for k, i in enumerate(range(lo, hi)):
         I.pack_register_inputs(g.passport_at(i), g.params, out=out[k])
     return lo, out
 
 
-def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None):
+def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
     from concurrent.futures import ProcessPoolExecutor
     from pzkwit import inputs as I
     workers = workers or max(1, min(16, os.cpu_count() or 1))
-    I.PassportGen.shared(seed, n_keys)  # keys generated once (parallel inside)
+    I.PassportGen.shared(seed, n_keys, sig)  # keys generated once (parallel inside)
     step = (batch + workers * 4 - 1) // (workers * 4)
-    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys) for lo in range(0, batch, step)]
-    n_in = I.PassportGen.shared(seed, n_keys).n_inputs
+    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig) for lo in range(0, batch, step)]
+    n_in = I.PassportGen.shared(seed, n_keys, sig).n_inputs
     buf = np.zeros((batch, n_in, 32), dtype=np.uint8)
     if workers == 1:
         res = map(_gen_slice, jobs)
@@ -67,8 +67,8 @@ def _cpu_work(args):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     from pzkwit import inputs as I
-    if kind == "register":
-        prm = pyoracle.register_params(**I.CANONICAL)
+    if kind.startswith("register"):
+        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=20 if kind == "register-ecdsa" else 1))
         nin, nw = pyoracle.register_sizes(prm)
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
@@ -97,7 +97,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "sha256"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "sha256"], default="register")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
     ap.add_argument("--cpu-sample", type=int, default=None)
@@ -117,14 +117,20 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.workload == "register":
+    scratch_pw = 1 << 20  # per-witness core scratch (bytes), for the slab sizing below
+    if args.workload.startswith("register"):
+        sig = 20 if args.workload == "register-ecdsa" else 1
         batch = args.batch or 4096
-        inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.CANONICAL)
+        inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, dict(I.CANONICAL, sig=sig))
         t0 = time.time()
-        host_in = make_register_inputs(batch, rank * batch)
+        host_in = make_register_inputs(batch, rank * batch, seed=3 if sig == 1 else 5, sig=sig)
         log("inputs: %d passports generated in %.1fs" % (batch, time.time() - t0))
         metric = "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline"
         workload = "RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports (config 3)"
+        if sig == 20:
+            metric = "registerIdentityBuilder ECDSA-secp256r1 witnesses/sec, batch=4096 (config 5 slice)"
+            workload = "RegisterIdentityBuilder(20,256,3,4,600,248,1,1496,3,256) synthetic P-256 passports"
+            scratch_pw = 10 << 20  # value tables (~8.4 MB) + EC core
     else:
         batch = args.batch or 1024
         inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
@@ -140,7 +146,7 @@ def main():
     else:
         # largest slab that fits next to the inputs and the per-witness core scratch (~1 MB/witness),
         # rounded down to an even split of the batch
-        fit = max(1, int((free * 0.85 - host_in.nbytes) // (stride + (1 << 20))))
+        fit = max(1, int((free * 0.85 - host_in.nbytes) // (stride + scratch_pw)))
         parts = 1
         while (batch + parts - 1) // parts > fit:
             parts += 1
@@ -196,7 +202,7 @@ def main():
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
     tfiles = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json")))
-    if tfiles and args.workload == "register":
+    if tfiles and args.workload == "register":  # PMC traffic is committed for the config-3 kernels
         tj = json.load(open(tfiles[-1]))
         ks = [tj["kernels"].get(k) for k in info[dom][0].split("+")]
         if all(ks):
@@ -225,9 +231,10 @@ def main():
     }
     if rank == 0 and not args.no_cpu:
         procs = max(1, min(16, os.cpu_count() or 1))
-        if args.workload == "register":
-            ns = args.cpu_sample or 128 * procs
-            rows = make_register_inputs(ns, 10 ** 6, workers=procs)
+        if args.workload.startswith("register"):
+            sig = 20 if args.workload == "register-ecdsa" else 1
+            ns = args.cpu_sample or (128 if sig == 1 else 48) * procs
+            rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=3 if sig == 1 else 5, sig=sig)
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)

@@ -5,9 +5,10 @@
 // per witness, every one a full template instance (EllipticCurveDouble / EllipticCurveAdd,
 // ec/curve.circom:281-345) whose PointOnCurve / PointOnTangent / PointOnLine sub-blocks hold
 // ~7-10 k signals. The path is split into
-//   * k_ec_core   — lane per witness: the scalars (s^-1, u1, u2 mod n) and the whole point chain in
-//                   Jacobian coordinates, then ONE batched inversion that yields every affine
-//                   point; writes an op RECORD (in1, in2, out) per point operation;
+//   * k_ec_scalars / k_ec_chain / k_ec_final — the scalars (s^-1, u1, u2 mod n) and the two point
+//                   chains (lane per (witness, chain)) in Jacobian coordinates;
+//   * k_ec_affine / k_ec_link / k_ec_inv — lane-parallel: affine points (one inversion per 8 ops),
+//                   an op RECORD (in1, in2, out) per point operation, the IsEqual inverses;
 //   * k_ec_table  — lane per (witness, op): the op's template walker (ec_walk.hpp) expands the
 //                   record into a VALUE TABLE (every distinct non-bit signal value, Fr normal form);
 //   * k_emit_ect  — workgroup per (witness, op): table -> LDS, then one u32 descriptor per signal
@@ -74,7 +75,7 @@ constexpr int EC_CORE_WORDS = ECC_REC + EC_N_OPS * ECC_REC_WORDS;
 // scalarMult isZeroResult[64], isZeroAddition[1..63]
 constexpr int ECI_GM = 0, ECI_SM_ZR = 124, ECI_SM_ZA = 188, EC_N_INV = 251;
 // Jacobian scratch of k_ec_core per witness (u64): X, Y, Z per op + prefix products
-constexpr int EC_JAC_WORDS = EC_N_OPS * 16;
+constexpr int EC_JAC_WORDS = EC_N_OPS * 16 + 112;
 
 // ---- table-block descriptor: op (3) | bit (9) | entry (20)
 enum : uint32_t { ECD_ZERO = 0, ECD_COPY = 1, ECD_BIT = 2, ECD_MASK = 3 };
@@ -82,6 +83,8 @@ __host__ __device__ constexpr uint32_t ecd(uint32_t op, uint32_t idx, uint32_t b
   return (op << 29) | (bit << 20) | idx;
 }
 enum EcType { ECT_DBL = 0, ECT_ADD = 1, ECT_MM = 2, ECT_N = 3 };
+
+
 
 // template sizes (ec/curve.circom; oracle/ecdsa_p256.inc.c derives them independently)
 __host__ __device__ constexpr uint32_t ec_n2b(int L) { return 2 * L + 1; }

@@ -5,7 +5,7 @@
 #include "ec_walk.hpp"
 #include "fr.hpp"
 #include "layout.hpp"
-#include "regcore.hpp"
+#include "core_util.hpp"
 
 namespace pzk {
 
@@ -251,6 +251,7 @@ struct ModP {
   static constexpr uint32_t e[8] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0x00000000u,
                                     0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
   static constexpr uint32_t minv = 1u;
+  static constexpr bool is_p = true;
 };
 struct ModN {
   static constexpr uint32_t m[8] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
@@ -262,7 +263,10 @@ struct ModN {
   static constexpr uint32_t e[8] = {0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
                                     0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
   static constexpr uint32_t minv = 0xee00bc4fu;
+  static constexpr bool is_p = false;
 };
+using ModPFwd = ModP;
+using ModNFwd = ModN;
 
 template <class M> __device__ __forceinline__ e8 m_const(const uint32_t (&c)[8]) { e8 r; for (int i = 0; i < 8; i++) r.v[i] = c[i]; return r; }
 // r = t - m if t >= m (t < 2m, t given with a carry word)
@@ -276,7 +280,7 @@ template <class M> __device__ __forceinline__ e8 m_reduce(const uint32_t* t, uin
   for (int i = 0; i < 8; i++) r.v[i] = t[i];
   return r;
 }
-template <class M> __device__ __forceinline__ e8 m_mul(const e8& a, const e8& b) {
+template <class M> __device__ __forceinline__ e8 m_mul_inl(const e8& a, const e8& b) {
   uint32_t t[10];
 #pragma unroll
   for (int j = 0; j < 10; j++) t[j] = 0;
@@ -293,6 +297,13 @@ template <class M> __device__ __forceinline__ e8 m_mul(const e8& a, const e8& b)
     s = (uint64_t)t[8] + C; t[7] = (uint32_t)s; t[8] = t[9] + (uint32_t)(s >> 32);
   }
   return m_reduce<M>(t, t[8]);
+}
+// Out of line: the point chains are long straight-line sequences of products; inlining every
+// 128-mad product makes k_ec_chain ~40 k instructions and instruction-fetch bound.
+__device__ __noinline__ e8 m_mul_p(e8 a, e8 b) { return m_mul_inl<ModPFwd>(a, b); }
+__device__ __noinline__ e8 m_mul_n(e8 a, e8 b) { return m_mul_inl<ModNFwd>(a, b); }
+template <class M> __device__ __forceinline__ e8 m_mul(const e8& a, const e8& b) {
+  if constexpr (M::is_p) return m_mul_p(a, b); else return m_mul_n(a, b);
 }
 template <class M> __device__ __forceinline__ e8 m_add(const e8& a, const e8& b) {
   uint32_t t[8]; uint64_t c = 0;
@@ -377,6 +388,25 @@ __device__ Jac jac_add(const Jac& P, const Jac& Q) {
   return R;
 }
 
+// madd-2007-bl: Q affine (Z2 = 1), 7M + 4S
+__device__ Jac jac_add_aff(const Jac& P, const e8& x2, const e8& y2) {
+  using M = ModP;
+  e8 z1z1 = m_mul<M>(P.z, P.z);
+  e8 u2 = m_mul<M>(x2, z1z1), s2 = m_mul<M>(m_mul<M>(y2, P.z), z1z1);
+  e8 h = m_sub<M>(u2, P.x), hh = m_mul<M>(h, h);
+  e8 i = m_add<M>(hh, hh); i = m_add<M>(i, i);
+  e8 j = m_mul<M>(h, i);
+  e8 r = m_sub<M>(s2, P.y); r = m_add<M>(r, r);
+  e8 v = m_mul<M>(P.x, i);
+  Jac R;
+  R.x = m_sub<M>(m_sub<M>(m_mul<M>(r, r), j), m_add<M>(v, v));
+  e8 yj = m_mul<M>(P.y, j);
+  R.y = m_sub<M>(m_mul<M>(r, m_sub<M>(v, R.x)), m_add<M>(yj, yj));
+  e8 zh = m_add<M>(P.z, h);
+  R.z = m_sub<M>(m_sub<M>(m_mul<M>(zh, zh), z1z1), hh);
+  return R;
+}
+
 // ============================================================ k_ec_core
 // handles of points: >= 0 op output; H_D dummy point; H_Q public key; <= -1000 fixed-base table entry
 constexpr int H_D = -1, H_Q = -2;
@@ -440,43 +470,55 @@ __device__ __forceinline__ fr fr_diff_u64(uint64_t a, uint64_t b) {
   return a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
 }
 
-// lane = witness
-__global__ void __launch_bounds__(64) k_ec_core(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
-                                                uint64_t* ec_core, uint64_t* ec_jac, fr* ec_inv, int32_t* status,
-                                                uint32_t batch) {
+// ---- k_ec_core scratch per witness (u64): per op X, Y, Z (Montgomery) + input handles; then the
+// handles of the forwarded points (gm_ap[32], gm_rp[31], pre[16], sm_ap[64], sm_rp[65])
+constexpr int ECJ_OP = 16, ECJ_PTS = EC_N_OPS * ECJ_OP, EC_N_PTS = 32 + 31 + 16 + 64 + 65;
+__host__ __device__ constexpr int ec_pt_index(int kind, int i) {
+  return kind == PT_GM_AP ? i : kind == PT_GM_RP ? 32 + i : kind == PT_PRE ? 63 + i : kind == PT_SM_AP ? 79 + i : 143 + i;
+}
+__host__ __device__ constexpr int ec_pt_base(int idx) {  // EC core word of forwarded point idx
+  return idx < 32 ? ECC_GM_AP + 8 * idx : idx < 63 ? ECC_GM_RP + 8 * (idx - 32) : idx < 79 ? ECC_PRE + 8 * (idx - 63)
+       : idx < 143 ? ECC_SM_AP + 8 * (idx - 79) : ECC_SM_RP + 8 * (idx - 143);
+}
+static_assert(EC_JAC_WORDS >= ECJ_PTS + (EC_N_PTS + 1) / 2, "EC Jacobian scratch");
+
+__device__ __forceinline__ void ec_aff_const(const DevLayout& L, const uint8_t* row, int hd, uint64_t* xy) {
+  if (hd == H_D) { for (int i = 0; i < 8; i++) xy[i] = EC_D[i]; }
+  else if (hd == H_Q) { for (int i = 0; i < 8; i++) xy[i] = *reinterpret_cast<const uint64_t*>(row + 32ull * (L.reg.in_pk + i)); }
+  else {
+    const uint64_t* T = L.ec_gpow + (size_t)(-hd - 1000) * 8;
+    for (int i = 0; i < 8; i++) xy[i] = T[i];
+  }
+}
+
+// Phase 0, lane = witness: the scalars mod n and the BigMultModP records
+__global__ void __launch_bounds__(64) k_ec_scalars(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
+                                                   uint64_t* ec_core, int32_t* status, uint32_t batch) {
   core_priority();
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
   const RegInfo& G = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
-  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
   int32_t* st = status ? status + w : nullptr;
   bool bad = false;
-  uint64_t r[4], s[4], q[8], h[4];
+  uint64_t r[4], s[4], h[4];
   for (int i = 0; i < 4; i++) {
     const uint8_t* a = row + 32ull * (G.in_sig + i);
     const uint8_t* b = row + 32ull * (G.in_sig + 4 + i);
     bad |= !in_is_u64(a) || !in_is_u64(b);
     r[i] = in_u64(a); s[i] = in_u64(b);
   }
-  for (int i = 0; i < 8; i++) {
-    const uint8_t* a = row + 32ull * (G.in_pk + i);
-    bad |= !in_is_u64(a);
-    q[i] = in_u64(a);
-  }
+  for (int i = 0; i < 8; i++) bad |= !in_is_u64(row + 32ull * (G.in_pk + i));
   if (bad) set_status(st, ST_INPUT_RANGE);
   {  // hashedChunked[j] (ecdsa.circom:30-38): 64-bit big-endian digest words, least significant first
     const ShaJob job = L.sha[G.j_sa];
     const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
     for (int j = 0; j < 4; j++) h[j] = ((uint64_t)H[2 * (3 - j)] << 32) | H[2 * (3 - j) + 1];
   }
-  // ---- scalars mod n: sinv = s^-1 (BigModInv, bigInt.circom:344-368), u1 = sinv h, u2 = sinv r
+  // sinv = s^-1 (BigModInv, bigInt.circom:344-368), u1 = sinv h, u2 = sinv r (mod n)
   using N = ModN;
-  auto red_n = [&](const uint64_t* x) {  // x mod n for x < 2^256 (< 2n)
-    e8 a = e8_from_u64(x);
-    return m_reduce<N>(a.v, 0);
-  };
+  auto red_n = [&](const uint64_t* x) { e8 a = e8_from_u64(x); return m_reduce<N>(a.v, 0); };
   const e8 sm = m_to<N>(red_n(s)), sinv_m = m_inv<N>(sm);
   const e8 u1 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(h))));
   const e8 u2 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(r))));
@@ -496,126 +538,226 @@ __global__ void __launch_bounds__(64) k_ec_core(DevLayout L, const uint8_t* inpu
     C[ECC_MM + 8 * EC_MM_U1 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U1 + 4 + i] = h[i];
     C[ECC_MM + 8 * EC_MM_U2 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U2 + 4 + i] = r[i];
   }
-  // ---- point chain, Jacobian (phase 1)
-  auto aff_const = [&](int hd, uint64_t* xy) {
-    if (hd == H_D) { for (int i = 0; i < 8; i++) xy[i] = EC_D[i]; }
-    else if (hd == H_Q) { for (int i = 0; i < 8; i++) xy[i] = q[i]; }
-    else {
-      const int t = -hd - 1000;
-      const uint64_t* T = L.ec_gpow + (size_t)t * 8;
-      for (int i = 0; i < 8; i++) xy[i] = T[i];
+}
+
+__device__ __forceinline__ void jac_store(uint64_t* d, const Jac& R, int h1, int h2) {
+  e8_to_u64(R.x, d); e8_to_u64(R.y, d + 4); e8_to_u64(R.z, d + 8);
+  d[12] = (uint64_t)(uint32_t)h1 | ((uint64_t)(uint32_t)h2 << 32);
+}
+__device__ __forceinline__ Jac jac_load(const uint64_t* s0) {
+  Jac P; P.x = e8_from_u64(s0); P.y = e8_from_u64(s0 + 4); P.z = e8_from_u64(s0 + 8); return P;
+}
+__device__ __forceinline__ Jac jac_of_aff(const uint64_t* xy) {
+  Jac P; P.x = m_to<ModP>(e8_from_u64(xy)); P.y = m_to<ModP>(e8_from_u64(xy + 4)); P.z = m_const<ModP>(ModP::r1); return P;
+}
+
+// Phase 1, lane = (witness, chain): chain 0 = the generator multiplication (ops 0..31,
+// curve.circom:672-906), chain 1 = precompute + the window-4 scalar multiplication of the public
+// key (ops 32..360, curve.circom:249-494). Jacobian coordinates, the running point in registers,
+// mixed additions for affine operands; every op's result and input handles go to the scratch.
+// The isDummy decisions compare handles (see ec_plan).
+__global__ void __launch_bounds__(64) k_ec_chain(DevLayout L, const uint8_t* inputs, const uint64_t* ec_core,
+                                                 uint64_t* ec_jac, uint32_t batch) {
+  core_priority();
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = gid >> 1, chain = gid & 1;
+  if (w >= batch) return;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
+  int32_t* pts = reinterpret_cast<int32_t*>(J + ECJ_PTS);
+  using M = ModP;
+  if (chain == 0) {
+    uint64_t u1[4];
+    for (int i = 0; i < 4; i++) u1[i] = C[ECC_U1 + i];
+    auto gm_ap = [&](int i) {
+      int b = (int)((u1[i >> 3] >> (8 * (i & 7))) & 255);
+      return b ? h_tab(i, b) : (i % 2 == 0 ? H_D : EC_OP_SD);
+    };
+    uint64_t dxy[8];
+    for (int i = 0; i < 8; i++) dxy[i] = EC_D[i];
+    const Jac D = jac_of_aff(dxy);
+    const Jac SD = jac_dbl(D);
+    jac_store(J + ECJ_OP * EC_OP_SD, SD, H_D, 0);
+    for (int i = 0; i < 32; i++) pts[ec_pt_index(PT_GM_AP, i)] = gm_ap(i);
+    auto point = [&](int hd) -> Jac {  // D, 2D or a table entry
+      if (hd == H_D) return D;
+      if (hd == EC_OP_SD) return SD;
+      return jac_of_aff(L.ec_gpow + (size_t)(-hd - 1000) * 8);
+    };
+    int left = gm_ap(0);
+    Jac acc = point(left);
+    for (int i = 0; i < 31; i++) {
+      const int right = gm_ap(i + 1);
+      Jac R;
+      if (right <= -1000) {
+        const uint64_t* T = L.ec_gpow + (size_t)(-right - 1000) * 8;
+        R = jac_add_aff(acc, m_to<M>(e8_from_u64(T)), m_to<M>(e8_from_u64(T + 4)));
+      } else {
+        R = jac_add(acc, right == H_D ? D : SD);
+      }
+      jac_store(J + ECJ_OP * ec_op_gm_add(i), R, left, right);
+      const bool ld = left == H_D || left == EC_OP_SD, rd = right == H_D || right == EC_OP_SD;
+      const int rp = ld ? right : rd ? left : ec_op_gm_add(i);
+      if (ld) acc = point(right);
+      else if (!rd) acc = R;
+      pts[ec_pt_index(PT_GM_RP, i)] = rp;
+      left = rp;
     }
-  };
-  auto get_jac = [&](int hd) {
-    Jac P;
-    if (hd >= 0) {
-      const uint64_t* s0 = J + 16 * hd;
-      P.x = e8_from_u64(s0); P.y = e8_from_u64(s0 + 4); P.z = e8_from_u64(s0 + 8);
-    } else {
-      uint64_t xy[8];
-      aff_const(hd, xy);
-      P.x = m_to<ModP>(e8_from_u64(xy)); P.y = m_to<ModP>(e8_from_u64(xy + 4)); P.z = m_const<ModP>(ModP::r1);
+  } else {
+    uint64_t u2[4], qxy[8], dxy[8];
+    for (int i = 0; i < 4; i++) u2[i] = C[ECC_U2 + i];
+    ec_aff_const(L, row, H_Q, qxy);
+    for (int i = 0; i < 8; i++) dxy[i] = EC_D[i];
+    const Jac Q = jac_of_aff(qxy), D = jac_of_aff(dxy);
+    const e8 qx = Q.x, qy = Q.y;
+    auto pre = [](int i) { return i == 0 ? H_D : i == 1 ? H_Q : ec_op_pre(i); };
+    auto pre_jac = [&](int i) -> Jac { return i == 0 ? D : i == 1 ? Q : jac_load(J + ECJ_OP * ec_op_pre(i)); };
+    pts[ec_pt_index(PT_PRE, 0)] = H_D;
+    pts[ec_pt_index(PT_PRE, 1)] = H_Q;
+    for (int i = 2; i < 16; i++) {
+      Jac R;
+      if (i % 2 == 0) { R = jac_dbl(pre_jac(i / 2)); jac_store(J + ECJ_OP * ec_op_pre(i), R, pre(i / 2), 0); }
+      else { R = jac_add_aff(pre_jac(i - 1), qx, qy); jac_store(J + ECJ_OP * ec_op_pre(i), R, H_Q, pre(i - 1)); }
+      pts[ec_pt_index(PT_PRE, i)] = ec_op_pre(i);
     }
-    return P;
-  };
-  ec_plan(U1, U2,
-          [&](int op, int h1, int h2) {
-            Jac P = get_jac(h1);
-            Jac R = ec_op_is_dbl(op) ? jac_dbl(P) : jac_add(P, get_jac(h2));
-            uint64_t* d = J + 16 * op;
-            e8_to_u64(R.x, d); e8_to_u64(R.y, d + 4); e8_to_u64(R.z, d + 8);
-          },
-          [](int, int, int) {});
-  // ---- one batched inversion of every Z (phase 2), affine outputs into the op records
-  {
-    using M = ModP;
-    e8 acc = m_const<M>(M::r1);
-    bool degenerate = false;
-    for (int op = 0; op < EC_N_OPS; op++) {
-      uint64_t* d = J + 16 * op;
-      e8_to_u64(acc, d + 12);
-      e8 z = e8_from_u64(d + 8);
-      if (m_is_zero<M>(z)) degenerate = true;
-      else acc = m_mul<M>(acc, z);
-    }
-    if (degenerate) set_status(st, ST_BIGISZERO);  // dx = 0 or y = 0: the affine formulas divide by 0
-    e8 inv = m_inv<M>(acc);
-    for (int op = EC_N_OPS - 1; op >= 0; op--) {
-      uint64_t* d = J + 16 * op;
-      e8 z = e8_from_u64(d + 8);
-      uint64_t* o = C + ECC_REC + ECC_REC_WORDS * op + 16;
-      if (m_is_zero<M>(z)) { for (int i = 0; i < 8; i++) o[i] = 0; continue; }
-      e8 zi = m_mul<M>(inv, e8_from_u64(d + 12));
-      inv = m_mul<M>(inv, z);
-      e8 zi2 = m_mul<M>(zi, zi), zi3 = m_mul<M>(zi2, zi);
-      e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d), zi2)), o);
-      e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d + 4), zi3)), o + 4);
+    auto nib = [&](int w4) { int b = 252 - 4 * w4; return (int)((u2[b >> 6] >> (b & 63)) & 15); };
+    pts[ec_pt_index(PT_SM_RP, 0)] = H_D;
+    int rp = pre(nib(0));
+    Jac rpv = pre_jac(nib(0));
+    pts[ec_pt_index(PT_SM_AP, 0)] = rp;
+    pts[ec_pt_index(PT_SM_RP, 1)] = rp;
+    for (int w4 = 1; w4 < 64; w4++) {
+      const int n = nib(w4), ap = pre(n);
+      pts[ec_pt_index(PT_SM_AP, w4)] = ap;
+      const bool izr = rp == H_D, iza = ap == H_D;
+      Jac d = izr ? D : rpv;
+      int hin = izr ? H_D : rp;
+      for (int j = 0; j < 4; j++) {
+        const int op = ec_op_sm_dbl(4 * w4 - 4 + j);
+        d = jac_dbl(d);
+        jac_store(J + ECJ_OP * op, d, hin, 0);
+        hin = op;
+      }
+      const int dl = ec_op_sm_dbl(4 * w4 - 1), ad = ec_op_sm_add(w4 - 1);
+      Jac R = n == 1 ? jac_add_aff(d, qx, qy) : jac_add(d, pre_jac(n));
+      jac_store(J + ECJ_OP * ad, R, dl, ap);
+      if (izr) { rp = ap; rpv = pre_jac(n); }
+      else if (iza) { rp = dl; rpv = d; }
+      else { rp = ad; rpv = R; }
+      pts[ec_pt_index(PT_SM_RP, w4 + 1)] = rp;
     }
   }
-  // ---- records' inputs and the forwarded points (phase 3)
+}
+
+// Phase 1b, lane = witness: verifyECDSABits.add (op 361) of the two chains' results
+__global__ void __launch_bounds__(64) k_ec_final(uint64_t* ec_jac, uint32_t batch) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= batch) return;
+  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
+  const int32_t* pts = reinterpret_cast<const int32_t*>(J + ECJ_PTS);
+  const int h1 = pts[ec_pt_index(PT_GM_RP, 30)], h2 = pts[ec_pt_index(PT_SM_RP, 64)];
+  // both are op outputs (a forwarded dummy would need an all-zero scalar, which fails BigModInv /
+  // the final check anyway): fall back to zero points otherwise
+  Jac P = h1 >= 0 ? jac_load(J + ECJ_OP * h1) : Jac{}, Q = h2 >= 0 ? jac_load(J + ECJ_OP * h2) : Jac{};
+  jac_store(J + ECJ_OP * EC_OP_FINAL, jac_add(P, Q), h1, h2);
+}
+
+// Phase 2, lane = (witness, group of 8 ops): affine out = (X / Z^2, Y / Z^3), one inversion per group
+constexpr int EC_AFF_GROUP = 8, EC_AFF_GROUPS = (EC_N_OPS + EC_AFF_GROUP - 1) / EC_AFF_GROUP;
+__global__ void __launch_bounds__(64) k_ec_affine(uint64_t* ec_core, const uint64_t* ec_jac, int32_t* status, uint32_t batch) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = gid / EC_AFF_GROUPS, g = gid % EC_AFF_GROUPS;
+  if (w >= batch) return;
+  using M = ModP;
+  const uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
+  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  const int op0 = g * EC_AFF_GROUP, n = min(EC_AFF_GROUP, EC_N_OPS - op0);
+  e8 pre[EC_AFF_GROUP];
+  e8 acc = m_const<M>(M::r1);
+  bool degenerate = false;
+  for (int k = 0; k < n; k++) {
+    pre[k] = acc;
+    e8 z = e8_from_u64(J + ECJ_OP * (op0 + k) + 8);
+    if (m_is_zero<M>(z)) degenerate = true;
+    else acc = m_mul<M>(acc, z);
+  }
+  if (degenerate && status) lane_status(status + w, ST_BIGISZERO);  // dx = 0 or y = 0: the affine formulas divide by 0
+  e8 inv = m_inv<M>(acc);
+  for (int k = n - 1; k >= 0; k--) {
+    const uint64_t* d = J + ECJ_OP * (op0 + k);
+    uint64_t* o = C + ECC_REC + ECC_REC_WORDS * (op0 + k) + 16;
+    e8 z = e8_from_u64(d + 8);
+    if (m_is_zero<M>(z)) { for (int i = 0; i < 8; i++) o[i] = 0; continue; }
+    e8 zi = m_mul<M>(inv, pre[k]);
+    inv = m_mul<M>(inv, z);
+    e8 zi2 = m_mul<M>(zi, zi), zi3 = m_mul<M>(zi2, zi);
+    e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d), zi2)), o);
+    e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d + 4), zi3)), o + 4);
+  }
+}
+
+// Phase 3, lane = (witness, item): op records' inputs (items < 362), forwarded points (next 208),
+// and the final x1 mod n === r check + modOrder record (last item)
+constexpr int EC_LINK_ITEMS = EC_N_OPS + EC_N_PTS + 1;
+__global__ void __launch_bounds__(64) k_ec_link(DevLayout L, const uint8_t* inputs, uint64_t* ec_core, const uint64_t* ec_jac,
+                                                int32_t* status, uint32_t batch) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = gid / EC_LINK_ITEMS;
+  const int it = (int)(gid % EC_LINK_ITEMS);
+  if (w >= batch) return;
+  const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+  const uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
+  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
   auto aff = [&](int hd, uint64_t* xy) {
     if (hd >= 0) { const uint64_t* o = C + ECC_REC + ECC_REC_WORDS * hd + 16; for (int i = 0; i < 8; i++) xy[i] = o[i]; }
-    else aff_const(hd, xy);
+    else ec_aff_const(L, row, hd, xy);
   };
-  int gm_out = 0, sm_out = 0;
-  ec_plan(U1, U2,
-          [&](int op, int h1, int h2) {
-            uint64_t* rc = C + ECC_REC + ECC_REC_WORDS * op;
-            aff(h1, rc);
-            if (ec_op_is_dbl(op)) { for (int i = 0; i < 8; i++) rc[8 + i] = 0; }
-            else aff(h2, rc + 8);
-            if (op == EC_OP_FINAL) { gm_out = h1; sm_out = h2; }
-          },
-          [&](int kind, int i, int hd) {
-            int base = kind == PT_GM_AP ? ECC_GM_AP : kind == PT_GM_RP ? ECC_GM_RP : kind == PT_PRE ? ECC_PRE
-                     : kind == PT_SM_AP ? ECC_SM_AP : ECC_SM_RP;
-            aff(hd, C + base + 8 * i);
-          });
-  (void)gm_out; (void)sm_out;
-  // ---- x1 mod n === r (ecdsa.circom:81-83); modOrder record
-  {
+  if (it < EC_N_OPS) {
+    const uint64_t hh = J[ECJ_OP * it + 12];
+    uint64_t* rc = C + ECC_REC + ECC_REC_WORDS * it;
+    aff((int32_t)(uint32_t)hh, rc);
+    if (ec_op_is_dbl(it)) { for (int i = 0; i < 8; i++) rc[8 + i] = 0; }
+    else aff((int32_t)(uint32_t)(hh >> 32), rc + 8);
+  } else if (it < EC_N_OPS + EC_N_PTS) {
+    const int idx = it - EC_N_OPS;
+    aff(reinterpret_cast<const int32_t*>(J + ECJ_PTS)[idx], C + ec_pt_base(idx));
+  } else {  // x1 mod n === r (ecdsa.circom:81-83); modOrder record
     const uint64_t* x1 = C + ECC_REC + ECC_REC_WORDS * EC_OP_FINAL + 16;
-    e8 xm = red_n(x1);
+    e8 xm = m_reduce<ModN>(e8_from_u64(x1).v, 0);
     uint64_t xr[4];
     e8_to_u64(xm, xr);
     bool ok = true;
     for (int i = 0; i < 4; i++) {
-      ok &= xr[i] == r[i];
+      ok &= xr[i] == *reinterpret_cast<const uint64_t*>(row + 32ull * (L.reg.in_sig + i));
       C[ECC_MM + 8 * EC_MM_XN + i] = x1[i];
       C[ECC_MM + 8 * EC_MM_XN + 4 + i] = i == 0 ? 1 : 0;
     }
-    if (!ok) set_status(st, ST_ECDSA_R);
+    if (!ok && status) lane_status(status + w, ST_ECDSA_R);
   }
-  // ---- IsEqual inverses (phase 4): genmult dummy tests, scalarMult isZeroResult / isZeroAddition
-  {
-    fr* I = ec_inv + (size_t)w * EC_N_INV;
-    const uint64_t dx = EC_D[0], sdx = C[ECC_REC + ECC_REC_WORDS * EC_OP_SD + 16];
-    for (int i = 0; i < 31; i++) {
-      const uint64_t lx = i == 0 ? C[ECC_GM_AP] : C[ECC_GM_RP + 8 * (i - 1)], rx = C[ECC_GM_AP + 8 * (i + 1)];
-      I[ECI_GM + 4 * i + 0] = fr_to_mont(fr_diff_u64(lx, dx));
-      I[ECI_GM + 4 * i + 1] = fr_to_mont(fr_diff_u64(lx, sdx));
-      I[ECI_GM + 4 * i + 2] = fr_to_mont(fr_diff_u64(rx, dx));
-      I[ECI_GM + 4 * i + 3] = fr_to_mont(fr_diff_u64(rx, sdx));
-    }
-    for (int k = 0; k < 64; k++) I[ECI_SM_ZR + k] = fr_to_mont(fr_diff_u64(dx, C[ECC_SM_RP + 8 * k]));
-    for (int k = 1; k < 64; k++) I[ECI_SM_ZA + k - 1] = fr_to_mont(fr_diff_u64(dx, C[ECC_SM_AP + 8 * k]));
-    // Montgomery's trick over the 251 differences (0 stays 0: IsZero's inv, comparators.circom:17)
-    fr* pre = reinterpret_cast<fr*>(J);
-    fr acc = fr_mont_one();
-    for (int i = 0; i < EC_N_INV; i++) {
-      pre[i] = acc;
-      fr x = I[i];
-      if (!fr_is_zero(x)) acc = fr_mul(acc, x);
-    }
-    fr inv = fr_inv(acc);
-    for (int i = EC_N_INV - 1; i >= 0; i--) {
-      fr x = I[i];
-      if (fr_is_zero(x)) continue;
-      I[i] = fr_mul(inv, pre[i]);
-      inv = fr_mul(inv, x);
-    }
-    for (int i = 0; i < EC_N_INV; i++) I[i] = fr_from_mont(I[i]);
+}
+
+// Phase 4, lane = (witness, j): IsEqual inverses (genmult dummy tests, scalarMult isZeroResult /
+// isZeroAddition) of the differences in[1] - in[0]; 0 -> 0 (comparators.circom:17)
+__global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_inv, uint32_t batch) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = gid / EC_N_INV;
+  const int j = (int)(gid % EC_N_INV);
+  if (w >= batch) return;
+  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  const uint64_t dx = EC_D[0];
+  fr d;
+  if (j < ECI_SM_ZR) {
+    const int i = j >> 2, k = j & 3;
+    const uint64_t lx = i == 0 ? C[ECC_GM_AP] : C[ECC_GM_RP + 8 * (i - 1)], rx = C[ECC_GM_AP + 8 * (i + 1)];
+    const uint64_t sdx = C[ECC_REC + ECC_REC_WORDS * EC_OP_SD + 16];
+    d = fr_diff_u64(k < 2 ? lx : rx, (k & 1) ? sdx : dx);
+  } else if (j < ECI_SM_ZA) {
+    d = fr_diff_u64(dx, C[ECC_SM_RP + 8 * (j - ECI_SM_ZR)]);
+  } else {
+    d = fr_diff_u64(dx, C[ECC_SM_AP + 8 * (j - ECI_SM_ZA + 1)]);
   }
+  ec_inv[(size_t)w * EC_N_INV + j] = fr_is_zero(d) ? d : fr_from_mont(fr_inv(fr_to_mont(d)));
 }
 
 // ============================================================ k_ec_table: lane per (witness, op)

@@ -41,7 +41,9 @@ struct EcWalk {
   // out[G+L-1] | in1[G], in2[L] | tmpMults[G][L], tmpResult[G+L-1][L]
   // column i sums tmpMults[a][j] (a + j = i) with a descending; every product is materialised
   // in the column that consumes it.
-  __host__ __device__ void bmneq(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+  // f(i, out[i]) is called per output column, so callers can consume columns without an array
+  template <class F>
+  __host__ __device__ void bmneq_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
     const uint32_t i1 = b + G + L - 1, i2 = i1 + G, tm = i2 + L, tr = tm + G * L;
     for (int i = 0; i < G; i++) c.cp(i1 + i, in1[i]);
     for (int j = 0; j < L; j++) c.cp(i2 + j, in2[j]);
@@ -55,16 +57,22 @@ struct EcWalk {
         else s = c.put(tr + i * L + k, c.add(s, p));
       }
       c.cp(b + i, s);
-      out[i] = s;
+      f(i, s);
     }
+  }
+  __host__ __device__ void bmneq(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+    bmneq_cb(b, G, L, in1, in2, [&](int i, const V& s) { out[i] = s; });
   }
   // BigMultOverflow(G,L) bigIntOverflow.circom:38-72 (schoolbook for these sizes):
   // out[G+L-1] | in1[G], in2[L] | mult
-  __host__ __device__ void bmo(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+  template <class F>
+  __host__ __device__ void bmo_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
     for (int i = 0; i < G; i++) c.cp(b + G + L - 1 + i, in1[i]);
     for (int j = 0; j < L; j++) c.cp(b + 2 * G + L - 1 + j, in2[j]);
-    bmneq(b + 2 * G + 2 * L - 1, G, L, in1, in2, out);
-    for (int i = 0; i < G + L - 1; i++) c.cp(b + i, out[i]);
+    bmneq_cb(b + 2 * G + 2 * L - 1, G, L, in1, in2, [&](int i, const V& s) { c.cp(b + i, s); f(i, s); });
+  }
+  __host__ __device__ void bmo(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+    bmo_cb(b, G, L, in1, in2, [&](int i, const V& s) { out[i] = s; });
   }
   // ScalarMultOverflow(N) bigIntOverflow.circom:101-111: out[N] | in[N], scalar
   __host__ __device__ void smo(uint32_t b, int N, const V* in, uint64_t k, V* out) {
@@ -112,10 +120,13 @@ struct EcWalk {
 
   // BigIntIsZeroModP(64,MAX,CN,MCN,4) bigIntComparators.circom:158-212:
   // in[CN], modulus[4] | sign, k[DIV] | kRangeChecks[DIV], mult, isZero, swicher[CN]
+  // The columns of mult = k * modulus feed the switchers, isZero.in and the carry chain of
+  // BigIntIsZero (bigIntComparators.circom:105-129) as they are produced (no column arrays).
   __host__ __device__ void bizmp(uint32_t b, int MAX, int CN, int MCN, const V* in, const V* mod) {
-    const int DIV = MCN - 3;
+    const int DIV = MCN - 3, LB = MAX + 3 - 64;
     const uint32_t o_mod = b + CN, o_sign = o_mod + 4, o_k = o_sign + 1, o_krc = o_k + DIV,
                    o_mult = o_krc + DIV * ec_n2b(64), o_isz = o_mult + ec_bmo(DIV, 4), o_sw = o_isz + ec_bisz(MAX, MCN);
+    const uint32_t o_carry = o_isz + MCN, o_rc = o_carry + MCN - 1;
     for (int i = 0; i < CN; i++) c.cp(b + i, in[i]);
     for (int i = 0; i < 4; i++) c.cp(o_mod + i, mod[i]);
     V sign, k[10];
@@ -125,22 +136,29 @@ struct EcWalk {
       k[i] = c.put(o_k + i, k[i]);
       n2b(o_krc + i * ec_n2b(64), k[i], 64);
     }
-    V mo[13];
-    bmo(o_mult, DIV, 4, k, mod, mo);
-    // swicher[i]: out[2] | bool, in[2] | aux (switcher.circom:16-26), in = (x, -x), bool = sign
-    V iz[13];
-    for (int i = 0; i < CN; i++) {
-      const uint32_t s = o_sw + 6 * i;
-      V neg = c.put(s + 4, c.neg(in[i]));
-      c.cp(s + 2, sign);
-      c.cp(s + 3, in[i]);
-      c.put(s + 5, c.sel(sign, c.add(neg, neg), c.u64(0)));  // aux = (in1 - in0) * bool
-      c.put(s + 0, c.sel(sign, neg, in[i]));
-      V o1 = c.put(s + 1, c.sel(sign, in[i], neg));
-      iz[i] = c.put(o_isz + i, c.sub(mo[i], o1));
-    }
-    for (int i = CN; i < MCN; i++) iz[i] = c.put(o_isz + i, mo[i]);
-    bisz(o_isz, MAX, MCN, iz);
+    V cy{};
+    bmo_cb(o_mult, DIV, 4, k, mod, [&](int i, const V& m) {
+      V iz;
+      if (i < CN) {  // swicher[i]: out[2] | bool, in[2] | aux (switcher.circom:16-26), in = (x, -x), bool = sign
+        const uint32_t s = o_sw + 6 * i;
+        V neg = c.put(s + 4, c.neg(in[i]));
+        c.cp(s + 2, sign);
+        c.cp(s + 3, in[i]);
+        c.put(s + 5, c.sel(sign, c.add(neg, neg), c.u64(0)));  // aux = (in1 - in0) * bool
+        c.put(s + 0, c.sel(sign, neg, in[i]));
+        V o1 = c.put(s + 1, c.sel(sign, in[i], neg));
+        iz = c.put(o_isz + i, c.sub(m, o1));
+      } else {
+        iz = c.put(o_isz + i, m);
+      }
+      if (i < MCN - 1) {  // carry[i] = (in[i] + carry[i-1]) / 2^64, Num2Bits(LB)(carry + 2^(LB-1))
+        V t = i == 0 ? iz : c.add(iz, cy);
+        cy = c.put(o_carry + i, c.shr64_exact(t));
+        n2b_new(o_rc + i * ec_n2b(LB), c.add(cy, c.pow2(LB - 1)), LB);
+      } else {
+        c.check_zero(c.add(iz, cy));  // bigIntComparators.circom:128
+      }
+    });
   }
 
   // PointOnCurve curve.circom:110-138: in[2][4] | squareX, cubeX, squareY, coefMult, isZeroModP
@@ -148,15 +166,16 @@ struct EcWalk {
     for (int i = 0; i < 8; i++) c.cp(b + i, pt[i]);
     const uint32_t sx = b + 8, cx = sx + ec_bmo(4, 4), sy = cx + ec_bmo(7, 4), cm = sy + ec_bmo(4, 4),
                    iz = cm + ec_bmo(4, 4);
-    V sxo[7], in[10], t[7], A[4], Bc[4], P[4];
-    bmo(sx, 4, 4, pt, pt, sxo);
-    bmo(cx, 7, 4, sxo, pt, in);
-    bmo(sy, 4, 4, pt + 4, pt + 4, t);
-    for (int i = 0; i < 7; i++) in[i] = c.sub(in[i], t[i]);
+    V in[10], A[4], Bc[4], P[4];
+    {
+      V sxo[7];
+      bmo(sx, 4, 4, pt, pt, sxo);
+      bmo(cx, 7, 4, sxo, pt, in);
+    }
+    bmo_cb(sy, 4, 4, pt + 4, pt + 4, [&](int i, const V& v) { in[i] = c.sub(in[i], v); });
     consts4(EC_A, A);
-    bmo(cm, 4, 4, pt, A, t);
+    bmo_cb(cm, 4, 4, pt, A, [&](int i, const V& v) { in[i] = c.add(in[i], v); });
     consts4(EC_B, Bc);
-    for (int i = 0; i < 7; i++) in[i] = c.add(in[i], t[i]);
     for (int i = 0; i < 10; i++) {
       if (i < 4) in[i] = c.add(in[i], Bc[i]);
       in[i] = c.put(iz + i, in[i]);
@@ -181,8 +200,8 @@ struct EcWalk {
     V y2[4], ys[4];
     smo(sm2, 4, p1 + 4, 2, y2);
     bao(ba2, 4, 4, p1 + 4, p2 + 4, ys);
-    bmo(lm, 4, 4, ys, y2, t7);
-    for (int i = 0; i < 10; i++) in[i] = c.put(iz + i, i < 7 ? c.sub(in[i], t7[i]) : in[i]);
+    bmo_cb(lm, 4, 4, ys, y2, [&](int i, const V& v) { in[i] = c.sub(in[i], v); });
+    for (int i = 0; i < 10; i++) in[i] = c.put(iz + i, in[i]);
     bizmp(iz, 200, 10, 13, in, P);
   }
   // PointOnLine curve.circom:204-245: in1, in2, in3 | bigAdd, bigSub, bigSub2, bigSub3, leftMult,
@@ -191,15 +210,14 @@ struct EcWalk {
     for (int i = 0; i < 8; i++) { c.cp(b + i, p1[i]); c.cp(b + 8 + i, p2[i]); c.cp(b + 16 + i, p3[i]); }
     const uint32_t ba = b + 24, s1 = ba + 12, s2 = s1 + 16, s3 = s2 + 16, lm = s3 + 16, rm = lm + ec_bmo(4, 4),
                    iz = rm + ec_bmo(4, 4);
-    V P[4], ys[4], d1[4], d2[4], d3[4], l7[7], r7[7];
+    V P[4], ys[4], d1[4], d2[4], d3[4], l7[7];
     bao(ba, 4, 4, p1 + 4, p3 + 4, ys);
     consts4(EC_P, P);
     bsmo(s1, p2, p1, P, d1);
     bsmo(s2, p2 + 4, p1 + 4, P, d2);
     bsmo(s3, p1, p3, P, d3);
     bmo(lm, 4, 4, ys, d1, l7);
-    bmo(rm, 4, 4, d2, d3, r7);
-    for (int i = 0; i < 7; i++) l7[i] = c.put(iz + i, c.sub(l7[i], r7[i]));
+    bmo_cb(rm, 4, 4, d2, d3, [&](int i, const V& v) { l7[i] = c.put(iz + i, c.sub(l7[i], v)); });
     bizmp(iz, 136, 7, 9, l7, P);
   }
 
@@ -262,14 +280,16 @@ struct EcWalk {
     c.cp(o_le, res);
     V gt = c.put(o_gt, c.sub(c.u64(1), res));
     c.check_one(gt);  // bigInt.circom:245
-    V m2[8];
-    bmneq(o_m2, 5, 4, q, n, m2);
-    for (int i = 0; i < 7; i++) {
-      V v = c.sub(mo[i], m2[i]);
-      if (i < 4) v = c.sub(v, r[i]);
-      m2[i] = c.put(o_isz + i, v);
-    }
-    bisz(o_isz, 132, 7, m2);
+    // mult2 = div * modulus; isZero.in[i] = mult[i] - mult2[i] - mod[i] (bigInt.circom:252-271)
+    V iz[7];
+    bmneq_cb(o_m2, 5, 4, q, n, [&](int i, const V& m2) {
+      if (i < 7) {
+        V v = c.sub(mo[i], m2);
+        if (i < 4) v = c.sub(v, r[i]);
+        iz[i] = c.put(o_isz + i, v);
+      }
+    });
+    bisz(o_isz, 132, 7, iz);
   }
 
   __host__ __device__ void run(int type) {

@@ -9,7 +9,6 @@
 #include "sha.hpp"
 #include "sha_prog.hpp"
 #include "kernels.hpp"
-#include "ec_core.hpp"
 
 namespace pzk {
 
@@ -362,25 +361,6 @@ hipError_t launch_inv_small(fr* out, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
-                          uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st) {
-  hipLaunchKernelGGL(k_ec_core, dim3((batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, ec_core, ec_jac, ec_inv,
-                     status, batch);
-  return hipGetLastError();
-}
-
-hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
-                           uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st) {
-  if (n_ops == 0) return hipSuccess;
-  dim3 g((batch + 63) / 64, n_ops);
-  switch (type) {
-    case ECT_DBL: hipLaunchKernelGGL(k_ec_table<ECT_DBL>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
-    case ECT_ADD: hipLaunchKernelGGL(k_ec_table<ECT_ADD>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
-    default: hipLaunchKernelGGL(k_ec_table<ECT_MM>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,
                        const Bufs& B, uint32_t batch, int max_t, hipStream_t st) {
   if (n_work == 0) return hipSuccess;
@@ -407,7 +387,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
       else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
       break;
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
-    case E_ECT: hipLaunchKernelGGL(k_emit_ect, g, blk, 0, st, L, work, B.ec_tab, B.wtns, B.stride); break;
+    case E_ECT: return launch_emit_ect(L, work, n_work, B, batch, st);
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -42,6 +42,8 @@ hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint3
 hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
                            uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st);
 hipError_t launch_inv_small(fr* out, hipStream_t st);
+hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                           hipStream_t st);
 hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,
                        const Bufs& B, uint32_t batch, int max_t, hipStream_t st);
 

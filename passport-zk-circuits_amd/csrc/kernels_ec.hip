@@ -1,0 +1,50 @@
+// ECDSA secp256r1 kernels (ec_core.hpp) and their launchers; a separate translation unit from
+// kernels.hip so the two compile in parallel.
+#include <hip/hip_runtime.h>
+
+#include "bufs.hpp"
+#include "ec_core.hpp"
+#include "kernels.hpp"
+
+namespace pzk {
+
+#define HIP_TRY(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
+                          uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st) {
+  hipLaunchKernelGGL(k_ec_scalars, dim3((batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, ec_core, status, batch);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_ec_chain, dim3((2 * batch + 63) / 64), dim3(64), 0, st, L, inputs, ec_core, ec_jac, batch);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_ec_final, dim3((batch + 63) / 64), dim3(64), 0, st, ec_jac, batch);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_ec_affine, dim3((batch * EC_AFF_GROUPS + 63) / 64), dim3(64), 0, st, ec_core, ec_jac, status,
+                     batch);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_ec_link, dim3((batch * EC_LINK_ITEMS + 63) / 64), dim3(64), 0, st, L, inputs, ec_core, ec_jac,
+                     status, batch);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_ec_inv, dim3((batch * EC_N_INV + 63) / 64), dim3(64), 0, st, ec_core, ec_inv, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
+                           uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st) {
+  if (n_ops == 0) return hipSuccess;
+  dim3 g((batch + 63) / 64, n_ops);
+  switch (type) {
+    case ECT_DBL: hipLaunchKernelGGL(k_ec_table<ECT_DBL>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
+    case ECT_ADD: hipLaunchKernelGGL(k_ec_table<ECT_ADD>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
+    default: hipLaunchKernelGGL(k_ec_table<ECT_MM>, g, dim3(64), 0, st, L, ops, ec_core, ec_tab, status, batch); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                           hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_emit_ect, dim3(n_work, batch), dim3(256), 0, st, L, work, B.ec_tab, B.wtns, B.stride);
+  return hipGetLastError();
+}
+
+}  // namespace pzk

@@ -225,10 +225,10 @@ class PassportGen:
         self._pkhash = {}
 
     @classmethod
-    def shared(cls, seed=3, n_keys=64):
-        key = (seed, n_keys)
+    def shared(cls, seed=3, n_keys=64, sig=1):
+        key = (seed, n_keys, sig)
         if key not in cls._shared:
-            cls._shared[key] = cls(seed, n_keys)
+            cls._shared[key] = cls(seed, n_keys, params=dict(CANONICAL, sig=sig))
         return cls._shared[key]
 
     @property

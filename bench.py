@@ -97,12 +97,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "register-ecdsa", "sha256"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "sha256", "mixed"], default="register")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.workload == "mixed":
+        return bench_mixed(args)
 
     import torch
     from pzkwit import native, inputs as I
@@ -242,6 +244,117 @@ def main():
         out["cpu_baseline"] = {"value": round(v, 2), "unit": "witnesses/s", "cores": procs, "kind": "port",
                                "sample": "%d witnesses of the same workload on %d processes (%.1fs wall)" % (
                                    ns, procs, cdt)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- config 5
+MIX = ((1, 0.4), (2, 0.3), (20, 0.3))  # RSA-2048 / RSA-4096 / ECDSA secp256r1
+
+
+def bench_mixed(args):
+    """Config 5: a mixed-flow batch (40 % RSA-2048, 30 % RSA-4096, 30 % ECDSA secp256r1, seed 5),
+    --batch witnesses per GPU on average, sharded across ranks by .wtns bytes (pzkwit.mixed),
+    each rank running its flows one instance at a time through a shared output slab."""
+    import torch
+    from pzkwit import native, inputs as I, mixed
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    per_gpu = args.batch or 4096
+    total = per_gpu * world
+    rng = np.random.default_rng(5)
+    sigs = rng.choice([m[0] for m in MIX], size=total, p=[m[1] for m in MIX])
+    flows = {sg: dict(I.CANONICAL, sig=int(sg)) for sg, _ in MIX}
+    costs = [mixed.witness_cost(flows[int(sg)]) for sg in sigs]
+    lo, hi = mixed.shard_by_cost(costs, world, rank)
+    t0 = time.time()
+    groups = {}
+    for i in range(lo, hi):
+        groups.setdefault(int(sigs[i]), []).append(i)
+    n_keys = {1: 64, 2: 8, 20: 64}
+    host = {}
+    for sg, idx in groups.items():
+        from concurrent.futures import ProcessPoolExecutor
+        workers = max(1, min(16, os.cpu_count() or 1))
+        I.PassportGen.shared(5, n_keys[sg], sg)
+        n_in = I.PassportGen.shared(5, n_keys[sg], sg).n_inputs
+        buf = np.zeros((len(idx), n_in, 32), dtype=np.uint8)
+        step = max(1, (len(idx) + workers * 4 - 1) // (workers * 4))
+        jobs = [(5, idx[a], idx[min(len(idx), a + step) - 1] + 1, n_keys[sg], sg) for a in range(0, len(idx), step)]
+        # items of one flow are not contiguous in the global batch: generate the covering range, keep members
+        with ProcessPoolExecutor(workers) as ex:
+            for first, arr in ex.map(_gen_slice, jobs):
+                for k in range(len(arr)):
+                    gi = first + k
+                    if gi < total and int(sigs[gi]) == sg:
+                        buf[idx.index(gi)] = arr[k]
+        host[sg] = buf
+    log("mixed inputs: %s generated in %.1fs" % ({k: len(v) for k, v in groups.items()}, time.time() - t0))
+    inst = {sg: native.Instance(native.PZK_CIRCUIT_REGISTER, 0, flows[sg]) for sg in groups}
+    d_in = {sg: torch.from_numpy(host[sg].reshape(-1)).to(dev) for sg in groups}
+    del host
+    free, _ = torch.cuda.mem_get_info(dev)
+    half = int(free * 0.8) // 2  # output slab <= half; each instance's scratch grows with its sub-batch
+    scratch = {1: 1 << 20, 2: 2 << 20, 20: 10 << 20}
+    sub = {sg: max(1, min(len(groups[sg]), half // (32 * inst[sg].witness_size + scratch[sg]))) for sg in groups}
+    d_out = torch.empty(max(sub[sg] * 32 * inst[sg].witness_size for sg in groups), dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        off = 0
+        for sg, idx in groups.items():
+            W, NIN = inst[sg].witness_size, inst[sg].n_inputs
+            for a in range(0, len(idx), sub[sg]):
+                n = min(sub[sg], len(idx) - a)
+                inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n, d_out.data_ptr(), 32 * W,
+                                              d_st.data_ptr() + 4 * (off + a), stream=stream.cuda_stream, device=local)
+            off += len(idx)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    bad = int((d_st != 0).sum().item())
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    my_bytes = sum(costs[lo:hi])
+    if dist:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        bt = torch.tensor([bad], device=dev, dtype=torch.int64)
+        dist.all_reduce(bt)
+        bad = int(bt.item())
+    value = total * args.steps / dt
+    job_gbs = sum(costs) * args.steps / dt / 1e9
+    out = {
+        "metric": "mixed-flow registerIdentityBuilder witnesses/sec (config 5: RSA-2048/RSA-4096/ECDSA-P256)",
+        "value": round(value, 2), "unit": "witnesses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "mixed flows %s, %d per GPU, cost-sharded" % (dict(MIX), per_gpu),
+                   "flows": {str(k): len(v) for k, v in groups.items()}, "rank0_bytes": my_bytes,
+                   "invalid_lanes": bad},
+        "job_hbm": {"achieved": round(job_gbs, 1), "unit": "GB/s", "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -96,6 +96,16 @@ def lib():
     return _lib
 
 
+def layout_witness_size(params, circuit=None):
+    """Witness elements of a RegisterIdentityBuilder instance, from the host layout (no device)."""
+    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit)
+    for k, v in param_fields(params).items():
+        setattr(p, k, v)
+    info = PzkInfo()
+    _check(lib().pzk_layout_query(ctypes.byref(p), ctypes.byref(info), None))
+    return int(info.witness_size)
+
+
 def _check(rc):
     if rc != 0:
         raise PzkError("pzkwit error %d: %s" % (rc, lib().pzk_last_error().decode()))

@@ -106,3 +106,20 @@ def test_two_rank_gloo_gather():
     assert ids == list(range(10))
     assert st == [1 if i % 3 == 0 else 0 for i in range(10)]
     assert t == 2.0
+
+
+def test_mixed_shard_by_cost_balances_bytes():
+    """Config 5: a mixed RSA-2048 / RSA-4096 / ECDSA batch sharded by .wtns bytes:
+    shards tile the batch in order and each is within one witness of the even byte split."""
+    from pzkwit import mixed
+    rng = np.random.default_rng(5)
+    sigs = rng.choice([1, 2, 20], size=997, p=[0.4, 0.3, 0.3])
+    costs = [mixed.witness_cost(dict(I.CANONICAL, sig=int(s))) for s in sigs]
+    assert costs[list(sigs).index(20)] == 32 * 5488453
+    for world in (1, 2, 8):
+        bounds = [mixed.shard_by_cost(costs, world, r) for r in range(world)]
+        assert bounds[0][0] == 0 and bounds[-1][1] == len(costs)
+        assert all(bounds[r][1] == bounds[r + 1][0] for r in range(world - 1))
+        share = sum(costs) / world
+        for lo, hi in bounds:
+            assert abs(sum(costs[lo:hi]) - share) <= max(costs)

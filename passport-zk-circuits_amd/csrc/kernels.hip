@@ -5,6 +5,7 @@
 
 #include "poseidon.hpp"
 #include "regcore.hpp"
+#include "rsa_coop.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
 #include "sha_prog.hpp"
@@ -304,23 +305,47 @@ hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uin
   return hipGetLastError();
 }
 
+// RSA core: the cooperative Barrett kernel (rsa_coop.hpp) by default; PZK_RSA_CORE=lane selects
+// the one-lane-per-witness Knuth D kernel (regcore.hpp) for A/B measurements.
+template <int K, int G>
+static hipError_t launch_rsa_core2(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
+                                   uint32_t batch, hipStream_t st) {
+  constexpr int WPB = 64 / G;
+  const size_t lds = sizeof(uint64_t) * rsa2_lds_words<K>() * WPB;
+  HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core2<K, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_rsa_core2<K, G>), dim3((batch + WPB - 1) / WPB), dim3(64), lds, st, L, inputs, rsa_core, status,
+                     batch);
+  return hipGetLastError();
+}
+
+template <int K, int NL>
+static hipError_t launch_rsa_lane(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
+                                  int32_t* status, uint32_t batch, hipStream_t st) {
+  const size_t lds = sizeof(uint64_t) * rsa_lds_words<K>() * NL;
+  HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<K, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_rsa_core<K, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
+                     status, batch);
+  return hipGetLastError();
+}
+
+static bool rsa_core_lane() {
+  static const int v = [] {
+    const char* e = getenv("PZK_RSA_CORE");
+    return e && e[0] == 'l' ? 1 : 0;
+  }();
+  return v;
+}
+
 hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
                            int32_t* status, uint32_t batch, hipStream_t st) {
+  const bool lane = rsa_core_lane() && colsum;
   if (L.reg.K == 32) {
-    constexpr int NL = 64;
-    size_t lds = sizeof(uint64_t) * rsa_lds_words<32>() * NL;
-    HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<32, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_rsa_core<32, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
-                       status, batch);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY((lane ? launch_rsa_lane<32, 64>(L, inputs, rsa_core, colsum, status, batch, st)
+                  : launch_rsa_core2<32, 8>(L, inputs, rsa_core, status, batch, st)));
     hipLaunchKernelGGL(k_rsa_inv<32>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
   } else {
-    constexpr int NL = 32;
-    size_t lds = sizeof(uint64_t) * rsa_lds_words<64>() * NL;
-    HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<64, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_rsa_core<64, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
-                       status, batch);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY((lane ? launch_rsa_lane<64, 32>(L, inputs, rsa_core, colsum, status, batch, st)
+                  : launch_rsa_core2<64, 16>(L, inputs, rsa_core, status, batch, st)));
     hipLaunchKernelGGL(k_rsa_inv<64>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
   }
   return hipGetLastError();

@@ -143,3 +143,31 @@ def test_register_failing_checks_flag_lanes(oracle, gen):
     assert st[1] == codes[1] == 7
     assert st[2] == codes[2] == 13
     assert codes[3] in (8, 9, 10) and st[3] in (8, 9, 10)
+
+
+def test_register_rsa_outside_barrett_domain_matches_oracle(oracle, gen):
+    """The cooperative RSA core (rsa_coop.hpp) uses Barrett reduction only when x*y < b^(2k), k the
+    modulus' significant limbs, and exact Knuth D otherwise. A 31-limb modulus (top limb zero) with a
+    full-width signature takes the Knuth D path for multiplications 0 and 16 and Barrett for the
+    rest; every witness element must still equal the oracle's (which fails the EM checks)."""
+    pps = [gen.passport_at(300 + i) for i in range(3)]
+    rows = np.stack([I.pack_register_inputs(p) for p in pps])
+    K = 32
+    ecL = I.CANONICAL["ec_blocks"] * 512
+    sig0 = 1 + ecL + 1024 + I.CANONICAL["dg15_blocks"] * 512 + 1024
+    pk0 = sig0 + K
+    for b in (1, 2):
+        n = rows[b, pk0:pk0 + K].copy()
+        rows[b, pk0:pk0 + K - 1] = n[1:]   # n' = n >> 64: 31 significant limbs, top limb >= 2^63
+        rows[b, pk0 + K - 1] = 0
+        rows[b, sig0 + K - 1] = 0
+        rows[b, sig0 + K - 1, 0] = 0x39 * b  # x = sig: x^2 >= b^62 = b^(2k) -> outside Barrett's domain
+    inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.CANONICAL)
+    wit, st = inst.witness_batch_host(rows)
+    prm = oracle.register_params(**I.CANONICAL)
+    regions = region_table(I.CANONICAL)
+    for b in range(3):
+        rc, ref = oracle.register_witness(prm, rows[b])
+        assert (rc == 0) == (b == 0) and (st[b] == 0) == (b == 0), (b, rc, st[b])
+        rep = mismatch_report(ref, wit[b], regions)
+        assert not rep, "row %d: %s" % (b, rep)

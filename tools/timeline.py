@@ -1,20 +1,18 @@
-"""Print the kernel timeline of the last batch from a rocprofv3 kernel-trace CSV."""
-import csv
+"""Print a per-kernel timeline (ms, relative) of one window of a rocprofv3 rocpd database:
+python tools/timeline.py DB [first_kernel_substring] [nth] [count]"""
+import sqlite3
 import sys
 
-
-def main(path, marker="k_load_values", which=-1):
-    rows = list(csv.DictReader(open(path)))
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-    s = idx[which]
-    e = idx[which + 1] if which + 1 < 0 or which + 1 < len(idx) and which != -1 else len(rows)
-    t0 = int(rows[s]["Start_Timestamp"])
-    for r in rows[s:e]:
-        n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pzk::", "")
-        a, b = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
-        print(f"{n:30s} q={r.get('Queue_Id', ''):2s} {a / 1e6:8.2f} {b / 1e6:8.2f} {(b - a) / 1e6:7.2f}")
-
-
-if __name__ == "__main__":
-    main(sys.argv[1], *(sys.argv[2:3]))
+db = sys.argv[1]
+anchor = sys.argv[2] if len(sys.argv) > 2 else "k_load_values"
+nth = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+count = int(sys.argv[4]) if len(sys.argv) > 4 else 40
+c = sqlite3.connect(db)
+cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+rows = list(c.execute("select name, start, end, queue_id from kernels order by start"))
+idx = [i for i, r in enumerate(rows) if anchor in r[0]]
+i0 = idx[nth]
+t0 = rows[i0][1]
+for name, s, e, q in rows[i0:i0 + count]:
+    short = name.split("(")[0].replace("void ", "").replace("pzk::", "")
+    print("%-32s q=%-3s %8.2f %8.2f %7.2f" % (short[:32], q, (s - t0) / 1e6, (e - t0) / 1e6, (e - s) / 1e6))

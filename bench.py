@@ -62,13 +62,18 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+# workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
+WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11}
+SIG_SEED = {1: 3, 20: 5, 11: 7}
+
+
 def _cpu_work(args):
     kind, rows = args
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     from pzkwit import inputs as I
     if kind.startswith("register"):
-        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=20 if kind == "register-ecdsa" else 1))
+        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=WL_SIG[kind]))
         nin, nw = pyoracle.register_sizes(prm)
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
@@ -97,7 +102,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "register-ecdsa", "sha256", "mixed"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "sha256", "mixed"], default="register")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
     ap.add_argument("--cpu-sample", type=int, default=None)
@@ -121,11 +126,11 @@ def main():
 
     scratch_pw = 1 << 20  # per-witness core scratch (bytes), for the slab sizing below
     if args.workload.startswith("register"):
-        sig = 20 if args.workload == "register-ecdsa" else 1
+        sig = WL_SIG[args.workload]
         batch = args.batch or 4096
         inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, dict(I.CANONICAL, sig=sig))
         t0 = time.time()
-        host_in = make_register_inputs(batch, rank * batch, seed=3 if sig == 1 else 5, sig=sig)
+        host_in = make_register_inputs(batch, rank * batch, seed=SIG_SEED[sig], sig=sig)
         log("inputs: %d passports generated in %.1fs" % (batch, time.time() - t0))
         metric = "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline"
         workload = "RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports (config 3)"
@@ -133,6 +138,9 @@ def main():
             metric = "registerIdentityBuilder ECDSA-secp256r1 witnesses/sec, batch=4096 (config 5 slice)"
             workload = "RegisterIdentityBuilder(20,256,3,4,600,248,1,1496,3,256) synthetic P-256 passports"
             scratch_pw = 10 << 20  # value tables (~8.4 MB) + EC core
+        if sig == 11:
+            metric = "registerIdentityBuilder RSA-PSS witnesses/sec, batch=4096 (SIGNATURE_TYPE 11)"
+            workload = "RegisterIdentityBuilder(11,256,3,4,600,248,1,1496,3,256) synthetic RSA-2048 PSS passports"
     else:
         batch = args.batch or 1024
         inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
@@ -234,9 +242,9 @@ def main():
     if rank == 0 and not args.no_cpu:
         procs = max(1, min(16, os.cpu_count() or 1))
         if args.workload.startswith("register"):
-            sig = 20 if args.workload == "register-ecdsa" else 1
-            ns = args.cpu_sample or (128 if sig == 1 else 48) * procs
-            rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=3 if sig == 1 else 5, sig=sig)
+            sig = WL_SIG[args.workload]
+            ns = args.cpu_sample or (48 if sig == 20 else 96 if sig == 11 else 128) * procs
+            rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=SIG_SEED[sig], sig=sig)
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)

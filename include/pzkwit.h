@@ -35,7 +35,8 @@ enum {
 typedef struct pzk_params {
   int32_t circuit;            /* PZK_CIRCUIT_* */
   int32_t size_arg;           /* n for POSEIDON, blocks for SHA256; ignored for REGISTER */
-  int32_t signature_type;     /* SIGNATURE_TYPE (1 = RSA-2048/SHA-256/65537, 2 = RSA-4096) */
+  int32_t signature_type;     /* SIGNATURE_TYPE (1 = RSA-2048/SHA-256/65537, 2 = RSA-4096, 10-12 = RSA-2048
+                                 PSS/SHA-256 (10: e = 3), 20 = ECDSA secp256r1/SHA-256) */
   int32_t dg_hash_type;       /* DG_HASH_TYPE (256) */
   int32_t document_type;      /* DOCUMENT_TYPE (1 = TD1, 3 = TD3) */
   int32_t ec_block_number;    /* EC_BLOCK_NUMBER */
@@ -84,6 +85,10 @@ enum {
   PZK_ST_BIGISZERO = 12,  /* bigIntComparators.circom:128 */
   PZK_ST_SMT_LAST = 13,   /* SMTVerifier.circom:54 */
   PZK_ST_BJJ_ADD = 14,    /* babyjubjub/curve.circom:98,102 */
+  PZK_ST_ECDSA_INV = 15,  /* bigInt.circom:364-368 (in * inv mod n === 1) */
+  PZK_ST_ECDSA_R = 16,    /* ecdsa.circom:81-83 (x1 mod n === r) */
+  PZK_ST_PSS_TRAILER = 17,/* rsaPss.circom:73 (assert eM[0] == 188) */
+  PZK_ST_PSS_HASH = 18,   /* rsaPss.circom:182,201 (hDash256.out === hash) */
   PZK_ST_INPUT_RANGE = 64 /* an input outside the domain the GPU path evaluates (e.g. a non-bit
                              SHA input, a limb >= 2^64); see DESIGN.md §5 */
 };

@@ -53,6 +53,8 @@ enum {
   S_BJJ_ADD = 14,        /* babyjubjub/curve.circom:98,102 */
   S_ECDSA_INV = 15,      /* bigInt.circom:364-368  in * inv mod n === 1 */
   S_ECDSA_R = 16,        /* ecdsa.circom:81-83  x1 mod n === r */
+  S_PSS_TRAILER = 17,    /* rsaPss.circom:73  assert(eM[0] == 188) */
+  S_PSS_HASH = 18,       /* rsaPss.circom:182,201  hDash256.out === hash */
 };
 
 /* ------------------------------------------------------------- fr helpers */
@@ -951,6 +953,106 @@ static void run_verifysig(ctx_t *c, size_t b, int K) {
   run_rsa(c, rsa, K, 65537);
 }
 
+/* ================================================= RSA-PSS (SIGNATURE_TYPE 10, 11, 12)
+ * VerifyRsaPssSig(64, K, SALT, EXP, 256) rsaPss.circom:18-204 with Mgf1Sha256 mgf1.circom:69-127.
+ * SIG 10: e = 3, salt 32; SIG 11: e = 65537, salt 32; SIG 12: e = 65537, salt 64
+ * (signatureVerification.circom:46-62). EM = PowerMod.out, 8K bytes; DB = EM_LEN - HASH_LEN - 1 bytes. */
+static int is_pss(int sig) { return sig >= 10 && sig <= 12; }
+static int pss_salt(int sig) { return sig == 12 ? 64 : 32; }
+static long sig_exp(int sig) { return sig == 10 ? 3 : 65537; }
+
+/* Mgf1Sha256(32, DBL): out[8 DBL] | seed[256] | hashed[256 IT] | (ShaHashChunks(1,256), Num2Bits(32)) x IT */
+static int mgf_iters(int DBL) { return DBL / 32 + 1; }
+static size_t sz_mgf1(int DBL) {
+  int IT = mgf_iters(DBL);
+  return 8 * (size_t)DBL + 256 + 256 * (size_t)IT + (size_t)IT * (sz_shahash(1) + sz_num2bits(32));
+}
+static void run_mgf1(ctx_t *c, size_t b, int DBL) {
+  int IT = mgf_iters(DBL);
+  size_t out = b, seed = out + 8 * (size_t)DBL, hashed = seed + 256, sub = hashed + 256 * (size_t)IT;
+  for (int i = 0; i < IT; i++) {
+    size_t sh = sub + (size_t)i * (sz_shahash(1) + sz_num2bits(32)), nb = sh + sz_shahash(1), in = sh + 256;
+    W(nb + 32) = fr_u64((uint64_t)i);
+    run_num2bits(c, nb, 32);
+    /* concated = seed | counter (MSB first) | padding for a 288-bit message (mgf1.circom:97-121) */
+    for (int j = 0; j < 256; j++) W(in + j) = W(seed + j);
+    for (int j = 0; j < 32; j++) W(in + 256 + j) = W(nb + 31 - j);
+    for (int j = 288; j < 512; j++) W(in + j) = fr_zero();
+    W(in + 288) = ONE(); W(in + 503) = ONE(); W(in + 506) = ONE();
+    run_shahash(c, sh, 1);
+    for (int j = 0; j < 256; j++) W(hashed + 256 * (size_t)i + j) = W(sh + j);
+  }
+  for (int i = 0; i < 8 * DBL; i++) W(out + i) = W(hashed + i);
+}
+
+/* own: pubkey[K], signature[K], hashed[256] | eM[EML], eMsgInBits[64K], encoded[K], dbMask[DB8], db[DB8],
+ *      salt[S8], maskedDB[DB8], hash[256], mDash[1024]
+ * subcomponents: powerMod, num2Bits[K] (Num2Bits(64)), bits2Num[EML] (Bits2Num(8)), MGF1_256, xor (Xor2(DB8):
+ * out | in1 | in2), hDash256 (ShaHashChunks(2, 256)) */
+static size_t sz_pss(int K, int S, long EXP) {
+  size_t EML = 8 * (size_t)K, DB8 = 8 * (EML - 33);
+  return 2 * (size_t)K + 256 + EML + 64 * (size_t)K + K + 3 * DB8 + 8 * (size_t)S + 256 + 1024 + sz_powermod(64, K, EXP) +
+         (size_t)K * sz_num2bits(64) + EML * sz_bits2num(8) + sz_mgf1((int)EML - 33) + 3 * DB8 + sz_shahash(2);
+}
+static void run_pss(ctx_t *c, size_t b, int K, int S, long EXP) {
+  const int EMB = 64 * K, EML = 8 * K, DBL = EML - 33, DB8 = 8 * DBL, S8 = 8 * S;
+  size_t pk = b, sig = pk + K, hashed = sig + K, eM = hashed + 256, bits = eM + EML, enc = bits + EMB,
+         dbMask = enc + K, db = dbMask + DB8, salt = db + DB8, masked = salt + S8, hash = masked + DB8,
+         mDash = hash + 256, pm = mDash + 1024, n2b = pm + sz_powermod(64, K, EXP),
+         b2n = n2b + (size_t)K * sz_num2bits(64), mgf = b2n + (size_t)EML * sz_bits2num(8), xr = mgf + sz_mgf1(DBL),
+         hd = xr + 3 * (size_t)DB8;
+  for (int i = 0; i < K; i++) { W(pm + K + i) = W(sig + i); W(pm + 2 * K + i) = W(pk + i); }
+  run_powermod(c, pm, 64, K, EXP);
+  for (int i = 0; i < K; i++) W(enc + i) = W(pm + i);
+  for (int i = 0; i < K; i++) { /* rsaPss.circom:45-53: eMsgInBits = EM bits, most significant first */
+    size_t nb = n2b + (size_t)i * sz_num2bits(64);
+    W(nb + 64) = W(enc + K - 1 - i);
+    run_num2bits(c, nb, 64);
+    for (int j = 0; j < 64; j++) W(bits + 64 * (size_t)i + j) = W(nb + 63 - j);
+  }
+  for (int i = 0; i < EML; i++) { /* :55-61: eM[EML-1-i] = byte i (big-endian) */
+    size_t bn = b2n + (size_t)i * sz_bits2num(8);
+    for (int j = 0; j < 8; j++) W(bn + 1 + 7 - j) = W(bits + 8 * (size_t)i + j);
+    run_bits2num(c, bn, 8);
+    W(eM + EML - 1 - i) = W(bn);
+  }
+  if (!fr_eq(W(eM), fr_u64(188)) && !c->err) c->err = S_PSS_TRAILER;
+  for (int i = 0; i < DB8; i++) W(masked + i) = W(bits + i);
+  for (int i = 0; i < 256; i++) W(hash + i) = W(bits + EMB - 256 - 8 + i);
+  for (int i = 0; i < 256; i++) W(mgf + DB8 + i) = W(hash + i);
+  run_mgf1(c, mgf, DBL);
+  for (int i = 0; i < DB8; i++) W(dbMask + i) = W(mgf + i);
+  for (int i = 0; i < DB8; i++) { /* Xor2 (bitGates.circom:232-240) */
+    fr_t x = W(masked + i), y = W(dbMask + i);
+    W(xr + DB8 + i) = x; W(xr + 2 * (size_t)DB8 + i) = y;
+    W(xr + i) = fr_sub(fr_add(x, y), fr_add(mulg(x, y), mulg(x, y)));
+  }
+  W(db) = fr_zero();
+  for (int i = 1; i < DB8; i++) W(db + i) = W(xr + i);
+  for (int i = 0; i < S8; i++) W(salt + S8 - 1 - i) = W(db + DB8 - 1 - i);
+  /* mDash = 0^64 | hashed | salt | SHA-256 padding of a (320 + S8)-bit message (:153-200) */
+  const int LM = 64 + 256 + S8;
+  for (int i = 0; i < 1024; i++) W(mDash + i) = fr_zero();
+  for (int i = 0; i < 256; i++) W(mDash + 64 + i) = W(hashed + i);
+  for (int i = 0; i < S8; i++) W(mDash + 320 + i) = W(salt + i);
+  W(mDash + LM) = ONE();
+  for (int k = 0; k < 11; k++)
+    if ((LM >> k) & 1) W(mDash + 1023 - k) = ONE();
+  for (int i = 0; i < 1024; i++) W(hd + 256 + i) = W(mDash + i);
+  run_shahash(c, hd, 2);
+  int bad = 0;
+  for (int i = 0; i < 256; i++) bad |= !fr_eq(W(hd + i), W(hash + i));
+  if (bad && !c->err) c->err = S_PSS_HASH;
+}
+
+/* VerifySignature(SIG 10-12): pubkey[K], signature[K], hashed[256] | VerifyRsaPssSig */
+static size_t sz_verifysig_pss(int K, int sig) { return 2 * (size_t)K + 256 + sz_pss(K, pss_salt(sig), sig_exp(sig)); }
+static void run_verifysig_pss(ctx_t *c, size_t b, int K, int sig) {
+  size_t v = b + 2 * K + 256;
+  for (int i = 0; i < 2 * K + 256; i++) W(v + i) = W(b + i);
+  run_pss(c, v, K, pss_salt(sig), sig_exp(sig));
+}
+
 #include "ecdsa_p256.inc.c"
 
 /* ======================================================== SMT (depth 80) */
@@ -1062,7 +1164,7 @@ static size_t sz_pvb(const orc_params *P) {
   size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 256 * 4 + 1 + (ec ? 512 : 5);
   size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   return own + sz_shahash(2) + (P->aa ? sz_shahash(P->dg15_blocks) : 0) + sz_shahash(P->ec_blocks) + sz_shahash(2) +
-         sz_flow(ecLen) + (ec ? sz_verifysig_ec() : sz_verifysig(K)) + sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
+         sz_flow(ecLen) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K)) + sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, isec = P->sig >= 20;
@@ -1075,7 +1177,7 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   size_t hEc = p; p += sz_shahash(P->ec_blocks);
   size_t hSa = p; p += sz_shahash(2);
   size_t flow = p; p += sz_flow(ecLen);
-  size_t vs = p; p += isec ? sz_verifysig_ec() : sz_verifysig(K);
+  size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K);
   size_t saNum = p; p += sz_bits2num(252);
   size_t pkH = p; p += isec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   size_t smt = p; p += sz_smt(80);
@@ -1111,6 +1213,7 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   for (int i = 0; i < K; i++) { W(vs + K + i) = W(sig + i); W(vs + i) = W(pk + i); }
   for (int i = 0; i < 256; i++) W(vs + 2 * K + i) = W(saH + i);
   if (isec) run_verifysig_ec(c, vs);
+  else if (is_pss(P->sig)) run_verifysig_pss(c, vs, K, P->sig);
   else run_verifysig(c, vs, K);
   /* passportHash bits */
   for (int i = 0; i < 252; i++) W(saNum + 1 + i) = W(saH + i);
@@ -1207,7 +1310,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2 || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa == 0 || P->aa == 1) &&
+  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa == 0 || P->aa == 1) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 

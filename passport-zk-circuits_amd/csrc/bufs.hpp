@@ -24,6 +24,7 @@ struct Bufs {
   const fr* ec_inv;       // IsEqual inverses, normal form
   const uint8_t* ec_tab;  // value tables of the table ops
   const fr* inv_small;    // 1/k mod p, k < 256, normal form
+  const uint8_t* derived; // derived SHA message elements (RSA-PSS, pss.hpp), n_derived per witness
 };
 
 }  // namespace pzk

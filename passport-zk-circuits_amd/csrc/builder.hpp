@@ -23,6 +23,7 @@ struct InputGroup {
 
 struct Layout {
   uint64_t wit_size = 0, n_inputs = 0;
+  uint64_t n_derived = 0;  // derived SHA message elements per witness (RSA-PSS)
   uint32_t n_outputs = 0, n_public = 0;
   std::vector<InputGroup> inputs;
   std::vector<Region> regions;

@@ -27,9 +27,10 @@ struct Builder {
     return (uint32_t)L.regions.size() - 1;
   }
 
-  int sha_job(int in_off, int blocks) {
+  int sha_job(int in_off, int blocks, int src = 0) {
     ShaJob j{};
     j.in_off = in_off;
+    j.src = src;
     j.blocks = blocks;
     j.core_off = (int)L.sha_core_words;
     j.digest_slot = -1;
@@ -40,8 +41,8 @@ struct Builder {
 
   // Sha256HashChunks(B) (sha256HashChunks.circom:8-48), optionally inside ShaHashChunks(B,256)
   // (hash.circom:32-68): own/wrapper signals as one RK_SHA_OWN region, then (sch, rds) per block.
-  int sha256(int in_off, int blocks, bool wrapper) {
-    int job = sha_job(in_off, blocks);
+  int sha256(int in_off, int blocks, bool wrapper, int src = 0) {
+    int job = sha_job(in_off, blocks, src);
     uint64_t own = (wrapper ? 256 + 512ull * blocks : 0) + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
     region(RK_SHA_OWN, own, {job, blocks, in_off, wrapper ? 1 : 0});
     for (int m = 0; m < blocks; m++) region(RK_SHA_BLOCK, SHA_BLOCK_LEN, {job, m});
@@ -102,6 +103,13 @@ struct Builder {
       }
       uint32_t chunk = emitter_whole(e) ? r.len : emit_chunk(e);
       for (uint32_t s = 0; s < r.len; s += chunk) wl->push_back(Work{ri, s, std::min(chunk, r.len - s), 0});
+    }
+    // SHA regions of hashers fed by derived messages are emitted after the chain that builds them
+    {
+      std::vector<Work> keep, later;
+      for (const Work& w : L.work[E_SHA]) (L.sha[L.regions[w.region].a[0]].src ? later : keep).push_back(w);
+      L.work[E_SHA].swap(keep);
+      L.work[E_SHAD].swap(later);
     }
     // Poseidon emission: one launch per width t, each with the LDS its image needs
     {

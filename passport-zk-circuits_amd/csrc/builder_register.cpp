@@ -38,9 +38,10 @@ uint32_t modmul_size(int K) {
 }
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
-  if (p.signature_type != 1 && p.signature_type != 2 && p.signature_type != 20) {
+  const bool pss = p.signature_type >= 10 && p.signature_type <= 12;  // RSA-2048 PSS, SHA-256 (e = 3 for 10)
+  if (p.signature_type != 1 && p.signature_type != 2 && !pss && p.signature_type != 20) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1, 2 and ECDSA secp256r1 type 20 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12 and ECDSA secp256r1 type 20 are)";
     return false;
   }
   const bool ecdsa = p.signature_type == 20;
@@ -153,28 +154,60 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   if (ecdsa) {
     ec_verify_regions(b, IN_PK, IN_SIG, J_SA);
   } else {
-    // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15
+    // PowerMod(64,K,EXP): out[K] | base[K], modulus[K] | muls[], resultMuls[] (bigInt.circom:280-340).
+    // exp_to_bits(65537) = [16, 2, 0, 16], exp_to_bits(3) = [1, 2, 0, 1]: muls[i] = muls[i-1]^2
+    // (muls[0] = base^2), then resultMuls[0] = base * muls[last]
+    const int n_modmul = p.signature_type == 10 ? 2 : 17;
+    auto power_mod = [&]() -> bool {
+      b.region(RK_RSA_OUT, K);
+      b.region(RK_INCOPY, K, {IN_SIG});
+      b.region(RK_INCOPY, K, {IN_PK});
+      const uint32_t mm = modmul_size(K);
+      L.reg.modmul_size = mm;
+      if (mm_section_start(K, MM_SECTIONS) != mm) { why = "internal: BigMultModP section sizes"; return false; }
+      L.reg.n_modmul = n_modmul;
+      L.rsa_core_words = n_modmul * MM_CORE_WORDS(K);
+      for (int i = 0; i < n_modmul; i++) b.region(RK_MODMUL, mm, {i, IN_PK});
+      return true;
+    };
+    // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15 or VerifyRsaPssSig
     b.region(RK_INCOPY, K, {IN_PK});
     b.region(RK_INCOPY, K, {IN_SIG});
     b.region(RK_DIGEST, 256, {J_SA});
-    //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
-    b.region(RK_INCOPY, K, {IN_SIG});
-    b.region(RK_INCOPY, K, {IN_PK});
-    b.region(RK_DIGEST, 256, {J_SA});
-    b.region(RK_HCHUNK, 4, {J_SA});
-    //   PowerMod(64,K,65537): out[K] | base[K], modulus[K] | muls[16], resultMuls[1]
-    b.region(RK_RSA_OUT, K);
-    b.region(RK_INCOPY, K, {IN_SIG});
-    b.region(RK_INCOPY, K, {IN_PK});
-    const uint32_t mm = modmul_size(K);
-    L.reg.modmul_size = mm;
-    if (mm_section_start(K, MM_SECTIONS) != mm) { why = "internal: BigMultModP section sizes"; return false; }
-    // exp_to_bits(65537) = [16, 2, 0, 16]: muls[i] = muls[i-1]^2 (muls[0] = base^2); resultMuls[0] = base * muls[15]
-    L.reg.n_modmul = 17;
-    L.rsa_core_words = 17 * MM_CORE_WORDS(K);
-    for (int i = 0; i < 17; i++) b.region(RK_MODMUL, mm, {i, IN_PK});
-    for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
-    b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
+    if (!pss) {
+      //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
+      b.region(RK_INCOPY, K, {IN_SIG});
+      b.region(RK_INCOPY, K, {IN_PK});
+      b.region(RK_DIGEST, 256, {J_SA});
+      b.region(RK_HCHUNK, 4, {J_SA});
+      if (!power_mod()) return false;
+      for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
+      b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
+    } else {
+      //   VerifyRsaPssSig(64,K,SALT,EXP,256) (rsaPss.circom:18-204): pubkey, signature, hashed | eM .. mDash
+      //   | powerMod, num2Bits[K], bits2Num[8K], MGF1_256, xor, hDash256 (pss.hpp)
+      const int S8 = p.signature_type == 12 ? 512 : 256, EML = 8 * K, DB8 = 8 * (EML - 33), IT = (EML - 33) / 32 + 1;
+      b.region(RK_INCOPY, K, {IN_PK});
+      b.region(RK_INCOPY, K, {IN_SIG});
+      b.region(RK_DIGEST, 256, {J_SA});
+      b.region(RK_PSS_OWN, EML + 64 * K + K + 3 * DB8 + S8 + 256 + 1024, {S8});
+      if (!power_mod()) return false;
+      for (int i = 0; i < K; i++) b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, K - 1 - i});  // EM limb K-1-i
+      b.region(RK_PSS_B2N8, 17 * EML);
+      //   Mgf1Sha256(32, DB) (mgf1.circom:69-127): out | seed | hashed, then (ShaHashChunks(1,256), Num2Bits(32))
+      //   per block; the hashers read derived messages (ShaJob.src = 1)
+      b.region(RK_PSS_MGF, DB8 + 256 + 256 * IT);
+      L.reg.j_mgf = (int)L.sha.size();
+      L.reg.n_mgf = IT;
+      for (int c = 0; c < IT; c++) {
+        b.sha256(512 * c, 1, true, 1);
+        b.region(RK_PSS_CTR, sz_num2bits(32), {c});
+      }
+      b.region(RK_PSS_XOR, 3 * DB8);
+      L.reg.j_hd = b.sha256(512 * IT, 2, true, 1);
+      L.reg.pss_s8 = S8;
+      L.n_derived = 512ull * IT + 1024;
+    }
   }
   // signedAttributesNum = Bits2Num(252)(saHash[0..251])
   b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, 0, 1, J_SA});

@@ -5,6 +5,7 @@
 
 #include "poseidon.hpp"
 #include "regcore.hpp"
+#include "pss.hpp"
 #include "rsa_coop.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
@@ -29,13 +30,15 @@ __global__ void k_load_values(const ValueLoad* loads, int n_loads, const uint8_t
 
 // ------------------------------------------------------------------- SHA core
 __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jobs, const uint8_t* inputs, uint64_t n_inputs,
-                           uint32_t* sha_core, uint32_t core_words, int32_t* status, uint32_t batch) {
+                           const uint8_t* derived, uint64_t n_derived, uint32_t* sha_core, uint32_t core_words,
+                           int32_t* status, uint32_t batch) {
   core_priority();
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   int j = blockIdx.y;
   if (w >= batch || j >= n_jobs) return;
-  sha_core_lane(inputs + 32ull * (uint64_t)w * n_inputs, jobs[j], sha_core + (size_t)w * core_words,
-                status ? status + w : nullptr);
+  const ShaJob& J = jobs[j];
+  const uint8_t* row = J.src ? derived + 32ull * (uint64_t)w * n_derived : inputs + 32ull * (uint64_t)w * n_inputs;
+  sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
 }
 
 // ------------------------------------------------------------------- Poseidon core
@@ -96,9 +99,9 @@ __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t*
 }
 
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
-                                                          const uint32_t* sha_core, uint8_t* wtns, size_t stride,
-                                                          int wit_major) {
-  __shared__ uint32_t core[SHA_BLOCK_CORE + 8 * 17];
+                                                          const uint8_t* derived, const uint32_t* sha_core,
+                                                          uint8_t* wtns, size_t stride, int wit_major) {
+  __shared__ uint32_t core[SHA_BLOCK_CORE + 8 * 65];  // RK_SHA_OWN: H_0..H_B, B <= 64
   __shared__ __attribute__((aligned(16))) uint64_t wt[SHA_WT_SIZE];
   // grid (witness, chunk): the blocks in flight together work on the same chunk of different
   // witnesses, so they share its slice of the block program in L2
@@ -151,7 +154,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
       core[i] = m < Bn ? wc[m * SHA_BLOCK_CORE + j] : wc[Bn * SHA_BLOCK_CORE + j];
     }
     __syncthreads();
-    const uint8_t* in_row = inputs + 32ull * (uint64_t)w * L.n_inputs;
+    const uint8_t* in_row = job.src ? derived + 32ull * (uint64_t)w * L.n_derived : inputs + 32ull * (uint64_t)w * L.n_inputs;
     uint4* stage = reinterpret_cast<uint4*>(wt);  // the word table is not used on this path
     emit_run(out, wk.count, stage, [&](uint32_t q) {
       bool cp; uint64_t src = 0;
@@ -242,12 +245,23 @@ hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inpu
   return hipGetLastError();
 }
 
-hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* sha_core, int32_t* status,
-                           uint32_t batch, hipStream_t st) {
-  if (L.n_sha == 0) return hipSuccess;
-  dim3 g((batch + 63) / 64, L.n_sha);
-  hipLaunchKernelGGL(k_sha_core, g, dim3(64), 0, st, L.sha, (int)L.n_sha, inputs, L.n_inputs, sha_core,
-                     L.sha_core_words, status, batch);
+hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, const uint8_t* derived, uint32_t first,
+                           uint32_t count, uint32_t* sha_core, int32_t* status, uint32_t batch, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  if (first + count > L.n_sha) return hipErrorInvalidValue;
+  dim3 g((batch + 63) / 64, count);
+  hipLaunchKernelGGL(k_sha_core, g, dim3(64), 0, st, L.sha + first, (int)count, inputs, L.n_inputs, derived,
+                     L.n_derived, sha_core, L.sha_core_words, status, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_pss(const DevLayout& L, int stage, const uint64_t* rsa_core, const uint32_t* sha_core,
+                      uint8_t* derived, uint32_t batch, hipStream_t st) {
+  if (stage == 0)
+    hipLaunchKernelGGL(k_pss_mgf, dim3((512 * L.reg.n_mgf + 255) / 256, batch), dim3(256), 0, st, L, rsa_core,
+                       sha_core, derived);
+  else
+    hipLaunchKernelGGL(k_pss_mdash, dim3(4, batch), dim3(256), 0, st, L, rsa_core, sha_core, derived);
   return hipGetLastError();
 }
 
@@ -392,8 +406,9 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
-    case E_SHA:  // witness-major grid (see k_emit_sha)
-      hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.sha_core, B.wtns, B.stride, 1);
+    case E_SHA: case E_SHAD:  // witness-major grid (see k_emit_sha)
+      hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
+                         B.stride, 1);
       break;
     case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
       switch (max_t) {

@@ -19,8 +19,12 @@ struct Bufs;
 
 hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inputs, uint64_t n_inputs, fr* values,
                               uint32_t batch, hipStream_t st);
-hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, uint32_t* sha_core, int32_t* status,
-                           uint32_t batch, hipStream_t st);
+// SHA jobs [first, first + count); a job with src = 1 reads its message from the derived row
+hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, const uint8_t* derived, uint32_t first,
+                           uint32_t count, uint32_t* sha_core, int32_t* status, uint32_t batch, hipStream_t st);
+// RSA-PSS derived messages (pss.hpp): stage 0 = MGF1 blocks (after the RSA core), 1 = M' (after the MGF1 hashes)
+hipError_t launch_pss(const DevLayout& L, int stage, const uint64_t* rsa_core, const uint32_t* sha_core,
+                      uint8_t* derived, uint32_t batch, hipStream_t st);
 hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
                            uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, const fr* smt_core,
                            uint32_t smt_core_fr, hipStream_t st);

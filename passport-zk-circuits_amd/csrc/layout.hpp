@@ -14,7 +14,8 @@ namespace pzk {
 // lane status codes (mirror include/pzkwit.h PZK_ST_*)
 constexpr int32_t ST_NUM2BITS = 1, ST_ALIAS = 2, ST_ISZERO = 3, ST_FLOW = 7, ST_RSA_HASH = 8,
                   ST_RSA_PREFIX = 9, ST_RSA_PAD = 10, ST_BIGMOD_GT = 11, ST_BIGISZERO = 12,
-                  ST_SMT_LAST = 13, ST_ECDSA_INV = 15, ST_ECDSA_R = 16, ST_INPUT_RANGE = 64;
+                  ST_SMT_LAST = 13, ST_ECDSA_INV = 15, ST_ECDSA_R = 16, ST_PSS_TRAILER = 17,
+                  ST_PSS_HASH = 18, ST_INPUT_RANGE = 64;
 
 // ---- emit regions: a contiguous run of witness signals with one closed-form generator
 enum RegionKind : uint32_t {
@@ -61,13 +62,20 @@ enum RegionKind : uint32_t {
   RK_EC_SM_RSW = 37,  // scalarMult window a0: isZeroAddition + (resultSwitcherAddition, resultSwitcherDoubling)[8]
   RK_EC_PKBITS = 38,  // PassportVerificationBuilder ecBitsX[256], ecBitsY[256] of pubkey input a0
   RK_EC_B2N248 = 39,  // Bits2Num(248) of the 4-limb input at a0 (xToNum / yToNum)
+  // ---- RSA-PSS (SIGNATURE_TYPE 10-12, rsaPss.circom:18-204; pss.hpp)
+  RK_PSS_OWN = 40,    // VerifyRsaPssSig eM .. mDash (after its pubkey/signature/hashed inputs); a0 = salt bits
+  RK_PSS_B2N8 = 41,   // bits2Num[8K] (Bits2Num(8)) of the EM bytes
+  RK_PSS_MGF = 42,    // Mgf1Sha256 own: out[DB8] | seed[256] | hashed[256 IT]
+  RK_PSS_CTR = 43,    // Mgf1Sha256 num2Bits[a0] = Num2Bits(32)(a0)
+  RK_PSS_XOR = 44,    // Xor2(DB8): out | in1 | in2
   RK_COUNT
 };
 
 // emit kernels (one work list each)
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
 // E_ECT = ECDSA table blocks (k_emit_ect)
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_COUNT };
+// E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -78,7 +86,7 @@ __host__ __device__ inline int emitter_of(uint32_t kind) {
     case RK_BJJ_STEPS: return E_BJJ;
     case RK_RSA_OUT: return E_GENR;
     case RK_ECT: return E_ECT;
-    default: return kind >= RK_EC_U64 && kind <= RK_EC_B2N248 ? E_GENR : E_GEN;
+    default: return kind >= RK_EC_U64 && kind <= RK_PSS_XOR ? E_GENR : E_GEN;
   }
 }
 // regions whose emit workgroup needs the whole region (LDS pre-pass over all of it)
@@ -117,6 +125,7 @@ struct ShaJob {
   int32_t blocks;   // number of 512-bit blocks
   int32_t core_off; // u32 offset of this hasher's core inside the per-witness SHA core
   int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
+  int32_t src;      // 0: message bits are input elements; 1: derived elements (RSA-PSS, pss.hpp)
 };
 
 // per block core: Hin[8] W[64] A[1..64] E[1..64]; per hasher: blocks*200 + Hout[8]
@@ -144,6 +153,8 @@ struct RegInfo {
   uint32_t modmul_size;
   int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (secp256r1)
   int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
+  int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)
+  int32_t j_mgf, n_mgf, j_hd;      // RSA-PSS SHA jobs: MGF1 blocks [j_mgf, j_mgf + n_mgf), M' hasher
 };
 
 // per-witness core sizes of the register-circuit kernels
@@ -188,6 +199,7 @@ struct PosParamIndex {
 struct DevLayout {
   uint64_t wit_size;      // elements per witness
   uint64_t n_inputs;      // elements per input row
+  uint64_t n_derived;     // derived message elements per witness (RSA-PSS MGF1 / M' hasher inputs)
   uint32_t n_regions, n_work;
   uint32_t n_sha, sha_core_words;   // SHA jobs; u32 words of SHA core per witness
   uint32_t n_pos, pos_core_elems;   // Poseidon tasks; Fr per witness of Poseidon core

@@ -20,6 +20,7 @@
 #include "poseidon.hpp"
 #include "sha.hpp"
 #include "core_util.hpp"
+#include "pss.hpp"
 
 namespace pzk {
 
@@ -146,20 +147,21 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
   uint64_t vinv_r;
   const uint64_t vinv = vtop ? divlu(~vtop, ~0ull, vtop, &vinv_r) : 0ull;  // a zero modulus is flagged below
   constexpr int MMW = MM_CORE_WORDS(K);
-  for (int k = 0; k < 17; k++) {
+  const int NM = L.reg.n_modmul;
+  for (int k = 0; k < NM; k++) {
     uint64_t* mc = core + (size_t)k * MMW;
     // operands (exp_to_bits(65537) = [16,2,0,16]): muls[k] = muls[k-1].mod^2 with muls[0] = base^2;
     // resultMuls[0] = base * muls[15].mod (bigInt.circom:299-327)
     for (int i = 0; i < K; i++) {
       uint64_t xi;
-      if (k == 0 || k == 16) {
+      if (k == 0 || k == NM - 1) {
         const uint8_t* e = row + 32ull * (L.reg.in_sig + i);
         bad |= !in_is_u64(e);
         xi = in_u64(e);
       } else {
         xi = core[(size_t)(k - 1) * MMW + 3 * K + 1 + i];
       }
-      uint64_t yi = k == 16 ? core[(size_t)15 * MMW + 3 * K + 1 + i] : xi;
+      uint64_t yi = k == NM - 1 ? core[(size_t)(k - 1) * MMW + 3 * K + 1 + i] : xi;
       x[i] = xi; y[i] = yi;
       mc[i] = xi; mc[K + i] = yi;
     }
@@ -303,7 +305,8 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
   const uint32_t w = blockIdx.x;
   if (w >= batch) return;
   const int lane = threadIdx.x;
-  constexpr int NE = 17 * K, PER = (NE + 63) / 64, MMW = MM_CORE_WORDS(K);
+  const int NE = L.reg.n_modmul * K, PER = (NE + 63) / 64;
+  constexpr int MMW = MM_CORE_WORDS(K);
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   uint64_t* core = rsa_core + (size_t)w * L.rsa_core_words;
   const int e0 = lane * PER, e1 = e0 + PER < NE ? e0 + PER : NE;
@@ -377,9 +380,13 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
     }
     gt_bad |= cmp != 1;
   }
-  if (hash_bad) lane_status(status + w, ST_RSA_HASH);
-  if (em[4] != RSA_EM4 || em[5] != RSA_EM5) lane_status(status + w, ST_RSA_PREFIX);
-  if (pad_bad) lane_status(status + w, ST_RSA_PAD);
+  if (L.reg.pss_s8) {
+    pss_check(pss_view(L, rsa_core, sha_core, w), status + w);
+  } else {
+    if (hash_bad) lane_status(status + w, ST_RSA_HASH);
+    if (em[4] != RSA_EM4 || em[5] != RSA_EM5) lane_status(status + w, ST_RSA_PREFIX);
+    if (pad_bad) lane_status(status + w, ST_RSA_PAD);
+  }
   if (gt_bad) lane_status(status + w, ST_BIGMOD_GT);
 }
 

@@ -12,6 +12,7 @@
 #include "sha.hpp"
 #include "mm_prog.hpp"
 #include "ec_emit.hpp"
+#include "pss.hpp"
 
 namespace pzk {
 
@@ -174,6 +175,8 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
         return el_w(r);
       }
     }
+    case RK_PSS_OWN: case RK_PSS_B2N8: case RK_PSS_MGF: case RK_PSS_CTR: case RK_PSS_XOR:
+      return pss_small(pss_view(L, B.rsa_core, B.sha_core, w), R, s);
     default: return ec_small(L, B, R, w, s);
   }
 }

@@ -150,20 +150,21 @@ __global__ void __launch_bounds__(64) k_rsa_core2(DevLayout L, const uint8_t* in
     kd_div(c2, 2 * nb + 1, n, nb, mu, nullptr, c2 + 2 * nb + 2, c2 + 4 * nb + 4);
   }
   __syncthreads();
-  for (int k = 0; k < 17; k++) {
+  const int NM = L.reg.n_modmul;
+  for (int k = 0; k < NM; k++) {
     uint64_t* mc = core + (size_t)k * MMW;
     // operands (exp_to_bits(65537) = [16,2,0,16]): muls[k] = muls[k-1].mod^2 with muls[0] = base^2;
     // resultMuls[0] = base * muls[15].mod (bigInt.circom:299-327)
     for (int i = g; i < K; i += G) {
       uint64_t xi;
-      if (k == 0 || k == 16) {
+      if (k == 0 || k == NM - 1) {
         const uint8_t* e = row + 32ull * (L.reg.in_sig + i);
         bad |= !in_is_u64(e);
         xi = in_u64(e);
       } else {
         xi = core[(size_t)(k - 1) * MMW + 3 * K + 1 + i];
       }
-      const uint64_t yi = k == 16 ? core[(size_t)15 * MMW + 3 * K + 1 + i] : xi;
+      const uint64_t yi = k == NM - 1 ? core[(size_t)(k - 1) * MMW + 3 * K + 1 + i] : xi;
       x[i] = xi; y[i] = yi;
       if (live) { mc[i] = xi; mc[K + i] = yi; }
     }

@@ -29,19 +29,21 @@ static int fail(int code, const std::string& msg) { g_err = msg; return code; }
 enum Phase {
   PH_LOAD, PH_SHA_CORE, PH_PREP, PH_RSA_CORE, PH_BJJ_CORE, PH_POS_CORE, PH_SMT,
   PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ,
-  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_COUNT
+  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_PSS, PH_COUNT
 };
 static const char* PHASE_NAMES[PH_COUNT] = {"load_values", "sha_core", "prep",     "rsa_core",  "bjj_core",
                                             "pos_core",    "smt",      "emit_gen", "emit_sha",  "emit_pos",
                                             "emit_bits",   "emit_flow", "emit_mm", "emit_bjj",
-                                            "ec_core",     "ec_table",  "emit_ect"};
+                                            "ec_core",     "ec_table",  "emit_ect", "pss"};
 static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k_prep",      "k_rsa_core",
                                               "k_bjj_core",    "k_pos_core",  "k_smt_prep+k_smt_chain",
                                               "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
                                               "k_emit_flow",   "k_emit_mm",   "k_emit_bjj",
-                                              "k_ec_core",     "k_ec_table",  "k_emit_ect"};
+                                              "k_ec_core",     "k_ec_table",  "k_emit_ect",
+                                              "k_pss_mgf+k_sha_core+k_pss_mdash"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
-                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT};
+                                        PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
+                                        PH_EMIT_SHA};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -136,6 +138,7 @@ struct pzk_instance {
   uint64_t *d_ec_core = nullptr, *d_ec_jac = nullptr;
   fr* d_ec_inv = nullptr;
   uint8_t* d_ec_tab = nullptr;
+  uint8_t* d_derived = nullptr;  // RSA-PSS derived SHA messages
   // staging for the host-buffer path
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -144,6 +147,7 @@ struct pzk_instance {
     DevLayout L{};
     L.wit_size = lay.wit_size;
     L.n_inputs = lay.n_inputs;
+    L.n_derived = lay.n_derived;
     L.n_regions = (uint32_t)lay.regions.size();
     L.n_sha = (uint32_t)lay.sha.size();
     L.sha_core_words = lay.sha_core_words;
@@ -244,12 +248,14 @@ static int upload(T** dst, const std::vector<T>& v) {
 
 static void free_scratch(pzk_instance* I) {
   void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_rsa_colsum, I->d_bjj_core,
-                  I->d_bjj_scratch, I->d_smt_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, I->d_ec_tab};
+                  I->d_bjj_scratch, I->d_smt_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, I->d_ec_tab,
+                  I->d_derived};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr; I->d_rsa_colsum = nullptr;
   I->d_bjj_core = nullptr; I->d_bjj_scratch = nullptr; I->d_smt_core = nullptr;
   I->d_ec_core = nullptr; I->d_ec_jac = nullptr; I->d_ec_inv = nullptr; I->d_ec_tab = nullptr;
+  I->d_derived = nullptr;
   I->cap = 0;
 }
 
@@ -419,6 +425,7 @@ static int ensure_scratch(pzk_instance* I, size_t batch) {
       {(void**)&I->d_ec_jac, L.is_ecdsa ? 8ull * EC_JAC_WORDS * batch : 0},
       {(void**)&I->d_ec_inv, L.is_ecdsa ? 32ull * EC_N_INV * batch : 0},
       {(void**)&I->d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
+      {(void**)&I->d_derived, 32ull * L.n_derived * batch},
   };
   for (auto& r : req)
     if (r.bytes && hipMalloc(r.p, r.bytes) != hipSuccess) {
@@ -451,7 +458,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   ValueStore vs{I->d_values, B};
   PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix};
   Bufs bufs{d_inputs, I->d_sha_core, I->d_rsa_core, I->d_pos_core, I->d_bjj_core, I->d_smt_core, vs, d_wtns, stride,
-            d_status, I->d_ec_core, I->d_ec_inv, I->d_ec_tab, I->d_inv_small};
+            d_status, I->d_ec_core, I->d_ec_inv, I->d_ec_tab, I->d_inv_small, I->d_derived};
   Timing* T = nullptr;
   int slot = 0;
   if (exec && (exec->flags & PZK_EXEC_TIMING)) {
@@ -483,7 +490,8 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   { PhaseScope ps(T, slot, PH_LOAD, st);
     HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, I->d_values, B, st)); }
   if (!lay.is_register) {
-    { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
+    { PhaseScope ps(T, slot, PH_SHA_CORE, st);
+      HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, 0, L.n_sha, I->d_sha_core, d_status, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
     for (int e = 0; e < E_COUNT; e++)
       if ((rc = emit(e, st))) return rc;
@@ -499,15 +507,37 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha;
     HIPCHK(hipEventRecord(I->ev_load, st));
     HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_load, 0));
+    const bool pss = lay.reg.pss_s8 != 0;
+    const uint32_t n_sha_main = pss ? (uint32_t)lay.reg.j_mgf : (uint32_t)lay.sha.size();
     if (!lay.is_ecdsa) {
       { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
         HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
+      if (!pss) {
+        HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+        if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
+        HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+      }
+    }
+    { PhaseScope ps(T, slot, PH_SHA_CORE, st);
+      HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, 0, n_sha_main, I->d_sha_core, d_status, B, st)); }
+    HIPCHK(hipEventRecord(I->ev_sha, st));
+    if (pss) {
+      // RSA-PSS chain (pss.hpp) behind the RSA core on s_rsa: MGF1 messages from EM, their hashes,
+      // M' (needs the SA digest), its hash; then the BigMultModP emitter and the derived hashers'
+      // SHA regions. ev_rsa marks the chain's end: the PSS checks and regions read all of it.
+      HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_sha, 0));
+      { PhaseScope ps(T, slot, PH_PSS, s_rsa);
+        HIPCHK(launch_pss(L, 0, I->d_rsa_core, I->d_sha_core, I->d_derived, B, s_rsa));
+        HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, (uint32_t)lay.reg.j_mgf, (uint32_t)lay.reg.n_mgf,
+                               I->d_sha_core, d_status, B, s_rsa));
+        HIPCHK(launch_pss(L, 1, I->d_rsa_core, I->d_sha_core, I->d_derived, B, s_rsa));
+        HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, (uint32_t)lay.reg.j_hd, 1, I->d_sha_core, d_status, B,
+                               s_rsa)); }
       HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
-      if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
+      if ((rc = emit(E_MM, s_rsa))) return rc;
+      if ((rc = emit(E_SHAD, s_rsa))) return rc;
       HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
     }
-    { PhaseScope ps(T, slot, PH_SHA_CORE, st); HIPCHK(launch_sha_core(L, d_inputs, I->d_sha_core, d_status, B, st)); }
-    HIPCHK(hipEventRecord(I->ev_sha, st));
     if (lay.is_ecdsa) {
       // ECDSA chain (needs the SA digest): EC core, value tables, table-block emission on s_rsa
       HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_sha, 0));

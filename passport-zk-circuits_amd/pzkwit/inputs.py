@@ -100,6 +100,29 @@ def pkcs1v15_sha256_sign(key: RsaKey, msg: bytes) -> int:
     return key.sign_raw(int.from_bytes(em, "big"))
 
 
+def mgf1_sha256(seed: bytes, length: int) -> bytes:
+    out = b""
+    for c in range((length + 31) // 32):
+        out += hashlib.sha256(seed + c.to_bytes(4, "big")).digest()
+    return out[:length]
+
+
+def pss_salt_len(sig):
+    """SALT_LEN of VerifyRsaPssSig for SIGNATURE_TYPE 10-12 (signatureVerification.circom:46-62)."""
+    return 64 if sig == 12 else 32
+
+
+def pss_sha256_sign(key: RsaKey, msg: bytes, salt: bytes) -> int:
+    """RSASSA-PSS (RFC 8017 9.1.1) with SHA-256 and MGF1-SHA-256, emBits = modBits - 1."""
+    h = hashlib.sha256(msg).digest()
+    em_len = key.bits // 8
+    hh = hashlib.sha256(b"\x00" * 8 + h + salt).digest()
+    db = b"\x00" * (em_len - len(salt) - 32 - 2) + b"\x01" + salt
+    masked = bytes(a ^ b for a, b in zip(db, mgf1_sha256(hh, len(db))))
+    masked = bytes([masked[0] & 0x7F]) + masked[1:]
+    return key.sign_raw(int.from_bytes(masked + hh + b"\xbc", "big"))
+
+
 # -------------------------------------------------------------- ECDSA P-256 (synthetic)
 # secp256r1 (signatureVerification.circom:177-182 passes its A, B, P as 4 x 64-bit limbs)
 P256_P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
@@ -193,9 +216,10 @@ def _dg15_rsa1024(rng):
 
 
 def _keygen(args):
-    seed, k, bits = args
+    seed, k, bits = args[:3]
+    e = args[3] if len(args) > 3 else 65537
     rng = SplitMix64((seed << 32) ^ (0x4B455900 + k))
-    return EcKey(rng) if bits == "p256" else RsaKey(bits, rng)
+    return EcKey(rng) if bits == "p256" else RsaKey(bits, rng, e)
 
 
 class PassportGen:
@@ -214,7 +238,8 @@ class PassportGen:
             key_bits = "p256"
         elif self.params["sig"] == 2 and key_bits == 2048:
             key_bits = 4096
-        jobs = [(seed, k, key_bits) for k in range(n_keys)]
+        e = 3 if self.params["sig"] == 10 else 65537  # SIG 10: RSA-PSS with e = 3
+        jobs = [(seed, k, key_bits) if e == 65537 else (seed, k, key_bits, e) for k in range(n_keys)]
         workers = workers or min(16, os.cpu_count() or 1)
         if n_keys >= 8 and workers > 1:
             from concurrent.futures import ProcessPoolExecutor
@@ -282,7 +307,12 @@ class PassportGen:
         sa[sa_shift - 2:sa_shift] = b"\x04\x20"
         sa[sa_shift:sa_shift + 32] = hashlib.sha256(ec).digest()
         sa = bytes(sa)
-        sig = key.sign(sa, rng) if isinstance(key, EcKey) else pkcs1v15_sha256_sign(key, sa)
+        if isinstance(key, EcKey):
+            sig = key.sign(sa, rng)
+        elif 10 <= pr["sig"] <= 12:
+            sig = pss_sha256_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])))
+        else:
+            sig = pkcs1v15_sha256_sign(key, sa)
         sk = int.from_bytes(hashlib.sha256(ec).digest()[:31], "big")  # getFakeIdenData :630
         pkh = self.pk_hash(key)
         siblings = [0] * 80

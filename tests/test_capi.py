@@ -69,6 +69,9 @@ PARAM_SETS = [
     dict(I.CANONICAL, sig=2),                      # RSA-4096 (K = 64 limbs)
     dict(I.CANONICAL, sig=20),                     # ECDSA secp256r1
     dict(I.CANONICAL, sig=20, aa=0, doc=1),        # ECDSA, TD1, no AA
+    dict(I.CANONICAL, sig=10),                     # RSA-PSS, e = 3, salt 32
+    dict(I.CANONICAL, sig=11),                     # RSA-PSS, e = 65537, salt 32
+    dict(I.CANONICAL, sig=12, aa=0),               # RSA-PSS, salt 64, no AA
 ]
 
 

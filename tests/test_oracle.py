@@ -182,3 +182,40 @@ def test_ecdsa_oracle_rejects_off_curve_key(oracle, ec_passports):
     # PointOnCurve of the first doubling: the non-exact carries of BigIntIsZero fail their
     # Num2Bits range checks (bitify.circom:26) before the final `=== 0` (bigIntComparators.circom:128)
     assert rc in (1, 12)
+
+
+# ---------------------------------------------------------------- RSA-PSS (SIGNATURE_TYPE 10-12)
+# Pin: synthetic signatures come from an independent RFC 8017 RSASSA-PSS signer (pzkwit.inputs,
+# hashlib MGF1-SHA-256). The restatement of VerifyRsaPssSig (rsaPss.circom:18-204) only passes its
+# final `hDash256.out === hash` if EM bits, MGF1 blocks, the XOR, the salt and M' are all right.
+@pytest.fixture(scope="module")
+def pss_gens():
+    return {sig: I.PassportGen(seed=11, n_keys=1, params=dict(I.CANONICAL, sig=sig), workers=1) for sig in (10, 11, 12)}
+
+
+@pytest.mark.parametrize("sig", [10, 11, 12])
+def test_pss_oracle_verifies_and_public_outputs(oracle, pss_gens, sig):
+    from refmath import aa_rsa_hash, dg1_commitment
+    params = dict(I.CANONICAL, sig=sig)
+    pp = pss_gens[sig].passport_at(0)
+    rc, w = oracle.register_witness(oracle.register_params(**params), I.pack_register_inputs(pp, params))
+    assert rc == 0
+    v = [oracle.from_elem(w[i]) for i in range(6)]
+    assert v[1] == aa_rsa_hash(pp["dg15"], 256)
+    sah = hashlib.sha256(pp["sa"]).digest()
+    hb = [(sah[i // 8] >> (7 - i % 8)) & 1 for i in range(256)]
+    assert v[2] == field.poseidon([sum(hb[i] << i for i in range(252))])
+    assert v[3] == dg1_commitment(pp["dg1"], pp["sk"])
+    assert v[5] == pp["root"] == field.poseidon([pp["pk_hash"]] * 2 + [1])
+
+
+def test_pss_oracle_rejects_bad_signatures(oracle, pss_gens):
+    params = dict(I.CANONICAL, sig=11)
+    prm = oracle.register_params(**params)
+    g = pss_gens[11]
+    pp = dict(g.passport_at(1))
+    pp["sig"] = pp["sig"] + 1  # EM no longer ends in 0xBC
+    assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 17  # rsaPss.circom:73
+    pp = dict(g.passport_at(1))
+    pp["sig"] = I.pss_sha256_sign(g.keys[0], pp["sa"] + b"x", bytes(32))  # a valid PSS signature of another message
+    assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 18  # rsaPss.circom:182

@@ -42,7 +42,7 @@ typedef struct pzk_params {
   int32_t ec_block_number;    /* EC_BLOCK_NUMBER */
   int32_t ec_shift;           /* EC_SHIFT (bits) */
   int32_t dg1_shift;          /* DG1_SHIFT (bits) */
-  int32_t aa_signature_algo;  /* AA_SIGNATURE_ALGO (0 = none, 1 = RSA-1024) */
+  int32_t aa_signature_algo;  /* AA_SIGNATURE_ALGO (0 = none, 1..19 = RSA-1024 key, 20..25 = EC key) */
   int32_t dg15_shift;         /* DG15_SHIFT (bits) */
   int32_t dg15_block_number;  /* DG15_BLOCK_NUMBER */
   int32_t aa_shift;           /* AA_SHIFT (bits) */

@@ -1251,16 +1251,35 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
 }
 
 /* ======================================================= RegisterIdentity */
+/* AA_SIGNATURE_ALGO >= 20: elliptic-curve AA key (identity.circom:51-84): x, y of EC_FIELD_SIZE bits
+ * each at AA_SHIFT, hashed as Poseidon2 of their low HASH_SIZE bits; 1..19: RSA-1024 key chunks */
+static int aa_is_ec(int aa) { return aa >= 20; }
+static int aa_field(int aa) { return aa == 22 ? 320 : aa == 23 ? 192 : 256; }
+static int aa_hsize(int aa) { return aa == 23 ? 192 : 248; }
 static size_t sz_regid(const orc_params *P) {
   int dg15Len = P->dg15_blocks * 512, ch = P->doc == 1 ? 190 : 186;
   size_t own = 3 + 1024 + (size_t)dg15Len + 1;
-  size_t aa = P->aa ? 4 * sz_bits2num(200) + sz_bits2num(224) + sz_poseidon(5) : 0;
+  size_t aa = !P->aa ? 0 : aa_is_ec(P->aa) ? 2 * sz_bits2num(aa_hsize(P->aa)) + sz_poseidon(2)
+                                           : 4 * sz_bits2num(200) + sz_bits2num(224) + sz_poseidon(5);
   return own + aa + sz_poseidon(5) + 4 * sz_bits2num(ch) + sz_poseidon(1) + sz_bjjmul() + sz_poseidon(2);
 }
 static void run_regid(ctx_t *c, size_t b, const orc_params *P) {
   int dg15Len = P->dg15_blocks * 512, ch = P->doc == 1 ? 190 : 186;
   size_t dg1 = b + 3, dg15 = dg1 + 1024, sk = dg15 + dg15Len, p = sk + 1;
-  if (P->aa) {
+  if (P->aa && aa_is_ec(P->aa)) {
+    int F = aa_field(P->aa), HS = aa_hsize(P->aa), XY = F - HS;
+    size_t xn = p, yn = xn + sz_bits2num(HS), h = yn + sz_bits2num(HS);
+    p = h + sz_poseidon(2);
+    for (int i = 0; i < HS; i++) {
+      W(xn + 1 + HS - 1 - i) = W(dg15 + P->aa_shift + i + XY);
+      W(yn + 1 + HS - 1 - i) = W(dg15 + P->aa_shift + F + i + XY);
+    }
+    run_bits2num(c, xn, HS);
+    run_bits2num(c, yn, HS);
+    W(h + 1) = W(xn); W(h + 2) = W(yn);
+    run_poseidon(c, h, 2);
+    W(b) = W(h);
+  } else if (P->aa) {
     size_t chunks[5];
     for (int j = 0; j < 4; j++) {
       chunks[j] = p; p += sz_bits2num(200);
@@ -1310,7 +1329,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa == 0 || P->aa == 1) &&
+  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 

@@ -47,14 +47,19 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool ecdsa = p.signature_type == 20;
   if (p.dg_hash_type != 256) { why = "DG_HASH_TYPE must be 256 (SHA-256 chunks)"; return false; }
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
-  if (p.aa_signature_algo != 0 && p.aa_signature_algo != 1) { why = "AA_SIGNATURE_ALGO must be 0 or 1"; return false; }
+  // AA_SIGNATURE_ALGO: 0 none, 1..19 RSA-1024 key (identity.circom:25-49), >= 20 EC key (:51-84); the raw value
+  // also scales the DG15 IsEqual inputs of the flow (passportVerificationFlow.circom:45-46,73-74)
+  if (p.aa_signature_algo < 0 || p.aa_signature_algo > 25) { why = "AA_SIGNATURE_ALGO must be 0..25"; return false; }
+  const bool aa_ec = p.aa_signature_algo >= 20;
+  const int aa_f = p.aa_signature_algo == 22 ? 320 : p.aa_signature_algo == 23 ? 192 : 256;
+  const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
   const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : 32;  // signature / pubkey input length
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
   const int dg15shift = aa ? p.dg15_shift : 256;
   if (p.dg1_shift < 0 || p.dg1_shift + 256 > ecLen || dg15shift < 24 || dg15shift + 256 > ecLen ||
-      p.ec_shift < 0 || p.ec_shift + 256 > 1024 || (aa && p.aa_shift + 1024 > d15Len)) {
+      p.ec_shift < 0 || p.ec_shift + 256 > 1024 || (aa && p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len)) {
     why = "shift parameters address bits outside the inputs";
     return false;
   }
@@ -83,6 +88,9 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   L.reg.in_dg15 = IN_DG15;
   L.reg.aa = aa ? 1 : 0;
   L.reg.aa_shift = p.aa_shift;
+  L.reg.aa_ec = aa_ec ? 1 : 0;
+  L.reg.aa_f = aa_f;
+  L.reg.aa_hs = aa_hs;
   L.reg.ecdsa = ecdsa ? 1 : 0;
   L.is_ecdsa = ecdsa;
   if (ecdsa && !ec_programs(L, why)) return false;
@@ -148,7 +156,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   sha_blocks(J_SA, IN_SA, 2);
   // PassportVerificationFlow(ecLen, 256, 256, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA)
   b.region(RK_FLOW, 1 + 256 + 256 + ecLen + 256 + 1024 + 776 + 776 * SZ_ISEQUAL,
-           {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, aa ? 1 : 0});
+           {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, p.aa_signature_algo});
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
   if (ecdsa) {
@@ -257,7 +265,13 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   if (d15Len) b.region(RK_INCOPY, d15Len, {IN_DG15});
   b.region(RK_INCOPY, 1, {IN_SK});
   int S_AA = -1;
-  if (aa) {
+  if (aa && aa_ec) {
+    // xToNum, yToNum = Bits2Num(HASH_SIZE) of the key's low bits, in[HS-1-i] = dg15[AA_SHIFT + XY + i] (+ EC_FIELD_SIZE for y)
+    const int xy = aa_f - aa_hs;
+    b.region(RK_BITS2NUM, sz_bits2num(aa_hs), {aa_hs, 0, IN_DG15 + p.aa_shift + xy + aa_hs - 1, -1});
+    b.region(RK_BITS2NUM, sz_bits2num(aa_hs), {aa_hs, 0, IN_DG15 + p.aa_shift + aa_f + xy + aa_hs - 1, -1});
+    S_AA = b.poseidon(2, {V_AA[0], V_AA[1]}, 0);
+  } else if (aa) {
     for (int j = 0; j < 4; j++) b.region(RK_BITS2NUM, sz_bits2num(200), {200, 0, IN_DG15 + p.aa_shift + j * 200 + 199, -1});
     b.region(RK_BITS2NUM, sz_bits2num(224), {224, 0, IN_DG15 + p.aa_shift + 800 + 223, -1});
     S_AA = b.poseidon(5, {V_AA[0], V_AA[1], V_AA[2], V_AA[3], V_AA[4]}, 0);

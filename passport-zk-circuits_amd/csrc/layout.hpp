@@ -153,6 +153,7 @@ struct RegInfo {
   uint32_t modmul_size;
   int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (secp256r1)
   int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
+  int32_t aa_ec, aa_f, aa_hs;      // EC active-authentication key: field bits, hashed bits (identity.circom:51-84)
   int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)
   int32_t j_mgf, n_mgf, j_hd;      // RSA-PSS SHA jobs: MGF1 blocks [j_mgf, j_mgf + n_mgf), M' hasher
 };

@@ -61,7 +61,14 @@ __global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inpu
     }
   }
   // AA key chunks: Bits2Num(200) x4 + Bits2Num(224), in[L-1-i] = dg15[AA_SHIFT + 200 j + i] (identity.circom:31-45)
-  if (R.aa) {
+  if (R.aa && R.aa_ec) {  // EC key: x, y low HASH_SIZE bits (identity.circom:70-81)
+    const int xy = R.aa_f - R.aa_hs;
+    for (int a = 0; a < 2; a++) {
+      const int base = R.in_dg15 + R.aa_shift + a * R.aa_f + xy;
+      fr v = bits_to_fr(R.aa_hs, [&](int k) { return in_bit(row, base + R.aa_hs - 1 - k, bad); });
+      vs.at(R.v_aa + a, w) = fr_to_mont(v);
+    }
+  } else if (R.aa) {
     for (int j = 0; j < 5; j++) {
       int Lb = j < 4 ? 200 : 224, base = R.in_dg15 + R.aa_shift + j * 200;
       fr v = bits_to_fr(Lb, [&](int k) { return in_bit(row, base + Lb - 1 - k, bad); });

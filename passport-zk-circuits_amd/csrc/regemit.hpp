@@ -296,6 +296,7 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
 // ------------------------------------------------------------------ PassportVerificationFlow
 __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint8_t eq[776], chain[776];
+  __shared__ fr invV;  // 1 / DG15_VERIFICATION (normal form): IsZero inverses of the scaled DG15 checks
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
@@ -316,6 +317,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
     else { a = (i >= 4 ? 1u : 0u) * V; b = ebit(d15s - 24 + i) * V; }  // 0x0F prefix, MSB first
   };
   for (int k = threadIdx.x; k < 776; k += blockDim.x) { uint32_t a, b; pair(k, a, b); eq[k] = a == b; }
+  if (threadIdx.x == 0) invV = V > 1 ? fr_from_mont(fr_inv(fr_to_mont(fr_u64((uint64_t)V)))) : fr_u64(1);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint8_t c = 1;
@@ -342,8 +344,10 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
     if (t == 0 || t == 3) return el_u64(a == b);
     if (t == 1) return el_u64(a);
     if (t == 2) return el_u64(b);
-    int d = (int)b - (int)a;  // in {-1, 0, 1}; inverse of +-1 is itself
-    return d >= 0 ? el_u64((uint64_t)d) : el_fr(fr_sub(fr_zero(), fr_u64(1)));
+    // in = in[1] - in[0] in {-1, 0, 1} (scale 1) or {-V, 0, V} (DG15 checks, V = AA_SIGNATURE_ALGO)
+    const int d = (int)b - (int)a, ad = d < 0 ? -d : d;
+    const fr m = t == 4 ? fr_u64((uint64_t)ad) : ad <= 1 ? fr_u64((uint64_t)ad) : invV;
+    return d >= 0 ? el_fr(m) : el_fr(fr_sub(fr_zero(), m));
   });
 }
 

@@ -72,6 +72,10 @@ PARAM_SETS = [
     dict(I.CANONICAL, sig=10),                     # RSA-PSS, e = 3, salt 32
     dict(I.CANONICAL, sig=11),                     # RSA-PSS, e = 65537, salt 32
     dict(I.CANONICAL, sig=12, aa=0),               # RSA-PSS, salt 64, no AA
+    dict(I.CANONICAL, aa=2),                       # RSA AA key, DG15 checks scaled by 2
+    dict(I.CANONICAL, aa=20),                      # EC AA key (256-bit field, 248 hashed bits)
+    dict(I.CANONICAL, aa=22),                      # EC AA key, 320-bit field
+    dict(I.CANONICAL, sig=20, aa=23),              # ECDSA signature, 192-bit EC AA key
 ]
 
 

@@ -219,3 +219,29 @@ def test_pss_oracle_rejects_bad_signatures(oracle, pss_gens):
     pp = dict(g.passport_at(1))
     pp["sig"] = I.pss_sha256_sign(g.keys[0], pp["sa"] + b"x", bytes(32))  # a valid PSS signature of another message
     assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 18  # rsaPss.circom:182
+
+
+# ---------------------------------------------------------------- active-authentication key variants
+def _dg15_bits(pp, params):
+    from pzkwit.inputs import bits_msb_first, sha_pad
+    return bits_msb_first(sha_pad(pp["dg15"]))[:params["dg15_blocks"] * 512]
+
+
+@pytest.mark.parametrize("aa", [2, 20, 22, 23])
+def test_aa_variants_oracle_public_outputs(oracle, passports, aa):
+    """AA_SIGNATURE_ALGO 2 (RSA key; the flow's DG15 IsEqual inputs are scaled by 2) and 20 / 22 / 23
+    (EC key: dg15PubKeyHash = Poseidon2(x, y) of the key's low HASH_SIZE bits, identity.circom:51-84)."""
+    from refmath import aa_rsa_hash
+    params = dict(I.CANONICAL, aa=aa)
+    pp = passports[0]
+    rc, w = oracle.register_witness(oracle.register_params(**params), I.pack_register_inputs(pp, params))
+    assert rc == 0
+    got = oracle.from_elem(w[1])
+    if aa < 20:
+        assert got == aa_rsa_hash(pp["dg15"], 256)
+    else:
+        bits = _dg15_bits(pp, params)
+        f, hs = (320 if aa == 22 else 192 if aa == 23 else 256), (192 if aa == 23 else 248)
+        sh = params["aa_shift"] + f - hs
+        num = lambda b: int("".join(str(x) for x in b), 2)
+        assert got == field.poseidon([num(bits[sh:sh + hs]), num(bits[sh + f:sh + f + hs])])

@@ -18,32 +18,49 @@
  */
 
 /* ------------------------------------------------------------ curve constants */
-/* A, B, P: signatureVerification.circom:179-182 */
-static const uint64_t EC_A[4] = {18446744073709551612ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL};
-static const uint64_t EC_B[4] = {4309448131093880907ULL, 7285987128567378166ULL, 12964664127075681980ULL,
-                                 6540974713487397863ULL};
-static const uint64_t EC_P[4] = {18446744073709551615ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL};
-/* order: get.circom:155-156 */
-static const uint64_t EC_N[4] = {17562291160714782033ULL, 13611842547513532036ULL, 18446744073709551615ULL,
-                                 18446744069414584320ULL};
-/* dummyPoint: get.circom:91-93 */
-static const uint64_t EC_DUMMY[2][4] = {
-    {4148137498610012746ULL, 51237685452122967ULL, 6555942389409504868ULL, 799804747332166731ULL},
-    {13395177781894339167ULL, 1107697421929919296ULL, 6228258783500845564ULL, 11862546499924939746ULL}};
+/* A, B, P: signatureVerification.circom:179-182 (20: secp256r1), :191-196 (21: brainpoolP256r1);
+ * order: get.circom:155-156 / :158-159; dummyPoint: get.circom:91-93 / :87-89 */
+typedef struct {
+  uint64_t A[4], B[4], P[4], N[4], D[2][4];
+} ec_curve_t;
+static const ec_curve_t EC_CURVES[2] = {
+    {{18446744073709551612ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
+     {4309448131093880907ULL, 7285987128567378166ULL, 12964664127075681980ULL, 6540974713487397863ULL},
+     {18446744073709551615ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
+     {17562291160714782033ULL, 13611842547513532036ULL, 18446744073709551615ULL, 18446744069414584320ULL},
+     {{4148137498610012746ULL, 51237685452122967ULL, 6555942389409504868ULL, 799804747332166731ULL},
+      {13395177781894339167ULL, 1107697421929919296ULL, 6228258783500845564ULL, 11862546499924939746ULL}}},
+    {{16810331318623712729ULL, 18122579188607900780ULL, 17219079075415130087ULL, 9032542404991529047ULL},
+     {7767825457231955894ULL, 10773760575486288334ULL, 17523706096862592191ULL, 2800214691157789508ULL},
+     {2311270323689771895ULL, 7943213001558335528ULL, 4496292894210231666ULL, 12248480212390422972ULL},
+     {10384753744809580199ULL, 10104242082523752183ULL, 4496292894210231665ULL, 12248480212390422972ULL},
+     {{5870538370169240658ULL, 13064052279558318326ULL, 1032222391323187885ULL, 10478252910764369874ULL},
+      {9125809427693782222ULL, 4479624720887462683ULL, 4313457861005768495ULL, 11848267593595748038ULL}}}};
+/* the curve of the witness being computed (ec_select) */
+static const uint64_t *EC_A = EC_CURVES[0].A, *EC_B = EC_CURVES[0].B, *EC_P = EC_CURVES[0].P, *EC_N = EC_CURVES[0].N;
+static const uint64_t (*EC_DUMMY)[4] = EC_CURVES[0].D;
 
-/* get_g_pow_stride8_table_p256 (ec/powers/p256pows.circom:3): [32][256][2][4], from
- * data/p256_gpow8.bin (tools/extract_p256_table.py) */
+/* get_g_pow_stride8_table_<curve> (ec/powers/p256pows.circom:3, brainpoolP256r1pows.circom:3): [32][256][2][4],
+ * from data/<p256|bp256>_gpow8.bin (tools/extract_ec_table.py) */
+static uint64_t *EC_GPOW_T[2] = {NULL, NULL};
 static uint64_t *EC_GPOW = NULL;
-int orc_load_p256(const char *path) {
+int orc_load_ec_table(int curve, const char *path) {
+  if (curve < 0 || curve > 1) return -3;
   FILE *f = fopen(path, "rb");
   if (!f) return -1;
   uint64_t *t = malloc(32 * 256 * 8 * sizeof(uint64_t));
   size_t got = fread(t, sizeof(uint64_t), 32 * 256 * 8, f);
   fclose(f);
   if (got != 32 * 256 * 8) { free(t); return -2; }
-  free(EC_GPOW);
-  EC_GPOW = t;
+  free(EC_GPOW_T[curve]);
+  EC_GPOW_T[curve] = t;
   return 0;
+}
+int orc_load_p256(const char *path) { return orc_load_ec_table(0, path); }
+static void ec_select(int curve) {
+  const ec_curve_t *C = &EC_CURVES[curve];
+  EC_A = C->A; EC_B = C->B; EC_P = C->P; EC_N = C->N; EC_DUMMY = C->D;
+  EC_GPOW = EC_GPOW_T[curve];
 }
 #define GPOW(i, j, a, k) EC_GPOW[((((size_t)(i) * 256 + (j)) * 2 + (a)) * 4) + (k)]
 

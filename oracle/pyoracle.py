@@ -15,6 +15,7 @@ REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "build", "liboracle.so")
 POSEIDON_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "poseidon_t2_6.bin")
 P256_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "p256_gpow8.bin")
+BP256_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "bp256_gpow8.bin")
 
 P = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
@@ -52,10 +53,11 @@ def lib():
         rc = L.orc_load_poseidon(POSEIDON_BIN.encode())
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
-        L.orc_load_p256.argtypes = [ctypes.c_char_p]
-        rc = L.orc_load_p256(P256_BIN.encode())
-        if rc != 0:
-            raise RuntimeError("oracle: cannot load the P-256 generator table (%d)" % rc)
+        L.orc_load_ec_table.argtypes = [ctypes.c_int, ctypes.c_char_p]
+        for curve, path in enumerate((P256_BIN, BP256_BIN)):
+            rc = L.orc_load_ec_table(curve, path.encode())
+            if rc != 0:
+                raise RuntimeError("oracle: cannot load the generator table %s (%d)" % (path, rc))
         _lib = L
     return _lib
 

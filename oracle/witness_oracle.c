@@ -1329,7 +1329,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || (P->sig == 20 && EC_GPOW)) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
+  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 
@@ -1349,6 +1349,7 @@ int orc_register_witness(const orc_params *P, const uint8_t *inputs, uint8_t *wi
   if (!pos_loaded || !params_ok(P)) return -1;
   orc_init();
   ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
+  if (P->sig >= 20) ec_select(P->sig - 20);
   size_t nIn = orc_register_n_inputs(P), nW = orc_register_witness_size(P);
   memset(wit, 0, nW * 32);
   W(0) = ONE();

@@ -39,12 +39,12 @@ uint32_t modmul_size(int K) {
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool pss = p.signature_type >= 10 && p.signature_type <= 12;  // RSA-2048 PSS, SHA-256 (e = 3 for 10)
-  if (p.signature_type != 1 && p.signature_type != 2 && !pss && p.signature_type != 20) {
+  if (p.signature_type != 1 && p.signature_type != 2 && !pss && p.signature_type != 20 && p.signature_type != 21) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12 and ECDSA secp256r1 type 20 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
     return false;
   }
-  const bool ecdsa = p.signature_type == 20;
+  const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
   if (p.dg_hash_type != 256) { why = "DG_HASH_TYPE must be 256 (SHA-256 chunks)"; return false; }
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
   // AA_SIGNATURE_ALGO: 0 none, 1..19 RSA-1024 key (identity.circom:25-49), >= 20 EC key (:51-84); the raw value
@@ -92,6 +92,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   L.reg.aa_f = aa_f;
   L.reg.aa_hs = aa_hs;
   L.reg.ecdsa = ecdsa ? 1 : 0;
+  L.reg.ec_curve = p.signature_type == 21 ? 1 : 0;
   L.is_ecdsa = ecdsa;
   if (ecdsa && !ec_programs(L, why)) return false;
 

@@ -20,31 +20,48 @@
 
 namespace pzk {
 
-// ---- curve constants, 64-bit limbs little-endian
-// A, B, P: signatureVerification.circom:179-182; order: ec/get.circom:155-156; dummy: get.circom:91-93
-#define PZK_EC_CONSTS                                                                                            \
-  constexpr uint64_t EC_A[4] = {18446744073709551612ull, 4294967295ull, 0ull, 18446744069414584321ull};        \
-  constexpr uint64_t EC_B[4] = {4309448131093880907ull, 7285987128567378166ull, 12964664127075681980ull,        \
-                                6540974713487397863ull};                                                        \
-  constexpr uint64_t EC_P[4] = {18446744073709551615ull, 4294967295ull, 0ull, 18446744069414584321ull};        \
-  constexpr uint64_t EC_N[4] = {17562291160714782033ull, 13611842547513532036ull, 18446744073709551615ull,      \
-                                18446744069414584320ull};                                                       \
-  constexpr uint64_t EC_D[8] = {4148137498610012746ull,  51237685452122967ull,   6555942389409504868ull,       \
-                                799804747332166731ull,   13395177781894339167ull, 1107697421929919296ull,      \
-                                6228258783500845564ull,  11862546499924939746ull};
-PZK_EC_CONSTS
+// ---- curve constants, 64-bit limbs little-endian: [curve][A, B, P, order, dummy][limb]
+// curve 0 = secp256r1 (SIGNATURE_TYPE 20), 1 = brainpoolP256r1 (21). A, B, P: signatureVerification.circom:179-182,
+// :191-196; order: ec/get.circom:155-159; dummy: get.circom:87-93
+constexpr int EC_N_CURVES = 2;
+constexpr uint64_t EC_CURVE_K[EC_N_CURVES][5][8] = {
+    {{18446744073709551612ull, 4294967295ull, 0ull, 18446744069414584321ull},
+     {4309448131093880907ull, 7285987128567378166ull, 12964664127075681980ull, 6540974713487397863ull},
+     {18446744073709551615ull, 4294967295ull, 0ull, 18446744069414584321ull},
+     {17562291160714782033ull, 13611842547513532036ull, 18446744073709551615ull, 18446744069414584320ull},
+     {4148137498610012746ull, 51237685452122967ull, 6555942389409504868ull, 799804747332166731ull,
+      13395177781894339167ull, 1107697421929919296ull, 6228258783500845564ull, 11862546499924939746ull}},
+    {{16810331318623712729ull, 18122579188607900780ull, 17219079075415130087ull, 9032542404991529047ull},
+     {7767825457231955894ull, 10773760575486288334ull, 17523706096862592191ull, 2800214691157789508ull},
+     {2311270323689771895ull, 7943213001558335528ull, 4496292894210231666ull, 12248480212390422972ull},
+     {10384753744809580199ull, 10104242082523752183ull, 4496292894210231665ull, 12248480212390422972ull},
+     {5870538370169240658ull, 13064052279558318326ull, 1032222391323187885ull, 10478252910764369874ull,
+      9125809427693782222ull, 4479624720887462683ull, 4313457861005768495ull, 11848267593595748038ull}}};
 // constant limb i of curve constant id (RK_EC_CONST regions)
 enum { EC_K_A = 0, EC_K_B = 1, EC_K_P = 2, EC_K_ORDER = 3, EC_K_DUMMY = 4, EC_K_ONE = 5 };
-__host__ __device__ inline uint64_t ec_k(int id, int i) {
-  switch (id) {
-    case EC_K_A: return EC_A[i];
-    case EC_K_B: return EC_B[i];
-    case EC_K_P: return EC_P[i];
-    case EC_K_ORDER: return EC_N[i];
-    case EC_K_DUMMY: return EC_D[i];
-    default: return i == 0 ? 1 : 0;
-  }
+__host__ __device__ inline uint64_t ec_k(int curve, int id, int i) {
+  return id == EC_K_ONE ? (i == 0 ? 1 : 0) : EC_CURVE_K[curve][id][i];
 }
+
+// The EC kernels are compiled once per curve (kernels_ec.hip: PZK_EC_CURVE 0, kernels_ec_bp.hip: 1); their
+// device code lives in an inline namespace per curve, so the two instantiations link side by side and
+// the constants below are compile-time immediates in each.
+#ifndef PZK_EC_CURVE
+#define PZK_EC_CURVE 0
+#endif
+#if PZK_EC_CURVE == 0
+#define PZK_EC_NS ec_c0
+#else
+#define PZK_EC_NS ec_c1
+#endif
+inline namespace PZK_EC_NS {
+static constexpr int EC_CV = PZK_EC_CURVE;
+static constexpr const uint64_t (&EC_A)[8] = EC_CURVE_K[EC_CV][EC_K_A];
+static constexpr const uint64_t (&EC_B)[8] = EC_CURVE_K[EC_CV][EC_K_B];
+static constexpr const uint64_t (&EC_P)[8] = EC_CURVE_K[EC_CV][EC_K_P];
+static constexpr const uint64_t (&EC_N)[8] = EC_CURVE_K[EC_CV][EC_K_ORDER];
+static constexpr const uint64_t (&EC_D)[8] = EC_CURVE_K[EC_CV][EC_K_DUMMY];
+}  // namespace PZK_EC_NS
 
 // ---- EC point operations of one witness (fixed numbering, execution order of k_ec_core)
 constexpr int EC_OP_SD = 0;                                          // genmult getSecondDummy = 2 D (DBL)

@@ -8,6 +8,7 @@
 #include "core_util.hpp"
 
 namespace pzk {
+inline namespace PZK_EC_NS {
 
 // ============================================================ signed 256-bit integers
 struct I256 { uint32_t w[8]; };
@@ -241,6 +242,7 @@ struct EcTabCtx {
 
 // ============================================================ P-256 Montgomery fields (p and n)
 struct e8 { uint32_t v[8]; };
+#if PZK_EC_CURVE == 0
 struct ModP {
   static constexpr uint32_t m[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u,
                                     0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
@@ -265,6 +267,35 @@ struct ModN {
   static constexpr uint32_t minv = 0xee00bc4fu;
   static constexpr bool is_p = false;
 };
+#else
+// brainpoolP256r1 (RFC 5639 3.4): m, R^2 mod m, R mod m, m - 2 (Fermat exponent), -m^-1 mod 2^32; aR = A R mod p
+struct ModP {
+  static constexpr uint32_t m[8] = {0x1f6e5377u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
+                                    0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t r2[8] = {0xa6465b6cu, 0x8cfedf7bu, 0x614d4f4du, 0x5cce4c26u,
+                                     0x6b1ac807u, 0xa1ecdacdu, 0xe5957fa8u, 0x4717aa21u};
+  static constexpr uint32_t r1[8] = {0xe091ac89u, 0xdfecb7e2u, 0x2ad9dfd7u, 0x91c409dcu,
+                                     0x627c728du, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
+  static constexpr uint32_t e[8] = {0x1f6e5375u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
+                                    0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t minv = 0xcefd89b9u;
+  static constexpr bool is_p = true;
+  static constexpr uint32_t aR[8] = {0x69696261u, 0xd5d18edfu, 0xc1d20c64u, 0xa68123f1u,
+                                     0x6398556eu, 0x95ec1e5eu, 0xd666bc17u, 0x1e4676abu};
+};
+struct ModN {
+  static constexpr uint32_t m[8] = {0x974856a7u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
+                                    0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t r2[8] = {0x3312fca6u, 0xe1d8d8deu, 0x1134e4a0u, 0xf35d176au,
+                                     0x6c815cb0u, 0x9b7f25e7u, 0xc3236762u, 0x0b25f1b9u};
+  static constexpr uint32_t r1[8] = {0x68b7a959u, 0x6fe1f17du, 0x4a9e5908u, 0x73c6855cu,
+                                     0x627c728eu, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
+  static constexpr uint32_t e[8] = {0x974856a5u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
+                                    0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t minv = 0xcbb40ee9u;
+  static constexpr bool is_p = false;
+};
+#endif
 using ModPFwd = ModP;
 using ModNFwd = ModN;
 
@@ -351,9 +382,10 @@ __device__ __forceinline__ void e8_to_u64(const e8& a, uint64_t* x) {
   for (int i = 0; i < 4; i++) x[i] = (uint64_t)a.v[2 * i + 1] << 32 | a.v[2 * i];
 }
 
-// Jacobian points (Montgomery mod p), a = -3 (P-256: A = p - 3)
+// Jacobian points (Montgomery mod p)
 struct Jac { e8 x, y, z; };
-// dbl-2001-b
+#if PZK_EC_CURVE == 0
+// dbl-2001-b, a = -3 (P-256: A = p - 3)
 __device__ Jac jac_dbl(const Jac& P) {
   using M = ModP;
   e8 delta = m_mul<M>(P.z, P.z), gamma = m_mul<M>(P.y, P.y), beta = m_mul<M>(P.x, gamma);
@@ -369,6 +401,25 @@ __device__ Jac jac_dbl(const Jac& P) {
   R.y = m_sub<M>(m_mul<M>(alpha, m_sub<M>(b4, R.x)), g8);
   return R;
 }
+#else
+// dbl-2007-bl, general a (brainpoolP256r1)
+__device__ Jac jac_dbl(const Jac& P) {
+  using M = ModP;
+  e8 xx = m_mul<M>(P.x, P.x), yy = m_mul<M>(P.y, P.y), zz = m_mul<M>(P.z, P.z), yyyy = m_mul<M>(yy, yy);
+  e8 xyy = m_add<M>(P.x, yy);
+  e8 s = m_sub<M>(m_sub<M>(m_mul<M>(xyy, xyy), xx), yyyy);
+  s = m_add<M>(s, s);
+  e8 mm = m_add<M>(m_add<M>(xx, xx), xx);
+  mm = m_add<M>(mm, m_mul<M>(m_const<M>(M::aR), m_mul<M>(zz, zz)));
+  Jac R;
+  R.x = m_sub<M>(m_mul<M>(mm, mm), m_add<M>(s, s));
+  e8 y8 = m_add<M>(yyyy, yyyy); y8 = m_add<M>(y8, y8); y8 = m_add<M>(y8, y8);
+  R.y = m_sub<M>(m_mul<M>(mm, m_sub<M>(s, R.x)), y8);
+  e8 yz = m_add<M>(P.y, P.z);
+  R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), yy), zz);
+  return R;
+}
+#endif
 // add-2007-bl (P != +-Q; H = 0 gives Z3 = 0, flagged by the caller)
 __device__ Jac jac_add(const Jac& P, const Jac& Q) {
   using M = ModP;
@@ -813,4 +864,5 @@ __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work,
   for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = ect_value(tab, prog[h >> 1], h & 1);
 }
 
+}  // namespace PZK_EC_NS
 }  // namespace pzk

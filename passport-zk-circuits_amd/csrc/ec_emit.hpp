@@ -63,9 +63,10 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
   const fr* I = B.ec_inv + (size_t)w * EC_N_INV;
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   auto rec_out = [&](int op) { return C + ECC_REC + ECC_REC_WORDS * op + 16; };
+  const int cv = L.reg.ec_curve;  // this TU is curve-generic: constants by run-time curve id
   switch (R.kind) {
     case RK_EC_U64: return el_u64(C[R.a[0] + s]);
-    case RK_EC_CONST: return el_u64(ec_k(R.a[0], (int)s));
+    case RK_EC_CONST: return el_u64(ec_k(cv, R.a[0], (int)s));
     case RK_EC_GM_RCC: {  // resultCoordinateComputation[i][j][a][k] = equal[i][j] * point  (curve.circom:724-749)
       const uint32_t i = s >> 11, j = (s >> 3) & 255u, q = s & 7u;
       const uint32_t b = (uint32_t)((C[ECC_U1 + (i >> 3)] >> (8 * (i & 7))) & 255);
@@ -88,7 +89,7 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
       const int i = R.a[0];
       const uint64_t* left = i == 0 ? C + ECC_GM_AP : C + ECC_GM_RP + 8 * (i - 1);
       const uint64_t* right = C + ECC_GM_AP + 8 * (i + 1);
-      const uint64_t dx = EC_D[0], sdx = rec_out(EC_OP_SD)[0];
+      const uint64_t dx = ec_k(cv, EC_K_DUMMY, 0), sdx = rec_out(EC_OP_SD)[0];
       if (s < 24) {
         const int k = (int)s / 6, e = (int)s % 6;
         const uint64_t in0 = (k & 1) ? sdx : dx, in1 = k < 2 ? left[0] : right[0];
@@ -122,13 +123,13 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
       if (s == 0) return el_u64(nib);
       if (s <= 4) return el_u64((nib >> (s - 1)) & 1);
       if (s <= 8) return el_u64(u64_mask(nib, (int)s - 4));
-      return iseq_sig((int)s - 9, C[ECC_SM_RP + 8 * w4], EC_D[0], I[ECI_SM_ZR + w4]);
+      return iseq_sig((int)s - 9, C[ECC_SM_RP + 8 * w4], ec_k(cv, EC_K_DUMMY, 0), I[ECI_SM_ZR + w4]);
     }
     case RK_EC_SM_DSW: {  // doubleSwitcher[w-1][a][k]: bool = isZeroResult[w], in = (D, rp[w])
       const int w4 = R.a[0];
       const uint32_t q = s / 6, e = s % 6;
-      const uint64_t zr = C[ECC_SM_RP + 8 * w4] == EC_D[0];
-      return switcher_sig((int)e, zr, EC_D[q], C[ECC_SM_RP + 8 * w4 + q]);
+      const uint64_t zr = C[ECC_SM_RP + 8 * w4] == ec_k(cv, EC_K_DUMMY, 0);
+      return switcher_sig((int)e, zr, ec_k(cv, EC_K_DUMMY, (int)q), C[ECC_SM_RP + 8 * w4 + q]);
     }
     case RK_EC_SM_SEL: {  // getSum[w][a][k] (GetSum(16)) | partsEqual[w][k]
       const int w4 = R.a[0], bb = 252 - 4 * w4;
@@ -146,9 +147,9 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
     case RK_EC_SM_RSW: {  // isZeroAddition[w] | (resultSwitcherAddition, resultSwitcherDoubling)[w-1][a][k]
       const int w4 = R.a[0];
       const uint64_t* ap = C + ECC_SM_AP + 8 * w4;
-      if (s < 6) return iseq_sig((int)s, ap[0], EC_D[0], I[ECI_SM_ZA + w4 - 1]);
+      if (s < 6) return iseq_sig((int)s, ap[0], ec_k(cv, EC_K_DUMMY, 0), I[ECI_SM_ZA + w4 - 1]);
       const uint32_t t = s - 6, q = t / 12, e = t % 12;
-      const uint64_t za = ap[0] == EC_D[0], zr = C[ECC_SM_RP + 8 * w4] == EC_D[0];
+      const uint64_t za = ap[0] == ec_k(cv, EC_K_DUMMY, 0), zr = C[ECC_SM_RP + 8 * w4] == ec_k(cv, EC_K_DUMMY, 0);
       const uint64_t addq = rec_out(ec_op_sm_add(w4 - 1))[q], dblq = rec_out(ec_op_sm_dbl(4 * w4 - 1))[q];
       if (e < 6) return switcher_sig((int)e, za, addq, dblq);
       const uint64_t rsa0 = za ? dblq : addq;

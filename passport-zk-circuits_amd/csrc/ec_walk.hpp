@@ -16,6 +16,7 @@
 #include "ec_common.hpp"
 
 namespace pzk {
+inline namespace PZK_EC_NS {
 
 template <class C>
 struct EcWalk {
@@ -299,4 +300,5 @@ struct EcWalk {
   }
 };
 
+}  // namespace PZK_EC_NS
 }  // namespace pzk

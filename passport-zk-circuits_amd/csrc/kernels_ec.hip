@@ -1,5 +1,7 @@
-// ECDSA secp256r1 kernels (ec_core.hpp) and their launchers; a separate translation unit from
-// kernels.hip so the two compile in parallel.
+// ECDSA kernels (ec_core.hpp) and their launchers; a separate translation unit from kernels.hip so the
+// two compile in parallel. Compiled once per curve: this file for PZK_EC_CURVE 0 (secp256r1), and
+// kernels_ec_bp.hip includes it with PZK_EC_CURVE 1 (brainpoolP256r1). The curve-0 unit also defines
+// the public launchers, which dispatch on the instance's curve.
 #include <hip/hip_runtime.h>
 
 #include "bufs.hpp"
@@ -7,10 +9,11 @@
 #include "kernels.hpp"
 
 namespace pzk {
+inline namespace PZK_EC_NS {
 
 #define HIP_TRY(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
 
-hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
+hipError_t launch_ec_core_cv(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
                           uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st) {
   hipLaunchKernelGGL(k_ec_scalars, dim3((batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, ec_core, status, batch);
   HIP_TRY(hipGetLastError());
@@ -28,7 +31,7 @@ hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint3
   return hipGetLastError();
 }
 
-hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
+hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
                            uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st) {
   if (n_ops == 0) return hipSuccess;
   dim3 g((batch + 63) / 64, n_ops);
@@ -40,11 +43,39 @@ hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uin
   return hipGetLastError();
 }
 
-hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st) {
   if (n_work == 0) return hipSuccess;
   hipLaunchKernelGGL(k_emit_ect, dim3(n_work, batch), dim3(256), 0, st, L, work, B.ec_tab, B.wtns, B.stride);
   return hipGetLastError();
 }
 
+}  // namespace PZK_EC_NS
+
+#if PZK_EC_CURVE == 0
+namespace ec_c1 {
+hipError_t launch_ec_core_cv(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
+                             uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st);
+hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
+                              uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st);
+hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                              hipStream_t st);
+}  // namespace ec_c1
+
+hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
+                          uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st) {
+  return L.reg.ec_curve ? ec_c1::launch_ec_core_cv(L, inputs, sha_core, ec_core, ec_jac, ec_inv, status, batch, st)
+                        : ec_c0::launch_ec_core_cv(L, inputs, sha_core, ec_core, ec_jac, ec_inv, status, batch, st);
+}
+hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
+                           uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st) {
+  return L.reg.ec_curve ? ec_c1::launch_ec_table_cv(L, type, ops, n_ops, ec_core, ec_tab, status, batch, st)
+                        : ec_c0::launch_ec_table_cv(L, type, ops, n_ops, ec_core, ec_tab, status, batch, st);
+}
+hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                           hipStream_t st) {
+  return L.reg.ec_curve ? ec_c1::launch_emit_ect_cv(L, work, n_work, B, batch, st)
+                        : ec_c0::launch_emit_ect_cv(L, work, n_work, B, batch, st);
+}
+#endif
 }  // namespace pzk

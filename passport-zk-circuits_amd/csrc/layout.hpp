@@ -151,7 +151,8 @@ struct RegInfo {
   int32_t dg1_chunk, aa_shift, in_dg1, in_dg15, aa;
   int32_t n_modmul;
   uint32_t modmul_size;
-  int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (secp256r1)
+  int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (ECDSA)
+  int32_t ec_curve;                // 0: secp256r1 (20), 1: brainpoolP256r1 (21) (ec_common.hpp)
   int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
   int32_t aa_ec, aa_f, aa_hs;      // EC active-authentication key: field bits, hashed bits (identity.circom:51-84)
   int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)

@@ -310,12 +310,12 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
       rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
   }
   if (!rc && I->lay.is_ecdsa) {
-    std::string path = data_dir() + "/p256_gpow8.bin";
+    std::string path = data_dir() + (I->lay.reg.ec_curve ? "/bp256_gpow8.bin" : "/p256_gpow8.bin");
     std::vector<uint64_t> tab(32 * 256 * 8);
     FILE* fp = fopen(path.c_str(), "rb");
     size_t got = fp ? fread(tab.data(), 8, tab.size(), fp) : 0;
     if (fp) fclose(fp);
-    if (got != tab.size()) rc = fail(PZK_E_DATA, "cannot read the P-256 generator table " + path);
+    if (got != tab.size()) rc = fail(PZK_E_DATA, "cannot read the EC generator table " + path);
     if (!rc) rc = upload(&I->d_ec_gpow, tab);
     if (!rc) rc = upload(&I->d_ec_prog, I->lay.ec_prog);
     if (!rc) rc = upload(&I->d_ec_tab_off, I->lay.ec_tab_off);

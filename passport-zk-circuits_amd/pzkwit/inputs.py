@@ -123,56 +123,86 @@ def pss_sha256_sign(key: RsaKey, msg: bytes, salt: bytes) -> int:
     return key.sign_raw(int.from_bytes(masked + hh + b"\xbc", "big"))
 
 
-# -------------------------------------------------------------- ECDSA P-256 (synthetic)
-# secp256r1 (signatureVerification.circom:177-182 passes its A, B, P as 4 x 64-bit limbs)
-P256_P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
-P256_A = P256_P - 3
-P256_N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
-P256_G = (0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
-          0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)
+# -------------------------------------------------------------- ECDSA (synthetic)
+class Curve:
+    """Short-Weierstrass curve y^2 = x^3 + a x + b over F_p with generator g of order n."""
+
+    def __init__(self, name, p, a, b, n, g):
+        self.name, self.p, self.a, self.b, self.n, self.g = name, p, a, b, n, g
+
+    def add(self, p1, p2):
+        """Affine addition (None = point at infinity)."""
+        if p1 is None:
+            return p2
+        if p2 is None:
+            return p1
+        P = self.p
+        (x1, y1), (x2, y2) = p1, p2
+        if x1 == x2:
+            if (y1 + y2) % P == 0:
+                return None
+            lam = (3 * x1 * x1 + self.a) * pow(2 * y1, -1, P) % P
+        else:
+            lam = (y2 - y1) * pow(x2 - x1, -1, P) % P
+        x3 = (lam * lam - x1 - x2) % P
+        return x3, (lam * (x1 - x3) - y1) % P
+
+    def mul(self, k, pt=None):
+        pt = self.g if pt is None else pt
+        r = None
+        for i in reversed(range(k.bit_length())):
+            r = self.add(r, r)
+            if (k >> i) & 1:
+                r = self.add(r, pt)
+        return r
+
+
+# secp256r1, FIPS 186-4 D.1.2.3 (signatureVerification.circom:177-182 passes its A, B, P as 4 x 64-bit limbs)
+P256 = Curve("secp256r1",
+             p=0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF,
+             a=0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFC,
+             b=0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B,
+             n=0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551,
+             g=(0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+                0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5))
+# brainpoolP256r1, RFC 5639 3.4 (signatureVerification.circom:191-196)
+BP256 = Curve("brainpoolP256r1",
+              p=0xA9FB57DBA1EEA9BC3E660A909D838D726E3BF623D52620282013481D1F6E5377,
+              a=0x7D5A0975FC2C3057EEF67530417AFFE7FB8055C126DC5C6CE94A4B44F330B5D9,
+              b=0x26DC5C6CE94A4B44F330B5D9BBD77CBF958416295CF7E1CE6BCCDC18FF8C07B6,
+              n=0xA9FB57DBA1EEA9BC3E660A909D838D718C397AA3B561A6F7901E0E82974856A7,
+              g=(0x8BD2AEB9CB7E57CB2C4B482FFC81B7AFB9DE27E1E3BD23C23A4453BD9ACE3262,
+                 0x547EF835C3DAC4FD97F8461A14611DC9C27745132DED8E545C1D54C72F046997))
+EC_CURVES = {20: P256, 21: BP256}  # SIGNATURE_TYPE -> curve
+
+P256_P, P256_A, P256_N, P256_G = P256.p, P256.a, P256.n, P256.g
 
 
 def p256_add(p1, p2):
-    """Affine addition (None = point at infinity)."""
-    if p1 is None:
-        return p2
-    if p2 is None:
-        return p1
-    (x1, y1), (x2, y2) = p1, p2
-    if x1 == x2:
-        if (y1 + y2) % P256_P == 0:
-            return None
-        lam = (3 * x1 * x1 + P256_A) * pow(2 * y1, -1, P256_P) % P256_P
-    else:
-        lam = (y2 - y1) * pow(x2 - x1, -1, P256_P) % P256_P
-    x3 = (lam * lam - x1 - x2) % P256_P
-    return x3, (lam * (x1 - x3) - y1) % P256_P
+    return P256.add(p1, p2)
 
 
 def p256_mul(k, pt=P256_G):
-    r = None
-    for i in reversed(range(k.bit_length())):
-        r = p256_add(r, r)
-        if (k >> i) & 1:
-            r = p256_add(r, pt)
-    return r
+    return P256.mul(k, pt)
 
 
 class EcKey:
-    """P-256 signer key (ECDSA, SIG 20)."""
+    """ECDSA signer key (SIG 20: P-256, SIG 21: brainpoolP256r1)."""
 
-    def __init__(self, rng):
-        self.d = 1 + rng.below(P256_N - 1)
-        self.q = p256_mul(self.d)
+    def __init__(self, rng, curve=P256):
+        self.curve = curve
+        self.d = 1 + rng.below(curve.n - 1)
+        self.q = curve.mul(self.d)
         self.n = self.q  # the "pubkey" of the passport dict: (x, y)
 
     def sign(self, msg: bytes, rng):
         """ECDSA-SHA256 (r, s); h = the digest as an integer, not reduced (ecdsa.circom:30-38)."""
+        c = self.curve
         h = int.from_bytes(hashlib.sha256(msg).digest(), "big")
         while True:
-            k = 1 + rng.below(P256_N - 1)
-            r = p256_mul(k)[0] % P256_N
-            s = pow(k, -1, P256_N) * (h + r * self.d) % P256_N
+            k = 1 + rng.below(c.n - 1)
+            r = c.mul(k)[0] % c.n
+            s = pow(k, -1, c.n) * (h + r * self.d) % c.n
             if r and s:
                 return r, s
 
@@ -219,7 +249,11 @@ def _keygen(args):
     seed, k, bits = args[:3]
     e = args[3] if len(args) > 3 else 65537
     rng = SplitMix64((seed << 32) ^ (0x4B455900 + k))
-    return EcKey(rng) if bits == "p256" else RsaKey(bits, rng, e)
+    if bits == "p256":
+        return EcKey(rng)
+    if bits == "bp256":
+        return EcKey(rng, BP256)
+    return RsaKey(bits, rng, e)
 
 
 class PassportGen:
@@ -235,7 +269,7 @@ class PassportGen:
         self.rng = SplitMix64(seed)
         self.params = dict(CANONICAL if params is None else params)
         if self.params["sig"] >= 20:
-            key_bits = "p256"
+            key_bits = "bp256" if self.params["sig"] == 21 else "p256"
         elif self.params["sig"] == 2 and key_bits == 2048:
             key_bits = 4096
         e = 3 if self.params["sig"] == 10 else 65537  # SIG 10: RSA-PSS with e = 3

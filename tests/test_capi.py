@@ -76,6 +76,7 @@ PARAM_SETS = [
     dict(I.CANONICAL, aa=20),                      # EC AA key (256-bit field, 248 hashed bits)
     dict(I.CANONICAL, aa=22),                      # EC AA key, 320-bit field
     dict(I.CANONICAL, sig=20, aa=23),              # ECDSA signature, 192-bit EC AA key
+    dict(I.CANONICAL, sig=21),                     # ECDSA brainpoolP256r1
 ]
 
 
@@ -106,7 +107,7 @@ def test_small_circuit_layouts(oracle):
 
 
 def test_unsupported_params_rejected():
-    rc, _, _ = layout_sizes(dict(I.CANONICAL, sig=21))  # brainpoolP256r1: not built yet
+    rc, _, _ = layout_sizes(dict(I.CANONICAL, sig=22))  # brainpoolP320r1: not built yet
     assert rc == -2
     assert b"SIGNATURE_TYPE" in native.lib().pzk_last_error()
     rc, _, _ = layout_sizes(dict(I.CANONICAL, dg1_shift=2000))

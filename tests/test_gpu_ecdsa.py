@@ -67,3 +67,17 @@ def test_ecdsa_bad_signature_flags_lane(oracle, ec_gen):
     _, st, codes = _run(oracle, ECDSA, rows, expect_ok=False)
     assert codes == [0, 16]
     assert st[0] == 0 and st[1] == 16  # ecdsa.circom:81-83
+
+
+def test_brainpool_matches_oracle(oracle):
+    """SIGNATURE_TYPE 21 (brainpoolP256r1, general-a Jacobian doubling, its own fixed-base table):
+    every element bit-exact; a tampered signature flags ecdsa.circom:81-83."""
+    params = dict(I.CANONICAL, sig=21)
+    g = I.PassportGen(seed=17, n_keys=2, params=params, workers=1)
+    pps = [g.passport_at(0), g.passport_at(1, smt_depth=3), dict(g.passport_at(2))]
+    r, s = pps[2]["sig"]
+    pps[2]["sig"] = (r, (s + 1) % I.BP256.n)
+    rows = np.stack([I.pack_register_inputs(pp, params) for pp in pps])
+    _, st, codes = _run(oracle, params, rows, expect_ok=False)
+    assert codes == [0, 0, 16]
+    assert list(st) == [0, 0, 16]

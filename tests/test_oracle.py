@@ -245,3 +245,29 @@ def test_aa_variants_oracle_public_outputs(oracle, passports, aa):
         sh = params["aa_shift"] + f - hs
         num = lambda b: int("".join(str(x) for x in b), 2)
         assert got == field.poseidon([num(bits[sh:sh + hs]), num(bits[sh + f:sh + f + hs])])
+
+
+def test_brainpool_generator_table_is_pinned():
+    """data/bp256_gpow8.bin (extracted from ec/powers/brainpoolP256r1pows.circom) = j * 2^(8i) * G (RFC 5639)."""
+    t = np.fromfile(os.path.join(os.path.dirname(__file__), "..", "passport-zk-circuits_amd", "data",
+                                 "bp256_gpow8.bin"), dtype="<u8").reshape(32, 256, 2, 4)
+    rng = np.random.default_rng(8)
+    for i, j in [(0, 1), (31, 255)] + [tuple(int(v) for v in x) for x in rng.integers([0, 1], [32, 256], (4, 2))]:
+        pt = I.BP256.mul(j << (8 * i))
+        assert [sum(int(t[i, j, a, k]) << (64 * k) for k in range(4)) for a in range(2)] == list(pt), (i, j)
+
+
+def test_brainpool_oracle_verifies_and_rejects(oracle):
+    """SIGNATURE_TYPE 21: a valid brainpoolP256r1 ECDSA-SHA256 signature passes every check of the
+    restatement; s + 1 fails x1 mod n === r (ecdsa.circom:81-83); the pubkey hash is Poseidon2 of x, y mod 2^248."""
+    params = dict(I.CANONICAL, sig=21)
+    prm = oracle.register_params(**params)
+    g = I.PassportGen(seed=16, n_keys=1, params=params, workers=1)
+    pp = g.passport_at(0)
+    rc, w = oracle.register_witness(prm, I.pack_register_inputs(pp, params))
+    assert rc == 0
+    assert oracle.from_elem(w[_pk_hash_offset(params)]) == I.ecdsa_pk_hash(pp["n"]) == pp["pk_hash"]
+    bad = dict(pp)
+    r, s_ = pp["sig"]
+    bad["sig"] = (r, (s_ + 1) % I.BP256.n)
+    assert oracle.register_witness(prm, I.pack_register_inputs(bad, params))[0] == 16

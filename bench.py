@@ -63,8 +63,8 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
-WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11}
-SIG_SEED = {1: 3, 20: 5, 11: 7}
+WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
+SIG_SEED = {1: 3, 20: 5, 11: 7, 21: 9}
 
 
 def _cpu_work(args):
@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "sha256", "mixed"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "sha256", "mixed"], default="register")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
     ap.add_argument("--cpu-sample", type=int, default=None)
@@ -134,6 +134,10 @@ def main():
         log("inputs: %d passports generated in %.1fs" % (batch, time.time() - t0))
         metric = "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline"
         workload = "RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports (config 3)"
+        if sig == 21:
+            metric = "registerIdentityBuilder ECDSA-brainpoolP256r1 witnesses/sec, batch=4096 (SIGNATURE_TYPE 21)"
+            workload = "RegisterIdentityBuilder(21,256,3,4,600,248,1,1496,3,256) synthetic brainpoolP256r1 passports"
+            scratch_pw = 10 << 20
         if sig == 20:
             metric = "registerIdentityBuilder ECDSA-secp256r1 witnesses/sec, batch=4096 (config 5 slice)"
             workload = "RegisterIdentityBuilder(20,256,3,4,600,248,1,1496,3,256) synthetic P-256 passports"
@@ -243,7 +247,7 @@ def main():
         procs = max(1, min(16, os.cpu_count() or 1))
         if args.workload.startswith("register"):
             sig = WL_SIG[args.workload]
-            ns = args.cpu_sample or (48 if sig == 20 else 96 if sig == 11 else 128) * procs
+            ns = args.cpu_sample or (48 if sig >= 20 else 96 if sig == 11 else 128) * procs
             rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=SIG_SEED[sig], sig=sig)
         else:
             ns = args.cpu_sample or 64 * procs

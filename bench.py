@@ -243,7 +243,7 @@ def main():
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
         "phases": phases,
     }
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
         procs = max(1, min(16, os.cpu_count() or 1))
         if args.workload.startswith("register"):
             sig = WL_SIG[args.workload]

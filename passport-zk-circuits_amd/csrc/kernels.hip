@@ -307,7 +307,7 @@ hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const Pos
 
 hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
                        int32_t* status, hipStream_t st) {
-  hipLaunchKernelGGL(k_prep, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, vs, status);
+  hipLaunchKernelGGL(k_prep, dim3(vs.batch), dim3(64), 0, st, L, inputs, sha_core, vs, status);
   return hipGetLastError();
 }
 

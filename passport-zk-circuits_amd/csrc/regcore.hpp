@@ -25,20 +25,39 @@
 namespace pzk {
 
 // ============================================================================ k_prep
-// lane = witness. Runs after k_sha_core (needs the SA digest).
-__global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
+// wave = witness. Runs after k_sha_core (needs the SA digest). The Bits2Num chunks (AA key,
+// dg1) are assembled 64 bits per ballot: lane l reads input element base +- (64 q + l), so each
+// load instruction of the wave covers 2 KiB of one input row (one lane per witness read a
+// 32-byte element per bit from 64 rows 185 KB apart: 2.5 ms per 2048 witnesses on the chain).
+__device__ __forceinline__ fr wave_bits_fr(const uint8_t* row, int base, int L, int dir, bool& bad) {
+  const int lane = threadIdx.x & 63;
+  fr v = fr_zero();
+  for (int q = 0; 64 * q < L; q++) {  // wave-uniform
+    const int k = 64 * q + lane;
+    uint32_t b = 0;
+    if (k < L) b = in_bit(row, dir > 0 ? base + k : base + L - 1 - k, bad);
+    const uint64_t m = __ballot(b);
+    v.v[2 * q] = (uint32_t)m;
+    v.v[2 * q + 1] = (uint32_t)(m >> 32);
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
   core_priority();
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= vs.batch) return;
+  const uint32_t w = blockIdx.x;
+  if (w >= vs.batch) return;  // whole wave
+  const int lane = threadIdx.x;
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   bool bad = false;
-  vs.at(R.v_one, w) = fr_mont_one();
+  if (lane == 0) vs.at(R.v_one, w) = fr_mont_one();
   // pubkeyHasherRsa inputs: tempModulus[i] + pk[3i+2] = pk[3i]*2^128 + pk[3i+1]*2^64 + pk[3i+2]
-  // (passportVerificationBuilder.circom:182-191), in field arithmetic
+  // (passportVerificationBuilder.circom:182-191), in field arithmetic; lane i computes input i
   if (R.ecdsa) {
     // ECDSA: pubkeyHasher = Poseidon2(x mod 2^248, y mod 2^248) (passportVerificationBuilder.circom:193-230)
-    for (int a = 0; a < 2; a++) {
+    if (lane < 2) {
+      const int a = lane;
       fr v = fr_zero();
       for (int j = 0; j < 4; j++) {
         const uint8_t* e = row + 32ull * (R.in_pk + 4 * a + j);
@@ -49,44 +68,42 @@ __global__ void __launch_bounds__(64, 1) k_prep(DevLayout L, const uint8_t* inpu
       }
       vs.at(a ? R.v_pky : R.v_pkx, w) = fr_to_mont(v);
     }
-  } else {
+  } else if (lane < 5) {
+    const int i = lane;
     fr two64 = fr_zero(); two64.v[2] = 1;
     fr two128 = fr_zero(); two128.v[4] = 1;
     two64 = fr_to_mont(two64); two128 = fr_to_mont(two128);
-    for (int i = 0; i < 5; i++) {
-      fr a = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i)));
-      fr b = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 1)));
-      fr c = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 2)));
-      vs.at(R.v_pk + i, w) = fr_add(fr_add(fr_mul(a, two128), fr_mul(b, two64)), c);
-    }
+    fr a = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i)));
+    fr b = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 1)));
+    fr c = fr_to_mont(load_fr(row + 32ull * (R.in_pk + 3 * i + 2)));
+    vs.at(R.v_pk + i, w) = fr_add(fr_add(fr_mul(a, two128), fr_mul(b, two64)), c);
   }
-  // AA key chunks: Bits2Num(200) x4 + Bits2Num(224), in[L-1-i] = dg15[AA_SHIFT + 200 j + i] (identity.circom:31-45)
   if (R.aa && R.aa_ec) {  // EC key: x, y low HASH_SIZE bits (identity.circom:70-81)
     const int xy = R.aa_f - R.aa_hs;
     for (int a = 0; a < 2; a++) {
-      const int base = R.in_dg15 + R.aa_shift + a * R.aa_f + xy;
-      fr v = bits_to_fr(R.aa_hs, [&](int k) { return in_bit(row, base + R.aa_hs - 1 - k, bad); });
-      vs.at(R.v_aa + a, w) = fr_to_mont(v);
+      fr v = wave_bits_fr(row, R.in_dg15 + R.aa_shift + a * R.aa_f + xy, R.aa_hs, -1, bad);
+      if (lane == 0) vs.at(R.v_aa + a, w) = fr_to_mont(v);
     }
   } else if (R.aa) {
+    // AA key chunks: Bits2Num(200) x4 + Bits2Num(224), in[L-1-i] = dg15[AA_SHIFT + 200 j + i] (identity.circom:31-45)
     for (int j = 0; j < 5; j++) {
-      int Lb = j < 4 ? 200 : 224, base = R.in_dg15 + R.aa_shift + j * 200;
-      fr v = bits_to_fr(Lb, [&](int k) { return in_bit(row, base + Lb - 1 - k, bad); });
-      vs.at(R.v_aa + j, w) = fr_to_mont(v);
+      fr v = wave_bits_fr(row, R.in_dg15 + R.aa_shift + j * 200, j < 4 ? 200 : 224, -1, bad);
+      if (lane == 0) vs.at(R.v_aa + j, w) = fr_to_mont(v);
     }
   }
   // dg1 chunks: Bits2Num(186|190), in[j] = dg1[i*chunk + j] (identity.circom:95-101)
   for (int i = 0; i < 4; i++) {
-    int base = R.in_dg1 + i * R.dg1_chunk;
-    fr v = bits_to_fr(R.dg1_chunk, [&](int k) { return in_bit(row, base + k, bad); });
-    vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
+    fr v = wave_bits_fr(row, R.in_dg1 + i * R.dg1_chunk, R.dg1_chunk, +1, bad);
+    if (lane == 0) vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
   }
   // signedAttributesNum = Bits2Num(252)(saHash[0..251]) (passportVerificationBuilder.circom:165-172)
-  const ShaJob job = L.sha[R.j_sa];
-  const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
-  fr sn = bits_to_fr(252, [&](int k) { return (H[k >> 5] >> (31 - (k & 31))) & 1u; });
-  vs.at(R.v_sanum, w) = fr_to_mont(sn);
-  if (bad) set_status(status ? status + w : nullptr, ST_INPUT_RANGE);
+  if (lane == 0) {
+    const ShaJob job = L.sha[R.j_sa];
+    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
+    fr sn = bits_to_fr(252, [&](int k) { return (H[k >> 5] >> (31 - (k & 31))) & 1u; });
+    vs.at(R.v_sanum, w) = fr_to_mont(sn);
+  }
+  if (__ballot(bad) && lane == 0) set_status(status ? status + w : nullptr, ST_INPUT_RANGE);
 }
 
 // ============================================================================ RSA core

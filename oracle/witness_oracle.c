@@ -957,7 +957,7 @@ static void run_verifysig(ctx_t *c, size_t b, int K) {
  * VerifyRsaPssSig(64, K, SALT, EXP, 256) rsaPss.circom:18-204 with Mgf1Sha256 mgf1.circom:69-127.
  * SIG 10: e = 3, salt 32; SIG 11: e = 65537, salt 32; SIG 12: e = 65537, salt 64
  * (signatureVerification.circom:46-62). EM = PowerMod.out, 8K bytes; DB = EM_LEN - HASH_LEN - 1 bytes. */
-static int is_pss(int sig) { return sig >= 10 && sig <= 12; }
+static int is_pss(int sig) { return (sig >= 10 && sig <= 12) || sig == 14; }
 static int pss_salt(int sig) { return sig == 12 ? 64 : 32; }
 static long sig_exp(int sig) { return sig == 10 ? 3 : 65537; }
 
@@ -1154,7 +1154,7 @@ static void run_flow(ctx_t *c, size_t b, int ecLen, int dg1s, int dg15s, int ecs
 }
 
 /* ============================================ PassportVerificationBuilder */
-static int sig_chunks(int sig) { return sig == 2 ? 64 : 32; }
+static int sig_chunks(int sig) { return sig == 2 ? 64 : sig == 14 ? 48 : 32; }
 /* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
 static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
 

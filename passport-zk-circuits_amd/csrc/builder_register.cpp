@@ -38,10 +38,11 @@ uint32_t modmul_size(int K) {
 }
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
-  const bool pss = p.signature_type >= 10 && p.signature_type <= 12;  // RSA-2048 PSS, SHA-256 (e = 3 for 10)
+  // RSA-PSS with SHA-256: 10-12 RSA-2048 (e = 3 for 10, salt 64 for 12), 14 RSA-3072 (signatureVerification.circom:46-75)
+  const bool pss = (p.signature_type >= 10 && p.signature_type <= 12) || p.signature_type == 14;
   if (p.signature_type != 1 && p.signature_type != 2 && !pss && p.signature_type != 20 && p.signature_type != 21) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
     return false;
   }
   const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
@@ -53,7 +54,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool aa_ec = p.aa_signature_algo >= 20;
   const int aa_f = p.aa_signature_algo == 22 ? 320 : p.aa_signature_algo == 23 ? 192 : 256;
   const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
-  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : 32;  // signature / pubkey input length
+  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : p.signature_type == 14 ? 48 : 32;  // signature / pubkey input length
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }

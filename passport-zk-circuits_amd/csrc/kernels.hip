@@ -353,7 +353,10 @@ static bool rsa_core_lane() {
 hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
                            int32_t* status, uint32_t batch, hipStream_t st) {
   const bool lane = rsa_core_lane() && colsum;
-  if (L.reg.K == 32) {
+  if (L.reg.K == 48) {  // RSA-3072 (SIGNATURE_TYPE 14): cooperative core only
+    HIP_TRY((launch_rsa_core2<48, 16>(L, inputs, rsa_core, status, batch, st)));
+    hipLaunchKernelGGL(k_rsa_inv<48>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
+  } else if (L.reg.K == 32) {
     HIP_TRY((lane ? launch_rsa_lane<32, 64>(L, inputs, rsa_core, colsum, status, batch, st)
                   : launch_rsa_core2<32, 8>(L, inputs, rsa_core, status, batch, st)));
     hipLaunchKernelGGL(k_rsa_inv<32>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
@@ -424,6 +427,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
     case E_FLOW: hipLaunchKernelGGL(k_emit_flow, g, blk, 0, st, L, work, B); break;
     case E_MM:
       if (L.reg.K == 32) hipLaunchKernelGGL(k_emit_mm<32>, g, blk, 0, st, L, work, B);
+      else if (L.reg.K == 48) hipLaunchKernelGGL(k_emit_mm<48>, g, blk, 0, st, L, work, B);
       else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
       break;
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;

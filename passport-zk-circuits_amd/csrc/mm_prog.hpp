@@ -28,7 +28,8 @@ __host__ __device__ constexpr uint32_t mm_section_size(int K, int sec) {
     case MM_XYN: return 3 * K;
     case MM_MOUT: return BASE - 1;
     case MM_MCOPY: return 2 * K;
-    case MM_KARA: return mm_kara_size(K);
+    case MM_KARA:  // KaratsubaOverflow(K) for K = 2^m, else BigMultNonEqualOverflow(K, K) (bigIntOverflow.circom:38-72)
+      return (K & (K - 1)) == 0 ? mm_kara_size(K) : (2 * K - 1) + 2 * K + K * K + (2 * K - 1) * K;
     case MM_MODCHK: return 129 * K;
     case MM_GT0: return 1;
     case MM_GTIN: return 2 * K;

@@ -362,6 +362,7 @@ struct MMCore {
   int K;
   const uint64_t *x, *y, *q, *r, *n, *inv, *cr;  // LDS
   const uint64_t *cxy, *cqn;                      // LDS: column sums of x*y (2K-1) and q*n (2K), 3 words each
+  bool kara;                                      // x*y by KaratsubaOverflow (K = 2^m), else schoolbook
   const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32; else null)
   const uint8_t* kt_hi;
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
@@ -467,6 +468,30 @@ __device__ __forceinline__ W256 w_sub(const W256& a, const W256& b) {
   return r;
 }
 
+// BigMultNonEqualOverflow(G, L) tmpResult[i][j] of a (G limbs) x b (L limbs), G >= L
+// (bigIntHelpers.circom:55-124): a running sum along row i. Consecutive signals of a row sit in
+// consecutive lanes, so each lane forms its own term and a segmented inclusive scan across the wave
+// adds the earlier ones; the row's terms before this wave (if the row started in an earlier wave)
+// are added by the wave's first lane.
+__device__ __forceinline__ W256 bmneq_tmpr(const uint64_t* a, int G, const uint64_t* b, int L, uint32_t s) {
+  const int i = s / L, j = s - i * L, lane = threadIdx.x & 63;
+  auto term = [&](int t) -> U192 {
+    U192 acc;
+    if (i < G) { if (t <= i) acc.mac(a[i - t], b[t]); }
+    else if (t < G + L - 1 - i) acc.mac(a[G - 1 - t], b[i + t - G + 1]);
+    return acc;
+  };
+  U192 v = term(j);
+  if (lane == 0)
+    for (int t = 0; t < j; t++) u192_addto(v, term(t));
+  for (unsigned dd = 1; dd < 64; dd <<= 1) {
+    U192 o = u192_shfl_up(v, dd);
+    if ((int)dd <= j && (unsigned)lane >= dd) u192_addto(v, o);
+  }
+  if (i < L ? j > i : (i >= G && j >= G + L - 1 - i)) return w_zero();
+  return u192w(v);
+}
+
 // BigMultModP(64,K,K,K) block signal (bigInt.circom:206-272), addressed by the block program
 // (mm_prog.hpp): section + index within the section, so the emitter does no range cascade.
 __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
@@ -486,7 +511,17 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
     case MM_XYN: { int g = s / K, i = s - g * K; return w_u64(g == 0 ? C.x[i] : g == 1 ? C.y[i] : C.n[i]); }
     case MM_MOUT: return u192w(u192_at(C.cxy, (int)s));                // mult.out = x*y columns
     case MM_MCOPY: return w_u64(s < (uint32_t)K ? C.x[s] : C.y[s - K]);
-    case MM_KARA: return kara_sig(C, K, s);
+    case MM_KARA: {
+      if (C.kara) return kara_sig(C, K, s);
+      // BigMultNonEqualOverflow(K, K) of x, y: out[2K-1] | in1[K], in2[K] | tmpMults[K][K] | tmpResult[2K-1][K]
+      uint32_t e = s;
+      if (e < (uint32_t)(2 * K - 1)) return u192w(u192_at(C.cxy, (int)e));
+      e -= 2 * K - 1;
+      if (e < (uint32_t)(2 * K)) return w_u64(e < (uint32_t)K ? C.x[e] : C.y[e - K]);
+      e -= 2 * K;
+      if (e < (uint32_t)(K * K)) { const uint32_t i = e / K, j = e - i * K; U192 acc; acc.mac(C.x[i], C.y[j]); return u192w(acc); }
+      return bmneq_tmpr(C.x, K, C.y, K, e - K * K);
+    }
     case MM_MODCHK: {  // Num2Bits(64)(mod_i): out[64] | in | sum[64]
       uint32_t i = s / 129, t = s - 129 * i;
       uint64_t v = C.r[i];
@@ -523,28 +558,7 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
     case MM_M2OUT: return u192w(u192_at(C.cqn, (int)s));               // mult2.out = q*n columns
     case MM_M2IN: return w_u64(s < (uint32_t)DIV ? C.q[s] : C.n[s - DIV]);
     case MM_TMPM: { uint32_t i = s / K, j = s - i * K; U192 acc; acc.mac(C.q[i], C.n[j]); return u192w(acc); }
-    case MM_TMPR: {
-      // tmpResult[i][j] = sum_{t<=j} term(i, t): a running sum along the row. Consecutive signals of
-      // a row sit in consecutive lanes, so each lane forms its own term and a segmented inclusive
-      // scan across the wave adds the earlier ones; the row's terms before this wave (if the row
-      // started in an earlier wave) are added by the wave's first lane.
-      const int i = s / K, j = s - i * K, lane = threadIdx.x & 63;
-      auto term = [&](int t) -> U192 {
-        U192 a;
-        if (i < DIV) { if (t <= i) a.mac(C.q[i - t], C.n[t]); }
-        else if (t < DIV + K - 1 - i) a.mac(C.q[DIV - 1 - t], C.n[i + t - DIV + 1]);
-        return a;
-      };
-      U192 v = term(j);
-      if (lane == 0)
-        for (int t = 0; t < j; t++) u192_addto(v, term(t));
-      for (unsigned dd = 1; dd < 64; dd <<= 1) {
-        U192 o = u192_shfl_up(v, dd);
-        if ((int)dd <= j && (unsigned)lane >= dd) u192_addto(v, o);
-      }
-      if (i < K ? j > i : (i >= DIV && j >= DIV + K - 1 - i)) return w_zero();
-      return u192w(v);
-    }
+    case MM_TMPR: return bmneq_tmpr(C.q, DIV, C.n, K, s);  // tmpResult of mult2 = q * n
     case MM_ISZIN: {  // BigIntIsZero.in = x*y - q*n - r (signed)
       const int i = s;
       W256 dd = w_sub(u192w(u192_at(C.cxy, i)), u192w(u192_at(C.cqn, i)));
@@ -553,7 +567,7 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
     }
     case MM_CARRY: return w_from_fr(fr_from_i128(C.cr[2 * s], C.cr[2 * s + 1]));
     default: {  // MM_RANGE: Num2Bits(RL)(carry + 2^(RL-1))
-      const int MAXB = 128 + (K == 32 ? 7 : 8);  // 2*64 + log_ceil(2K)
+      const int MAXB = 128 + mm_log_ceil(2 * K);  // 2*64 + log_ceil(K + DIV - 1)
       const int RL = MAXB + 3 - 64;
       uint32_t per = 2 * RL + 1, i = s / per, t = s - per * i;
       uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1];
@@ -627,7 +641,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
     }
   }
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
-           cxy, cqn, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
+           cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   // section by section: every wave works inside one section (uniform branch), and each section

@@ -215,7 +215,7 @@ def ecdsa_pk_hash(q):
 
 def sig_input_len(sig):
     """signature / pubkey input lengths (registerIdentityBuilder.circom:131-140)."""
-    return 8 if sig >= 20 else 64 if sig == 2 else 32
+    return 8 if sig >= 20 else 64 if sig == 2 else 48 if sig == 14 else 32
 
 
 def sig_limbs(v, sig):
@@ -272,6 +272,8 @@ class PassportGen:
             key_bits = "bp256" if self.params["sig"] == 21 else "p256"
         elif self.params["sig"] == 2 and key_bits == 2048:
             key_bits = 4096
+        elif self.params["sig"] == 14 and key_bits == 2048:
+            key_bits = 3072
         e = 3 if self.params["sig"] == 10 else 65537  # SIG 10: RSA-PSS with e = 3
         jobs = [(seed, k, key_bits) if e == 65537 else (seed, k, key_bits, e) for k in range(n_keys)]
         workers = workers or min(16, os.cpu_count() or 1)
@@ -343,7 +345,7 @@ class PassportGen:
         sa = bytes(sa)
         if isinstance(key, EcKey):
             sig = key.sign(sa, rng)
-        elif 10 <= pr["sig"] <= 12:
+        elif 10 <= pr["sig"] <= 12 or pr["sig"] == 14:
             sig = pss_sha256_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])))
         else:
             sig = pkcs1v15_sha256_sign(key, sa)

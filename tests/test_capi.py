@@ -77,6 +77,7 @@ PARAM_SETS = [
     dict(I.CANONICAL, aa=22),                      # EC AA key, 320-bit field
     dict(I.CANONICAL, sig=20, aa=23),              # ECDSA signature, 192-bit EC AA key
     dict(I.CANONICAL, sig=21),                     # ECDSA brainpoolP256r1
+    dict(I.CANONICAL, sig=14),                     # RSA-3072 PSS (K = 48: schoolbook BigMultOverflow)
 ]
 
 

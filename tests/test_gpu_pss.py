@@ -1,5 +1,6 @@
 """GPU parity for RegisterIdentityBuilder with RSA-PSS signatures (SIGNATURE_TYPE 10, 11, 12:
-RSA-2048, SHA-256, MGF1-SHA-256; e = 3 / 65537, salt 32 / 64 bytes):
+RSA-2048, SHA-256, MGF1-SHA-256; e = 3 / 65537, salt 32 / 64 bytes; 14: RSA-3072, whose 48-limb
+BigMultModP multiplies by schoolbook BigMultNonEqualOverflow):
 every element of the O0 witness (3.29 M / 3.65 M elements) equals the CPU oracle's
 (VerifyRsaPssSig restatement, oracle/witness_oracle.c), lane status is OK, and lanes whose
 signature fails carry the check-site code of rsaPss.circom:73 / :182."""
@@ -17,10 +18,10 @@ KIND_NAMES.update({40: "PSS_OWN", 41: "PSS_B2N8", 42: "PSS_MGF", 43: "PSS_CTR", 
 
 @pytest.fixture(scope="module")
 def gens():
-    return {sig: I.PassportGen(seed=12, n_keys=2, params=dict(I.CANONICAL, sig=sig), workers=1) for sig in (10, 11, 12)}
+    return {sig: I.PassportGen(seed=12, n_keys=2, params=dict(I.CANONICAL, sig=sig), workers=1) for sig in (10, 11, 12, 14)}
 
 
-@pytest.mark.parametrize("sig", [10, 11, 12])
+@pytest.mark.parametrize("sig", [10, 11, 12, 14])
 def test_pss_matches_oracle(oracle, gens, sig):
     params = dict(I.CANONICAL, sig=sig)
     g = gens[sig]

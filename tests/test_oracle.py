@@ -190,10 +190,10 @@ def test_ecdsa_oracle_rejects_off_curve_key(oracle, ec_passports):
 # final `hDash256.out === hash` if EM bits, MGF1 blocks, the XOR, the salt and M' are all right.
 @pytest.fixture(scope="module")
 def pss_gens():
-    return {sig: I.PassportGen(seed=11, n_keys=1, params=dict(I.CANONICAL, sig=sig), workers=1) for sig in (10, 11, 12)}
+    return {sig: I.PassportGen(seed=11, n_keys=1, params=dict(I.CANONICAL, sig=sig), workers=1) for sig in (10, 11, 12, 14)}
 
 
-@pytest.mark.parametrize("sig", [10, 11, 12])
+@pytest.mark.parametrize("sig", [10, 11, 12, 14])
 def test_pss_oracle_verifies_and_public_outputs(oracle, pss_gens, sig):
     from refmath import aa_rsa_hash, dg1_commitment
     params = dict(I.CANONICAL, sig=sig)

@@ -64,7 +64,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
 WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
-SIG_SEED = {1: 3, 20: 5, 11: 7, 21: 9}
+SIG_SEED = {1: 3, 2: 4, 10: 6, 11: 7, 12: 8, 14: 10, 20: 5, 21: 9}
 
 
 def _cpu_work(args):
@@ -73,7 +73,7 @@ def _cpu_work(args):
     import pyoracle
     from pzkwit import inputs as I
     if kind.startswith("register"):
-        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=WL_SIG[kind]))
+        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=int(kind.split(":")[1])))
         nin, nw = pyoracle.register_sizes(prm)
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "sha256", "mixed"], default="register")
+    ap.add_argument("--sig", type=int, default=None, help="SIGNATURE_TYPE of a register workload (overrides --workload's)")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slab) size")
     ap.add_argument("--cpu-sample", type=int, default=None)
@@ -126,7 +127,7 @@ def main():
 
     scratch_pw = 1 << 20  # per-witness core scratch (bytes), for the slab sizing below
     if args.workload.startswith("register"):
-        sig = WL_SIG[args.workload]
+        sig = args.sig or WL_SIG[args.workload]
         batch = args.batch or 4096
         inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, dict(I.CANONICAL, sig=sig))
         t0 = time.time()
@@ -142,6 +143,9 @@ def main():
             metric = "registerIdentityBuilder ECDSA-secp256r1 witnesses/sec, batch=4096 (config 5 slice)"
             workload = "RegisterIdentityBuilder(20,256,3,4,600,248,1,1496,3,256) synthetic P-256 passports"
             scratch_pw = 10 << 20  # value tables (~8.4 MB) + EC core
+        if sig not in (1, 20, 21):
+            metric = "registerIdentityBuilder witnesses/sec, batch=4096 (SIGNATURE_TYPE %d)" % sig
+            workload = "RegisterIdentityBuilder(%d,256,3,4,600,248,1,1496,3,256) synthetic passports" % sig
         if sig == 11:
             metric = "registerIdentityBuilder RSA-PSS witnesses/sec, batch=4096 (SIGNATURE_TYPE 11)"
             workload = "RegisterIdentityBuilder(11,256,3,4,600,248,1,1496,3,256) synthetic RSA-2048 PSS passports"
@@ -246,13 +250,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
         procs = max(1, min(16, os.cpu_count() or 1))
         if args.workload.startswith("register"):
-            sig = WL_SIG[args.workload]
+            sig = args.sig or WL_SIG[args.workload]
             ns = args.cpu_sample or (48 if sig >= 20 else 96 if sig == 11 else 128) * procs
             rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=SIG_SEED[sig], sig=sig)
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)
-        v, cdt = cpu_baseline(args.workload, list(rows), procs)
+        kind = "register:%d" % sig if args.workload.startswith("register") else args.workload
+        v, cdt = cpu_baseline(kind, list(rows), procs)
         out["cpu_baseline"] = {"value": round(v, 2), "unit": "witnesses/s", "cores": procs, "kind": "port",
                                "sample": "%d witnesses of the same workload on %d processes (%.1fs wall)" % (
                                    ns, procs, cdt)}

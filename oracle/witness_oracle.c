@@ -429,6 +429,174 @@ static void run_shahash(ctx_t *c, size_t b, int B) {
   for (int q = 0; q < 256; q++) W(b + q) = W(h + q);
 }
 
+/* =================================================================== SHA-1
+ * Sha1HashChunks(B) hasher/sha1/sha1.circom:7-57 and its templates (sha1compression.circom,
+ * t.circom, f.circom, parity.circom, rotate.circom, xor4.circom, constants.circom; BinSum
+ * bitify/operations.circom:9-29; XOR3_v3 sha2/sha2Common.circom:102-113). Bit arrays named
+ * "MSB-first" hold bit 31 of the word at index 0. */
+static const uint32_t SHA1_H[5] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0};
+static const uint32_t SHA1_K[4] = {0x5a827999, 0x6ed9eba1, 0x8f1bbcdc, 0xca62c1d6};
+
+/* RotL(32, L) rotate.circom: out[32] | in[32]; out[i] = in[(i + L) % 32] */
+static void run_rotl(ctx_t *c, size_t b, int L) {
+  for (int i = 0; i < 32; i++) W(b + i) = W(b + 32 + (i + L) % 32);
+}
+/* H(x) / K(t) constants.circom: out[32] (MSB first) | Num2Bits(32)(constant) */
+static size_t sz_sha1const(void) { return 32 + sz_num2bits(32); }
+static void run_sha1const(ctx_t *c, size_t b, uint32_t v) {
+  size_t n = b + 32;
+  W(n + 32) = fr_u64(v);
+  run_num2bits(c, n, 32);
+  for (int k = 0; k < 32; k++) W(b + k) = W(n + 31 - k);
+}
+/* Xor4(32) xor4.circom: out | a | b | c | d | mid | aTemp */
+static void run_xor4(ctx_t *c, size_t b) {
+  for (int k = 0; k < 32; k++) {
+    uint64_t a = small(W(b + 32 + k)), bb = small(W(b + 64 + k)), cc = small(W(b + 96 + k)), d = small(W(b + 128 + k));
+    uint64_t mid = bb * cc, at = a ^ bb ^ cc;
+    W(b + 160 + k) = fr_u64(mid);
+    W(b + 192 + k) = fr_u64(at);
+    W(b + k) = fr_u64(at ^ d);
+  }
+}
+/* BinSum(N, L) operations.circom:9-29: out[L+N-1] | in[N][L] | sumN, bits2Num[N], num2Bits(L+N-1) */
+static size_t sz_binsum(int N, int L) { return (size_t)(L + N - 1) + (size_t)N * L + 2 * (size_t)N + (size_t)N * sz_bits2num(L) + sz_num2bits(L + N - 1); }
+static void run_binsum(ctx_t *c, size_t b, int N, int L) {
+  int O = L + N - 1;
+  size_t in = b + O, gs = in + (size_t)N * L, b2n = gs + 2 * (size_t)N, n2b = b2n + (size_t)N * sz_bits2num(L);
+  for (int i = 0; i < N; i++) {
+    size_t bn = b2n + (size_t)i * sz_bits2num(L);
+    for (int k = 0; k < L; k++) W(bn + 1 + k) = W(in + (size_t)i * L + k);
+    run_bits2num(c, bn, L);
+    W(gs + 1 + i) = W(bn);
+  }
+  run_getsum(c, gs, N);
+  W(n2b + O) = W(gs);
+  run_num2bits(c, n2b, O);
+  for (int k = 0; k < O; k++) W(b + k) = W(n2b + k);
+}
+/* fT(t) f.circom:34-74: out | b | c | d | maj (MajT: out|a|b|c|mid), parity (ParityT: out|a|b|c |
+ * XOR3_v3: out|a|b|c|mid), ch (ChT: out|a|b|c) */
+static size_t sz_ft(void) { return 128 + 160 + (128 + 160) + 128; }
+static void run_ft(ctx_t *c, size_t b, int t) {
+  size_t maj = b + 128, par = maj + 160, x3 = par + 128, ch = x3 + 160;
+  for (int k = 0; k < 32; k++) {
+    uint64_t x = small(W(b + 32 + k)), y = small(W(b + 64 + k)), z = small(W(b + 96 + k));
+    W(maj + 32 + k) = W(b + 32 + k); W(maj + 64 + k) = W(b + 64 + k); W(maj + 96 + k) = W(b + 96 + k);
+    W(maj + 128 + k) = fr_u64(y * z);
+    W(maj + k) = fr_u64((x & y) | (x & z) | (y & z));
+    W(par + 32 + k) = W(b + 32 + k); W(par + 64 + k) = W(b + 64 + k); W(par + 96 + k) = W(b + 96 + k);
+    W(x3 + 32 + k) = W(b + 32 + k); W(x3 + 64 + k) = W(b + 64 + k); W(x3 + 96 + k) = W(b + 96 + k);
+    W(x3 + 128 + k) = fr_u64(y * z);
+    W(x3 + k) = fr_u64(x ^ y ^ z);
+    W(par + k) = W(x3 + k);
+    W(ch + 32 + k) = W(b + 32 + k); W(ch + 64 + k) = W(b + 64 + k); W(ch + 96 + k) = W(b + 96 + k);
+    W(ch + k) = fr_u64(x ? y : z);
+    W(b + k) = t <= 19 ? W(ch + k) : (t <= 39 || t >= 60) ? W(par + k) : W(maj + k);
+  }
+}
+/* T(t) t.circom:8-57: out | a | b | c | d | e | kT | w | rotatel5, f, sumBinary (BinSum(5,32)),
+ * sum (Bits2Num(35)), getLastNBits(32) */
+static size_t sz_sha1t(void) { return 256 + 64 + sz_ft() + sz_binsum(5, 32) + sz_bits2num(35) + sz_lastnbits(32); }
+static void run_sha1t(ctx_t *c, size_t b, int t) {
+  size_t a = b + 32, bb = a + 32, cc = bb + 32, dd = cc + 32, e = dd + 32, kt = e + 32, w = kt + 32;
+  size_t r5 = b + 256, f = r5 + 64, bs = f + sz_ft(), sm = bs + sz_binsum(5, 32), ln = sm + sz_bits2num(35);
+  for (int k = 0; k < 32; k++) {
+    W(r5 + 32 + k) = W(a + k);
+    W(f + 32 + k) = W(bb + k); W(f + 64 + k) = W(cc + k); W(f + 96 + k) = W(dd + k);
+  }
+  run_rotl(c, r5, 5);
+  run_ft(c, f, t);
+  size_t bin = bs + 36;
+  for (int k = 0; k < 32; k++) {
+    W(bin + k) = W(r5 + 31 - k);
+    W(bin + 32 + k) = W(f + 31 - k);
+    W(bin + 64 + k) = W(e + 31 - k);
+    W(bin + 96 + k) = W(kt + 31 - k);
+    W(bin + 128 + k) = W(w + 31 - k);
+  }
+  run_binsum(c, bs, 5, 32);
+  for (int k = 0; k < 35; k++) W(sm + 1 + k) = W(bs + k);
+  run_bits2num(c, sm, 35);
+  W(ln + 33) = W(sm);
+  run_lastnbits(c, ln, 32);
+  for (int k = 0; k < 32; k++) W(b + k) = W(ln + 1 + 31 - k);
+}
+/* Sha1compression sha1compression.circom:7-132: out[160] | hin[160] | inp[512] | a, b, c, d, e [81][32] |
+ * w[80][32] | rotl1[64], xor4[64], rotl30[80], kT[80], tTmp[80], fSum[5] (BinSum(2,32)) */
+static size_t sz_sha1comp(void) {
+  return 160 + 160 + 512 + 5 * 81 * 32 + 80 * 32 + 64 * 64 + 64 * 224 + 80 * 64 + 80 * sz_sha1const() + 80 * sz_sha1t() +
+         5 * sz_binsum(2, 32);
+}
+static void run_sha1comp(ctx_t *c, size_t b) {
+  size_t hin = b + 160, inp = hin + 160, A = inp + 512, Bv = A + 81 * 32, Cv = Bv + 81 * 32, Dv = Cv + 81 * 32,
+         Ev = Dv + 81 * 32, Wv = Ev + 81 * 32, r1 = Wv + 80 * 32, x4 = r1 + 64 * 64, r30 = x4 + 64 * 224,
+         kk = r30 + 80 * 64, tt = kk + 80 * sz_sha1const(), fs = tt + 80 * sz_sha1t();
+  for (int t = 0; t < 16; t++)
+    for (int k = 0; k < 32; k++) W(Wv + 32 * t + k) = W(inp + 32 * t + k);
+  for (int t = 16; t < 80; t++) {
+    size_t x = x4 + (size_t)(t - 16) * 224, r = r1 + (size_t)(t - 16) * 64;
+    for (int k = 0; k < 32; k++) {
+      W(x + 32 + k) = W(Wv + 32 * (t - 3) + k); W(x + 64 + k) = W(Wv + 32 * (t - 8) + k);
+      W(x + 96 + k) = W(Wv + 32 * (t - 14) + k); W(x + 128 + k) = W(Wv + 32 * (t - 16) + k);
+    }
+    run_xor4(c, x);
+    for (int k = 0; k < 32; k++) W(r + 32 + k) = W(x + k);
+    run_rotl(c, r, 1);
+    for (int k = 0; k < 32; k++) W(Wv + 32 * t + k) = W(r + k);
+  }
+  for (int k = 0; k < 32; k++) {
+    W(A + k) = W(hin + k); W(Bv + k) = W(hin + 32 + k); W(Cv + k) = W(hin + 64 + k);
+    W(Dv + k) = W(hin + 96 + k); W(Ev + k) = W(hin + 128 + k);
+  }
+  for (int t = 0; t < 80; t++) {
+    size_t K = kk + (size_t)t * sz_sha1const(), T = tt + (size_t)t * sz_sha1t(), r = r30 + (size_t)t * 64;
+    run_sha1const(c, K, SHA1_K[t / 20]);
+    for (int k = 0; k < 32; k++) {
+      W(T + 32 + k) = W(A + 32 * t + k); W(T + 64 + k) = W(Bv + 32 * t + k); W(T + 96 + k) = W(Cv + 32 * t + k);
+      W(T + 128 + k) = W(Dv + 32 * t + k); W(T + 160 + k) = W(Ev + 32 * t + k); W(T + 192 + k) = W(K + k);
+      W(T + 224 + k) = W(Wv + 32 * t + k);
+      W(r + 32 + k) = W(Bv + 32 * t + k);
+    }
+    run_sha1t(c, T, t);
+    run_rotl(c, r, 30);
+    for (int k = 0; k < 32; k++) {
+      W(Ev + 32 * (t + 1) + k) = W(Dv + 32 * t + k);
+      W(Dv + 32 * (t + 1) + k) = W(Cv + 32 * t + k);
+      W(Cv + 32 * (t + 1) + k) = W(r + k);
+      W(Bv + 32 * (t + 1) + k) = W(A + 32 * t + k);
+      W(A + 32 * (t + 1) + k) = W(T + k);
+    }
+  }
+  const size_t regs[5] = {A, Bv, Cv, Dv, Ev};
+  for (int i = 0; i < 5; i++) {
+    size_t f = fs + (size_t)i * sz_binsum(2, 32), in = f + 33;
+    for (int k = 0; k < 32; k++) {
+      W(in + k) = W(hin + 32 * i + 31 - k);
+      W(in + 32 + k) = W(regs[i] + 80 * 32 + 31 - k);
+    }
+    run_binsum(c, f, 2, 32);
+    for (int k = 0; k < 32; k++) W(b + 32 * i + k) = W(f + k);
+  }
+}
+/* Sha1HashChunks(B) sha1.circom:7-57: out[160] | in[512B] | ha0..he0 (H(0..4)), sha1Compression[B] */
+static size_t sz_sha1chunks(int B) { return 160 + 512 * (size_t)B + 5 * sz_sha1const() + (size_t)B * sz_sha1comp(); }
+static void run_sha1chunks(ctx_t *c, size_t b, int B) {
+  size_t in = b + 160, hs = in + 512 * (size_t)B, cp = hs + 5 * sz_sha1const();
+  for (int j = 0; j < 5; j++) run_sha1const(c, hs + (size_t)j * sz_sha1const(), SHA1_H[j]);
+  for (int m = 0; m < B; m++) {
+    size_t q = cp + (size_t)m * sz_sha1comp(), hin = q + 160, inp = hin + 160;
+    for (int w = 0; w < 5; w++)
+      for (int k = 0; k < 32; k++)
+        W(hin + 32 * w + k) = m == 0 ? W(hs + (size_t)w * sz_sha1const() + k) : W(q - sz_sha1comp() + 32 * w + 31 - k);
+    for (int k = 0; k < 512; k++) W(inp + k) = W(in + 512 * (size_t)m + k);
+    run_sha1comp(c, q);
+  }
+  size_t last = cp + (size_t)(B - 1) * sz_sha1comp();
+  for (int i = 0; i < 5; i++)
+    for (int k = 0; k < 32; k++) W(b + (31 - k) + 32 * i) = W(last + k + 32 * i);
+}
+
 /* ================================================================ Poseidon */
 typedef struct { int t, nRP; fr_t *C, *M, *P, *S; } pos_params_t;
 static pos_params_t POS[18];
@@ -1402,6 +1570,18 @@ int orc_poseidon_hash(int n, const uint8_t *inputs, uint8_t *out) {
 }
 /* config 2: component main = Sha256HashChunks(B): [1, out[256], in[512B], ...] */
 size_t orc_sha256_witness_size(int B) { orc_init(); return 1 + sz_sha256chunks(B); }
+/* Sha1HashChunks(B) as main: [1, out[160], in[512B], ...] */
+size_t orc_sha1_witness_size(int B) { orc_init(); return 1 + sz_sha1chunks(B); }
+int orc_sha1_witness(int B, const uint8_t *inputs, uint8_t *wit) {
+  orc_init();
+  ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
+  size_t nW = orc_sha1_witness_size(B);
+  memset(wit, 0, nW * 32);
+  W(0) = ONE();
+  memcpy(&W(1 + 160), inputs, 512 * (size_t)B * 32);
+  run_sha1chunks(c, 1, B);
+  return c->err;
+}
 int orc_sha256_witness(int B, const uint8_t *inputs, uint8_t *wit) {
   orc_init();
   ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;

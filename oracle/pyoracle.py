@@ -50,6 +50,8 @@ def lib():
         L.orc_poseidon_hash.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_sha256_witness_size.restype = ctypes.c_size_t
         L.orc_sha256_witness.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sha1_witness_size.restype = ctypes.c_size_t
+        L.orc_sha1_witness.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         rc = L.orc_load_poseidon(POSEIDON_BIN.encode())
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
@@ -119,4 +121,14 @@ def register_witness(params, inputs, out=None):
     assert a.shape == (nin, 32), (a.shape, nin)
     w = out if out is not None else np.zeros((nw, 32), dtype=np.uint8)
     rc = L.orc_register_witness(ctypes.byref(params), a.ctypes.data, w.ctypes.data)
+    return rc, w
+
+
+def sha1_witness(in_elems, blocks):
+    """Sha1HashChunks(blocks) witness; in_elems: (512*blocks, 32) uint8 array of input signals."""
+    L = lib()
+    sz = L.orc_sha1_witness_size(blocks)
+    w = np.zeros((sz, 32), dtype=np.uint8)
+    a = np.ascontiguousarray(in_elems, dtype=np.uint8)
+    rc = L.orc_sha1_witness(blocks, a.ctypes.data, w.ctypes.data)
     return rc, w

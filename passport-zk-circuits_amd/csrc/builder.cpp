@@ -178,6 +178,19 @@ bool build_sha256(const pzk_params& p, Layout& L, std::string& why) {
   return true;
 }
 
+bool build_sha1(const pzk_params& p, Layout& L, std::string& why) {
+  int B = p.size_arg;
+  if (B < 1 || B > 64) { why = "Sha1HashChunks(blocks): blocks must be 1..64"; return false; }
+  Builder b(L);
+  L.n_inputs = 512ull * B;
+  L.n_outputs = 160;
+  L.inputs.push_back({"in", 0, L.n_inputs});
+  b.region(RK_ONE, 1);
+  b.sha1(0, B);
+  b.finalize();
+  return true;
+}
+
 }  // namespace
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why);
@@ -188,6 +201,7 @@ bool build_layout(const pzk_params& p, Layout& L, std::string& why) {
   switch (p.circuit) {
     case PZK_CIRCUIT_POSEIDON: ok = build_poseidon(p, L, why); break;
     case PZK_CIRCUIT_SHA256: ok = build_sha256(p, L, why); break;
+    case PZK_CIRCUIT_SHA1: ok = build_sha1(p, L, why); break;
     case PZK_CIRCUIT_REGISTER: ok = build_register(p, L, why); break;
     default: why = "unknown circuit family"; return false;
   }

@@ -49,6 +49,24 @@ struct Builder {
     return job;
   }
 
+  // Sha1HashChunks(B) (hasher/sha1/sha1.circom:7-57): own signals + H(0..4) as one RK_SHA1_OWN
+  // region, then one RK_SHA1_BLOCK per Sha1compression
+  int sha1(int in_off, int blocks, int src = 0) {
+    ShaJob j{};
+    j.in_off = in_off;
+    j.blocks = blocks;
+    j.core_off = (int)L.sha_core_words;
+    j.digest_slot = -1;
+    j.src = src;
+    j.algo = 1;
+    L.sha_core_words += blocks * SHA1_BLOCK_CORE + 8;
+    L.sha.push_back(j);
+    const int job = (int)L.sha.size() - 1;
+    region(RK_SHA1_OWN, 160 + 512ull * blocks + 5 * SHA1_CONST_SIGS, {job, blocks, in_off});
+    for (int m = 0; m < blocks; m++) region(RK_SHA1_BLOCK, SHA1_BLOCK_SIGS, {job, m});
+    return job;
+  }
+
   // PoseidonHash(n) (poseidon.circom:214-226) as one RK_POSEIDON region; returns output slot
   int poseidon(int n, const std::vector<int>& in_slots, int level, int out_slot = -1) {
     PosTask t{};

@@ -9,6 +9,7 @@
 #include "rsa_coop.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
+#include "sha1.hpp"
 #include "sha_prog.hpp"
 #include "kernels.hpp"
 
@@ -38,7 +39,8 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
   if (w >= batch || j >= n_jobs) return;
   const ShaJob& J = jobs[j];
   const uint8_t* row = J.src ? derived + 32ull * (uint64_t)w * n_derived : inputs + 32ull * (uint64_t)w * n_inputs;
-  sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
+  if (J.algo) sha1_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
+  else sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
 }
 
 // ------------------------------------------------------------------- Poseidon core
@@ -160,6 +162,42 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
       bool cp; uint64_t src = 0;
       uint64_t v = sha_own_sig(R, core, wk.start + q, cp, src);
       return cp ? el_load(in_row + 32ull * src) : el_u64(v);
+    });
+  }
+}
+
+// ------------------------------------------------------------------- emit: SHA-1 regions
+// workgroup per (witness, chunk) of a region: the block's 165 core words go to LDS (with A[-4..-1]
+// so that B..E of every round are A-history lookups), then one closed-form signal per lane.
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha1(DevLayout L, const Work* work, const uint8_t* inputs,
+                                                           const uint8_t* derived, const uint32_t* sha_core,
+                                                           uint8_t* wtns, size_t stride) {
+  __shared__ uint32_t wd[5 + 80 + 85];
+  __shared__ uint4 stage[2 * EMIT_THREADS];
+  const Work wk = work[blockIdx.y];
+  const uint32_t w = blockIdx.x;
+  const Region R = L.regions[wk.region];
+  const ShaJob job = L.sha[R.a[0]];
+  const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
+  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  if (R.kind == RK_SHA1_BLOCK) {
+    const uint32_t* bc = wc + R.a[1] * SHA1_BLOCK_CORE;
+    for (int i = threadIdx.x; i < SHA1_BLOCK_CORE; i += blockDim.x) wd[i < 85 ? i : i + 5] = bc[i];
+    if (threadIdx.x == 0) {
+      wd[89] = bc[0]; wd[88] = bc[1];
+      wd[87] = rol32(bc[2], 2); wd[86] = rol32(bc[3], 2); wd[85] = rol32(bc[4], 2);
+    }
+    __syncthreads();
+    const Sha1Blk X{wd, wd + 5, wd + 85};
+    emit_run(out, wk.count, stage, [&](uint32_t q) { return el_u64(sha1_block_sig(X, wk.start + q)); });
+  } else {  // RK_SHA1_OWN
+    const int Bn = R.a[1];
+    const uint32_t* hout = wc + Bn * SHA1_BLOCK_CORE;
+    const uint8_t* in_row = job.src ? derived + 32ull * (uint64_t)w * L.n_derived : inputs + 32ull * (uint64_t)w * L.n_inputs;
+    emit_run(out, wk.count, stage, [&](uint32_t q) {
+      bool cp;
+      const uint64_t v = sha1_own_sig(hout, Bn, wk.start + q, cp);
+      return cp ? el_load(in_row + 32ull * (R.a[2] + v)) : el_u64(v);
     });
   }
 }
@@ -431,6 +469,10 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
       else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
       break;
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
+    case E_SHA1:  // witness-major grid, as k_emit_sha
+      hipLaunchKernelGGL(k_emit_sha1, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
+                         B.stride);
+      break;
     case E_ECT: return launch_emit_ect(L, work, n_work, B, batch, st);
     default: return hipErrorInvalidValue;
   }

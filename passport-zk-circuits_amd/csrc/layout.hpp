@@ -68,6 +68,9 @@ enum RegionKind : uint32_t {
   RK_PSS_MGF = 42,    // Mgf1Sha256 own: out[DB8] | seed[256] | hashed[256 IT]
   RK_PSS_CTR = 43,    // Mgf1Sha256 num2Bits[a0] = Num2Bits(32)(a0)
   RK_PSS_XOR = 44,    // Xor2(DB8): out | in1 | in2
+  // ---- SHA-1 (hasher/sha1/*.circom; sha1.hpp)
+  RK_SHA1_OWN = 45,   // Sha1HashChunks out[160] | in[512B] | H(0..4); a0 = sha slot, a1 = blocks, a2 = input offset
+  RK_SHA1_BLOCK = 46, // Sha1compression of one block; a0 = sha slot, a1 = block
   RK_COUNT
 };
 
@@ -75,10 +78,12 @@ enum RegionKind : uint32_t {
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
 // E_ECT = ECDSA table blocks (k_emit_ect)
 // E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_COUNT };
+// E_SHA1 = SHA-1 hasher regions (k_emit_sha1)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
+    case RK_SHA1_OWN: case RK_SHA1_BLOCK: return E_SHA1;
     case RK_POSEIDON: return E_POS;
     case RK_BITS2NUM: case RK_NUM2BITS: return E_BITS;
     case RK_FLOW: return E_FLOW;
@@ -126,10 +131,15 @@ struct ShaJob {
   int32_t core_off; // u32 offset of this hasher's core inside the per-witness SHA core
   int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
   int32_t src;      // 0: message bits are input elements; 1: derived elements (RSA-PSS, pss.hpp)
+  int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp)
 };
 
 // per block core: Hin[8] W[64] A[1..64] E[1..64]; per hasher: blocks*200 + Hout[8]
 constexpr int SHA_BLOCK_CORE = 200;
+// SHA-1: per block Hin[5] W[80] A[1..80]; per hasher blocks*165 + Hout[5] (+3 pad)
+constexpr int SHA1_BLOCK_CORE = 165;
+constexpr uint32_t SHA1_BLOCK_SIGS = 198034;  // Sha1compression (sha1.hpp)
+constexpr uint32_t SHA1_CONST_SIGS = 97;      // H(x): out[32] | Num2Bits(32)
 
 // Poseidon task: one permutation PoseidonHash(n) per (witness, task) lane
 struct PosTask {

@@ -43,7 +43,7 @@ static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k
                                               "k_pss_mgf+k_sha_core+k_pss_mdash"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
                                         PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
-                                        PH_EMIT_SHA};
+                                        PH_EMIT_SHA, PH_EMIT_SHA};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket

@@ -105,6 +105,9 @@ def test_small_circuit_layouts(oracle):
         assert rc == 0 and nin == n and nw == oracle.lib().orc_poseidon_witness_size(n)
     rc, nin, nw = layout_sizes(None, native.PZK_CIRCUIT_SHA256, 6)
     assert rc == 0 and nin == 3072 and nw == oracle.lib().orc_sha256_witness_size(6)
+    for b in (1, 2, 4):
+        rc, nin, nw = layout_sizes(None, native.PZK_CIRCUIT_SHA1, b)
+        assert rc == 0 and nin == 512 * b and nw == oracle.lib().orc_sha1_witness_size(b)
 
 
 def test_unsupported_params_rejected():

@@ -271,3 +271,17 @@ def test_brainpool_oracle_verifies_and_rejects(oracle):
     r, s_ = pp["sig"]
     bad["sig"] = (r, (s_ + 1) % I.BP256.n)
     assert oracle.register_witness(prm, I.pack_register_inputs(bad, params))[0] == 16
+
+
+def test_sha1_oracle_digest(oracle):
+    """Sha1HashChunks(B) restatement (hasher/sha1/*.circom): digest bits equal hashlib.sha1, every check passes."""
+    rng = np.random.default_rng(31)
+    for ln in (0, 3, 55, 56, 119, 200):
+        msg = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        p = I.sha_pad(msg)
+        blocks = len(p) // 64
+        inp = np.zeros((512 * blocks, 32), np.uint8)
+        inp[:, 0] = I.bits_msb_first(p)
+        rc, w = oracle.sha1_witness(inp, blocks)
+        assert rc == 0
+        assert np.packbits(w[1:161, 0]).tobytes() == hashlib.sha1(msg).digest()

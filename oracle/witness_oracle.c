@@ -597,6 +597,16 @@ static void run_sha1chunks(ctx_t *c, size_t b, int B) {
     for (int k = 0; k < 32; k++) W(b + (31 - k) + 32 * i) = W(last + k + 32 * i);
 }
 
+/* ShaHashChunks(B, ALGO) hash.circom:32-68 for ALGO 160 / 256: out[ALGO] | in[512B] | Sha1/Sha256HashChunks(B) */
+static size_t sz_hashc(int algo, int B) { return algo == 160 ? 160 + 512 * (size_t)B + sz_sha1chunks(B) : sz_shahash(B); }
+static void run_hashc(ctx_t *c, size_t b, int algo, int B) {
+  if (algo != 160) { run_shahash(c, b, B); return; }
+  size_t in = b + 160, h = in + 512 * (size_t)B;
+  for (size_t q = 0; q < 512 * (size_t)B; q++) W(h + 160 + q) = W(in + q);
+  run_sha1chunks(c, h, B);
+  for (int q = 0; q < 160; q++) W(b + q) = W(h + q);
+}
+
 /* ================================================================ Poseidon */
 typedef struct { int t, nRP; fr_t *C, *M, *P, *S; } pos_params_t;
 static pos_params_t POS[18];
@@ -1112,13 +1122,47 @@ static void run_rsa(ctx_t *c, size_t b, int K, long EXP) {
   if (bad && !c->err) c->err = S_RSA_PAD;
 }
 
-/* VerifySignature(SIG 1|2) signatureVerification.circom:9-127: pubkey[K], signature[K], hashed[256] | rsa */
-static size_t sz_verifysig(int K) { return 2 * (size_t)K + 256 + sz_rsa(K, 65537); }
-static void run_verifysig(ctx_t *c, size_t b, int K) {
-  size_t rsa = b + 2 * K + 256;
+/* RsaVerifyPkcs1v15(64,K,EXP,160) rsa.circom:73-109 (SHA-1 DigestInfo):
+ * signature[K], pubkey[K], hashed[160] | hashed_chunks[2] (never assigned) | pm, bits2num[0..1], getBits, getDiv.
+ * The bits2num outputs are not constrained against EM (rsa.circom:82-88): only the first digest word is checked. */
+static size_t sz_rsa160(int K, long EXP) {
+  return 2 * (size_t)K + 160 + 2 + sz_powermod(64, K, EXP) + 2 * sz_bits2num(64) + sz_num2bits(64) + sz_bits2num(32);
+}
+static void run_rsa160(ctx_t *c, size_t b, int K, long EXP) {
+  size_t sig = b, pk = b + K, hashed = pk + K, hc = hashed + 160, pm = hc + 2, b2n = pm + sz_powermod(64, K, EXP),
+         gb = b2n + 2 * sz_bits2num(64), gd = gb + sz_num2bits(64);
+  for (int i = 0; i < K; i++) { W(pm + K + i) = W(sig + i); W(pm + 2 * K + i) = W(pk + i); }
+  run_powermod(c, pm, 64, K, EXP);
+  W(hc) = fr_zero(); W(hc + 1) = fr_zero();
+  for (int i = 0; i < 2; i++) {
+    size_t bn = b2n + (size_t)i * sz_bits2num(64);
+    for (int j = 0; j < 64; j++) W(bn + 1 + j) = W(hashed + 159 - j - i * 64);
+    run_bits2num(c, bn, 64);
+  }
+  W(gb + 64) = W(pm + 2);
+  run_num2bits(c, gb, 64);
+  int bad = 0;
+  for (int i = 0; i < 32; i++) bad |= !fr_eq(W(gb + i), W(hashed + 31 - i));
+  if (bad && !c->err) c->err = S_RSA_HASH;  /* rsa.circom:95-97 */
+  for (int i = 32; i < 64; i++) W(gd + 1 + i - 32) = W(gb + i);
+  run_bits2num(c, gd, 32);
+  if ((!fr_eq(W(gd), fr_u64(83887124ULL)) || !fr_eq(W(pm + 3), fr_u64(650212878678426138ULL)) ||
+       !fr_eq(W(pm + 4), fr_u64(18446744069417738544ULL))) && !c->err)
+    c->err = S_RSA_PREFIX;  /* rsa.circom:102-106 */
+  bad = 0;
+  for (int i = 5; i < K - 1; i++) bad |= !fr_eq(W(pm + i), fr_u64(0xFFFFFFFFFFFFFFFFULL));
+  bad |= !fr_eq(W(pm + K - 1), fr_u64(562949953421311ULL));
+  if (bad && !c->err) c->err = S_RSA_PAD;  /* rsa.circom:107-111 */
+}
+
+/* VerifySignature(SIG 1|2|3) signatureVerification.circom:9-145: pubkey[K], signature[K], hashed[HT] | rsa */
+static size_t sz_verifysig(int K, int HT) { return 2 * (size_t)K + HT + (HT == 160 ? sz_rsa160(K, 65537) : sz_rsa(K, 65537)); }
+static void run_verifysig(ctx_t *c, size_t b, int K, int HT) {
+  size_t rsa = b + 2 * K + HT;
   for (int i = 0; i < K; i++) { W(rsa + i) = W(b + K + i); W(rsa + K + i) = W(b + i); }
-  for (int i = 0; i < 256; i++) W(rsa + 2 * K + i) = W(b + 2 * K + i);
-  run_rsa(c, rsa, K, 65537);
+  for (int i = 0; i < HT; i++) W(rsa + 2 * K + i) = W(b + 2 * K + i);
+  if (HT == 160) run_rsa160(c, rsa, K, 65537);
+  else run_rsa(c, rsa, K, 65537);
 }
 
 /* ================================================= RSA-PSS (SIGNATURE_TYPE 10, 11, 12)
@@ -1294,31 +1338,37 @@ typedef struct {
   int sig, dg_hash, doc, ec_blocks, ec_shift, dg1_shift, aa, dg15_shift, dg15_blocks, aa_shift;
 } orc_params;
 
-static size_t sz_flow(int ecLen) { return 1 + 256 + 256 + (size_t)ecLen + 256 + 1024 + 776 + (256 * 3 + 8) * 6; }
-static void run_flow(ctx_t *c, size_t b, int ecLen, int dg1s, int dg15s, int ecs, int V) {
-  size_t h1 = b + 1, h15 = h1 + 256, ec = h15 + 256, ech = ec + ecLen, sa = ech + 256, v = sa + 1024, eq = v + 776;
+/* PassportVerificationFlow(ecLen, H = DG hash bits, EH = EC hash bits, ...) passportVerificationFlow.circom:6-109:
+ * flowResult | dg1Hash[H], dg15Hash[H], encapsulatedContent[ecLen], encapsulatedContentHash[EH], signedAttributes[1024]
+ * | verifyAllChecksPassed[3H+8] | IsEqual x (3H + 8) */
+static size_t sz_flow(int ecLen, int H, int EH) {
+  return 1 + 2 * (size_t)H + (size_t)ecLen + EH + 1024 + (3 * (size_t)H + 8) * 7;
+}
+static void run_flow(ctx_t *c, size_t b, int ecLen, int H, int EH, int dg1s, int dg15s, int ecs, int V) {
+  const int NC = 3 * H + 8;
+  size_t h1 = b + 1, h15 = h1 + H, ec = h15 + H, ech = ec + ecLen, sa = ech + EH, v = sa + 1024, eq = v + NC;
   fr_t Vf = fr_u64((uint64_t)V);
-  for (int i = 0; i < 256; i++) {
+  for (int i = 0; i < H; i++) {
     size_t e = eq + 6 * (size_t)i;
     W(e + 1) = W(h1 + i); W(e + 2) = W(ec + dg1s + i); run_isequal(c, e);
   }
-  for (int i = 0; i < 256; i++) {
-    size_t e = eq + 6 * (size_t)(256 + i);
+  for (int i = 0; i < H; i++) {
+    size_t e = eq + 6 * (size_t)(H + i);
     W(e + 1) = mulg(W(h15 + i), Vf); W(e + 2) = mulg(W(ec + dg15s + i), Vf); run_isequal(c, e);
   }
-  for (int i = 0; i < 256; i++) {
-    size_t e = eq + 6 * (size_t)(512 + i);
+  for (int i = 0; i < H; i++) {  /* :36-40 reads encapsulatedContentHash[i] for i < HASH_SIZE */
+    size_t e = eq + 6 * (size_t)(2 * H + i);
     W(e + 1) = W(ech + i); W(e + 2) = W(sa + ecs + i); run_isequal(c, e);
   }
   static const int prefix[8] = {0, 0, 0, 0, 1, 1, 1, 1};
   for (int i = 0; i < 8; i++) {
-    size_t e = eq + 6 * (size_t)(768 + i);
+    size_t e = eq + 6 * (size_t)(3 * H + i);
     W(e + 1) = mulg(fr_u64((uint64_t)prefix[i]), Vf); W(e + 2) = mulg(W(ec + dg15s - 24 + i), Vf);
     run_isequal(c, e);
   }
   W(v) = W(eq);
-  for (int i = 1; i < 776; i++) W(v + i) = mulg(W(v + i - 1), W(eq + 6 * (size_t)i));
-  W(b) = W(v + 775);
+  for (int i = 1; i < NC; i++) W(v + i) = mulg(W(v + i - 1), W(eq + 6 * (size_t)i));
+  W(b) = W(v + NC - 1);
 }
 
 /* ============================================ PassportVerificationBuilder */
@@ -1326,65 +1376,72 @@ static int sig_chunks(int sig) { return sig == 2 ? 64 : sig == 14 ? 48 : 32; }
 /* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
 static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
 
+/* HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:19-50): 160 for SIG 3 */
+static int sig_hash(int sig) { return sig == 3 ? 160 : 256; }
 static size_t sz_pvb(const orc_params *P) {
   int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, ec = P->sig >= 20;
-  /* own: ..., pubkeyHash, then tempModulus[5] (RSA, :184) or ecBitsX[256], ecBitsY[256] (ECDSA, :197-198) */
-  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 256 * 4 + 1 + (ec ? 512 : 5);
+  int DG = P->dg_hash, HT = sig_hash(P->sig);
+  /* own: ..., dg1Hash[DG], dg15Hash[DG], ecHash[HT], saHash[HT], pubkeyHash, then tempModulus[5] (RSA, :184) or
+   * ecBitsX[256], ecBitsY[256] (ECDSA, :197-198) */
+  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 2 * (size_t)DG + 2 * (size_t)HT + 1 + (ec ? 512 : 5);
   size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
-  return own + sz_shahash(2) + (P->aa ? sz_shahash(P->dg15_blocks) : 0) + sz_shahash(P->ec_blocks) + sz_shahash(2) +
-         sz_flow(ecLen) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K)) + sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
+  return own + sz_hashc(DG, 2) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(HT, P->ec_blocks) + sz_hashc(HT, 2) +
+         sz_flow(ecLen, DG, HT) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT)) +
+         sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, isec = P->sig >= 20;
+  int DG = P->dg_hash, HT = sig_hash(P->sig);
   size_t ec = b + 1, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
-         br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + 256, ecH = dg15H + 256, saH = ecH + 256,
-         pkHash = saH + 256, tmpMod = pkHash + 1;
+         br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + DG, ecH = dg15H + DG, saH = ecH + HT,
+         pkHash = saH + HT, tmpMod = pkHash + 1;
   size_t p = tmpMod + (isec ? 512 : 5);
-  size_t hDg1 = p; p += sz_shahash(2);
-  size_t hDg15 = 0; if (P->aa) { hDg15 = p; p += sz_shahash(P->dg15_blocks); }
-  size_t hEc = p; p += sz_shahash(P->ec_blocks);
-  size_t hSa = p; p += sz_shahash(2);
-  size_t flow = p; p += sz_flow(ecLen);
-  size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K);
+  size_t hDg1 = p; p += sz_hashc(DG, 2);
+  size_t hDg15 = 0; if (P->aa) { hDg15 = p; p += sz_hashc(DG, P->dg15_blocks); }
+  size_t hEc = p; p += sz_hashc(HT, P->ec_blocks);
+  size_t hSa = p; p += sz_hashc(HT, 2);
+  size_t flow = p; p += sz_flow(ecLen, DG, HT);
+  size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT);
   size_t saNum = p; p += sz_bits2num(252);
   size_t pkH = p; p += isec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   size_t smt = p; p += sz_smt(80);
   size_t saHH = p;
   /* hashes */
-  for (int i = 0; i < 1024; i++) W(hDg1 + 256 + i) = W(dg1 + i);
-  run_shahash(c, hDg1, 2);
-  for (int i = 0; i < 256; i++) W(dg1H + i) = W(hDg1 + i);
+  for (int i = 0; i < 1024; i++) W(hDg1 + DG + i) = W(dg1 + i);
+  run_hashc(c, hDg1, DG, 2);
+  for (int i = 0; i < DG; i++) W(dg1H + i) = W(hDg1 + i);
   if (P->aa) {
-    for (int i = 0; i < dg15Len; i++) W(hDg15 + 256 + i) = W(dg15 + i);
-    run_shahash(c, hDg15, P->dg15_blocks);
-    for (int i = 0; i < 256; i++) W(dg15H + i) = W(hDg15 + i);
+    for (int i = 0; i < dg15Len; i++) W(hDg15 + DG + i) = W(dg15 + i);
+    run_hashc(c, hDg15, DG, P->dg15_blocks);
+    for (int i = 0; i < DG; i++) W(dg15H + i) = W(hDg15 + i);
   } else {
-    for (int i = 0; i < 256; i++) W(dg15H + i) = fr_zero();
+    for (int i = 0; i < DG; i++) W(dg15H + i) = fr_zero();
   }
-  for (int i = 0; i < ecLen; i++) W(hEc + 256 + i) = W(ec + i);
-  run_shahash(c, hEc, P->ec_blocks);
-  for (int i = 0; i < 256; i++) W(ecH + i) = W(hEc + i);
-  for (int i = 0; i < 1024; i++) W(hSa + 256 + i) = W(sa + i);
-  run_shahash(c, hSa, 2);
-  for (int i = 0; i < 256; i++) W(saH + i) = W(hSa + i);
+  for (int i = 0; i < ecLen; i++) W(hEc + HT + i) = W(ec + i);
+  run_hashc(c, hEc, HT, P->ec_blocks);
+  for (int i = 0; i < HT; i++) W(ecH + i) = W(hEc + i);
+  for (int i = 0; i < 1024; i++) W(hSa + HT + i) = W(sa + i);
+  run_hashc(c, hSa, HT, 2);
+  for (int i = 0; i < HT; i++) W(saH + i) = W(hSa + i);
   /* flow */
   {
-    size_t h1 = flow + 1, h15 = h1 + 256, fec = h15 + 256, fech = fec + ecLen, fsa = fech + 256;
-    for (int i = 0; i < 256; i++) { W(h1 + i) = W(dg1H + i); W(h15 + i) = W(dg15H + i); W(fech + i) = W(ecH + i); }
+    size_t h1 = flow + 1, h15 = h1 + DG, fec = h15 + DG, fech = fec + ecLen, fsa = fech + HT;
+    for (int i = 0; i < DG; i++) { W(h1 + i) = W(dg1H + i); W(h15 + i) = W(dg15H + i); }
+    for (int i = 0; i < HT; i++) W(fech + i) = W(ecH + i);
     for (int i = 0; i < ecLen; i++) W(fec + i) = W(ec + i);
     for (int i = 0; i < 1024; i++) W(fsa + i) = W(sa + i);
-    int dg15shift = P->aa ? P->dg15_shift : 256;
-    run_flow(c, flow, ecLen, P->dg1_shift, dg15shift, P->ec_shift, P->aa);
+    int dg15shift = P->aa ? P->dg15_shift : DG;
+    run_flow(c, flow, ecLen, DG, HT, P->dg1_shift, dg15shift, P->ec_shift, P->aa);
     if (!fr_eq(W(flow), ONE()) && !c->err) c->err = S_FLOW;
   }
   /* signature */
   for (int i = 0; i < K; i++) { W(vs + K + i) = W(sig + i); W(vs + i) = W(pk + i); }
-  for (int i = 0; i < 256; i++) W(vs + 2 * K + i) = W(saH + i);
+  for (int i = 0; i < HT; i++) W(vs + 2 * K + i) = W(saH + i);
   if (isec) run_verifysig_ec(c, vs);
   else if (is_pss(P->sig)) run_verifysig_pss(c, vs, K, P->sig);
-  else run_verifysig(c, vs, K);
-  /* passportHash bits */
-  for (int i = 0; i < 252; i++) W(saNum + 1 + i) = W(saH + i);
+  else run_verifysig(c, vs, K, HT);
+  /* passportHash bits (:164-177): the hash's first 252 bits, or all HT < 252 bits shifted up by 252 - HT */
+  for (int i = 0; i < 252; i++) W(saNum + 1 + i) = HT >= 252 ? W(saH + i) : i < 252 - HT ? fr_zero() : W(saH + i - (252 - HT));
   run_bits2num(c, saNum, 252);
   if (!isec) { /* RSA pubkey hash (:182-191) */
     for (int i = 0; i < 5; i++) {
@@ -1497,7 +1554,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2 || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && P->dg_hash == 256 && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
+  return (P->sig == 1 || P->sig == 2 || P->sig == 3 || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 160) && (P->sig != 3 || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 

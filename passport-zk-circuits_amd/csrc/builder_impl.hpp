@@ -34,6 +34,7 @@ struct Builder {
     j.blocks = blocks;
     j.core_off = (int)L.sha_core_words;
     j.digest_slot = -1;
+    j.hout = j.core_off + blocks * SHA_BLOCK_CORE;
     L.sha_core_words += blocks * SHA_BLOCK_CORE + 8;
     L.sha.push_back(j);
     return (int)L.sha.size() - 1;
@@ -59,12 +60,32 @@ struct Builder {
     j.digest_slot = -1;
     j.src = src;
     j.algo = 1;
+    j.hout = j.core_off + blocks * SHA1_BLOCK_CORE;
     L.sha_core_words += blocks * SHA1_BLOCK_CORE + 8;
     L.sha.push_back(j);
     const int job = (int)L.sha.size() - 1;
-    region(RK_SHA1_OWN, 160 + 512ull * blocks + 5 * SHA1_CONST_SIGS, {job, blocks, in_off});
-    for (int m = 0; m < blocks; m++) region(RK_SHA1_BLOCK, SHA1_BLOCK_SIGS, {job, m});
+    sha1_regions(job, in_off, blocks, false);
     return job;
+  }
+  // Sha1HashChunks regions of job (optionally inside ShaHashChunks(B,160): wrapper out[160] | in[512B] first)
+  void sha1_regions(int job, int in_off, int blocks, bool wrapper) {
+    region(RK_SHA1_OWN, (wrapper ? 160 + 512ull * blocks : 0) + 160 + 512ull * blocks + 5 * SHA1_CONST_SIGS,
+           {job, blocks, in_off, wrapper ? 1 : 0});
+    for (int m = 0; m < blocks; m++) region(RK_SHA1_BLOCK, SHA1_BLOCK_SIGS, {job, m});
+  }
+  // a SHA job of either algorithm whose regions are placed later (sha_regions)
+  int hash_job(int algo, int in_off, int blocks) {
+    if (algo != 160) return sha_job(in_off, blocks);
+    ShaJob j{};
+    j.in_off = in_off;
+    j.blocks = blocks;
+    j.core_off = (int)L.sha_core_words;
+    j.digest_slot = -1;
+    j.algo = 1;
+    j.hout = j.core_off + blocks * SHA1_BLOCK_CORE;
+    L.sha_core_words += blocks * SHA1_BLOCK_CORE + 8;
+    L.sha.push_back(j);
+    return (int)L.sha.size() - 1;
   }
 
   // PoseidonHash(n) (poseidon.circom:214-226) as one RK_POSEIDON region; returns output slot

@@ -40,13 +40,18 @@ uint32_t modmul_size(int K) {
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   // RSA-PSS with SHA-256: 10-12 RSA-2048 (e = 3 for 10, salt 64 for 12), 14 RSA-3072 (signatureVerification.circom:46-75)
   const bool pss = (p.signature_type >= 10 && p.signature_type <= 12) || p.signature_type == 14;
-  if (p.signature_type != 1 && p.signature_type != 2 && !pss && p.signature_type != 20 && p.signature_type != 21) {
+  if (p.signature_type != 1 && p.signature_type != 2 && p.signature_type != 3 && !pss && p.signature_type != 20 &&
+      p.signature_type != 21) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1, 2, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1-3, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
     return false;
   }
   const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
-  if (p.dg_hash_type != 256) { why = "DG_HASH_TYPE must be 256 (SHA-256 chunks)"; return false; }
+  // DG_HASH_TYPE 256 or 160; SIGNATURE_TYPE 3 hashes the EC / SA with SHA-1 (HASH_TYPE 160), which the flow's
+  // `encapsulatedContentHash[i], i < HASH_SIZE` loop (passportVerificationFlow.circom:36-40) allows only with DG 160
+  if (p.dg_hash_type != 256 && p.dg_hash_type != 160) { why = "DG_HASH_TYPE must be 256 or 160"; return false; }
+  if (p.signature_type == 3 && p.dg_hash_type != 160) { why = "SIGNATURE_TYPE 3 needs DG_HASH_TYPE 160"; return false; }
+  const int DG = p.dg_hash_type, HT = p.signature_type == 3 ? 160 : 256;
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
   // AA_SIGNATURE_ALGO: 0 none, 1..19 RSA-1024 key (identity.circom:25-49), >= 20 EC key (:51-84); the raw value
   // also scales the DG15 IsEqual inputs of the flow (passportVerificationFlow.circom:45-46,73-74)
@@ -58,7 +63,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
-  const int dg15shift = aa ? p.dg15_shift : 256;
+  const int dg15shift = aa ? p.dg15_shift : DG;
   if (p.dg1_shift < 0 || p.dg1_shift + 256 > ecLen || dg15shift < 24 || dg15shift + 256 > ecLen ||
       p.ec_shift < 0 || p.ec_shift + 256 > 1024 || (aa && p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len)) {
     why = "shift parameters address bits outside the inputs";
@@ -134,20 +139,21 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   b.region(RK_INCOPY, 1, {IN_ROOT});
   // SHA jobs are created when the hashers are created; their digests are referenced earlier,
   // so reserve the job ids first (creation order dg1, dg15, ec, sa).
-  const int J_DG1 = b.sha_job(IN_DG1, 2);
-  const int J_DG15 = aa ? b.sha_job(IN_DG15, d15B) : -1;
-  const int J_EC = b.sha_job(IN_EC, ecB);
-  const int J_SA = b.sha_job(IN_SA, 2);
+  const int J_DG1 = b.hash_job(DG, IN_DG1, 2);
+  const int J_DG15 = aa ? b.hash_job(DG, IN_DG15, d15B) : -1;
+  const int J_EC = b.hash_job(HT, IN_EC, ecB);
+  const int J_SA = b.hash_job(HT, IN_SA, 2);
   L.reg.j_dg1 = J_DG1; L.reg.j_dg15 = J_DG15; L.reg.j_ec = J_EC; L.reg.j_sa = J_SA;
-  b.region(RK_DIGEST, 256, {J_DG1});
-  if (aa) b.region(RK_DIGEST, 256, {J_DG15});
-  else b.region(RK_VALUE, 256, {-2});  // dg15Hash <== 0 (zeros)
-  b.region(RK_DIGEST, 256, {J_EC});
-  b.region(RK_DIGEST, 256, {J_SA});
+  b.region(RK_DIGEST, DG, {J_DG1});
+  if (aa) b.region(RK_DIGEST, DG, {J_DG15});
+  else b.region(RK_VALUE, DG, {-2});  // dg15Hash <== 0 (zeros)
+  b.region(RK_DIGEST, HT, {J_EC});
+  b.region(RK_DIGEST, HT, {J_SA});
   const uint32_t r_pkhash = b.region(RK_VALUE, 1, {-1});
   if (ecdsa) b.region(RK_EC_PKBITS, 512, {IN_PK});  // ecBitsX[256], ecBitsY[256]
   else b.region(RK_TEMPMOD, 5, {IN_PK});
   auto sha_blocks = [&](int job, int in_off, int blocks) {
+    if (L.sha[job].algo) { b.sha1_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 160)
     uint64_t own = 256 + 512ull * blocks + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
     b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1});
     for (int m = 0; m < blocks; m++) b.region(RK_SHA_BLOCK, 150762, {job, m});
@@ -156,8 +162,8 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   if (aa) sha_blocks(J_DG15, IN_DG15, d15B);
   sha_blocks(J_EC, IN_EC, ecB);
   sha_blocks(J_SA, IN_SA, 2);
-  // PassportVerificationFlow(ecLen, 256, 256, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA)
-  b.region(RK_FLOW, 1 + 256 + 256 + ecLen + 256 + 1024 + 776 + 776 * SZ_ISEQUAL,
+  // PassportVerificationFlow(ecLen, DG, HT, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA): 3 DG + 8 IsEqual
+  b.region(RK_FLOW, 1 + 2 * DG + ecLen + HT + 1024 + (3 * DG + 8) * (1 + SZ_ISEQUAL),
            {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, p.aa_signature_algo});
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
@@ -183,8 +189,19 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
     // VerifySignature(SIG): pubkey[K], signature[K], hashed[256] | RsaVerifyPkcs1v15 or VerifyRsaPssSig
     b.region(RK_INCOPY, K, {IN_PK});
     b.region(RK_INCOPY, K, {IN_SIG});
-    b.region(RK_DIGEST, 256, {J_SA});
-    if (!pss) {
+    b.region(RK_DIGEST, HT, {J_SA});
+    if (HT == 160) {
+      //   RsaVerifyPkcs1v15(64,K,65537,160) (rsa.circom:73-109): signature, pubkey, hashed[160] | hashed_chunks[2]
+      //   (never assigned) | pm, bits2num[0..1], getBits = Num2Bits(64)(EM limb 2), getDiv = Bits2Num(32)(its top bits)
+      b.region(RK_INCOPY, K, {IN_SIG});
+      b.region(RK_INCOPY, K, {IN_PK});
+      b.region(RK_DIGEST, 160, {J_SA});
+      b.region(RK_VALUE, 2, {-2});
+      if (!power_mod()) return false;
+      for (int i = 0; i < 2; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, 159 - 64 * i, -1, J_SA});
+      b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 2});
+      b.region(RK_BITS2NUM, sz_bits2num(32), {32, 2, 32, 1, 2});
+    } else if (!pss) {
       //   RsaVerifyPkcs1v15(64,K,65537,256): signature, pubkey, hashed | hashed_chunks[4] | pm, bits2num[3..0], num2bits_6
       b.region(RK_INCOPY, K, {IN_SIG});
       b.region(RK_INCOPY, K, {IN_PK});
@@ -219,8 +236,8 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
       L.n_derived = 512ull * IT + 1024;
     }
   }
-  // signedAttributesNum = Bits2Num(252)(saHash[0..251])
-  b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, 0, 1, J_SA});
+  // signedAttributesNum = Bits2Num(252)(saHash[0..251]), or of 92 zeros | saHash[0..159] for SHA-1
+  b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, HT == 160 ? -92 : 0, 1, J_SA});
   int S_PKH;
   if (ecdsa) {
     // num2bitsX[i], num2bitsY[i] (Num2Bits(64)), xToNum, yToNum (Bits2Num(248)), PoseidonHash(2)

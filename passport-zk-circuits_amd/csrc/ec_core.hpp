@@ -564,7 +564,7 @@ __global__ void __launch_bounds__(64) k_ec_scalars(DevLayout L, const uint8_t* i
   if (bad) set_status(st, ST_INPUT_RANGE);
   {  // hashedChunked[j] (ecdsa.circom:30-38): 64-bit big-endian digest words, least significant first
     const ShaJob job = L.sha[G.j_sa];
-    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
+    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.hout;
     for (int j = 0; j < 4; j++) h[j] = ((uint64_t)H[2 * (3 - j)] << 32) | H[2 * (3 - j) + 1];
   }
   // sinv = s^-1 (BigModInv, bigInt.circom:344-368), u1 = sinv h, u2 = sinv r (mod n)

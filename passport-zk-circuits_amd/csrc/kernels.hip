@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha1(DevLayout L, const W
     const uint8_t* in_row = job.src ? derived + 32ull * (uint64_t)w * L.n_derived : inputs + 32ull * (uint64_t)w * L.n_inputs;
     emit_run(out, wk.count, stage, [&](uint32_t q) {
       bool cp;
-      const uint64_t v = sha1_own_sig(hout, Bn, wk.start + q, cp);
+      const uint64_t v = sha1_own_sig(hout, Bn, R.a[3] != 0, wk.start + q, cp);
       return cp ? el_load(in_row + 32ull * (R.a[2] + v)) : el_u64(v);
     });
   }

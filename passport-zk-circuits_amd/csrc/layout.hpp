@@ -132,6 +132,7 @@ struct ShaJob {
   int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
   int32_t src;      // 0: message bits are input elements; 1: derived elements (RSA-PSS, pss.hpp)
   int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp)
+  int32_t hout;     // u32 offset of the digest words (Hout[8] / Hout[5]) inside the per-witness SHA core
 };
 
 // per block core: Hin[8] W[64] A[1..64] E[1..64]; per hasher: blocks*200 + Hout[8]

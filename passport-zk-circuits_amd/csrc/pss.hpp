@@ -36,7 +36,7 @@ struct PssView {
   __device__ __forceinline__ uint32_t em_byte(int k) const { return (uint32_t)(em[k >> 3] >> (8 * (k & 7))) & 0xFFu; }
   __device__ __forceinline__ uint32_t dig(int job, int i) const {  // digest bit i (MSB first) of a SHA job
     const ShaJob& J = jobs[job];
-    const uint32_t* H = sha + J.core_off + J.blocks * SHA_BLOCK_CORE;
+    const uint32_t* H = sha + J.hout;
     return (H[i >> 5] >> (31 - (i & 31))) & 1u;
   }
   __device__ __forceinline__ uint32_t hash_bit(int i) const { return em_bit(emb() - 264 + i); }     // hash (:86-89)

@@ -99,8 +99,10 @@ __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs,
   // signedAttributesNum = Bits2Num(252)(saHash[0..251]) (passportVerificationBuilder.circom:165-172)
   if (lane == 0) {
     const ShaJob job = L.sha[R.j_sa];
-    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.core_off + job.blocks * SHA_BLOCK_CORE;
-    fr sn = bits_to_fr(252, [&](int k) { return (H[k >> 5] >> (31 - (k & 31))) & 1u; });
+    const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.hout;
+    // the hash's first 252 bits, or a 160-bit SHA-1 hash shifted up by 92 (passportVerificationBuilder.circom:164-177)
+    const int sh = job.algo ? 92 : 0;
+    fr sn = bits_to_fr(252, [&](int k) { return k < sh ? 0u : (H[(k - sh) >> 5] >> (31 - ((k - sh) & 31))) & 1u; });
     vs.at(R.v_sanum, w) = fr_to_mont(sn);
   }
   if (__ballot(bad) && lane == 0) set_status(status ? status + w : nullptr, ST_INPUT_RANGE);
@@ -386,7 +388,7 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
   const uint64_t* core = rsa_core + (size_t)w * L.rsa_core_words;
   const uint64_t* em = core + (size_t)(L.reg.n_modmul - 1) * MM_CORE_WORDS(K) + 3 * K + 1;
   const ShaJob& J = L.sha[L.reg.j_sa];
-  const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + J.core_off + J.blocks * SHA_BLOCK_CORE;
+  const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + J.hout;
   bool hash_bad = false;
   for (int i = 0; i < 4; i++) {  // hashed_chunks[i] = digest bits [64(3-i), 64(4-i)) as a number
     const int wd = 3 - i;
@@ -406,6 +408,16 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
   }
   if (L.reg.pss_s8) {
     pss_check(pss_view(L, rsa_core, sha_core, w), status + w);
+  } else if (J.algo) {
+    // RsaVerifyPkcs1v15(64,K,65537,160) (rsa.circom:73-109): EM limb 2 = 0x05000414 | first digest word,
+    // limbs 3, 4 = DigestInfo, then 0xFF.. padding and the 00 01 top limb; digest words 1-4 are not constrained
+    const uint64_t em2 = em[2];
+    if ((uint32_t)em2 != H[0]) lane_status(status + w, ST_RSA_HASH);
+    if ((em2 >> 32) != 83887124ull || em[3] != 650212878678426138ull || em[4] != 18446744069417738544ull)
+      lane_status(status + w, ST_RSA_PREFIX);
+    bool pb = em[K - 1] != 562949953421311ull;
+    for (int i = 5; i < K - 1; i++) pb |= em[i] != ~0ull;
+    if (pb) lane_status(status + w, ST_RSA_PAD);
   } else {
     if (hash_bad) lane_status(status + w, ST_RSA_HASH);
     if (em[4] != RSA_EM4 || em[5] != RSA_EM5) lane_status(status + w, ST_RSA_PREFIX);

@@ -58,7 +58,7 @@ __device__ __forceinline__ void copy_el(uint8_t* dst, const uint8_t* src) {
 }
 __device__ __forceinline__ const uint32_t* sha_hout(const DevLayout& L, const Bufs& B, uint32_t w, int job) {
   const ShaJob& J = L.sha[job];
-  return B.sha_core + (size_t)w * L.sha_core_words + J.core_off + J.blocks * SHA_BLOCK_CORE;
+  return B.sha_core + (size_t)w * L.sha_core_words + J.hout;
 }
 __device__ __forceinline__ uint32_t digest_bit(const uint32_t* H, int i) { return (H[i >> 5] >> (31 - (i & 31))) & 1u; }
 
@@ -241,9 +241,15 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
   __syncthreads();
   const bool b2n = R.kind == RK_BITS2NUM;
   const uint32_t* H = (b2n && R.a[1] == 1) ? sha_hout(L, B, w, R.a[4]) : nullptr;
+  // bit sources: 0 input elements, 1 digest bits of SHA job a4 (index < 0: a zero, the SHA-1 passportHash
+  // padding), 2 bits of EM limb a4 (RSA core)
+  const uint64_t emw = (b2n && R.a[1] == 2)
+      ? B.rsa_core[(size_t)w * L.rsa_core_words + (size_t)(L.reg.n_modmul - 1) * MM_CORE_WORDS(L.reg.K) + 3 * L.reg.K + 1 + R.a[4]]
+      : 0ull;
   auto src_bit = [&](int j) -> uint32_t {
     int idx = R.a[2] + R.a[3] * j;
-    if (R.a[1] == 1) return digest_bit(H, idx);
+    if (R.a[1] == 1) return idx < 0 ? 0u : digest_bit(H, idx);
+    if (R.a[1] == 2) return (uint32_t)(emw >> idx) & 1u;
     return *(row + 32ull * idx) & 1u;
   };
   if (b2n) {
@@ -283,7 +289,8 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
       if (s == 0) return el_w(V);
       if (s <= (uint32_t)Lb) {
         int idx = R.a[2] + R.a[3] * (int)(s - 1);
-        return R.a[1] == 1 ? el_u64(digest_bit(H, idx)) : el_load(row + 32ull * idx);
+        return R.a[1] == 1 ? el_u64(idx < 0 ? 0u : digest_bit(H, idx)) : R.a[1] == 2 ? el_u64((emw >> idx) & 1u)
+                                                                                  : el_load(row + 32ull * idx);
       }
       return el_w(w_mask(V, (int)(s - Lb)));
     }
@@ -303,6 +310,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
   const int jd1 = R.a[0], jd15 = R.a[1], jec = R.a[2], jsa = R.a[3], in_ec = R.a[4], in_sa = R.a[5];
   const int d1s = R.a[6], d15s = R.a[7], ecs = R.a[8], V = R.a[9];
   const int ecLen = 512 * L.sha[jec].blocks;
+  const int H = L.sha[jd1].algo ? 160 : 256, EH = L.sha[jec].algo ? 160 : 256, NC = 3 * H + 8;
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   const uint32_t* H1 = sha_hout(L, B, w, jd1);
   const uint32_t* H15 = jd15 >= 0 ? sha_hout(L, B, w, jd15) : nullptr;
@@ -310,28 +318,28 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
   auto ebit = [&](int i) -> uint32_t { return *(row + 32ull * (in_ec + i)) & 1u; };
   auto sbit = [&](int i) -> uint32_t { return *(row + 32ull * (in_sa + i)) & 1u; };
   auto pair = [&](int k, uint32_t& a, uint32_t& b) {  // IsEqual k: in[0], in[1]
-    int g = k >> 8, i = k & 255;
+    const int g = k < 3 * H ? k / H : 3, i = k - g * H;
     if (g == 0) { a = digest_bit(H1, i); b = ebit(d1s + i); }
     else if (g == 1) { a = H15 ? digest_bit(H15, i) * V : 0; b = ebit(d15s + i) * V; }
     else if (g == 2) { a = digest_bit(HE, i); b = sbit(ecs + i); }
     else { a = (i >= 4 ? 1u : 0u) * V; b = ebit(d15s - 24 + i) * V; }  // 0x0F prefix, MSB first
   };
-  for (int k = threadIdx.x; k < 776; k += blockDim.x) { uint32_t a, b; pair(k, a, b); eq[k] = a == b; }
+  for (int k = threadIdx.x; k < NC; k += blockDim.x) { uint32_t a, b; pair(k, a, b); eq[k] = a == b; }
   if (threadIdx.x == 0) invV = V > 1 ? fr_from_mont(fr_inv(fr_to_mont(fr_u64((uint64_t)V)))) : fr_u64(1);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint8_t c = 1;
-    for (int k = 0; k < 776; k++) { c &= eq[k]; chain[k] = c; }
+    for (int k = 0; k < NC; k++) { c &= eq[k]; chain[k] = c; }
     if (!c && B.status) lane_status(B.status + w, ST_FLOW);
   }
   __syncthreads();
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
-  const uint32_t o_d1 = 1, o_d15 = 257, o_ec = 513, o_eh = o_ec + ecLen, o_sa = o_eh + 256, o_v = o_sa + 1024,
-                 o_eq = o_v + 776;
+  const uint32_t o_d1 = 1, o_d15 = 1 + H, o_ec = 1 + 2 * H, o_eh = o_ec + ecLen, o_sa = o_eh + EH, o_v = o_sa + 1024,
+                 o_eq = o_v + NC;
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     uint32_t s = wk.start + q;
-    if (s == 0) return el_u64(chain[775]);
+    if (s == 0) return el_u64(chain[NC - 1]);
     if (s < o_d15) return el_u64(digest_bit(H1, s - o_d1));
     if (s < o_ec) return el_u64(H15 ? digest_bit(H15, s - o_d15) : 0);
     if (s < o_eh) return el_load(row + 32ull * (in_ec + s - o_ec));

@@ -553,6 +553,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     }
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
+    if ((rc = emit(E_SHA1, s_sha))) return rc;  // SHA-1 hashers (SIGNATURE_TYPE 3, DG_HASH_TYPE 160)
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
@@ -649,7 +650,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);
     }
     if (phase == PH_SHA_CORE)
-      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * SHA_BLOCK_CORE + 8);
+      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
     if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;

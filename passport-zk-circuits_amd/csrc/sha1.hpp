@@ -202,8 +202,14 @@ __device__ __forceinline__ uint64_t sha1_block_sig(const Sha1Blk& X, uint32_t s)
 }
 
 // Sha1HashChunks(B) own signals + H(0..4): out[160] (MSB-first digest) | in[512B] (copies) | 5 x K-style constants
-__device__ __forceinline__ uint64_t sha1_own_sig(const uint32_t* hout, int B, uint32_t s, bool& is_copy) {
+__device__ __forceinline__ uint64_t sha1_own_sig(const uint32_t* hout, int B, bool wrapper, uint32_t s, bool& is_copy) {
   is_copy = false;
+  if (wrapper) {  // ShaHashChunks(B, 160) (hash.circom:32-68): out[160] | in[512B]
+    if (s < 160) return s1_mbit(hout[s >> 5], s & 31);
+    s -= 160;
+    if (s < 512u * B) { is_copy = true; return s; }
+    s -= 512u * B;
+  }
   if (s < 160) return s1_mbit(hout[s >> 5], s & 31);
   s -= 160;
   if (s < 512u * B) { is_copy = true; return s; }

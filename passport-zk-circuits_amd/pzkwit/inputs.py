@@ -92,10 +92,20 @@ class RsaKey:
 _DIGESTINFO_SHA256 = bytes.fromhex("3031300d060960864801650304020105000420")
 
 
+_DIGESTINFO_SHA1 = bytes.fromhex("3021300906052b0e03021a05000414")
+
+
+def pkcs1v15_sha1_sign(key: RsaKey, msg: bytes) -> int:
+    """RSASSA-PKCS1-v1_5 with SHA-1 (SIGNATURE_TYPE 3, rsa.circom:73-109)."""
+    return _pkcs1v15_sign(key, _DIGESTINFO_SHA1 + hashlib.sha1(msg).digest())
+
+
 def pkcs1v15_sha256_sign(key: RsaKey, msg: bytes) -> int:
-    h = hashlib.sha256(msg).digest()
+    return _pkcs1v15_sign(key, _DIGESTINFO_SHA256 + hashlib.sha256(msg).digest())
+
+
+def _pkcs1v15_sign(key: RsaKey, t: bytes) -> int:
     k = key.bits // 8
-    t = _DIGESTINFO_SHA256 + h
     em = b"\x00\x01" + b"\xff" * (k - len(t) - 3) + b"\x00" + t
     return key.sign_raw(int.from_bytes(em, "big"))
 
@@ -329,24 +339,29 @@ class PassportGen:
         dg15 = _dg15_rsa1024(rng)
         ec_len = 219 + rng.below(pr["ec_blocks"] * 64 - 9 - 219 + 1)
         ec = bytearray(rng.bytes(ec_len))
-        h1, h15 = hashlib.sha256(dg1).digest(), hashlib.sha256(dg15).digest()
+        # DG hashes: DG_HASH_TYPE; EC / SA hashes: SHA-1 for SIGNATURE_TYPE 3 (passportVerificationBuilder.circom:19-50)
+        dgh = hashlib.sha1 if pr["dg_hash"] == 160 else hashlib.sha256
+        sah = hashlib.sha1 if pr["sig"] == 3 else hashlib.sha256
+        h1, h15 = dgh(dg1).digest(), dgh(dg15).digest()
         d1 = pr["dg1_shift"] // 8
         ec[d1 - 7:d1] = bytes.fromhex("30250201010420")
-        ec[d1:d1 + 32] = h1
+        ec[d1:d1 + len(h1)] = h1
         d15 = pr["dg15_shift"] // 8
         ec[d15 - 7:d15] = bytes.fromhex("302502010f0420")
-        ec[d15:d15 + 32] = h15
+        ec[d15:d15 + len(h15)] = h15
         ec = bytes(ec)
         sa_shift = pr["ec_shift"] // 8
         sa_len = sa_shift + 32 + rng.below(119 - (sa_shift + 32) + 1)
         sa = bytearray(rng.bytes(sa_len))
         sa[sa_shift - 2:sa_shift] = b"\x04\x20"
-        sa[sa_shift:sa_shift + 32] = hashlib.sha256(ec).digest()
+        sa[sa_shift:sa_shift + 32] = (sah(ec).digest() + bytes(32))[:32]
         sa = bytes(sa)
         if isinstance(key, EcKey):
             sig = key.sign(sa, rng)
         elif 10 <= pr["sig"] <= 12 or pr["sig"] == 14:
             sig = pss_sha256_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])))
+        elif pr["sig"] == 3:
+            sig = pkcs1v15_sha1_sign(key, sa)
         else:
             sig = pkcs1v15_sha256_sign(key, sa)
         sk = int.from_bytes(hashlib.sha256(ec).digest()[:31], "big")  # getFakeIdenData :630

@@ -171,3 +171,19 @@ def test_register_rsa_outside_barrett_domain_matches_oracle(oracle, gen):
         assert (rc == 0) == (b == 0) and (st[b] == 0) == (b == 0), (b, rc, st[b])
         rep = mismatch_report(ref, wit[b], regions)
         assert not rep, "row %d: %s" % (b, rep)
+
+
+@pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160, aa=0)],
+                         ids=["sig3-dg160", "sig1-dg160-aa0"])
+def test_register_sha1_instances_match_oracle(oracle, params):
+    """SHA-1 hashers inside RegisterIdentityBuilder (ShaHashChunks(B, 160) around Sha1HashChunks) for the DG
+    hashes and, with SIGNATURE_TYPE 3, the EC / SA hashes and the PKCS#1 v1.5 SHA-1 check; a bad signature
+    carries the rsa.circom hash-check code."""
+    from test_gpu_ecdsa import _run
+    g = I.PassportGen(seed=19, n_keys=2, params=params, workers=1)
+    pps = [g.passport_at(0), g.passport_at(1, smt_depth=4), dict(g.passport_at(2))]
+    pps[2]["sig"] = pps[2]["sig"] + 1
+    rows = np.stack([I.pack_register_inputs(pp, params) for pp in pps])
+    _, st, codes = _run(oracle, params, rows, expect_ok=False)
+    assert codes == [0, 0, 8]
+    assert list(st) == [0, 0, 8]

@@ -64,7 +64,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
 WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
-SIG_SEED = {1: 3, 2: 4, 10: 6, 11: 7, 12: 8, 14: 10, 20: 5, 21: 9}
+SIG_SEED = {1: 3, 2: 4, 3: 11, 10: 6, 11: 7, 12: 8, 14: 10, 20: 5, 21: 9}
 
 
 def _cpu_work(args):
@@ -73,7 +73,7 @@ def _cpu_work(args):
     import pyoracle
     from pzkwit import inputs as I
     if kind.startswith("register"):
-        prm = pyoracle.register_params(**dict(I.CANONICAL, sig=int(kind.split(":")[1])))
+        prm = pyoracle.register_params(**I.instance_params(int(kind.split(":")[1])))
         nin, nw = pyoracle.register_sizes(prm)
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
@@ -129,7 +129,7 @@ def main():
     if args.workload.startswith("register"):
         sig = args.sig or WL_SIG[args.workload]
         batch = args.batch or 4096
-        inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, dict(I.CANONICAL, sig=sig))
+        inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.instance_params(sig))
         t0 = time.time()
         host_in = make_register_inputs(batch, rank * batch, seed=SIG_SEED[sig], sig=sig)
         log("inputs: %d passports generated in %.1fs" % (batch, time.time() - t0))
@@ -145,7 +145,8 @@ def main():
             scratch_pw = 10 << 20  # value tables (~8.4 MB) + EC core
         if sig not in (1, 20, 21):
             metric = "registerIdentityBuilder witnesses/sec, batch=4096 (SIGNATURE_TYPE %d)" % sig
-            workload = "RegisterIdentityBuilder(%d,256,3,4,600,248,1,1496,3,256) synthetic passports" % sig
+            workload = "RegisterIdentityBuilder(%d,%d,3,4,600,248,1,1496,3,256) synthetic passports" % (
+                sig, I.instance_params(sig)["dg_hash"])
         if sig == 11:
             metric = "registerIdentityBuilder RSA-PSS witnesses/sec, batch=4096 (SIGNATURE_TYPE 11)"
             workload = "RegisterIdentityBuilder(11,256,3,4,600,248,1,1496,3,256) synthetic RSA-2048 PSS passports"

@@ -239,6 +239,11 @@ def sig_limbs(v, sig):
 CANONICAL = dict(sig=1, dg_hash=256, doc=3, ec_blocks=4, ec_shift=600, dg1_shift=248, aa=1,
                  dg15_shift=1496, dg15_blocks=3, aa_shift=256)  # hardhat.config.ts:30
 
+
+def instance_params(sig):
+    """The canonical instance with SIGNATURE_TYPE sig (SIG 3 hashes with SHA-1 and needs DG_HASH_TYPE 160)."""
+    return dict(CANONICAL, sig=sig, dg_hash=160 if sig == 3 else 256)
+
 _MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789<"
 _DG15_PREFIX = bytes.fromhex("6f81a230819f300d06092a864886f70d010101050003818d00308189028181")
 
@@ -299,7 +304,7 @@ class PassportGen:
     def shared(cls, seed=3, n_keys=64, sig=1):
         key = (seed, n_keys, sig)
         if key not in cls._shared:
-            cls._shared[key] = cls(seed, n_keys, params=dict(CANONICAL, sig=sig))
+            cls._shared[key] = cls(seed, n_keys, params=instance_params(sig))
         return cls._shared[key]
 
     @property

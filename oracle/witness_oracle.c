@@ -1156,13 +1156,13 @@ static void run_rsa160(ctx_t *c, size_t b, int K, long EXP) {
 }
 
 /* VerifySignature(SIG 1|2|3) signatureVerification.circom:9-145: pubkey[K], signature[K], hashed[HT] | rsa */
-static size_t sz_verifysig(int K, int HT) { return 2 * (size_t)K + HT + (HT == 160 ? sz_rsa160(K, 65537) : sz_rsa(K, 65537)); }
-static void run_verifysig(ctx_t *c, size_t b, int K, int HT) {
+static size_t sz_verifysig(int K, int HT, long EXP) { return 2 * (size_t)K + HT + (HT == 160 ? sz_rsa160(K, EXP) : sz_rsa(K, EXP)); }
+static void run_verifysig(ctx_t *c, size_t b, int K, int HT, long EXP) {
   size_t rsa = b + 2 * K + HT;
   for (int i = 0; i < K; i++) { W(rsa + i) = W(b + K + i); W(rsa + K + i) = W(b + i); }
   for (int i = 0; i < HT; i++) W(rsa + 2 * K + i) = W(b + 2 * K + i);
-  if (HT == 160) run_rsa160(c, rsa, K, 65537);
-  else run_rsa(c, rsa, K, 65537);
+  if (HT == 160) run_rsa160(c, rsa, K, EXP);
+  else run_rsa(c, rsa, K, EXP);
 }
 
 /* ================================================= RSA-PSS (SIGNATURE_TYPE 10, 11, 12)
@@ -1171,7 +1171,7 @@ static void run_verifysig(ctx_t *c, size_t b, int K, int HT) {
  * (signatureVerification.circom:46-62). EM = PowerMod.out, 8K bytes; DB = EM_LEN - HASH_LEN - 1 bytes. */
 static int is_pss(int sig) { return (sig >= 10 && sig <= 12) || sig == 14; }
 static int pss_salt(int sig) { return sig == 12 ? 64 : 32; }
-static long sig_exp(int sig) { return sig == 10 ? 3 : 65537; }
+static long sig_exp(int sig) { return sig == 10 ? 3 : sig == 4 ? 37187 : 65537; }
 
 /* Mgf1Sha256(32, DBL): out[8 DBL] | seed[256] | hashed[256 IT] | (ShaHashChunks(1,256), Num2Bits(32)) x IT */
 static int mgf_iters(int DBL) { return DBL / 32 + 1; }
@@ -1372,12 +1372,12 @@ static void run_flow(ctx_t *c, size_t b, int ecLen, int H, int EH, int dg1s, int
 }
 
 /* ============================================ PassportVerificationBuilder */
-static int sig_chunks(int sig) { return sig == 2 ? 64 : sig == 14 ? 48 : 32; }
+static int sig_chunks(int sig) { return sig == 2 ? 64 : (sig == 14 || sig == 4) ? 48 : 32; }
 /* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
 static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
 
 /* HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:19-50): 160 for SIG 3 */
-static int sig_hash(int sig) { return sig == 3 ? 160 : 256; }
+static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : 256; }
 static size_t sz_pvb(const orc_params *P) {
   int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, ec = P->sig >= 20;
   int DG = P->dg_hash, HT = sig_hash(P->sig);
@@ -1386,7 +1386,7 @@ static size_t sz_pvb(const orc_params *P) {
   size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 2 * (size_t)DG + 2 * (size_t)HT + 1 + (ec ? 512 : 5);
   size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   return own + sz_hashc(DG, 2) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(HT, P->ec_blocks) + sz_hashc(HT, 2) +
-         sz_flow(ecLen, DG, HT) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT)) +
+         sz_flow(ecLen, DG, HT) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig))) +
          sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
@@ -1401,7 +1401,7 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   size_t hEc = p; p += sz_hashc(HT, P->ec_blocks);
   size_t hSa = p; p += sz_hashc(HT, 2);
   size_t flow = p; p += sz_flow(ecLen, DG, HT);
-  size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT);
+  size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig));
   size_t saNum = p; p += sz_bits2num(252);
   size_t pkH = p; p += isec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
   size_t smt = p; p += sz_smt(80);
@@ -1439,7 +1439,7 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   for (int i = 0; i < HT; i++) W(vs + 2 * K + i) = W(saH + i);
   if (isec) run_verifysig_ec(c, vs);
   else if (is_pss(P->sig)) run_verifysig_pss(c, vs, K, P->sig);
-  else run_verifysig(c, vs, K, HT);
+  else run_verifysig(c, vs, K, HT, sig_exp(P->sig));
   /* passportHash bits (:164-177): the hash's first 252 bits, or all HT < 252 bits shifted up by 252 - HT */
   for (int i = 0; i < 252; i++) W(saNum + 1 + i) = HT >= 252 ? W(saH + i) : i < 252 - HT ? fr_zero() : W(saH + i - (252 - HT));
   run_bits2num(c, saNum, 252);
@@ -1554,7 +1554,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return (P->sig == 1 || P->sig == 2 || P->sig == 3 || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 160) && (P->sig != 3 || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
+  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 160) && ((P->sig != 3 && P->sig != 4) || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 

@@ -40,18 +40,20 @@ uint32_t modmul_size(int K) {
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   // RSA-PSS with SHA-256: 10-12 RSA-2048 (e = 3 for 10, salt 64 for 12), 14 RSA-3072 (signatureVerification.circom:46-75)
   const bool pss = (p.signature_type >= 10 && p.signature_type <= 12) || p.signature_type == 14;
-  if (p.signature_type != 1 && p.signature_type != 2 && p.signature_type != 3 && !pss && p.signature_type != 20 &&
-      p.signature_type != 21) {
+  // RSA exponent (signatureVerification.circom:14-75): 3 for SIG 10, 37187 for SIG 4, else 65537
+  const long EXP = p.signature_type == 10 ? 3 : p.signature_type == 4 ? 37187 : 65537;
+  if ((p.signature_type < 1 || p.signature_type > 4) && !pss && p.signature_type != 20 && p.signature_type != 21) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1-3, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1-4, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
     return false;
   }
   const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
   // DG_HASH_TYPE 256 or 160; SIGNATURE_TYPE 3 hashes the EC / SA with SHA-1 (HASH_TYPE 160), which the flow's
   // `encapsulatedContentHash[i], i < HASH_SIZE` loop (passportVerificationFlow.circom:36-40) allows only with DG 160
   if (p.dg_hash_type != 256 && p.dg_hash_type != 160) { why = "DG_HASH_TYPE must be 256 or 160"; return false; }
-  if (p.signature_type == 3 && p.dg_hash_type != 160) { why = "SIGNATURE_TYPE 3 needs DG_HASH_TYPE 160"; return false; }
-  const int DG = p.dg_hash_type, HT = p.signature_type == 3 ? 160 : 256;
+  const bool sha1_sig = p.signature_type == 3 || p.signature_type == 4;
+  if (sha1_sig && p.dg_hash_type != 160) { why = "SIGNATURE_TYPE 3 / 4 need DG_HASH_TYPE 160"; return false; }
+  const int DG = p.dg_hash_type, HT = sha1_sig ? 160 : 256;
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
   // AA_SIGNATURE_ALGO: 0 none, 1..19 RSA-1024 key (identity.circom:25-49), >= 20 EC key (:51-84); the raw value
   // also scales the DG15 IsEqual inputs of the flow (passportVerificationFlow.circom:45-46,73-74)
@@ -59,7 +61,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool aa_ec = p.aa_signature_algo >= 20;
   const int aa_f = p.aa_signature_algo == 22 ? 320 : p.aa_signature_algo == 23 ? 192 : 256;
   const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
-  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : p.signature_type == 14 ? 48 : 32;  // signature / pubkey input length
+  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : (p.signature_type == 14 || p.signature_type == 4) ? 48 : 32;  // signature / pubkey input length
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
@@ -173,7 +175,20 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
     // PowerMod(64,K,EXP): out[K] | base[K], modulus[K] | muls[], resultMuls[] (bigInt.circom:280-340).
     // exp_to_bits(65537) = [16, 2, 0, 16], exp_to_bits(3) = [1, 2, 0, 1]: muls[i] = muls[i-1]^2
     // (muls[0] = base^2), then resultMuls[0] = base * muls[last]
-    const int n_modmul = p.signature_type == 10 ? 2 : 17;
+    // exp_to_bits(EXP): bit-length - 1 squarings muls[i] = muls[i-1]^2 (muls[0] = base^2), then one
+    // resultMuls per further set bit: resultMuls[0] = (bit 0 ? base : muls[b0-1]) * muls[b1-1],
+    // resultMuls[i] = resultMuls[i-1] * muls[b_{i+1}-1]
+    int ones[64], n_ones = 0, nbits = 0;
+    for (long v = EXP; v > 0; v >>= 1, nbits++)
+      if (v & 1) ones[n_ones++] = nbits;
+    const int nsq = nbits - 1, n_modmul = nsq + n_ones - 1;
+    if (n_modmul > 32 || n_ones < 2) { why = "internal: PowerMod schedule"; return false; }
+    for (int i = 0; i < nsq; i++) L.reg.mm_x[i] = L.reg.mm_y[i] = (int8_t)(i == 0 ? -1 : i - 1);
+    for (int i = 0; i + 1 < n_ones; i++) {
+      const int k = nsq + i;
+      L.reg.mm_x[k] = (int8_t)(i == 0 ? (ones[0] == 0 ? -1 : ones[0] - 1) : k - 1);
+      L.reg.mm_y[k] = (int8_t)(ones[i + 1] - 1);
+    }
     auto power_mod = [&]() -> bool {
       b.region(RK_RSA_OUT, K);
       b.region(RK_INCOPY, K, {IN_SIG});

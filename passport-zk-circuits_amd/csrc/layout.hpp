@@ -161,6 +161,9 @@ struct RegInfo {
   int32_t v_pkhash, v_leaf, v_smt_h;  // Poseidon outputs (v_smt_h: first of 80 level hashes)
   int32_t dg1_chunk, aa_shift, in_dg1, in_dg15, aa;
   int32_t n_modmul;
+  // PowerMod schedule (bigInt.circom:280-340, exp_to_bits bigIntFunc.circom:590-616): operands of BigMultModP k
+  // are the remainders of multiplications mm_x[k], mm_y[k] (-1: the signature)
+  int8_t mm_x[32], mm_y[32];
   uint32_t modmul_size;
   int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (ECDSA)
   int32_t ec_curve;                // 0: secp256r1 (20), 1: brainpoolP256r1 (21) (ec_common.hpp)

@@ -180,14 +180,15 @@ __device__ void rsa_lane(const DevLayout& L, const uint8_t* row, uint64_t* core,
     // resultMuls[0] = base * muls[15].mod (bigInt.circom:299-327)
     for (int i = 0; i < K; i++) {
       uint64_t xi;
-      if (k == 0 || k == NM - 1) {
+      const int sx = L.reg.mm_x[k], sy = L.reg.mm_y[k];
+      if (sx < 0) {
         const uint8_t* e = row + 32ull * (L.reg.in_sig + i);
         bad |= !in_is_u64(e);
         xi = in_u64(e);
       } else {
-        xi = core[(size_t)(k - 1) * MMW + 3 * K + 1 + i];
+        xi = core[(size_t)sx * MMW + 3 * K + 1 + i];
       }
-      uint64_t yi = k == NM - 1 ? core[(size_t)(k - 1) * MMW + 3 * K + 1 + i] : xi;
+      uint64_t yi = sy == sx ? xi : core[(size_t)sy * MMW + 3 * K + 1 + i];
       x[i] = xi; y[i] = yi;
       mc[i] = xi; mc[K + i] = yi;
     }

@@ -153,18 +153,19 @@ __global__ void __launch_bounds__(64) k_rsa_core2(DevLayout L, const uint8_t* in
   const int NM = L.reg.n_modmul;
   for (int k = 0; k < NM; k++) {
     uint64_t* mc = core + (size_t)k * MMW;
-    // operands (exp_to_bits(65537) = [16,2,0,16]): muls[k] = muls[k-1].mod^2 with muls[0] = base^2;
-    // resultMuls[0] = base * muls[15].mod (bigInt.circom:299-327)
+    // operands from the PowerMod schedule (e.g. 65537: muls[k] = muls[k-1].mod^2, muls[0] = base^2, then
+    // resultMuls[0] = base * muls[15].mod; bigInt.circom:299-327)
     for (int i = g; i < K; i += G) {
       uint64_t xi;
-      if (k == 0 || k == NM - 1) {
+      const int sx = L.reg.mm_x[k], sy = L.reg.mm_y[k];
+      if (sx < 0) {
         const uint8_t* e = row + 32ull * (L.reg.in_sig + i);
         bad |= !in_is_u64(e);
         xi = in_u64(e);
       } else {
-        xi = core[(size_t)(k - 1) * MMW + 3 * K + 1 + i];
+        xi = core[(size_t)sx * MMW + 3 * K + 1 + i];
       }
-      const uint64_t yi = k == NM - 1 ? core[(size_t)(k - 1) * MMW + 3 * K + 1 + i] : xi;
+      const uint64_t yi = sy == sx ? xi : core[(size_t)sy * MMW + 3 * K + 1 + i];  // squaring, or a muls remainder
       x[i] = xi; y[i] = yi;
       if (live) { mc[i] = xi; mc[K + i] = yi; }
     }

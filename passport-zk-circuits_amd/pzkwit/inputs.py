@@ -6,6 +6,7 @@ bigintToArrayString :125-135, getFakeIdenData :628-657, writeToJson :659-672).
 Synthetic workloads follow SURVEY.md §8d (configs 2-4, seeds 0x2-0x4).
 """
 import hashlib
+import math
 import os
 
 import numpy as np
@@ -74,7 +75,7 @@ class RsaKey:
                 continue
             n = p * q
             phi = (p - 1) * (q - 1)
-            if n.bit_length() != bits or phi % e == 0:
+            if n.bit_length() != bits or math.gcd(phi, e) != 1:
                 continue
             break
         self.n, self.e, self.p, self.q = n, e, p, q
@@ -225,7 +226,7 @@ def ecdsa_pk_hash(q):
 
 def sig_input_len(sig):
     """signature / pubkey input lengths (registerIdentityBuilder.circom:131-140)."""
-    return 8 if sig >= 20 else 64 if sig == 2 else 48 if sig == 14 else 32
+    return 8 if sig >= 20 else 64 if sig == 2 else 48 if sig in (4, 14) else 32
 
 
 def sig_limbs(v, sig):
@@ -242,7 +243,7 @@ CANONICAL = dict(sig=1, dg_hash=256, doc=3, ec_blocks=4, ec_shift=600, dg1_shift
 
 def instance_params(sig):
     """The canonical instance with SIGNATURE_TYPE sig (SIG 3 hashes with SHA-1 and needs DG_HASH_TYPE 160)."""
-    return dict(CANONICAL, sig=sig, dg_hash=160 if sig == 3 else 256)
+    return dict(CANONICAL, sig=sig, dg_hash=160 if sig in (3, 4) else 256)
 
 _MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789<"
 _DG15_PREFIX = bytes.fromhex("6f81a230819f300d06092a864886f70d010101050003818d00308189028181")
@@ -287,9 +288,9 @@ class PassportGen:
             key_bits = "bp256" if self.params["sig"] == 21 else "p256"
         elif self.params["sig"] == 2 and key_bits == 2048:
             key_bits = 4096
-        elif self.params["sig"] == 14 and key_bits == 2048:
+        elif self.params["sig"] in (4, 14) and key_bits == 2048:
             key_bits = 3072
-        e = 3 if self.params["sig"] == 10 else 65537  # SIG 10: RSA-PSS with e = 3
+        e = 3 if self.params["sig"] == 10 else 37187 if self.params["sig"] == 4 else 65537  # SIG 10: e = 3, SIG 4: 37187
         jobs = [(seed, k, key_bits) if e == 65537 else (seed, k, key_bits, e) for k in range(n_keys)]
         workers = workers or min(16, os.cpu_count() or 1)
         if n_keys >= 8 and workers > 1:
@@ -346,7 +347,7 @@ class PassportGen:
         ec = bytearray(rng.bytes(ec_len))
         # DG hashes: DG_HASH_TYPE; EC / SA hashes: SHA-1 for SIGNATURE_TYPE 3 (passportVerificationBuilder.circom:19-50)
         dgh = hashlib.sha1 if pr["dg_hash"] == 160 else hashlib.sha256
-        sah = hashlib.sha1 if pr["sig"] == 3 else hashlib.sha256
+        sah = hashlib.sha1 if pr["sig"] in (3, 4) else hashlib.sha256
         h1, h15 = dgh(dg1).digest(), dgh(dg15).digest()
         d1 = pr["dg1_shift"] // 8
         ec[d1 - 7:d1] = bytes.fromhex("30250201010420")
@@ -365,7 +366,7 @@ class PassportGen:
             sig = key.sign(sa, rng)
         elif 10 <= pr["sig"] <= 12 or pr["sig"] == 14:
             sig = pss_sha256_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])))
-        elif pr["sig"] == 3:
+        elif pr["sig"] in (3, 4):
             sig = pkcs1v15_sha1_sign(key, sa)
         else:
             sig = pkcs1v15_sha256_sign(key, sa)

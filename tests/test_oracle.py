@@ -287,8 +287,8 @@ def test_sha1_oracle_digest(oracle):
         assert np.packbits(w[1:161, 0]).tobytes() == hashlib.sha1(msg).digest()
 
 
-@pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160)],
-                         ids=["sig3-dg160", "sig1-dg160"])
+@pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160),
+                                    dict(I.CANONICAL, sig=4, dg_hash=160)], ids=["sig3-dg160", "sig1-dg160", "sig4-dg160"])
 def test_sha1_instances_oracle(oracle, params):
     """SIGNATURE_TYPE 3 (RSA PKCS#1 v1.5 over SHA-1 signed attributes, rsa.circom:73-109) and DG_HASH_TYPE 160:
     a hashlib-SHA-1 / PKCS#1 v1.5 signed synthetic passport passes every check; passportHash = Poseidon1 of the
@@ -298,9 +298,9 @@ def test_sha1_instances_oracle(oracle, params):
     pp = g.passport_at(0)
     rc, w = oracle.register_witness(prm, I.pack_register_inputs(pp, params))
     assert rc == 0
-    h = (hashlib.sha1 if params["sig"] == 3 else hashlib.sha256)(pp["sa"]).digest()
+    h = (hashlib.sha1 if params["sig"] in (3, 4) else hashlib.sha256)(pp["sa"]).digest()
     bits = [(h[i // 8] >> (7 - i % 8)) & 1 for i in range(8 * len(h))]
-    sh = 92 if params["sig"] == 3 else 0
+    sh = 92 if params["sig"] in (3, 4) else 0
     assert oracle.from_elem(w[2]) == field.poseidon([sum(bits[i] << (i + sh) for i in range(min(252, len(bits))))])
     bad = dict(pp)
     bad["sig"] = pp["sig"] + 1

@@ -395,15 +395,20 @@ static void run_rounds(ctx_t *c, size_t b) {
   }
 }
 
-/* Sha256HashChunks(B) sha256HashChunks.circom:8-48
- * out[256] | in[512B] | states[B+1][8][32] | iv, (sch[m], rds[m]) x B */
-static size_t sz_sha256chunks(int B) {
-  return 256 + 512 * (size_t)B + 256 * (size_t)(B + 1) + 256 + (size_t)B * (sz_schedule() + sz_rounds());
+/* Sha256HashChunks(B) sha256HashChunks.circom:8-48 / Sha224HashChunks(B) sha224/sha224HashChunks.circom:8-51
+ * (O = 256 / 224): out[O] | in[512B] | states[B+1][8][32] | iv, (sch[m], rds[m]) x B; the SHA-224 IV
+ * sha224InitialValue.circom:10-20 */
+static const uint32_t SHA224_IV[8] = {0xc1059ed8, 0x367cd507, 0x3070dd17, 0xf70e5939,
+                                      0xffc00b31, 0x68581511, 0x64f98fa7, 0xbefa4fa4};
+static size_t sz_sha2chunks(int O, int B) {
+  return (size_t)O + 512 * (size_t)B + 256 * (size_t)(B + 1) + 256 + (size_t)B * (sz_schedule() + sz_rounds());
 }
-static void run_sha256chunks(ctx_t *c, size_t b, int B) {
-  size_t out = b, in = b + 256, states = in + 512 * (size_t)B, iv = states + 256 * (size_t)(B + 1);
+static size_t sz_sha256chunks(int B) { return sz_sha2chunks(256, B); }
+static void run_sha2chunks(ctx_t *c, size_t b, int B, int O) {
+  size_t out = b, in = b + O, states = in + 512 * (size_t)B, iv = states + 256 * (size_t)(B + 1);
+  const uint32_t *IV = O == 224 ? SHA224_IV : SHA_IV;
   for (int k = 0; k < 8; k++)
-    for (int i = 0; i < 32; i++) W(iv + 32 * k + i) = fr_u64((SHA_IV[k] >> i) & 1);
+    for (int i = 0; i < 32; i++) W(iv + 32 * k + i) = fr_u64((IV[k] >> i) & 1);
   for (int q = 0; q < 256; q++) W(states + q) = W(iv + q);
   size_t blk = iv + 256;
   for (int m = 0; m < B; m++) {
@@ -416,9 +421,10 @@ static void run_sha256chunks(ctx_t *c, size_t b, int B) {
     run_rounds(c, rds);
     for (int q = 0; q < 256; q++) W(states + 256 * (size_t)(m + 1) + q) = W(rds + q);
   }
-  for (int j = 0; j < 8; j++)
+  for (int j = 0; j < O / 32; j++)
     for (int i = 0; i < 32; i++) W(out + 32 * j + i) = W(states + 256 * (size_t)B + 32 * j + 31 - i);
 }
+static void run_sha256chunks(ctx_t *c, size_t b, int B) { run_sha2chunks(c, b, B, 256); }
 
 /* ShaHashChunks(B, 256) hash.circom:32-68: out[256] | in[512B] | hash256 */
 static size_t sz_shahash(int B) { return 256 + 512 * (size_t)B + sz_sha256chunks(B); }
@@ -598,8 +604,18 @@ static void run_sha1chunks(ctx_t *c, size_t b, int B) {
 }
 
 /* ShaHashChunks(B, ALGO) hash.circom:32-68 for ALGO 160 / 256: out[ALGO] | in[512B] | Sha1/Sha256HashChunks(B) */
-static size_t sz_hashc(int algo, int B) { return algo == 160 ? 160 + 512 * (size_t)B + sz_sha1chunks(B) : sz_shahash(B); }
+static size_t sz_hashc(int algo, int B) {
+  return algo == 160 ? 160 + 512 * (size_t)B + sz_sha1chunks(B) : algo == 224 ? 224 + 512 * (size_t)B + sz_sha2chunks(224, B)
+                                                                  : sz_shahash(B);
+}
 static void run_hashc(ctx_t *c, size_t b, int algo, int B) {
+  if (algo == 224) {
+    size_t in = b + 224, h = in + 512 * (size_t)B;
+    for (size_t q = 0; q < 512 * (size_t)B; q++) W(h + 224 + q) = W(in + q);
+    run_sha2chunks(c, h, B, 224);
+    for (int q = 0; q < 224; q++) W(b + q) = W(h + q);
+    return;
+  }
   if (algo != 160) { run_shahash(c, b, B); return; }
   size_t in = b + 160, h = in + 512 * (size_t)B;
   for (size_t q = 0; q < 512 * (size_t)B; q++) W(h + 160 + q) = W(in + q);
@@ -1554,7 +1570,7 @@ static void orc_init(void) {
 }
 
 static int params_ok(const orc_params *P) {
-  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 160) && ((P->sig != 3 && P->sig != 4) || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
+  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160) && ((P->sig != 3 && P->sig != 4) || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 

@@ -75,6 +75,7 @@ struct Builder {
   }
   // a SHA job of either algorithm whose regions are placed later (sha_regions)
   int hash_job(int algo, int in_off, int blocks) {
+    if (algo == 224) { const int j = sha_job(in_off, blocks); L.sha[j].algo = 2; return j; }
     if (algo != 160) return sha_job(in_off, blocks);
     ShaJob j{};
     j.in_off = in_off;

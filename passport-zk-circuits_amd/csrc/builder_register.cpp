@@ -50,7 +50,10 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
   // DG_HASH_TYPE 256 or 160; SIGNATURE_TYPE 3 hashes the EC / SA with SHA-1 (HASH_TYPE 160), which the flow's
   // `encapsulatedContentHash[i], i < HASH_SIZE` loop (passportVerificationFlow.circom:36-40) allows only with DG 160
-  if (p.dg_hash_type != 256 && p.dg_hash_type != 160) { why = "DG_HASH_TYPE must be 256 or 160"; return false; }
+  if (p.dg_hash_type != 256 && p.dg_hash_type != 224 && p.dg_hash_type != 160) {
+    why = "DG_HASH_TYPE must be 256, 224 or 160";
+    return false;
+  }
   const bool sha1_sig = p.signature_type == 3 || p.signature_type == 4;
   if (sha1_sig && p.dg_hash_type != 160) { why = "SIGNATURE_TYPE 3 / 4 need DG_HASH_TYPE 160"; return false; }
   const int DG = p.dg_hash_type, HT = sha1_sig ? 160 : 256;
@@ -155,9 +158,10 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   if (ecdsa) b.region(RK_EC_PKBITS, 512, {IN_PK});  // ecBitsX[256], ecBitsY[256]
   else b.region(RK_TEMPMOD, 5, {IN_PK});
   auto sha_blocks = [&](int job, int in_off, int blocks) {
-    if (L.sha[job].algo) { b.sha1_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 160)
-    uint64_t own = 256 + 512ull * blocks + 256 + 512ull * blocks + 256ull * (blocks + 1) + 256;
-    b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1});
+    if (L.sha[job].algo == 1) { b.sha1_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 160)
+    const int O = L.sha[job].algo == 2 ? 224 : 256;  // ShaHashChunks(B, 224 | 256)
+    uint64_t own = O + 512ull * blocks + O + 512ull * blocks + 256ull * (blocks + 1) + 256;
+    b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1, O});
     for (int m = 0; m < blocks; m++) b.region(RK_SHA_BLOCK, 150762, {job, m});
   };
   sha_blocks(J_DG1, IN_DG1, 2);

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
   if (w >= batch || j >= n_jobs) return;
   const ShaJob& J = jobs[j];
   const uint8_t* row = J.src ? derived + 32ull * (uint64_t)w * n_derived : inputs + 32ull * (uint64_t)w * n_inputs;
-  if (J.algo) sha1_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
+  if (J.algo == 1) sha1_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
   else sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
 }
 
@@ -83,21 +83,21 @@ __global__ void __launch_bounds__(256) k_pos_core(PosConsts K, const PosTask* ta
 __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t* H /* (B+1)*8 in LDS */, uint32_t s,
                                                 bool& is_copy, uint64_t& src) {
   const int B = R.a[1];
-  const uint32_t inLen = 512u * B;
+  const uint32_t inLen = 512u * B, O = R.a[4] == 224 ? 224u : 256u;  // SHA-224: out[224], its own IV
   is_copy = false;
-  if (R.a[3]) {  // ShaHashChunks wrapper: out[256] | in[512B]
-    if (s < 256) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
-    s -= 256;
+  if (R.a[3]) {  // ShaHashChunks wrapper: out[O] | in[512B]
+    if (s < O) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
+    s -= O;
     if (s < inLen) { is_copy = true; src = (uint64_t)R.a[2] + s; return 0; }
     s -= inLen;
   }
-  if (s < 256) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
-  s -= 256;
+  if (s < O) { uint32_t j = s >> 5, i = s & 31; return (H[B * 8 + j] >> (31 - i)) & 1; }
+  s -= O;
   if (s < inLen) { is_copy = true; src = (uint64_t)R.a[2] + s; return 0; }
   s -= inLen;
   if (s < 256u * (B + 1)) { uint32_t m = s >> 8, j = (s >> 5) & 7, i = s & 31; return (H[m * 8 + j] >> i) & 1; }
   s -= 256u * (B + 1);
-  return (SHA_IV[s >> 5] >> (s & 31)) & 1;
+  return ((O == 224 ? SHA224_IV[s >> 5] : SHA_IV[s >> 5]) >> (s & 31)) & 1;
 }
 
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,

@@ -131,7 +131,7 @@ struct ShaJob {
   int32_t core_off; // u32 offset of this hasher's core inside the per-witness SHA core
   int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
   int32_t src;      // 0: message bits are input elements; 1: derived elements (RSA-PSS, pss.hpp)
-  int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp)
+  int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp), 2: SHA-224 (SHA-256 blocks, own IV, 224-bit out)
   int32_t hout;     // u32 offset of the digest words (Hout[8] / Hout[5]) inside the per-witness SHA core
 };
 

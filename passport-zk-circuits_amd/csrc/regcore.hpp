@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs,
     const ShaJob job = L.sha[R.j_sa];
     const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.hout;
     // the hash's first 252 bits, or a 160-bit SHA-1 hash shifted up by 92 (passportVerificationBuilder.circom:164-177)
-    const int sh = job.algo ? 92 : 0;
+    const int sh = job.algo == 1 ? 92 : 0;
     fr sn = bits_to_fr(252, [&](int k) { return k < sh ? 0u : (H[(k - sh) >> 5] >> (31 - ((k - sh) & 31))) & 1u; });
     vs.at(R.v_sanum, w) = fr_to_mont(sn);
   }
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
   }
   if (L.reg.pss_s8) {
     pss_check(pss_view(L, rsa_core, sha_core, w), status + w);
-  } else if (J.algo) {
+  } else if (J.algo == 1) {
     // RsaVerifyPkcs1v15(64,K,65537,160) (rsa.circom:73-109): EM limb 2 = 0x05000414 | first digest word,
     // limbs 3, 4 = DigestInfo, then 0xFF.. padding and the 00 01 top limb; digest words 1-4 are not constrained
     const uint64_t em2 = em[2];

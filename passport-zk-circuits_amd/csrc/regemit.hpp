@@ -310,7 +310,8 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
   const int jd1 = R.a[0], jd15 = R.a[1], jec = R.a[2], jsa = R.a[3], in_ec = R.a[4], in_sa = R.a[5];
   const int d1s = R.a[6], d15s = R.a[7], ecs = R.a[8], V = R.a[9];
   const int ecLen = 512 * L.sha[jec].blocks;
-  const int H = L.sha[jd1].algo ? 160 : 256, EH = L.sha[jec].algo ? 160 : 256, NC = 3 * H + 8;
+  auto hbits = [&](int j) { return L.sha[j].algo == 1 ? 160 : L.sha[j].algo == 2 ? 224 : 256; };
+  const int H = hbits(jd1), EH = hbits(jec), NC = 3 * H + 8;
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   const uint32_t* H1 = sha_hout(L, B, w, jd1);
   const uint32_t* H15 = jd15 >= 0 ? sha_hout(L, B, w, jd15) : nullptr;

@@ -650,7 +650,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);
     }
     if (phase == PH_SHA_CORE)
-      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
+      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo == 1 ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
     if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;

@@ -25,6 +25,9 @@ __device__ __constant__ uint32_t SHA_K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 __device__ __constant__ uint32_t SHA_IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                                               0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+// SHA-224 (sha224InitialValue.circom:10-20): the same blocks from another IV, 224 output bits
+__device__ __constant__ uint32_t SHA224_IV[8] = {0xc1059ed8, 0x367cd507, 0x3070dd17, 0xf70e5939,
+                                                 0xffc00b31, 0x68581511, 0x64f98fa7, 0xbefa4fa4};
 
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 __device__ __forceinline__ uint32_t bsig0(uint32_t a) { return rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22); }
@@ -39,7 +42,7 @@ __device__ __forceinline__ void sha_core_lane(const uint8_t* in_row, const ShaJo
                                               int32_t* status) {
   uint32_t H[8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) H[j] = SHA_IV[j];
+  for (int j = 0; j < 8; j++) H[j] = job.algo == 2 ? SHA224_IV[j] : SHA_IV[j];
   bool bad = false;
   for (int m = 0; m < job.blocks; m++) {
     uint32_t* bc = core + job.core_off + m * SHA_BLOCK_CORE;

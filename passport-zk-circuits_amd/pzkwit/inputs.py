@@ -346,7 +346,7 @@ class PassportGen:
         ec_len = 219 + rng.below(pr["ec_blocks"] * 64 - 9 - 219 + 1)
         ec = bytearray(rng.bytes(ec_len))
         # DG hashes: DG_HASH_TYPE; EC / SA hashes: SHA-1 for SIGNATURE_TYPE 3 (passportVerificationBuilder.circom:19-50)
-        dgh = hashlib.sha1 if pr["dg_hash"] == 160 else hashlib.sha256
+        dgh = {160: hashlib.sha1, 224: hashlib.sha224}.get(pr["dg_hash"], hashlib.sha256)
         sah = hashlib.sha1 if pr["sig"] in (3, 4) else hashlib.sha256
         h1, h15 = dgh(dg1).digest(), dgh(dg15).digest()
         d1 = pr["dg1_shift"] // 8

@@ -81,6 +81,7 @@ PARAM_SETS = [
     dict(I.CANONICAL, sig=3, dg_hash=160),         # RSA-2048 PKCS#1 v1.5 SHA-1, SHA-1 DG hashes
     dict(I.CANONICAL, sig=1, dg_hash=160, aa=0),   # SHA-1 DG hashes, SHA-256 signed attributes
     dict(I.CANONICAL, sig=4, dg_hash=160),         # RSA-3072 PKCS#1 v1.5 SHA-1, e = 37187 (20 BigMultModP)
+    dict(I.CANONICAL, dg_hash=224),                # SHA-224 DG hashes
 ]
 
 

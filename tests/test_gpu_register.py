@@ -174,7 +174,8 @@ def test_register_rsa_outside_barrett_domain_matches_oracle(oracle, gen):
 
 
 @pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160, aa=0),
-                                    dict(I.CANONICAL, sig=4, dg_hash=160)], ids=["sig3-dg160", "sig1-dg160-aa0", "sig4-dg160"])
+                                    dict(I.CANONICAL, sig=4, dg_hash=160), dict(I.CANONICAL, dg_hash=224)],
+                         ids=["sig3-dg160", "sig1-dg160-aa0", "sig4-dg160", "sig1-dg224"])
 def test_register_sha1_instances_match_oracle(oracle, params):
     """SHA-1 hashers inside RegisterIdentityBuilder (ShaHashChunks(B, 160) around Sha1HashChunks) for the DG
     hashes and, with SIGNATURE_TYPE 3, the EC / SA hashes and the PKCS#1 v1.5 SHA-1 check; a bad signature

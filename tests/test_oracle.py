@@ -288,7 +288,8 @@ def test_sha1_oracle_digest(oracle):
 
 
 @pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160),
-                                    dict(I.CANONICAL, sig=4, dg_hash=160)], ids=["sig3-dg160", "sig1-dg160", "sig4-dg160"])
+                                    dict(I.CANONICAL, sig=4, dg_hash=160), dict(I.CANONICAL, dg_hash=224)],
+                         ids=["sig3-dg160", "sig1-dg160", "sig4-dg160", "sig1-dg224"])
 def test_sha1_instances_oracle(oracle, params):
     """SIGNATURE_TYPE 3 (RSA PKCS#1 v1.5 over SHA-1 signed attributes, rsa.circom:73-109) and DG_HASH_TYPE 160:
     a hashlib-SHA-1 / PKCS#1 v1.5 signed synthetic passport passes every check; passportHash = Poseidon1 of the

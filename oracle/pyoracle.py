@@ -52,6 +52,9 @@ def lib():
         L.orc_sha256_witness.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_sha1_witness_size.restype = ctypes.c_size_t
         L.orc_sha1_witness.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_sha512_witness_size.restype = ctypes.c_size_t
+        L.orc_sha512_witness_size.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_sha512_witness.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         rc = L.orc_load_poseidon(POSEIDON_BIN.encode())
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
@@ -131,4 +134,15 @@ def sha1_witness(in_elems, blocks):
     w = np.zeros((sz, 32), dtype=np.uint8)
     a = np.ascontiguousarray(in_elems, dtype=np.uint8)
     rc = L.orc_sha1_witness(blocks, a.ctypes.data, w.ctypes.data)
+    return rc, w
+
+
+def sha512_witness(in_elems, blocks, out_bits=512):
+    """Sha512HashChunks(blocks) (out_bits 512) / Sha384HashChunks(blocks) (384) witness;
+    in_elems: (1024*blocks, 32) uint8 array of input signals."""
+    L = lib()
+    sz = L.orc_sha512_witness_size(blocks, out_bits)
+    w = np.zeros((sz, 32), dtype=np.uint8)
+    a = np.ascontiguousarray(in_elems, dtype=np.uint8)
+    rc = L.orc_sha512_witness(blocks, out_bits, a.ctypes.data, w.ctypes.data)
     return rc, w

@@ -435,6 +435,206 @@ static void run_shahash(ctx_t *c, size_t b, int B) {
   for (int q = 0; q < 256; q++) W(b + q) = W(h + q);
 }
 
+/* ============================================================ SHA-384 / SHA-512
+ * Sha384HashChunks(B) / Sha512HashChunks(B) (sha2/sha384/sha384HashChunks.circom:8-49,
+ * sha2/sha512/sha512HashChunks.circom:8-46) over Sha2_384_512Schedule (sha512Schedule.circom:11-75),
+ * Sha2_384_512Rounds(80) (sha512Rounds.circom:11-126) and Sha2_384_512CompressInner
+ * (sha512Compress.circom:11-96): the SHA-256 templates above with 64-bit words, 80 rounds, the
+ * FIPS 180-4 SHA-512 rotations and constants (sha512RoundConst.circom, sha512InitialValue.circom,
+ * sha384InitialValue.circom). Word sums exceed 64 bits (overflowA < 7 * 2^64): fr arithmetic. */
+static const uint64_t SHA512_IV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                                      0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                      0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+static const uint64_t SHA384_IV[8] = {0xcbbb9d5dc1059ed8ull, 0x629a292a367cd507ull, 0x9159015a3070dd17ull,
+                                      0x152fecd8f70e5939ull, 0x67332667ffc00b31ull, 0x8eb44a8768581511ull,
+                                      0xdb0c2e0d64f98fa7ull, 0x47b5481dbefa4fa4ull};
+static const uint64_t SHA512_K[80] = {
+    0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull, 0x3956c25bf348b538ull,
+    0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull, 0xd807aa98a3030242ull, 0x12835b0145706fbeull,
+    0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull, 0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull,
+    0xc19bf174cf692694ull, 0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+    0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull, 0x983e5152ee66dfabull,
+    0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull, 0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull,
+    0x06ca6351e003826full, 0x142929670a0e6e70ull, 0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull,
+    0x53380d139d95b3dfull, 0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+    0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull, 0xd192e819d6ef5218ull,
+    0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull, 0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull,
+    0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull, 0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull,
+    0x682e6ff3d6b2b8a3ull, 0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+    0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull, 0xca273eceea26619cull,
+    0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull, 0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull,
+    0x113f9804bef90daeull, 0x1b710b35131c471bull, 0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull,
+    0x431d67c49c100d4cull, 0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
+
+/* GetSumOfNElements(64) fed with (1 << i) * bits[i]: out | in[64] | sum[63] (128 signals) */
+static void run_wordsum64(ctx_t *c, size_t s, size_t bits) {
+  for (int i = 0; i < 64; i++) W(s + 1 + i) = mulg(POW2[i], W(bits + i));
+  run_getsum(c, s, 64);
+}
+
+/* Sha2_384_512Schedule sha512Schedule.circom:11-75
+ * outWords[80] | chunkBits[16][64] | outBits[80][64] | sumN[16], {s0Sum,s1Sum,(s0Xor,s1Xor)x64,modulo,bits2Num}x64 */
+#define SCH5_OWN (80 + 1024 + 5120)
+#define SCH5_PER_M (128 + 128 + 64 * 10 + 322 + 129)
+static size_t sz_schedule512(void) { return SCH5_OWN + 16 * 128 + 64 * SCH5_PER_M; }
+static void run_schedule512(ctx_t *c, size_t b) {
+  size_t outWords = b, chunk = b + 80, outBits = b + 1104;
+  size_t sub = b + SCH5_OWN;
+  for (int k = 0; k < 16; k++) {
+    size_t s = sub + 128 * (size_t)k;
+    run_wordsum64(c, s, chunk + 64 * k);
+    W(outWords + k) = W(s);
+    for (int i = 0; i < 64; i++) W(outBits + 64 * k + i) = W(chunk + 64 * k + i);
+  }
+  sub += 16 * 128;
+  for (int m = 16; m < 80; m++) {
+    int r = m - 16, k = m - 15, l = m - 2;
+    size_t s0Sum = sub + (size_t)r * SCH5_PER_M, s1Sum = s0Sum + 128, xo = s1Sum + 128;
+    size_t modulo = xo + 640, b2n = modulo + 322;
+    for (int i = 0; i < 64; i++) {
+      size_t x0 = xo + 10 * (size_t)i, x1 = x0 + 5;
+      W(x0 + 1) = W(outBits + 64 * k + (i + 1) % 64);
+      W(x0 + 2) = W(outBits + 64 * k + (i + 8) % 64);
+      W(x0 + 3) = (i < 64 - 7) ? W(outBits + 64 * k + i + 7) : fr_zero();
+      run_xor3(c, x0);
+      W(s0Sum + 1 + i) = mulg(POW2[i], W(x0));
+      W(x1 + 1) = W(outBits + 64 * l + (i + 19) % 64);
+      W(x1 + 2) = W(outBits + 64 * l + (i + 61) % 64);
+      W(x1 + 3) = (i < 64 - 6) ? W(outBits + 64 * l + i + 6) : fr_zero();
+      run_xor3(c, x1);
+      W(s1Sum + 1 + i) = mulg(POW2[i], W(x1));
+    }
+    run_getsum(c, s0Sum, 64);
+    run_getsum(c, s1Sum, 64);
+    W(modulo + 65) = fr_add(fr_add(fr_add(W(s1Sum), W(outWords + m - 7)), W(s0Sum)), W(outWords + m - 16));
+    run_lastnbits(c, modulo, 64);
+    for (int i = 0; i < 64; i++) W(outBits + 64 * m + i) = W(modulo + 1 + i);
+    for (int i = 0; i < 64; i++) W(b2n + 1 + i) = W(outBits + 64 * m + i);
+    run_bits2num(c, b2n, 64);
+    W(outWords + m) = W(b2n);
+  }
+}
+
+/* Sha2_384_512CompressInner sha512Compress.circom:11-96
+ * outA,outB,outC[64],outDD,outE,outF,outG[64],outHH (386) | inp,key,a,b,c,dd,e,f,g,hh (388) |
+ * chb[64],overflowE,overflowA | dSum,hSum,s0Sum,s1Sum,mjSum,chSum, (major,s0Xor,s1Xor)x64, decomposeE, decomposeA */
+#define CI5_OWN 840
+static size_t sz_compress512(void) { return CI5_OWN + 6 * 128 + 64 * 13 + 2 * 322; }
+static void run_compress512(ctx_t *c, size_t b) {
+  size_t oA = b, oB = b + 64, oC = b + 128, oDD = b + 192, oE = b + 193, oF = b + 257, oG = b + 321, oHH = b + 385;
+  size_t inp = b + 386, key = b + 387, A = b + 388, B = b + 452, C = b + 516, DD = b + 580, E = b + 581,
+         F = b + 645, G = b + 709, HH = b + 773, chb = b + 774, ovE = b + 838, ovA = b + 839;
+  size_t dSum = b + CI5_OWN, hSum = dSum + 128, s0Sum = hSum + 128, s1Sum = s0Sum + 128, mjSum = s1Sum + 128,
+         chSum = mjSum + 128, loop = chSum + 128, decE = loop + 64 * 13, decA = decE + 322;
+  for (int i = 0; i < 64; i++) {
+    W(oG + i) = W(F + i); W(oF + i) = W(E + i); W(oC + i) = W(B + i); W(oB + i) = W(A + i);
+  }
+  run_wordsum64(c, dSum, C); run_wordsum64(c, hSum, G);
+  W(oDD) = W(dSum); W(oHH) = W(hSum);
+  for (int i = 0; i < 64; i++) {
+    int64_t e = (int64_t)small(W(E + i)), f = (int64_t)small(W(F + i)), g = (int64_t)small(W(G + i));
+    W(chb + i) = fr_i64(e * (f - g) + g);
+    W(chSum + 1 + i) = mulg(POW2[i], W(chb + i));
+    size_t mj = loop + 13 * (size_t)i, x0 = mj + 3, x1 = x0 + 5;
+    W(mj + 2) = fr_add(fr_add(W(A + i), W(B + i)), W(C + i));
+    run_bits2(c, mj);
+    W(mjSum + 1 + i) = mulg(POW2[i], W(mj + 1));
+    W(x0 + 1) = W(A + (i + 28) % 64); W(x0 + 2) = W(A + (i + 34) % 64); W(x0 + 3) = W(A + (i + 39) % 64);
+    run_xor3(c, x0);
+    W(s0Sum + 1 + i) = mulg(POW2[i], W(x0));
+    W(x1 + 1) = W(E + (i + 14) % 64); W(x1 + 2) = W(E + (i + 18) % 64); W(x1 + 3) = W(E + (i + 41) % 64);
+    run_xor3(c, x1);
+    W(s1Sum + 1 + i) = mulg(POW2[i], W(x1));
+  }
+  run_getsum(c, s0Sum, 64); run_getsum(c, s1Sum, 64); run_getsum(c, mjSum, 64); run_getsum(c, chSum, 64);
+  fr_t t1 = fr_add(fr_add(fr_add(fr_add(W(HH), W(s1Sum)), W(chSum)), W(key)), W(inp));
+  W(ovE) = fr_add(fr_add(W(DD), W(HH)), fr_add(fr_add(fr_add(W(s1Sum), W(chSum)), W(key)), W(inp)));
+  W(ovA) = fr_add(fr_add(t1, W(s0Sum)), W(mjSum));
+  W(decE + 65) = W(ovE); run_lastnbits(c, decE, 64);
+  W(decA + 65) = W(ovA); run_lastnbits(c, decA, 64);
+  for (int i = 0; i < 64; i++) { W(oE + i) = W(decE + 1 + i); W(oA + i) = W(decA + 1 + i); }
+}
+
+/* Sha2_384_512Rounds(80) sha512Rounds.circom:11-126
+ * outHash[8][64] | words[80], inpHash[8][64] | a,b,c[81][64], dd[81], e,f,g[81][64], hh[81], ROUND_KEYS[80],
+ * hashWords[8] | roundKeys, sumDd, sumHh, sum[8], compress[80], modulo[8], sumA,sumB,sumC,sumE,sumF,sumG */
+#define RD5_N 80
+#define RD5_OWN (512 + 80 + 512 + 6 * 81 * 64 + 2 * 81 + 80 + 8)
+static size_t sz_rounds512(void) { return RD5_OWN + 80 + 2 * 128 + 8 * 128 + RD5_N * sz_compress512() + 8 * 322 + 6 * 128; }
+static void run_rounds512(ctx_t *c, size_t b) {
+  const size_t n1 = RD5_N + 1;
+  size_t outHash = b, words = b + 512, inpHash = b + 592;
+  size_t a = b + 1104, bb = a + n1 * 64, cc = bb + n1 * 64, dd = cc + n1 * 64, e = dd + n1, f = e + n1 * 64,
+         g = f + n1 * 64, hh = g + n1 * 64, RK = hh + n1, hashWords = RK + 80;
+  size_t roundKeys = b + RD5_OWN, sumDd = roundKeys + 80, sumHh = sumDd + 128, sum = sumHh + 128,
+         comp = sum + 8 * 128, modulo = comp + RD5_N * sz_compress512(), sumA = modulo + 8 * 322;
+  for (int j = 0; j < 80; j++) W(roundKeys + j) = fr_u64(SHA512_K[j]);
+  for (int j = 0; j < 80; j++) W(RK + j) = W(roundKeys + j);
+  for (int i = 0; i < 64; i++) {
+    W(a + i) = W(inpHash + 0 * 64 + i); W(bb + i) = W(inpHash + 1 * 64 + i); W(cc + i) = W(inpHash + 2 * 64 + i);
+    W(e + i) = W(inpHash + 4 * 64 + i); W(f + i) = W(inpHash + 5 * 64 + i); W(g + i) = W(inpHash + 6 * 64 + i);
+  }
+  run_wordsum64(c, sumDd, inpHash + 3 * 64); run_wordsum64(c, sumHh, inpHash + 7 * 64);
+  W(dd) = W(sumDd); W(hh) = W(sumHh);
+  for (int j = 0; j < 8; j++) {
+    size_t s = sum + 128 * (size_t)j;
+    run_wordsum64(c, s, inpHash + 64 * j);
+    W(hashWords + j) = W(s);
+  }
+  for (int k = 0; k < RD5_N; k++) {
+    size_t cp = comp + (size_t)k * sz_compress512();
+    W(cp + 386) = W(words + k); W(cp + 387) = W(RK + k);
+    for (int i = 0; i < 64; i++) {
+      W(cp + 388 + i) = W(a + 64 * k + i); W(cp + 452 + i) = W(bb + 64 * k + i); W(cp + 516 + i) = W(cc + 64 * k + i);
+      W(cp + 581 + i) = W(e + 64 * k + i); W(cp + 645 + i) = W(f + 64 * k + i); W(cp + 709 + i) = W(g + 64 * k + i);
+    }
+    W(cp + 580) = W(dd + k); W(cp + 773) = W(hh + k);
+    run_compress512(c, cp);
+    for (int i = 0; i < 64; i++) {
+      W(a + 64 * (k + 1) + i) = W(cp + i); W(bb + 64 * (k + 1) + i) = W(cp + 64 + i);
+      W(cc + 64 * (k + 1) + i) = W(cp + 128 + i); W(e + 64 * (k + 1) + i) = W(cp + 193 + i);
+      W(f + 64 * (k + 1) + i) = W(cp + 257 + i); W(g + 64 * (k + 1) + i) = W(cp + 321 + i);
+    }
+    W(dd + k + 1) = W(cp + 192); W(hh + k + 1) = W(cp + 385);
+  }
+  size_t srcs[6] = {a, bb, cc, e, f, g};
+  for (int q = 0; q < 6; q++) run_wordsum64(c, sumA + 128 * (size_t)q, srcs[q] + 64 * RD5_N);
+  fr_t add[8] = {W(sumA), W(sumA + 128), W(sumA + 256), W(dd + RD5_N), W(sumA + 384), W(sumA + 512), W(sumA + 640),
+                 W(hh + RD5_N)};
+  for (int j = 0; j < 8; j++) {
+    size_t md = modulo + 322 * (size_t)j;
+    W(md + 65) = fr_add(W(hashWords + j), add[j]);
+    run_lastnbits(c, md, 64);
+    for (int i = 0; i < 64; i++) W(outHash + 64 * j + i) = W(md + 1 + i);
+  }
+}
+
+/* Sha384HashChunks(B) / Sha512HashChunks(B) (O = 384 / 512):
+ * out[O] | in[1024B] | states[B+1][8][64] | iv (512), (sch[m], rds[m]) x B */
+static size_t sz_sha5chunks(int O, int B) {
+  return (size_t)O + 1024 * (size_t)B + 512 * (size_t)(B + 1) + 512 + (size_t)B * (sz_schedule512() + sz_rounds512());
+}
+static void run_sha5chunks(ctx_t *c, size_t b, int B, int O) {
+  size_t out = b, in = b + O, states = in + 1024 * (size_t)B, iv = states + 512 * (size_t)(B + 1);
+  const uint64_t *IV = O == 384 ? SHA384_IV : SHA512_IV;
+  for (int k = 0; k < 8; k++)
+    for (int i = 0; i < 64; i++) W(iv + 64 * k + i) = fr_u64((IV[k] >> i) & 1);
+  for (int q = 0; q < 512; q++) W(states + q) = W(iv + q);
+  size_t blk = iv + 512;
+  for (int m = 0; m < B; m++) {
+    size_t sch = blk + (size_t)m * (sz_schedule512() + sz_rounds512()), rds = sch + sz_schedule512();
+    for (int k = 0; k < 16; k++)
+      for (int i = 0; i < 64; i++) W(sch + 80 + 64 * k + i) = W(in + 1024 * (size_t)m + 64 * k + (63 - i));
+    run_schedule512(c, sch);
+    for (int k = 0; k < 80; k++) W(rds + 512 + k) = W(sch + k);
+    for (int q = 0; q < 512; q++) W(rds + 592 + q) = W(states + 512 * (size_t)m + q);
+    run_rounds512(c, rds);
+    for (int q = 0; q < 512; q++) W(states + 512 * (size_t)(m + 1) + q) = W(rds + q);
+  }
+  for (int j = 0; j < O / 64; j++)
+    for (int i = 0; i < 64; i++) W(out + 64 * j + i) = W(states + 512 * (size_t)B + 64 * j + 63 - i);
+}
+
 /* =================================================================== SHA-1
  * Sha1HashChunks(B) hasher/sha1/sha1.circom:7-57 and its templates (sha1compression.circom,
  * t.circom, f.circom, parity.circom, rotate.circom, xor4.circom, constants.circom; BinSum
@@ -1653,6 +1853,18 @@ int orc_sha1_witness(int B, const uint8_t *inputs, uint8_t *wit) {
   W(0) = ONE();
   memcpy(&W(1 + 160), inputs, 512 * (size_t)B * 32);
   run_sha1chunks(c, 1, B);
+  return c->err;
+}
+/* Sha384HashChunks(B) / Sha512HashChunks(B) as main (O = 384 / 512): [1, out[O], in[1024B], ...] */
+size_t orc_sha512_witness_size(int B, int O) { orc_init(); return 1 + sz_sha5chunks(O, B); }
+int orc_sha512_witness(int B, int O, const uint8_t *inputs, uint8_t *wit) {
+  orc_init();
+  if (O != 384 && O != 512) return -1;
+  ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
+  memset(wit, 0, orc_sha512_witness_size(B, O) * 32);
+  W(0) = ONE();
+  memcpy(&W(1 + (size_t)O), inputs, (size_t)B * 1024 * 32);
+  run_sha5chunks(c, 1, B, O);
   return c->err;
 }
 int orc_sha256_witness(int B, const uint8_t *inputs, uint8_t *wit) {

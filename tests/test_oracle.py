@@ -287,6 +287,36 @@ def test_sha1_oracle_digest(oracle):
         assert np.packbits(w[1:161, 0]).tobytes() == hashlib.sha1(msg).digest()
 
 
+def _sha512_pad(msg):
+    """FIPS 180-4 SHA-384/512 padding: 1024-bit blocks, 128-bit big-endian length."""
+    ln = 8 * len(msg)
+    p = msg + b"\x80" + b"\x00" * ((111 - len(msg)) % 128) + ln.to_bytes(16, "big")
+    assert len(p) % 128 == 0
+    return p
+
+
+@pytest.mark.parametrize("out_bits", [384, 512])
+def test_sha512_oracle_digest(oracle, out_bits):
+    """Sha384HashChunks(B) / Sha512HashChunks(B) restatement (hasher/sha2/sha384, sha512/*.circom): digest bits
+    equal hashlib.sha384 / sha512 across 1-3 blocks, every GetLastNBits / Bits2 check passes, and the
+    schedule's outWords are the FIPS message words (words > 2^64 would break the 64-bit decompositions)."""
+    rng = np.random.default_rng(37 + out_bits)
+    ref = hashlib.sha384 if out_bits == 384 else hashlib.sha512
+    for ln in (0, 3, 111, 112, 200, 300):
+        msg = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        p = _sha512_pad(msg)
+        blocks = len(p) // 128
+        inp = np.zeros((1024 * blocks, 32), np.uint8)
+        inp[:, 0] = I.bits_msb_first(p)
+        rc, w = oracle.sha512_witness(inp, blocks, out_bits)
+        assert rc == 0
+        assert np.packbits(w[1:1 + out_bits, 0]).tobytes() == ref(msg).digest()
+        # Sha2_384_512Schedule of block 0 starts after out | in | states | iv; its outWords[0..15] = message words
+        sch = 1 + out_bits + 1024 * blocks + 512 * (blocks + 1) + 512
+        words = [int.from_bytes(p[8 * k:8 * k + 8], "big") for k in range(16)]
+        assert [oracle.from_elem(w[sch + k]) for k in range(16)] == words
+
+
 @pytest.mark.parametrize("params", [dict(I.CANONICAL, sig=3, dg_hash=160), dict(I.CANONICAL, sig=1, dg_hash=160),
                                     dict(I.CANONICAL, sig=4, dg_hash=160), dict(I.CANONICAL, dg_hash=224)],
                          ids=["sig3-dg160", "sig1-dg160", "sig4-dg160", "sig1-dg224"])

@@ -220,13 +220,14 @@ def main():
     bytes_per_launch = info[dom][1] * sub
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
-    tfiles = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json")))
-    if tfiles and args.workload == "register":  # PMC traffic is committed for the config-3 kernels
-        tj = json.load(open(tfiles[-1]))
+    # PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per witness, tools/pmc_summary.py) committed under
+    # profiles/pmc_*/traffic.json for the workload this line measures; none -> null
+    for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
+        tj = json.load(open(tf))
         ks = [tj["kernels"].get(k) for k in info[dom][0].split("+")]
-        if all(ks):
+        if tj.get("workload") == workload and all(ks):
             traffic = sum(k["traffic_bytes_per_witness"] for k in ks) * sub
-            traffic_src = os.path.relpath(tfiles[-1], REPO)
+            traffic_src = os.path.relpath(tf, REPO)
     # whole-job algorithmic bytes: inputs read once + .wtns header and elements written once
     job_bytes = 32 * NIN + 76 + 32 * W
     job_gbs = value * job_bytes / 1e9

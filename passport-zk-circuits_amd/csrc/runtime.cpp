@@ -634,7 +634,13 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
                    uint64_t* bytes_per_witness) {
   if (!I || phase >= PH_COUNT) return fail(PZK_E_ARG, "bad phase");
   if (name) *name = PHASE_NAMES[phase];
-  if (kernel) *kernel = PHASE_KERNELS[phase];
+  if (kernel) {
+    *kernel = PHASE_KERNELS[phase];
+    if (phase == PH_EMIT_SHA) {  // the SHA-2 and SHA-1 emitters share the phase: name the ones this instance runs
+      const bool s2 = !I->lay.work[E_SHA].empty() || !I->lay.work[E_SHAD].empty(), s1 = !I->lay.work[E_SHA1].empty();
+      *kernel = s1 ? (s2 ? "k_emit_sha+k_emit_sha1" : "k_emit_sha1") : "k_emit_sha";
+    }
+  }
   if (bytes_per_witness) {
     // ALGORITHMIC HBM bytes per witness: every witness element the phase writes (32 B) + the
     // unique bytes it must read (input elements copied, core state it expands)
@@ -645,6 +651,8 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       b += 32ull * r.len;
       if (r.kind == RK_SHA_OWN) b += 32ull * 512 * r.a[1] * (r.a[3] ? 2 : 1);  // message bits copied
       if (r.kind == RK_SHA_BLOCK) b += 4ull * SHA_BLOCK_CORE;
+      if (r.kind == RK_SHA1_OWN) b += 32ull * 512 * r.a[1];  // message bits copied
+      if (r.kind == RK_SHA1_BLOCK) b += 4ull * SHA1_BLOCK_CORE;
       if (r.kind == RK_INCOPY) b += 32ull * r.len;
       if (r.kind == RK_POSEIDON) b += 32ull * pos_core_len(r.a[1] + 1);
       if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);

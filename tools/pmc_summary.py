@@ -1,7 +1,7 @@
 """Per-kernel PMC summary (last dispatch of each kernel) from rocprofv3 counter_collection CSVs.
 
 usage: pmc_summary.py DIR_PREFIX   (reads DIR_PREFIX_sq, _rd, _wr)
-       pmc_summary.py DIR_PREFIX --json BATCH OUT.json
+       pmc_summary.py DIR_PREFIX --json BATCH OUT.json [WORKLOAD]   (WORKLOAD: bench.py's config.workload)
 FETCH_SIZE is doubled (gfx950 reports half the bytes of wide streaming reads; MI355X_MICROARCH.md
 HBM section); FETCH_SIZE / WRITE_SIZE are in KB."""
 import csv
@@ -45,15 +45,15 @@ def main(prefix):
               f"{(rgb + wgb) / ms if ms else 0:10.1f}")
 
 
-def traffic_json(prefix, batch, out_path):
+def traffic_json(prefix, batch, out_path, workload=None):
     """Per-kernel HBM traffic per witness (FETCH_SIZE x 2 + WRITE_SIZE, bytes) for bench.py's
     roofline.traffic; batch = witnesses per launch of the profiled run."""
     import json
     def sums(path):
         tot, calls = defaultdict(lambda: defaultdict(float)), defaultdict(int)
         for r in csv.DictReader(open(path)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pzk::", "")
-            k = k.split("<")[0]
+            # bare kernel name: no return type, template arguments or namespaces (pzk::ec_c1::k_...)
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
             tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
             calls[(k, r["Dispatch_Id"])] = 1
         return tot
@@ -70,11 +70,11 @@ def traffic_json(prefix, batch, out_path):
         w = wr.get(k, {}).get("WRITE_SIZE", 0) * 1024 / n_batches
         res[k] = {"fetch_bytes_per_witness": round(f / batch), "write_bytes_per_witness": round(w / batch),
                   "traffic_bytes_per_witness": round((f + w) / batch)}
-    json.dump({"source": prefix, "batch": batch, "kernels": res}, open(out_path, "w"), indent=1)
+    json.dump({"source": prefix, "batch": batch, "workload": workload, "kernels": res}, open(out_path, "w"), indent=1)
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 3 and sys.argv[2] == "--json":
-        traffic_json(sys.argv[1], int(sys.argv[3]), sys.argv[4])
+        traffic_json(sys.argv[1], int(sys.argv[3]), sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None)
     else:
         main(sys.argv[1])

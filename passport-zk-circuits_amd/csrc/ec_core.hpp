@@ -861,7 +861,24 @@ __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work,
   __syncthreads();
   const uint32_t* prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
   uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
-  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = ect_value(tab, prog[h >> 1], h & 1);
+  // ECT_U descriptors are loaded before the ECT_U stores that use them: a global load issued
+  // after a store waits for it (gfx9 vmcnt counts both), which would put every element's store
+  // latency in series under the saturated write path. Two lanes per element, 1 KiB per wave store.
+  constexpr int ECT_U = 8;
+  const uint32_t tot = 2 * wk.count;
+  for (uint32_t base = threadIdx.x; base < tot; base += ECT_U * blockDim.x) {
+    uint32_t d[ECT_U];
+#pragma unroll
+    for (int k = 0; k < ECT_U; k++) {
+      const uint32_t h = base + k * blockDim.x;
+      d[k] = h < tot ? prog[h >> 1] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < ECT_U; k++) {
+      const uint32_t h = base + k * blockDim.x;
+      if (h < tot) out[h] = ect_value(tab, d[k], h & 1);
+    }
+  }
 }
 
 }  // namespace PZK_EC_NS

@@ -143,11 +143,24 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     // Two lanes per element (16 B each), so every wave store is 1 KiB contiguous: the element
     // is cheap enough to evaluate twice, and this store shape writes ~19 % faster than 32 B per
     // lane (emit_run stages through LDS for the emitters whose elements are expensive).
+    // SHA_U descriptors are loaded before the SHA_U stores that use them (a global load issued
+    // after a store waits for it: gfx9 vmcnt counts both)
     const uint32_t* prog = L.sha_prog + wk.start;
-    for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) {
-      const uint32_t d = prog[h >> 1];
-      const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d, wt[d & 2047]);
-      reinterpret_cast<uint4*>(out)[h] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+    constexpr int SHA_U = 8;
+    const uint32_t tot = 2 * wk.count;
+    for (uint32_t base = threadIdx.x; base < tot; base += SHA_U * blockDim.x) {
+      uint32_t d[SHA_U];
+#pragma unroll
+      for (int k = 0; k < SHA_U; k++) {
+        const uint32_t h = base + k * blockDim.x;
+        d[k] = h < tot ? prog[h >> 1] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < SHA_U; k++) {
+        const uint32_t h = base + k * blockDim.x;
+        const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d[k], wt[d[k] & 2047]);
+        if (h < tot) reinterpret_cast<uint4*>(out)[h] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+      }
     }
   } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)
     const int Bn = R.a[1];

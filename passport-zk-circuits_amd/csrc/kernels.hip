@@ -100,6 +100,7 @@ __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t*
   return ((O == 224 ? SHA224_IV[s >> 5] : SHA_IV[s >> 5]) >> (s & 31)) & 1;
 }
 
+template <int SHA_U>  // descriptors loaded ahead of their stores (see stage 2)
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
                                                           const uint8_t* derived, const uint32_t* sha_core,
                                                           uint8_t* wtns, size_t stride, int wit_major) {
@@ -146,7 +147,6 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     // SHA_U descriptors are loaded before the SHA_U stores that use them (a global load issued
     // after a store waits for it: gfx9 vmcnt counts both)
     const uint32_t* prog = L.sha_prog + wk.start;
-    constexpr int SHA_U = 8;
     const uint32_t tot = 2 * wk.count;
     for (uint32_t base = threadIdx.x; base < tot; base += SHA_U * blockDim.x) {
       uint32_t d[SHA_U];
@@ -461,9 +461,13 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
     case E_SHA: case E_SHAD:  // witness-major grid (see k_emit_sha)
-      hipLaunchKernelGGL(k_emit_sha, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
+    {  // PZK_SHA_U (8 / 16 / 32): prefetch depth, for tuning runs
+      static const int u = getenv("PZK_SHA_U") ? atoi(getenv("PZK_SHA_U")) : 16;
+      auto kern = u == 8 ? k_emit_sha<8> : u == 32 ? k_emit_sha<32> : k_emit_sha<16>;
+      hipLaunchKernelGGL(kern, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
                          B.stride, 1);
       break;
+    }
     case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
       switch (max_t) {
         case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;

@@ -11,7 +11,9 @@
  *
  * Conventions: plain pointers and sizes; every function returns 0 on success or a negative
  * PZK_E_* code, with a message in pzk_last_error() (thread-local). Caller owns all input and
- * output buffers; the instance owns its device scratch. One in-flight call per instance.
+ * output buffers; the instance owns its device scratch. Calls on one instance are serialised by an
+ * internal mutex (concurrent callers wait); every call runs on the instance's device, whatever the
+ * calling thread's current device (which is restored on return).
  * Field elements are 32 bytes, little-endian, NORMAL form (< p), as in a .wtns file.
  */
 #ifndef PZKWIT_H
@@ -59,9 +61,11 @@ typedef struct pzk_info {
 } pzk_info;
 
 typedef struct pzk_exec {
-  int32_t device;   /* HIP device ordinal */
+  int32_t device;   /* HIP device ordinal: must be the instance's device, or < 0 for "the instance's" */
   int32_t flags;    /* PZK_EXEC_* */
-  void* stream;     /* hipStream_t to launch on (NULL = the instance's own stream) */
+  void* stream;     /* hipStream_t the call is ordered after and joined into at exit (serialises calls);
+                       NULL = the instance's own streams, pipelined across calls: complete after
+                       pzk_instance_sync() (or PZK_EXEC_SYNC / a device-wide synchronise) */
 } pzk_exec;
 
 enum {
@@ -129,9 +133,15 @@ int pzk_wtns_header(const pzk_instance* inst, uint8_t header[76]);
  *   d_wtns   : batch x witness_size x 32 B elements, row stride wtns_stride bytes (>= 32*witness_size,
  *              multiple of 16), device pointer
  *   d_status : batch x int32 lane status (PZK_ST_*), device pointer (may be NULL)
+ * The buffers must stay untouched until the call has completed (see pzk_exec.stream). With a NULL
+ * stream consecutive calls overlap: call k + 1's cores run beside call k's emitters (two scratch
+ * sets); call k + 2 starts after call k has completed.
  * Replaces: for (input of inputs) await wc.calculateWitness(input) (automatisationTest.js:24-50). */
 int pzk_witness_batch(pzk_instance* inst, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns,
                       size_t wtns_stride, int32_t* d_status, const pzk_exec* exec);
+
+/* Wait until every call issued on the instance so far has completed (all instance streams). */
+int pzk_instance_sync(pzk_instance* inst);
 
 /* Host-buffer convenience (copies in/out; used by the single-input calculateWitness path). */
 int pzk_witness_batch_host(pzk_instance* inst, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,

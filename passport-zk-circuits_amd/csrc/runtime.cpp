@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -96,18 +97,38 @@ struct PhaseScope {
   }
 };
 
+// per-witness core state of one batch (one set per pipeline slot)
+struct Scratch {
+  size_t cap = 0;
+  uint32_t* d_sha_core = nullptr;
+  fr* d_pos_core = nullptr;
+  fr* d_values = nullptr;
+  uint64_t* d_rsa_core = nullptr;
+  uint64_t* d_rsa_colsum = nullptr;  // RSA x*y column sums, SoA [(3 i + c)][witness]
+  fr *d_bjj_core = nullptr, *d_bjj_scratch = nullptr, *d_smt_core = nullptr;
+  uint64_t *d_ec_core = nullptr, *d_ec_jac = nullptr;
+  fr* d_ec_inv = nullptr;
+  uint8_t* d_ec_tab = nullptr;
+  uint8_t* d_derived = nullptr;  // RSA-PSS derived SHA messages
+  void free_all() {
+    void* ptrs[] = {d_sha_core, d_pos_core, d_values, d_rsa_core, d_rsa_colsum, d_bjj_core, d_bjj_scratch,
+                    d_smt_core, d_ec_core, d_ec_jac, d_ec_inv, d_ec_tab, d_derived};
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+    *this = Scratch();
+  }
+};
+
 struct pzk_instance {
   pzk_params params;
   Timing timing;
   Layout lay;
   int device = 0;
   hipStream_t stream = nullptr;
-  // side streams of the register pipeline (RSA core + emission; SHA + BJJ emission).
-  // Three streams in all: with the null stream they fit the 4 hardware queues HIP maps
-  // streams onto by default, so no two of them share a queue.
+  // side streams of the register pipeline (signature core; SHA emitters; other emitters, s_emit
+  // below): four streams in all, one per hardware queue (GPU_MAX_HW_QUEUES = 4)
   hipStream_t s_rsa = nullptr, s_sha = nullptr;
-  hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_j_rsa = nullptr,
-             ev_j_bjj = nullptr, ev_entry = nullptr, ev_exit = nullptr;
+  hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_entry = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
   Work* d_work[E_COUNT] = {};
@@ -127,18 +148,15 @@ struct pzk_instance {
   fr* d_inv_small = nullptr;
   PosParamIndex pix{};
   int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
-  // per-batch scratch, grown on demand
-  size_t cap = 0;
-  uint32_t* d_sha_core = nullptr;
-  fr* d_pos_core = nullptr;
-  fr* d_values = nullptr;
-  uint64_t* d_rsa_core = nullptr;
-  uint64_t* d_rsa_colsum = nullptr;  // RSA x*y column sums, SoA [(3 i + c)][witness]
-  fr *d_bjj_core = nullptr, *d_bjj_scratch = nullptr, *d_smt_core = nullptr;
-  uint64_t *d_ec_core = nullptr, *d_ec_jac = nullptr;
-  fr* d_ec_inv = nullptr;
-  uint8_t* d_ec_tab = nullptr;
-  uint8_t* d_derived = nullptr;  // RSA-PSS derived SHA messages
+  // per-batch scratch, grown on demand; two sets, alternating per call, so that call k + 1's
+  // cores can run while call k's emitters still read set k % 2
+  Scratch scr[2];
+  uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
+  // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit)
+  hipEvent_t ev_done[2][4] = {};
+  hipStream_t s_emit = nullptr;
+  hipEvent_t ev_pos = nullptr, ev_tab = nullptr;
+  std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
   // staging for the host-buffer path
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -247,16 +265,7 @@ static int upload(T** dst, const std::vector<T>& v) {
 }
 
 static void free_scratch(pzk_instance* I) {
-  void* ptrs[] = {I->d_sha_core, I->d_pos_core, I->d_values, I->d_rsa_core, I->d_rsa_colsum, I->d_bjj_core,
-                  I->d_bjj_scratch, I->d_smt_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, I->d_ec_tab,
-                  I->d_derived};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-  I->d_sha_core = nullptr; I->d_pos_core = nullptr; I->d_values = nullptr; I->d_rsa_core = nullptr; I->d_rsa_colsum = nullptr;
-  I->d_bjj_core = nullptr; I->d_bjj_scratch = nullptr; I->d_smt_core = nullptr;
-  I->d_ec_core = nullptr; I->d_ec_jac = nullptr; I->d_ec_inv = nullptr; I->d_ec_tab = nullptr;
-  I->d_derived = nullptr;
-  I->cap = 0;
+  for (Scratch& s : I->scr) s.free_all();
 }
 
 static void free_all(pzk_instance* I) {
@@ -268,10 +277,13 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit})
     if (s) (void)hipStreamDestroy(s);
-  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_j_rsa, I->ev_j_bjj, I->ev_entry, I->ev_exit})
+  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_pos, I->ev_tab})
     if (e) (void)hipEventDestroy(e);
+  for (auto& set : I->ev_done)
+    for (hipEvent_t e : set)
+      if (e) (void)hipEventDestroy(e);
   I->timing.destroy();
 }
 
@@ -282,6 +294,10 @@ const char* pzk_version(void) { return "pzkwit 0.2.0 (gfx950)"; }
 
 int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   if (!params || !out) return fail(PZK_E_ARG, "null argument");
+  if (const char* u = getenv("PZK_SHA_U")) {  // tuning switch of the SHA emitter (kernels.hip)
+    int v = atoi(u);
+    if (v != 8 && v != 16 && v != 32) return fail(PZK_E_ARG, std::string("PZK_SHA_U=") + u + ": valid values are 8, 16, 32");
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(PZK_E_NODEVICE, "no HIP device visible: pzkwit has no CPU fallback");
@@ -332,10 +348,16 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess;
-  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_j_rsa, &I->ev_j_bjj, &I->ev_entry,
-                        &I->ev_exit})
+            hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
+  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_pos, &I->ev_tab})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  for (auto& set : I->ev_done)
+    for (hipEvent_t& e : set) {
+      ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+      // recorded once on the null stream, so the first two calls' waits are satisfied
+      ok = ok && hipEventRecord(e, nullptr) == hipSuccess;
+    }
   if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
   *out = I;
   return 0;
@@ -408,46 +430,77 @@ int pzk_wtns_header(const pzk_instance* I, uint8_t h[76]) {
   return 0;
 }
 
-static int ensure_scratch(pzk_instance* I, size_t batch) {
-  if (batch <= I->cap) return 0;
-  free_scratch(I);
+static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
+  if (batch <= S.cap) return 0;
+  S.free_all();
   const Layout& L = I->lay;
   struct { void** p; size_t bytes; } req[] = {
-      {(void**)&I->d_sha_core, 4ull * L.sha_core_words * batch},
-      {(void**)&I->d_pos_core, 32ull * L.pos_core_elems * batch},
-      {(void**)&I->d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
-      {(void**)&I->d_rsa_core, 8ull * L.rsa_core_words * batch},
-      {(void**)&I->d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
-      {(void**)&I->d_bjj_core, 32ull * L.bjj_core_fr * batch},
-      {(void**)&I->d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
-      {(void**)&I->d_smt_core, 32ull * L.smt_core_fr * batch},
-      {(void**)&I->d_ec_core, L.is_ecdsa ? 8ull * EC_CORE_WORDS * batch : 0},
-      {(void**)&I->d_ec_jac, L.is_ecdsa ? 8ull * EC_JAC_WORDS * batch : 0},
-      {(void**)&I->d_ec_inv, L.is_ecdsa ? 32ull * EC_N_INV * batch : 0},
-      {(void**)&I->d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
-      {(void**)&I->d_derived, 32ull * L.n_derived * batch},
+      {(void**)&S.d_sha_core, 4ull * L.sha_core_words * batch},
+      {(void**)&S.d_pos_core, 32ull * L.pos_core_elems * batch},
+      {(void**)&S.d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
+      {(void**)&S.d_rsa_core, 8ull * L.rsa_core_words * batch},
+      {(void**)&S.d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
+      {(void**)&S.d_bjj_core, 32ull * L.bjj_core_fr * batch},
+      {(void**)&S.d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
+      {(void**)&S.d_smt_core, 32ull * L.smt_core_fr * batch},
+      {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_CORE_WORDS * batch : 0},
+      {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_JAC_WORDS * batch : 0},
+      {(void**)&S.d_ec_inv, L.is_ecdsa ? 32ull * EC_N_INV * batch : 0},
+      {(void**)&S.d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
+      {(void**)&S.d_derived, 32ull * L.n_derived * batch},
   };
   for (auto& r : req)
     if (r.bytes && hipMalloc(r.p, r.bytes) != hipSuccess) {
-      free_scratch(I);
+      S.free_all();
       return fail(PZK_E_NOMEM, "device scratch allocation failed");
     }
-  I->cap = batch;
+  S.cap = batch;
   return 0;
 }
 
-int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
-                      int32_t* d_status, const pzk_exec* exec) {
-  if (!I || !d_inputs || !d_wtns) return fail(PZK_E_ARG, "null argument");
-  if (batch == 0) return 0;
-  if (batch > 65535) return fail(PZK_E_ARG, "batch > 65535: split it");
-  if (stride < 32ull * I->lay.wit_size || stride % 16) return fail(PZK_E_ARG, "bad witness stride");
-  if (exec && exec->device != I->device) HIPCHK(hipSetDevice(exec->device));
-  int rc = ensure_scratch(I, batch);
+// The caller's current device is switched to the instance's for the duration of a call and
+// restored on return (every stream, event and buffer of an instance lives on its device).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
+  if (exec && exec->device >= 0 && exec->device != I->device)
+    return fail(PZK_E_ARG, "pzk_exec.device " + std::to_string(exec->device) + " != the instance's device " +
+                               std::to_string(I->device) + " (create one instance per device)");
+  return 0;
+}
+
+// wait until every stream of the instance has drained (all calls issued so far are complete)
+static int sync_all(pzk_instance* I) {
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit}) HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// One call, with the instance lock held and the device set.
+//
+// Pipelining: call k uses scratch set k % 2 and four instance streams — main (the
+// Poseidon/SMT/BabyJubJub chain), rsa (the signature core), sha (the SHA emitters) and emit (the other
+// emitters). Streams are not joined at the end of a call: call k + 1's cores start while call k's
+// emitters still run. Before touching set k % 2 again, call k + 2 waits for the end of call k on all
+// four streams (ev_done). With a caller stream the call is joined into it at exit (serialised).
+static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
+                        int32_t* d_status, const pzk_exec* exec) {
+  const int set = (int)(I->calls & 1);
+  Scratch& S = I->scr[set];
+  int rc = ensure_scratch(I, S, batch);
   if (rc) return rc;
-  // all work runs on the instance's streams; a caller stream is joined at entry and exit
+  I->calls++;
   hipStream_t user = (exec && exec->stream) ? (hipStream_t)exec->stream : nullptr;
   hipStream_t st = I->stream;
+  for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(st, e, 0));
   if (user) {
     HIPCHK(hipEventRecord(I->ev_entry, user));
     HIPCHK(hipStreamWaitEvent(st, I->ev_entry, 0));
@@ -455,10 +508,10 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   const uint32_t B = (uint32_t)batch;
   const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
-  ValueStore vs{I->d_values, B};
+  ValueStore vs{S.d_values, B};
   PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix};
-  Bufs bufs{d_inputs, I->d_sha_core, I->d_rsa_core, I->d_pos_core, I->d_bjj_core, I->d_smt_core, vs, d_wtns, stride,
-            d_status, I->d_ec_core, I->d_ec_inv, I->d_ec_tab, I->d_inv_small, I->d_derived};
+  Bufs bufs{d_inputs, S.d_sha_core, S.d_rsa_core, S.d_pos_core, S.d_bjj_core, S.d_smt_core, vs, d_wtns, stride,
+            d_status, S.d_ec_core, S.d_ec_inv, S.d_ec_tab, I->d_inv_small, S.d_derived};
   Timing* T = nullptr;
   int slot = 0;
   if (exec && (exec->flags & PZK_EXEC_TIMING)) {
@@ -471,8 +524,8 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   auto pos_levels = [&](int lo, int hi) -> int {
     for (int l = lo; l < hi && l + 1 < (int)lay.pos_level_start.size(); l++) {
       uint32_t a = lay.pos_level_start[l], b = lay.pos_level_start[l + 1];
-      HIPCHK(launch_pos_core(K, I->d_pos, lay.pos.data(), a, b - a, vs, I->d_pos_core, lay.pos_core_elems,
-                             I->d_smt_core, lay.smt_core_fr, st));
+      HIPCHK(launch_pos_core(K, I->d_pos, lay.pos.data(), a, b - a, vs, S.d_pos_core, lay.pos_core_elems,
+                             S.d_smt_core, lay.smt_core_fr, st));
     }
     return 0;
   };
@@ -486,112 +539,152 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
     }
     return 0;
   };
+  // PZK_SERIAL=1 (profiling): every phase on the main stream, so kernel times are standalone
+  static const bool serial = getenv("PZK_SERIAL") != nullptr;
+  hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha, s_emit = serial ? st : I->s_emit;
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
-    HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, I->d_values, B, st)); }
+    HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, S.d_values, B, st)); }
   if (!lay.is_register) {
     { PhaseScope ps(T, slot, PH_SHA_CORE, st);
-      HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, 0, L.n_sha, I->d_sha_core, d_status, B, st)); }
+      HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, 0, L.n_sha, S.d_sha_core, d_status, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
     for (int e = 0; e < E_COUNT; e++)
       if ((rc = emit(e, st))) return rc;
+    s_rsa = s_sha = s_emit = st;
   } else {
-    // Three streams (DESIGN.md §4 "Schedule"). The RSA core depends only on the inputs, so it
-    // starts at once on its own (high-priority) stream with the VALU-heavy BigMultModP emitter
-    // behind it, which then overlaps the bandwidth-bound SHA emitter (low-priority stream, with
-    // the BabyJubJub emitter after it); the main
-    // (high-priority) stream runs the Poseidon/SMT dependency chain, the BabyJubJub core and the
-    // remaining emitters, then joins.
-    // PZK_SERIAL=1 (profiling): every phase on the launch stream, so kernel times are standalone
-    static const bool serial = getenv("PZK_SERIAL") != nullptr;
-    hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha;
+    // Four streams. The dependency chains get the high-priority streams: the
+    // signature core (rsa) depends only on the inputs; the Poseidon/SMT/BabyJubJub chain (main)
+    // on the SHA core. The emitters run on the two low-priority streams: the SHA emitters
+    // (bandwidth-bound) on sha, everything else (the VALU-heavy BigMultModP / Poseidon emitters,
+    // the small regions and the checks) on emit.
     HIPCHK(hipEventRecord(I->ev_load, st));
     HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_load, 0));
     const bool pss = lay.reg.pss_s8 != 0;
     const uint32_t n_sha_main = pss ? (uint32_t)lay.reg.j_mgf : (uint32_t)lay.sha.size();
     if (!lay.is_ecdsa) {
-      { PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
-        HIPCHK(launch_rsa_core(L, d_inputs, I->d_rsa_core, I->d_rsa_colsum, d_status, B, s_rsa)); }
-      if (!pss) {
-        HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
-        if ((rc = emit(E_MM, s_rsa))) return rc;  // VALU-heavy: overlaps the bandwidth-bound SHA emitter
-        HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
-      }
+      PhaseScope ps(T, slot, PH_RSA_CORE, s_rsa);
+      HIPCHK(launch_rsa_core(L, d_inputs, S.d_rsa_core, S.d_rsa_colsum, d_status, B, s_rsa));
     }
     { PhaseScope ps(T, slot, PH_SHA_CORE, st);
-      HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, 0, n_sha_main, I->d_sha_core, d_status, B, st)); }
+      HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, 0, n_sha_main, S.d_sha_core, d_status, B, st)); }
     HIPCHK(hipEventRecord(I->ev_sha, st));
     if (pss) {
-      // RSA-PSS chain (pss.hpp) behind the RSA core on s_rsa: MGF1 messages from EM, their hashes,
-      // M' (needs the SA digest), its hash; then the BigMultModP emitter and the derived hashers'
-      // SHA regions. ev_rsa marks the chain's end: the PSS checks and regions read all of it.
+      // RSA-PSS chain (pss.hpp) behind the RSA core: MGF1 messages from EM, their hashes, M' (needs
+      // the SA digest), its hash. ev_rsa marks the chain's end: the PSS checks and regions read all of it.
       HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_sha, 0));
-      { PhaseScope ps(T, slot, PH_PSS, s_rsa);
-        HIPCHK(launch_pss(L, 0, I->d_rsa_core, I->d_sha_core, I->d_derived, B, s_rsa));
-        HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, (uint32_t)lay.reg.j_mgf, (uint32_t)lay.reg.n_mgf,
-                               I->d_sha_core, d_status, B, s_rsa));
-        HIPCHK(launch_pss(L, 1, I->d_rsa_core, I->d_sha_core, I->d_derived, B, s_rsa));
-        HIPCHK(launch_sha_core(L, d_inputs, I->d_derived, (uint32_t)lay.reg.j_hd, 1, I->d_sha_core, d_status, B,
-                               s_rsa)); }
-      HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
-      if ((rc = emit(E_MM, s_rsa))) return rc;
-      if ((rc = emit(E_SHAD, s_rsa))) return rc;
-      HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+      PhaseScope ps(T, slot, PH_PSS, s_rsa);
+      HIPCHK(launch_pss(L, 0, S.d_rsa_core, S.d_sha_core, S.d_derived, B, s_rsa));
+      HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, (uint32_t)lay.reg.j_mgf, (uint32_t)lay.reg.n_mgf,
+                             S.d_sha_core, d_status, B, s_rsa));
+      HIPCHK(launch_pss(L, 1, S.d_rsa_core, S.d_sha_core, S.d_derived, B, s_rsa));
+      HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, (uint32_t)lay.reg.j_hd, 1, S.d_sha_core, d_status, B,
+                             s_rsa));
     }
     if (lay.is_ecdsa) {
-      // ECDSA chain (needs the SA digest): EC core, value tables, table-block emission on s_rsa
+      // ECDSA chain (needs the SA digest): EC core, then the value tables of the table ops
       HIPCHK(hipStreamWaitEvent(s_rsa, I->ev_sha, 0));
       { PhaseScope ps(T, slot, PH_EC_CORE, s_rsa);
-        HIPCHK(launch_ec_core(L, d_inputs, I->d_sha_core, I->d_ec_core, I->d_ec_jac, I->d_ec_inv, d_status, B, s_rsa)); }
-      HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+        HIPCHK(launch_ec_core(L, d_inputs, S.d_sha_core, S.d_ec_core, S.d_ec_jac, S.d_ec_inv, d_status, B, s_rsa)); }
+    }
+    HIPCHK(hipEventRecord(I->ev_rsa, s_rsa));
+    if (lay.is_ecdsa) {
       { PhaseScope ps(T, slot, PH_EC_TABLE, s_rsa);
         for (int t = 0; t < 3; t++)
-          HIPCHK(launch_ec_table(L, t, I->d_ec_ops[t], (uint32_t)lay.ec_ops[t].size(), I->d_ec_core, I->d_ec_tab,
+          HIPCHK(launch_ec_table(L, t, I->d_ec_ops[t], (uint32_t)lay.ec_ops[t].size(), S.d_ec_core, S.d_ec_tab,
                                  d_status, B, s_rsa)); }
-      if ((rc = emit(E_ECT, s_rsa))) return rc;
-      HIPCHK(hipEventRecord(I->ev_j_rsa, s_rsa));
+      HIPCHK(hipEventRecord(I->ev_tab, s_rsa));
     }
+    // SHA emitters (all hashers of the main SHA core)
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
     if ((rc = emit(E_SHA1, s_sha))) return rc;  // SHA-1 hashers (SIGNATURE_TYPE 3, DG_HASH_TYPE 160)
-    { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, I->d_sha_core, vs, d_status, st)); }
+    // signature emitters: BigMultModP blocks / EC table blocks, PSS derived hashers
+    HIPCHK(hipStreamWaitEvent(s_emit, I->ev_rsa, 0));
+    if ((rc = emit(E_MM, s_emit))) return rc;
+    if ((rc = emit(E_SHAD, s_emit))) return rc;
+    if (lay.is_ecdsa) {
+      HIPCHK(hipStreamWaitEvent(s_emit, I->ev_tab, 0));
+      if ((rc = emit(E_ECT, s_emit))) return rc;
+    }
+    // main chain
+    { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, S.d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
-    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, I->d_smt_core, d_status, st)); }
+    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, I->d_pos_core, I->d_smt_core, st)); }
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, st)); }
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
-      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, I->d_bjj_core, I->d_bjj_scratch, st)); }
+      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
     HIPCHK(hipEventRecord(I->ev_bjj, st));
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
+    HIPCHK(hipEventRecord(I->ev_pos, st));
+    // BabyJubJub emitter behind the SHA emitters, then the chain's tail emitters (Poseidon blocks,
+    // small regions, flow, checks) on the stream that finishes first per sub-batch: behind the SHA
+    // emitters by default (the BigMultModP emitter is the longer one), PZK_TAIL=emit for the other
+    static const bool tail_on_emit = getenv("PZK_TAIL") && !strcmp(getenv("PZK_TAIL"), "emit");
+    hipStream_t s_tail = tail_on_emit ? s_emit : s_sha;
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_sha))) return rc;
-    HIPCHK(hipEventRecord(I->ev_j_bjj, s_sha));
-    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
-    if ((rc = emit(E_POS, st))) return rc;
-    if ((rc = emit(E_GEN, st))) return rc;
-    if ((rc = emit(E_FLOW, st))) return rc;
-    HIPCHK(hipStreamWaitEvent(st, I->ev_rsa, 0));
+    HIPCHK(hipStreamWaitEvent(s_tail, I->ev_pos, 0));
+    HIPCHK(hipStreamWaitEvent(s_tail, I->ev_rsa, 0));
+    if ((rc = emit(E_POS, s_tail))) return rc;
+    if ((rc = emit(E_GEN, s_tail))) return rc;
+    if ((rc = emit(E_FLOW, s_tail))) return rc;
     if (!lay.is_ecdsa) {
-      PhaseScope ps(T, slot, PH_PREP, st);
-      HIPCHK(launch_rsa_check(L, d_inputs, I->d_sha_core, I->d_rsa_core, d_status, B, st));
+      PhaseScope ps(T, slot, PH_PREP, s_tail);
+      HIPCHK(launch_rsa_check(L, d_inputs, S.d_sha_core, S.d_rsa_core, d_status, B, s_tail));
     }
-    if ((rc = emit(E_BITS, st))) return rc;
-    if ((rc = emit(E_GENR, st))) return rc;
-    for (hipEvent_t e : {I->ev_j_rsa, I->ev_j_bjj}) HIPCHK(hipStreamWaitEvent(st, e, 0));
+    if ((rc = emit(E_BITS, s_tail))) return rc;
+    if ((rc = emit(E_GENR, s_tail))) return rc;
   }
+  hipStream_t streams[4] = {st, s_rsa, s_sha, s_emit};
+  for (int i = 0; i < 4; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
-    HIPCHK(hipEventRecord(I->ev_exit, st));
-    HIPCHK(hipStreamWaitEvent(user, I->ev_exit, 0));
+    for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));
   }
-  if (exec && (exec->flags & PZK_EXEC_SYNC)) HIPCHK(hipStreamSynchronize(user ? user : st));
+  if (exec && (exec->flags & PZK_EXEC_SYNC)) {
+    if (user) HIPCHK(hipStreamSynchronize(user));
+    else if ((rc = sync_all(I))) return rc;
+  }
   return 0;
+}
+
+int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
+                      int32_t* d_status, const pzk_exec* exec) {
+  if (!I || !d_inputs || !d_wtns) return fail(PZK_E_ARG, "null argument");
+  if (batch == 0) return 0;
+  if (batch > 65535) return fail(PZK_E_ARG, "batch > 65535: split it");
+  if (stride < 32ull * I->lay.wit_size || stride % 16) return fail(PZK_E_ARG, "bad witness stride");
+  int rc = check_exec_device(I, exec);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(I->mu);
+  DeviceGuard dg(I->device);
+  if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
+  return batch_locked(I, d_inputs, batch, d_wtns, stride, d_status, exec);
+}
+
+int pzk_instance_sync(pzk_instance* I) {
+  if (!I) return fail(PZK_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lock(I->mu);
+  DeviceGuard dg(I->device);
+  if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
+  return sync_all(I);
 }
 
 int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
                            int32_t* h_status, const pzk_exec* exec) {
   if (!I || !h_inputs || !h_wtns) return fail(PZK_E_ARG, "null argument");
   if (batch == 0) return 0;
+  if (batch > 65535) return fail(PZK_E_ARG, "batch > 65535: split it");
+  int rc = check_exec_device(I, exec);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(I->mu);
+  DeviceGuard dg(I->device);
+  if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
   size_t in_bytes = 32ull * I->lay.n_inputs * batch, out_bytes = 32ull * I->lay.wit_size * batch;
+  // the staging buffers may still be read/written by an earlier device call: drain before reuse
+  if ((rc = sync_all(I))) return rc;
   if (batch > I->host_cap) {
     if (I->d_in) (void)hipFree(I->d_in);
     if (I->d_out) (void)hipFree(I->d_out);
@@ -602,14 +695,13 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
     HIPCHK(hipMalloc(&I->d_status, 4 * batch));
     I->host_cap = batch;
   }
-  hipStream_t st = (exec && exec->stream) ? (hipStream_t)exec->stream : I->stream;
+  hipStream_t st = I->stream;
   HIPCHK(hipMemcpyAsync(I->d_in, h_inputs, in_bytes, hipMemcpyHostToDevice, st));
-  pzk_exec ex{I->device, 0, st};
-  int rc = pzk_witness_batch(I, I->d_in, batch, I->d_out, 32ull * I->lay.wit_size, I->d_status, &ex);
-  if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost, st));
-  if (h_status) HIPCHK(hipMemcpyAsync(h_status, I->d_status, 4 * batch, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
+  if ((rc = batch_locked(I, I->d_in, batch, I->d_out, 32ull * I->lay.wit_size, I->d_status, &ex))) return rc;
+  if ((rc = sync_all(I))) return rc;
+  HIPCHK(hipMemcpy(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost));
+  if (h_status) HIPCHK(hipMemcpy(h_status, I->d_status, 4 * batch, hipMemcpyDeviceToHost));
   return 0;
 }
 

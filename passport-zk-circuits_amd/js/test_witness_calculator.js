@@ -37,6 +37,9 @@ async function cpu() {
   assert.throws(() => c.marshal({ a: [1, 2, 3], b: 1 }), /Too many values for input signal a/);
   assert.throws(() => c.marshal({ a: [1, 2] }), /Not all inputs have been set/);
   assert.ok(/Error in template RsaVerifyPkcs1v15 line: 48/.test(wcmod.statusMessage(8)));
+  assert.ok(/Error in template verifyECDSABits line: 81/.test(wcmod.statusMessage(16)));
+  assert.ok(/Error in template VerifyRsaPssSig line: 182/.test(wcmod.statusMessage(18)));
+  assert.strictEqual(wcmod.CIRCUIT.SHA1, 3);
   console.log("js cpu ok");
 }
 
@@ -57,6 +60,12 @@ async function gpu(inPath, outPath) {
   assert.strictEqual(b.status.length, 2);
   assert.ok(Buffer.compare(Buffer.from(b.wtns[0]), Buffer.from(b.wtns[1])) === 0);
   assert.ok(Buffer.compare(Buffer.from(b.wtns[0]), Buffer.from(wtns)) === 0);
+  // concurrent, unawaited calls on one instance (libuv pool threads): serialised inside the
+  // library, each result equal to the serial one
+  const conc = await Promise.all([rc.calculateWTNSBin(input, true), rc.calculateWTNSBinBatch([input, input], true),
+                                  rc.calculateWTNSBin(input, true)]);
+  for (const x of [conc[0], conc[1].wtns[0], conc[1].wtns[1], conc[2]])
+    assert.ok(Buffer.compare(Buffer.from(x), Buffer.from(wtns)) === 0);
   console.log(`js gpu ok (witnessSize ${rc.witnessSize}, ${Date.now() - t0} ms)`);
 }
 

@@ -13,6 +13,15 @@ import numpy as np
 
 from .field import P, SplitMix64, poseidon
 
+def process_pool(workers):
+    """Worker pool for input generation. Spawned, not forked: a fork of a process that has
+    initialised HIP (torch, libpzkwit) hands the children a runtime they cannot use, and the
+    parent's device state must not be touched by them either."""
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    return ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn"))
+
+
 # ----------------------------------------------------------- process_passport.js
 def sha_pad(msg: bytes, block_bits=512) -> bytes:
     """padding() test/process_passport.js:11-91 (0x80, zeros, big-endian bit length)."""
@@ -294,8 +303,7 @@ class PassportGen:
         jobs = [(seed, k, key_bits) if e == 65537 else (seed, k, key_bits, e) for k in range(n_keys)]
         workers = workers or min(16, os.cpu_count() or 1)
         if n_keys >= 8 and workers > 1:
-            from concurrent.futures import ProcessPoolExecutor
-            with ProcessPoolExecutor(min(workers, n_keys)) as ex:
+            with process_pool(min(workers, n_keys)) as ex:
                 self.keys = list(ex.map(_keygen, jobs))
         else:
             self.keys = [_keygen(j) for j in jobs]

@@ -17,7 +17,7 @@ PZK_EXEC_SYNC = 1
 
 # C-ABI entry points declared in include/pzkwit.h (checked by tests/test_capi.py)
 EXPORTS = ("pzk_instance_create", "pzk_instance_destroy", "pzk_instance_info", "pzk_instance_input",
-           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_timing", "pzk_phase_info", "pzk_last_error",
+           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_instance_sync", "pzk_timing", "pzk_phase_info", "pzk_last_error",
            "pzk_version")
 
 STATUS_NAMES = {
@@ -28,7 +28,9 @@ STATUS_NAMES = {
     8: "RsaVerifyPkcs1v15 (rsa.circom:48)", 9: "RsaVerifyPkcs1v15 (rsa.circom:53)",
     10: "RsaVerifyPkcs1v15 (rsa.circom:57)", 11: "BigMultModP (bigInt.circom:245)",
     12: "BigIntIsZero (bigIntComparators.circom:128)", 13: "SMTLevIns (SMTVerifier.circom:54)",
-    14: "BabyjubjubAdd (babyjubjub/curve.circom:98)", 64: "input out of range",
+    14: "BabyjubjubAdd (babyjubjub/curve.circom:98)", 15: "BigModInv (bigInt.circom:364)",
+    16: "verifyECDSABits (ecdsa.circom:81)", 17: "VerifyRsaPssSig (rsaPss.circom:73)",
+    18: "VerifyRsaPssSig (rsaPss.circom:182)", 64: "input out of range",
 }
 
 
@@ -82,6 +84,7 @@ def lib():
                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(PzkExec)]
         L.pzk_witness_batch_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(PzkExec)]
+        L.pzk_instance_sync.argtypes = [ctypes.c_void_p]
         L.pzk_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
         L.pzk_phase_info.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
@@ -155,11 +158,17 @@ class Instance:
         _check(lib().pzk_wtns_header(self._h, h))
         return bytes(h)
 
-    def witness_batch_device(self, d_inputs, batch, d_wtns, stride, d_status=None, stream=None, device=0, sync=False,
+    def witness_batch_device(self, d_inputs, batch, d_wtns, stride, d_status=None, stream=None, device=-1, sync=False,
                              timing=False):
+        """stream=None: pipelined on the instance's streams (complete after sync()); a stream
+        handle: ordered after and joined into it. device -1 = the instance's device."""
         ex = PzkExec(device=device, flags=(PZK_EXEC_SYNC if sync else 0) | (2 if timing else 0), stream=stream)
         _check(lib().pzk_witness_batch(self._h, ctypes.c_void_p(d_inputs), batch, ctypes.c_void_p(d_wtns), stride,
                                        ctypes.c_void_p(d_status) if d_status else None, ctypes.byref(ex)))
+
+    def sync(self):
+        """Wait for every call issued on this instance (pzk_instance_sync)."""
+        _check(lib().pzk_instance_sync(self._h))
 
     def timing(self, reset=False):
         """{phase: (ms accumulated, launches)} from calls made with timing=True (HIP events)."""
@@ -190,7 +199,7 @@ class Instance:
         assert a.shape[1:] == (self.n_inputs, 32), a.shape
         out = np.empty((b, self.witness_size, 32), dtype=np.uint8)
         st = np.zeros(b, dtype=np.int32)
-        ex = PzkExec(device=0, flags=0, stream=None)
+        ex = PzkExec(device=-1, flags=0, stream=None)
         _check(lib().pzk_witness_batch_host(self._h, a.ctypes.data, b, out.ctypes.data, st.ctypes.data,
                                             ctypes.byref(ex)))
         return out, st

@@ -22,8 +22,10 @@ def oracle():
 @pytest.fixture(scope="session", autouse=True)
 def _torch_device_first(request):
     """When GPU tests are selected, torch's HIP runtime takes the device before libpzkwit's does
-    (the order bench.py uses). With the native library first and worker pools forked in between
-    (PassportGen key generation), torch's later lazy init found no device."""
+    (the order bench.py uses). Cause of the round-1 failure this guards against: PassportGen's
+    key-generation pool was FORKED after libpzkwit had initialised HIP, and torch's later lazy init
+    then found no device. The pools are spawned now (pzkwit.inputs.process_pool); the fixture only
+    fixes the init order."""
     if any(item.get_closest_marker("gpu") for item in request.session.items):
         import torch
         if torch.cuda.device_count() > 0:

@@ -50,6 +50,7 @@ def test_config3_fullsize_properties(oracle):
     prm = oracle.register_params(**params)
 
     def run(lo, n):
+        torch.cuda.synchronize()  # the library's streams do not wait for torch's stream
         inst.witness_batch_device(d_in.data_ptr() + lo * NIN * 32, n, d_out.data_ptr(), 32 * W, d_st.data_ptr(),
                                   device=0, sync=True)
         torch.cuda.synchronize()
@@ -79,3 +80,53 @@ def test_config3_fullsize_properties(oracle):
     finally:
         del d_out, d_in
         torch.cuda.empty_cache()
+
+
+def test_pipelined_calls_match_serial_calls():
+    """Calls issued back to back on the instance's own streams overlap (call k + 1's cores beside
+    call k's emitters, alternating scratch sets; pzkwit.h pzk_exec.stream): five unsynchronised
+    calls of ragged sizes into separate outputs give the same rows as one synchronised call each."""
+    import torch
+    params = I.CANONICAL
+    g = I.PassportGen(seed=3, n_keys=4, params=params, workers=1)
+    rows = np.stack([I.pack_register_inputs(g.passport_at(i, smt_depth=i % 5), params) for i in range(200)])
+    inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params)
+    W, NIN = inst.witness_size, inst.n_inputs
+    dev = torch.device("cuda:0")
+    d_in = torch.from_numpy(rows).to(dev)
+    cuts = [0, 37, 101, 102, 160, 200]
+    d_out = torch.empty((200, 32 * W), dtype=torch.uint8, device=dev)
+    d_st = torch.full((200,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # the library's streams do not wait for torch's stream
+    try:
+        for a, b in zip(cuts, cuts[1:]):
+            inst.witness_batch_device(d_in.data_ptr() + a * NIN * 32, b - a, d_out[a].data_ptr(), 32 * W,
+                                      d_st.data_ptr() + 4 * a)
+        inst.sync()
+        assert (d_st.cpu().numpy() == 0).all()
+        piped = d_out.view(torch.int64).sum(dim=1)
+        d_out.zero_()
+        torch.cuda.synchronize()
+        for a, b in zip(cuts, cuts[1:]):
+            inst.witness_batch_device(d_in.data_ptr() + a * NIN * 32, b - a, d_out[a].data_ptr(), 32 * W,
+                                      d_st.data_ptr() + 4 * a, sync=True)
+        diff = torch.nonzero(d_out.view(torch.int64).sum(dim=1) != piped).flatten().tolist()
+        assert not diff, "rows %s differ between pipelined and serial calls" % diff[:16]
+    finally:
+        del d_out, d_in
+        torch.cuda.empty_cache()
+
+
+def test_exec_device_mismatch_is_rejected():
+    """pzk_exec.device must name the instance's device (pzkwit.h); the caller's current device is
+    left as it was."""
+    import torch
+    inst = native.Instance(native.PZK_CIRCUIT_POSEIDON, 2)
+    dev = torch.device("cuda:0")
+    d_in = torch.zeros((1, inst.n_inputs, 32), dtype=torch.uint8, device=dev)
+    d_out = torch.empty((1, 32 * inst.witness_size), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    with pytest.raises(native.PzkError, match="instance's device"):
+        inst.witness_batch_device(d_in.data_ptr(), 1, d_out.data_ptr(), 32 * inst.witness_size, device=5)
+    inst.witness_batch_device(d_in.data_ptr(), 1, d_out.data_ptr(), 32 * inst.witness_size, device=0, sync=True)
+    assert torch.cuda.current_device() == 0

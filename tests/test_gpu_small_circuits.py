@@ -89,3 +89,40 @@ def test_sha1_circuit_matches_oracle_and_hashlib(oracle, blocks):
         assert rc == 0
         bad = np.nonzero((ref != wit[b]).any(axis=1))[0]
         assert bad.size == 0, "msg %d: %d mismatching signals, first %s" % (b, bad.size, bad[:8].tolist())
+
+
+def test_sha256_config2_fullsize(oracle):
+    """Config 2 at its stated size (BASELINE.json configs[1]): Sha256HashChunks(6),
+    batch 1024, seed 2, on the device-buffer path. All 1024 digests equal hashlib.sha256; rows 0, 1,
+    511, 1023 are bit-exact against the oracle; a re-run reproduces every row's checksum."""
+    import torch
+    n = 1024
+    msgs, rows = inputs.sha256_config2_batch(n, seed=2, blocks=6)
+    inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
+    W, NIN = inst.witness_size, inst.n_inputs
+    assert rows.shape == (n, NIN, 32)
+    dev = torch.device("cuda:0")
+    d_in = torch.from_numpy(rows).to(dev)
+    d_out = torch.empty((n, W * 32), dtype=torch.uint8, device=dev)
+    d_st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # the library's streams do not wait for torch's stream
+    try:
+        inst.witness_batch_device(d_in.data_ptr(), n, d_out.data_ptr(), 32 * W, d_st.data_ptr(), sync=True)
+        assert (d_st.cpu().numpy() == 0).all()
+        bits = d_out.view(n, W, 32)[:, 1:257, 0].cpu().numpy()
+        for b, m in enumerate(msgs):
+            assert np.packbits(bits[b]).tobytes() == hashlib.sha256(m).digest(), b
+        for b in (0, 1, 511, 1023):
+            rc, ref = oracle.sha256_witness(rows[b], 6)
+            assert rc == 0
+            got = d_out[b].view(W, 32).cpu().numpy()
+            bad = np.nonzero((ref != got).any(axis=1))[0]
+            assert bad.size == 0, "msg %d: first mismatching signal %d" % (b, bad[0])
+        sums = d_out.view(torch.int64).sum(dim=1)
+        d_out.zero_()
+        torch.cuda.synchronize()
+        inst.witness_batch_device(d_in.data_ptr(), n, d_out.data_ptr(), 32 * W, d_st.data_ptr(), sync=True)
+        assert bool((d_out.view(torch.int64).sum(dim=1) == sums).all()), "re-run is not deterministic"
+    finally:
+        del d_out, d_in
+        torch.cuda.empty_cache()

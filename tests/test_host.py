@@ -2,6 +2,7 @@
 witness calculator's error semantics, sharding and the multi-process (gloo) result gather."""
 import hashlib
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -123,3 +124,82 @@ def test_mixed_shard_by_cost_balances_bytes():
         share = sum(costs) / world
         for lo, hi in bounds:
             assert abs(sum(costs[lo:hi]) - share) <= max(costs)
+
+
+class _StubInst:
+    """timing / phase_info of a libpzkwit instance, for bench.report without a GPU"""
+
+    def timing(self, reset=False):
+        return {"emit_sha": (2.0, 4)}
+
+    def phase_info(self):
+        return [("emit_sha", "k_emit_sha", 1000)]
+
+
+class _StubEngine:
+    """bench.GpuEngine's interface on the CPU: 'witness' = the row's first 4 input elements, status =
+    bit 0 of the row (config-2 message bits), so the gather's order can be checked."""
+
+    def __init__(self, args, workload, dev):
+        import torch
+        self.torch, self.NIN, self.W, self.n_pub, self.inst = torch, 3072, 3072 + 300, 4, _StubInst()
+
+    def setup(self, d_in, batch, sub, slots, steps):
+        self.rows = d_in.view(batch, self.NIN, 32)
+        self.d_st = self.torch.zeros((steps, batch), dtype=self.torch.int32)
+
+    def step(self, k, timing):
+        self.d_st[k] = self.rows[:, 0, 0].to(self.torch.int32)
+
+    def sync(self):
+        pass
+
+    def statuses(self, steps):
+        return self.d_st[:steps]
+
+    def public_pass(self):
+        return self.rows[:, 0, 0].to(self.torch.int32).clone(), self.rows[:, : self.n_pub].clone()
+
+
+def _bench_rank(rank, world, port, q):
+    import argparse
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = argparse.Namespace(workload="sha256", batch=6, sub=None, slots=1, steps=2, warmup=1, sig_eff=0, no_cpu=True,
+                              gpus=world)
+    r = bench.run_rank(args, rank, world, 0, dist, engine_cls=_StubEngine, device="cpu")
+    if rank == 0:
+        q.put(bench.report(args, r, world))
+    dist.destroy_process_group()
+
+
+def test_bench_two_ranks_gloo_scatter_gather():
+    """bench.run_rank over a 2-rank gloo group with the GPU path stubbed: rank 0 generates the job's
+    inputs and scatters the shards, the ranks' statuses and public rows are gathered in global order,
+    and the record reports n_gpus = 2."""
+    import hashlib
+    import socket
+    import torch.multiprocessing as mp
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if repo not in sys.path:
+        sys.path.insert(0, repo)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = q.get(timeout=180)
+    for p in ps:
+        p.join(60)
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    g = out["config"]["gathered"]
+    _, rows = I.sha256_config2_batch(12, seed=2, blocks=6)
+    assert g["witnesses"] == 12
+    assert g["status_nonzero"] == int((rows[:, 0, 0] != 0).sum())
+    assert g["public_sha256"] == hashlib.sha256(rows[:, :4].tobytes()).hexdigest()[:16]
+    assert out["config"]["invalid_lanes"] == 2 * int((rows[:, 0, 0] != 0).sum())

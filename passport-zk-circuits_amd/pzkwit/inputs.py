@@ -36,6 +36,28 @@ def bits_msb_first(data: bytes):
     return np.unpackbits(np.frombuffer(data, dtype=np.uint8)).astype(np.uint8)
 
 
+def padded_bits(msg: bytes, block_bits=512):
+    """The bit array processPassport builds from padding()'s hex (process_passport.js:701-757):
+    BigInt("0x" + padded).toString(2).split(""), then zeros prepended up to a multiple of the block
+    length. Equal to the MSB-first bits of the padded message except when the padded message starts
+    with a whole block of zero bits: the BigInt round trip drops it (reproduced, not fixed)."""
+    bits = bits_msb_first(sha_pad(msg, block_bits))
+    nz = np.flatnonzero(bits)
+    sig = bits[nz[0]:] if nz.size else bits[:0]
+    total = -(-len(sig) // block_bits) * block_bits if len(sig) % block_bits else len(sig)
+    out = np.zeros(total, dtype=np.uint8)
+    out[total - len(sig):] = sig
+    return out
+
+
+def fake_iden_data(ec: bytes, pk_hash: int):
+    """getFakeIdenData (process_passport.js:628-657): skIdentity = the first 62 hex digits of
+    SHA-256(EC) (as a hex string, leading zeros kept), the one-leaf SMT root Poseidon3(pkHash,
+    pkHash, 1) as bare hex, 80 zero siblings. -> (sk_hex, root_hex, branches)."""
+    sk_hex = hashlib.sha256(ec).hexdigest()[:62]
+    return sk_hex, "%x" % poseidon([pk_hash, pk_hash, 1]), [0] * 80
+
+
 def chunk_limbs(x: int, n=64, k=32):
     """bigintToArrayString(n, k, x) process_passport.js:125-135 (little-endian limbs)."""
     m = (1 << n) - 1
@@ -378,8 +400,9 @@ class PassportGen:
             sig = pkcs1v15_sha1_sign(key, sa)
         else:
             sig = pkcs1v15_sha256_sign(key, sa)
-        sk = int.from_bytes(hashlib.sha256(ec).digest()[:31], "big")  # getFakeIdenData :630
         pkh = self.pk_hash(key)
+        sk_hex, root_hex, _ = fake_iden_data(ec, pkh)  # getFakeIdenData :628-657
+        sk = int(sk_hex, 16)
         siblings = [0] * 80
         if smt_depth:
             for k in range(smt_depth):
@@ -389,7 +412,7 @@ class PassportGen:
                 siblings[k] = v
             root = None  # computed by the caller (config 4); not enforced by the circuit
         else:
-            root = poseidon([pkh, pkh, 1])  # getFakeIdenData :654
+            root = int(root_hex, 16)
         return dict(dg1=dg1, dg15=dg15, ec=ec, sa=sa, sig=sig, n=key.n, sk=sk, root=root,
                     siblings=siblings, pk_hash=pkh)
 
@@ -399,7 +422,7 @@ def passport_json(pp, params=CANONICAL):
     sg = params["sig"]
 
     def bits(b, nbits):
-        arr = bits_msb_first(sha_pad(b, 512))
+        arr = padded_bits(b, 512)
         assert len(arr) == nbits, (len(arr), nbits)
         return [str(int(x)) for x in arr]
 
@@ -410,7 +433,7 @@ def passport_json(pp, params=CANONICAL):
         "encapsulatedContent": bits(pp["ec"], params["ec_blocks"] * 512),
         "pubkey": [str(x) for x in sig_limbs(pp["n"], sg)],
         "signature": [str(x) for x in sig_limbs(pp["sig"], sg)],
-        "skIdentity": hex(pp["sk"]),
+        "skIdentity": "0x%062x" % pp["sk"],  # getFakeIdenData's 62 hex digits, leading zeros kept
         "slaveMerkleRoot": hex(pp["root"] or 0),
         "slaveMerkleInclusionBranches": [str(x) for x in pp["siblings"]],
     }
@@ -434,7 +457,7 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
 
     def put_bits(b, nbits):
         nonlocal o
-        arr = bits_msb_first(sha_pad(b, 512))
+        arr = padded_bits(b, 512)
         if len(arr) != nbits:
             raise ValueError("padded length %d != %d bits" % (len(arr), nbits))
         buf[o:o + nbits, 0] = arr

@@ -1,0 +1,90 @@
+"""ctypes front-end of the constraint checker (oracle/r1cs_check.c).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/ as a checker; the product path never imports
+anything under oracle/."""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libr1cs.so")
+
+
+class Report(ctypes.Structure):
+    _fields_ = [("n_constraints", ctypes.c_uint64), ("n_failed", ctypes.c_uint64),
+                ("n_uncovered", ctypes.c_uint64), ("size_walked", ctypes.c_uint64),
+                ("first_failed", ctypes.c_int64), ("first_line", ctypes.c_int32), ("oob", ctypes.c_int32),
+                ("first_template", ctypes.c_char * 96), ("first_component", ctypes.c_uint64),
+                ("first_uncovered", ctypes.c_int64), ("n_uncovered_nonzero", ctypes.c_uint64)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["first_template"] = self.first_template.decode()
+        return d
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = ctypes.CDLL(LIB)
+        for fn in ("ck_sha256", "ck_poseidon_circuit"):
+            getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
+        L.ck_load_poseidon.argtypes = [ctypes.c_char_p]
+        L.ck_register.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
+        _lib = L
+    return _lib
+
+
+def _run(fn, arg, wit):
+    import numpy as np
+    w = np.ascontiguousarray(wit, dtype=np.uint8)
+    r = Report()
+    rc = getattr(lib(), fn)(arg, w.ctypes.data, w.shape[0], ctypes.byref(r))
+    return rc, r.as_dict()
+
+
+def check_sha256(wit, blocks):
+    """Sha256HashChunks(blocks) as main: (rc, report); rc 0 = every constraint holds and the walk
+    covered exactly the witness."""
+    return _run("ck_sha256", blocks, wit)
+
+
+class CkParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "sig", "dg_hash", "doc", "ec_blocks", "ec_shift", "dg1_shift", "aa",
+        "dg15_shift", "dg15_blocks", "aa_shift")]
+
+
+_pos_loaded = False
+
+
+def _load_poseidon():
+    global _pos_loaded
+    if not _pos_loaded:
+        path = os.path.join(os.path.dirname(HERE), "passport-zk-circuits_amd", "data", "poseidon_t2_6.bin")
+        rc = lib().ck_load_poseidon(path.encode())
+        if rc:
+            raise RuntimeError("r1cs_check: cannot load Poseidon constants (%d)" % rc)
+        _pos_loaded = True
+
+
+def check_poseidon(wit, n):
+    """PoseidonHash(n) as main."""
+    _load_poseidon()
+    return _run("ck_poseidon_circuit", n, wit)
+
+
+def check_register(wit, **params):
+    """RegisterIdentityBuilder(...) as main (short parameter names of pzkwit.inputs.CANONICAL)."""
+    import numpy as np
+    _load_poseidon()
+    p = CkParams(**params)
+    w = np.ascontiguousarray(wit, dtype=np.uint8)
+    r = Report()
+    rc = lib().ck_register(ctypes.byref(p), w.ctypes.data, w.shape[0], ctypes.byref(r))
+    return rc, r.as_dict()

@@ -1,0 +1,1332 @@
+/* oracle/r1cs_check.c — constraint checker for RegisterIdentityBuilder witnesses.
+ *
+ * TEST INFRASTRUCTURE ONLY (like witness_oracle.c): loaded by tests/ as a checker; the shipped
+ * library never links or loads it.
+ *
+ * What it restates: the CONSTRAINTS of every template on the hot path — each `<==` and `===` of
+ * the .circom sources, as the quadratic relation A * B = C (or the linear A = C) it compiles to —
+ * and checks them over a whole witness. This is the acceptance test the reference applies to a
+ * witness (circom_tester's checkConstraints, test/automatisationTest.js:51), restated because the
+ * reference's .r1cs cannot be compiled here. It is written from the templates
+ * independently of the witness oracle: it walks the component tree itself, allocating every
+ * component's signals in the --O0 numbering of DESIGN.md §2 (own outputs, inputs, intermediates in
+ * declaration order, then subcomponents in creation order), and never computes a witness value —
+ * it only evaluates constraints on the values it is given. `<--` assignments are not constraints:
+ * the signals they set (bits, quotients, inverses) are pinned by the constraints that follow them.
+ *
+ * Coverage: every signal a constraint reads is marked; ck_report() returns how many witness
+ * elements no constraint touches (declared-but-unconstrained signals of the templates, listed in
+ * tests/test_r1cs.py).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fr.h"
+
+typedef struct {
+  const fr_t *w;
+  size_t n;
+  uint8_t *cov;
+  uint64_t n_cons, n_bad;
+  int64_t first_bad;        /* index of the first failing constraint (in evaluation order) */
+  const char *first_tmpl;   /* its template and reference file:line */
+  int first_line;
+  size_t first_at;          /* base offset of the component it belongs to */
+  int oob;                  /* a signal index past the witness: allocation mismatch */
+} ck_t;
+
+/* signal read: marks coverage */
+static inline fr_t S(ck_t *c, size_t i) {
+  if (i >= c->n) { c->oob = 1; return fr_zero(); }
+  c->cov[i] = 1;
+  return c->w[i];
+}
+static void req(ck_t *c, fr_t lhs, fr_t rhs, const char *tmpl, int line, size_t at) {
+  if (!fr_eq(lhs, rhs)) {
+    if (!c->n_bad) { c->first_bad = (int64_t)c->n_cons; c->first_tmpl = tmpl; c->first_line = line; c->first_at = at; }
+    c->n_bad++;
+  }
+  c->n_cons++;
+}
+#define EQ(lhs, rhs, T, L) req(c, (lhs), (rhs), T, L, b)
+static inline fr_t KC(uint64_t v) { return fr_u64(v); }
+static inline fr_t ADD(fr_t a, fr_t b) { return fr_add(a, b); }
+static inline fr_t SUB(fr_t a, fr_t b) { return fr_sub(a, b); }
+static inline fr_t MUL(fr_t a, fr_t b) { return fr_mul(a, b); }
+static fr_t P2[256];
+
+/* ============================================================ bitify / comparators */
+static size_t ck_aliascheck(ck_t *c, size_t b);
+
+/* Num2Bits(LEN) bitify.circom:10-32: out[LEN] | in | sum[LEN] | [AliasCheck] */
+static size_t ck_num2bits(ck_t *c, size_t b, int L) {
+  const char *T = "Num2Bits bitify.circom";
+  size_t out = b, in = b + L, sum = b + L + 1;
+  for (int i = 0; i < L; i++) EQ(MUL(S(c, out + i), SUB(S(c, out + i), KC(1))), fr_zero(), T, 18);
+  EQ(MUL(S(c, out), S(c, out)), S(c, sum), T, 21);
+  for (int i = 1; i < L; i++) EQ(ADD(MUL(P2[i], S(c, out + i)), S(c, sum + i - 1)), S(c, sum + i), T, 23);
+  EQ(S(c, in), S(c, sum + L - 1), T, 26);
+  size_t sz = 2 * (size_t)L + 1;
+  if (L == 254) {
+    size_t a = b + sz;  /* aliascheck.in <== out (:30) */
+    for (int i = 0; i < 254; i++) EQ(S(c, a + i), S(c, out + i), T, 30);
+    sz += ck_aliascheck(c, a);
+  }
+  return sz;
+}
+
+/* Bits2Num(LEN) bitify.circom:38-55: out | in[LEN] | sum[LEN] | [AliasCheck] */
+static size_t ck_bits2num(ck_t *c, size_t b, int L) {
+  const char *T = "Bits2Num bitify.circom";
+  size_t out = b, in = b + 1, sum = b + 1 + L;
+  EQ(MUL(S(c, in), S(c, in)), S(c, sum), T, 45);
+  for (int i = 1; i < L; i++) EQ(ADD(MUL(P2[i], S(c, in + i)), S(c, sum + i - 1)), S(c, sum + i), T, 48);
+  EQ(S(c, out), S(c, sum + L - 1), T, 50);
+  size_t sz = 2 * (size_t)L + 1;
+  if (L == 254) {
+    size_t a = b + sz;
+    for (int i = 0; i < 254; i++) EQ(S(c, a + i), S(c, in + i), T, 53);
+    sz += ck_aliascheck(c, a);
+  }
+  return sz;
+}
+
+/* CompConstant(ct) compconstant.circom:7-55: out | in[254] | parts[127] | sout | Num2Bits(135) */
+static size_t ck_compconst(ck_t *c, size_t b, fr_t ct) {
+  const char *T = "CompConstant compconstant.circom";
+  size_t out = b, in = b + 1, parts = b + 255, sout = b + 382, n2b = b + 383;
+  fr_t bb = SUB(P2[128], KC(1)), a = KC(1), e = KC(1), sum = fr_zero();
+  for (int i = 0; i < 127; i++) {
+    int clsb = fr_bit(ct, 2 * i), cmsb = fr_bit(ct, 2 * i + 1);
+    fr_t sl = S(c, in + 2 * i), sm = S(c, in + 2 * i + 1), sms = MUL(sm, sl), rhs;
+    if (!cmsb && !clsb) rhs = ADD(ADD(fr_neg(MUL(bb, sms)), MUL(bb, sm)), MUL(bb, sl));
+    else if (!cmsb && clsb) rhs = ADD(SUB(ADD(SUB(MUL(a, sms), MUL(a, sl)), MUL(bb, sm)), MUL(a, sm)), a);
+    else if (cmsb && !clsb) rhs = ADD(SUB(MUL(bb, sms), MUL(a, sm)), a);
+    else rhs = ADD(fr_neg(MUL(a, sms)), a);
+    EQ(S(c, parts + i), rhs, T, 30);
+    sum = ADD(sum, S(c, parts + i));
+    bb = SUB(bb, e); a = ADD(a, e); e = ADD(e, e);
+  }
+  EQ(S(c, sout), sum, T, 46);
+  EQ(S(c, n2b + 135), S(c, sout), T, 50);
+  EQ(S(c, out), S(c, n2b + 127), T, 52);
+  return 383 + ck_num2bits(c, n2b, 135);
+}
+
+/* AliasCheck aliascheck.circom:7-14: in[254] | CompConstant(-1) */
+static size_t ck_aliascheck(ck_t *c, size_t b) {
+  const char *T = "AliasCheck aliascheck.circom";
+  size_t cc = b + 254;
+  for (int i = 0; i < 254; i++) EQ(S(c, cc + 1 + i), S(c, b + i), T, 12);
+  size_t sz = 254 + ck_compconst(c, cc, fr_neg(KC(1)));
+  EQ(S(c, cc), fr_zero(), T, 14);
+  return sz;
+}
+
+/* IsZero comparators.circom:11-21: out | in | inv */
+static size_t ck_iszero(ck_t *c, size_t b) {
+  const char *T = "IsZero comparators.circom";
+  EQ(S(c, b), ADD(fr_neg(MUL(S(c, b + 1), S(c, b + 2))), KC(1)), T, 19);
+  EQ(MUL(S(c, b + 1), S(c, b)), fr_zero(), T, 20);
+  return 3;
+}
+
+/* IsEqual comparators.circom:24-33: out | in[2] | IsZero */
+static size_t ck_isequal(ck_t *c, size_t b) {
+  const char *T = "IsEqual comparators.circom";
+  size_t z = b + 3;
+  EQ(S(c, z + 1), SUB(S(c, b + 2), S(c, b + 1)), T, 30);
+  ck_iszero(c, z);
+  EQ(S(c, b), S(c, z), T, 32);
+  return 6;
+}
+
+/* LessThan(LEN) comparators.circom:46-57: out | in[2] | Num2Bits(LEN+1) */
+static size_t ck_lessthan(ck_t *c, size_t b, int L) {
+  const char *T = "LessThan comparators.circom";
+  size_t n = b + 3;
+  EQ(S(c, n + L + 1), SUB(ADD(S(c, b + 1), P2[L]), S(c, b + 2)), T, 53);
+  size_t sz = 3 + ck_num2bits(c, n, L + 1);
+  EQ(S(c, b), SUB(KC(1), S(c, n + L)), T, 55);
+  return sz;
+}
+
+/* ============================================================ int/arithmetic.circom */
+/* GetLastBitUnsecure arithmetic.circom:161-171: bit, div | in */
+static size_t ck_lastbit(ck_t *c, size_t b) {
+  const char *T = "GetLastBitUnsecure int/arithmetic.circom";
+  fr_t bit = S(c, b), div = S(c, b + 1);
+  EQ(MUL(SUB(KC(1), bit), bit), fr_zero(), T, 169);
+  EQ(ADD(MUL(div, KC(2)), MUL(bit, bit)), S(c, b + 2), T, 170);
+  return 3;
+}
+
+/* GetLastNBits(N) arithmetic.circom:178-204: div, out[N] | in | check[N] | GetLastBitUnsecure[N] */
+static size_t ck_lastnbits(ck_t *c, size_t b, int N) {
+  const char *T = "GetLastNBits int/arithmetic.circom";
+  size_t div = b, out = b + 1, in = b + 1 + N, chk = b + 2 + N, g = b + 2 + 2 * (size_t)N;
+  for (int i = 0; i < N; i++) {
+    size_t gi = g + 3 * (size_t)i;
+    ck_lastbit(c, gi);
+    EQ(S(c, gi + 2), i == 0 ? S(c, in) : S(c, gi - 3 + 1), T, i == 0 ? 188 : 190);
+    EQ(S(c, out + i), S(c, gi), T, 192);
+  }
+  EQ(S(c, div), S(c, g + 3 * (size_t)(N - 1) + 1), T, 195);
+  EQ(MUL(S(c, out), S(c, out)), S(c, chk), T, 198);
+  for (int i = 1; i < N; i++) EQ(ADD(S(c, chk + i - 1), MUL(S(c, out + i), P2[i])), S(c, chk + i), T, 200);
+  EQ(ADD(S(c, chk + N - 1), MUL(S(c, div), P2[N])), S(c, in), T, 203);
+  return 5 * (size_t)N + 2;
+}
+
+/* GetSumOfNElements(N) arithmetic.circom:210-226: out | in[N] | sum[N-1] */
+static size_t ck_getsum(ck_t *c, size_t b, int N) {
+  const char *T = "GetSumOfNElements int/arithmetic.circom";
+  size_t in = b + 1, sum = b + 1 + N;
+  EQ(S(c, sum), ADD(S(c, in), S(c, in + 1)), T, 219);
+  for (int i = 1; i < N - 1; i++) EQ(S(c, sum + i), ADD(S(c, sum + i - 1), S(c, in + i + 1)), T, 221);
+  EQ(S(c, b), S(c, sum + N - 2), T, 224);
+  return 2 * (size_t)N;
+}
+
+/* ============================================================ SHA-2 (224/256) */
+/* XOR3_v2 sha2Common.circom:80-88: out | x, y, z | tmp */
+static size_t ck_xor3(ck_t *c, size_t b) {
+  const char *T = "XOR3_v2 hasher/sha2/sha2Common.circom";
+  fr_t x = S(c, b + 1), y = S(c, b + 2), z = S(c, b + 3), tmp = S(c, b + 4);
+  EQ(tmp, MUL(y, z), T, 86);
+  fr_t f = ADD(SUB(SUB(KC(1), MUL(KC(2), y)), MUL(KC(2), z)), MUL(KC(4), tmp));
+  EQ(S(c, b), SUB(ADD(ADD(MUL(x, f), y), z), MUL(KC(2), tmp)), T, 87);
+  return 5;
+}
+
+/* Bits2 sha2Common.circom:57-68: lo, hi | xy */
+static size_t ck_bits2(ck_t *c, size_t b) {
+  const char *T = "Bits2 hasher/sha2/sha2Common.circom";
+  fr_t lo = S(c, b), hi = S(c, b + 1);
+  EQ(MUL(lo, SUB(KC(1), lo)), fr_zero(), T, 65);
+  EQ(MUL(hi, SUB(KC(1), hi)), fr_zero(), T, 66);
+  EQ(S(c, b + 2), ADD(MUL(KC(2), hi), lo), T, 68);
+  return 3;
+}
+
+/* the (1 << i) * bit[i] inputs of a GetSumOfNElements(32) at g from 32 bits at `bits` (stride st) */
+static void wire_sum32(ck_t *c, size_t b, size_t g, size_t bits, size_t st, const char *T, int line) {
+  for (int i = 0; i < 32; i++) EQ(S(c, g + 1 + i), MUL(P2[i], S(c, bits + (size_t)i * st)), T, line);
+}
+
+/* Sha2_224_256Shedule sha256Schedule.circom:11-72:
+ * outWords[64] | chunkBits[16][32] | outBits[64][32] | sumN[16], then per m: s0Sum, s1Sum, (s0Xor, s1Xor)[32], modulo, bits2Num */
+static size_t ck_schedule(ck_t *c, size_t b) {
+  const char *T = "Sha2_224_256Shedule hasher/sha2/sha256/sha256Schedule.circom";
+  size_t ow = b, cb = b + 64, ob = b + 64 + 512, o = b + 64 + 512 + 2048;
+  for (int k = 0; k < 16; k++) {
+    o += ck_getsum(c, o, 32);
+    size_t g = o - 64;
+    wire_sum32(c, b, g, cb + 32 * (size_t)k, 1, T, 22);
+    EQ(S(c, ow + k), S(c, g), T, 24);
+    for (int i = 0; i < 32; i++) EQ(S(c, ob + 32 * (size_t)k + i), S(c, cb + 32 * (size_t)k + i), T, 25);
+  }
+  for (int m = 16; m < 64; m++) {
+    size_t k = m - 15, l = m - 2;
+    size_t s0 = o, s1 = o + 64;
+    o += ck_getsum(c, s0, 32) + ck_getsum(c, s1, 32);
+    for (int i = 0; i < 32; i++) {
+      size_t x0 = o, x1 = o + 5;
+      o += ck_xor3(c, x0) + ck_xor3(c, x1);
+      EQ(S(c, x0 + 1), S(c, ob + 32 * k + (i + 7) % 32), T, 51);
+      EQ(S(c, x0 + 2), S(c, ob + 32 * k + (i + 18) % 32), T, 52);
+      EQ(S(c, x0 + 3), i < 29 ? S(c, ob + 32 * k + i + 3) : fr_zero(), T, 53);
+      EQ(S(c, s0 + 1 + i), MUL(P2[i], S(c, x0)), T, 54);
+      EQ(S(c, x1 + 1), S(c, ob + 32 * l + (i + 17) % 32), T, 57);
+      EQ(S(c, x1 + 2), S(c, ob + 32 * l + (i + 19) % 32), T, 58);
+      EQ(S(c, x1 + 3), i < 22 ? S(c, ob + 32 * l + i + 10) : fr_zero(), T, 59);
+      EQ(S(c, s1 + 1 + i), MUL(P2[i], S(c, x1)), T, 60);
+    }
+    size_t md = o;
+    o += ck_lastnbits(c, md, 32);
+    EQ(S(c, md + 33), ADD(ADD(ADD(S(c, s1), S(c, ow + m - 7)), S(c, s0)), S(c, ow + m - 16)), T, 65);
+    for (int i = 0; i < 32; i++) EQ(S(c, ob + 32 * (size_t)m + i), S(c, md + 1 + i), T, 66);
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 32);
+    for (int i = 0; i < 32; i++) EQ(S(c, bn + 1 + i), S(c, ob + 32 * (size_t)m + i), T, 68);
+    EQ(S(c, ow + m), S(c, bn), T, 69);
+  }
+  return o - b;
+}
+
+static const uint32_t SHA256_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+/* Sha2_224_256CompressInner sha256Compress.circom:11-96:
+ * outA[32] outB[32] outC[32] outDD outE[32] outF[32] outG[32] outHH | inp key a[32] b[32] c[32] dd e[32] f[32] g[32] hh |
+ * chb[32] overflowE overflowA | dSum hSum s0Sum s1Sum mjSum chSum (major, s0Xor, s1Xor)[32] decomposeE decomposeA */
+static size_t ck_compress(ck_t *c, size_t b) {
+  const char *T = "Sha2_224_256CompressInner hasher/sha2/sha256/sha256Compress.circom";
+  size_t oA = b, oB = b + 32, oC = b + 64, oDD = b + 96, oE = b + 97, oF = b + 129, oG = b + 161, oHH = b + 193;
+  size_t inp = b + 194, key = b + 195, a = b + 196, bb = b + 228, cc = b + 260, dd = b + 292, e = b + 293,
+         f = b + 325, g = b + 357, hh = b + 389;
+  size_t chb = b + 390, ovE = b + 422, ovA = b + 423, o = b + 424;
+  for (int i = 0; i < 32; i++) {
+    EQ(S(c, oG + i), S(c, f + i), T, 37);
+    EQ(S(c, oF + i), S(c, e + i), T, 38);
+    EQ(S(c, oC + i), S(c, bb + i), T, 39);
+    EQ(S(c, oB + i), S(c, a + i), T, 40);
+  }
+  size_t dS = o, hS = o + 64, s0S = o + 128, s1S = o + 192, mjS = o + 256, chS = o + 320;
+  for (int q = 0; q < 6; q++) o += ck_getsum(c, o, 32);
+  wire_sum32(c, b, dS, cc, 1, T, 46);
+  wire_sum32(c, b, hS, g, 1, T, 47);
+  EQ(S(c, oDD), S(c, dS), T, 49);
+  EQ(S(c, oHH), S(c, hS), T, 50);
+  for (int i = 0; i < 32; i++) {
+    size_t mj = o, x0 = o + 3, x1 = o + 8;
+    o += ck_bits2(c, mj) + ck_xor3(c, x0) + ck_xor3(c, x1);
+    EQ(S(c, chb + i), ADD(MUL(S(c, e + i), SUB(S(c, f + i), S(c, g + i))), S(c, g + i)), T, 65);
+    EQ(S(c, chS + 1 + i), MUL(P2[i], S(c, chb + i)), T, 66);
+    EQ(S(c, mj + 2), ADD(ADD(S(c, a + i), S(c, bb + i)), S(c, cc + i)), T, 70);
+    EQ(S(c, mjS + 1 + i), MUL(P2[i], S(c, mj + 1)), T, 71);
+    EQ(S(c, x0 + 1), S(c, a + (i + 2) % 32), T, 74);
+    EQ(S(c, x0 + 2), S(c, a + (i + 13) % 32), T, 75);
+    EQ(S(c, x0 + 3), S(c, a + (i + 22) % 32), T, 76);
+    EQ(S(c, s0S + 1 + i), MUL(P2[i], S(c, x0)), T, 77);
+    EQ(S(c, x1 + 1), S(c, e + (i + 6) % 32), T, 80);
+    EQ(S(c, x1 + 2), S(c, e + (i + 11) % 32), T, 81);
+    EQ(S(c, x1 + 3), S(c, e + (i + 25) % 32), T, 82);
+    EQ(S(c, s1S + 1 + i), MUL(P2[i], S(c, x1)), T, 83);
+  }
+  fr_t t1 = ADD(ADD(ADD(S(c, s1S), S(c, chS)), S(c, key)), S(c, inp));
+  EQ(S(c, ovE), ADD(ADD(S(c, dd), S(c, hh)), t1), T, 87);
+  EQ(S(c, ovA), ADD(ADD(ADD(S(c, hh), t1), S(c, s0S)), S(c, mjS)), T, 88);
+  size_t dE = o;
+  o += ck_lastnbits(c, dE, 32);
+  EQ(S(c, dE + 33), S(c, ovE), T, 91);
+  for (int i = 0; i < 32; i++) EQ(S(c, oE + i), S(c, dE + 1 + i), T, 92);
+  size_t dA = o;
+  o += ck_lastnbits(c, dA, 32);
+  EQ(S(c, dA + 33), S(c, ovA), T, 95);
+  for (int i = 0; i < 32; i++) EQ(S(c, oA + i), S(c, dA + 1 + i), T, 96);
+  return o - b;
+}
+
+/* Sha2_224_256Rounds(64) sha256Rounds.circom:12-125:
+ * outHash[8][32] | words[64] inpHash[8][32] | a b c [65][32] dd[65] e f g [65][32] hh[65] ROUND_KEYS[64] hashWords[8] |
+ * roundKeys sumDd sumHh sum[8] compress[64] modulo[8] sumA sumB sumC sumE sumF sumG */
+static size_t ck_rounds(ck_t *c, size_t b) {
+  const char *T = "Sha2_224_256Rounds hasher/sha2/sha256/sha256Rounds.circom";
+  const int n = 64;
+  size_t outH = b, words = b + 256, inH = b + 320;
+  size_t A = b + 576, B = A + 65 * 32, C = B + 65 * 32, DD = C + 65 * 32, E = DD + 65, F = E + 65 * 32, G = F + 65 * 32,
+         HH = G + 65 * 32, RK = HH + 65, HW = RK + 64, o = HW + 8;
+  size_t rk = o;  /* Sha2_224_256RoundKeys sha256RoundConst.circom:6-25: out[64] */
+  for (int j = 0; j < 64; j++) req(c, S(c, rk + j), KC(SHA256_K[j]), "Sha2_224_256RoundKeys sha256RoundConst.circom", 23, rk);
+  o += 64;
+  for (int j = 0; j < 64; j++) EQ(S(c, RK + j), S(c, rk + j), T, 38);
+  for (int i = 0; i < 32; i++) {
+    EQ(S(c, A + i), S(c, inH + i), T, 40);
+    EQ(S(c, B + i), S(c, inH + 32 + i), T, 41);
+    EQ(S(c, C + i), S(c, inH + 64 + i), T, 42);
+    EQ(S(c, E + i), S(c, inH + 128 + i), T, 44);
+    EQ(S(c, F + i), S(c, inH + 160 + i), T, 45);
+    EQ(S(c, G + i), S(c, inH + 192 + i), T, 46);
+  }
+  size_t sDd = o, sHh = o + 64;
+  o += ck_getsum(c, sDd, 32) + ck_getsum(c, sHh, 32);
+  wire_sum32(c, b, sDd, inH + 96, 1, T, 51);
+  wire_sum32(c, b, sHh, inH + 224, 1, T, 52);
+  EQ(S(c, DD), S(c, sDd), T, 54);
+  EQ(S(c, HH), S(c, sHh), T, 55);
+  for (int j = 0; j < 8; j++) {
+    size_t s = o;
+    o += ck_getsum(c, s, 32);
+    wire_sum32(c, b, s, inH + 32 * (size_t)j, 1, T, 62);
+    EQ(S(c, HW + j), S(c, s), T, 64);
+  }
+  for (int k = 0; k < n; k++) {
+    size_t ci = o;
+    o += ck_compress(c, ci);
+    EQ(S(c, ci + 194), S(c, words + k), T, 73);
+    EQ(S(c, ci + 195), S(c, RK + k), T, 74);
+    for (int i = 0; i < 32; i++) {
+      EQ(S(c, ci + 196 + i), S(c, A + 32 * (size_t)k + i), T, 76);
+      EQ(S(c, ci + 228 + i), S(c, B + 32 * (size_t)k + i), T, 77);
+      EQ(S(c, ci + 260 + i), S(c, C + 32 * (size_t)k + i), T, 78);
+      EQ(S(c, ci + 293 + i), S(c, E + 32 * (size_t)k + i), T, 80);
+      EQ(S(c, ci + 325 + i), S(c, F + 32 * (size_t)k + i), T, 81);
+      EQ(S(c, ci + 357 + i), S(c, G + 32 * (size_t)k + i), T, 82);
+      EQ(S(c, A + 32 * (size_t)(k + 1) + i), S(c, ci + i), T, 85);
+      EQ(S(c, B + 32 * (size_t)(k + 1) + i), S(c, ci + 32 + i), T, 86);
+      EQ(S(c, C + 32 * (size_t)(k + 1) + i), S(c, ci + 64 + i), T, 87);
+      EQ(S(c, E + 32 * (size_t)(k + 1) + i), S(c, ci + 97 + i), T, 89);
+      EQ(S(c, F + 32 * (size_t)(k + 1) + i), S(c, ci + 129 + i), T, 90);
+      EQ(S(c, G + 32 * (size_t)(k + 1) + i), S(c, ci + 161 + i), T, 91);
+    }
+    EQ(S(c, ci + 292), S(c, DD + k), T, 79);
+    EQ(S(c, ci + 389), S(c, HH + k), T, 83);
+    EQ(S(c, DD + k + 1), S(c, ci + 96), T, 88);
+    EQ(S(c, HH + k + 1), S(c, ci + 193), T, 92);
+  }
+  size_t md = o;
+  for (int j = 0; j < 8; j++) o += ck_lastnbits(c, o, 32);
+  size_t sums[6], src[6] = {A, B, C, E, F, G};
+  for (int q = 0; q < 6; q++) {
+    sums[q] = o;
+    o += ck_getsum(c, o, 32);
+    wire_sum32(c, b, sums[q], src[q] + 32 * (size_t)n, 1, T, 106);
+  }
+  static const int which[8] = {0, 1, 2, -1, 3, 4, 5, -2};
+  for (int j = 0; j < 8; j++) {
+    size_t mj = md + 162 * (size_t)j;
+    fr_t rhs = which[j] >= 0 ? S(c, sums[which[j]]) : which[j] == -1 ? S(c, DD + n) : S(c, HH + n);
+    EQ(S(c, mj + 33), ADD(S(c, HW + j), rhs), T, 114);
+    for (int i = 0; i < 32; i++) EQ(S(c, outH + 32 * (size_t)j + i), S(c, mj + 1 + i), T, 123);
+  }
+  return o - b;
+}
+
+static const uint32_t SHA256_IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+static const uint32_t SHA224_IV[8] = {0xc1059ed8, 0x367cd507, 0x3070dd17, 0xf70e5939,
+                                      0xffc00b31, 0x68581511, 0x64f98fa7, 0xbefa4fa4};
+
+/* Sha256HashChunks(B) sha256HashChunks.circom:8-48 (O = 256) / Sha224HashChunks(B) sha224/sha224HashChunks.circom
+ * (O = 224, SHA-224 IV): out[O] | in[512B] | states[B+1][8][32] | iv, (sch, rds)[B] */
+static size_t ck_sha2chunks(ck_t *c, size_t b, int B, int O) {
+  const char *T = O == 256 ? "Sha256HashChunks hasher/sha2/sha256/sha256HashChunks.circom"
+                           : "Sha224HashChunks hasher/sha2/sha224/sha224HashChunks.circom";
+  size_t out = b, in = b + O, st = in + 512 * (size_t)B, o = st + (size_t)(B + 1) * 256;
+  size_t iv = o;
+  const uint32_t *IV = O == 256 ? SHA256_IV : SHA224_IV;
+  for (int k = 0; k < 8; k++)
+    for (int i = 0; i < 32; i++)
+      req(c, S(c, iv + 32 * k + i), KC((IV[k] >> i) & 1), "Sha256InitialValue sha256InitialValue.circom", 24, iv);
+  o += 256;
+  for (int q = 0; q < 256; q++) EQ(S(c, st + q), S(c, iv + q), T, 21);
+  for (int m = 0; m < B; m++) {
+    size_t sch = o;
+    o += ck_schedule(c, sch);
+    size_t rds = o;
+    o += ck_rounds(c, rds);
+    for (int k = 0; k < 16; k++)
+      for (int i = 0; i < 32; i++)
+        EQ(S(c, sch + 64 + 32 * k + i), S(c, in + 512 * (size_t)m + 32 * k + 31 - i), T, 33);
+    for (int q = 0; q < 64; q++) EQ(S(c, rds + 256 + q), S(c, sch + q), T, 38);
+    for (int q = 0; q < 256; q++) {
+      EQ(S(c, rds + 320 + q), S(c, st + 256 * (size_t)m + q), T, 40);
+      EQ(S(c, st + 256 * (size_t)(m + 1) + q), S(c, rds + q), T, 41);
+    }
+  }
+  for (int j = 0; j < O / 32; j++)
+    for (int i = 0; i < 32; i++) EQ(S(c, out + 32 * j + i), S(c, st + 256 * (size_t)B + 32 * j + 31 - i), T, 46);
+  return o - b;
+}
+
+/* ============================================================ Poseidon (hasher/poseidon/poseidon.circom) */
+typedef struct { int t, nRP; fr_t *C, *M, *P, *S; } pos_t;
+static pos_t POS[7];
+static int pos_loaded = 0;
+
+int ck_load_poseidon(const char *path) {
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return -1;
+  char magic[8]; uint32_t nt;
+  if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, "PZKPOS01", 8) || fread(&nt, 4, 1, fp) != 1) { fclose(fp); return -2; }
+  for (uint32_t q = 0; q < nt; q++) {
+    uint32_t h[4];
+    if (fread(h, 4, 4, fp) != 4 || h[0] < 2 || h[0] > 6) { fclose(fp); return -3; }
+    int t = (int)h[0];
+    pos_t *pp = &POS[t];
+    pp->t = t; pp->nRP = (int)h[1];
+    pp->C = malloc(32 * h[2]); pp->M = malloc(32 * t * t); pp->P = malloc(32 * t * t); pp->S = malloc(32 * h[3]);
+    if (fread(pp->C, 32, h[2], fp) != h[2] || fread(pp->M, 32, (size_t)t * t, fp) != (size_t)t * t ||
+        fread(pp->P, 32, (size_t)t * t, fp) != (size_t)t * t || fread(pp->S, 32, h[3], fp) != h[3]) {
+      fclose(fp); return -4;
+    }
+  }
+  fclose(fp);
+  pos_loaded = 1;
+  return 0;
+}
+
+/* Sigma :10-21: out | in | in2, in4 */
+static size_t ck_sigma(ck_t *c, size_t b) {
+  const char *T = "Sigma hasher/poseidon/poseidon.circom";
+  fr_t in = S(c, b + 1), in2 = S(c, b + 2), in4 = S(c, b + 3);
+  EQ(in2, MUL(in, in), T, 17);
+  EQ(in4, MUL(in2, in2), T, 18);
+  EQ(S(c, b), MUL(in4, in), T, 20);
+  return 4;
+}
+/* Ark(t, C, r) :23-30: out[t] | in[t] */
+static size_t ck_ark(ck_t *c, size_t b, int t, const fr_t *C, int r) {
+  for (int i = 0; i < t; i++) EQ(S(c, b + i), ADD(S(c, b + t + i), C[i + r]), "Ark hasher/poseidon/poseidon.circom", 28);
+  return 2 * (size_t)t;
+}
+/* Mix(t, M) :32-46: out[t] | in[t] | sum[t] */
+static size_t ck_mix(ck_t *c, size_t b, int t, const fr_t *M) {
+  const char *T = "Mix hasher/poseidon/poseidon.circom";
+  size_t o = b + 2 * t;
+  for (int i = 0; i < t; i++) {
+    size_t s = o;
+    o += ck_getsum(c, s, t);
+    for (int j = 0; j < t; j++) EQ(S(c, s + 1 + j), MUL(M[j * t + i], S(c, b + t + j)), T, 42);
+    EQ(S(c, b + i), S(c, s), T, 44);
+  }
+  return o - b;
+}
+/* MixLast(t, M, s) :48-58: out | in[t] | sum */
+static size_t ck_mixlast(ck_t *c, size_t b, int t, const fr_t *M, int s_) {
+  const char *T = "MixLast hasher/poseidon/poseidon.circom";
+  size_t s = b + 1 + t;
+  for (int j = 0; j < t; j++) EQ(S(c, s + 1 + j), MUL(M[j * t + s_], S(c, b + 1 + j)), T, 55);
+  EQ(S(c, b), S(c, s), T, 57);
+  return 1 + (size_t)t + ck_getsum(c, s, t);
+}
+/* MixS(t, S, r) :60-78: out[t] | in[t] | sum */
+static size_t ck_mixs(ck_t *c, size_t b, int t, const fr_t *Sc, int r) {
+  const char *T = "MixS hasher/poseidon/poseidon.circom";
+  size_t s = b + 2 * t;
+  for (int i = 0; i < t; i++) EQ(S(c, s + 1 + i), MUL(Sc[(t * 2 - 1) * r + i], S(c, b + t + i)), T, 71);
+  EQ(S(c, b), S(c, s), T, 73);
+  for (int i = 1; i < t; i++)
+    EQ(S(c, b + i), ADD(S(c, b + t + i), MUL(S(c, b + t), Sc[(t * 2 - 1) * r + t + i - 1])), T, 76);
+  return 2 * (size_t)t + ck_getsum(c, s, t);
+}
+
+/* PoseidonEx(nIn, 1) :80-209: out[1] | in[nIn] initialState | components in creation order */
+static size_t ck_poseidonex(ck_t *c, size_t b, int nIn) {
+  const char *T = "PoseidonEx hasher/poseidon/poseidon.circom";
+  const int t = nIn + 1, F = 8;
+  const pos_t *pp = &POS[t];
+  const int RP = pp->nRP;
+  size_t out = b, in = b + 1, init = b + 1 + nIn, o = b + 2 + nIn;
+  size_t ark = o;  /* ark[0] */
+  o += ck_ark(c, ark, t, pp->C, 0);
+  for (int j = 0; j < t; j++) EQ(S(c, ark + t + j), j > 0 ? S(c, in + j - 1) : S(c, init), T, j > 0 ? 127 : 129);
+  size_t prev = ark;  /* block whose out[0..t) feeds the next sigma layer */
+  for (int r = 0; r < F / 2; r++) {
+    size_t sg = o;
+    for (int j = 0; j < t; j++) {
+      o += ck_sigma(c, o);
+      EQ(S(c, sg + 4 * j + 1), S(c, prev + j), T, r == 0 ? 137 : 139);
+    }
+    size_t ak = o;
+    o += ck_ark(c, ak, t, pp->C, (r + 1) * t);
+    for (int j = 0; j < t; j++) EQ(S(c, ak + t + j), S(c, sg + 4 * j), T, 145);
+    size_t mx = o;
+    o += ck_mix(c, mx, t, r < F / 2 - 1 ? pp->M : pp->P);
+    for (int j = 0; j < t; j++) EQ(S(c, mx + t + j), S(c, ak + j), T, 150);
+    prev = mx;
+  }
+  size_t mixP = prev, ms = 0;
+  for (int r = 0; r < RP; r++) {
+    size_t sp = o;
+    o += ck_sigma(c, sp);
+    EQ(S(c, sp + 1), r == 0 ? S(c, mixP) : S(c, ms), T, r == 0 ? 178 : 180);
+    size_t m = o;
+    o += ck_mixs(c, m, t, pp->S, r);
+    for (int j = 0; j < t; j++) {
+      if (j == 0) EQ(S(c, m + t), ADD(S(c, sp), pp->C[(F / 2 + 1) * t + r]), T, 186);
+      else EQ(S(c, m + t + j), r == 0 ? S(c, mixP + j) : S(c, ms + j), T, r == 0 ? 189 : 191);
+    }
+    ms = m;
+  }
+  prev = ms;
+  for (int r = 0; r < F / 2 - 1; r++) {
+    size_t sg = o;
+    for (int j = 0; j < t; j++) {
+      o += ck_sigma(c, o);
+      EQ(S(c, sg + 4 * j + 1), S(c, prev + j), T, r == 0 ? 201 : 203);
+    }
+    size_t ak = o;
+    o += ck_ark(c, ak, t, pp->C, (F / 2 + 1) * t + RP + r * t);
+    for (int j = 0; j < t; j++) EQ(S(c, ak + t + j), S(c, sg + 4 * j), T, 209);
+    size_t mx = o;
+    o += ck_mix(c, mx, t, pp->M);
+    for (int j = 0; j < t; j++) EQ(S(c, mx + t + j), S(c, ak + j), T, 214);
+    prev = mx;
+  }
+  size_t sg = o;
+  for (int j = 0; j < t; j++) {
+    o += ck_sigma(c, o);
+    EQ(S(c, sg + 4 * j + 1), S(c, prev + j), T, 221);
+  }
+  size_t ml = o;
+  o += ck_mixlast(c, ml, t, pp->M, 0);
+  for (int j = 0; j < t; j++) EQ(S(c, ml + 1 + j), S(c, sg + 4 * j), T, 227);
+  EQ(S(c, out), S(c, ml), T, 229);
+  return o - b;
+}
+
+/* PoseidonHash(n) :214-226: out | in[n] | pEx */
+static size_t ck_poseidon(ck_t *c, size_t b, int n) {
+  const char *T = "PoseidonHash hasher/poseidon/poseidon.circom";
+  size_t px = b + 1 + n;
+  size_t sz = 1 + (size_t)n + ck_poseidonex(c, px, n);
+  EQ(S(c, px + 1 + n), fr_zero(), T, 221);
+  for (int i = 0; i < n; i++) EQ(S(c, px + 1 + i), S(c, b + 1 + i), T, 223);
+  EQ(S(c, b), S(c, px), T, 225);
+  return sz;
+}
+
+/* ============================================================ SMT (merkleTree/SMTVerifier.circom) */
+/* Switcher utils/switcher.circom:16-26: out[2] | bool in[2] | aux */
+static size_t ck_switcher(ck_t *c, size_t b) {
+  const char *T = "Switcher utils/switcher.circom";
+  fr_t bo = S(c, b + 2), i0 = S(c, b + 3), i1 = S(c, b + 4), aux = S(c, b + 5);
+  EQ(aux, MUL(SUB(i1, i0), bo), T, 23);
+  EQ(S(c, b), ADD(aux, i0), T, 24);
+  EQ(S(c, b + 1), ADD(fr_neg(aux), i1), T, 25);
+  return 6;
+}
+
+/* SMTLevIns(N) :39-65: levIns[N] | siblings[N] | done[N-1] | isZero[N] */
+static size_t ck_smtlevins(ck_t *c, size_t b, int N) {
+  const char *T = "SMTLevIns merkleTree/SMTVerifier.circom";
+  size_t lev = b, sib = b + N, done = b + 2 * (size_t)N, z = b + 3 * (size_t)N - 1;
+  for (int i = 0; i < N; i++) {
+    ck_iszero(c, z + 3 * (size_t)i);
+    EQ(S(c, z + 3 * (size_t)i + 1), S(c, sib + i), T, 51);
+  }
+#define ZO(i) S(c, z + 3 * (size_t)(i))
+  EQ(SUB(ZO(N - 1), KC(1)), fr_zero(), T, 54);
+  EQ(S(c, lev + N - 1), SUB(KC(1), ZO(N - 2)), T, 56);
+  EQ(S(c, done + N - 2), S(c, lev + N - 1), T, 57);
+  for (int i = N - 2; i > 0; i--) {
+    EQ(S(c, lev + i), MUL(SUB(KC(1), S(c, done + i)), SUB(KC(1), ZO(i - 1))), T, 60);
+    EQ(S(c, done + i - 1), ADD(S(c, lev + i), S(c, done + i)), T, 61);
+  }
+  EQ(S(c, lev), SUB(KC(1), S(c, done)), T, 64);
+#undef ZO
+  return 3 * (size_t)N - 1 + 3 * (size_t)N;
+}
+
+/* SMTVerifierLevel :82-107: root | st_top st_inew sibling new1leaf lrbit child | fromProof | proofHash(SMTHash2) switcher */
+static size_t ck_smtlevel(ck_t *c, size_t b) {
+  const char *T = "SMTVerifierLevel merkleTree/SMTVerifier.circom";
+  size_t root = b, top = b + 1, inew = b + 2, sib = b + 3, leaf = b + 4, lr = b + 5, child = b + 6, fp = b + 7;
+  size_t ph = b + 8;           /* SMTHash2: out | L R | h = PoseidonHash(2) */
+  size_t h = ph + 3;
+  size_t sz_ph = 3 + ck_poseidon(c, h, 2);
+  EQ(S(c, h + 1), S(c, ph + 1), "SMTHash2 merkleTree/SMTVerifier.circom", 28);
+  EQ(S(c, h + 2), S(c, ph + 2), "SMTHash2 merkleTree/SMTVerifier.circom", 29);
+  EQ(S(c, ph), S(c, h), "SMTHash2 merkleTree/SMTVerifier.circom", 31);
+  size_t sw = ph + sz_ph;
+  ck_switcher(c, sw);
+  EQ(S(c, sw + 3), S(c, child), T, 96);
+  EQ(S(c, sw + 4), S(c, sib), T, 97);
+  EQ(S(c, sw + 2), S(c, lr), T, 99);
+  EQ(S(c, ph + 1), S(c, sw), T, 100);
+  EQ(S(c, ph + 2), S(c, sw + 1), T, 101);
+  EQ(S(c, fp), MUL(S(c, ph), S(c, top)), T, 103);
+  EQ(S(c, root), ADD(S(c, fp), MUL(S(c, leaf), S(c, inew))), T, 105);
+  return 8 + sz_ph + 6;
+}
+
+/* SMTVerifier(N) :109-176: isVerified | root leaf key siblings[N] | value |
+ * hash1New(SMTHash1) n2bNew(Num2Bits(254)) smtLevIns sm[0..N) levels[N-1..0] isEqual */
+static size_t ck_smt(ck_t *c, size_t b, int N) {
+  const char *T = "SMTVerifier merkleTree/SMTVerifier.circom";
+  size_t isv = b, root = b + 1, leaf = b + 2, key = b + 3, sib = b + 4, value = b + 4 + N, o = b + 5 + N;
+  EQ(S(c, value), S(c, leaf), T, 118);
+  size_t h1 = o, h = h1 + 3;   /* SMTHash1: out | key value | h = PoseidonHash(3) */
+  o += 3 + ck_poseidon(c, h, 3);
+  EQ(S(c, h + 1), S(c, h1 + 1), "SMTHash1 merkleTree/SMTVerifier.circom", 16);
+  EQ(S(c, h + 2), S(c, h1 + 2), "SMTHash1 merkleTree/SMTVerifier.circom", 17);
+  EQ(S(c, h + 3), KC(1), "SMTHash1 merkleTree/SMTVerifier.circom", 18);
+  EQ(S(c, h1), S(c, h), "SMTHash1 merkleTree/SMTVerifier.circom", 20);
+  EQ(S(c, h1 + 1), S(c, key), T, 121);
+  EQ(S(c, h1 + 2), S(c, value), T, 122);
+  size_t n2b = o;
+  o += ck_num2bits(c, n2b, 254);
+  EQ(S(c, n2b + 254), S(c, key), T, 126);
+  size_t li = o;
+  o += ck_smtlevins(c, li, N);
+  for (int i = 0; i < N; i++) EQ(S(c, li + N + i), S(c, sib + i), T, 131);
+  size_t sm = o;  /* SMTVerifierSM :71-80: st_top st_inew | levIns prev_top */
+  for (int i = 0; i < N; i++) {
+    size_t q = sm + 4 * (size_t)i;
+    const char *TS = "SMTVerifierSM merkleTree/SMTVerifier.circom";
+    req(c, S(c, q + 1), MUL(S(c, q + 3), S(c, q + 2)), TS, 78, q);
+    req(c, S(c, q), SUB(S(c, q + 3), S(c, q + 1)), TS, 79, q);
+    EQ(S(c, q + 3), i == 0 ? KC(1) : S(c, q - 4), T, i == 0 ? 140 : 142);
+    EQ(S(c, q + 2), S(c, li + i), T, 145);
+  }
+  o += 4 * (size_t)N;
+  size_t lvl_at[128];
+  for (int i = N - 1; i >= 0; i--) {
+    size_t L = o;
+    lvl_at[i] = L;
+    o += ck_smtlevel(c, L);
+    size_t q = sm + 4 * (size_t)i;
+    EQ(S(c, L + 1), S(c, q), T, 153);
+    EQ(S(c, L + 2), S(c, q + 1), T, 154);
+    EQ(S(c, L + 3), S(c, sib + i), T, 156);
+    EQ(S(c, L + 4), S(c, h1), T, 157);
+    EQ(S(c, L + 5), S(c, n2b + i), T, 159);
+    EQ(S(c, L + 6), i == N - 1 ? fr_zero() : S(c, lvl_at[i + 1]), T, i == N - 1 ? 162 : 164);
+  }
+  size_t ie = o;
+  o += ck_isequal(c, ie);
+  EQ(S(c, ie + 1), S(c, lvl_at[0]), T, 171);
+  EQ(S(c, ie + 2), S(c, root), T, 172);
+  EQ(S(c, isv), S(c, ie), T, 173);
+  return o - b;
+}
+
+/* ============================================================ BabyJubJub (babyjubjub/curve.circom) */
+/* BabyjubjubAdd :71-105: out[2] | in1[2] in2[2] | beta gamma delta tau */
+static size_t ck_bjjadd(ck_t *c, size_t b) {
+  const char *T = "BabyjubjubAdd babyjubjub/curve.circom";
+  const fr_t a = KC(168700), d = KC(168696);
+  fr_t x1 = S(c, b + 2), y1 = S(c, b + 3), x2 = S(c, b + 4), y2 = S(c, b + 5);
+  fr_t be = S(c, b + 6), ga = S(c, b + 7), de = S(c, b + 8), ta = S(c, b + 9);
+  EQ(be, MUL(x1, y2), T, 83);
+  EQ(ga, MUL(y1, x2), T, 86);
+  EQ(de, MUL(SUB(y1, MUL(a, x1)), ADD(x2, y2)), T, 89);
+  EQ(ta, MUL(be, ga), T, 92);
+  EQ(MUL(ADD(KC(1), MUL(d, ta)), S(c, b)), ADD(be, ga), T, 96);
+  EQ(MUL(SUB(KC(1), MUL(d, ta)), S(c, b + 1)), SUB(ADD(de, MUL(a, be)), ga), T, 100);
+  return 10;
+}
+/* BabyjubjubDouble :109-118: out[2] | in[2] | adder */
+static size_t ck_bjjdouble(ck_t *c, size_t b) {
+  const char *T = "BabyjubjubDouble babyjubjub/curve.circom";
+  size_t ad = b + 4;
+  ck_bjjadd(c, ad);
+  for (int i = 0; i < 2; i++) {
+    EQ(S(c, ad + 2 + i), S(c, b + 2 + i), T, 114);
+    EQ(S(c, ad + 4 + i), S(c, b + 2 + i), T, 115);
+    EQ(S(c, b + i), S(c, ad + i), T, 117);
+  }
+  return 14;
+}
+/* addZeroBabyjub :19-58: out[2] | in1[2] in2[2] | isZeroIn1 isZeroIn2 adder (switcherLeft[i], switcherRight[i])[2] */
+static size_t ck_addzero(ck_t *c, size_t b) {
+  const char *T = "addZeroBabyjub babyjubjub/curve.circom";
+  size_t z1 = b + 6, z2 = b + 9, ad = b + 12, sw = b + 22;
+  ck_iszero(c, z1);
+  EQ(S(c, z1 + 1), S(c, b + 2), T, 25);
+  ck_iszero(c, z2);
+  EQ(S(c, z2 + 1), S(c, b + 4), T, 27);
+  ck_bjjadd(c, ad);
+  for (int i = 0; i < 2; i++) {
+    EQ(S(c, ad + 2 + i), S(c, b + 2 + i), T, 31);
+    EQ(S(c, ad + 4 + i), S(c, b + 4 + i), T, 32);
+  }
+  for (int i = 0; i < 2; i++) {
+    size_t L = sw + 12 * (size_t)i, R = L + 6;
+    ck_switcher(c, L);
+    EQ(S(c, L + 2), S(c, z2), T, 47);
+    EQ(S(c, L + 3), S(c, ad + i), T, 48);
+    EQ(S(c, L + 4), S(c, b + 2 + i), T, 49);
+    ck_switcher(c, R);
+    EQ(S(c, R + 2), S(c, z1), T, 52);
+    EQ(S(c, R + 3), S(c, L), T, 53);
+    EQ(S(c, R + 4), S(c, b + 4 + i), T, 54);
+  }
+  EQ(S(c, b), S(c, sw + 6), T, 57);
+  EQ(S(c, b + 1), S(c, sw + 18), T, 58);
+  return 46;
+}
+
+/* BabyjubjubBase8Multiplication :143-171: out[2] | scalar | getBase8 num2Bits adders[0] (doublers[i-1] adders[i])[i=1..253] */
+static size_t ck_bjjmul(ck_t *c, size_t b) {
+  const char *T = "BabyjubjubBase8Multiplication babyjubjub/curve.circom";
+  static const uint64_t B8X[4] = {0x2893f3f6bb957051ULL, 0x2ab8d8010534e0b6ULL, 0x4eacb2e09d6277c1ULL, 0x0bb77a6ad63e739bULL};
+  static const uint64_t B8Y[4] = {0x4b3c257a872d7d8bULL, 0xfce0051fb9e13377ULL, 0x25572e1cd16bf9edULL, 0x25797203f7a0b249ULL};
+  fr_t bx, by;
+  memcpy(bx.l, B8X, 32); memcpy(by.l, B8Y, 32);
+  size_t g8 = b + 3, n2b = b + 5, o = b + 5;
+  req(c, S(c, g8), bx, "GetBabyjubjubBase8 babyjubjub/get.circom", 9, g8);
+  req(c, S(c, g8 + 1), by, "GetBabyjubjubBase8 babyjubjub/get.circom", 10, g8);
+  o += ck_num2bits(c, n2b, 254);
+  EQ(S(c, n2b + 254), S(c, b + 2), T, 150);
+  size_t prev = 0;
+  for (int i = 0; i < 254; i++) {  /* adders[i] is created before doublers[i - 1] (:153-160) */
+    size_t ad = o;
+    o += ck_addzero(c, ad);
+    size_t dbl = 0;
+    if (i > 0) {
+      dbl = o;
+      o += ck_bjjdouble(c, dbl);
+      EQ(S(c, dbl + 2), S(c, prev), T, 162);
+      EQ(S(c, dbl + 3), S(c, prev + 1), T, 162);
+    }
+    fr_t bit = S(c, n2b + 253 - i);
+    EQ(S(c, ad + 2), i == 0 ? fr_zero() : S(c, dbl), T, i == 0 ? 157 : 163);
+    EQ(S(c, ad + 3), i == 0 ? fr_zero() : S(c, dbl + 1), T, i == 0 ? 157 : 163);
+    EQ(S(c, ad + 4), MUL(S(c, g8), bit), T, i == 0 ? 158 : 164);
+    EQ(S(c, ad + 5), MUL(S(c, g8 + 1), bit), T, i == 0 ? 159 : 165);
+    prev = ad;
+  }
+  EQ(S(c, b), S(c, prev), T, 169);
+  EQ(S(c, b + 1), S(c, prev + 1), T, 169);
+  return o - b;
+}
+
+/* ============================================================ big integers (lib/circuits/bigInt) */
+/* KaratsubaOverflow(N) bigIntHelpers.circom:11-53: out[2N] | in[2][N] | A1B1 A2B2 A1A2B1B2 */
+static size_t ck_karatsuba(ck_t *c, size_t b, int N) {
+  const char *T = "KaratsubaOverflow bigInt/bigIntHelpers.circom";
+  size_t out = b, in0 = b + 2 * (size_t)N, in1 = in0 + N;
+  if (N == 1) {
+    EQ(S(c, out), MUL(S(c, in0), S(c, in1)), T, 16);
+    return 4;  /* out[1] is declared and never assigned */
+  }
+  int h = N / 2;
+  size_t k1 = b + 4 * (size_t)N, o = k1;
+  o += ck_karatsuba(c, k1, h);
+  size_t k2 = o;
+  o += ck_karatsuba(c, k2, h);
+  size_t k3 = o;
+  o += ck_karatsuba(c, k3, h);
+#define KI(k, j, i) ((k) + 2 * (size_t)h + (size_t)(j) * h + (i))
+  for (int i = 0; i < h; i++) {
+    EQ(S(c, KI(k1, 0, i)), S(c, in0 + i), T, 23);
+    EQ(S(c, KI(k1, 1, i)), S(c, in1 + i), T, 24);
+    EQ(S(c, KI(k2, 0, i)), S(c, in0 + i + h), T, 25);
+    EQ(S(c, KI(k2, 1, i)), S(c, in1 + i + h), T, 26);
+    EQ(S(c, KI(k3, 0, i)), ADD(S(c, in0 + i), S(c, in0 + i + h)), T, 27);
+    EQ(S(c, KI(k3, 1, i)), ADD(S(c, in1 + i), S(c, in1 + i + h)), T, 28);
+  }
+#undef KI
+  for (int i = 0; i < 2 * N; i++) {
+    fr_t rhs;
+    int mid = h <= i && i < 3 * h;
+    if (i < N) rhs = mid ? SUB(SUB(ADD(S(c, k1 + i), S(c, k3 + i - h)), S(c, k1 + i - h)), S(c, k2 + i - h)) : S(c, k1 + i);
+    else rhs = mid ? SUB(SUB(ADD(S(c, k2 + i - N), S(c, k3 + i - h)), S(c, k1 + i - h)), S(c, k2 + i - h)) : S(c, k2 + i - N);
+    EQ(S(c, out + i), rhs, T, i < N ? (mid ? 34 : 39) : (mid ? 43 : 48));
+  }
+  return o - b;
+}
+
+/* BigMultNonEqualOverflow(n, G, L) bigIntHelpers.circom:55-124: out[G+L-1] | in1[G] in2[L] | tmpMults[G][L] tmpResult[G+L-1][L] */
+static size_t ck_bmneq(ck_t *c, size_t b, int G, int L) {
+  const char *T = "BigMultNonEqualOverflow bigInt/bigIntHelpers.circom";
+  size_t out = b, in1 = b + G + L - 1, in2 = in1 + G, tm = in2 + L, tr = tm + (size_t)G * L;
+#define TM(i, j) S(c, tm + (size_t)(i) * L + (j))
+#define TR(i, j) (tr + (size_t)(i) * L + (j))
+  for (int i = 0; i < G; i++)
+    for (int j = 0; j < L; j++) EQ(TM(i, j), MUL(S(c, in1 + i), S(c, in2 + j)), T, 69);
+  for (int i = 0; i < G + L - 1; i++) {
+    int n;
+    if (i < L) n = i + 1;
+    else if (i < G) n = L;
+    else n = G + L - 1 - i;
+    for (int j = 0; j < n; j++) {
+      fr_t m = (i < G) ? TM(i - j, j) : TM(G - 1 - j, i + j - G + 1);
+      EQ(S(c, TR(i, j)), j == 0 ? m : ADD(m, S(c, TR(i, j - 1))), T, i < L ? 91 : i < G ? 101 : 111);
+    }
+    EQ(S(c, out + i), S(c, TR(i, n - 1)), T, i < L ? 95 : i < G ? 104 : 115);
+  }
+#undef TM
+#undef TR
+  return (size_t)(G + L - 1) + G + L + (size_t)G * L + (size_t)(G + L - 1) * L;
+}
+
+static int karatsuba_path(int G, int L) {
+  /* BigMultOverflow bigIntOverflow.circom:43-53: power-of-two G and is_karatsuba_optimal(G, L)
+   * (bigIntFunc.circom:617-629 with get_a_coeff, dontOpenPlease.circom); the instances here use
+   * G = L in {4, 32, 48, 64}: optimal for 32 and 64, not for 4 (< 8); 48 is not a power of two */
+  if (G != L || !(G == 4 || G == 32 || G == 48 || G == 64)) { fprintf(stderr, "r1cs_check: BigMultOverflow(%d,%d) unsupported\n", G, L); abort(); }
+  return G == 32 || G == 64;
+}
+
+/* BigMultOverflow(n, G, L) bigIntOverflow.circom:38-72: out[G+L-1] | in1[G] in2[L] | karatsuba or mult */
+static size_t ck_bmo(ck_t *c, size_t b, int G, int L) {
+  const char *T = "BigMultOverflow bigInt/bigIntOverflow.circom";
+  size_t out = b, in1 = b + G + L - 1, in2 = in1 + G, sub = in2 + L, sz;
+  if (karatsuba_path(G, L)) {
+    sz = ck_karatsuba(c, sub, G);
+    for (int i = 0; i < G; i++) {
+      EQ(S(c, sub + 2 * G + i), S(c, in1 + i), T, 56);
+      EQ(S(c, sub + 3 * G + i), i < L ? S(c, in2 + i) : fr_zero(), T, i < L ? 58 : 61);
+    }
+    for (int i = 0; i < G + L - 1; i++) EQ(S(c, out + i), S(c, sub + i), T, 64);
+  } else {
+    sz = ck_bmneq(c, sub, G, L);
+    for (int i = 0; i < G; i++) EQ(S(c, sub + G + L - 1 + i), S(c, in1 + i), T, 68);
+    for (int i = 0; i < L; i++) EQ(S(c, sub + G + L - 1 + G + i), S(c, in2 + i), T, 69);
+    for (int i = 0; i < G + L - 1; i++) EQ(S(c, out + i), S(c, sub + i), T, 70);
+  }
+  return (size_t)(G + L - 1) + G + L + sz;
+}
+
+/* BigLessEqThan(n, K) bigIntComparators.circom:50-75: out | in[2][K] | result[K] | (lessThan[i] isEqual[i])[K] */
+static size_t ck_blet(ck_t *c, size_t b, int n, int K) {
+  const char *T = "BigLessEqThan bigInt/bigIntComparators.circom";
+  size_t in0 = b + 1, in1 = in0 + K, res = in1 + K, o = res + K;
+  for (int i = 0; i < K; i++) {
+    size_t lt = o;
+    o += ck_lessthan(c, lt, n);
+    EQ(S(c, lt + 1), S(c, in0 + i), T, 60);
+    EQ(S(c, lt + 2), S(c, in1 + i), T, 61);
+    size_t eq = o;
+    o += ck_isequal(c, eq);
+    EQ(S(c, eq + 1), S(c, in0 + i), T, 64);
+    EQ(S(c, eq + 2), S(c, in1 + i), T, 65);
+    EQ(S(c, res + i), i == 0 ? ADD(S(c, lt), S(c, eq)) : ADD(S(c, lt), MUL(S(c, eq), S(c, res + i - 1))), T, i == 0 ? 70 : 72);
+  }
+  EQ(S(c, b), S(c, res + K - 1), T, 76);
+  return o - b;
+}
+
+/* BigGreaterThan(n, K) bigIntComparators.circom:79-87: out | in[2][K] | lessEqThan */
+static size_t ck_bgt(ck_t *c, size_t b, int n, int K) {
+  const char *T = "BigGreaterThan bigInt/bigIntComparators.circom";
+  size_t le = b + 1 + 2 * (size_t)K;
+  size_t sz = 1 + 2 * (size_t)K + ck_blet(c, le, n, K);
+  for (int i = 0; i < 2 * K; i++) EQ(S(c, le + 1 + i), S(c, b + 1 + i), T, 85);
+  EQ(S(c, b), SUB(KC(1), S(c, le)), T, 86);
+  return sz;
+}
+
+/* BigIntIsZero(n, MAX, K) bigIntComparators.circom:105-129: in[K] | carry[K-1] | carryRangeChecks[K-1] */
+static fr_t INV2_64;
+static size_t ck_bisz(ck_t *c, size_t b, int n, int MAX, int K) {
+  const char *T = "BigIntIsZero bigInt/bigIntComparators.circom";
+  int L = MAX + 3 - n;
+  size_t in = b, carry = b + K, o = carry + K - 1;
+  for (int i = 0; i < K - 1; i++) {
+    size_t rc = o;
+    o += ck_num2bits(c, rc, L);
+    /* carry <== (in + carry_prev) / 2^n: the linear constraint carry * 2^n = in + carry_prev */
+    EQ(MUL(S(c, carry + i), P2[n]), i == 0 ? S(c, in) : ADD(S(c, in + i), S(c, carry + i - 1)), T, i == 0 ? 120 : 123);
+    EQ(S(c, rc + L), ADD(S(c, carry + i), P2[L - 1]), T, 126);
+  }
+  EQ(ADD(S(c, in + K - 1), S(c, carry + K - 2)), fr_zero(), T, 129);
+  return o - b;
+}
+
+static int log_ceil(int n) { int i = 0; while (n) { n /= 2; i++; } return i; }  /* bigIntFunc.circom:20-29 */
+
+/* BigMultModP(n, K, K, K) bigInt.circom:206-272: div[K+1] mod[K] | in1[K] in2[K] modulus[K] |
+ * mult modChecks[K] greaterThan mult2 isZero */
+static size_t ck_bmm(ck_t *c, size_t b, int K) {
+  const char *T = "BigMultModP bigInt/bigInt.circom";
+  const int n = 64, BASE = 2 * K, DIV = K + 1;
+  size_t div = b, mod = b + DIV, in1 = mod + K, in2 = in1 + K, md = in2 + K, o = md + K;
+  size_t mult = o;
+  o += ck_bmo(c, mult, K, K);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, mult + BASE - 1 + i), S(c, in1 + i), T, 218);
+    EQ(S(c, mult + BASE - 1 + K + i), S(c, in2 + i), T, 219);
+  }
+  for (int i = 0; i < K; i++) {
+    size_t mc = o;
+    o += ck_num2bits(c, mc, n);
+    EQ(S(c, mc + n), S(c, mod + i), T, 233);
+  }
+  size_t gt = o;
+  o += ck_bgt(c, gt, n, K);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, gt + 1 + i), S(c, md + i), T, 240);
+    EQ(S(c, gt + 1 + K + i), S(c, mod + i), T, 241);
+  }
+  EQ(S(c, gt), KC(1), T, 242);
+  size_t m2 = o;  /* DIV >= K: BigMultNonEqualOverflow(n, DIV, K)(div, modulus) */
+  o += ck_bmneq(c, m2, DIV, K);
+  for (int i = 0; i < DIV; i++) EQ(S(c, m2 + DIV + K - 1 + i), S(c, div + i), T, 252);
+  for (int i = 0; i < K; i++) EQ(S(c, m2 + DIV + K - 1 + DIV + i), S(c, md + i), T, 253);
+  size_t iz = o;
+  o += ck_bisz(c, iz, n, 2 * n + log_ceil(K + DIV - 1), BASE - 1);
+  for (int i = 0; i < BASE - 1; i++) {
+    fr_t v = SUB(S(c, mult + i), S(c, m2 + i));
+    EQ(S(c, iz + i), i < K ? SUB(v, S(c, mod + i)) : v, T, i < K ? 266 : 269);
+  }
+  return o - b;
+}
+
+/* exp_to_bits bigIntFunc.circom:590-616 (result_counter starts at 0, circom's default for a var) */
+static void exp_to_bits(uint32_t e, int *idx) {
+  int mul_num = 0, res_num = 0, rc = 0, counter = 0;
+  while (e > 0) {
+    int bit = e & 1;
+    e >>= 1;
+    if (bit) { res_num++; idx[rc + 2] = counter; rc++; }
+    mul_num++; counter++;
+  }
+  idx[0] = mul_num - 1;
+  idx[1] = res_num;
+}
+
+/* PowerMod(n, K, EXP) bigInt.circom:280-340: out[K] | base[K] modulus[K] | muls[e0] resultMuls[e1-1] */
+static size_t ck_powermod(ck_t *c, size_t b, int K, uint32_t EXP) {
+  const char *T = "PowerMod bigInt/bigInt.circom";
+  int ep[40] = {0};
+  exp_to_bits(EXP, ep);
+  size_t out = b, base = b + K, modl = base + K, o = modl + K;
+  size_t muls[40], rm[40];
+  for (int i = 0; i < ep[0]; i++) { muls[i] = o; o += ck_bmm(c, o, K); }
+  for (int i = 0; i < ep[1] - 1; i++) { rm[i] = o; o += ck_bmm(c, o, K); }
+#define BIN1(m) ((m) + 2 * (size_t)K + 1)
+#define BIN2(m) (BIN1(m) + K)
+#define BMOD(m) (BIN2(m) + K)
+#define BOUT(m) ((m) + (size_t)K + 1)
+  for (int i = 0; i < ep[0]; i++)
+    for (int j = 0; j < K; j++) EQ(S(c, BMOD(muls[i]) + j), S(c, modl + j), T, 307);
+  for (int i = 0; i < ep[1] - 1; i++)
+    for (int j = 0; j < K; j++) EQ(S(c, BMOD(rm[i]) + j), S(c, modl + j), T, 312);
+  for (int j = 0; j < K; j++) {
+    EQ(S(c, BIN1(muls[0]) + j), S(c, base + j), T, 316);
+    EQ(S(c, BIN2(muls[0]) + j), S(c, base + j), T, 317);
+  }
+  for (int i = 1; i < ep[0]; i++)
+    for (int j = 0; j < K; j++) {
+      EQ(S(c, BIN1(muls[i]) + j), S(c, BOUT(muls[i - 1]) + j), T, 320);
+      EQ(S(c, BIN2(muls[i]) + j), S(c, BOUT(muls[i - 1]) + j), T, 321);
+    }
+  for (int i = 0; i < ep[1] - 1; i++)
+    for (int j = 0; j < K; j++) {
+      fr_t in1;
+      if (i == 0) in1 = ep[2] == 0 ? S(c, base + j) : S(c, BOUT(muls[ep[2] - 1]) + j);
+      else in1 = S(c, BOUT(rm[i - 1]) + j);
+      EQ(S(c, BIN1(rm[i]) + j), in1, T, i == 0 ? 328 : 334);
+      EQ(S(c, BIN2(rm[i]) + j), S(c, BOUT(muls[ep[i + 3] - 1]) + j), T, i == 0 ? 332 : 335);
+    }
+  for (int j = 0; j < K; j++)
+    EQ(S(c, out + j), ep[1] == 1 ? S(c, BOUT(muls[ep[0] - 1]) + j) : S(c, BOUT(rm[ep[1] - 2]) + j), T, 338);
+#undef BIN1
+#undef BIN2
+#undef BMOD
+#undef BOUT
+  return o - b;
+}
+
+/* RsaVerifyPkcs1v15(64, K, EXP, 256) signatures/rsa.circom:16-72:
+ * signature[K] pubkey[K] hashed[256] | hashed_chunks[4] | pm bits2num[3..0] num2bits_6 */
+static size_t ck_rsa_pkcs256(ck_t *c, size_t b, int K, uint32_t EXP) {
+  const char *T = "RsaVerifyPkcs1v15 signatures/rsa.circom";
+  size_t sig = b, pk = b + K, hs = pk + K, hc = hs + 256, o = hc + 4;
+  size_t pm = o;
+  o += ck_powermod(c, pm, K, EXP);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, pm + K + i), S(c, sig + i), T, 29);
+    EQ(S(c, pm + 2 * K + i), S(c, pk + i), T, 30);
+  }
+  for (int i = 0; i < 4; i++) {  /* bits2num[3 - i] created in this order */
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 64);
+    for (int j = 0; j < 64; j++) EQ(S(c, bn + 1 + j), S(c, hs + i * 64 + 63 - j), T, 39);
+    EQ(S(c, hc + 3 - i), S(c, bn), T, 41);
+  }
+  for (int i = 0; i < 4; i++) EQ(S(c, hc + i), S(c, pm + i), T, 46);
+  EQ(S(c, pm + 4), KC(217300885422736416ULL), T, 50);
+  EQ(S(c, pm + 5), KC(938447882527703397ULL), T, 51);
+  size_t n6 = o;
+  o += ck_num2bits(c, n6, 64);
+  EQ(S(c, n6 + 64), S(c, pm + 6), T, 55);
+  static const int rb[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 1, 0, 0, 1, 1, 0, 0, 0, 0};
+  for (int i = 0; i < 32; i++) EQ(S(c, n6 + i), KC(rb[31 - i]), T, 58);
+  for (int i = 32; i < 64; i++) EQ(S(c, n6 + i), KC(1), T, 63);
+  for (int i = 7; i < K - 1; i++) EQ(S(c, pm + i), KC(18446744073709551615ULL), T, 67);
+  return o - b;
+}
+
+/* ============================================================ passport verification */
+/* PassportVerificationFlow(ECS, H, EHT, DG1S, DG15S, SAS, DG15V) passportVerificationFlow.circom:6-109:
+ * flowResult | dg1Hash[H] dg15Hash[H] encapsulatedContent[ECS] encapsulatedContentHash[EHT] signedAttributes[1024] |
+ * verifyAllChecksPassed[3H+8] | dg1Eq[H] dg15Eq[H] encEq[H] prefix[8] */
+static size_t ck_flow(ck_t *c, size_t b, int ECS, int H, int EHT, int DG1S, int DG15S, int SAS, int DG15V) {
+  const char *T = "PassportVerificationFlow passportVerification/passportVerificationFlow.circom";
+  size_t fr_ = b, d1 = b + 1, d15 = d1 + H, ec = d15 + H, ech = ec + ECS, sa = ech + EHT, v = sa + 1024,
+         o = v + 3 * (size_t)H + 8;
+  fr_t aa = KC((uint64_t)DG15V);
+  size_t eq0 = o;
+  for (int i = 0; i < 3 * H + 8; i++) o += ck_isequal(c, o);
+#define EQB(i) (eq0 + 6 * (size_t)(i))
+  for (int i = 0; i < H; i++) {
+    EQ(S(c, EQB(i) + 1), S(c, d1 + i), T, 30);
+    EQ(S(c, EQB(i) + 2), S(c, ec + DG1S + i), T, 31);
+    EQ(S(c, EQB(H + i) + 1), MUL(S(c, d15 + i), aa), T, 45);
+    EQ(S(c, EQB(H + i) + 2), MUL(S(c, ec + DG15S + i), aa), T, 46);
+    EQ(S(c, EQB(2 * H + i) + 1), S(c, ech + i), T, 59);
+    EQ(S(c, EQB(2 * H + i) + 2), S(c, sa + SAS + i), T, 60);
+  }
+  static const int pre[8] = {0, 0, 0, 0, 1, 1, 1, 1};
+  for (int i = 0; i < 8; i++) {
+    EQ(S(c, EQB(3 * H + i) + 1), MUL(KC(pre[i]), aa), T, 74);
+    EQ(S(c, EQB(3 * H + i) + 2), MUL(S(c, ec + DG15S - 24 + i), aa), T, 75);
+  }
+  EQ(S(c, v), S(c, EQB(0)), T, 84);
+  for (int i = 1; i < 3 * H + 8; i++) EQ(S(c, v + i), MUL(S(c, v + i - 1), S(c, EQB(i))), T, 87);
+#undef EQB
+  EQ(S(c, fr_), S(c, v + 3 * H + 7), T, 108);
+  return o - b;
+}
+
+/* ShaHashChunks(B, ALGO) hasher/hash.circom:32-68 (ALGO 224 / 256): out[ALGO] | in[512B] | hashALGO */
+static size_t ck_shahash(ck_t *c, size_t b, int B, int algo) {
+  const char *T = "ShaHashChunks hasher/hash.circom";
+  size_t out = b, in = b + algo, h = in + 512 * (size_t)B;
+  size_t sz = (size_t)algo + 512 * (size_t)B + ck_sha2chunks(c, h, B, algo);
+  for (int i = 0; i < 512 * B; i++) EQ(S(c, h + algo + i), S(c, in + i), T, algo == 256 ? 56 : 51);
+  for (int i = 0; i < algo; i++) EQ(S(c, out + i), S(c, h + i), T, algo == 256 ? 57 : 52);
+  return sz;
+}
+
+typedef struct { int sig, dg_hash, doc, ec_blocks, ec_shift, dg1_shift, aa, dg15_shift, dg15_blocks, aa_shift; } ck_params;
+
+static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : sig >= 20 ? 4 : 32; }
+
+/* PassportVerificationBuilder(...) passportVerificationBuilder.circom:11-246 (RSA PKCS#1 v1.5 over SHA-2):
+ * passportHash | encapsulatedContent dg1 dg15 signedAttributes signature pubkey slaveMerkleInclusionBranches[80]
+ * slaveMerkleRoot | dg1Hash dg15Hash encapsulatedContentHash signedAttributesHash pubkeyHash tempModulus[5] |
+ * dg1PassportHasher [dg15PassportHasher] ecPassportHasher saPassportHasher passportVerificationFlow
+ * signatureVerification signedAttributesNum pubkeyHasherRsa smtVerifier signedAttributesHashHasher */
+static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
+  const char *T = "PassportVerificationBuilder passportVerification/passportVerificationBuilder.circom";
+  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = 256, ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
+  size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + K,
+         br = pk + K, root = br + 80;
+  size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1, o = tmod + 5;
+  size_t hs = o;
+  o += ck_shahash(c, hs, 2, DGH);
+  for (int j = 0; j < 1024; j++) EQ(S(c, hs + DGH + j), S(c, dg1 + j), T, 97);
+  for (int j = 0; j < DGH; j++) EQ(S(c, d1h + j), S(c, hs + j), T, 98);
+  if (P->aa) {
+    hs = o;
+    o += ck_shahash(c, hs, P->dg15_blocks, DGH);
+    for (int j = 0; j < D15L; j++) EQ(S(c, hs + DGH + j), S(c, dg15 + j), T, 111);
+    for (int j = 0; j < DGH; j++) EQ(S(c, d15h + j), S(c, hs + j), T, 113);
+  } else {
+    for (int j = 0; j < DGH; j++) EQ(S(c, d15h + j), fr_zero(), T, 118);
+  }
+  hs = o;
+  o += ck_shahash(c, hs, P->ec_blocks, HT);
+  for (int j = 0; j < ECL; j++) EQ(S(c, hs + HT + j), S(c, ec + j), T, 124);
+  for (int j = 0; j < HT; j++) EQ(S(c, ech + j), S(c, hs + j), T, 126);
+  hs = o;
+  o += ck_shahash(c, hs, 2, HT);
+  for (int j = 0; j < 1024; j++) EQ(S(c, hs + HT + j), S(c, sa + j), T, 129);
+  for (int j = 0; j < HT; j++) EQ(S(c, sah + j), S(c, hs + j), T, 130);
+  size_t fl = o;
+  o += ck_flow(c, fl, ECL, DGH, HT, P->dg1_shift, P->aa ? P->dg15_shift : DGH, P->ec_shift, P->aa);
+  for (int j = 0; j < DGH; j++) {
+    EQ(S(c, fl + 1 + j), S(c, d1h + j), T, 140);
+    EQ(S(c, fl + 1 + DGH + j), S(c, d15h + j), T, 141);
+  }
+  for (int j = 0; j < ECL; j++) EQ(S(c, fl + 1 + 2 * DGH + j), S(c, ec + j), T, 142);
+  for (int j = 0; j < HT; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + j), S(c, ech + j), T, 143);
+  for (int j = 0; j < 1024; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + HT + j), S(c, sa + j), T, 144);
+  EQ(S(c, fl), KC(1), T, 146);
+  size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[K] signature[K] hashed[256] | rsa */
+  const char *TV = "VerifySignature signatureVerifier/signatureVerification.circom";
+  size_t rsa = sv + 2 * (size_t)K + HT;
+  o += 2 * (size_t)K + HT + ck_rsa_pkcs256(c, rsa, K, 65537);
+  for (int i = 0; i < K; i++) {
+    req(c, S(c, rsa + K + i), S(c, sv + i), TV, 124, sv);
+    req(c, S(c, rsa + i), S(c, sv + K + i), TV, 125, sv);
+  }
+  for (int i = 0; i < HT; i++) req(c, S(c, rsa + 2 * K + i), S(c, sv + 2 * K + i), TV, 126, sv);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, sv + K + i), S(c, sig + i), T, 150);
+    EQ(S(c, sv + i), S(c, pk + i), T, 151);
+  }
+  for (int i = 0; i < HT; i++) EQ(S(c, sv + 2 * K + i), S(c, sah + i), T, 152);
+  size_t san = o;
+  o += ck_bits2num(c, san, 252);
+  for (int i = 0; i < 252; i++) EQ(S(c, san + 1 + i), S(c, sah + i), T, 159);
+  size_t pkr = o;
+  o += ck_poseidon(c, pkr, 5);
+  for (int i = 0; i < 5; i++) {
+    EQ(S(c, tmod + i), ADD(MUL(S(c, pk + 3 * i), P2[128]), MUL(S(c, pk + 3 * i + 1), P2[64])), T, 176);
+    EQ(S(c, pkr + 1 + i), ADD(S(c, tmod + i), S(c, pk + 3 * i + 2)), T, 177);
+  }
+  EQ(S(c, pkh), S(c, pkr), T, 179);
+  size_t smt = o;
+  o += ck_smt(c, smt, 80);
+  EQ(S(c, smt + 1), S(c, root), T, 226);
+  EQ(S(c, smt + 2), S(c, pkh), T, 227);
+  EQ(S(c, smt + 3), S(c, pkh), T, 228);
+  for (int i = 0; i < 80; i++) EQ(S(c, smt + 4 + i), S(c, br + i), T, 229);
+  size_t sh = o;
+  o += ck_poseidon(c, sh, 1);
+  EQ(S(c, sh + 1), S(c, san), T, 234);
+  EQ(S(c, ph), S(c, sh), T, 235);
+  return o - b;
+}
+
+/* RegisterIdentity(DG15_SIZE, HBS, SIG, DOC, AA, AA_SHIFT) identityManagement/identity.circom:6-121:
+ * dg15PubKeyHash dg1Commitment pkIdentityHash | dg1[1024] dg15[..] skIdentity | AA key hashing components,
+ * dg1Hasher dg1Chunking[4] skIndentityHasher pkIdentityCalc pkIdentityHasher */
+static size_t ck_regid(ck_t *c, size_t b, const ck_params *P) {
+  const char *T = "RegisterIdentity identityManagement/identity.circom";
+  const int D15L = P->dg15_blocks * 512;
+  size_t d15ph = b, d1c = b + 1, pkih = b + 2, dg1 = b + 3, dg15 = dg1 + 1024, sk = dg15 + D15L, o = sk + 1;
+  if (P->aa && P->aa < 20) {
+    size_t ch[5];
+    for (int j = 0; j < 5; j++) {
+      int L = j < 4 ? 200 : 224;
+      ch[j] = o;
+      o += ck_bits2num(c, o, L);
+      for (int i = 0; i < L; i++) EQ(S(c, ch[j] + 1 + L - 1 - i), S(c, dg15 + P->aa_shift + j * 200 + i), T, j < 4 ? 34 : 40);
+    }
+    size_t h = o;
+    o += ck_poseidon(c, h, 5);
+    for (int i = 0; i < 5; i++) EQ(S(c, h + 1 + i), S(c, ch[i]), T, 46);
+    EQ(S(c, d15ph), S(c, h), T, 49);
+  } else if (P->aa >= 20) {
+    int HS = 248, EFS = 256;
+    if (P->aa == 22) EFS = 320;
+    if (P->aa == 23) { EFS = 192; HS = 192; }
+    int XY = EFS - HS;
+    size_t xn = o;
+    o += ck_bits2num(c, xn, HS);
+    size_t yn = o;
+    o += ck_bits2num(c, yn, HS);
+    for (int i = 0; i < HS; i++) {
+      EQ(S(c, xn + 1 + HS - 1 - i), S(c, dg15 + P->aa_shift + i + XY), T, 73);
+      EQ(S(c, yn + 1 + HS - 1 - i), S(c, dg15 + P->aa_shift + EFS + i + XY), T, 74);
+    }
+    size_t h = o;
+    o += ck_poseidon(c, h, 2);
+    EQ(S(c, h + 1), S(c, xn), T, 79);
+    EQ(S(c, h + 2), S(c, yn), T, 80);
+    EQ(S(c, d15ph), S(c, h), T, 82);
+  } else {
+    EQ(S(c, d15ph), fr_zero(), T, 86);
+  }
+  size_t dh = o;
+  o += ck_poseidon(c, dh, 5);
+  const int CS = P->doc == 1 ? 190 : 186;
+  for (int i = 0; i < 4; i++) {
+    size_t ch = o;
+    o += ck_bits2num(c, ch, CS);
+    for (int j = 0; j < CS; j++) EQ(S(c, ch + 1 + j), S(c, dg1 + i * CS + j), T, 99);
+    EQ(S(c, dh + 1 + i), S(c, ch), T, 101);
+  }
+  size_t skh = o;
+  o += ck_poseidon(c, skh, 1);
+  EQ(S(c, skh + 1), S(c, sk), T, 105);
+  EQ(S(c, dh + 5), S(c, skh), T, 106);
+  EQ(S(c, d1c), S(c, dh), T, 108);
+  size_t pc = o;
+  o += ck_bjjmul(c, pc);
+  EQ(S(c, pc + 2), S(c, sk), T, 113);
+  size_t ph = o;
+  o += ck_poseidon(c, ph, 2);
+  EQ(S(c, ph + 1), S(c, pc), T, 116);
+  EQ(S(c, ph + 2), S(c, pc + 1), T, 117);
+  EQ(S(c, pkih), S(c, ph), T, 119);
+  return o - b;
+}
+
+/* RegisterIdentityBuilder(...) identityManagement/registerIdentityBuilder.circom:41-196, main (public
+ * slaveMerkleRoot): [1] dg15PubKeyHash passportHash dg1Commitment pkIdentityHash | slaveMerkleRoot
+ * encapsulatedContent dg1 dg15 signedAttributes signature pubkey slaveMerkleInclusionBranches skIdentity |
+ * passportVerifier registerIdentity */
+static size_t ck_builder(ck_t *c, size_t b, const ck_params *P) {
+  const char *T = "RegisterIdentityBuilder identityManagement/registerIdentityBuilder.circom";
+  const int K = sig_K(P->sig), ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
+  size_t d15ph = b, ph = b + 1, d1c = b + 2, pkih = b + 3, root = b + 4, ec = b + 5, dg1 = ec + ECL, dg15 = dg1 + 1024,
+         sa = dg15 + D15L, sig = sa + 1024, pk = sig + K, br = pk + K, sk = br + 80, o = sk + 1;
+  size_t pv = o;
+  o += ck_pvb(c, pv, P);
+  size_t pv_ec = pv + 1, pv_dg1 = pv_ec + ECL, pv_dg15 = pv_dg1 + 1024, pv_sa = pv_dg15 + D15L, pv_sig = pv_sa + 1024,
+         pv_pk = pv_sig + K, pv_br = pv_pk + K, pv_root = pv_br + 80;
+  for (int i = 0; i < ECL; i++) EQ(S(c, pv_ec + i), S(c, ec + i), T, 174);
+  for (int i = 0; i < 1024; i++) EQ(S(c, pv_dg1 + i), S(c, dg1 + i), T, 175);
+  for (int i = 0; i < D15L; i++) EQ(S(c, pv_dg15 + i), S(c, dg15 + i), T, 176);
+  for (int i = 0; i < 1024; i++) EQ(S(c, pv_sa + i), S(c, sa + i), T, 177);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, pv_sig + i), S(c, sig + i), T, 178);
+    EQ(S(c, pv_pk + i), S(c, pk + i), T, 179);
+  }
+  for (int i = 0; i < 80; i++) EQ(S(c, pv_br + i), S(c, br + i), T, 180);
+  EQ(S(c, pv_root), S(c, root), T, 181);
+  EQ(S(c, ph), S(c, pv), T, 182);
+  size_t ri = o;
+  o += ck_regid(c, ri, P);
+  for (int i = 0; i < 1024; i++) EQ(S(c, ri + 3 + i), S(c, dg1 + i), T, 193);
+  for (int i = 0; i < D15L; i++) EQ(S(c, ri + 3 + 1024 + i), S(c, dg15 + i), T, 194);
+  EQ(S(c, ri + 3 + 1024 + D15L), S(c, sk), T, 195);
+  EQ(S(c, d15ph), S(c, ri), T, 196);
+  EQ(S(c, d1c), S(c, ri + 1), T, 197);
+  EQ(S(c, pkih), S(c, ri + 2), T, 198);
+  return o - b;
+}
+
+/* ============================================================ entry points */
+static int ck_ready = 0;
+static void ck_init(void) {
+  if (ck_ready) return;
+  for (int i = 0; i < 254; i++) P2[i] = fr_pow2(i);
+  INV2_64 = fr_inv(P2[64]);
+  ck_ready = 1;
+}
+
+typedef struct {
+  uint64_t n_constraints, n_failed, n_uncovered, size_walked;
+  int64_t first_failed;
+  int32_t first_line, oob;
+  char first_template[96];
+  uint64_t first_component;
+  int64_t first_uncovered;
+  uint64_t n_uncovered_nonzero;  /* uncovered signals holding a non-zero value (an unassigned signal is 0) */
+} ck_report;
+
+static ck_t ck_begin(const uint8_t *wit, size_t n) {
+  ck_init();
+  ck_t c;
+  memset(&c, 0, sizeof c);
+  c.w = (const fr_t *)wit;
+  c.n = n;
+  c.cov = calloc(n, 1);
+  c.first_bad = -1;
+  return c;
+}
+
+static int ck_end(ck_t *c, size_t walked, ck_report *r) {
+  memset(r, 0, sizeof *r);
+  r->n_constraints = c->n_cons;
+  r->n_failed = c->n_bad;
+  r->first_failed = c->first_bad;
+  r->first_line = c->first_line;
+  r->first_component = c->first_at;
+  r->oob = c->oob;
+  r->size_walked = walked;
+  if (c->first_tmpl) snprintf(r->first_template, sizeof r->first_template, "%s", c->first_tmpl);
+  r->first_uncovered = -1;
+  c->cov[0] = 1;  /* the constant 1 */
+  for (size_t i = 0; i < c->n; i++)
+    if (!c->cov[i]) {
+      if (r->first_uncovered < 0) r->first_uncovered = (int64_t)i;
+      r->n_uncovered++;
+      if (!fr_is_zero(c->w[i])) r->n_uncovered_nonzero++;
+    }
+  free(c->cov);
+  return (c->n_bad || c->oob || walked != c->n || r->n_uncovered_nonzero) ? 1 : 0;
+}
+
+int ck_sha256(int B, const uint8_t *wit, size_t n, ck_report *r) {
+  ck_t c = ck_begin(wit, n);
+  size_t walked = 1 + ck_sha2chunks(&c, 1, B, 256);
+  return ck_end(&c, walked, r);
+}
+
+int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r) {
+  if (!pos_loaded) return -1;
+  ck_t c = ck_begin(wit, nw);
+  size_t walked = 1 + ck_poseidon(&c, 1, n);
+  return ck_end(&c, walked, r);
+}
+
+/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 over SHA-256 (SIG 1, 2) with DG hash 224 / 256 */
+int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r) {
+  if (!pos_loaded) return -1;
+  if (!(P->sig == 1 || P->sig == 2) || !(P->dg_hash == 256 || P->dg_hash == 224)) return -2;
+  ck_t c = ck_begin(wit, nw);
+  size_t walked = 1 + ck_builder(&c, 1, P);
+  req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);
+  return ck_end(&c, walked, r);
+}

@@ -1,0 +1,107 @@
+"""CPU: the constraint checker (oracle/r1cs_check.c) over oracle witnesses.
+
+The reference accepts a witness when every constraint of the compiled circuit holds
+(circom_tester checkConstraints, test/automatisationTest.js:51). r1cs_check.c restates the
+constraints of every template on the path from the .circom sources — walking the component tree
+itself in the --O0 numbering — and evaluates them on a witness. Here it pins the oracle's
+intermediate signals (values the witness restatement computes but no reference-run fixture covers):
+a witness passes only if the checker's own allocation matches the oracle's signal for signal and
+every `<==` / `===` holds. tests/test_gpu_r1cs.py applies the same checker to device witnesses.
+
+Signals no constraint reads: the declared-but-never-assigned tmpResult entries of
+BigMultNonEqualOverflow (bigIntHelpers.circom:83-118, the triangle outside each row's sum), 992 per
+BigMultModP(64,32,32,32) and 4,032 per BigMultModP(64,64,64,64); they must hold 0.
+"""
+import numpy as np
+import pytest
+
+from pzkwit import field, inputs as I
+
+pyr1cs = pytest.importorskip("pyr1cs")
+
+UNASSIGNED_PER_BMM = {32: 992, 64: 4032}
+
+
+def _ok(res, uncovered):
+    rc, r = res
+    assert r["oob"] == 0 and r["n_failed"] == 0, r
+    assert r["n_uncovered"] == uncovered and r["n_uncovered_nonzero"] == 0, r
+    assert rc == 0, r
+    return r
+
+
+def test_poseidon_circuits(oracle):
+    for n in (1, 2, 3, 4, 5):
+        for ins in ([0] * n, [field.P - 1 - i for i in range(n)], [field.SplitMix64(n).fr() for _ in range(n)]):
+            rc, w = oracle.poseidon_witness(ins)
+            assert rc == 0
+            _ok(pyr1cs.check_poseidon(w, n), 0)
+
+
+def test_sha256_config2(oracle):
+    _, rows = I.sha256_config2_batch(3, seed=2, blocks=6)
+    for r in rows:
+        rc, w = oracle.sha256_witness(r, 6)
+        assert rc == 0
+        rep = _ok(pyr1cs.check_sha256(w, 6), 0)
+        assert rep["size_walked"] == w.shape[0]
+
+
+REGISTER_CASES = [
+    ("canonical", dict(I.CANONICAL), 0),
+    ("canonical_smt7", dict(I.CANONICAL), 7),
+    ("canonical_smt79", dict(I.CANONICAL), 79),
+    ("rsa4096", dict(I.CANONICAL, sig=2), 3),
+    ("td1_no_aa", dict(I.CANONICAL, doc=1, aa=0), 0),
+    ("ec_aa", dict(I.CANONICAL, aa=20), 0),
+    ("dg224", dict(I.CANONICAL, dg_hash=224, dg15_shift=1496), 0),
+]
+
+
+def _register_witness(oracle, params, depth, idx=0, seed=0x31):
+    g = I.PassportGen(seed=seed, n_keys=2, params=params, workers=1)
+    pp = g.passport_at(idx, smt_depth=depth)
+    if pp["root"] is None:
+        pp["root"] = field.SplitMix64(idx).fr()  # the SMT check is not enforced (passportVerificationBuilder.circom:240)
+    row = I.pack_register_inputs(pp, params)
+    rc, w = oracle.register_witness(oracle.register_params(**params), row)
+    return rc, w
+
+
+@pytest.mark.parametrize("name,params,depth", REGISTER_CASES, ids=[c[0] for c in REGISTER_CASES])
+def test_register_oracle_witness_satisfies_constraints(oracle, name, params, depth):
+    rc, w = _register_witness(oracle, params, depth)
+    assert rc == 0
+    K = I.sig_input_len(params["sig"])
+    r = _ok(pyr1cs.check_register(w, **params), 17 * UNASSIGNED_PER_BMM[K])
+    assert r["size_walked"] == w.shape[0]
+
+
+def test_tampered_signals_break_constraints(oracle):
+    """One flipped bit anywhere (a SHA round bit, a Karatsuba node, a BigIntIsZero carry, a Poseidon
+    S-box, a BabyJubJub ladder point, ...) violates at least one constraint."""
+    rc, w = _register_witness(oracle, dict(I.CANONICAL), 3)
+    assert rc == 0
+    rng = np.random.default_rng(7)
+    covered = pyr1cs.check_register(w, **I.CANONICAL)[1]
+    assert covered["n_failed"] == 0
+    for idx in list(rng.integers(1, w.shape[0], 40)) + [2, 5, w.shape[0] - 1]:
+        v = w.copy()
+        v[idx, 0] ^= 1
+        if int.from_bytes(v[idx].tobytes(), "little") >= field.P:
+            continue
+        rc, r = pyr1cs.check_register(v, **I.CANONICAL)
+        assert rc != 0 and (r["n_failed"] > 0 or r["n_uncovered_nonzero"] > 0), idx
+
+
+def test_invalid_signature_witness_fails_constraints(oracle):
+    """A passport whose signature does not verify: the oracle flags its check site, and the same
+    witness violates the RSA constraints (rsa.circom:46-67)."""
+    g = I.PassportGen(seed=0x32, n_keys=2, workers=1)
+    pp = g.passport_at(1)
+    pp["sig"] = (pp["sig"] + 1) % pp["n"]
+    rc, w = oracle.register_witness(oracle.register_params(**I.CANONICAL), I.pack_register_inputs(pp))
+    assert rc != 0
+    rc2, r = pyr1cs.check_register(w, **I.CANONICAL)
+    assert rc2 != 0 and r["n_failed"] > 0
+    assert "RsaVerifyPkcs1v15" in r["first_template"] or "BigIntIsZero" in r["first_template"], r

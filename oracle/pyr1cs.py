@@ -32,7 +32,7 @@ def lib():
         if not os.path.exists(LIB):
             subprocess.check_call(["make", "-s", "-C", HERE])
         L = ctypes.CDLL(LIB)
-        for fn in ("ck_sha256", "ck_poseidon_circuit"):
+        for fn in ("ck_sha256", "ck_sha1", "ck_poseidon_circuit"):
             getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
         L.ck_load_poseidon.argtypes = [ctypes.c_char_p]
         L.ck_register.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
@@ -46,6 +46,11 @@ def _run(fn, arg, wit):
     r = Report()
     rc = getattr(lib(), fn)(arg, w.ctypes.data, w.shape[0], ctypes.byref(r))
     return rc, r.as_dict()
+
+
+def check_sha1(wit, blocks):
+    """Sha1HashChunks(blocks) as main."""
+    return _run("ck_sha1", blocks, wit)
 
 
 def check_sha256(wit, blocks):

@@ -429,6 +429,213 @@ static size_t ck_sha2chunks(ck_t *c, size_t b, int B, int O) {
   return o - b;
 }
 
+/* ============================================================ SHA-1 (hasher/sha1) */
+/* RotL(32, L) rotate.circom: out[32] | in[32] */
+static size_t ck_rotl(ck_t *c, size_t b, int L) {
+  for (int i = 31; i >= 0; i--) EQ(S(c, b + i), S(c, b + 32 + (i + L) % 32), "RotL hasher/sha1/rotate.circom", 8);
+  return 64;
+}
+/* H(x) / K(t) constants.circom: out[32] | bitify (Num2Bits(32)) */
+static size_t ck_sha1const(ck_t *c, size_t b, uint32_t v, int line) {
+  const char *T = "H / K hasher/sha1/constants.circom";
+  size_t n = b + 32;
+  size_t sz = 32 + ck_num2bits(c, n, 32);
+  EQ(S(c, n + 32), KC(v), T, line);
+  for (int k = 0; k < 32; k++) EQ(S(c, b + k), S(c, n + 31 - k), T, line + 2);
+  return sz;
+}
+/* Xor4(n) xor4.circom: out[n] | a b c d | mid[n] aTemp[n] */
+static size_t ck_xor4(ck_t *c, size_t b) {
+  const char *T = "Xor4 hasher/sha1/xor4.circom";
+  size_t out = b, a = b + 32, bb = b + 64, cc = b + 96, d = b + 128, mid = b + 160, at = b + 192;
+  for (int k = 0; k < 32; k++) {
+    fr_t B = S(c, bb + k), C = S(c, cc + k), M = S(c, mid + k), A = S(c, at + k), D = S(c, d + k);
+    EQ(M, MUL(B, C), T, 15);
+    EQ(A, SUB(ADD(ADD(MUL(S(c, a + k), ADD(SUB(SUB(KC(1), MUL(KC(2), B)), MUL(KC(2), C)), MUL(KC(4), M))), B), C), MUL(KC(2), M)), T, 16);
+    EQ(S(c, out + k), ADD(SUB(A, MUL(MUL(KC(2), D), A)), D), T, 17);
+  }
+  return 224;
+}
+/* BinSum(NUM, LEN) bitify/operations.circom:9-29: out[LEN+NUM-1] | in[NUM][LEN] | sumN bits2Num[NUM] num2Bits */
+static size_t ck_binsum(ck_t *c, size_t b, int N, int L) {
+  const char *T = "BinSum bitify/operations.circom";
+  int OL = L + N - 1;
+  size_t out = b, in = b + OL, sn = in + (size_t)N * L, o = sn;
+  o += ck_getsum(c, sn, N);
+  for (int i = 0; i < N; i++) {
+    size_t bn = o;
+    o += ck_bits2num(c, bn, L);
+    for (int k = 0; k < L; k++) EQ(S(c, bn + 1 + k), S(c, in + (size_t)i * L + k), T, 22);
+    EQ(S(c, sn + 1 + i), S(c, bn), T, 23);
+  }
+  size_t nb = o;
+  o += ck_num2bits(c, nb, OL);
+  EQ(S(c, nb + OL), S(c, sn), T, 26);
+  for (int k = 0; k < OL; k++) EQ(S(c, out + k), S(c, nb + k), T, 28);
+  return o - b;
+}
+/* fT(t) f.circom: out[32] | b c d | maj (MajT) parity (ParityT -> XOR3_v3) ch (ChT) */
+static size_t ck_ft(ck_t *c, size_t b, int t) {
+  const char *T = "fT hasher/sha1/f.circom";
+  size_t out = b, ib = b + 32, ic = b + 64, id = b + 96;
+  size_t mj = b + 128;               /* MajT: out | a b c | mid : 160 */
+  size_t pa = mj + 160;              /* ParityT: out | a b c | xor3 (XOR3_v3: out | a b c | mid : 160) : 128 + 160 */
+  size_t x3 = pa + 128;
+  size_t ch = x3 + 160;              /* ChT: out | a b c : 128 */
+  for (int k = 0; k < 32; k++) {
+    fr_t A, B, C;
+    /* ChT :5-14 */
+    EQ(S(c, ch + 32 + k), S(c, ib + k), T, 31); EQ(S(c, ch + 64 + k), S(c, ic + k), T, 32); EQ(S(c, ch + 96 + k), S(c, id + k), T, 33);
+    A = S(c, ch + 32 + k); B = S(c, ch + 64 + k); C = S(c, ch + 96 + k);
+    req(c, S(c, ch + k), ADD(MUL(A, SUB(B, C)), C), "ChT hasher/sha1/f.circom", 12, ch);
+    /* ParityT parity.circom -> XOR3_v3 sha2Common.circom:102-113 */
+    EQ(S(c, pa + 32 + k), S(c, ib + k), T, 38); EQ(S(c, pa + 64 + k), S(c, ic + k), T, 39); EQ(S(c, pa + 96 + k), S(c, id + k), T, 40);
+    req(c, S(c, x3 + 32 + k), S(c, pa + 32 + k), "ParityT hasher/sha1/parity.circom", 13, pa);
+    req(c, S(c, x3 + 64 + k), S(c, pa + 64 + k), "ParityT hasher/sha1/parity.circom", 14, pa);
+    req(c, S(c, x3 + 96 + k), S(c, pa + 96 + k), "ParityT hasher/sha1/parity.circom", 15, pa);
+    A = S(c, x3 + 32 + k); B = S(c, x3 + 64 + k); C = S(c, x3 + 96 + k);
+    fr_t M = S(c, x3 + 128 + k);
+    req(c, M, MUL(B, C), "XOR3_v3 hasher/sha2/sha2Common.circom", 110, x3);
+    req(c, S(c, x3 + k), SUB(ADD(ADD(MUL(A, ADD(SUB(SUB(KC(1), MUL(KC(2), B)), MUL(KC(2), C)), MUL(KC(4), M))), B), C), MUL(KC(2), M)),
+        "XOR3_v3 hasher/sha2/sha2Common.circom", 111, x3);
+    req(c, S(c, pa + k), S(c, x3 + k), "ParityT hasher/sha1/parity.circom", 19, pa);
+    /* MajT :16-27 */
+    EQ(S(c, mj + 32 + k), S(c, ib + k), T, 45); EQ(S(c, mj + 64 + k), S(c, ic + k), T, 46); EQ(S(c, mj + 96 + k), S(c, id + k), T, 47);
+    A = S(c, mj + 32 + k); B = S(c, mj + 64 + k); C = S(c, mj + 96 + k);
+    M = S(c, mj + 128 + k);
+    req(c, M, MUL(B, C), "MajT hasher/sha1/f.circom", 24, mj);
+    req(c, S(c, mj + k), ADD(MUL(A, SUB(ADD(B, C), MUL(KC(2), M))), M), "MajT hasher/sha1/f.circom", 25, mj);
+    size_t src = t <= 19 ? ch : (t <= 39 || t >= 60) ? pa : mj;
+    EQ(S(c, out + k), S(c, src + k), T, t <= 19 ? 52 : (t <= 39 || t >= 60) ? 57 : 61);
+  }
+  return ch + 128 - b;
+}
+/* T(t) t.circom:8-57: out[32] | a b c d e kT w | rotatel5 f sumBinary (BinSum(5,32)) sum (Bits2Num(35)) getLastNBits(32) */
+static size_t ck_sha1t(ck_t *c, size_t b, int t) {
+  const char *T = "T hasher/sha1/t.circom";
+  size_t out = b, a = b + 32, bb = b + 64, cc = b + 96, d = b + 128, e = b + 160, kt = b + 192, w = b + 224, o = b + 256;
+  size_t r5 = o;
+  o += ck_rotl(c, r5, 5);
+  size_t f = o;
+  o += ck_ft(c, f, t);
+  for (int k = 0; k < 32; k++) {
+    EQ(S(c, r5 + 32 + k), S(c, a + k), T, 27);
+    EQ(S(c, f + 32 + k), S(c, bb + k), T, 28);
+    EQ(S(c, f + 64 + k), S(c, cc + k), T, 29);
+    EQ(S(c, f + 96 + k), S(c, d + k), T, 30);
+  }
+  size_t bs = o;
+  o += ck_binsum(c, bs, 5, 32);
+  for (int k = 0; k < 32; k++) {
+    size_t in = bs + 36;
+    EQ(S(c, in + k), S(c, r5 + 31 - k), T, 37);
+    EQ(S(c, in + 32 + k), S(c, f + 31 - k), T, 38);
+    EQ(S(c, in + 64 + k), S(c, e + 31 - k), T, 39);
+    EQ(S(c, in + 96 + k), S(c, kt + 31 - k), T, 40);
+    EQ(S(c, in + 128 + k), S(c, w + 31 - k), T, 41);
+  }
+  size_t sm = o;
+  o += ck_bits2num(c, sm, 35);
+  for (int k = 0; k < 35; k++) EQ(S(c, sm + 1 + k), S(c, bs + k), T, 46);
+  size_t gl = o;
+  o += ck_lastnbits(c, gl, 32);
+  EQ(S(c, gl + 33), S(c, sm), T, 51);
+  for (int k = 0; k < 32; k++) EQ(S(c, out + k), S(c, gl + 1 + 31 - k), T, 54);
+  return o - b;
+}
+/* Sha1compression sha1compression.circom:7-132: out[160] | hin[160] inp[512] | a b c d e [81][32] w[80][32] |
+ * rotl1[64] xor4[64] rotl30[80] kT[80] tTmp[80] fSum[5] */
+static const uint32_t SHA1_K[4] = {0x5a827999, 0x6ed9eba1, 0x8f1bbcdc, 0xca62c1d6};
+static size_t ck_sha1comp(ck_t *c, size_t b) {
+  const char *T = "Sha1compression hasher/sha1/sha1compression.circom";
+  size_t out = b, hin = b + 160, inp = hin + 160, A = inp + 512, B = A + 81 * 32, C = B + 81 * 32, D = C + 81 * 32,
+         E = D + 81 * 32, Wd = E + 81 * 32, o = Wd + 80 * 32;
+  size_t r1 = o; o += 64 * 64;
+  size_t x4 = o; o += 64 * 224;
+  size_t r30 = o; o += 80 * 64;
+  size_t kt = o;
+  size_t kt_at[80];
+  for (int i = 0; i < 80; i++) { kt_at[i] = o; o += ck_sha1const(c, o, SHA1_K[i / 20], 29); }
+  (void)kt;
+  size_t tt[80];
+  for (int i = 0; i < 80; i++) { tt[i] = o; o += ck_sha1t(c, o, i); }
+  size_t fs[5];
+  for (int i = 0; i < 5; i++) { fs[i] = o; o += ck_binsum(c, o, 2, 32); }
+  for (int i = 0; i < 64; i++) { ck_rotl(c, r1 + 64 * (size_t)i, 1); ck_xor4(c, x4 + 224 * (size_t)i); ck_rotl(c, r30 + 64 * (size_t)i, 30); }
+  for (int i = 64; i < 80; i++) ck_rotl(c, r30 + 64 * (size_t)i, 30);
+#define WB(t, k) (Wd + 32 * (size_t)(t) + (k))
+  for (int t = 0; t < 16; t++)
+    for (int k = 0; k < 32; k++) EQ(S(c, WB(t, k)), S(c, inp + t * 32 + k), T, 60);
+  for (int t = 16; t < 80; t++) {
+    size_t X = x4 + 224 * (size_t)(t - 16), R = r1 + 64 * (size_t)(t - 16);
+    for (int k = 0; k < 32; k++) {
+      EQ(S(c, X + 32 + k), S(c, WB(t - 3, k)), T, 66);
+      EQ(S(c, X + 64 + k), S(c, WB(t - 8, k)), T, 67);
+      EQ(S(c, X + 96 + k), S(c, WB(t - 14, k)), T, 68);
+      EQ(S(c, X + 128 + k), S(c, WB(t - 16, k)), T, 69);
+      EQ(S(c, R + 32 + k), S(c, X + k), T, 72);
+      EQ(S(c, WB(t, k)), S(c, R + k), T, 75);
+    }
+  }
+#define AB(arr, t, k) ((arr) + 32 * (size_t)(t) + (k))
+  for (int k = 0; k < 32; k++) {
+    EQ(S(c, AB(A, 0, k)), S(c, hin + k), T, 81);
+    EQ(S(c, AB(B, 0, k)), S(c, hin + 32 + k), T, 82);
+    EQ(S(c, AB(C, 0, k)), S(c, hin + 64 + k), T, 83);
+    EQ(S(c, AB(D, 0, k)), S(c, hin + 96 + k), T, 84);
+    EQ(S(c, AB(E, 0, k)), S(c, hin + 128 + k), T, 85);
+  }
+  for (int t = 0; t < 80; t++) {
+    size_t Tt = tt[t], R = r30 + 64 * (size_t)t;
+    for (int k = 0; k < 32; k++) {
+      EQ(S(c, Tt + 32 + k), S(c, AB(A, t, k)), T, 90);
+      EQ(S(c, Tt + 64 + k), S(c, AB(B, t, k)), T, 91);
+      EQ(S(c, Tt + 96 + k), S(c, AB(C, t, k)), T, 92);
+      EQ(S(c, Tt + 128 + k), S(c, AB(D, t, k)), T, 93);
+      EQ(S(c, Tt + 160 + k), S(c, AB(E, t, k)), T, 94);
+      EQ(S(c, Tt + 192 + k), S(c, kt_at[t] + k), T, 95);
+      EQ(S(c, Tt + 224 + k), S(c, WB(t, k)), T, 96);
+      EQ(S(c, R + 32 + k), S(c, AB(B, t, k)), T, 98);
+      EQ(S(c, AB(E, t + 1, k)), S(c, AB(D, t, k)), T, 102);
+      EQ(S(c, AB(D, t + 1, k)), S(c, AB(C, t, k)), T, 103);
+      EQ(S(c, AB(C, t + 1, k)), S(c, R + k), T, 104);
+      EQ(S(c, AB(B, t + 1, k)), S(c, AB(A, t, k)), T, 105);
+      EQ(S(c, AB(A, t + 1, k)), S(c, Tt + k), T, 106);
+    }
+  }
+  size_t arr[5] = {A, B, C, D, E};
+  for (int q = 0; q < 5; q++)
+    for (int k = 0; k < 32; k++) {
+      size_t in = fs[q] + 33;  /* BinSum(2,32): out[33] | in[2][32] */
+      EQ(S(c, in + k), S(c, hin + 31 * (q + 1) - k + q), T, 111);
+      EQ(S(c, in + 32 + k), S(c, AB(arr[q], 80, 31 - k)), T, 112);
+      EQ(S(c, out + 32 * q + k), S(c, fs[q] + k), T, 127);
+    }
+#undef WB
+#undef AB
+  return o - b;
+}
+/* Sha1HashChunks(B) sha1.circom:7-57: out[160] | in[512B] | ha0..he0 sha1Compression[B] */
+static const uint32_t SHA1_H[5] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0};
+static size_t ck_sha1chunks(ck_t *c, size_t b, int Bn) {
+  const char *T = "Sha1HashChunks hasher/sha1/sha1.circom";
+  size_t out = b, in = b + 160, o = in + 512 * (size_t)Bn, h[5];
+  for (int i = 0; i < 5; i++) { h[i] = o; o += ck_sha1const(c, o, SHA1_H[i], 15); }
+  size_t prev = 0;
+  for (int i = 0; i < Bn; i++) {
+    size_t sc = o;
+    o += ck_sha1comp(c, sc);
+    for (int q = 0; q < 5; q++)
+      for (int k = 0; k < 32; k++)
+        EQ(S(c, sc + 160 + 32 * q + k), i == 0 ? S(c, h[q] + k) : S(c, prev + 32 * q + 31 - k), T, i == 0 ? 26 : 34);
+    for (int k = 0; k < 512; k++) EQ(S(c, sc + 320 + k), S(c, in + (size_t)i * 512 + k), T, 42);
+    prev = sc;
+  }
+  for (int i = 0; i < 5; i++)
+    for (int k = 0; k < 32; k++) EQ(S(c, out + (31 - k) + 32 * i), S(c, prev + k + 32 * i), T, 49);
+  return o - b;
+}
+
 /* ============================================================ Poseidon (hasher/poseidon/poseidon.circom) */
 typedef struct { int t, nRP; fr_t *C, *M, *P, *S; } pos_t;
 static pos_t POS[7];
@@ -1032,6 +1239,95 @@ static size_t ck_rsa_pkcs256(ck_t *c, size_t b, int K, uint32_t EXP) {
   return o - b;
 }
 
+/* ============================================================ RSA-PSS (signatures/rsaPss.circom, mgf1.circom) */
+static size_t ck_shahash(ck_t *c, size_t b, int B, int algo);
+/* Mgf1Sha256(SEED_LEN, MASK_LEN) mgf1.circom:70-127: out[8 MASK] | seed[8 SEED] | hashed[256 ITER] | (sha256[i] num2Bits[i])[ITER] */
+static size_t ck_mgf1(ck_t *c, size_t b, int SEED, int MASK) {
+  const char *T = "Mgf1Sha256 signatures/mgf1.circom";
+  int SB = SEED * 8, MB = MASK * 8, IT = MASK / 32 + 1;
+  size_t out = b, seed = b + MB, hs = seed + SB, o = hs + 256 * (size_t)IT;
+  for (int i = 0; i < IT; i++) {
+    size_t sh = o;
+    o += ck_shahash(c, sh, 1, 256);
+    size_t nb = o;
+    o += ck_num2bits(c, nb, 32);
+    EQ(S(c, nb + 32), KC((uint64_t)i), T, 99);
+    size_t in = sh + 256;
+    for (int j = 0; j < 512; j++) {
+      fr_t v;
+      if (j < SB) v = S(c, seed + j);
+      else if (j < SB + 32) v = S(c, nb + 31 - (j - SB));
+      else v = KC(j == 288 || j == 503 || j == 506);  /* padding of the 288-bit message (:106-117) */
+      EQ(S(c, in + j), v, T, 120);
+    }
+    for (int j = 0; j < 256; j++) EQ(S(c, hs + (size_t)i * 256 + j), S(c, sh + j), T, 123);
+  }
+  for (int i = 0; i < MB; i++) EQ(S(c, out + i), S(c, hs + i), T, 128);
+  return o - b;
+}
+
+/* VerifyRsaPssSig(64, K, SALT, EXP, 256) rsaPss.circom:18-254: pubkey[K] signature[K] hashed[256] |
+ * eM[EM] eMsgInBits[8 EM] encoded[K] dbMask db salt maskedDB hash mDash[1024] |
+ * powerMod num2Bits[K] bits2Num[EM] MGF1_256 xor hDash256 */
+static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP) {
+  const char *T = "VerifyRsaPssSig signatures/rsaPss.circom";
+  const int EM = 8 * K, EMB = 64 * K, HL = 32, DBL = EM - HL - 1, SB = SALT * 8;
+  size_t pk = b, sig = b + K, hd = sig + K, eM = hd + 256, bits = eM + EM, enc = bits + EMB, dbm = enc + K,
+         db = dbm + 8 * (size_t)DBL, salt = db + 8 * (size_t)DBL, mdb = salt + SB, hash = mdb + 8 * (size_t)DBL,
+         md = hash + 256, o = md + 1024;
+  size_t pm = o;
+  o += ck_powermod(c, pm, K, EXP);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, pm + K + i), S(c, sig + i), T, 43);
+    EQ(S(c, pm + 2 * K + i), S(c, pk + i), T, 44);
+    EQ(S(c, enc + i), S(c, pm + i), T, 48);
+  }
+  for (int i = 0; i < K; i++) {
+    size_t nb = o;
+    o += ck_num2bits(c, nb, 64);
+    EQ(S(c, nb + 64), S(c, enc + K - 1 - i), T, 53);
+    for (int j = 0; j < 64; j++) EQ(S(c, bits + (size_t)i * 64 + j), S(c, nb + 63 - j), T, 56);
+  }
+  for (int i = 0; i < EM; i++) {
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 8);
+    for (int j = 0; j < 8; j++) EQ(S(c, bn + 1 + 7 - j), S(c, bits + (size_t)i * 8 + j), T, 64);
+    EQ(S(c, eM + EM - i - 1), S(c, bn), T, 66);
+  }
+  for (int i = 0; i < 8 * DBL; i++) EQ(S(c, mdb + i), S(c, bits + i), T, 86);
+  for (int i = 0; i < 256; i++) EQ(S(c, hash + i), S(c, bits + EMB - 256 - 8 + i), T, 93);
+  size_t mg = o;
+  o += ck_mgf1(c, mg, HL, DBL);
+  for (int i = 0; i < 256; i++) EQ(S(c, mg + 8 * (size_t)DBL + i), S(c, hash + i), T, 100);
+  for (int i = 0; i < 8 * DBL; i++) EQ(S(c, dbm + i), S(c, mg + i), T, 103);
+  size_t xr = o;  /* Xor2(n) bitify/bitGates.circom:232-240: out[n] | in1[n] in2[n] */
+  o += 3 * 8 * (size_t)DBL;
+  for (int i = 0; i < 8 * DBL; i++) {
+    size_t n8 = 8 * (size_t)DBL;
+    fr_t a = S(c, xr + n8 + i), bb = S(c, xr + 2 * n8 + i);
+    req(c, S(c, xr + i), SUB(ADD(a, bb), MUL(MUL(KC(2), a), bb)), "Xor2 bitify/bitGates.circom", 238, xr);
+    EQ(a, S(c, mdb + i), T, 129);
+    EQ(bb, S(c, dbm + i), T, 130);
+    EQ(S(c, db + i), i == 0 ? fr_zero() : S(c, xr + i), T, i == 0 ? 135 : 137);
+  }
+  for (int i = 0; i < SB; i++) EQ(S(c, salt + SB - 1 - i), S(c, db + 8 * (size_t)DBL - 1 - i), T, 143);
+  for (int i = 0; i < 64; i++) EQ(S(c, md + i), fr_zero(), T, 155);
+  for (int i = 0; i < 256; i++) EQ(S(c, md + 64 + i), S(c, hd + i), T, 159);
+  for (int i = 0; i < SB; i++) EQ(S(c, md + 64 + 256 + i), S(c, salt + i), T, 163);
+  /* SHA-256 padding of M' (576 bits for salt 32, 832 for salt 64) */
+  int L = 64 + 256 + SB;
+  for (int i = L; i < 1024; i++) {
+    int v = (i == L);
+    if (i >= 960) v = (((uint64_t)L >> (1023 - i)) & 1);
+    EQ(S(c, md + i), KC((uint64_t)v), T, SALT == 32 ? 170 : 196);
+  }
+  size_t hh = o;
+  o += ck_shahash(c, hh, 2, 256);
+  for (int i = 0; i < 1024; i++) EQ(S(c, hh + 256 + i), S(c, md + i), T, SALT == 32 ? 185 : 209);
+  for (int i = 0; i < 256; i++) EQ(S(c, hh + i), S(c, hash + i), T, SALT == 32 ? 186 : 210);
+  return o - b;
+}
+
 /* ============================================================ passport verification */
 /* PassportVerificationFlow(ECS, H, EHT, DG1S, DG15S, SAS, DG15V) passportVerificationFlow.circom:6-109:
  * flowResult | dg1Hash[H] dg15Hash[H] encapsulatedContent[ECS] encapsulatedContentHash[EHT] signedAttributes[1024] |
@@ -1064,14 +1360,46 @@ static size_t ck_flow(ck_t *c, size_t b, int ECS, int H, int EHT, int DG1S, int 
   return o - b;
 }
 
-/* ShaHashChunks(B, ALGO) hasher/hash.circom:32-68 (ALGO 224 / 256): out[ALGO] | in[512B] | hashALGO */
+/* ShaHashChunks(B, ALGO) hasher/hash.circom:32-68 (ALGO 160 / 224 / 256): out[ALGO] | in[512B] | hashALGO */
 static size_t ck_shahash(ck_t *c, size_t b, int B, int algo) {
   const char *T = "ShaHashChunks hasher/hash.circom";
   size_t out = b, in = b + algo, h = in + 512 * (size_t)B;
-  size_t sz = (size_t)algo + 512 * (size_t)B + ck_sha2chunks(c, h, B, algo);
-  for (int i = 0; i < 512 * B; i++) EQ(S(c, h + algo + i), S(c, in + i), T, algo == 256 ? 56 : 51);
-  for (int i = 0; i < algo; i++) EQ(S(c, out + i), S(c, h + i), T, algo == 256 ? 57 : 52);
+  size_t sz = (size_t)algo + 512 * (size_t)B + (algo == 160 ? ck_sha1chunks(c, h, B) : ck_sha2chunks(c, h, B, algo));
+  int l0 = algo == 160 ? 46 : algo == 224 ? 51 : 56;
+  for (int i = 0; i < 512 * B; i++) EQ(S(c, h + algo + i), S(c, in + i), T, l0);
+  for (int i = 0; i < algo; i++) EQ(S(c, out + i), S(c, h + i), T, l0 + 1);
   return sz;
+}
+
+/* RsaVerifyPkcs1v15(64, K, EXP, 160) signatures/rsa.circom:73-109:
+ * signature[K] pubkey[K] hashed[160] | hashed_chunks[2] | pm bits2num[0] bits2num[1] getBits getDiv */
+static size_t ck_rsa_pkcs160(ck_t *c, size_t b, int K, uint32_t EXP) {
+  const char *T = "RsaVerifyPkcs1v15 signatures/rsa.circom";
+  size_t sig = b, pk = b + K, hs = pk + K, o = hs + 160 + 2;  /* hashed_chunks[2] are never assigned */
+  size_t pm = o;
+  o += ck_powermod(c, pm, K, EXP);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, pm + K + i), S(c, sig + i), T, 76);
+    EQ(S(c, pm + 2 * K + i), S(c, pk + i), T, 77);
+  }
+  for (int i = 0; i < 2; i++) {
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 64);
+    for (int j = 0; j < 64; j++) EQ(S(c, bn + 1 + j), S(c, hs + 159 - j - i * 64), T, 86);
+  }
+  size_t gb = o;
+  o += ck_num2bits(c, gb, 64);
+  size_t gd = o;
+  o += ck_bits2num(c, gd, 32);
+  EQ(S(c, gb + 64), S(c, pm + 2), T, 92);
+  for (int i = 0; i < 32; i++) EQ(S(c, gb + i), S(c, hs + 31 - i), T, 95);
+  for (int i = 32; i < 64; i++) EQ(S(c, gd + 1 + i - 32), S(c, gb + i), T, 99);
+  EQ(S(c, gd), KC(83887124), T, 101);
+  EQ(S(c, pm + 3), KC(650212878678426138ULL), T, 104);
+  EQ(S(c, pm + 4), KC(18446744069417738544ULL), T, 105);
+  for (int i = 5; i < K - 1; i++) EQ(S(c, pm + i), KC(18446744073709551615ULL), T, 107);
+  EQ(S(c, pm + K - 1), KC(562949953421311ULL), T, 110);
+  return o - b;
 }
 
 typedef struct { int sig, dg_hash, doc, ec_blocks, ec_shift, dg1_shift, aa, dg15_shift, dg15_blocks, aa_shift; } ck_params;
@@ -1085,7 +1413,8 @@ static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 
  * signatureVerification signedAttributesNum pubkeyHasherRsa smtVerifier signedAttributesHashHasher */
 static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "PassportVerificationBuilder passportVerification/passportVerificationBuilder.circom";
-  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = 256, ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
+  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = (P->sig == 3 || P->sig == 4) ? 160 : 256,
+            ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
   size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + K,
          br = pk + K, root = br + 80;
   size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1, o = tmod + 5;
@@ -1119,15 +1448,24 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   for (int j = 0; j < HT; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + j), S(c, ech + j), T, 143);
   for (int j = 0; j < 1024; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + HT + j), S(c, sa + j), T, 144);
   EQ(S(c, fl), KC(1), T, 146);
-  size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[K] signature[K] hashed[256] | rsa */
+  size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[K] signature[K] hashed[HT] | rsa */
   const char *TV = "VerifySignature signatureVerifier/signatureVerification.circom";
   size_t rsa = sv + 2 * (size_t)K + HT;
-  o += 2 * (size_t)K + HT + ck_rsa_pkcs256(c, rsa, K, 65537);
-  for (int i = 0; i < K; i++) {
-    req(c, S(c, rsa + K + i), S(c, sv + i), TV, 124, sv);
-    req(c, S(c, rsa + i), S(c, sv + K + i), TV, 125, sv);
+  const int pss = P->sig >= 10 && P->sig <= 14;
+  if (pss) {  /* VerifyRsaPssSig: pubkey, signature, hashed */
+    o += 2 * (size_t)K + HT + ck_pss(c, rsa, K, P->sig == 12 ? 64 : 32, P->sig == 10 ? 3 : 65537);
+    for (int i = 0; i < K; i++) {
+      req(c, S(c, rsa + i), S(c, sv + i), TV, 147, sv);
+      req(c, S(c, rsa + K + i), S(c, sv + K + i), TV, 148, sv);
+    }
+  } else {    /* RsaVerifyPkcs1v15: signature, pubkey, hashed */
+    o += 2 * (size_t)K + HT + (HT == 256 ? ck_rsa_pkcs256(c, rsa, K, 65537) : ck_rsa_pkcs160(c, rsa, K, P->sig == 4 ? 37187 : 65537));
+    for (int i = 0; i < K; i++) {
+      req(c, S(c, rsa + K + i), S(c, sv + i), TV, 124, sv);
+      req(c, S(c, rsa + i), S(c, sv + K + i), TV, 125, sv);
+    }
   }
-  for (int i = 0; i < HT; i++) req(c, S(c, rsa + 2 * K + i), S(c, sv + 2 * K + i), TV, 126, sv);
+  for (int i = 0; i < HT; i++) req(c, S(c, rsa + 2 * K + i), S(c, sv + 2 * K + i), TV, pss ? 149 : 126, sv);
   for (int i = 0; i < K; i++) {
     EQ(S(c, sv + K + i), S(c, sig + i), T, 150);
     EQ(S(c, sv + i), S(c, pk + i), T, 151);
@@ -1135,7 +1473,12 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   for (int i = 0; i < HT; i++) EQ(S(c, sv + 2 * K + i), S(c, sah + i), T, 152);
   size_t san = o;
   o += ck_bits2num(c, san, 252);
-  for (int i = 0; i < 252; i++) EQ(S(c, san + 1 + i), S(c, sah + i), T, 159);
+  if (HT >= 252) {
+    for (int i = 0; i < 252; i++) EQ(S(c, san + 1 + i), S(c, sah + i), T, 159);
+  } else {
+    for (int i = 0; i < 252 - HT; i++) EQ(S(c, san + 1 + i), fr_zero(), T, 163);
+    for (int i = 0; i < HT; i++) EQ(S(c, san + 1 + 252 - HT + i), S(c, sah + i), T, 166);
+  }
   size_t pkr = o;
   o += ck_poseidon(c, pkr, 5);
   for (int i = 0; i < 5; i++) {
@@ -1321,12 +1664,20 @@ int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r) {
   return ck_end(&c, walked, r);
 }
 
-/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 over SHA-256 (SIG 1, 2) with DG hash 224 / 256 */
+/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-12, 14), DG hash 160 / 224 / 256 */
 int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r) {
   if (!pos_loaded) return -1;
-  if (!(P->sig == 1 || P->sig == 2) || !(P->dg_hash == 256 || P->dg_hash == 224)) return -2;
+  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 12) || P->sig == 14) ||
+      !(P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160))
+    return -2;
   ck_t c = ck_begin(wit, nw);
   size_t walked = 1 + ck_builder(&c, 1, P);
   req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);
+  return ck_end(&c, walked, r);
+}
+
+int ck_sha1(int B, const uint8_t *wit, size_t n, ck_report *r) {
+  ck_t c = ck_begin(wit, n);
+  size_t walked = 1 + ck_sha1chunks(&c, 1, B);
   return ck_end(&c, walked, r);
 }

@@ -9,7 +9,7 @@ from pzkwit import field, inputs as I, native
 
 pytestmark = pytest.mark.gpu
 pyr1cs = pytest.importorskip("pyr1cs")
-UNASSIGNED_PER_BMM = {32: 992, 64: 4032}
+from test_r1cs import expected_uncovered  # noqa: E402
 
 
 def _ok(res, uncovered):
@@ -37,10 +37,12 @@ def test_config2_sha256_device_witnesses():
         _ok(pyr1cs.check_sha256(w, 6), 0)
 
 
-@pytest.mark.parametrize("sig,depths", [(1, [0, 1, 2, 40, 79, 0, 5, 17]), (2, [0, 9, 33])])
+@pytest.mark.parametrize("sig,depths", [(1, [0, 1, 2, 40, 79, 0, 5, 17]), (2, [0, 9, 33]), (3, [0, 4]), (4, [2]),
+                                        (10, [0, 3]), (11, [0, 6]), (12, [1]), (14, [0])])
 def test_config3_4_register_device_witnesses(sig, depths):
-    """Config 3 (canonical, SMT root of the one-leaf tree) and config 4 (depth-k SMT paths), and the
-    RSA-4096 flow of config 5: every device witness satisfies all ~2.25 M (RSA-4096: ~3.3 M) constraints."""
+    """Config 3 (canonical, SMT root of the one-leaf tree) and config 4 (depth-k SMT paths), the
+    RSA-4096 flow of config 5 and the SHA-1 / RSA-3072 / RSA-PSS instances: every device witness
+    satisfies all of its constraints (2.25 M for the canonical instance)."""
     params = I.instance_params(sig)
     g = I.PassportGen(seed=0x40 + sig, n_keys=2, params=params, workers=1)
     pps = []
@@ -52,9 +54,8 @@ def test_config3_4_register_device_witnesses(sig, depths):
     rows = np.stack([I.pack_register_inputs(pp, params) for pp in pps])
     wit, st = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params).witness_batch_host(rows)
     assert (st == 0).all(), st
-    K = I.sig_input_len(sig)
     for w in wit:
-        _ok(pyr1cs.check_register(w, **params), 17 * UNASSIGNED_PER_BMM[K])
+        _ok(pyr1cs.check_register(w, **params), expected_uncovered(sig))
 
 
 def test_failing_lane_violates_constraints():

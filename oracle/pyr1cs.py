@@ -35,6 +35,7 @@ def lib():
         for fn in ("ck_sha256", "ck_sha1", "ck_poseidon_circuit"):
             getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
         L.ck_load_poseidon.argtypes = [ctypes.c_char_p]
+        L.ck_load_ec_table.argtypes = [ctypes.c_int, ctypes.c_char_p]
         L.ck_register.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
         _lib = L
     return _lib
@@ -75,6 +76,11 @@ def _load_poseidon():
         rc = lib().ck_load_poseidon(path.encode())
         if rc:
             raise RuntimeError("r1cs_check: cannot load Poseidon constants (%d)" % rc)
+        data = os.path.join(os.path.dirname(HERE), "passport-zk-circuits_amd", "data")
+        for curve, name in ((0, "p256_gpow8.bin"), (1, "bp256_gpow8.bin")):
+            rc = lib().ck_load_ec_table(curve, os.path.join(data, name).encode())
+            if rc:
+                raise RuntimeError("r1cs_check: cannot load %s (%d)" % (name, rc))
         _pos_loaded = True
 
 

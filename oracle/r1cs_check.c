@@ -1043,9 +1043,12 @@ static size_t ck_bmneq(ck_t *c, size_t b, int G, int L) {
 static int karatsuba_path(int G, int L) {
   /* BigMultOverflow bigIntOverflow.circom:43-53: power-of-two G and is_karatsuba_optimal(G, L)
    * (bigIntFunc.circom:617-629 with get_a_coeff, dontOpenPlease.circom); the instances here use
-   * G = L in {4, 32, 48, 64}: optimal for 32 and 64, not for 4 (< 8); 48 is not a power of two */
-  if (G != L || !(G == 4 || G == 32 || G == 48 || G == 64)) { fprintf(stderr, "r1cs_check: BigMultOverflow(%d,%d) unsupported\n", G, L); abort(); }
-  return G == 32 || G == 64;
+   * G = L in {32, 48, 64} and, for the 4-limb EC templates, G in {4, 5, 6, 7, 9, 10} x L = 4: optimal for
+   * 32 and 64 (2.5 G^1.6 <= G L), never below G = 8; 48, 5..10 are no powers of two */
+  int pow2 = (G & (G - 1)) == 0;
+  if ((G == L && (G == 32 || G == 48 || G == 64)) || (L == 4 && G >= 4 && G <= 10 && G != 8)) return pow2 && G >= 32;
+  fprintf(stderr, "r1cs_check: BigMultOverflow(%d,%d) unsupported\n", G, L);
+  abort();
 }
 
 /* BigMultOverflow(n, G, L) bigIntOverflow.circom:38-72: out[G+L-1] | in1[G] in2[L] | karatsuba or mult */
@@ -1328,6 +1331,502 @@ static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP) {
   return o - b;
 }
 
+/* ============================================================ ECDSA (signatures/ecdsa.circom, ec/curve.circom, ec/get.circom) */
+/* curve constants, 4 x 64-bit limbs little-endian (signatureVerification.circom:177-196, ec/get.circom) */
+typedef struct { uint64_t A[4], B[4], P[4], order[4], dummy[2][4]; uint64_t *gpow; } ec_curve_t;
+static ec_curve_t EC[2] = {
+    {{18446744073709551612ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
+     {4309448131093880907ULL, 7285987128567378166ULL, 12964664127075681980ULL, 6540974713487397863ULL},
+     {18446744073709551615ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
+     {17562291160714782033ULL, 13611842547513532036ULL, 18446744073709551615ULL, 18446744069414584320ULL},
+     {{4148137498610012746ULL, 51237685452122967ULL, 6555942389409504868ULL, 799804747332166731ULL},
+      {13395177781894339167ULL, 1107697421929919296ULL, 6228258783500845564ULL, 11862546499924939746ULL}}, NULL},
+    {{16810331318623712729ULL, 18122579188607900780ULL, 17219079075415130087ULL, 9032542404991529047ULL},
+     {7767825457231955894ULL, 10773760575486288334ULL, 17523706096862592191ULL, 2800214691157789508ULL},
+     {2311270323689771895ULL, 7943213001558335528ULL, 4496292894210231666ULL, 12248480212390422972ULL},
+     {10384753744809580199ULL, 10104242082523752183ULL, 4496292894210231665ULL, 12248480212390422972ULL},
+     {{5870538370169240658ULL, 13064052279558318326ULL, 1032222391323187885ULL, 10478252910764369874ULL},
+      {9125809427693782222ULL, 4479624720887462683ULL, 4313457861005768495ULL, 11848267593595748038ULL}}, NULL}};
+static const ec_curve_t *CV;  /* the curve of the witness being checked */
+
+int ck_load_ec_table(int curve, const char *path) {
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return -1;
+  uint64_t *t = malloc(8ull * 32 * 256 * 2 * 4);
+  size_t n = fread(t, 8, 32 * 256 * 2 * 4, fp);
+  fclose(fp);
+  if (n != 32 * 256 * 2 * 4) { free(t); return -2; }
+  free(EC[curve].gpow);
+  EC[curve].gpow = t;
+  return 0;
+}
+#define GPOW(i, j, a, k) CV->gpow[((((size_t)(i) * 256 + (j)) * 2 + (a)) * 4) + (k)]
+
+/* ScalarMultOverflow(N) bigIntOverflow.circom:101-110: out[N] | in[N] scalar */
+static size_t ck_smo(ck_t *c, size_t b, int N) {
+  for (int i = 0; i < N; i++)
+    EQ(S(c, b + i), MUL(S(c, b + 2 * N), S(c, b + N + i)), "ScalarMultOverflow bigInt/bigIntOverflow.circom", 108);
+  return 2 * (size_t)N + 1;
+}
+/* BigAddOverflow(G, L) bigIntOverflow.circom:22-35: out[G] | in1[G] in2[L] */
+static size_t ck_bao(ck_t *c, size_t b, int G, int L) {
+  for (int i = 0; i < G; i++)
+    EQ(S(c, b + i), i < L ? ADD(S(c, b + G + i), S(c, b + 2 * G + i)) : S(c, b + G + i), "BigAddOverflow bigInt/bigIntOverflow.circom",
+       i < L ? 30 : 33);
+  return 2 * (size_t)G + L;
+}
+/* BigSubModOverflow(K) bigIntOverflow.circom:78-98: out[K] | in1[K] in2[K] modulus[K] */
+static size_t ck_bsmo(ck_t *c, size_t b, int K) {
+  const char *T = "BigSubModOverflow bigInt/bigIntOverflow.circom";
+  for (int i = 0; i < K; i++) {
+    fr_t v = SUB(ADD(S(c, b + 3 * K + i), S(c, b + K + i)), S(c, b + 2 * K + i));
+    if (i == 0) v = ADD(v, P2[64]);
+    else if (i == K - 1) v = SUB(v, KC(1));
+    else v = SUB(ADD(v, P2[64]), KC(1));
+    EQ(S(c, b + i), v, T, i == 0 ? 89 : i == K - 1 ? 92 : 94);
+  }
+  return 4 * (size_t)K;
+}
+/* BigIntIsZeroModP(n, MAX, N, MAXN, NM) bigIntComparators.circom:158-212:
+ * in[N] modulus[NM] | sign k[DIV] | kRangeChecks[DIV] mult isZero swicher[N]  (kRangeChecks.in is set by `<--`) */
+static size_t ck_biszmp(ck_t *c, size_t b, int N, int MAX, int MAXN, int NM) {
+  const char *T = "BigIntIsZeroModP bigInt/bigIntComparators.circom";
+  const int DIV = MAXN - NM + 1;
+  size_t in = b, md = b + N, sign = md + NM, k = sign + 1, o = k + DIV;
+  EQ(MUL(S(c, sign), SUB(KC(1), S(c, sign))), fr_zero(), T, 167);
+  for (int i = 0; i < DIV; i++) o += ck_num2bits(c, o, 64);
+  size_t mult = o;
+  int G = DIV >= NM ? DIV : NM, L = DIV >= NM ? NM : DIV;
+  o += ck_bmo(c, mult, G, L);
+  size_t m1 = mult + G + L - 1, m2 = m1 + G;
+  for (int i = 0; i < NM; i++) EQ(S(c, (DIV >= NM ? m2 : m1) + i), S(c, md + i), T, DIV >= NM ? 185 : 189);
+  for (int i = 0; i < DIV; i++) EQ(S(c, (DIV >= NM ? m1 : m2) + i), S(c, k + i), T, DIV >= NM ? 186 : 190);
+  size_t iz = o;
+  o += ck_bisz(c, iz, 64, MAX, MAXN);
+  for (int i = 0; i < N; i++) {
+    size_t sw = o;
+    o += ck_switcher(c, sw);
+    EQ(S(c, sw + 3), S(c, in + i), T, 197);
+    EQ(S(c, sw + 4), fr_neg(S(c, in + i)), T, 198);
+    EQ(S(c, sw + 2), S(c, sign), T, 199);
+    EQ(S(c, iz + i), SUB(S(c, mult + i), S(c, sw + 1)), T, 201);
+  }
+  for (int i = N; i < MAXN; i++) EQ(S(c, iz + i), S(c, mult + i), T, 204);
+  return o - b;
+}
+
+static fr_t L64(uint64_t v) { return fr_u64(v); }
+
+/* PointOnCurve curve.circom:107-138: in[2][K] | squareX cubeX squareY coefMult isZeroModP */
+static size_t ck_ponc(ck_t *c, size_t b) {
+  const char *T = "PointOnCurve ec/curve.circom";
+  const int K = 4;
+  size_t x = b, y = b + K, o = b + 2 * K;
+  size_t sx = o; o += ck_bmo(c, sx, 4, 4);
+  size_t cx = o; o += ck_bmo(c, cx, 7, 4);
+  size_t sy = o; o += ck_bmo(c, sy, 4, 4);
+  size_t cm = o; o += ck_bmo(c, cm, 4, 4);
+  size_t iz = o; o += ck_biszmp(c, iz, 10, 200, 12, 4);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, sx + 7 + i), S(c, x + i), T, 111); EQ(S(c, sx + 11 + i), S(c, x + i), T, 112);
+    EQ(S(c, cx + 10 + 7 + i), S(c, x + i), T, 116);
+    EQ(S(c, sy + 7 + i), S(c, y + i), T, 119); EQ(S(c, sy + 11 + i), S(c, y + i), T, 120);
+    EQ(S(c, cm + 7 + i), S(c, x + i), T, 123); EQ(S(c, cm + 11 + i), L64(CV->A[i]), T, 124);
+    EQ(S(c, iz + 10 + i), L64(CV->P[i]), T, 137);
+  }
+  for (int i = 0; i < 7; i++) EQ(S(c, cx + 10 + i), S(c, sx + i), T, 115);
+  for (int i = 0; i < 10; i++) {
+    fr_t v = S(c, cx + i);
+    if (i < 7) v = SUB(ADD(v, S(c, cm + i)), S(c, sy + i));
+    if (i < K) v = ADD(v, L64(CV->B[i]));
+    EQ(S(c, iz + i), v, T, i < K ? 128 : i < 7 ? 131 : 134);
+  }
+  return o - b;
+}
+
+/* PointOnTangent curve.circom:144-190: in1[2][K] in2[2][K] | squareX scalarMult bigAdd bigSub rightMult scalarMult2
+ * bigAdd2 leftMult isZeroModP */
+static size_t ck_pont(ck_t *c, size_t b) {
+  const char *T = "PointOnTangent ec/curve.circom";
+  const int K = 4;
+  size_t x1 = b, y1 = b + 4, x3 = b + 8, y3 = b + 12, o = b + 16;
+  size_t sx = o; o += ck_bmo(c, sx, 4, 4);
+  size_t sm = o; o += ck_smo(c, sm, 7);
+  size_t ba = o; o += ck_bao(c, ba, 7, 4);
+  size_t bs = o; o += ck_bsmo(c, bs, 4);
+  size_t rm = o; o += ck_bmo(c, rm, 7, 4);
+  size_t sm2 = o; o += ck_smo(c, sm2, 4);
+  size_t ba2 = o; o += ck_bao(c, ba2, 4, 4);
+  size_t lm = o; o += ck_bmo(c, lm, 4, 4);
+  size_t iz = o; o += ck_biszmp(c, iz, 10, 200, 13, 4);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, sx + 7 + i), S(c, x1 + i), T, 148); EQ(S(c, sx + 11 + i), S(c, x1 + i), T, 149);
+    EQ(S(c, ba + 14 + i), L64(CV->A[i]), T, 157);
+    EQ(S(c, bs + 4 + i), S(c, x1 + i), T, 161); EQ(S(c, bs + 8 + i), S(c, x3 + i), T, 162);
+    EQ(S(c, bs + 12 + i), L64(CV->P[i]), T, 163);
+    EQ(S(c, rm + 10 + 7 + i), S(c, bs + i), T, 167);
+    EQ(S(c, sm2 + 4 + i), S(c, y1 + i), T, 170);
+    EQ(S(c, ba2 + 4 + i), S(c, y1 + i), T, 174); EQ(S(c, ba2 + 8 + i), S(c, y3 + i), T, 175);
+    EQ(S(c, lm + 7 + i), S(c, ba2 + i), T, 178); EQ(S(c, lm + 11 + i), S(c, sm2 + i), T, 179);
+    EQ(S(c, iz + 10 + i), L64(CV->P[i]), T, 189);
+  }
+  for (int i = 0; i < 7; i++) {
+    EQ(S(c, sm + 7 + i), S(c, sx + i), T, 152);
+    EQ(S(c, ba + 7 + i), S(c, sm + i), T, 156);
+    EQ(S(c, rm + 10 + i), S(c, ba + i), T, 166);
+  }
+  EQ(S(c, sm + 14), KC(3), T, 153);
+  EQ(S(c, sm2 + 8), KC(2), T, 171);
+  for (int i = 0; i < 10; i++) EQ(S(c, iz + i), i < 7 ? SUB(S(c, rm + i), S(c, lm + i)) : S(c, rm + i), T, i < 7 ? 182 : 185);
+  return o - b;
+}
+
+/* PointOnLine curve.circom:198-238: in1 in2 in3 [2][K] | bigAdd bigSub bigSub2 bigSub3 leftMult rightMult isZeroModP */
+static size_t ck_ponl(ck_t *c, size_t b) {
+  const char *T = "PointOnLine ec/curve.circom";
+  const int K = 4;
+  size_t x1 = b, y1 = b + 4, x2 = b + 8, y2 = b + 12, x3 = b + 16, y3 = b + 20, o = b + 24;
+  size_t ba = o; o += ck_bao(c, ba, 4, 4);
+  size_t s1 = o; o += ck_bsmo(c, s1, 4);
+  size_t s2 = o; o += ck_bsmo(c, s2, 4);
+  size_t s3 = o; o += ck_bsmo(c, s3, 4);
+  size_t lm = o; o += ck_bmo(c, lm, 4, 4);
+  size_t rm = o; o += ck_bmo(c, rm, 4, 4);
+  size_t iz = o; o += ck_biszmp(c, iz, 7, 136, 9, 4);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, ba + 4 + i), S(c, y1 + i), T, 204); EQ(S(c, ba + 8 + i), S(c, y3 + i), T, 205);
+    EQ(S(c, s1 + 4 + i), S(c, x2 + i), T, 208); EQ(S(c, s1 + 8 + i), S(c, x1 + i), T, 209);
+    EQ(S(c, s2 + 4 + i), S(c, y2 + i), T, 213); EQ(S(c, s2 + 8 + i), S(c, y1 + i), T, 214);
+    EQ(S(c, s3 + 4 + i), S(c, x1 + i), T, 218); EQ(S(c, s3 + 8 + i), S(c, x3 + i), T, 219);
+    EQ(S(c, s1 + 12 + i), L64(CV->P[i]), T, 210); EQ(S(c, s2 + 12 + i), L64(CV->P[i]), T, 215);
+    EQ(S(c, s3 + 12 + i), L64(CV->P[i]), T, 220);
+    EQ(S(c, lm + 7 + i), S(c, ba + i), T, 223); EQ(S(c, lm + 11 + i), S(c, s1 + i), T, 224);
+    EQ(S(c, rm + 7 + i), S(c, s2 + i), T, 227); EQ(S(c, rm + 11 + i), S(c, s3 + i), T, 228);
+    EQ(S(c, iz + 7 + i), L64(CV->P[i]), T, 236);
+  }
+  for (int i = 0; i < 7; i++) EQ(S(c, iz + i), SUB(S(c, lm + i), S(c, rm + i)), T, 233);
+  return o - b;
+}
+
+/* EllipticCurveDouble curve.circom:281-313: out[2][K] | in[2][K] | onTangentCheck onCurveCheck */
+static size_t ck_ecdbl(ck_t *c, size_t b) {
+  const char *T = "EllipticCurveDouble ec/curve.circom";
+  size_t o = b + 16, tg = o;
+  o += ck_pont(c, tg);
+  size_t oc = o;
+  o += ck_ponc(c, oc);
+  for (int i = 0; i < 8; i++) {
+    EQ(S(c, tg + i), S(c, b + 8 + i), T, 301);
+    EQ(S(c, tg + 8 + i), S(c, b + i), T, 302);
+    EQ(S(c, oc + i), S(c, b + i), T, 305);
+  }
+  return o - b;
+}
+/* EllipticCurveAdd curve.circom:316-350: out[2][K] | in1 in2 | onCurveCheck onLineCheck */
+static size_t ck_ecadd(ck_t *c, size_t b) {
+  const char *T = "EllipticCurveAdd ec/curve.circom";
+  size_t o = b + 24, oc = o;
+  o += ck_ponc(c, oc);
+  size_t ln = o;
+  o += ck_ponl(c, ln);
+  for (int i = 0; i < 8; i++) {
+    EQ(S(c, oc + i), S(c, b + i), T, 339);
+    EQ(S(c, ln + i), S(c, b + 8 + i), T, 342);
+    EQ(S(c, ln + 8 + i), S(c, b + 16 + i), T, 343);
+    EQ(S(c, ln + 16 + i), S(c, b + i), T, 344);
+  }
+  return o - b;
+}
+/* EllipticCurveGetDummy ec/get.circom:79-140: dummyPoint[2][K] */
+static size_t ck_getdummy(ck_t *c, size_t b) {
+  for (int a = 0; a < 2; a++)
+    for (int i = 0; i < 4; i++) EQ(S(c, b + 4 * a + i), L64(CV->dummy[a][i]), "EllipticCurveGetDummy ec/get.circom", 92 + a);
+  return 8;
+}
+
+/* EllipticCurvePrecomputePipinger(.., 4) curve.circom:242-278: out[16][2][K] | in[2][K] | getDummy (doublers, adders) */
+static size_t ck_precompute(ck_t *c, size_t b) {
+  const char *T = "EllipticCurvePrecomputePipinger ec/curve.circom";
+  size_t out = b, in = b + 128, o = b + 136;
+  size_t gd = o;
+  o += ck_getdummy(c, gd);
+  for (int i = 0; i < 8; i++) {
+    EQ(S(c, out + i), S(c, gd + i), T, 253);
+    EQ(S(c, out + 8 + i), S(c, in + i), T, 255);
+  }
+  for (int i = 2; i < 16; i++) {
+    size_t x = o;
+    if (i % 2 == 0) {
+      o += ck_ecdbl(c, x);
+      for (int q = 0; q < 8; q++) {
+        EQ(S(c, x + 8 + q), S(c, out + 8 * (size_t)(i / 2) + q), T, 263);
+        EQ(S(c, out + 8 * (size_t)i + q), S(c, x + q), T, 264);
+      }
+    } else {
+      o += ck_ecadd(c, x);
+      for (int q = 0; q < 8; q++) {
+        EQ(S(c, x + 8 + q), S(c, out + 8 + q), T, 269);
+        EQ(S(c, x + 16 + q), S(c, out + 8 * (size_t)(i - 1) + q), T, 270);
+        EQ(S(c, out + 8 * (size_t)i + q), S(c, x + q), T, 271);
+      }
+    }
+  }
+  return o - b;
+}
+
+/* EllipticCurveScalarMult(.., 4) curve.circom:359-512: out[2][K] | in[2][K] scalar[K] |
+ * scalarBits[256] resultingPoints[65][2][K] additionPoints[64][2][K] | precompute getDummy num2Bits[4], then per
+ * window: bits2Num isZeroResult [doublers (doubleSwitcher x8 after the first) ] getSum x8 partsEqual x16
+ * [adders isZeroAddition (resultSwitcherAddition resultSwitcherDoubling) x8] */
+static size_t ck_ecmul(ck_t *c, size_t b) {
+  const char *T = "EllipticCurveScalarMult ec/curve.circom";
+  size_t out = b, in = b + 8, sc = b + 16, bits = b + 20, rp = bits + 256, ap = rp + 65 * 8, o = ap + 64 * 8;
+  size_t pc = o;
+  o += ck_precompute(c, pc);
+  for (int i = 0; i < 8; i++) EQ(S(c, pc + 128 + i), S(c, in + i), T, 368);
+  size_t gd = o;
+  o += ck_getdummy(c, gd);
+  for (int i = 0; i < 4; i++) {
+    size_t nb = o;
+    o += ck_num2bits(c, nb, 64);
+    EQ(S(c, nb + 64), S(c, sc + i), T, 387);
+    for (int j = 0; j < 64; j++) EQ(S(c, bits + 256 - 64 * (i + 1) + j), S(c, nb + 63 - j), T, 389);
+  }
+  for (int q = 0; q < 8; q++) EQ(S(c, rp + q), S(c, pc + q), T, 409);
+  size_t dbl_at[256];
+  for (int i = 0; i < 256; i += 4) {
+    int w = i / 4;
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 4);
+    for (int j = 0; j < 4; j++) EQ(S(c, bn + 1 + j), S(c, bits + i + 3 - j), T, 414);
+    size_t izr = o;
+    o += ck_isequal(c, izr);
+    EQ(S(c, izr + 1), S(c, rp + 8 * (size_t)w), T, 418);
+    EQ(S(c, izr + 2), S(c, gd), T, 419);
+    if (i != 0) {
+      for (int j = 0; j < 4; j++) {
+        size_t d = o;
+        dbl_at[i + j - 4] = d;
+        o += ck_ecdbl(c, d);
+        if (j == 0) {
+          for (int q = 0; q < 8; q++) {
+            size_t sw = o;
+            o += ck_switcher(c, sw);
+            EQ(S(c, sw + 2), S(c, izr), T, 431);
+            EQ(S(c, sw + 3), S(c, gd + q), T, 432);
+            EQ(S(c, sw + 4), S(c, rp + 8 * (size_t)w + q), T, 433);
+            EQ(S(c, d + 8 + q), S(c, sw + 1), T, 435);
+          }
+        } else {
+          for (int q = 0; q < 8; q++) EQ(S(c, d + 8 + q), S(c, dbl_at[i + j - 5] + q), T, 440);
+        }
+      }
+    }
+    size_t gs = o;
+    for (int q = 0; q < 8; q++) o += ck_getsum(c, o, 16);
+    for (int pt = 0; pt < 16; pt++) {
+      size_t pe = o;
+      o += ck_isequal(c, pe);
+      EQ(S(c, pe + 1), KC((uint64_t)pt), T, 457);
+      EQ(S(c, pe + 2), S(c, bn), T, 458);
+      for (int q = 0; q < 8; q++) EQ(S(c, gs + 32 * (size_t)q + 1 + pt), MUL(S(c, pe), S(c, pc + 8 * (size_t)pt + q)), T, 461);
+    }
+    for (int q = 0; q < 8; q++) EQ(S(c, ap + 8 * (size_t)w + q), S(c, gs + 32 * (size_t)q), T, 470);
+    if (i == 0) {
+      for (int q = 0; q < 8; q++) EQ(S(c, rp + 8 + q), S(c, ap + q), T, 476);
+    } else {
+      size_t ad = o;
+      o += ck_ecadd(c, ad);
+      for (int q = 0; q < 8; q++) {
+        EQ(S(c, ad + 8 + q), S(c, dbl_at[i - 1] + q), T, 482);
+        EQ(S(c, ad + 16 + q), S(c, ap + 8 * (size_t)w + q), T, 483);
+      }
+      size_t iza = o;
+      o += ck_isequal(c, iza);
+      EQ(S(c, iza + 1), S(c, ap + 8 * (size_t)w), T, 486);
+      EQ(S(c, iza + 2), S(c, gd), T, 487);
+      for (int q = 0; q < 8; q++) {
+        size_t sa = o, sd = o + 6;
+        o += 12;
+        ck_switcher(c, sa);
+        ck_switcher(c, sd);
+        EQ(S(c, sa + 2), S(c, iza), T, 500);
+        EQ(S(c, sa + 3), S(c, ad + q), T, 501);
+        EQ(S(c, sa + 4), S(c, dbl_at[i - 1] + q), T, 502);
+        EQ(S(c, sd + 2), S(c, izr), T, 504);
+        EQ(S(c, sd + 3), S(c, ap + 8 * (size_t)w + q), T, 505);
+        EQ(S(c, sd + 4), S(c, sa), T, 506);
+        EQ(S(c, rp + 8 * (size_t)(w + 1) + q), S(c, sd + 1), T, 508);
+      }
+    }
+  }
+  for (int q = 0; q < 8; q++) EQ(S(c, out + q), S(c, rp + 64 * 8 + q), T, 513);
+  return o - b;
+}
+
+/* EllipicCurveScalarGeneratorMult curve.circom:680-906: out[2][K] | scalar[K] | resultCoordinateComputation[32][256][2][K]
+ * additionPoints[32][2][K] resultingPointsLeft/Left2/Right/Right2 (never assigned) resultingPoints[32][2][K] |
+ * num2bits[4] bits2num[32] getDummy getSecondDummy equal[32][256] getSumOfNElements[32][2][4]
+ * (adders isFirstDummyLeft isSecondDummyLeft isFirstDummyRight isSecondDummyRight (switcherRight switcherLeft) x8)[31] */
+static size_t ck_ecgen(ck_t *c, size_t b) {
+  const char *T = "EllipicCurveScalarGeneratorMult ec/curve.circom";
+  const size_t NP = 32, PT = 8;
+  size_t out = b, sc = b + 8, rcc = b + 12, ap = rcc + NP * 256 * PT, unused = ap + NP * PT, rp = unused + 4 * NP * PT,
+         o = rp + NP * PT;
+  size_t n2b[4];
+  for (int i = 0; i < 4; i++) {
+    n2b[i] = o;
+    o += ck_num2bits(c, o, 64);
+    EQ(S(c, n2b[i] + 64), S(c, sc + i), T, 733);
+  }
+  size_t b2n[32];
+  for (int i = 0; i < 32; i++) {
+    b2n[i] = o;
+    o += ck_bits2num(c, o, 8);
+    for (int j = 0; j < 8; j++) EQ(S(c, b2n[i] + 1 + j), S(c, n2b[(i * 8 + j) / 64] + (i * 8 + j) % 64), T, 739);
+  }
+  size_t gd = o;
+  o += ck_getdummy(c, gd);
+  size_t g2 = o;
+  o += ck_ecdbl(c, g2);
+  for (int q = 0; q < 8; q++) EQ(S(c, g2 + 8 + q), S(c, gd + q), T, 745);
+  for (size_t i = 0; i < NP; i++)
+    for (int j = 0; j < 256; j++) {
+      size_t e = o;
+      o += ck_isequal(c, e);
+      EQ(S(c, e + 1), KC((uint64_t)j), T, 751);
+      EQ(S(c, e + 2), S(c, b2n[i]), T, 752);
+      for (int q = 0; q < 8; q++) {
+        fr_t v;
+        if (j == 0) v = (i % 2 == 0) ? S(c, gd + q) : S(c, g2 + q);
+        else v = L64(GPOW(i, j, q / 4, q % 4));
+        EQ(S(c, rcc + (i * 256 + j) * PT + q), MUL(S(c, e), v), T, j == 0 ? (i % 2 == 0 ? 756 : 764) : 772);
+      }
+    }
+  size_t gs = o;
+  for (size_t i = 0; i < NP; i++)
+    for (int q = 0; q < 8; q++) {
+      size_t g = o;
+      o += ck_getsum(c, g, 256);
+      for (int j = 0; j < 256; j++) EQ(S(c, g + 1 + j), S(c, rcc + (i * 256 + j) * PT + q), T, 787);
+      EQ(S(c, ap + i * PT + q), S(c, g), T, 797);
+    }
+  (void)gs;
+  for (size_t i = 0; i + 1 < NP; i++) {
+    size_t ad = o;
+    o += ck_ecadd(c, ad);
+    size_t fl = o, sl = o + 6, fr = o + 12, sr = o + 18;
+    o += 24;
+    ck_isequal(c, fl); ck_isequal(c, sl); ck_isequal(c, fr); ck_isequal(c, sr);
+    EQ(S(c, fl + 1), S(c, gd), T, 826);
+    EQ(S(c, sl + 1), S(c, g2), T, 828);
+    EQ(S(c, fr + 1), S(c, gd), T, 831);
+    EQ(S(c, sr + 1), S(c, g2), T, 833);
+    fr_t left0 = i == 0 ? S(c, ap) : S(c, rp + (i - 1) * PT);
+    EQ(S(c, fl + 2), left0, T, i == 0 ? 838 : 866);
+    EQ(S(c, sl + 2), left0, T, i == 0 ? 839 : 867);
+    EQ(S(c, fr + 2), S(c, ap + (i + 1) * PT), T, i == 0 ? 840 : 868);
+    EQ(S(c, sr + 2), S(c, ap + (i + 1) * PT), T, i == 0 ? 841 : 869);
+    for (int q = 0; q < 8; q++) {
+      EQ(S(c, ad + 8 + q), i == 0 ? S(c, ap + q) : S(c, rp + (i - 1) * PT + q), T, i == 0 ? 842 : 871);
+      EQ(S(c, ad + 16 + q), S(c, ap + (i + 1) * PT + q), T, i == 0 ? 843 : 872);
+    }
+    for (int q = 0; q < 8; q++) {
+      size_t swr = o, swl = o + 6;
+      o += 12;
+      ck_switcher(c, swr);
+      ck_switcher(c, swl);
+      EQ(S(c, swr + 2), ADD(S(c, sr), S(c, fr)), T, 853);
+      EQ(S(c, swr + 3), S(c, ad + q), T, 854);
+      EQ(S(c, swr + 4), i == 0 ? S(c, ap + q) : S(c, rp + (i - 1) * PT + q), T, i == 0 ? 855 : 883);
+      EQ(S(c, swl + 2), ADD(S(c, sl), S(c, fl)), T, 858);
+      EQ(S(c, swl + 3), S(c, ap + (i + 1) * PT + q), T, 859);
+      EQ(S(c, swl + 4), S(c, swr), T, 860);
+      EQ(S(c, rp + i * PT + q), S(c, swl + 1), T, 862);
+    }
+  }
+  for (int q = 0; q < 8; q++) EQ(S(c, out + q), S(c, rp + (NP - 2) * PT + q), T, 905);
+  return o - b;
+}
+
+/* BigModInv(n, K) bigInt.circom:344-368: out[K] | in[K] modulus[K] | mult */
+static size_t ck_bminv(ck_t *c, size_t b, int K) {
+  const char *T = "BigModInv bigInt/bigInt.circom";
+  size_t m = b + 3 * (size_t)K;
+  size_t sz = 3 * (size_t)K + ck_bmm(c, m, K);
+  size_t md_out = m + K + 1, in1 = md_out + K, in2 = in1 + K, modl = in2 + K;
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, in1 + i), S(c, b + K + i), T, 357);
+    EQ(S(c, in2 + i), S(c, b + i), T, 358);
+    EQ(S(c, modl + i), S(c, b + 2 * K + i), T, 359);
+    EQ(S(c, md_out + i), KC(i == 0), T, i == 0 ? 362 : 364);
+  }
+  return sz;
+}
+
+/* verifyECDSABits(64, 4, A, B, P, 256) signatures/ecdsa.circom:18-87: pubkey[2][K] signature[2][K] hashed[256] |
+ * hashedChunked[K] one[K] order[K] sinv[K] | bits2Num[K] getOrder modInv mult mult2 scalarMult1 scalarMult2 add modOrder */
+static size_t ck_ecdsa(ck_t *c, size_t b) {
+  const char *T = "verifyECDSABits signatures/ecdsa.circom";
+  const int K = 4;
+  size_t pk = b, sig = b + 8, hs = b + 16, hc = hs + 256, one = hc + K, ord = one + K, sinv = ord + K, o = sinv + K;
+  EQ(S(c, one), KC(1), T, 27);
+  for (int i = 1; i < K; i++) EQ(S(c, one + i), fr_zero(), T, 29);
+  for (int i = 0; i < K; i++) {
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 64);
+    for (int j = 0; j < 64; j++) EQ(S(c, bn + 1 + 63 - j), S(c, hs + i * 64 + j), T, 36);
+    EQ(S(c, hc + K - 1 - i), S(c, bn), T, 38);
+  }
+  size_t go = o;  /* EllipicCurveGetOrder ec/get.circom:146: order[K] */
+  for (int i = 0; i < K; i++) req(c, S(c, go + i), L64(CV->order[i]), "EllipicCurveGetOrder ec/get.circom", 156, go);
+  o += K;
+  for (int i = 0; i < K; i++) EQ(S(c, ord + i), S(c, go + i), T, 43);
+  size_t mi = o;
+  o += ck_bminv(c, mi, K);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, mi + K + i), S(c, sig + K + i), T, 50);
+    EQ(S(c, mi + 2 * K + i), S(c, ord + i), T, 51);
+    EQ(S(c, sinv + i), S(c, mi + i), T, 52);
+  }
+  size_t m1 = o;
+  o += ck_bmm(c, m1, K);
+  size_t m2 = o;
+  o += ck_bmm(c, m2, K);
+#define BI1(m) ((m) + 2 * (size_t)K + 1)
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, BI1(m1) + i), S(c, sinv + i), T, 56);
+    EQ(S(c, BI1(m1) + K + i), S(c, hc + i), T, 57);
+    EQ(S(c, BI1(m1) + 2 * K + i), S(c, ord + i), T, 58);
+    EQ(S(c, BI1(m2) + i), S(c, sinv + i), T, 62);
+    EQ(S(c, BI1(m2) + K + i), S(c, sig + i), T, 63);
+    EQ(S(c, BI1(m2) + 2 * K + i), S(c, ord + i), T, 64);
+  }
+  size_t g = o;
+  o += ck_ecgen(c, g);
+  for (int i = 0; i < K; i++) EQ(S(c, g + 8 + i), S(c, m1 + K + 1 + i), T, 68);
+  size_t sm = o;
+  o += ck_ecmul(c, sm);
+  for (int i = 0; i < K; i++) EQ(S(c, sm + 16 + i), S(c, m2 + K + 1 + i), T, 72);
+  for (int i = 0; i < 8; i++) EQ(S(c, sm + 8 + i), S(c, pk + i), T, 73);
+  size_t ad = o;
+  o += ck_ecadd(c, ad);
+  for (int i = 0; i < 8; i++) {
+    EQ(S(c, ad + 8 + i), S(c, g + i), T, 77);
+    EQ(S(c, ad + 16 + i), S(c, sm + i), T, 78);
+  }
+  size_t mo = o;
+  o += ck_bmm(c, mo, K);
+  for (int i = 0; i < K; i++) {
+    EQ(S(c, BI1(mo) + i), S(c, ad + i), T, 83);
+    EQ(S(c, BI1(mo) + K + i), S(c, one + i), T, 84);
+    EQ(S(c, BI1(mo) + 2 * K + i), S(c, ord + i), T, 85);
+    EQ(S(c, mo + K + 1 + i), S(c, sig + i), T, 89);
+  }
+#undef BI1
+  return o - b;
+}
+
 /* ============================================================ passport verification */
 /* PassportVerificationFlow(ECS, H, EHT, DG1S, DG15S, SAS, DG15V) passportVerificationFlow.circom:6-109:
  * flowResult | dg1Hash[H] dg15Hash[H] encapsulatedContent[ECS] encapsulatedContentHash[EHT] signedAttributes[1024] |
@@ -1414,10 +1913,12 @@ static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 
 static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "PassportVerificationBuilder passportVerification/passportVerificationBuilder.circom";
   const int K = sig_K(P->sig), DGH = P->dg_hash, HT = (P->sig == 3 || P->sig == 4) ? 160 : 256,
-            ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
-  size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + K,
-         br = pk + K, root = br + 80;
-  size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1, o = tmod + 5;
+            ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512, ecdsa = P->sig >= 20, PKL = ecdsa ? 2 * K : K;
+  size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + PKL,
+         br = pk + PKL, root = br + 80;
+  /* intermediates: ..., pubkeyHash, then tempModulus[5] (RSA, :170) or ecBitsX[256] ecBitsY[256] (ECDSA, :188-189) */
+  size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1,
+         ebx = pkh + 1, eby = ebx + 256, o = ecdsa ? eby + 256 : tmod + 5;
   size_t hs = o;
   o += ck_shahash(c, hs, 2, DGH);
   for (int j = 0; j < 1024; j++) EQ(S(c, hs + DGH + j), S(c, dg1 + j), T, 97);
@@ -1448,11 +1949,18 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   for (int j = 0; j < HT; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + j), S(c, ech + j), T, 143);
   for (int j = 0; j < 1024; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + HT + j), S(c, sa + j), T, 144);
   EQ(S(c, fl), KC(1), T, 146);
-  size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[K] signature[K] hashed[HT] | rsa */
+  size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[PK] signature[PK] hashed[HT] | verifier */
   const char *TV = "VerifySignature signatureVerifier/signatureVerification.circom";
-  size_t rsa = sv + 2 * (size_t)K + HT;
+  const int PK = ecdsa ? 2 * K : K;
+  size_t rsa = sv + 2 * (size_t)PK + HT;
   const int pss = P->sig >= 10 && P->sig <= 14;
-  if (pss) {  /* VerifyRsaPssSig: pubkey, signature, hashed */
+  if (ecdsa) {    /* verifyECDSABits: pubkey[2][4], signature[2][4], hashed */
+    o += 2 * (size_t)PK + HT + ck_ecdsa(c, rsa);
+    for (int i = 0; i < 2 * K; i++) {
+      req(c, S(c, rsa + i), S(c, sv + i), TV, 184, sv);
+      req(c, S(c, rsa + 8 + i), S(c, sv + PK + i), TV, 186, sv);
+    }
+  } else if (pss) {  /* VerifyRsaPssSig: pubkey, signature, hashed */
     o += 2 * (size_t)K + HT + ck_pss(c, rsa, K, P->sig == 12 ? 64 : 32, P->sig == 10 ? 3 : 65537);
     for (int i = 0; i < K; i++) {
       req(c, S(c, rsa + i), S(c, sv + i), TV, 147, sv);
@@ -1465,12 +1973,12 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
       req(c, S(c, rsa + i), S(c, sv + K + i), TV, 125, sv);
     }
   }
-  for (int i = 0; i < HT; i++) req(c, S(c, rsa + 2 * K + i), S(c, sv + 2 * K + i), TV, pss ? 149 : 126, sv);
-  for (int i = 0; i < K; i++) {
-    EQ(S(c, sv + K + i), S(c, sig + i), T, 150);
+  for (int i = 0; i < HT; i++) req(c, S(c, rsa + 2 * PK + i), S(c, sv + 2 * PK + i), TV, ecdsa ? 189 : pss ? 149 : 126, sv);
+  for (int i = 0; i < PK; i++) {
+    EQ(S(c, sv + PK + i), S(c, sig + i), T, 150);
     EQ(S(c, sv + i), S(c, pk + i), T, 151);
   }
-  for (int i = 0; i < HT; i++) EQ(S(c, sv + 2 * K + i), S(c, sah + i), T, 152);
+  for (int i = 0; i < HT; i++) EQ(S(c, sv + 2 * PK + i), S(c, sah + i), T, 152);
   size_t san = o;
   o += ck_bits2num(c, san, 252);
   if (HT >= 252) {
@@ -1479,13 +1987,37 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
     for (int i = 0; i < 252 - HT; i++) EQ(S(c, san + 1 + i), fr_zero(), T, 163);
     for (int i = 0; i < HT; i++) EQ(S(c, san + 1 + 252 - HT + i), S(c, sah + i), T, 166);
   }
-  size_t pkr = o;
-  o += ck_poseidon(c, pkr, 5);
-  for (int i = 0; i < 5; i++) {
-    EQ(S(c, tmod + i), ADD(MUL(S(c, pk + 3 * i), P2[128]), MUL(S(c, pk + 3 * i + 1), P2[64])), T, 176);
-    EQ(S(c, pkr + 1 + i), ADD(S(c, tmod + i), S(c, pk + 3 * i + 2)), T, 177);
+  if (!ecdsa) {
+    size_t pkr = o;
+    o += ck_poseidon(c, pkr, 5);
+    for (int i = 0; i < 5; i++) {
+      EQ(S(c, tmod + i), ADD(MUL(S(c, pk + 3 * i), P2[128]), MUL(S(c, pk + 3 * i + 1), P2[64])), T, 176);
+      EQ(S(c, pkr + 1 + i), ADD(S(c, tmod + i), S(c, pk + 3 * i + 2)), T, 177);
+    }
+    EQ(S(c, pkh), S(c, pkr), T, 179);
+  } else {  /* :184-218, EC_FIELD_SIZE 256, DIFF 8 */
+    for (int i = 0; i < K; i++) {
+      size_t nx = o, ny = o + 129;
+      o += ck_num2bits(c, nx, 64) + ck_num2bits(c, ny, 64);
+      EQ(S(c, nx + 64), S(c, pk + i), T, 195);
+      EQ(S(c, ny + 64), S(c, pk + i + K), T, 196);
+      for (int j = 0; j < 64; j++) {
+        EQ(S(c, ebx + 255 - j - 64 * i), S(c, nx + j), T, 199);
+        EQ(S(c, eby + 255 - j - 64 * i), S(c, ny + j), T, 200);
+      }
+    }
+    size_t xn = o, yn = o + 497;
+    o += ck_bits2num(c, xn, 248) + ck_bits2num(c, yn, 248);
+    for (int i = 0; i < 248; i++) {
+      EQ(S(c, xn + 1 + 247 - i), S(c, ebx + i + 8), T, 212);
+      EQ(S(c, yn + 1 + 247 - i), S(c, eby + i + 8), T, 213);
+    }
+    size_t h = o;
+    o += ck_poseidon(c, h, 2);
+    EQ(S(c, h + 1), S(c, xn), T, 218);
+    EQ(S(c, h + 2), S(c, yn), T, 219);
+    EQ(S(c, pkh), S(c, h), T, 221);
   }
-  EQ(S(c, pkh), S(c, pkr), T, 179);
   size_t smt = o;
   o += ck_smt(c, smt, 80);
   EQ(S(c, smt + 1), S(c, root), T, 226);
@@ -1570,7 +2102,7 @@ static size_t ck_regid(ck_t *c, size_t b, const ck_params *P) {
  * passportVerifier registerIdentity */
 static size_t ck_builder(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "RegisterIdentityBuilder identityManagement/registerIdentityBuilder.circom";
-  const int K = sig_K(P->sig), ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
+  const int K = sig_K(P->sig) * (P->sig >= 20 ? 2 : 1), ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
   size_t d15ph = b, ph = b + 1, d1c = b + 2, pkih = b + 3, root = b + 4, ec = b + 5, dg1 = ec + ECL, dg15 = dg1 + 1024,
          sa = dg15 + D15L, sig = sa + 1024, pk = sig + K, br = pk + K, sk = br + 80, o = sk + 1;
   size_t pv = o;
@@ -1664,12 +2196,17 @@ int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r) {
   return ck_end(&c, walked, r);
 }
 
-/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-12, 14), DG hash 160 / 224 / 256 */
+/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-12, 14), ECDSA P-256 / brainpoolP256r1
+ * (SIG 20 / 21), DG hash 160 / 224 / 256 */
 int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r) {
   if (!pos_loaded) return -1;
-  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 12) || P->sig == 14) ||
+  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 12) || P->sig == 14 || P->sig == 20 || P->sig == 21) ||
       !(P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160))
     return -2;
+  if (P->sig >= 20) {
+    CV = &EC[P->sig - 20];
+    if (!CV->gpow) return -3;
+  }
   ck_t c = ck_begin(wit, nw);
   size_t walked = 1 + ck_builder(&c, 1, P);
   req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);

@@ -38,7 +38,7 @@ def test_config2_sha256_device_witnesses():
 
 
 @pytest.mark.parametrize("sig,depths", [(1, [0, 1, 2, 40, 79, 0, 5, 17]), (2, [0, 9, 33]), (3, [0, 4]), (4, [2]),
-                                        (10, [0, 3]), (11, [0, 6]), (12, [1]), (14, [0])])
+                                        (10, [0, 3]), (11, [0, 6]), (12, [1]), (14, [0]), (20, [0, 2]), (21, [1])])
 def test_config3_4_register_device_witnesses(sig, depths):
     """Config 3 (canonical, SMT root of the one-leaf tree) and config 4 (depth-k SMT paths), the
     RSA-4096 flow of config 5 and the SHA-1 / RSA-3072 / RSA-PSS instances: every device witness

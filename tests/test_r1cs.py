@@ -24,9 +24,16 @@ UNASSIGNED_PER_BMM = {32: 992, 64: 4032, 48: 4512}
 # 3 -> 1 + 1, 37187 -> 15 + 5; SIG 3 / 4 add the two never-assigned hashed_chunks of rsa.circom:81
 N_BMM = {1: 17, 2: 17, 3: 17, 4: 20, 10: 2, 11: 17, 12: 17, 14: 17}
 EXTRA = {3: 2, 4: 2}
+# ECDSA (verifyECDSABits over 4 x 64-bit limbs): every BigMultNonEqualOverflow(G, 4) leaves 4 * 3 tmpResult entries
+# unassigned; 3,164 of them per witness = 260 EllipticCurveDouble x 9 + 102 EllipticCurveAdd x 8 + 4 BigMultModP x 2
+# (PointOnCurve 5, PointOnTangent 4, PointOnLine 3 products); plus EllipicCurveScalarGeneratorMult's never-assigned
+# resultingPointsLeft/Left2/Right/Right2 (4 x 32 x 8) and resultingPoints[31] (8) (ec/curve.circom:812-816, 904)
+ECDSA_UNCOVERED = 12 * (260 * 9 + 102 * 8 + 4 * 2) + 4 * 32 * 8 + 8
 
 
 def expected_uncovered(sig):
+    if sig >= 20:
+        return ECDSA_UNCOVERED
     return N_BMM[sig] * UNASSIGNED_PER_BMM[I.sig_input_len(sig)] + EXTRA.get(sig, 0)
 
 
@@ -79,6 +86,8 @@ REGISTER_CASES = [
     ("sig11_pss", I.instance_params(11), 0),
     ("sig12_pss_salt64", I.instance_params(12), 0),
     ("sig14_pss3072", I.instance_params(14), 1),
+    ("sig20_ecdsa_p256", I.instance_params(20), 0),
+    ("sig21_ecdsa_brainpool", I.instance_params(21), 3),
 ]
 
 
@@ -115,6 +124,20 @@ def test_tampered_signals_break_constraints(oracle):
             continue
         rc, r = pyr1cs.check_register(v, **I.CANONICAL)
         assert rc != 0 and (r["n_failed"] > 0 or r["n_uncovered_nonzero"] > 0), idx
+
+
+def test_invalid_ecdsa_signature_fails_constraints(oracle):
+    """A tampered ECDSA s: the oracle flags its site and the witness violates the constraints of
+    verifyECDSABits (ecdsa.circom:88-90 x1 mod n === r, or an EC point check)."""
+    params = I.instance_params(20)
+    g = I.PassportGen(seed=0x33, n_keys=2, params=params, workers=1)
+    pp = g.passport_at(0)
+    r_, s_ = pp["sig"]
+    pp["sig"] = (r_, s_ ^ 1)
+    rc, w = oracle.register_witness(oracle.register_params(**params), I.pack_register_inputs(pp, params))
+    assert rc != 0
+    rc2, r = pyr1cs.check_register(w, **params)
+    assert rc2 != 0 and r["n_failed"] > 0
 
 
 def test_invalid_signature_witness_fails_constraints(oracle):

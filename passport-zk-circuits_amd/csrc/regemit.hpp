@@ -591,6 +591,77 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
   }
 }
 
+// ---- section-specialised element functions of the BigMultModP emitter
+// A 128-bit non-negative value (lo, hi) as an element, its bit t, and its low n bits (n in 1..128).
+__device__ __forceinline__ El el_u128(uint64_t lo, uint64_t hi) {
+  return El{make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)), make_uint4(0u, 0u, 0u, 0u)};
+}
+__device__ __forceinline__ uint32_t u128_bit(uint64_t lo, uint64_t hi, uint32_t t) {
+  return (uint32_t)((t < 64 ? lo >> (t & 63) : hi >> (t & 63)) & 1u);
+}
+__device__ __forceinline__ El el_u128_low(uint64_t lo, uint64_t hi, uint32_t n) {
+  const uint64_t ml = n >= 64 ? ~0ull : (1ull << n) - 1ull;
+  const uint64_t mh = n >= 128 ? ~0ull : n > 64 ? (1ull << (n - 64)) - 1ull : 0ull;
+  return el_u128(lo & ml, hi & mh);
+}
+// Num2Bits(L) block (bitify.circom:10-32) of a value < 2^128: out[L] | in | sum[L] (sum[j] = v mod 2^(j+1))
+__device__ __forceinline__ El el_num2bits(uint64_t lo, uint64_t hi, uint32_t L, uint32_t t) {
+  if (t < L) return el_u64(u128_bit(lo, hi, t));
+  if (t == L) return el_u128(lo, hi);
+  return el_u128_low(lo, hi, t - L);
+}
+
+template <int K, int SEC>
+__device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
+  if constexpr (SEC == MM_MODCHK) {  // Num2Bits(64)(mod_i): out[64] | in | sum[64]
+    const uint32_t i = s / 129, t = s - 129 * i;
+    return el_num2bits(C.r[i], 0, 64, t);
+  } else if constexpr (SEC == MM_LT) {
+    const uint32_t i = s / 140;
+    uint32_t t = s - 140 * i;
+    const uint64_t a = C.n[i], b = C.r[i];
+    if (t < 134) {  // LessThan(64): out | in[2] | Num2Bits(65)(a + 2^64 - b)
+      const uint64_t vlo = a - b, vhi = a >= b ? 1u : 0u;
+      if (t < 3) return el_u64(t == 0 ? 1 - vhi : t == 1 ? a : b);
+      return el_num2bits(vlo, vhi, 65, t - 3);
+    }
+    t -= 134;  // IsEqual: out | in[2] | IsZero(out, in, inv)
+    if (t == 0 || t == 3) return el_u64(a == b);
+    if (t == 1) return el_u64(a);
+    if (t == 2) return el_u64(b);
+    if (t == 4) return a <= b ? el_u64(b - a) : el_fr(fr_sub(fr_zero(), fr_u64(a - b)));
+    const uint64_t* iv = C.inv + 4 * i;
+    return El{make_uint4((uint32_t)iv[0], (uint32_t)(iv[0] >> 32), (uint32_t)iv[1], (uint32_t)(iv[1] >> 32)),
+              make_uint4((uint32_t)iv[2], (uint32_t)(iv[2] >> 32), (uint32_t)iv[3], (uint32_t)(iv[3] >> 32))};
+  } else if constexpr (SEC == MM_RANGE) {  // Num2Bits(RL)(carry + 2^(RL-1)), RL = 2*64 + log_ceil(2K) + 3 - 64
+    constexpr uint32_t RL = 128 + mm_log_ceil(2 * K) + 3 - 64, PER = 2 * RL + 1;
+    const uint32_t i = s / PER, t = s - PER * i;
+    const uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1] + (1ull << (RL - 1 - 64));
+    return el_num2bits(lo, hi, RL, t);
+  } else if constexpr (SEC == MM_Q) {
+    return el_u64(C.q[s]);
+  } else if constexpr (SEC == MM_R) {
+    return el_u64(C.r[s]);
+  } else if constexpr (SEC == MM_TMPM) {
+    const uint32_t i = s / K, j = s - i * K;
+    U192 acc;
+    acc.mac(C.q[i], C.n[j]);
+    return el_w(u192w(acc));
+  } else {
+    return el_w(mm_sig(C, ((uint32_t)SEC << 24) | s));
+  }
+}
+
+template <int K, int SEC>
+__device__ __forceinline__ void mm_sections(const MMCore C, uint8_t* out, uint4* stage) {
+  if constexpr (SEC < (int)MM_SECTIONS) {
+    constexpr MMStarts S = mm_starts(K);
+    constexpr uint32_t a = S.v[SEC], n = S.v[SEC + 1] - S.v[SEC];
+    emit_run(out + 32ull * a, n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    mm_sections<K, SEC + 1>(C, out, stage);
+  }
+}
+
 template <int K>
 __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint64_t lds[MM_CORE_WORDS(K) + K + 3 * (4 * K - 1)];
@@ -653,14 +724,10 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
            cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
   uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
-  // section by section: every wave works inside one section (uniform branch), and each section
-  // starts wave-aligned, so a tmpResult row never straddles the start of a wave (K = 32: two rows
-  // per wave; K = 64: one)
-  constexpr MMStarts S = mm_starts(K);
-  for (int sec = 0; sec < (int)MM_SECTIONS; sec++) {
-    const uint32_t a = S.v[sec], n = S.v[sec + 1] - a;
-    emit_run(out + 32ull * a, n, stage, [&](uint32_t q) { return el_w(mm_sig(C, ((uint32_t)sec << 24) | q)); });
-  }
+  // section by section, each with its own specialised element function (mm_el<K, SEC>): every
+  // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never
+  // straddles the start of a wave (K = 32: two rows per wave; K = 64: one)
+  mm_sections<K, 0>(C, out, stage);
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps

@@ -131,8 +131,25 @@ class GpuEngine:
         import torch
         from pzkwit import native, inputs as I
         self.torch, self.dev = torch, dev
+        self.layout = "O0 (all signals)"
         if workload.startswith("register"):
-            self.inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, I.instance_params(args.sig_eff))
+            params = I.instance_params(args.sig_eff)
+            sym = None
+            if getattr(args, "sym", None):
+                from pzkwit import symmap
+                if args.sym.startswith("synthetic"):
+                    frac = int(args.sym.split(":")[1]) if ":" in args.sym else 4
+                    n_in = I.PassportGen.shared(SIG_SEED[args.sig_eff], 64, args.sig_eff).n_inputs
+                    keep = symmap.synthetic_keep(native.layout_witness_size(params), 1 + 4 + n_in, fraction=frac)
+                    sym = symmap.sym_text(keep)
+                    self.layout = ("synthetic .sym map: outputs + inputs + 1/%d of the O0 signals (hash subset; NOT "
+                                   "circom's O2, which cannot be built here)" % frac)
+                else:
+                    sym = open(args.sym).read()
+                    self.layout = ".sym map %s" % os.path.basename(args.sym)
+            self.inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params, sym=sym)
+            if sym is not None:  # two O0 chunks of up to 1024 witnesses (runtime.cpp MAP_CHUNK)
+                self.o0_staging_bytes = 2 * 1024 * 32 * native.layout_witness_size(params)
         else:
             self.inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
         self.W, self.NIN = self.inst.witness_size, self.inst.n_inputs
@@ -223,7 +240,8 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
     elif device == "cuda":
         free, _ = torch.cuda.mem_get_info(dev)
         scratch_pw = 10 << 20 if args.sig_eff >= 20 else 1 << 20  # per-witness core scratch, two sets
-        fit = max(1, int((free * 0.85) // (slots * stride + 2 * scratch_pw)))
+        staging = getattr(engine, "o0_staging_bytes", 0)  # mapped layouts: the library's O0 chunk slots
+        fit = max(1, int((free * 0.85 - staging) // (slots * stride + 2 * scratch_pw)))
         parts_n = 1
         while (batch + parts_n - 1) // parts_n > fit:
             parts_n += 1
@@ -279,6 +297,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slot) size")
     ap.add_argument("--slots", type=int, default=1, help="output slots (ring) per GPU")
+    ap.add_argument("--sym", default=None, help="signal -> witness map: a circom .sym file, or synthetic[:N]")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -364,7 +383,7 @@ def report(args, r, world):
                    "output": "device-resident generation: each sub-batch's .wtns rows are written to HBM into a "
                              "ring of output slots that the next sub-batches overwrite (a 4096 batch of 72 MB "
                              "witnesses exceeds one GPU's HBM); host delivery is not in the timed region",
-                   "witness_elements": W, "witness_bytes": 32 * W, "layout": "O0 (all signals)",
+                   "witness_elements": W, "witness_bytes": 32 * W, "layout": r["engine"].layout,
                    "parallelism": "shard%d" % world, "invalid_lanes": r["bad"], "gathered": r["gathered"]},
         "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -113,6 +113,16 @@ typedef struct pzk_instance pzk_instance;
 int pzk_instance_create(const pzk_params* params, pzk_instance** out);
 void pzk_instance_destroy(pzk_instance* inst);
 
+/* Same, with a signal -> witness map in circom's .sym format (circom --sym: one line per signal,
+ * "signal_idx,witness_idx,component_idx,name", witness_idx = -1 for a signal the compiler eliminated;
+ * signal indices in the --O0 numbering of DESIGN.md §2). The instance's witness is then the mapped
+ * one: witness_size = number of kept signals + 1, element k = the O0 signal whose witness_idx is k,
+ * and the .wtns header reports that size. sym = NULL is pzk_instance_create (the identity map).
+ * Replaces: the witness layout circom --O1/--O2 bakes into the WASM (circuits/scripts/compile-circuit.sh:34). */
+int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t sym_len, pzk_instance** out);
+/* Host-only: validate a .sym against an instance's O0 numbering; *witness_size = mapped size. */
+int pzk_sym_check(const pzk_params* params, const char* sym, size_t sym_len, uint64_t* witness_size);
+
 /* Host-only layout queries (no device needed): witness/input sizes of an instance and its
  * emit-region table (offset, length, kind). Used by the CPU test suite. */
 int pzk_layout_query(const pzk_params* params, pzk_info* info, uint32_t* n_regions);

@@ -285,8 +285,28 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
     }
 }
 
+// ------------------------------------------------------------------- signal map (.sym) gather
+// out[k] = o0[map[k]] per witness row: 16 B per lane (two lanes per element), so every wave store is
+// 1 KiB contiguous; the O0 reads follow the map (monotonic maps read mostly forward).
+__global__ void __launch_bounds__(256) k_wtns_gather(const uint8_t* o0, size_t o0_stride, const uint32_t* map,
+                                                     uint64_t out_size, uint8_t* out, size_t out_stride) {
+  const uint32_t w = blockIdx.y;
+  const uint4* src = reinterpret_cast<const uint4*>(o0 + o0_stride * w);
+  uint4* dst = reinterpret_cast<uint4*>(out + out_stride * w);
+  const uint64_t n2 = 2 * out_size;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n2; h += (uint64_t)gridDim.x * blockDim.x)
+    dst[h] = src[2ull * map[h >> 1] + (h & 1)];
+}
+
 // ------------------------------------------------------------------- launchers
 #define HIP_TRY(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+hipError_t launch_wtns_gather(const uint8_t* o0, size_t o0_stride, const uint32_t* map, uint64_t out_size, uint8_t* out,
+                              size_t out_stride, uint32_t batch, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((2 * out_size + 255) / 256, 512);
+  hipLaunchKernelGGL(k_wtns_gather, dim3(blocks, batch), dim3(256), 0, st, o0, o0_stride, map, out_size, out, out_stride);
+  return hipGetLastError();
+}
 
 hipError_t launch_load_values(const ValueLoad* loads, int n, const uint8_t* inputs, uint64_t n_inputs, fr* values,
                               uint32_t batch, hipStream_t st) {

@@ -157,6 +157,12 @@ struct pzk_instance {
   hipStream_t s_emit = nullptr;
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
+  // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
+  // --O0 witness of a chunk into d_o0[slot]; k_wtns_gather compacts it into the caller's rows
+  uint64_t out_size = 0;          // elements per output witness (= lay.wit_size without a map)
+  uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
+  uint8_t* d_o0[2] = {};
+  size_t o0_cap = 0;
   // staging for the host-buffer path
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -272,7 +278,8 @@ static void free_all(pzk_instance* I) {
   free_scratch(I);
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
-                  I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small};
+                  I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small, I->d_map,
+                  I->d_o0[0], I->d_o0[1]};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
@@ -359,6 +366,81 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
       ok = ok && hipEventRecord(e, nullptr) == hipSuccess;
     }
   if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
+  I->out_size = I->lay.wit_size;
+  *out = I;
+  return 0;
+}
+
+// circom .sym text ("signal_idx,witness_idx,component_idx,name" per line; witness_idx -1 = eliminated)
+// -> inv[k] = O0 index of output witness element k (inv[0] = 0, the constant 1). Signal indices are the
+// --O0 numbering (1 .. o0_size - 1); witness indices must cover 1 .. max exactly once.
+static bool parse_sym(const char* text, size_t len, uint64_t o0_size, std::vector<uint32_t>& inv, std::string& why) {
+  std::vector<int64_t> w_of;  // witness index -> signal index
+  size_t i = 0;
+  uint64_t line = 0;
+  auto num = [&](int64_t& v) -> bool {
+    bool neg = false, any = false;
+    v = 0;
+    if (i < len && text[i] == '-') { neg = true; i++; }
+    while (i < len && text[i] >= '0' && text[i] <= '9') { v = v * 10 + (text[i] - '0'); i++; any = true; if (v > (1ll << 40)) return false; }
+    if (neg) v = -v;
+    return any;
+  };
+  while (i < len) {
+    line++;
+    if (text[i] == '\n' || text[i] == '\r') { i++; continue; }
+    int64_t sig, wit, comp;
+    if (!num(sig) || i >= len || text[i++] != ',' || !num(wit) || i >= len || text[i++] != ',' || !num(comp)) {
+      why = "sym line " + std::to_string(line) + ": expected signal_idx,witness_idx,component_idx,name";
+      return false;
+    }
+    while (i < len && text[i] != '\n') i++;
+    if (sig < 1 || (uint64_t)sig >= o0_size) {
+      why = "sym line " + std::to_string(line) + ": signal index " + std::to_string(sig) + " outside 1.." +
+            std::to_string(o0_size - 1);
+      return false;
+    }
+    if (wit == -1) continue;
+    if (wit < 1) { why = "sym line " + std::to_string(line) + ": bad witness index"; return false; }
+    if ((uint64_t)wit >= w_of.size()) w_of.resize(wit + 1, -1);
+    if (w_of[wit] != -1) { why = "sym: witness index " + std::to_string(wit) + " assigned twice"; return false; }
+    w_of[wit] = sig;
+  }
+  if (w_of.size() < 2) { why = "sym: no signal is kept"; return false; }
+  inv.assign(w_of.size(), 0);
+  for (size_t k = 1; k < w_of.size(); k++) {
+    if (w_of[k] < 0) { why = "sym: witness index " + std::to_string(k) + " is not assigned"; return false; }
+    inv[k] = (uint32_t)w_of[k];
+  }
+  return true;
+}
+
+int pzk_sym_check(const pzk_params* params, const char* sym, size_t sym_len, uint64_t* witness_size) {
+  if (!params || !sym) return fail(PZK_E_ARG, "null argument");
+  Layout L;
+  std::string why;
+  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
+  std::vector<uint32_t> inv;
+  if (!parse_sym(sym, sym_len, L.wit_size, inv, why)) return fail(PZK_E_ARG, why);
+  if (witness_size) *witness_size = inv.size();
+  return 0;
+}
+
+int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t sym_len, pzk_instance** out) {
+  if (!params || !out) return fail(PZK_E_ARG, "null argument");
+  if (!sym) return pzk_instance_create(params, out);
+  pzk_instance* I = nullptr;
+  int rc = pzk_instance_create(params, &I);
+  if (rc) return rc;
+  std::vector<uint32_t> inv;
+  std::string why;
+  if (!parse_sym(sym, sym_len, I->lay.wit_size, inv, why)) { pzk_instance_destroy(I); return fail(PZK_E_ARG, why); }
+  if (hipMalloc(&I->d_map, 4 * inv.size()) != hipSuccess ||
+      hipMemcpy(I->d_map, inv.data(), 4 * inv.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    pzk_instance_destroy(I);
+    return fail(PZK_E_NOMEM, "device allocation of the signal map failed");
+  }
+  I->out_size = inv.size();
   *out = I;
   return 0;
 }
@@ -399,7 +481,7 @@ void pzk_instance_destroy(pzk_instance* inst) {
 int pzk_instance_info(const pzk_instance* I, pzk_info* info) {
   if (!I || !info) return fail(PZK_E_ARG, "null argument");
   memset(info, 0, sizeof *info);
-  info->witness_size = I->lay.wit_size;
+  info->witness_size = I->out_size;
   info->n_inputs = I->lay.n_inputs;
   info->n_outputs = I->lay.n_outputs;
   info->n_public_inputs = I->lay.n_public;
@@ -425,8 +507,8 @@ int pzk_wtns_header(const pzk_instance* I, uint8_t h[76]) {
   auto u64 = [&](uint64_t v) { memcpy(p, &v, 8); p += 8; };
   memcpy(p, "wtns", 4); p += 4;
   u32(2); u32(2);
-  u32(1); u64(40); u32(32); memcpy(p, prime, 32); p += 32; u32((uint32_t)I->lay.wit_size);
-  u32(2); u64(32ull * I->lay.wit_size);
+  u32(1); u64(40); u32(32); memcpy(p, prime, 32); p += 32; u32((uint32_t)I->out_size);
+  u32(2); u64(32ull * I->out_size);
   return 0;
 }
 
@@ -650,17 +732,70 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   return 0;
 }
 
+// With a signal map: chunks of MAP_CHUNK witnesses, each through the O0 pipeline into d_o0[slot]
+// (slot = the chunk's scratch set, so chunk k + 2, which waits for ev_done of set k, never overwrites a
+// slot chunk k's gather still reads), then k_wtns_gather into the caller's rows on the main stream.
+static constexpr size_t MAP_CHUNK = 1024, MAP_CHUNK_MIN = 64;  // witnesses per O0 chunk (halved while it does not fit)
+static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
+                        int32_t* d_status, const pzk_exec* exec) {
+  const size_t o0_stride = 32ull * I->lay.wit_size;
+  size_t chunk = std::min(batch, MAP_CHUNK);
+  if (chunk > I->o0_cap) {  // the chains cost the same for any chunk size: take the largest that fits
+    int rc = sync_all(I);  // the slots may still be read by an earlier call's gather
+    if (rc) return rc;
+    for (auto& p : I->d_o0) { if (p) (void)hipFree(p); p = nullptr; }
+    I->o0_cap = 0;
+    for (;;) {
+      bool ok = true;
+      for (auto& p : I->d_o0) ok = ok && hipMalloc(&p, o0_stride * chunk) == hipSuccess;
+      if (ok) break;
+      for (auto& p : I->d_o0) { if (p) (void)hipFree(p); p = nullptr; }
+      (void)hipGetLastError();
+      if (chunk <= MAP_CHUNK_MIN) return fail(PZK_E_NOMEM, "device O0 staging allocation failed");
+      chunk /= 2;
+    }
+    I->o0_cap = chunk;
+  }
+  chunk = std::min(chunk, I->o0_cap);
+  hipStream_t user = (exec && exec->stream) ? (hipStream_t)exec->stream : nullptr;
+  if (user) {  // inputs may come from the caller's stream
+    HIPCHK(hipEventRecord(I->ev_entry, user));
+    HIPCHK(hipStreamWaitEvent(I->stream, I->ev_entry, 0));
+  }
+  pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
+  for (size_t lo = 0; lo < batch; lo += chunk) {
+    const size_t n = std::min(chunk, batch - lo);
+    const int set = (int)(I->calls & 1);
+    int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[set], o0_stride,
+                          d_status ? d_status + lo : nullptr, &ex);
+    if (rc) return rc;
+    for (int i = 1; i < 4; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
+    HIPCHK(launch_wtns_gather(I->d_o0[set], o0_stride, I->d_map, I->out_size, d_wtns + stride * lo, stride, (uint32_t)n,
+                              I->stream));
+    HIPCHK(hipEventRecord(I->ev_done[set][0], I->stream));
+  }
+  if (user)
+    for (auto& set : I->ev_done)
+      for (hipEvent_t e : set) HIPCHK(hipStreamWaitEvent(user, e, 0));
+  if (exec && (exec->flags & PZK_EXEC_SYNC)) {
+    if (user) HIPCHK(hipStreamSynchronize(user));
+    else return sync_all(I);
+  }
+  return 0;
+}
+
 int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
                       int32_t* d_status, const pzk_exec* exec) {
   if (!I || !d_inputs || !d_wtns) return fail(PZK_E_ARG, "null argument");
   if (batch == 0) return 0;
   if (batch > 65535) return fail(PZK_E_ARG, "batch > 65535: split it");
-  if (stride < 32ull * I->lay.wit_size || stride % 16) return fail(PZK_E_ARG, "bad witness stride");
+  if (stride < 32ull * I->out_size || stride % 16) return fail(PZK_E_ARG, "bad witness stride");
   int rc = check_exec_device(I, exec);
   if (rc) return rc;
   std::lock_guard<std::mutex> lock(I->mu);
   DeviceGuard dg(I->device);
   if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
+  if (I->d_map) return batch_mapped(I, d_inputs, batch, d_wtns, stride, d_status, exec);
   return batch_locked(I, d_inputs, batch, d_wtns, stride, d_status, exec);
 }
 
@@ -682,7 +817,7 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
   std::lock_guard<std::mutex> lock(I->mu);
   DeviceGuard dg(I->device);
   if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
-  size_t in_bytes = 32ull * I->lay.n_inputs * batch, out_bytes = 32ull * I->lay.wit_size * batch;
+  size_t in_bytes = 32ull * I->lay.n_inputs * batch, out_bytes = 32ull * I->out_size * batch;
   // the staging buffers may still be read/written by an earlier device call: drain before reuse
   if ((rc = sync_all(I))) return rc;
   if (batch > I->host_cap) {
@@ -698,7 +833,9 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
   hipStream_t st = I->stream;
   HIPCHK(hipMemcpyAsync(I->d_in, h_inputs, in_bytes, hipMemcpyHostToDevice, st));
   pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
-  if ((rc = batch_locked(I, I->d_in, batch, I->d_out, 32ull * I->lay.wit_size, I->d_status, &ex))) return rc;
+  rc = I->d_map ? batch_mapped(I, I->d_in, batch, I->d_out, 32ull * I->out_size, I->d_status, &ex)
+                : batch_locked(I, I->d_in, batch, I->d_out, 32ull * I->out_size, I->d_status, &ex);
+  if (rc) return rc;
   if ((rc = sync_all(I))) return rc;
   HIPCHK(hipMemcpy(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost));
   if (h_status) HIPCHK(hipMemcpy(h_status, I->d_status, 4 * batch, hipMemcpyDeviceToHost));

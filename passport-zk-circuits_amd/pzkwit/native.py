@@ -17,7 +17,8 @@ PZK_EXEC_SYNC = 1
 
 # C-ABI entry points declared in include/pzkwit.h (checked by tests/test_capi.py)
 EXPORTS = ("pzk_instance_create", "pzk_instance_destroy", "pzk_instance_info", "pzk_instance_input",
-           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_instance_sync", "pzk_timing", "pzk_phase_info", "pzk_last_error",
+           "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_instance_sync",
+           "pzk_instance_create_mapped", "pzk_sym_check", "pzk_timing", "pzk_phase_info", "pzk_last_error",
            "pzk_version")
 
 STATUS_NAMES = {
@@ -85,6 +86,10 @@ def lib():
         L.pzk_witness_batch_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(PzkExec)]
         L.pzk_instance_sync.argtypes = [ctypes.c_void_p]
+        L.pzk_instance_create_mapped.argtypes = [ctypes.POINTER(PzkParams), ctypes.c_char_p, ctypes.c_size_t,
+                                                 ctypes.POINTER(ctypes.c_void_p)]
+        L.pzk_sym_check.argtypes = [ctypes.POINTER(PzkParams), ctypes.c_char_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_uint64)]
         L.pzk_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
         L.pzk_phase_info.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
@@ -109,6 +114,17 @@ def layout_witness_size(params, circuit=None):
     return int(info.witness_size)
 
 
+def sym_check(params, sym, circuit=None):
+    """Validate a .sym text against an instance's O0 numbering (host only) -> mapped witness size."""
+    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit)
+    for k, v in param_fields(params).items():
+        setattr(p, k, v)
+    b = sym.encode() if isinstance(sym, str) else sym
+    n = ctypes.c_uint64()
+    _check(lib().pzk_sym_check(ctypes.byref(p), b, len(b), ctypes.byref(n)))
+    return int(n.value)
+
+
 def _check(rc):
     if rc != 0:
         raise PzkError("pzkwit error %d: %s" % (rc, lib().pzk_last_error().decode()))
@@ -117,7 +133,8 @@ def _check(rc):
 class Instance:
     """One compiled circuit instance (the analogue of circom's compiled WASM module)."""
 
-    def __init__(self, circuit=PZK_CIRCUIT_REGISTER, size_arg=0, params=None):
+    def __init__(self, circuit=PZK_CIRCUIT_REGISTER, size_arg=0, params=None, sym=None):
+        """sym: optional signal -> witness map in circom .sym text (pzk_instance_create_mapped)."""
         L = lib()
         p = PzkParams(circuit=circuit, size_arg=size_arg)
         if params:
@@ -128,7 +145,11 @@ class Instance:
             for k, v in params.items():
                 setattr(p, m.get(k, k), int(v))
         h = ctypes.c_void_p()
-        _check(L.pzk_instance_create(ctypes.byref(p), ctypes.byref(h)))
+        if sym is None:
+            _check(L.pzk_instance_create(ctypes.byref(p), ctypes.byref(h)))
+        else:
+            b = sym.encode() if isinstance(sym, str) else sym
+            _check(L.pzk_instance_create_mapped(ctypes.byref(p), b, len(b), ctypes.byref(h)))
         self._h = h
         info = PzkInfo()
         _check(L.pzk_instance_info(h, ctypes.byref(info)))

@@ -1,0 +1,48 @@
+"""Signal -> witness maps in circom's .sym format (pzk_instance_create_mapped, include/pzkwit.h).
+
+circom --sym writes one line per signal: "signal_idx,witness_idx,component_idx,name", witness_idx
+-1 for a signal its --O1/--O2 simplification eliminated (circuits/scripts/compile-circuit.sh:34). The
+witness the prover reads (circuits/scripts/prove.sh:27) is then element k = the signal whose
+witness_idx is k. Here the signal indices are the --O0 numbering of DESIGN.md §2; a real circom .sym
+can be dropped in where circom is available (none is here: SURVEY.md §8c).
+"""
+import numpy as np
+
+
+def sym_text(keep, names=None):
+    """keep: bool array over the O0 signals (index 0 = the constant 1, ignored). Kept signals get
+    witness indices 1, 2, ... in O0 order."""
+    keep = np.asarray(keep, dtype=bool)
+    wit = np.full(keep.shape[0], -1, dtype=np.int64)
+    idx = np.flatnonzero(keep[1:]) + 1
+    wit[idx] = np.arange(1, idx.size + 1)
+    lines = ["%d,%d,0,%s" % (s, wit[s], names[s] if names else "s%d" % s) for s in range(1, keep.shape[0])]
+    return "\n".join(lines) + "\n"
+
+
+def parse_sym(text):
+    """-> inv: inv[k] = O0 signal index of output element k (inv[0] = 0)."""
+    pairs = {}
+    for ln in text.splitlines():
+        if not ln.strip():
+            continue
+        sig, wit = (int(x) for x in ln.split(",")[:2])
+        if wit >= 0:
+            if wit in pairs:
+                raise ValueError("witness index %d assigned twice" % wit)
+            pairs[wit] = sig
+    n = max(pairs) + 1
+    inv = np.zeros(n, dtype=np.int64)
+    for k in range(1, n):
+        inv[k] = pairs[k]
+    return inv
+
+
+def synthetic_keep(o0_size, n_prefix, fraction=4, salt=0x5A):
+    """A deterministic synthetic map (NOT circom's O2): the outputs and inputs (the first n_prefix
+    signals) plus every signal whose index hashes to 0 mod `fraction`."""
+    s = np.arange(o0_size, dtype=np.uint64)
+    h = (s * np.uint64(0x9E3779B97F4A7C15) + np.uint64(salt)) >> np.uint64(40)
+    keep = (h % np.uint64(fraction)) == 0
+    keep[:n_prefix] = True
+    return keep

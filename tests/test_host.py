@@ -143,6 +143,7 @@ class _StubEngine:
     def __init__(self, args, workload, dev):
         import torch
         self.torch, self.NIN, self.W, self.n_pub, self.inst = torch, 3072, 3072 + 300, 4, _StubInst()
+        self.layout = "stub"
 
     def setup(self, d_in, batch, sub, slots, steps):
         self.rows = d_in.view(batch, self.NIN, 32)
@@ -203,3 +204,19 @@ def test_bench_two_ranks_gloo_scatter_gather():
     assert g["status_nonzero"] == int((rows[:, 0, 0] != 0).sum())
     assert g["public_sha256"] == hashlib.sha256(rows[:, :4].tobytes()).hexdigest()[:16]
     assert out["config"]["invalid_lanes"] == 2 * int((rows[:, 0, 0] != 0).sum())
+
+
+def test_sym_map_validation():
+    """.sym maps (pzk_sym_check, the host half of pzk_instance_create_mapped): kept signals get dense
+    witness indices; malformed, out-of-range, duplicate and gapped maps are rejected with a message."""
+    from pzkwit import native, symmap
+    n_o0 = native.layout_witness_size(I.CANONICAL)
+    keep = symmap.synthetic_keep(n_o0, 1 + 4 + 5778)
+    txt = symmap.sym_text(keep)
+    assert native.sym_check(I.CANONICAL, txt) == int(keep[1:].sum()) + 1
+    inv = symmap.parse_sym(txt)
+    assert inv.shape[0] == int(keep[1:].sum()) + 1 and (np.diff(inv[1:]) > 0).all()
+    for bad, msg in [("1,1,0,a\n2,1,0,b\n", "assigned twice"), ("1,2,0,a\n", "not assigned"),
+                     ("%d,1,0,a\n" % n_o0, "outside"), ("x,1,0,a\n", "expected"), ("1,-1,0,a\n", "no signal")]:
+        with pytest.raises(native.PzkError, match=msg):
+            native.sym_check(I.CANONICAL, bad)

@@ -119,6 +119,9 @@ struct Scratch {
   }
 };
 
+// scratch sets (pipeline depth): call k uses set k % NSETS and waits for call k - NSETS
+static constexpr int NSETS = 3;
+
 struct pzk_instance {
   pzk_params params;
   Timing timing;
@@ -150,10 +153,11 @@ struct pzk_instance {
   int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
   // per-batch scratch, grown on demand; two sets, alternating per call, so that call k + 1's
   // cores can run while call k's emitters still read set k % 2
-  Scratch scr[2];
+  Scratch scr[NSETS];
   uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
   // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit)
-  hipEvent_t ev_done[2][4] = {};
+  hipEvent_t ev_done[NSETS][4] = {};
+  hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
@@ -291,6 +295,8 @@ static void free_all(pzk_instance* I) {
   for (auto& set : I->ev_done)
     for (hipEvent_t e : set)
       if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : I->ev_gather)
+    if (e) (void)hipEventDestroy(e);
   I->timing.destroy();
 }
 
@@ -359,6 +365,10 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
             hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_pos, &I->ev_tab})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  for (hipEvent_t& e : I->ev_gather) {
+    ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventRecord(e, nullptr) == hipSuccess;
+  }
   for (auto& set : I->ev_done)
     for (hipEvent_t& e : set) {
       ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -568,14 +578,14 @@ static int sync_all(pzk_instance* I) {
 
 // One call, with the instance lock held and the device set.
 //
-// Pipelining: call k uses scratch set k % 2 and four instance streams — main (the
+// Pipelining: call k uses scratch set k % NSETS and four instance streams — main (the
 // Poseidon/SMT/BabyJubJub chain), rsa (the signature core), sha (the SHA emitters) and emit (the other
 // emitters). Streams are not joined at the end of a call: call k + 1's cores start while call k's
-// emitters still run. Before touching set k % 2 again, call k + 2 waits for the end of call k on all
-// four streams (ev_done). With a caller stream the call is joined into it at exit (serialised).
+// emitters still run. Before touching set k % NSETS again, call k + NSETS waits for the end of call k
+// on all four streams (ev_done). With a caller stream the call is joined into it at exit (serialised).
 static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
                         int32_t* d_status, const pzk_exec* exec) {
-  const int set = (int)(I->calls & 1);
+  const int set = (int)(I->calls % NSETS);
   Scratch& S = I->scr[set];
   int rc = ensure_scratch(I, S, batch);
   if (rc) return rc;
@@ -701,16 +711,19 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     HIPCHK(hipEventRecord(I->ev_bjj, st));
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(3, 1 << 20))) return rc; }
     HIPCHK(hipEventRecord(I->ev_pos, st));
-    // BabyJubJub emitter behind the SHA emitters, then the chain's tail emitters (Poseidon blocks,
-    // small regions, flow, checks) on the stream that finishes first per sub-batch: behind the SHA
-    // emitters by default (the BigMultModP emitter is the longer one), PZK_TAIL=emit for the other
-    static const bool tail_on_emit = getenv("PZK_TAIL") && !strcmp(getenv("PZK_TAIL"), "emit");
-    hipStream_t s_tail = tail_on_emit ? s_emit : s_sha;
+    // BabyJubJub emitter behind the SHA emitters; of the chain's tail emitters, the Poseidon blocks go
+    // behind the signature emitters and the small regions / flow / checks behind the SHA emitters
+    // (default, "split": 70.7k vs 68.3k / 69.0k witnesses/s for all-on-sha / all-on-emit, tuning switch
+    // PZK_TAIL=sha|emit|split, profiles/README.md)
+    static const char* tail_env = getenv("PZK_TAIL");
+    static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0 : 2;
+    hipStream_t s_tail = tail_mode == 1 ? s_emit : s_sha, s_pos = tail_mode == 0 ? s_sha : s_emit;
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_sha))) return rc;
+    HIPCHK(hipStreamWaitEvent(s_pos, I->ev_pos, 0));
+    if ((rc = emit(E_POS, s_pos))) return rc;
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_pos, 0));
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_rsa, 0));
-    if ((rc = emit(E_POS, s_tail))) return rc;
     if ((rc = emit(E_GEN, s_tail))) return rc;
     if ((rc = emit(E_FLOW, s_tail))) return rc;
     if (!lay.is_ecdsa) {
@@ -765,14 +778,16 @@ static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
   for (size_t lo = 0; lo < batch; lo += chunk) {
     const size_t n = std::min(chunk, batch - lo);
-    const int set = (int)(I->calls & 1);
-    int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[set], o0_stride,
+    const int set = (int)(I->calls % NSETS), slot = (int)((lo / chunk) & 1);
+    HIPCHK(hipStreamWaitEvent(I->stream, I->ev_gather[slot], 0));  // the gather two chunks back read this slot
+    int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[slot], o0_stride,
                           d_status ? d_status + lo : nullptr, &ex);
     if (rc) return rc;
     for (int i = 1; i < 4; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
-    HIPCHK(launch_wtns_gather(I->d_o0[set], o0_stride, I->d_map, I->out_size, d_wtns + stride * lo, stride, (uint32_t)n,
+    HIPCHK(launch_wtns_gather(I->d_o0[slot], o0_stride, I->d_map, I->out_size, d_wtns + stride * lo, stride, (uint32_t)n,
                               I->stream));
     HIPCHK(hipEventRecord(I->ev_done[set][0], I->stream));
+    HIPCHK(hipEventRecord(I->ev_gather[slot], I->stream));
   }
   if (user)
     for (auto& set : I->ev_done)

@@ -30,14 +30,16 @@ enum {
   PZK_CIRCUIT_REGISTER = 0, /* RegisterIdentityBuilder(...)  registerIdentityBuilder.circom:41 */
   PZK_CIRCUIT_POSEIDON = 1, /* PoseidonHash(n)               poseidon.circom:214 (config 1) */
   PZK_CIRCUIT_SHA256 = 2,   /* Sha256HashChunks(blocks)      sha256HashChunks.circom:8 (config 2) */
-  PZK_CIRCUIT_SHA1 = 3      /* Sha1HashChunks(blocks)        hasher/sha1/sha1.circom:7 */
+  PZK_CIRCUIT_SHA1 = 3,     /* Sha1HashChunks(blocks)        hasher/sha1/sha1.circom:7 */
+  PZK_CIRCUIT_SHA384 = 4,   /* Sha384HashChunks(blocks)      hasher/sha2/sha384/sha384HashChunks.circom:8 */
+  PZK_CIRCUIT_SHA512 = 5    /* Sha512HashChunks(blocks)      hasher/sha2/sha512/sha512HashChunks.circom */
 };
 
 /* Template parameters of RegisterIdentityBuilder (registerIdentityBuilder.circom:41-52),
  * verbatim, plus the circuit family and its size argument for the standalone circuits. */
 typedef struct pzk_params {
   int32_t circuit;            /* PZK_CIRCUIT_* */
-  int32_t size_arg;           /* n for POSEIDON, blocks for SHA256 / SHA1; ignored for REGISTER */
+  int32_t size_arg;           /* n for POSEIDON, blocks for SHA256 / SHA1 / SHA384 / SHA512; ignored for REGISTER */
   int32_t signature_type;     /* SIGNATURE_TYPE (1 = RSA-2048/SHA-256/65537, 2 = RSA-4096, 10-12 = RSA-2048
                                  PSS/SHA-256 (10: e = 3), 20 = ECDSA secp256r1/SHA-256) */
   int32_t dg_hash_type;       /* DG_HASH_TYPE (256) */

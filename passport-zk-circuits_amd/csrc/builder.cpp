@@ -191,6 +191,19 @@ bool build_sha1(const pzk_params& p, Layout& L, std::string& why) {
   return true;
 }
 
+bool build_sha512(const pzk_params& p, Layout& L, std::string& why, int O) {
+  int B = p.size_arg;
+  if (B < 1 || B > 16) { why = "Sha384/Sha512HashChunks(blocks): blocks must be 1..16"; return false; }
+  Builder b(L);
+  L.n_inputs = 1024ull * B;
+  L.n_outputs = O;
+  L.inputs.push_back({"in", 0, L.n_inputs});
+  b.region(RK_ONE, 1);
+  b.sha512(0, B, O);
+  b.finalize();
+  return true;
+}
+
 }  // namespace
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why);
@@ -202,6 +215,8 @@ bool build_layout(const pzk_params& p, Layout& L, std::string& why) {
     case PZK_CIRCUIT_POSEIDON: ok = build_poseidon(p, L, why); break;
     case PZK_CIRCUIT_SHA256: ok = build_sha256(p, L, why); break;
     case PZK_CIRCUIT_SHA1: ok = build_sha1(p, L, why); break;
+    case PZK_CIRCUIT_SHA384: ok = build_sha512(p, L, why, 384); break;
+    case PZK_CIRCUIT_SHA512: ok = build_sha512(p, L, why, 512); break;
     case PZK_CIRCUIT_REGISTER: ok = build_register(p, L, why); break;
     default: why = "unknown circuit family"; return false;
   }

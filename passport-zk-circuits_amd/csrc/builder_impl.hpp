@@ -73,6 +73,26 @@ struct Builder {
            {job, blocks, in_off, wrapper ? 1 : 0});
     for (int m = 0; m < blocks; m++) region(RK_SHA1_BLOCK, SHA1_BLOCK_SIGS, {job, m});
   }
+  // Sha384HashChunks / Sha512HashChunks(B) (hasher/sha2/sha384/sha384HashChunks.circom:8-48): own signals as
+  // one RK_SHA5_OWN region, then one RK_SHA5_BLOCK (schedule + rounds) per 1024-bit block
+  int sha512(int in_off, int blocks, int O, int src = 0) {
+    ShaJob j{};
+    j.in_off = in_off;
+    j.blocks = blocks;
+    j.core_off = (int)L.sha_core_words;
+    j.digest_slot = -1;
+    j.src = src;
+    j.algo = O == 384 ? 3 : 4;
+    L.sha_core_words += L.sha_core_words & 1;  // 64-bit words: 8-byte aligned within the row
+    j.core_off = (int)L.sha_core_words;
+    j.hout = j.core_off + blocks * SHA5_BLOCK_CORE;
+    L.sha_core_words += blocks * SHA5_BLOCK_CORE + 16;
+    L.sha.push_back(j);
+    const int job = (int)L.sha.size() - 1;
+    region(RK_SHA5_OWN, (uint64_t)O + 1024ull * blocks + 512ull * (blocks + 1) + 512, {job, blocks, in_off, O});
+    for (int m = 0; m < blocks; m++) region(RK_SHA5_BLOCK, SHA5_BLOCK_SIGS, {job, m});
+    return job;
+  }
   // a SHA job of either algorithm whose regions are placed later (sha_regions)
   int hash_job(int algo, int in_off, int blocks) {
     if (algo == 224) { const int j = sha_job(in_off, blocks); L.sha[j].algo = 2; return j; }

@@ -10,6 +10,7 @@
 #include "regemit.hpp"
 #include "sha.hpp"
 #include "sha1.hpp"
+#include "sha512.hpp"
 #include "sha_prog.hpp"
 #include "kernels.hpp"
 
@@ -40,6 +41,7 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
   const ShaJob& J = jobs[j];
   const uint8_t* row = J.src ? derived + 32ull * (uint64_t)w * n_derived : inputs + 32ull * (uint64_t)w * n_inputs;
   if (J.algo == 1) sha1_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
+  else if (J.algo >= 3) sha512_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
   else sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
 }
 
@@ -210,6 +212,48 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha1(DevLayout L, const W
     emit_run(out, wk.count, stage, [&](uint32_t q) {
       bool cp;
       const uint64_t v = sha1_own_sig(hout, Bn, R.a[3] != 0, wk.start + q, cp);
+      return cp ? el_load(in_row + 32ull * (R.a[2] + v)) : el_u64(v);
+    });
+  }
+}
+
+// ------------------------------------------------------------------- emit: SHA-384/512 regions
+// workgroup per (witness, chunk) of a region: the block's 64-bit core words go to LDS (with the
+// Hin words in front of A and E, so B..D / F..H of every round are history lookups), then one
+// closed-form signal per lane (sha512.hpp), staged through LDS for wave-contiguous stores.
+__device__ __forceinline__ El el_u128v(U128 v) {
+  return El{make_uint4((uint32_t)v.lo, (uint32_t)(v.lo >> 32), (uint32_t)v.hi, (uint32_t)(v.hi >> 32)), make_uint4(0u, 0u, 0u, 0u)};
+}
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha512(DevLayout L, const Work* work, const uint8_t* inputs,
+                                                             const uint8_t* derived, const uint32_t* sha_core,
+                                                             uint8_t* wtns, size_t stride) {
+  __shared__ uint64_t wd[8 + 80 + 84 + 84];
+  __shared__ uint4 stage[2 * EMIT_THREADS];
+  const Work wk = work[blockIdx.y];
+  const uint32_t w = blockIdx.x;
+  const Region R = L.regions[wk.region];
+  const ShaJob job = L.sha[R.a[0]];
+  const uint64_t* wc = reinterpret_cast<const uint64_t*>(sha_core + (size_t)w * L.sha_core_words + job.core_off);
+  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  if (R.kind == RK_SHA5_BLOCK) {
+    const uint64_t* bc = wc + (size_t)R.a[1] * (SHA5_BLOCK_CORE / 2);  // Hin[8] W[80] A[1..80] E[1..80]
+    for (int i = threadIdx.x; i < 8 + 80; i += blockDim.x) wd[i] = bc[i];
+    for (int i = threadIdx.x; i < 80; i += blockDim.x) { wd[88 + 4 + i] = bc[88 + i]; wd[172 + 4 + i] = bc[168 + i]; }
+    if (threadIdx.x < 4) {  // A[-3..0] = Hin[3..0], E[-3..0] = Hin[7..4]
+      wd[88 + threadIdx.x] = bc[3 - threadIdx.x];
+      wd[172 + threadIdx.x] = bc[7 - threadIdx.x];
+    }
+    __syncthreads();
+    const Sha5Blk X{wd, wd + 8, wd + 88, wd + 172};  // A(t) = wd[88 + t + 3], E(t) = wd[172 + t + 3]
+    emit_run(out, wk.count, stage, [&](uint32_t q) { return el_u128v(sha5_block_sig(X, wk.start + q)); });
+  } else {  // RK_SHA5_OWN
+    const int Bn = R.a[1], O = R.a[3];
+    const uint8_t* in_row = job.src ? derived + 32ull * (uint64_t)w * L.n_derived : inputs + 32ull * (uint64_t)w * L.n_inputs;
+    const uint64_t* iv = job.algo == 3 ? SHA384_IV_ : SHA512_IV_;
+    auto hin = [&](int m, uint32_t j) -> uint64_t { return m < Bn ? wc[(size_t)m * (SHA5_BLOCK_CORE / 2) + j] : wc[(size_t)Bn * (SHA5_BLOCK_CORE / 2) + j]; };
+    emit_run(out, wk.count, stage, [&](uint32_t q) {
+      bool cp;
+      const uint64_t v = sha5_own_sig(hin, Bn, O, iv, wk.start + q, cp);
       return cp ? el_load(in_row + 32ull * (R.a[2] + v)) : el_u64(v);
     });
   }
@@ -506,6 +550,10 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
       else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
       break;
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
+    case E_SHA5:
+      hipLaunchKernelGGL(k_emit_sha512, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
+                         B.stride);
+      break;
     case E_SHA1:  // witness-major grid, as k_emit_sha
       hipLaunchKernelGGL(k_emit_sha1, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
                          B.stride);

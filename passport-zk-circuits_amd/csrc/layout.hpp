@@ -71,6 +71,9 @@ enum RegionKind : uint32_t {
   // ---- SHA-1 (hasher/sha1/*.circom; sha1.hpp)
   RK_SHA1_OWN = 45,   // Sha1HashChunks out[160] | in[512B] | H(0..4); a0 = sha slot, a1 = blocks, a2 = input offset
   RK_SHA1_BLOCK = 46, // Sha1compression of one block; a0 = sha slot, a1 = block
+  // ---- SHA-384 / SHA-512 (hasher/sha2/sha384, sha512; sha512.hpp)
+  RK_SHA5_OWN = 47,   // Sha384/512HashChunks out[O] | in[1024B] | states | iv; a0 = sha slot, a1 = blocks, a2 = input offset
+  RK_SHA5_BLOCK = 48, // Sha2_384_512Schedule + Sha2_384_512Rounds(80) of one block; a0 = sha slot, a1 = block
   RK_COUNT
 };
 
@@ -78,12 +81,13 @@ enum RegionKind : uint32_t {
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
 // E_ECT = ECDSA table blocks (k_emit_ect)
 // E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
-// E_SHA1 = SHA-1 hasher regions (k_emit_sha1)
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_COUNT };
+// E_SHA1 = SHA-1 hasher regions (k_emit_sha1); E_SHA5 = SHA-384/512 hasher regions (k_emit_sha512)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
     case RK_SHA1_OWN: case RK_SHA1_BLOCK: return E_SHA1;
+    case RK_SHA5_OWN: case RK_SHA5_BLOCK: return E_SHA5;
     case RK_POSEIDON: return E_POS;
     case RK_BITS2NUM: case RK_NUM2BITS: return E_BITS;
     case RK_FLOW: return E_FLOW;
@@ -131,7 +135,8 @@ struct ShaJob {
   int32_t core_off; // u32 offset of this hasher's core inside the per-witness SHA core
   int32_t digest_slot; // value-store slot receiving the 256 digest bits (packed) or -1
   int32_t src;      // 0: message bits are input elements; 1: derived elements (RSA-PSS, pss.hpp)
-  int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp), 2: SHA-224 (SHA-256 blocks, own IV, 224-bit out)
+  int32_t algo;     // 0: SHA-256 (sha.hpp), 1: SHA-1 (sha1.hpp), 2: SHA-224 (SHA-256 blocks, own IV, 224-bit out),
+                    // 3 / 4: SHA-384 / SHA-512 (sha512.hpp, 1024-bit blocks)
   int32_t hout;     // u32 offset of the digest words (Hout[8] / Hout[5]) inside the per-witness SHA core
 };
 
@@ -141,6 +146,9 @@ constexpr int SHA_BLOCK_CORE = 200;
 constexpr int SHA1_BLOCK_CORE = 165;
 constexpr uint32_t SHA1_BLOCK_SIGS = 198034;  // Sha1compression (sha1.hpp)
 constexpr uint32_t SHA1_CONST_SIGS = 97;      // H(x): out[32] | Num2Bits(32)
+// SHA-384/512: per block Hin[8] W[80] A[1..80] E[1..80] as 64-bit words; per hasher blocks*496 + Hout[16]
+constexpr int SHA5_BLOCK_CORE = 496;
+constexpr uint32_t SHA5_BLOCK_SIGS = 378362;  // Sha2_384_512Schedule (94,480) + Sha2_384_512Rounds(80) (283,882)
 
 // Poseidon task: one permutation PoseidonHash(n) per (witness, task) lane
 struct PosTask {

@@ -44,7 +44,7 @@ static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k
                                               "k_pss_mgf+k_sha_core+k_pss_mdash"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
                                         PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
-                                        PH_EMIT_SHA, PH_EMIT_SHA};
+                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -178,7 +178,7 @@ struct pzk_instance {
     L.n_derived = lay.n_derived;
     L.n_regions = (uint32_t)lay.regions.size();
     L.n_sha = (uint32_t)lay.sha.size();
-    L.sha_core_words = lay.sha_core_words;
+    L.sha_core_words = (lay.sha_core_words + 1) & ~1u;  // even: SHA-512 cores are read as 64-bit words
     L.n_pos = (uint32_t)lay.pos.size();
     L.pos_core_elems = lay.pos_core_elems;
     L.n_values = lay.n_values;
@@ -527,7 +527,7 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
   S.free_all();
   const Layout& L = I->lay;
   struct { void** p; size_t bytes; } req[] = {
-      {(void**)&S.d_sha_core, 4ull * L.sha_core_words * batch},
+      {(void**)&S.d_sha_core, 4ull * ((L.sha_core_words + 1) & ~1u) * batch},
       {(void**)&S.d_pos_core, 32ull * L.pos_core_elems * batch},
       {(void**)&S.d_values, 32ull * std::max<uint32_t>(L.n_values, 1) * batch},
       {(void**)&S.d_rsa_core, 8ull * L.rsa_core_words * batch},
@@ -691,6 +691,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_sha, 0));
     if ((rc = emit(E_SHA, s_sha))) return rc;
     if ((rc = emit(E_SHA1, s_sha))) return rc;  // SHA-1 hashers (SIGNATURE_TYPE 3, DG_HASH_TYPE 160)
+    if ((rc = emit(E_SHA5, s_sha))) return rc;  // SHA-384/512 hashers (standalone circuits)
     // signature emitters: BigMultModP blocks / EC table blocks, PSS derived hashers
     HIPCHK(hipStreamWaitEvent(s_emit, I->ev_rsa, 0));
     if ((rc = emit(E_MM, s_emit))) return rc;
@@ -882,7 +883,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
     *kernel = PHASE_KERNELS[phase];
     if (phase == PH_EMIT_SHA) {  // the SHA-2 and SHA-1 emitters share the phase: name the ones this instance runs
       const bool s2 = !I->lay.work[E_SHA].empty() || !I->lay.work[E_SHAD].empty(), s1 = !I->lay.work[E_SHA1].empty();
-      *kernel = s1 ? (s2 ? "k_emit_sha+k_emit_sha1" : "k_emit_sha1") : "k_emit_sha";
+      *kernel = !I->lay.work[E_SHA5].empty() ? "k_emit_sha512" : s1 ? (s2 ? "k_emit_sha+k_emit_sha1" : "k_emit_sha1") : "k_emit_sha";
     }
   }
   if (bytes_per_witness) {
@@ -897,12 +898,16 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       if (r.kind == RK_SHA_BLOCK) b += 4ull * SHA_BLOCK_CORE;
       if (r.kind == RK_SHA1_OWN) b += 32ull * 512 * r.a[1];  // message bits copied
       if (r.kind == RK_SHA1_BLOCK) b += 4ull * SHA1_BLOCK_CORE;
+      if (r.kind == RK_SHA5_OWN) b += 32ull * 1024 * r.a[1];  // message bits copied
+      if (r.kind == RK_SHA5_BLOCK) b += 4ull * SHA5_BLOCK_CORE;
       if (r.kind == RK_INCOPY) b += 32ull * r.len;
       if (r.kind == RK_POSEIDON) b += 32ull * pos_core_len(r.a[1] + 1);
       if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);
     }
     if (phase == PH_SHA_CORE)
-      for (const ShaJob& j : L.sha) b += 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo == 1 ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
+      for (const ShaJob& j : L.sha)
+        b += j.algo >= 3 ? 32ull * 1024 * j.blocks + 4ull * (j.blocks * SHA5_BLOCK_CORE + 16)
+                         : 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo == 1 ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
     if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;

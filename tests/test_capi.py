@@ -112,6 +112,11 @@ def test_small_circuit_layouts(oracle):
     for b in (1, 2, 4):
         rc, nin, nw = layout_sizes(None, native.PZK_CIRCUIT_SHA1, b)
         assert rc == 0 and nin == 512 * b and nw == oracle.lib().orc_sha1_witness_size(b)
+    for circ, o in ((native.PZK_CIRCUIT_SHA384, 384), (native.PZK_CIRCUIT_SHA512, 512)):
+        for b in (1, 2, 16):
+            rc, nin, nw = layout_sizes(None, circ, b)
+            assert rc == 0 and nin == 1024 * b and nw == oracle.lib().orc_sha512_witness_size(b, o)
+        assert layout_sizes(None, circ, 0)[0] == -2 and layout_sizes(None, circ, 17)[0] == -2
 
 
 def test_unsupported_params_rejected():

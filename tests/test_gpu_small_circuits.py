@@ -91,6 +91,47 @@ def test_sha1_circuit_matches_oracle_and_hashlib(oracle, blocks):
         assert bad.size == 0, "msg %d: %d mismatching signals, first %s" % (b, bad.size, bad[:8].tolist())
 
 
+@pytest.mark.parametrize("out_bits,blocks", [(384, 1), (512, 1), (384, 2), (512, 3)])
+def test_sha512_circuit_matches_oracle_and_hashlib(oracle, out_bits, blocks):
+    """Sha384HashChunks / Sha512HashChunks(blocks) (hasher/sha2/sha384/sha384HashChunks.circom:8-48,
+    sha512/sha512HashChunks.circom) on the GPU: digests equal hashlib.sha384 / sha512, and every one of
+    the 378,362 signals per Sha2_384_512 block (round sums up to 67 bits) equals the oracle's."""
+    circ = native.PZK_CIRCUIT_SHA384 if out_bits == 384 else native.PZK_CIRCUIT_SHA512
+    ref = hashlib.sha384 if out_bits == 384 else hashlib.sha512
+    rng = np.random.default_rng(50 + out_bits + blocks)
+    msgs, rows = [], []
+    for i in range(40):
+        ln = int(rng.integers(max(128 * blocks - 144, 0), 128 * blocks - 16))
+        m = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        p = inputs.sha_pad(m, 1024)
+        assert len(p) == 128 * blocks
+        r = np.zeros((1024 * blocks, 32), np.uint8)
+        r[:, 0] = inputs.bits_msb_first(p)
+        msgs.append(m)
+        rows.append(r)
+    batch = np.stack(rows)
+    inst = native.Instance(circ, blocks)
+    wit, st = inst.witness_batch_host(batch)
+    assert (st == 0).all()
+    for b, m in enumerate(msgs):
+        assert np.packbits(wit[b, 1:1 + out_bits, 0]).tobytes() == ref(m).digest(), b
+    for b in range(3):
+        rc, refw = oracle.sha512_witness(batch[b], blocks, out_bits)
+        assert rc == 0
+        assert refw.shape == wit[b].shape
+        bad = np.nonzero((refw != wit[b]).any(axis=1))[0]
+        assert bad.size == 0, "msg %d: %d mismatching signals, first %s" % (b, bad.size, bad[:8].tolist())
+
+
+def test_sha512_circuit_rejects_nonbinary_input():
+    """A message element outside {0, 1} fails the core's range check (status ST_INPUT_RANGE)."""
+    r = np.zeros((2, 1024, 32), np.uint8)
+    r[1, 5, 0] = 2
+    inst = native.Instance(native.PZK_CIRCUIT_SHA512, 1)
+    _, st = inst.witness_batch_host(r)
+    assert st[0] == 0 and st[1] != 0
+
+
 def test_sha256_config2_fullsize(oracle):
     """Config 2 at its stated size (BASELINE.json configs[1]): Sha256HashChunks(6),
     batch 1024, seed 2, on the device-buffer path. All 1024 digests equal hashlib.sha256; rows 0, 1,

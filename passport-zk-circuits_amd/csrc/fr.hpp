@@ -4,7 +4,7 @@
 // that are Fr products are carried in Montgomery form inside the core kernels and
 // converted once, in the emit kernels, right before the 32-byte store.
 //
-// Multiplication is CIOS with the "no final carry" shortcut that is valid because the
+// Multiplication is CIOS with the "no final carry" shortcut (fr_mul), or FIPS (fr_mul_fast) that is valid because the
 // top word of p (0x30644e72) is < (2^32-1)/2 - 1: each step is one v_mad_u64_u32
 // (32x32 + 64 -> 64) per limb product. p < 2^254 also lets additions skip the
 // 257th bit.
@@ -72,6 +72,82 @@ __device__ __forceinline__ fr fr_sub(const fr& a, const fr& b) {
 
 __device__ __forceinline__ fr fr_neg(const fr& a) { return fr_sub(fr_zero(), a); }
 
+// Throughput form of the Montgomery product for the emitters (pos_img_fill in poseidon.hpp,
+// regemit.hpp), FIPS order (product scanning with the reduction interleaved
+// per column): column k accumulates a_j*b_(k-j) and m_j*p_(k-j) into a 96-bit accumulator, each
+// 32x32 product being one v_mad_u64_u32 into the accumulator's low 64 bits whose carry-out (vcc)
+// goes into the top word — 2 VALU per product, no register moves. The carry read is 2 wait states
+// after its write (s_nop 1), the spacing hipcc itself keeps on gfx950 between a VALU write of VCC
+// and a VALU carry-in read. Measured on MI355X
+// (tools/fieldbench): 1,200 cycles per wave64 product per SIMD against 1,554 for operand-scanning
+// CIOS (whose carries cost ~3 moves per product). On a dependent chain at one wave per SIMD the
+// carry pad makes it slower (1,233 ns against 1,091 ns), so the latency-bound cores keep fr_mul. A column sums at most 16 products plus the carry-in (< 2^69).
+__device__ __forceinline__ void fr_mac(uint64_t& acc, uint32_t& top, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(top) : "v"(x), "v"(y) : "vcc");
+}
+// same with y a wave-uniform constant (the modulus words) in an SGPR
+__device__ __forceinline__ void fr_mac_s(uint64_t& acc, uint32_t& top, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(top) : "v"(x), "s"(y) : "vcc");
+}
+__device__ __forceinline__ fr fr_mul_fast(const fr& a, const fr& b) {
+  uint32_t m[8];
+  fr r;
+  uint64_t acc = 0;
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int j0 = k < 8 ? 0 : k - 7, j1 = k < 8 ? k : 7;
+#pragma unroll
+    for (int j = j0; j <= j1; j++) {
+      fr_mac(acc, top, a.v[j], b.v[k - j]);
+      if (j < k && j < 8 && k - j < 8) fr_mac_s(acc, top, m[j], P_[k - j]);
+    }
+    if (k < 8) {
+      m[k] = (uint32_t)acc * PINV;
+      fr_mac_s(acc, top, m[k], P_[0]);  // clears the column's low word
+    } else {
+      r.v[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  return fr_reduce_once(r);
+}
+
+// (a dedicated FIPS squaring, 36 instead of 64 operand products but doubled per column, measured
+// slower than fr_mul_fast(a, a): 1,289 vs 1,200 cycles)
+__device__ __forceinline__ fr fr_sqr_fast(const fr& a) { return fr_mul_fast(a, a); }
+
+// a*2^-256 mod p (Montgomery -> normal form): the reduction half of fr_mul_fast
+__device__ __forceinline__ fr fr_from_mont_fast(const fr& a) {
+  uint32_t m[8];
+  fr r;
+  uint64_t acc = 0;
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    if (k < 8) acc += a.v[k];  // < 2^64: the carry-in is < 2^37 here
+#pragma unroll
+    for (int j = (k < 8 ? 0 : k - 7); j < (k < 8 ? k : 8); j++) fr_mac_s(acc, top, m[j], P_[k - j]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * PINV;
+      fr_mac_s(acc, top, m[k], P_[0]);
+    } else {
+      r.v[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  return fr_reduce_once(r);
+}
+// The general fr_mul / fr_sqr / fr_from_mont below stay operand-scanning CIOS: with the FIPS
+// product inlined, the EC table walker (ec_walk.hpp, EcWalk<EcTabCtx>::run, a ~50 k-instruction
+// callable function) did not terminate on MI355X and the brainpoolP256r1 path faulted, although
+// the FIPS product equals the CIOS one on every input of tools/fieldbench's stress kernel
+// (divergent lanes; product, square, inverse chains). Cause not isolated;
+// the _fast forms are used only where GPU parity tests cover every output element.
 // Montgomery product a*b*2^-256 mod p
 __device__ __forceinline__ fr fr_mul(const fr& a, const fr& b) {
   uint32_t t[8];

@@ -195,8 +195,8 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
       const int ci = f < 4 ? f * t + j : f == 4 ? 4 * t + RP * t + j : 4 * t + (RP + 1) * t + (f - 5) * t + j;
       // mixed forms: mont_mul(aR, b) = ab, so normal-form powers come straight out of products
       // with the Montgomery-form x and x^2 (3.4 products per S-box instead of 5.3)
-      const fr xm = core[ci], x2m = fr_sqr(xm), x2 = fr_from_mont(x2m), x4 = fr_mul(x2m, x2), x5 = fr_mul(x4, xm);
-      img[I.in + q] = fr_from_mont(xm); img[I.p2 + q] = x2;
+      const fr xm = core[ci], x2m = fr_sqr_fast(xm), x2 = fr_from_mont_fast(x2m), x4 = fr_mul_fast(x2m, x2), x5 = fr_mul_fast(x4, xm);
+      img[I.in + q] = fr_from_mont_fast(xm); img[I.p2 + q] = x2;
       img[I.p4 + q] = x4; img[I.p5 + q] = x5;
       if (f < 7) {
         const int cidx = f < 4 ? (f + 1) * t + j : 5 * t + RP + (f - 4) * t + j;
@@ -204,9 +204,9 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
       }
     } else if (q < NA) {
       const int r = q - 8 * t;
-      const fr xm = core[4 * t + r * t], x2m = fr_sqr(xm), x2 = fr_from_mont(x2m), x4 = fr_mul(x2m, x2),
-               x5 = fr_mul(x4, xm);
-      img[I.pin + r * t] = fr_from_mont(xm); img[I.pp2 + r] = x2;
+      const fr xm = core[4 * t + r * t], x2m = fr_sqr_fast(xm), x2 = fr_from_mont_fast(x2m), x4 = fr_mul_fast(x2m, x2),
+               x5 = fr_mul_fast(x4, xm);
+      img[I.pin + r * t] = fr_from_mont_fast(xm); img[I.pp2 + r] = x2;
       img[I.pp4 + r] = x4; img[I.pp5 + r] = x5;
       img[I.pin0 + r] = fr_add(x5, K.Cn(t, 5 * t + r));
     } else if (q < NA + NC) {
@@ -214,11 +214,11 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
       int r, i;
       if (c < RP * (t - 1)) { r = c / (t - 1); i = 1 + (c - r * (t - 1)); }
       else { r = RP; i = c - RP * (t - 1); }
-      img[I.pin + r * t + i] = fr_from_mont(core[4 * t + r * t + i]);
+      img[I.pin + r * t + i] = fr_from_mont_fast(core[4 * t + r * t + i]);
     } else {
       const int k = q - NA - NC;
-      if (k < task.n) img[I.inp + k] = fr_from_mont(vs.at(task.in_slot[k], w));
-      else if (k == 5) img[I.hash] = fr_from_mont(vs.at(task.out_slot, w));
+      if (k < task.n) img[I.inp + k] = fr_from_mont_fast(vs.at(task.in_slot[k], w));
+      else if (k == 5) img[I.hash] = fr_from_mont_fast(vs.at(task.out_slot, w));
       else if (k == 6) img[I.zero] = fr_zero();
     }
   }
@@ -245,7 +245,7 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
       v = k == 0 ? img[I.pin0 + r] : img[I.pin + r * t + k];
       dst = I.ps + r * t + k;
     }
-    img[dst] = fr_mul(c, v);
+    img[dst] = fr_mul_fast(c, v);
   }
   __syncthreads();
   // prefix sums along each row

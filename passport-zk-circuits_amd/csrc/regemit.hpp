@@ -69,7 +69,7 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   const fr* smt = B.smt_core + (size_t)w * L.smt_core_fr;
   const uint32_t* flags = reinterpret_cast<const uint32_t*>(smt + 2 * SMT_LEVELS);
-  auto V = [&](int slot) { return fr_from_mont(B.vs.at(slot, w)); };
+  auto V = [&](int slot) { return fr_from_mont_fast(B.vs.at(slot, w)); };
   switch (R.kind) {
     case RK_ONE: return el_u64(1);
     case RK_INCOPY: return el_load(row + 32ull * ((uint64_t)R.a[0] + s));
@@ -90,8 +90,8 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
       } else {
         fr t64 = fr_zero(); t64.v[2] = 1;
         fr t128 = fr_zero(); t128.v[4] = 1;
-        fr v = fr_add(fr_mul(fr_to_mont(load_fr(a)), fr_to_mont(t128)), fr_mul(fr_to_mont(load_fr(b)), fr_to_mont(t64)));
-        return el_fr(fr_from_mont(v));
+        fr v = fr_add(fr_mul_fast(fr_to_mont(load_fr(a)), fr_to_mont(t128)), fr_mul_fast(fr_to_mont(load_fr(b)), fr_to_mont(t64)));
+        return el_fr(fr_from_mont_fast(v));
       }
     }
     case RK_HCHUNK: {
@@ -105,7 +105,7 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
     }
     case RK_SMT_OWN: {  // isVerified | root, leaf, key, siblings[80] | value
       if (s == 0) {
-        fr r0 = fr_from_mont(smt[SMT_LEVELS]);
+        fr r0 = fr_from_mont_fast(smt[SMT_LEVELS]);
         return el_u64(fr_eq(r0, load_fr(row + 32ull * R.a[0])) ? 1 : 0);
       } else if (s == 1) return el_load(row + 32ull * R.a[0]);
       else if (s == 2 || s == 3 || s == 84) return el_fr(V(G.v_pkhash));
@@ -135,13 +135,13 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
       int i = R.a[0];
       uint32_t f = flags[i];
       switch (s) {
-        case 0: return el_fr(fr_from_mont(smt[SMT_LEVELS + i]));
+        case 0: return el_fr(fr_from_mont_fast(smt[SMT_LEVELS + i]));
         case 1: return el_u64((f >> 2) & 1);
         case 2: return el_u64((f >> 3) & 1);
         case 3: return el_load(row + 32ull * (R.a[1] + i));
         case 4: return el_fr(V(G.v_leaf));
         case 5: return el_u64((f >> 4) & 1);
-        case 6: return el_fr(i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1]));
+        case 6: return el_fr(i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont_fast(smt[SMT_LEVELS + i + 1]));
         default: return el_fr((f & 4) ? V(G.v_smt_h + i) : fr_zero());
       }
     }
@@ -150,25 +150,25 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
       uint32_t lr = (flags[i] >> 4) & 1;
       if (s < 2) { return el_fr(V(G.v_smt_lr + 2 * i + (int)s)); }
       if (s == 2) { return el_u64(lr); }
-      fr child = i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont(smt[SMT_LEVELS + i + 1]);
+      fr child = i == SMT_LEVELS - 1 ? fr_zero() : fr_from_mont_fast(smt[SMT_LEVELS + i + 1]);
       fr sib = load_fr(row + 32ull * (R.a[1] + i));
       if (s == 3) return el_fr(child);
       else if (s == 4) return el_load(row + 32ull * (R.a[1] + i));
       else return el_fr(lr ? fr_sub(sib, child) : fr_zero());
     }
     case RK_ISEQ_ROOT: {  // out | in[2] | IsZero(out, in, inv)
-      fr r0 = fr_from_mont(smt[SMT_LEVELS]);
+      fr r0 = fr_from_mont_fast(smt[SMT_LEVELS]);
       fr rin = load_fr(row + 32ull * R.a[0]);
       uint32_t eq = fr_eq(r0, rin);
       if (s == 0 || s == 3) return el_u64(eq);
       else if (s == 1) return el_fr(r0);
       else if (s == 2) return el_load(row + 32ull * R.a[0]);
       else if (s == 4) return el_fr(fr_sub(rin, r0));
-      else return el_fr(fr_from_mont(smt[3 * SMT_LEVELS + 1]));
+      else return el_fr(fr_from_mont_fast(smt[3 * SMT_LEVELS + 1]));
     }
     case RK_BJJ_OWN: {  // out[2] | scalar | base8[2]
       const fr* bc = B.bjj_core + (size_t)w * L.bjj_core_fr + 5 * (BJJ_STEPS - 1);
-      if (s < 2) return el_fr(fr_from_mont(bc[2 + s]));
+      if (s < 2) return el_fr(fr_from_mont_fast(bc[2 + s]));
       else if (s == 2) return el_fr(V(G.v_sk));
       else {
         W256 r; for (int i = 0; i < 8; i++) r.v[i] = s == 3 ? BJJ_B8X[i] : BJJ_B8Y[i];
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
       if (src_bit(j)) atomicOr(&val[j >> 5], 1u << (j & 31));
   } else if (threadIdx.x == 0) {
     fr v;
-    if (R.a[1] == 0) v = fr_from_mont(B.vs.at(R.a[2], w));
+    if (R.a[1] == 0) v = fr_from_mont_fast(B.vs.at(R.a[2], w));
     else v = fr_u64(B.rsa_core[(size_t)w * L.rsa_core_words + (size_t)(L.reg.n_modmul - 1) * MM_CORE_WORDS(L.reg.K) +
                                3 * L.reg.K + 1 + R.a[2]]);
     inval = v;
@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
     else { a = (i >= 4 ? 1u : 0u) * V; b = ebit(d15s - 24 + i) * V; }  // 0x0F prefix, MSB first
   };
   for (int k = threadIdx.x; k < NC; k += blockDim.x) { uint32_t a, b; pair(k, a, b); eq[k] = a == b; }
-  if (threadIdx.x == 0) invV = V > 1 ? fr_from_mont(fr_inv(fr_to_mont(fr_u64((uint64_t)V)))) : fr_u64(1);
+  if (threadIdx.x == 0) invV = V > 1 ? fr_from_mont_fast(fr_inv(fr_to_mont(fr_u64((uint64_t)V)))) : fr_u64(1);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint8_t c = 1;
@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
   const int nrec = (int)i1 - base;
   {
     fr skm = B.vs.at(L.reg.v_sk, w);
-    fr sk = fr_from_mont(skm);
+    fr sk = fr_from_mont_fast(skm);
     for (int j = threadIdx.x; j < nrec; j += blockDim.x) {
       int i = base + j;
       bits[j] = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
@@ -770,10 +770,10 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
       if (i == 0) r = fr_zero();
       else {
         fr xp = P[-3], yp = P[-2];  // core + 5(i-1) + 2, + 3
-        fr xy = fr_mul(xp, yp);
+        fr xy = fr_mul_fast(xp, yp);
         if (v == BR_XYD) r = xy;
-        else if (v == BR_DELTAD) r = fr_mul(fr_sub(yp, fr_mul(fr_to_mont(fr_u64(BJJ_A)), xp)), fr_add(xp, yp));
-        else r = fr_sqr(xy);
+        else if (v == BR_DELTAD) r = fr_mul_fast(fr_sub(yp, fr_mul_fast(fr_to_mont(fr_u64(BJJ_A)), xp)), fr_add(xp, yp));
+        else r = fr_sqr_fast(xy);
       }
     } else if (v == BR_OX || v == BR_OY) {
       r = P[v];
@@ -785,13 +785,13 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
         case BR_X1: r = x1; break;
         case BR_Y1: r = y1; break;
         case BR_INV: r = i == 0 ? fr_zero() : P[4]; break;
-        case BR_X1Y2: r = fr_mul(x1, y2); break;
-        case BR_Y1X2: r = fr_mul(y1, x2); break;
-        case BR_DELTA: r = fr_mul(fr_sub(y1, fr_mul(fr_to_mont(fr_u64(BJJ_A)), x1)), fr_add(x2, y2)); break;
-        default: r = fr_mul(fr_mul(x1, y2), fr_mul(y1, x2)); break;
+        case BR_X1Y2: r = fr_mul_fast(x1, y2); break;
+        case BR_Y1X2: r = fr_mul_fast(y1, x2); break;
+        case BR_DELTA: r = fr_mul_fast(fr_sub(y1, fr_mul_fast(fr_to_mont(fr_u64(BJJ_A)), x1)), fr_add(x2, y2)); break;
+        default: r = fr_mul_fast(fr_mul_fast(x1, y2), fr_mul_fast(y1, x2)); break;
       }
     }
-    rec[j * BR_N + v] = fr_from_mont(r);
+    rec[j * BR_N + v] = fr_from_mont_fast(r);
   }
   __syncthreads();
   const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);

@@ -803,12 +803,21 @@ static void run_sha1chunks(ctx_t *c, size_t b, int B) {
     for (int k = 0; k < 32; k++) W(b + (31 - k) + 32 * i) = W(last + k + 32 * i);
 }
 
-/* ShaHashChunks(B, ALGO) hash.circom:32-68 for ALGO 160 / 256: out[ALGO] | in[512B] | Sha1/Sha256HashChunks(B) */
+/* ShaHashChunks(B, ALGO) hash.circom:32-68: out[ALGO] | in[BS x B] | Sha1 / Sha224 / Sha256 / Sha384 / Sha512HashChunks(B),
+ * BS = 512 bits for ALGO <= 256, 1024 above */
 static size_t sz_hashc(int algo, int B) {
+  if (algo > 256) return (size_t)algo + 1024 * (size_t)B + sz_sha5chunks(algo, B);
   return algo == 160 ? 160 + 512 * (size_t)B + sz_sha1chunks(B) : algo == 224 ? 224 + 512 * (size_t)B + sz_sha2chunks(224, B)
                                                                   : sz_shahash(B);
 }
 static void run_hashc(ctx_t *c, size_t b, int algo, int B) {
+  if (algo > 256) {
+    size_t in = b + algo, h = in + 1024 * (size_t)B;
+    for (size_t q = 0; q < 1024 * (size_t)B; q++) W(h + algo + q) = W(in + q);
+    run_sha5chunks(c, h, B, algo);
+    for (int q = 0; q < algo; q++) W(b + q) = W(h + q);
+    return;
+  }
   if (algo == 224) {
     size_t in = b + 224, h = in + 512 * (size_t)B;
     for (size_t q = 0; q < 512 * (size_t)B; q++) W(h + 224 + q) = W(in + q);
@@ -1381,53 +1390,57 @@ static void run_verifysig(ctx_t *c, size_t b, int K, int HT, long EXP) {
   else run_rsa(c, rsa, K, EXP);
 }
 
-/* ================================================= RSA-PSS (SIGNATURE_TYPE 10, 11, 12)
- * VerifyRsaPssSig(64, K, SALT, EXP, 256) rsaPss.circom:18-204 with Mgf1Sha256 mgf1.circom:69-127.
- * SIG 10: e = 3, salt 32; SIG 11: e = 65537, salt 32; SIG 12: e = 65537, salt 64
- * (signatureVerification.circom:46-62). EM = PowerMod.out, 8K bytes; DB = EM_LEN - HASH_LEN - 1 bytes. */
-static int is_pss(int sig) { return (sig >= 10 && sig <= 12) || sig == 14; }
-static int pss_salt(int sig) { return sig == 12 ? 64 : 32; }
+/* ================================================= RSA-PSS (SIGNATURE_TYPE 10-14)
+ * VerifyRsaPssSig(64, K, SALT, EXP, H) rsaPss.circom:18-254 with Mgf1Sha256 / Mgf1Sha384 mgf1.circom:5-133.
+ * SIG 10: e = 3, salt 32; SIG 11: e = 65537, salt 32; SIG 12: e = 65537, salt 64; SIG 13: SHA-384, salt 48;
+ * SIG 14: RSA-3072 (signatureVerification.circom:46-75). EM = PowerMod.out, 8K bytes; DB = EM_LEN - H/8 - 1 bytes. */
+static int is_pss(int sig) { return sig >= 10 && sig <= 14; }
+static int pss_salt(int sig) { return sig == 12 ? 64 : sig == 13 ? 48 : 32; }
+static int pss_hash(int sig) { return sig == 13 ? 384 : 256; }
 static long sig_exp(int sig) { return sig == 10 ? 3 : sig == 4 ? 37187 : 65537; }
 
-/* Mgf1Sha256(32, DBL): out[8 DBL] | seed[256] | hashed[256 IT] | (ShaHashChunks(1,256), Num2Bits(32)) x IT */
-static int mgf_iters(int DBL) { return DBL / 32 + 1; }
-static size_t sz_mgf1(int DBL) {
-  int IT = mgf_iters(DBL);
-  return 8 * (size_t)DBL + 256 + 256 * (size_t)IT + (size_t)IT * (sz_shahash(1) + sz_num2bits(32));
+/* Mgf1ShaH(H/8, DBL): out[8 DBL] | seed[H] | hashed[H IT] | (ShaHashChunks(1, H), Num2Bits(32)) x IT, IT = DBL / (H/8) + 1;
+ * each block hashes seed | counter (MSB first) | the padding of an (H + 32)-bit message in one BS-bit block */
+static int mgf_iters(int DBL, int H) { return DBL / (H / 8) + 1; }
+static size_t sz_mgf1(int DBL, int H) {
+  int IT = mgf_iters(DBL, H);
+  return 8 * (size_t)DBL + H + (size_t)H * IT + (size_t)IT * (sz_hashc(H, 1) + sz_num2bits(32));
 }
-static void run_mgf1(ctx_t *c, size_t b, int DBL) {
-  int IT = mgf_iters(DBL);
-  size_t out = b, seed = out + 8 * (size_t)DBL, hashed = seed + 256, sub = hashed + 256 * (size_t)IT;
+static void run_mgf1(ctx_t *c, size_t b, int DBL, int H) {
+  const int IT = mgf_iters(DBL, H), BS = H > 256 ? 1024 : 512, LM = H + 32;
+  size_t out = b, seed = out + 8 * (size_t)DBL, hashed = seed + H, sub = hashed + (size_t)H * IT;
   for (int i = 0; i < IT; i++) {
-    size_t sh = sub + (size_t)i * (sz_shahash(1) + sz_num2bits(32)), nb = sh + sz_shahash(1), in = sh + 256;
+    size_t sh = sub + (size_t)i * (sz_hashc(H, 1) + sz_num2bits(32)), nb = sh + sz_hashc(H, 1), in = sh + H;
     W(nb + 32) = fr_u64((uint64_t)i);
     run_num2bits(c, nb, 32);
-    /* concated = seed | counter (MSB first) | padding for a 288-bit message (mgf1.circom:97-121) */
-    for (int j = 0; j < 256; j++) W(in + j) = W(seed + j);
-    for (int j = 0; j < 32; j++) W(in + 256 + j) = W(nb + 31 - j);
-    for (int j = 288; j < 512; j++) W(in + j) = fr_zero();
-    W(in + 288) = ONE(); W(in + 503) = ONE(); W(in + 506) = ONE();
-    run_shahash(c, sh, 1);
-    for (int j = 0; j < 256; j++) W(hashed + 256 * (size_t)i + j) = W(sh + j);
+    /* concated (mgf1.circom:30-58, 95-121) */
+    for (int j = 0; j < H; j++) W(in + j) = W(seed + j);
+    for (int j = 0; j < 32; j++) W(in + H + j) = W(nb + 31 - j);
+    for (int j = LM; j < BS; j++) W(in + j) = fr_zero();
+    W(in + LM) = ONE();
+    for (int k = 0; k < 11; k++)
+      if ((LM >> k) & 1) W(in + BS - 1 - k) = ONE();
+    run_hashc(c, sh, H, 1);
+    for (int j = 0; j < H; j++) W(hashed + (size_t)H * i + j) = W(sh + j);
   }
   for (int i = 0; i < 8 * DBL; i++) W(out + i) = W(hashed + i);
 }
 
-/* own: pubkey[K], signature[K], hashed[256] | eM[EML], eMsgInBits[64K], encoded[K], dbMask[DB8], db[DB8],
- *      salt[S8], maskedDB[DB8], hash[256], mDash[1024]
- * subcomponents: powerMod, num2Bits[K] (Num2Bits(64)), bits2Num[EML] (Bits2Num(8)), MGF1_256, xor (Xor2(DB8):
- * out | in1 | in2), hDash256 (ShaHashChunks(2, 256)) */
-static size_t sz_pss(int K, int S, long EXP) {
-  size_t EML = 8 * (size_t)K, DB8 = 8 * (EML - 33);
-  return 2 * (size_t)K + 256 + EML + 64 * (size_t)K + K + 3 * DB8 + 8 * (size_t)S + 256 + 1024 + sz_powermod(64, K, EXP) +
-         (size_t)K * sz_num2bits(64) + EML * sz_bits2num(8) + sz_mgf1((int)EML - 33) + 3 * DB8 + sz_shahash(2);
+/* own: pubkey[K], signature[K], hashed[H] | eM[EML], eMsgInBits[64K], encoded[K], dbMask[DB8], db[DB8],
+ *      salt[S8], maskedDB[DB8], hash[H], mDash[1024]
+ * subcomponents: powerMod, num2Bits[K] (Num2Bits(64)), bits2Num[EML] (Bits2Num(8)), MGF1_H, xor (Xor2(DB8):
+ * out | in1 | in2), hDash (ShaHashChunks(2, 256) or ShaHashChunks(1, 384): M' is 1024 bits either way) */
+static size_t sz_pss(int K, int S, long EXP, int H) {
+  size_t EML = 8 * (size_t)K, DBL = EML - H / 8 - 1, DB8 = 8 * DBL;
+  return 2 * (size_t)K + H + EML + 64 * (size_t)K + K + 3 * DB8 + 8 * (size_t)S + H + 1024 + sz_powermod(64, K, EXP) +
+         (size_t)K * sz_num2bits(64) + EML * sz_bits2num(8) + sz_mgf1((int)DBL, H) + 3 * DB8 + sz_hashc(H, 1024 / (H > 256 ? 1024 : 512));
 }
-static void run_pss(ctx_t *c, size_t b, int K, int S, long EXP) {
-  const int EMB = 64 * K, EML = 8 * K, DBL = EML - 33, DB8 = 8 * DBL, S8 = 8 * S;
-  size_t pk = b, sig = pk + K, hashed = sig + K, eM = hashed + 256, bits = eM + EML, enc = bits + EMB,
+static void run_pss(ctx_t *c, size_t b, int K, int S, long EXP, int H) {
+  const int EMB = 64 * K, EML = 8 * K, DBL = EML - H / 8 - 1, DB8 = 8 * DBL, S8 = 8 * S, MB = H > 256 ? 1 : 2;
+  size_t pk = b, sig = pk + K, hashed = sig + K, eM = hashed + H, bits = eM + EML, enc = bits + EMB,
          dbMask = enc + K, db = dbMask + DB8, salt = db + DB8, masked = salt + S8, hash = masked + DB8,
-         mDash = hash + 256, pm = mDash + 1024, n2b = pm + sz_powermod(64, K, EXP),
-         b2n = n2b + (size_t)K * sz_num2bits(64), mgf = b2n + (size_t)EML * sz_bits2num(8), xr = mgf + sz_mgf1(DBL),
+         mDash = hash + H, pm = mDash + 1024, n2b = pm + sz_powermod(64, K, EXP),
+         b2n = n2b + (size_t)K * sz_num2bits(64), mgf = b2n + (size_t)EML * sz_bits2num(8), xr = mgf + sz_mgf1(DBL, H),
          hd = xr + 3 * (size_t)DB8;
   for (int i = 0; i < K; i++) { W(pm + K + i) = W(sig + i); W(pm + 2 * K + i) = W(pk + i); }
   run_powermod(c, pm, 64, K, EXP);
@@ -1446,9 +1459,9 @@ static void run_pss(ctx_t *c, size_t b, int K, int S, long EXP) {
   }
   if (!fr_eq(W(eM), fr_u64(188)) && !c->err) c->err = S_PSS_TRAILER;
   for (int i = 0; i < DB8; i++) W(masked + i) = W(bits + i);
-  for (int i = 0; i < 256; i++) W(hash + i) = W(bits + EMB - 256 - 8 + i);
-  for (int i = 0; i < 256; i++) W(mgf + DB8 + i) = W(hash + i);
-  run_mgf1(c, mgf, DBL);
+  for (int i = 0; i < H; i++) W(hash + i) = W(bits + EMB - H - 8 + i);
+  for (int i = 0; i < H; i++) W(mgf + DB8 + i) = W(hash + i);
+  run_mgf1(c, mgf, DBL, H);
   for (int i = 0; i < DB8; i++) W(dbMask + i) = W(mgf + i);
   for (int i = 0; i < DB8; i++) { /* Xor2 (bitGates.circom:232-240) */
     fr_t x = W(masked + i), y = W(dbMask + i);
@@ -1458,27 +1471,30 @@ static void run_pss(ctx_t *c, size_t b, int K, int S, long EXP) {
   W(db) = fr_zero();
   for (int i = 1; i < DB8; i++) W(db + i) = W(xr + i);
   for (int i = 0; i < S8; i++) W(salt + S8 - 1 - i) = W(db + DB8 - 1 - i);
-  /* mDash = 0^64 | hashed | salt | SHA-256 padding of a (320 + S8)-bit message (:153-200) */
-  const int LM = 64 + 256 + S8;
+  /* mDash = 0^64 | hashed | salt | padding of a (64 + H + S8)-bit message to 1024 bits (:146-226) */
+  const int LM = 64 + H + S8;
   for (int i = 0; i < 1024; i++) W(mDash + i) = fr_zero();
-  for (int i = 0; i < 256; i++) W(mDash + 64 + i) = W(hashed + i);
-  for (int i = 0; i < S8; i++) W(mDash + 320 + i) = W(salt + i);
+  for (int i = 0; i < H; i++) W(mDash + 64 + i) = W(hashed + i);
+  for (int i = 0; i < S8; i++) W(mDash + 64 + H + i) = W(salt + i);
   W(mDash + LM) = ONE();
   for (int k = 0; k < 11; k++)
     if ((LM >> k) & 1) W(mDash + 1023 - k) = ONE();
-  for (int i = 0; i < 1024; i++) W(hd + 256 + i) = W(mDash + i);
-  run_shahash(c, hd, 2);
+  for (int i = 0; i < 1024; i++) W(hd + H + i) = W(mDash + i);
+  run_hashc(c, hd, H, MB);
   int bad = 0;
-  for (int i = 0; i < 256; i++) bad |= !fr_eq(W(hd + i), W(hash + i));
+  for (int i = 0; i < H; i++) bad |= !fr_eq(W(hd + i), W(hash + i));
   if (bad && !c->err) c->err = S_PSS_HASH;
 }
 
-/* VerifySignature(SIG 10-12): pubkey[K], signature[K], hashed[256] | VerifyRsaPssSig */
-static size_t sz_verifysig_pss(int K, int sig) { return 2 * (size_t)K + 256 + sz_pss(K, pss_salt(sig), sig_exp(sig)); }
+/* VerifySignature(SIG 10-14): pubkey[K], signature[K], hashed[H] | VerifyRsaPssSig */
+static size_t sz_verifysig_pss(int K, int sig) {
+  return 2 * (size_t)K + pss_hash(sig) + sz_pss(K, pss_salt(sig), sig_exp(sig), pss_hash(sig));
+}
 static void run_verifysig_pss(ctx_t *c, size_t b, int K, int sig) {
-  size_t v = b + 2 * K + 256;
-  for (int i = 0; i < 2 * K + 256; i++) W(v + i) = W(b + i);
-  run_pss(c, v, K, pss_salt(sig), sig_exp(sig));
+  const int H = pss_hash(sig);
+  size_t v = b + 2 * K + H;
+  for (int i = 0; i < 2 * K + H; i++) W(v + i) = W(b + i);
+  run_pss(c, v, K, pss_salt(sig), sig_exp(sig), H);
 }
 
 #include "ecdsa_p256.inc.c"
@@ -1592,30 +1608,34 @@ static int sig_chunks(int sig) { return sig == 2 ? 64 : (sig == 14 || sig == 4) 
 /* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
 static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
 
-/* HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:19-50): 160 for SIG 3 */
-static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : 256; }
+/* HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:19-50): 160 for
+ * SIG 3 / 4, 384 for SIG 13; inputs hashed with it come in HASH_BLOCK_SIZE = 512 / 1024-bit blocks (:61-68) */
+static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : sig == 13 ? 384 : 256; }
+static int hblock(int algo) { return algo > 256 ? 1024 : 512; }
 static size_t sz_pvb(const orc_params *P) {
-  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, ec = P->sig >= 20;
   int DG = P->dg_hash, HT = sig_hash(P->sig);
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * hblock(HT), dg15Len = P->dg15_blocks * hblock(HT), ec = P->sig >= 20;
   /* own: ..., dg1Hash[DG], dg15Hash[DG], ecHash[HT], saHash[HT], pubkeyHash, then tempModulus[5] (RSA, :184) or
    * ecBitsX[256], ecBitsY[256] (ECDSA, :197-198) */
   size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 2 * (size_t)DG + 2 * (size_t)HT + 1 + (ec ? 512 : 5);
   size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
-  return own + sz_hashc(DG, 2) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(HT, P->ec_blocks) + sz_hashc(HT, 2) +
+  return own + sz_hashc(DG, 1024 / hblock(DG)) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(HT, P->ec_blocks) +
+         sz_hashc(HT, 1024 / hblock(HT)) +
          sz_flow(ecLen, DG, HT) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig))) +
          sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
-  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512, isec = P->sig >= 20;
   int DG = P->dg_hash, HT = sig_hash(P->sig);
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * hblock(HT), dg15Len = P->dg15_blocks * hblock(HT), isec = P->sig >= 20;
+  const int dg1B = 1024 / hblock(DG), saB = 1024 / hblock(HT), dg15HB = P->dg15_blocks * hblock(DG);
   size_t ec = b + 1, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
          br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + DG, ecH = dg15H + DG, saH = ecH + HT,
          pkHash = saH + HT, tmpMod = pkHash + 1;
   size_t p = tmpMod + (isec ? 512 : 5);
-  size_t hDg1 = p; p += sz_hashc(DG, 2);
+  size_t hDg1 = p; p += sz_hashc(DG, dg1B);
   size_t hDg15 = 0; if (P->aa) { hDg15 = p; p += sz_hashc(DG, P->dg15_blocks); }
   size_t hEc = p; p += sz_hashc(HT, P->ec_blocks);
-  size_t hSa = p; p += sz_hashc(HT, 2);
+  size_t hSa = p; p += sz_hashc(HT, saB);
   size_t flow = p; p += sz_flow(ecLen, DG, HT);
   size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig));
   size_t saNum = p; p += sz_bits2num(252);
@@ -1624,10 +1644,11 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   size_t saHH = p;
   /* hashes */
   for (int i = 0; i < 1024; i++) W(hDg1 + DG + i) = W(dg1 + i);
-  run_hashc(c, hDg1, DG, 2);
+  run_hashc(c, hDg1, DG, dg1B);
   for (int i = 0; i < DG; i++) W(dg1H + i) = W(hDg1 + i);
   if (P->aa) {
-    for (int i = 0; i < dg15Len; i++) W(hDg15 + DG + i) = W(dg15 + i);
+    /* dg15PassportHasher.in[j] <== dg15[j] for j < DG_HASH_BLOCK_SIZE * DG15_BLOCK_NUMBER (:117-120) */
+    for (int i = 0; i < dg15HB; i++) W(hDg15 + DG + i) = W(dg15 + i);
     run_hashc(c, hDg15, DG, P->dg15_blocks);
     for (int i = 0; i < DG; i++) W(dg15H + i) = W(hDg15 + i);
   } else {
@@ -1637,7 +1658,7 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   run_hashc(c, hEc, HT, P->ec_blocks);
   for (int i = 0; i < HT; i++) W(ecH + i) = W(hEc + i);
   for (int i = 0; i < 1024; i++) W(hSa + HT + i) = W(sa + i);
-  run_hashc(c, hSa, HT, 2);
+  run_hashc(c, hSa, HT, saB);
   for (int i = 0; i < HT; i++) W(saH + i) = W(hSa + i);
   /* flow */
   {
@@ -1697,15 +1718,16 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
 static int aa_is_ec(int aa) { return aa >= 20; }
 static int aa_field(int aa) { return aa == 22 ? 320 : aa == 23 ? 192 : 256; }
 static int aa_hsize(int aa) { return aa == 23 ? 192 : 248; }
+/* RegisterIdentity(DG15_SIZE, DG_HASH_BLOCK_SIZE, ...): dg15[DG15_SIZE x DG_HASH_BLOCK_SIZE] (identity.circom:6-23) */
 static size_t sz_regid(const orc_params *P) {
-  int dg15Len = P->dg15_blocks * 512, ch = P->doc == 1 ? 190 : 186;
+  int dg15Len = P->dg15_blocks * hblock(P->dg_hash), ch = P->doc == 1 ? 190 : 186;
   size_t own = 3 + 1024 + (size_t)dg15Len + 1;
   size_t aa = !P->aa ? 0 : aa_is_ec(P->aa) ? 2 * sz_bits2num(aa_hsize(P->aa)) + sz_poseidon(2)
                                            : 4 * sz_bits2num(200) + sz_bits2num(224) + sz_poseidon(5);
   return own + aa + sz_poseidon(5) + 4 * sz_bits2num(ch) + sz_poseidon(1) + sz_bjjmul() + sz_poseidon(2);
 }
 static void run_regid(ctx_t *c, size_t b, const orc_params *P) {
-  int dg15Len = P->dg15_blocks * 512, ch = P->doc == 1 ? 190 : 186;
+  int dg15Len = P->dg15_blocks * hblock(P->dg_hash), ch = P->doc == 1 ? 190 : 186;
   size_t dg1 = b + 3, dg15 = dg1 + 1024, sk = dg15 + dg15Len, p = sk + 1;
   if (P->aa && aa_is_ec(P->aa)) {
     int F = aa_field(P->aa), HS = aa_hsize(P->aa), XY = F - HS;
@@ -1769,14 +1791,21 @@ static void orc_init(void) {
   orc_init_done = 1;
 }
 
+/* The flow reads encapsulatedContentHash[i] for i < DG_HASH_TYPE (passportVerificationFlow.circom:36-40), so DG <= HT;
+ * RegisterIdentity's dg15 (DG15_SIZE x DG_HASH_BLOCK_SIZE) is assigned from an input of DG15_BLOCK_NUMBER x
+ * HASH_BLOCK_SIZE (registerIdentityBuilder.circom:151), so the block sizes agree or there is no dg15 */
 static int params_ok(const orc_params *P) {
-  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) && (P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160) && ((P->sig != 3 && P->sig != 4) || P->dg_hash == 160) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
+  const int HT = sig_hash(P->sig);
+  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) &&
+         (P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160 || P->dg_hash == 384) && P->dg_hash <= HT &&
+         (hblock(P->dg_hash) == hblock(HT) || P->dg15_blocks == 0) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
 
 size_t orc_register_n_inputs(const orc_params *P) {
   int K = sig_len(P->sig);
-  return 1 + (size_t)P->ec_blocks * 512 + 1024 + (size_t)P->dg15_blocks * 512 + 1024 + 2 * K + 80 + 1;
+  const int bs = hblock(sig_hash(P->sig));
+  return 1 + (size_t)P->ec_blocks * bs + 1024 + (size_t)P->dg15_blocks * bs + 1024 + 2 * K + 80 + 1;
 }
 size_t orc_register_witness_size(const orc_params *P) {
   if (!pos_loaded || !params_ok(P)) return 0;
@@ -1795,7 +1824,7 @@ int orc_register_witness(const orc_params *P, const uint8_t *inputs, uint8_t *wi
   memset(wit, 0, nW * 32);
   W(0) = ONE();
   memcpy(&W(5), inputs, nIn * 32);
-  int K = sig_len(P->sig), ecLen = P->ec_blocks * 512, dg15Len = P->dg15_blocks * 512;
+  int K = sig_len(P->sig), ecLen = P->ec_blocks * hblock(sig_hash(P->sig)), dg15Len = P->dg15_blocks * hblock(sig_hash(P->sig));
   size_t root = 5, ec = 6, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
          br = pk + K, sk = br + 80;
   size_t pvb = 5 + nIn, rid = pvb + sz_pvb(P);

@@ -142,27 +142,36 @@ def _pkcs1v15_sign(key: RsaKey, t: bytes) -> int:
     return key.sign_raw(int.from_bytes(em, "big"))
 
 
-def mgf1_sha256(seed: bytes, length: int) -> bytes:
-    out = b""
-    for c in range((length + 31) // 32):
-        out += hashlib.sha256(seed + c.to_bytes(4, "big")).digest()
+def mgf1(seed: bytes, length: int, hf=hashlib.sha256) -> bytes:
+    """MGF1 (RFC 8017 B.2.1) over hash hf."""
+    out, n = b"", hf().digest_size
+    for c in range((length + n - 1) // n):
+        out += hf(seed + c.to_bytes(4, "big")).digest()
     return out[:length]
 
 
+def mgf1_sha256(seed: bytes, length: int) -> bytes:
+    return mgf1(seed, length, hashlib.sha256)
+
+
 def pss_salt_len(sig):
-    """SALT_LEN of VerifyRsaPssSig for SIGNATURE_TYPE 10-12 (signatureVerification.circom:46-62)."""
-    return 64 if sig == 12 else 32
+    """SALT_LEN of VerifyRsaPssSig for SIGNATURE_TYPE 10-14 (signatureVerification.circom:46-75)."""
+    return 64 if sig == 12 else 48 if sig == 13 else 32
+
+
+def pss_sign(key: RsaKey, msg: bytes, salt: bytes, hf=hashlib.sha256) -> int:
+    """RSASSA-PSS (RFC 8017 9.1.1) with hash hf and MGF1 over hf, emBits = modBits - 1."""
+    h = hf(msg).digest()
+    em_len = key.bits // 8
+    hh = hf(b"\x00" * 8 + h + salt).digest()
+    db = b"\x00" * (em_len - len(salt) - len(h) - 2) + b"\x01" + salt
+    masked = bytes(a ^ b for a, b in zip(db, mgf1(hh, len(db), hf)))
+    masked = bytes([masked[0] & 0x7F]) + masked[1:]
+    return key.sign_raw(int.from_bytes(masked + hh + b"\xbc", "big"))
 
 
 def pss_sha256_sign(key: RsaKey, msg: bytes, salt: bytes) -> int:
-    """RSASSA-PSS (RFC 8017 9.1.1) with SHA-256 and MGF1-SHA-256, emBits = modBits - 1."""
-    h = hashlib.sha256(msg).digest()
-    em_len = key.bits // 8
-    hh = hashlib.sha256(b"\x00" * 8 + h + salt).digest()
-    db = b"\x00" * (em_len - len(salt) - 32 - 2) + b"\x01" + salt
-    masked = bytes(a ^ b for a, b in zip(db, mgf1_sha256(hh, len(db))))
-    masked = bytes([masked[0] & 0x7F]) + masked[1:]
-    return key.sign_raw(int.from_bytes(masked + hh + b"\xbc", "big"))
+    return pss_sign(key, msg, salt, hashlib.sha256)
 
 
 # -------------------------------------------------------------- ECDSA (synthetic)
@@ -255,6 +264,19 @@ def ecdsa_pk_hash(q):
     return poseidon([q[0] & m, q[1] & m])
 
 
+def sig_hash_type(sig):
+    """HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:16-59)."""
+    return 160 if sig in (3, 4) else 384 if sig == 13 else 256
+
+
+def hash_block(algo):
+    """Block size in bits of the hash algo (DG_HASH_BLOCK_SIZE / HASH_BLOCK_SIZE, registerIdentityBuilder.circom:95-102)."""
+    return 1024 if algo > 256 else 512
+
+
+HASHES = {160: hashlib.sha1, 224: hashlib.sha224, 256: hashlib.sha256, 384: hashlib.sha384, 512: hashlib.sha512}
+
+
 def sig_input_len(sig):
     """signature / pubkey input lengths (registerIdentityBuilder.circom:131-140)."""
     return 8 if sig >= 20 else 64 if sig == 2 else 48 if sig in (4, 14) else 32
@@ -273,7 +295,11 @@ CANONICAL = dict(sig=1, dg_hash=256, doc=3, ec_blocks=4, ec_shift=600, dg1_shift
 
 
 def instance_params(sig):
-    """The canonical instance with SIGNATURE_TYPE sig (SIG 3 hashes with SHA-1 and needs DG_HASH_TYPE 160)."""
+    """The canonical instance with SIGNATURE_TYPE sig (SIG 3 / 4 hash with SHA-1 and need DG_HASH_TYPE 160).
+    SIG 13 hashes with SHA-384 in 1024-bit blocks: DG_HASH_TYPE 384, and the block counts / EC_SHIFT the
+    synthetic messages fit (EC and the RSA-1024 DG15 pad to 2 blocks; the SA, one block, holds at most 111 bytes)."""
+    if sig == 13:
+        return dict(CANONICAL, sig=13, dg_hash=384, ec_blocks=2, dg15_blocks=2, ec_shift=336)
     return dict(CANONICAL, sig=sig, dg_hash=160 if sig in (3, 4) else 256)
 
 _MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789<"
@@ -342,7 +368,8 @@ class PassportGen:
     def n_inputs(self):
         pr = self.params
         K = sig_input_len(pr["sig"])
-        return 1 + pr["ec_blocks"] * 512 + 1024 + pr["dg15_blocks"] * 512 + 1024 + 2 * K + 80 + 1
+        bs = hash_block(sig_hash_type(pr["sig"]))
+        return 1 + pr["ec_blocks"] * bs + 1024 + pr["dg15_blocks"] * bs + 1024 + 2 * K + 80 + 1
 
     def passport_at(self, i, smt_depth=0):
         """Passport i from its own stream (independent of generation order)."""
@@ -373,29 +400,33 @@ class PassportGen:
         key = self.keys[i % len(self.keys)]
         dg1 = _mrz_dg1(rng)
         dg15 = _dg15_rsa1024(rng)
-        ec_len = 219 + rng.below(pr["ec_blocks"] * 64 - 9 - 219 + 1)
+        # DG hashes: DG_HASH_TYPE; EC / SA hashes: HASH_TYPE (SHA-1 for SIG 3 / 4, SHA-384 for SIG 13,
+        # passportVerificationBuilder.circom:16-59), whose block size sets the EC length (it pads to ec_blocks blocks)
+        ht = sig_hash_type(pr["sig"])
+        bs = hash_block(ht) // 8
+        ec_len = 219 + rng.below(pr["ec_blocks"] * bs - (bs // 8 + 1) - 219 + 1)
         ec = bytearray(rng.bytes(ec_len))
-        # DG hashes: DG_HASH_TYPE; EC / SA hashes: SHA-1 for SIGNATURE_TYPE 3 (passportVerificationBuilder.circom:19-50)
-        dgh = {160: hashlib.sha1, 224: hashlib.sha224}.get(pr["dg_hash"], hashlib.sha256)
-        sah = hashlib.sha1 if pr["sig"] in (3, 4) else hashlib.sha256
+        dgh, sah = HASHES[pr["dg_hash"]], HASHES[ht]
         h1, h15 = dgh(dg1).digest(), dgh(dg15).digest()
         d1 = pr["dg1_shift"] // 8
-        ec[d1 - 7:d1] = bytes.fromhex("30250201010420")
+        ec[d1 - 7:d1] = bytes.fromhex("302502010104") + bytes([max(32, len(h1))])
         ec[d1:d1 + len(h1)] = h1
         d15 = pr["dg15_shift"] // 8
-        ec[d15 - 7:d15] = bytes.fromhex("302502010f0420")
+        ec[d15 - 7:d15] = bytes.fromhex("302502010f04") + bytes([max(32, len(h15))])
         ec[d15:d15 + len(h15)] = h15
         ec = bytes(ec)
         sa_shift = pr["ec_shift"] // 8
-        sa_len = sa_shift + 32 + rng.below(119 - (sa_shift + 32) + 1)
+        hl = max(32, sah().digest_size)
+        sa_max = 119 if bs == 64 else 111  # two 512-bit blocks, or one 1024-bit block (SHA-384)
+        sa_len = sa_shift + hl + rng.below(sa_max - (sa_shift + hl) + 1)
         sa = bytearray(rng.bytes(sa_len))
-        sa[sa_shift - 2:sa_shift] = b"\x04\x20"
-        sa[sa_shift:sa_shift + 32] = (sah(ec).digest() + bytes(32))[:32]
+        sa[sa_shift - 2:sa_shift] = bytes([0x04, hl])
+        sa[sa_shift:sa_shift + hl] = (sah(ec).digest() + bytes(32))[:hl]
         sa = bytes(sa)
         if isinstance(key, EcKey):
             sig = key.sign(sa, rng)
-        elif 10 <= pr["sig"] <= 12 or pr["sig"] == 14:
-            sig = pss_sha256_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])))
+        elif 10 <= pr["sig"] <= 14:
+            sig = pss_sign(key, sa, rng.bytes(pss_salt_len(pr["sig"])), sah)
         elif pr["sig"] in (3, 4):
             sig = pkcs1v15_sha1_sign(key, sa)
         else:
@@ -420,17 +451,18 @@ class PassportGen:
 def passport_json(pp, params=CANONICAL):
     """The reference's input JSON (writeToJson, process_passport.js:659-672)."""
     sg = params["sig"]
+    hb, db = hash_block(sig_hash_type(sg)), hash_block(params["dg_hash"])
 
-    def bits(b, nbits):
-        arr = padded_bits(b, 512)
+    def bits(b, nbits, block):
+        arr = padded_bits(b, block)
         assert len(arr) == nbits, (len(arr), nbits)
         return [str(int(x)) for x in arr]
 
     return {
-        "dg1": bits(pp["dg1"], 1024),
-        "dg15": bits(pp["dg15"], params["dg15_blocks"] * 512),
-        "signedAttributes": bits(pp["sa"], 1024),
-        "encapsulatedContent": bits(pp["ec"], params["ec_blocks"] * 512),
+        "dg1": bits(pp["dg1"], 1024, db),
+        "dg15": bits(pp["dg15"], params["dg15_blocks"] * hb, db) if params["dg15_blocks"] else [],
+        "signedAttributes": bits(pp["sa"], 1024, hb),
+        "encapsulatedContent": bits(pp["ec"], params["ec_blocks"] * hb, hb),
         "pubkey": [str(x) for x in sig_limbs(pp["n"], sg)],
         "signature": [str(x) for x in sig_limbs(pp["sig"], sg)],
         "skIdentity": "0x%062x" % pp["sk"],  # getFakeIdenData's 62 hex digits, leading zeros kept
@@ -444,7 +476,8 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
     signedAttributes, signature, pubkey, slaveMerkleInclusionBranches, skIdentity
     (registerIdentityBuilder.circom:143-152, public input first). -> (nIn, 32) uint8."""
     K = sig_input_len(params["sig"])
-    ecL, d15L = params["ec_blocks"] * 512, params["dg15_blocks"] * 512
+    hb, db = hash_block(sig_hash_type(params["sig"])), hash_block(params["dg_hash"])
+    ecL, d15L = params["ec_blocks"] * hb, params["dg15_blocks"] * hb
     n_in = 1 + ecL + 1024 + d15L + 1024 + 2 * K + 80 + 1
     buf = out if out is not None else np.zeros((n_in, 32), dtype=np.uint8)
     buf[:] = 0
@@ -455,9 +488,11 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
         buf[o] = np.frombuffer(int(v % P).to_bytes(32, "little"), dtype=np.uint8)
         o += 1
 
-    def put_bits(b, nbits):
+    def put_bits(b, nbits, block):
         nonlocal o
-        arr = padded_bits(b, 512)
+        if nbits == 0:
+            return
+        arr = padded_bits(b, block)
         if len(arr) != nbits:
             raise ValueError("padded length %d != %d bits" % (len(arr), nbits))
         buf[o:o + nbits, 0] = arr
@@ -470,10 +505,10 @@ def pack_register_inputs(pp, params=CANONICAL, out=None):
             o += 1
 
     put_int(pp["root"] or 0)
-    put_bits(pp["ec"], ecL)
-    put_bits(pp["dg1"], 1024)
-    put_bits(pp["dg15"], d15L)
-    put_bits(pp["sa"], 1024)
+    put_bits(pp["ec"], ecL, hb)  # the message each field's hasher reads, padded for that hash
+    put_bits(pp["dg1"], 1024, db)
+    put_bits(pp["dg15"], d15L, db)
+    put_bits(pp["sa"], 1024, hb)
     put_u64s(sig_limbs(pp["sig"], params["sig"]))
     put_u64s(sig_limbs(pp["n"], params["sig"]))
     for s in pp["siblings"]:

@@ -221,6 +221,43 @@ def test_pss_oracle_rejects_bad_signatures(oracle, pss_gens):
     assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 18  # rsaPss.circom:182
 
 
+def test_pss384_oracle_sig13(oracle):
+    """SIGNATURE_TYPE 13: VerifyRsaPssSig(64, 32, 48, 65537, 384) (rsaPss.circom:18-254) with Mgf1Sha384
+    (mgf1.circom:5-68, 5 SHA-384 blocks) and a one-block SHA-384 M' hasher; the EC / SA hashers and
+    DG_HASH_TYPE 384 run ShaHashChunks(B, 384) over 1024-bit blocks. Pinned by an independent RFC 8017
+    RSASSA-PSS-SHA384 signer: a valid signature passes every check (the M' digest equals the EM hash
+    only if every SHA-384 / MGF1 intermediate is right), the public outputs match independent math, and a
+    signature + 1 / a valid signature of another message fail at rsaPss.circom:73 / :225."""
+    from refmath import aa_rsa_hash, dg1_commitment
+    params = I.instance_params(13)
+    prm = oracle.register_params(**params)
+    g = I.PassportGen(seed=13, n_keys=1, params=params, workers=1)
+    for i in range(2):
+        pp = g.passport_at(i)
+        rows = I.pack_register_inputs(pp, params)
+        assert rows.shape[0] == oracle.register_sizes(prm)[0]
+        rc, w = oracle.register_witness(prm, rows)
+        assert rc == 0
+        v = [oracle.from_elem(w[k]) for k in range(6)]
+        assert v[1] == aa_rsa_hash(pp["dg15"], 256)
+        sah = hashlib.sha384(pp["sa"]).digest()
+        hb = [(sah[k // 8] >> (7 - k % 8)) & 1 for k in range(384)]
+        assert v[2] == field.poseidon([sum(hb[k] << k for k in range(252))])
+        assert v[3] == dg1_commitment(pp["dg1"], pp["sk"])
+        assert v[5] == pp["root"] == field.poseidon([pp["pk_hash"]] * 2 + [1])
+    pp = dict(g.passport_at(1))
+    pp["sig"] += 1
+    assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 17
+    pp = dict(g.passport_at(1))
+    pp["sig"] = I.pss_sign(g.keys[0], pp["sa"] + b"x", bytes(48), hashlib.sha384)
+    assert oracle.register_witness(prm, I.pack_register_inputs(pp, params))[0] == 18
+    # the combinations the reference cannot compile are rejected: DG hash wider than the EC hash, and a
+    # dg15 whose block size differs between the builder and RegisterIdentity
+    assert oracle.register_sizes(oracle.register_params(**dict(I.CANONICAL, dg_hash=384)))[1] == 0
+    assert oracle.register_sizes(oracle.register_params(**dict(params, dg_hash=256)))[1] == 0
+    assert oracle.register_sizes(oracle.register_params(**dict(params, dg_hash=256, aa=0, dg15_blocks=0)))[1] > 0
+
+
 # ---------------------------------------------------------------- active-authentication key variants
 def _dg15_bits(pp, params):
     from pzkwit.inputs import bits_msb_first, sha_pad

@@ -64,7 +64,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
 WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
-SIG_SEED = {1: 3, 2: 4, 3: 11, 10: 6, 11: 7, 12: 8, 14: 10, 20: 5, 21: 9}
+SIG_SEED = {1: 3, 2: 4, 3: 11, 4: 12, 10: 6, 11: 7, 12: 8, 13: 13, 14: 10, 20: 5, 21: 9}
 CPU_SHARE = 16  # host CPUs a one-GPU job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
 
 
@@ -342,8 +342,10 @@ def report(args, r, world):
             workload = "RegisterIdentityBuilder(11,256,3,4,600,248,1,1496,3,256) synthetic RSA-2048 PSS passports"
         elif sig != 1:
             metric = "registerIdentityBuilder witnesses/sec, batch=4096 (SIGNATURE_TYPE %d)" % sig
-            workload = "RegisterIdentityBuilder(%d,%d,3,4,600,248,1,1496,3,256) synthetic passports" % (
-                sig, I.instance_params(sig)["dg_hash"])
+            q = I.instance_params(sig)
+            workload = "RegisterIdentityBuilder(%d,%d,%d,%d,%d,%d,%d,%d,%d,%d) synthetic passports" % tuple(
+                q[k] for k in ("sig", "dg_hash", "doc", "ec_blocks", "ec_shift", "dg1_shift", "aa", "dg15_shift",
+                               "dg15_blocks", "aa_shift"))
     else:
         metric = "Sha256HashChunks(6) witnesses/sec, batch=1024 (config 2)"
         workload = "Sha256HashChunks(6) synthetic 312-375 B messages (config 2)"

@@ -75,26 +75,37 @@ struct Builder {
   }
   // Sha384HashChunks / Sha512HashChunks(B) (hasher/sha2/sha384/sha384HashChunks.circom:8-48): own signals as
   // one RK_SHA5_OWN region, then one RK_SHA5_BLOCK (schedule + rounds) per 1024-bit block
-  int sha512(int in_off, int blocks, int O, int src = 0) {
+  int sha512(int in_off, int blocks, int O, int src = 0, bool wrapper = false) {
+    const int job = sha512_job(in_off, blocks, O, src);
+    sha512_regions(job, in_off, blocks, wrapper);
+    return job;
+  }
+  // the job alone: core = per block Hin, W, A, E (SHA5_BLOCK_CORE u32), then Hout as 8 u64 and as 16 big-endian
+  // u32 words (hout: the form every digest consumer reads, bit i = word i / 32, bit 31 - i % 32)
+  int sha512_job(int in_off, int blocks, int O, int src = 0) {
     ShaJob j{};
     j.in_off = in_off;
     j.blocks = blocks;
-    j.core_off = (int)L.sha_core_words;
     j.digest_slot = -1;
     j.src = src;
     j.algo = O == 384 ? 3 : 4;
     L.sha_core_words += L.sha_core_words & 1;  // 64-bit words: 8-byte aligned within the row
     j.core_off = (int)L.sha_core_words;
-    j.hout = j.core_off + blocks * SHA5_BLOCK_CORE;
-    L.sha_core_words += blocks * SHA5_BLOCK_CORE + 16;
+    j.hout = j.core_off + blocks * SHA5_BLOCK_CORE + 16;
+    L.sha_core_words += blocks * SHA5_BLOCK_CORE + 32;
     L.sha.push_back(j);
-    const int job = (int)L.sha.size() - 1;
-    region(RK_SHA5_OWN, (uint64_t)O + 1024ull * blocks + 512ull * (blocks + 1) + 512, {job, blocks, in_off, O});
+    return (int)L.sha.size() - 1;
+  }
+  // regions of a SHA-384/512 job, optionally inside ShaHashChunks(B, O) (hash.circom:32-68: out[O] | in[1024B] first)
+  void sha512_regions(int job, int in_off, int blocks, bool wrapper) {
+    const uint64_t O = L.sha[job].algo == 3 ? 384 : 512;
+    region(RK_SHA5_OWN, (wrapper ? O + 1024ull * blocks : 0) + O + 1024ull * blocks + 512ull * (blocks + 1) + 512,
+           {job, blocks, in_off, (int32_t)O, wrapper ? 1 : 0});
     for (int m = 0; m < blocks; m++) region(RK_SHA5_BLOCK, SHA5_BLOCK_SIGS, {job, m});
-    return job;
   }
   // a SHA job of either algorithm whose regions are placed later (sha_regions)
   int hash_job(int algo, int in_off, int blocks) {
+    if (algo > 256) return sha512_job(in_off, blocks, algo);
     if (algo == 224) { const int j = sha_job(in_off, blocks); L.sha[j].algo = 2; return j; }
     if (algo != 160) return sha_job(in_off, blocks);
     ShaJob j{};
@@ -165,11 +176,11 @@ struct Builder {
       for (uint32_t s = 0; s < r.len; s += chunk) wl->push_back(Work{ri, s, std::min(chunk, r.len - s), 0});
     }
     // SHA regions of hashers fed by derived messages are emitted after the chain that builds them
-    {
+    for (auto [e, ed] : {std::pair<int, int>{E_SHA, E_SHAD}, std::pair<int, int>{E_SHA5, E_SHA5D}}) {
       std::vector<Work> keep, later;
-      for (const Work& w : L.work[E_SHA]) (L.sha[L.regions[w.region].a[0]].src ? later : keep).push_back(w);
-      L.work[E_SHA].swap(keep);
-      L.work[E_SHAD].swap(later);
+      for (const Work& w : L.work[e]) (L.sha[L.regions[w.region].a[0]].src ? later : keep).push_back(w);
+      L.work[e].swap(keep);
+      L.work[ed].swap(later);
     }
     // Poseidon emission: one launch per width t, each with the LDS its image needs
     {

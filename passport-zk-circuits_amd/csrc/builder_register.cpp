@@ -38,25 +38,33 @@ uint32_t modmul_size(int K) {
 }
 
 bool build_register(const pzk_params& p, Layout& L, std::string& why) {
-  // RSA-PSS with SHA-256: 10-12 RSA-2048 (e = 3 for 10, salt 64 for 12), 14 RSA-3072 (signatureVerification.circom:46-75)
-  const bool pss = (p.signature_type >= 10 && p.signature_type <= 12) || p.signature_type == 14;
+  // RSA-PSS: 10-12 RSA-2048 SHA-256 (e = 3 for 10, salt 64 for 12), 13 RSA-2048 SHA-384 salt 48, 14 RSA-3072 SHA-256
+  // (signatureVerification.circom:46-75)
+  const bool pss = p.signature_type >= 10 && p.signature_type <= 14;
   // RSA exponent (signatureVerification.circom:14-75): 3 for SIG 10, 37187 for SIG 4, else 65537
   const long EXP = p.signature_type == 10 ? 3 : p.signature_type == 4 ? 37187 : 65537;
   if ((p.signature_type < 1 || p.signature_type > 4) && !pss && p.signature_type != 20 && p.signature_type != 21) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1-4, RSA-PSS types 10-12 and 14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
+          " not built yet (RSA PKCS#1 v1.5 types 1-4, RSA-PSS types 10-14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
     return false;
   }
   const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
-  // DG_HASH_TYPE 256 or 160; SIGNATURE_TYPE 3 hashes the EC / SA with SHA-1 (HASH_TYPE 160), which the flow's
-  // `encapsulatedContentHash[i], i < HASH_SIZE` loop (passportVerificationFlow.circom:36-40) allows only with DG 160
-  if (p.dg_hash_type != 256 && p.dg_hash_type != 224 && p.dg_hash_type != 160) {
-    why = "DG_HASH_TYPE must be 256, 224 or 160";
+  // DG_HASH_TYPE 160, 224, 256 or 384. HASH_TYPE (EC / SA hashers, passportVerificationBuilder.circom:16-59): 160 for
+  // SIG 3 / 4, 384 for SIG 13, else 256. The flow's `encapsulatedContentHash[i], i < HASH_SIZE` loop
+  // (passportVerificationFlow.circom:36-40) runs over the DG hash bits, so DG <= HASH_TYPE or the reference cannot compile.
+  if (p.dg_hash_type != 256 && p.dg_hash_type != 224 && p.dg_hash_type != 160 && p.dg_hash_type != 384) {
+    why = "DG_HASH_TYPE must be 160, 224, 256 or 384";
     return false;
   }
   const bool sha1_sig = p.signature_type == 3 || p.signature_type == 4;
-  if (sha1_sig && p.dg_hash_type != 160) { why = "SIGNATURE_TYPE 3 / 4 need DG_HASH_TYPE 160"; return false; }
-  const int DG = p.dg_hash_type, HT = sha1_sig ? 160 : 256;
+  const int DG = p.dg_hash_type, HT = sha1_sig ? 160 : p.signature_type == 13 ? 384 : 256;
+  if (DG > HT) {
+    why = "DG_HASH_TYPE " + std::to_string(DG) + " is wider than this SIGNATURE_TYPE's hash (" + std::to_string(HT) +
+          "): passportVerificationFlow.circom:36-40 would read encapsulatedContentHash past its end";
+    return false;
+  }
+  // HASH_BLOCK_SIZE / DG_HASH_BLOCK_SIZE (registerIdentityBuilder.circom:95-102): 1024-bit blocks above 256-bit hashes
+  const int HBS = HT > 256 ? 1024 : 512, DBS = DG > 256 ? 1024 : 512;
   if (p.document_type != 1 && p.document_type != 3) { why = "DOCUMENT_TYPE must be 1 or 3"; return false; }
   // AA_SIGNATURE_ALGO: 0 none, 1..19 RSA-1024 key (identity.circom:25-49), >= 20 EC key (:51-84); the raw value
   // also scales the DG15 IsEqual inputs of the flow (passportVerificationFlow.circom:45-46,73-74)
@@ -65,12 +73,17 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const int aa_f = p.aa_signature_algo == 22 ? 320 : p.aa_signature_algo == 23 ? 192 : 256;
   const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
   const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : (p.signature_type == 14 || p.signature_type == 4) ? 48 : 32;  // signature / pubkey input length
-  const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = 512 * ecB, d15Len = 512 * d15B;
+  const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = HBS * ecB, d15Len = HBS * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
+  if (HBS != DBS && d15B) {
+    why = "dg15 block sizes differ: registerIdentityBuilder.circom:151 assigns dg15[DG15_BLOCK_NUMBER * HASH_BLOCK_SIZE] to "
+          "RegisterIdentity's dg15[DG15_SIZE * DG_HASH_BLOCK_SIZE] (identity.circom:22)";
+    return false;
+  }
   const int dg15shift = aa ? p.dg15_shift : DG;
-  if (p.dg1_shift < 0 || p.dg1_shift + 256 > ecLen || dg15shift < 24 || dg15shift + 256 > ecLen ||
-      p.ec_shift < 0 || p.ec_shift + 256 > 1024 || (aa && p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len)) {
+  if (p.dg1_shift < 0 || p.dg1_shift + DG > ecLen || dg15shift < 24 || dg15shift + DG > ecLen ||
+      p.ec_shift < 0 || p.ec_shift + HT > 1024 || (aa && p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len)) {
     why = "shift parameters address bits outside the inputs";
     return false;
   }
@@ -144,10 +157,10 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   b.region(RK_INCOPY, 1, {IN_ROOT});
   // SHA jobs are created when the hashers are created; their digests are referenced earlier,
   // so reserve the job ids first (creation order dg1, dg15, ec, sa).
-  const int J_DG1 = b.hash_job(DG, IN_DG1, 2);
-  const int J_DG15 = aa ? b.hash_job(DG, IN_DG15, d15B) : -1;
+  const int J_DG1 = b.hash_job(DG, IN_DG1, 1024 / DBS);
+  const int J_DG15 = aa ? b.hash_job(DG, IN_DG15, d15B) : -1;  // the first d15B x DG_HASH_BLOCK_SIZE bits (:117-120)
   const int J_EC = b.hash_job(HT, IN_EC, ecB);
-  const int J_SA = b.hash_job(HT, IN_SA, 2);
+  const int J_SA = b.hash_job(HT, IN_SA, 1024 / HBS);
   L.reg.j_dg1 = J_DG1; L.reg.j_dg15 = J_DG15; L.reg.j_ec = J_EC; L.reg.j_sa = J_SA;
   b.region(RK_DIGEST, DG, {J_DG1});
   if (aa) b.region(RK_DIGEST, DG, {J_DG15});
@@ -159,15 +172,16 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   else b.region(RK_TEMPMOD, 5, {IN_PK});
   auto sha_blocks = [&](int job, int in_off, int blocks) {
     if (L.sha[job].algo == 1) { b.sha1_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 160)
+    if (L.sha[job].algo >= 3) { b.sha512_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 384 | 512)
     const int O = L.sha[job].algo == 2 ? 224 : 256;  // ShaHashChunks(B, 224 | 256)
     uint64_t own = O + 512ull * blocks + O + 512ull * blocks + 256ull * (blocks + 1) + 256;
     b.region(RK_SHA_OWN, own, {job, blocks, in_off, 1, O});
     for (int m = 0; m < blocks; m++) b.region(RK_SHA_BLOCK, 150762, {job, m});
   };
-  sha_blocks(J_DG1, IN_DG1, 2);
+  sha_blocks(J_DG1, IN_DG1, 1024 / DBS);
   if (aa) sha_blocks(J_DG15, IN_DG15, d15B);
   sha_blocks(J_EC, IN_EC, ecB);
-  sha_blocks(J_SA, IN_SA, 2);
+  sha_blocks(J_SA, IN_SA, 1024 / HBS);
   // PassportVerificationFlow(ecLen, DG, HT, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA): 3 DG + 8 IsEqual
   b.region(RK_FLOW, 1 + 2 * DG + ecLen + HT + 1024 + (3 * DG + 8) * (1 + SZ_ISEQUAL),
            {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, p.aa_signature_algo});
@@ -230,29 +244,33 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
       for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
       b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
     } else {
-      //   VerifyRsaPssSig(64,K,SALT,EXP,256) (rsaPss.circom:18-204): pubkey, signature, hashed | eM .. mDash
-      //   | powerMod, num2Bits[K], bits2Num[8K], MGF1_256, xor, hDash256 (pss.hpp)
-      const int S8 = p.signature_type == 12 ? 512 : 256, EML = 8 * K, DB8 = 8 * (EML - 33), IT = (EML - 33) / 32 + 1;
+      //   VerifyRsaPssSig(64,K,SALT,EXP,H) (rsaPss.circom:18-254): pubkey, signature, hashed | eM .. mDash
+      //   | powerMod, num2Bits[K], bits2Num[8K], MGF1_H, xor, hDash (pss.hpp); H = 384, salt 48 for SIG 13
+      const int H = HT, S8 = p.signature_type == 12 ? 512 : p.signature_type == 13 ? 384 : 256, EML = 8 * K,
+                DBL = EML - H / 8 - 1, DB8 = 8 * DBL, IT = DBL / (H / 8) + 1, BS = H > 256 ? 1024 : 512;
       b.region(RK_INCOPY, K, {IN_PK});
       b.region(RK_INCOPY, K, {IN_SIG});
-      b.region(RK_DIGEST, 256, {J_SA});
-      b.region(RK_PSS_OWN, EML + 64 * K + K + 3 * DB8 + S8 + 256 + 1024, {S8});
+      b.region(RK_DIGEST, H, {J_SA});
+      b.region(RK_PSS_OWN, EML + 64 * K + K + 3 * DB8 + S8 + H + 1024, {S8});
       if (!power_mod()) return false;
       for (int i = 0; i < K; i++) b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, K - 1 - i});  // EM limb K-1-i
       b.region(RK_PSS_B2N8, 17 * EML);
-      //   Mgf1Sha256(32, DB) (mgf1.circom:69-127): out | seed | hashed, then (ShaHashChunks(1,256), Num2Bits(32))
+      //   Mgf1ShaH(H/8, DB) (mgf1.circom:5-133): out | seed | hashed, then (ShaHashChunks(1,H), Num2Bits(32))
       //   per block; the hashers read derived messages (ShaJob.src = 1)
-      b.region(RK_PSS_MGF, DB8 + 256 + 256 * IT);
+      b.region(RK_PSS_MGF, DB8 + H + H * IT);
       L.reg.j_mgf = (int)L.sha.size();
       L.reg.n_mgf = IT;
       for (int c = 0; c < IT; c++) {
-        b.sha256(512 * c, 1, true, 1);
+        if (H > 256) b.sha512(BS * c, 1, H, 1, true);
+        else b.sha256(BS * c, 1, true, 1);
         b.region(RK_PSS_CTR, sz_num2bits(32), {c});
       }
       b.region(RK_PSS_XOR, 3 * DB8);
-      L.reg.j_hd = b.sha256(512 * IT, 2, true, 1);
+      // hDash: ShaHashChunks(2, 256) or ShaHashChunks(1, 384) over the 1024-bit M'
+      L.reg.j_hd = H > 256 ? b.sha512(BS * IT, 1, H, 1, true) : b.sha256(BS * IT, 2, true, 1);
       L.reg.pss_s8 = S8;
-      L.n_derived = 512ull * IT + 1024;
+      L.reg.pss_h = H;
+      L.n_derived = (uint64_t)BS * IT + 1024;
     }
   }
   // signedAttributesNum = Bits2Num(252)(saHash[0..251]), or of 92 zeros | saHash[0..159] for SHA-1

@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha512(DevLayout L, const
     auto hin = [&](int m, uint32_t j) -> uint64_t { return m < Bn ? wc[(size_t)m * (SHA5_BLOCK_CORE / 2) + j] : wc[(size_t)Bn * (SHA5_BLOCK_CORE / 2) + j]; };
     emit_run(out, wk.count, stage, [&](uint32_t q) {
       bool cp;
-      const uint64_t v = sha5_own_sig(hin, Bn, O, iv, wk.start + q, cp);
+      const uint64_t v = sha5_own_sig(hin, Bn, O, iv, wk.start + q, cp, R.a[4] != 0);
       return cp ? el_load(in_row + 32ull * (R.a[2] + v)) : el_u64(v);
     });
   }
@@ -373,7 +373,8 @@ hipError_t launch_sha_core(const DevLayout& L, const uint8_t* inputs, const uint
 hipError_t launch_pss(const DevLayout& L, int stage, const uint64_t* rsa_core, const uint32_t* sha_core,
                       uint8_t* derived, uint32_t batch, hipStream_t st) {
   if (stage == 0)
-    hipLaunchKernelGGL(k_pss_mgf, dim3((512 * L.reg.n_mgf + 255) / 256, batch), dim3(256), 0, st, L, rsa_core,
+    hipLaunchKernelGGL(k_pss_mgf, dim3(((L.reg.pss_h > 256 ? 1024 : 512) * L.reg.n_mgf + 255) / 256, batch), dim3(256), 0, st,
+                       L, rsa_core,
                        sha_core, derived);
   else
     hipLaunchKernelGGL(k_pss_mdash, dim3(4, batch), dim3(256), 0, st, L, rsa_core, sha_core, derived);
@@ -551,6 +552,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
       break;
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
     case E_SHA5:
+    case E_SHA5D:
       hipLaunchKernelGGL(k_emit_sha512, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
                          B.stride);
       break;

@@ -72,7 +72,8 @@ enum RegionKind : uint32_t {
   RK_SHA1_OWN = 45,   // Sha1HashChunks out[160] | in[512B] | H(0..4); a0 = sha slot, a1 = blocks, a2 = input offset
   RK_SHA1_BLOCK = 46, // Sha1compression of one block; a0 = sha slot, a1 = block
   // ---- SHA-384 / SHA-512 (hasher/sha2/sha384, sha512; sha512.hpp)
-  RK_SHA5_OWN = 47,   // Sha384/512HashChunks out[O] | in[1024B] | states | iv; a0 = sha slot, a1 = blocks, a2 = input offset
+  RK_SHA5_OWN = 47,   // [ShaHashChunks out[O] | in[1024B] (a4 = 1)] Sha384/512HashChunks out[O] | in[1024B] | states | iv;
+                      // a0 = sha slot, a1 = blocks, a2 = input offset, a3 = O
   RK_SHA5_BLOCK = 48, // Sha2_384_512Schedule + Sha2_384_512Rounds(80) of one block; a0 = sha slot, a1 = block
   RK_COUNT
 };
@@ -81,8 +82,9 @@ enum RegionKind : uint32_t {
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
 // E_ECT = ECDSA table blocks (k_emit_ect)
 // E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
-// E_SHA1 = SHA-1 hasher regions (k_emit_sha1); E_SHA5 = SHA-384/512 hasher regions (k_emit_sha512)
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_COUNT };
+// E_SHA1 = SHA-1 hasher regions (k_emit_sha1); E_SHA5 = SHA-384/512 hasher regions (k_emit_sha512); E_SHA5D = the
+// SHA-384 hashers of derived messages (RSA-PSS SHA-384 MGF1 / M'), emitted after the PSS chain like E_SHAD
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_SHA5D, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -178,6 +180,7 @@ struct RegInfo {
   int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
   int32_t aa_ec, aa_f, aa_hs;      // EC active-authentication key: field bits, hashed bits (identity.circom:51-84)
   int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)
+  int32_t pss_h;                   // RSA-PSS hash bits (256 or 384)
   int32_t j_mgf, n_mgf, j_hd;      // RSA-PSS SHA jobs: MGF1 blocks [j_mgf, j_mgf + n_mgf), M' hasher
 };
 

@@ -302,15 +302,18 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
 
 // ------------------------------------------------------------------ PassportVerificationFlow
 __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work, Bufs B) {
-  __shared__ uint8_t eq[776], chain[776];
+  __shared__ uint8_t eq[3 * 512 + 8], chain[3 * 512 + 8];  // 3 DG + 8 IsEqual, DG <= 512
   __shared__ fr invV;  // 1 / DG15_VERIFICATION (normal form): IsZero inverses of the scaled DG15 checks
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
   const int jd1 = R.a[0], jd15 = R.a[1], jec = R.a[2], jsa = R.a[3], in_ec = R.a[4], in_sa = R.a[5];
   const int d1s = R.a[6], d15s = R.a[7], ecs = R.a[8], V = R.a[9];
-  const int ecLen = 512 * L.sha[jec].blocks;
-  auto hbits = [&](int j) { return L.sha[j].algo == 1 ? 160 : L.sha[j].algo == 2 ? 224 : 256; };
+  const int ecLen = (L.sha[jec].algo >= 3 ? 1024 : 512) * L.sha[jec].blocks;
+  auto hbits = [&](int j) {
+    const int a = L.sha[j].algo;
+    return a == 1 ? 160 : a == 2 ? 224 : a == 3 ? 384 : a == 4 ? 512 : 256;
+  };
   const int H = hbits(jd1), EH = hbits(jec), NC = 3 * H + 8;
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
   const uint32_t* H1 = sha_hout(L, B, w, jd1);

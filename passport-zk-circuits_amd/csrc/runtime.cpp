@@ -44,7 +44,7 @@ static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k
                                               "k_pss_mgf+k_sha_core+k_pss_mdash"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
                                         PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
-                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA};
+                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -696,6 +696,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     HIPCHK(hipStreamWaitEvent(s_emit, I->ev_rsa, 0));
     if ((rc = emit(E_MM, s_emit))) return rc;
     if ((rc = emit(E_SHAD, s_emit))) return rc;
+    if ((rc = emit(E_SHA5D, s_emit))) return rc;  // SHA-384 PSS hashers (SIGNATURE_TYPE 13)
     if (lay.is_ecdsa) {
       HIPCHK(hipStreamWaitEvent(s_emit, I->ev_tab, 0));
       if ((rc = emit(E_ECT, s_emit))) return rc;
@@ -883,7 +884,9 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
     *kernel = PHASE_KERNELS[phase];
     if (phase == PH_EMIT_SHA) {  // the SHA-2 and SHA-1 emitters share the phase: name the ones this instance runs
       const bool s2 = !I->lay.work[E_SHA].empty() || !I->lay.work[E_SHAD].empty(), s1 = !I->lay.work[E_SHA1].empty();
-      *kernel = !I->lay.work[E_SHA5].empty() ? "k_emit_sha512" : s1 ? (s2 ? "k_emit_sha+k_emit_sha1" : "k_emit_sha1") : "k_emit_sha";
+      const bool s5 = !I->lay.work[E_SHA5].empty() || !I->lay.work[E_SHA5D].empty();
+      *kernel = s5 ? (s2 ? "k_emit_sha+k_emit_sha512" : "k_emit_sha512")
+                   : s1 ? (s2 ? "k_emit_sha+k_emit_sha1" : "k_emit_sha1") : "k_emit_sha";
     }
   }
   if (bytes_per_witness) {
@@ -898,7 +901,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       if (r.kind == RK_SHA_BLOCK) b += 4ull * SHA_BLOCK_CORE;
       if (r.kind == RK_SHA1_OWN) b += 32ull * 512 * r.a[1];  // message bits copied
       if (r.kind == RK_SHA1_BLOCK) b += 4ull * SHA1_BLOCK_CORE;
-      if (r.kind == RK_SHA5_OWN) b += 32ull * 1024 * r.a[1];  // message bits copied
+      if (r.kind == RK_SHA5_OWN) b += 32ull * 1024 * r.a[1] * (r.a[4] ? 2 : 1);  // message bits copied
       if (r.kind == RK_SHA5_BLOCK) b += 4ull * SHA5_BLOCK_CORE;
       if (r.kind == RK_INCOPY) b += 32ull * r.len;
       if (r.kind == RK_POSEIDON) b += 32ull * pos_core_len(r.a[1] + 1);
@@ -906,7 +909,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
     }
     if (phase == PH_SHA_CORE)
       for (const ShaJob& j : L.sha)
-        b += j.algo >= 3 ? 32ull * 1024 * j.blocks + 4ull * (j.blocks * SHA5_BLOCK_CORE + 16)
+        b += j.algo >= 3 ? 32ull * 1024 * j.blocks + 4ull * (j.blocks * SHA5_BLOCK_CORE + 32)
                          : 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo == 1 ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
     if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;

@@ -81,6 +81,9 @@ __device__ __forceinline__ void sha512_core_lane(const uint8_t* in_row, const Sh
   }
   uint64_t* hout = reinterpret_cast<uint64_t*>(core + job.core_off + job.blocks * SHA5_BLOCK_CORE);
   for (int j = 0; j < 8; j++) hout[j] = H[j];
+  // the digest again as big-endian 32-bit words (job.hout): the form the digest consumers read (regemit.hpp digest_bit)
+  uint32_t* hbe = core + job.hout;
+  for (int j = 0; j < 8; j++) { hbe[2 * j] = (uint32_t)(H[j] >> 32); hbe[2 * j + 1] = (uint32_t)H[j]; }
   if (bad) lane_status(status, ST_INPUT_RANGE);
 }
 
@@ -267,10 +270,18 @@ __device__ __forceinline__ U128 sha5_block_sig(const Sha5Blk& X, uint32_t s) {
 }
 
 // Sha384HashChunks / Sha512HashChunks(B) own signals: out[O] (MSB-first digest) | in[1024B] (copies) |
-// states[B+1][8][64] | iv.out[8][64]. hin(m, j) = H_m[j] (H_B = Hout).
+// states[B+1][8][64] | iv.out[8][64], after the ShaHashChunks(B, O) wrapper's out[O] | in[1024B] when wrap.
+// hin(m, j) = H_m[j] (H_B = Hout).
 template <typename HF>
-__device__ __forceinline__ uint64_t sha5_own_sig(HF hin, int B, int O, const uint64_t* iv, uint32_t s, bool& is_copy) {
+__device__ __forceinline__ uint64_t sha5_own_sig(HF hin, int B, int O, const uint64_t* iv, uint32_t s, bool& is_copy,
+                                                 bool wrap = false) {
   is_copy = false;
+  if (wrap) {
+    if (s < (uint32_t)O) return s5_bit(hin(B, s >> 6), 63 - (s & 63));
+    s -= O;
+    if (s < 1024u * B) { is_copy = true; return s; }
+    s -= 1024u * B;
+  }
   if (s < (uint32_t)O) return s5_bit(hin(B, s >> 6), 63 - (s & 63));
   s -= O;
   if (s < 1024u * B) { is_copy = true; return s; }

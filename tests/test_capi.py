@@ -76,6 +76,9 @@ PARAM_SETS = [
     dict(I.CANONICAL, aa=20),                      # EC AA key (256-bit field, 248 hashed bits)
     dict(I.CANONICAL, aa=22),                      # EC AA key, 320-bit field
     dict(I.CANONICAL, sig=20, aa=23),              # ECDSA signature, 192-bit EC AA key
+    I.instance_params(13),                         # RSA-PSS SHA-384, salt 48, DG hash 384, 1024-bit blocks
+    dict(I.instance_params(13), dg_hash=256, aa=0, dg15_blocks=0),  # SIG 13 with SHA-256 DG hashes, no DG15
+    dict(I.instance_params(13), aa=20),            # SIG 13 with an EC AA key
     dict(I.CANONICAL, sig=21),                     # ECDSA brainpoolP256r1
     dict(I.CANONICAL, sig=14),                     # RSA-3072 PSS (K = 48: schoolbook BigMultOverflow)
     dict(I.CANONICAL, sig=3, dg_hash=160),         # RSA-2048 PKCS#1 v1.5 SHA-1, SHA-1 DG hashes
@@ -123,6 +126,11 @@ def test_unsupported_params_rejected():
     rc, _, _ = layout_sizes(dict(I.CANONICAL, sig=22))  # brainpoolP320r1: not built yet
     assert rc == -2
     assert b"SIGNATURE_TYPE" in native.lib().pzk_last_error()
+    # combinations the reference cannot compile (oracle params_ok agrees: test_oracle.py::test_pss384_oracle_sig13)
+    assert layout_sizes(dict(I.CANONICAL, dg_hash=384))[0] == -2  # DG hash wider than the EC hash
+    assert b"wider" in native.lib().pzk_last_error()
+    assert layout_sizes(dict(I.instance_params(13), dg_hash=256))[0] == -2  # dg15 block sizes differ
+    assert b"dg15 block sizes" in native.lib().pzk_last_error()
     rc, _, _ = layout_sizes(dict(I.CANONICAL, dg1_shift=2000))
     assert rc == -2
 

@@ -13,7 +13,7 @@ from test_gpu_register import KIND_NAMES
 
 pytestmark = pytest.mark.gpu
 
-KIND_NAMES.update({40: "PSS_OWN", 41: "PSS_B2N8", 42: "PSS_MGF", 43: "PSS_CTR", 44: "PSS_XOR"})
+KIND_NAMES.update({40: "PSS_OWN", 41: "PSS_B2N8", 42: "PSS_MGF", 43: "PSS_CTR", 44: "PSS_XOR", 47: "SHA5_OWN", 48: "SHA5_BLOCK"})
 
 
 @pytest.fixture(scope="module")
@@ -28,6 +28,35 @@ def test_pss_matches_oracle(oracle, gens, sig):
     pps = [g.passport_at(0), g.passport_at(1), g.passport_at(2, smt_depth=5)]
     pps[2]["root"] = 12345
     _run(oracle, params, np.stack([I.pack_register_inputs(pp, params) for pp in pps]))
+
+
+@pytest.mark.parametrize("variant", ["dg384", "dg256-noaa", "ec-aa"])
+def test_pss384_sig13_matches_oracle(oracle, variant):
+    """SIGNATURE_TYPE 13: RSA-2048 PSS over SHA-384 (salt 48, Mgf1Sha384 with 5 SHA-384 blocks, one-block
+    SHA-384 M' hasher; rsaPss.circom:18-254, mgf1.circom:5-68) with SHA-384 EC / SA hashers in 1024-bit
+    blocks (k_sha_core algo 3, k_emit_sha512 with the ShaHashChunks wrapper; the derived-message hashers
+    through E_SHA5D). DG hash 384, or SHA-256 DG hashes without DG15; every element vs the oracle, plus a
+    failing lane per PSS check site."""
+    params = I.instance_params(13)
+    if variant == "dg256-noaa":
+        params = dict(params, dg_hash=256, aa=0, dg15_blocks=0)
+    elif variant == "ec-aa":
+        params = dict(params, aa=20)
+    g = I.PassportGen(seed=31, n_keys=2, params=params, workers=1)
+    pps = [g.passport_at(0), g.passport_at(1, smt_depth=4)]
+    pps[1]["root"] = 4242
+    if variant == "dg384":
+        bad = dict(g.passport_at(2))
+        bad["sig"] += 1
+        other = dict(g.passport_at(3))
+        import hashlib
+        other["sig"] = I.pss_sign(g.keys[1], other["sa"] + b"x", bytes(48), hashlib.sha384)
+        pps += [bad, other]
+        _, st, codes = _run(oracle, params, np.stack([I.pack_register_inputs(pp, params) for pp in pps]),
+                            expect_ok=False)
+        assert codes == [0, 0, 17, 18] and list(st) == codes  # rsaPss.circom:73, :225
+    else:
+        _run(oracle, params, np.stack([I.pack_register_inputs(pp, params) for pp in pps]))
 
 
 def test_pss_td1_no_aa_matches_oracle(oracle):

@@ -34,6 +34,7 @@ def lib():
         L = ctypes.CDLL(LIB)
         for fn in ("ck_sha256", "ck_sha1", "ck_poseidon_circuit"):
             getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
+        L.ck_sha512.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
         L.ck_load_poseidon.argtypes = [ctypes.c_char_p]
         L.ck_load_ec_table.argtypes = [ctypes.c_int, ctypes.c_char_p]
         L.ck_register.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
@@ -52,6 +53,15 @@ def _run(fn, arg, wit):
 def check_sha1(wit, blocks):
     """Sha1HashChunks(blocks) as main."""
     return _run("ck_sha1", blocks, wit)
+
+
+def check_sha512(wit, blocks, out_bits=512):
+    """Sha384HashChunks / Sha512HashChunks(blocks) as main."""
+    import numpy as np
+    w = np.ascontiguousarray(wit, dtype=np.uint8)
+    r = Report()
+    rc = lib().ck_sha512(blocks, out_bits, w.ctypes.data, w.shape[0], ctypes.byref(r))
+    return rc, r.as_dict()
 
 
 def check_sha256(wit, blocks):

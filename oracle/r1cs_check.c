@@ -429,6 +429,238 @@ static size_t ck_sha2chunks(ck_t *c, size_t b, int B, int O) {
   return o - b;
 }
 
+
+/* ============================================================ SHA-2 (384/512) */
+/* the (1 << i) * bit[i] inputs of a GetSumOfNElements(64) at g from 64 bits at `bits` */
+static void wire_sum64(ck_t *c, size_t b, size_t g, size_t bits, const char *T, int line) {
+  for (int i = 0; i < 64; i++) EQ(S(c, g + 1 + i), MUL(P2[i], S(c, bits + i)), T, line);
+}
+
+/* Sha2_384_512Schedule sha512/sha512Schedule.circom:11-74:
+ * outWords[80] | chunkBits[16][64] | outBits[80][64] | sumN[16], then per m: s0Sum, s1Sum, (s0Xor, s1Xor)[64], modulo, bits2Num */
+static size_t ck_schedule512(ck_t *c, size_t b) {
+  const char *T = "Sha2_384_512Schedule hasher/sha2/sha512/sha512Schedule.circom";
+  size_t ow = b, cb = b + 80, ob = cb + 1024, o = ob + 5120;
+  for (int k = 0; k < 16; k++) {
+    size_t g = o;
+    o += ck_getsum(c, g, 64);
+    wire_sum64(c, b, g, cb + 64 * (size_t)k, T, 25);
+    EQ(S(c, ow + k), S(c, g), T, 27);
+    for (int i = 0; i < 64; i++) EQ(S(c, ob + 64 * (size_t)k + i), S(c, cb + 64 * (size_t)k + i), T, 28);
+  }
+  for (int m = 16; m < 80; m++) {
+    size_t k = m - 15, l = m - 2;
+    size_t s0 = o, s1 = o + 128;
+    o += ck_getsum(c, s0, 64) + ck_getsum(c, s1, 64);
+    for (int i = 0; i < 64; i++) {
+      size_t x0 = o, x1 = o + 5;
+      o += ck_xor3(c, x0) + ck_xor3(c, x1);
+      EQ(S(c, x0 + 1), S(c, ob + 64 * k + (i + 1) % 64), T, 54);
+      EQ(S(c, x0 + 2), S(c, ob + 64 * k + (i + 8) % 64), T, 55);
+      EQ(S(c, x0 + 3), i < 57 ? S(c, ob + 64 * k + i + 7) : fr_zero(), T, 56);
+      EQ(S(c, s0 + 1 + i), MUL(P2[i], S(c, x0)), T, 57);
+      EQ(S(c, x1 + 1), S(c, ob + 64 * l + (i + 19) % 64), T, 60);
+      EQ(S(c, x1 + 2), S(c, ob + 64 * l + (i + 61) % 64), T, 61);
+      EQ(S(c, x1 + 3), i < 58 ? S(c, ob + 64 * l + i + 6) : fr_zero(), T, 62);
+      EQ(S(c, s1 + 1 + i), MUL(P2[i], S(c, x1)), T, 63);
+    }
+    size_t md = o;
+    o += ck_lastnbits(c, md, 64);
+    EQ(S(c, md + 65), ADD(ADD(ADD(S(c, s1), S(c, ow + m - 7)), S(c, s0)), S(c, ow + m - 16)), T, 68);
+    for (int i = 0; i < 64; i++) EQ(S(c, ob + 64 * (size_t)m + i), S(c, md + 1 + i), T, 69);
+    size_t bn = o;
+    o += ck_bits2num(c, bn, 64);
+    for (int i = 0; i < 64; i++) EQ(S(c, bn + 1 + i), S(c, ob + 64 * (size_t)m + i), T, 71);
+    EQ(S(c, ow + m), S(c, bn), T, 72);
+  }
+  return o - b;
+}
+
+static const uint64_t SHA512_K[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL, 0x3956c25bf348b538ULL,
+    0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL, 0xd807aa98a3030242ULL, 0x12835b0145706fbeULL,
+    0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL, 0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL,
+    0xc19bf174cf692694ULL, 0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL, 0x983e5152ee66dfabULL,
+    0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL, 0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL,
+    0x06ca6351e003826fULL, 0x142929670a0e6e70ULL, 0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL,
+    0x53380d139d95b3dfULL, 0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL, 0xd192e819d6ef5218ULL,
+    0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL, 0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL,
+    0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL, 0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL,
+    0x682e6ff3d6b2b8a3ULL, 0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL, 0xca273eceea26619cULL,
+    0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL, 0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL,
+    0x113f9804bef90daeULL, 0x1b710b35131c471bULL, 0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
+    0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+/* Sha2_384_512CompressInner sha512/sha512Compress.circom:11-96:
+ * outA[64] outB[64] outC[64] outDD outE[64] outF[64] outG[64] outHH | inp key a[64] b[64] c[64] dd e[64] f[64] g[64] hh |
+ * chb[64] overflowE overflowA | dSum hSum s0Sum s1Sum mjSum chSum (major, s0Xor, s1Xor)[64] decomposeE decomposeA */
+static size_t ck_compress512(ck_t *c, size_t b) {
+  const char *T = "Sha2_384_512CompressInner hasher/sha2/sha512/sha512Compress.circom";
+  size_t oA = b, oB = b + 64, oC = b + 128, oDD = b + 192, oE = b + 193, oF = b + 257, oG = b + 321, oHH = b + 385;
+  size_t inp = b + 386, key = b + 387, a = b + 388, bb = b + 452, cc = b + 516, dd = b + 580, e = b + 581,
+         f = b + 645, g = b + 709, hh = b + 773;
+  size_t chb = b + 774, ovE = b + 838, ovA = b + 839, o = b + 840;
+  size_t dS = o, hS = o + 128, s0S = o + 256, s1S = o + 384, mjS = o + 512, chS = o + 640;
+  for (int q = 0; q < 6; q++) o += ck_getsum(c, o, 64);
+  wire_sum64(c, b, dS, cc, T, 43);
+  wire_sum64(c, b, hS, g, T, 44);
+  for (int i = 0; i < 64; i++) {
+    EQ(S(c, oG + i), S(c, f + i), T, 39);
+    EQ(S(c, oF + i), S(c, e + i), T, 40);
+    EQ(S(c, oC + i), S(c, bb + i), T, 41);
+    EQ(S(c, oB + i), S(c, a + i), T, 42);
+  }
+  EQ(S(c, oDD), S(c, dS), T, 46);
+  EQ(S(c, oHH), S(c, hS), T, 47);
+  for (int i = 0; i < 64; i++) {
+    size_t mj = o, x0 = o + 3, x1 = o + 8;
+    o += ck_bits2(c, mj) + ck_xor3(c, x0) + ck_xor3(c, x1);
+    EQ(S(c, chb + i), ADD(MUL(S(c, e + i), SUB(S(c, f + i), S(c, g + i))), S(c, g + i)), T, 63);
+    EQ(S(c, chS + 1 + i), MUL(P2[i], S(c, chb + i)), T, 64);
+    EQ(S(c, mj + 2), ADD(ADD(S(c, a + i), S(c, bb + i)), S(c, cc + i)), T, 68);
+    EQ(S(c, mjS + 1 + i), MUL(P2[i], S(c, mj + 1)), T, 69);
+    EQ(S(c, x0 + 1), S(c, a + (i + 28) % 64), T, 72);
+    EQ(S(c, x0 + 2), S(c, a + (i + 34) % 64), T, 73);
+    EQ(S(c, x0 + 3), S(c, a + (i + 39) % 64), T, 74);
+    EQ(S(c, s0S + 1 + i), MUL(P2[i], S(c, x0)), T, 75);
+    EQ(S(c, x1 + 1), S(c, e + (i + 14) % 64), T, 78);
+    EQ(S(c, x1 + 2), S(c, e + (i + 18) % 64), T, 79);
+    EQ(S(c, x1 + 3), S(c, e + (i + 41) % 64), T, 80);
+    EQ(S(c, s1S + 1 + i), MUL(P2[i], S(c, x1)), T, 81);
+  }
+  fr_t t1 = ADD(ADD(ADD(S(c, s1S), S(c, chS)), S(c, key)), S(c, inp));
+  EQ(S(c, ovE), ADD(ADD(S(c, dd), S(c, hh)), t1), T, 85);
+  EQ(S(c, ovA), ADD(ADD(ADD(S(c, hh), t1), S(c, s0S)), S(c, mjS)), T, 86);
+  size_t dE = o;
+  o += ck_lastnbits(c, dE, 64);
+  EQ(S(c, dE + 65), S(c, ovE), T, 89);
+  for (int i = 0; i < 64; i++) EQ(S(c, oE + i), S(c, dE + 1 + i), T, 90);
+  size_t dA = o;
+  o += ck_lastnbits(c, dA, 64);
+  EQ(S(c, dA + 65), S(c, ovA), T, 93);
+  for (int i = 0; i < 64; i++) EQ(S(c, oA + i), S(c, dA + 1 + i), T, 94);
+  return o - b;
+}
+
+/* Sha2_384_512Rounds(80) sha512/sha512Rounds.circom:11-126:
+ * outHash[8][64] | words[80] inpHash[8][64] | a b c [81][64] dd[81] e f g [81][64] hh[81] ROUND_KEYS[80] hashWords[8] |
+ * roundKeys sumDd sumHh sum[8] compress[80] modulo[8] sumA sumB sumC sumE sumF sumG */
+static size_t ck_rounds512(ck_t *c, size_t b) {
+  const char *T = "Sha2_384_512Rounds hasher/sha2/sha512/sha512Rounds.circom";
+  const int n = 80;
+  size_t outH = b, words = b + 512, inH = b + 592;
+  size_t A = b + 1104, B = A + 81 * 64, C = B + 81 * 64, DD = C + 81 * 64, E = DD + 81, F = E + 81 * 64, G = F + 81 * 64,
+         HH = G + 81 * 64, RK = HH + 81, HW = RK + 80, o = HW + 8;
+  size_t rk = o;  /* SHA2_384_512RoundKeys sha512RoundConst.circom:6-38: out[80] */
+  for (int j = 0; j < 80; j++) req(c, S(c, rk + j), KC(SHA512_K[j]), "SHA2_384_512RoundKeys sha512RoundConst.circom", 35, rk);
+  o += 80;
+  for (int j = 0; j < 80; j++) EQ(S(c, RK + j), S(c, rk + j), T, 34);
+  for (int i = 0; i < 64; i++) {
+    EQ(S(c, A + i), S(c, inH + i), T, 36);
+    EQ(S(c, B + i), S(c, inH + 64 + i), T, 37);
+    EQ(S(c, C + i), S(c, inH + 128 + i), T, 38);
+    EQ(S(c, E + i), S(c, inH + 256 + i), T, 40);
+    EQ(S(c, F + i), S(c, inH + 320 + i), T, 41);
+    EQ(S(c, G + i), S(c, inH + 384 + i), T, 42);
+  }
+  size_t sDd = o, sHh = o + 128;
+  o += ck_getsum(c, sDd, 64) + ck_getsum(c, sHh, 64);
+  wire_sum64(c, b, sDd, inH + 192, T, 47);
+  wire_sum64(c, b, sHh, inH + 448, T, 48);
+  EQ(S(c, DD), S(c, sDd), T, 50);
+  EQ(S(c, HH), S(c, sHh), T, 51);
+  for (int j = 0; j < 8; j++) {
+    size_t sj = o;
+    o += ck_getsum(c, sj, 64);
+    wire_sum64(c, b, sj, inH + 64 * (size_t)j, T, 58);
+    EQ(S(c, HW + j), S(c, sj), T, 60);
+  }
+  for (int k = 0; k < n; k++) {
+    size_t ci = o;
+    o += ck_compress512(c, ci);
+    EQ(S(c, ci + 386), S(c, words + k), T, 69);
+    EQ(S(c, ci + 387), S(c, RK + k), T, 70);
+    for (int i = 0; i < 64; i++) {
+      EQ(S(c, ci + 388 + i), S(c, A + 64 * (size_t)k + i), T, 73);
+      EQ(S(c, ci + 452 + i), S(c, B + 64 * (size_t)k + i), T, 74);
+      EQ(S(c, ci + 516 + i), S(c, C + 64 * (size_t)k + i), T, 75);
+      EQ(S(c, ci + 581 + i), S(c, E + 64 * (size_t)k + i), T, 77);
+      EQ(S(c, ci + 645 + i), S(c, F + 64 * (size_t)k + i), T, 78);
+      EQ(S(c, ci + 709 + i), S(c, G + 64 * (size_t)k + i), T, 79);
+      EQ(S(c, A + 64 * (size_t)(k + 1) + i), S(c, ci + i), T, 82);
+      EQ(S(c, B + 64 * (size_t)(k + 1) + i), S(c, ci + 64 + i), T, 83);
+      EQ(S(c, C + 64 * (size_t)(k + 1) + i), S(c, ci + 128 + i), T, 84);
+      EQ(S(c, E + 64 * (size_t)(k + 1) + i), S(c, ci + 193 + i), T, 86);
+      EQ(S(c, F + 64 * (size_t)(k + 1) + i), S(c, ci + 257 + i), T, 87);
+      EQ(S(c, G + 64 * (size_t)(k + 1) + i), S(c, ci + 321 + i), T, 88);
+    }
+    EQ(S(c, ci + 580), S(c, DD + k), T, 76);
+    EQ(S(c, ci + 773), S(c, HH + k), T, 80);
+    EQ(S(c, DD + k + 1), S(c, ci + 192), T, 85);
+    EQ(S(c, HH + k + 1), S(c, ci + 385), T, 89);
+  }
+  size_t md = o;
+  for (int j = 0; j < 8; j++) o += ck_lastnbits(c, o, 64);
+  size_t sums[6], src[6] = {A, B, C, E, F, G};
+  for (int q = 0; q < 6; q++) {
+    sums[q] = o;
+    o += ck_getsum(c, o, 64);
+    wire_sum64(c, b, sums[q], src[q] + 64 * (size_t)n, T, 105);
+  }
+  static const int which[8] = {0, 1, 2, -1, 3, 4, 5, -2};
+  for (int j = 0; j < 8; j++) {
+    size_t mj = md + 322 * (size_t)j;
+    fr_t rhs = which[j] >= 0 ? S(c, sums[which[j]]) : which[j] == -1 ? S(c, DD + n) : S(c, HH + n);
+    EQ(S(c, mj + 65), ADD(S(c, HW + j), rhs), T, 113);
+    for (int i = 0; i < 64; i++) EQ(S(c, outH + 64 * (size_t)j + i), S(c, mj + 1 + i), T, 123);
+  }
+  return o - b;
+}
+
+static const uint64_t SHA512_IV64[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                        0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                        0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+static const uint64_t SHA384_IV64[8] = {0xcbbb9d5dc1059ed8ULL, 0x629a292a367cd507ULL, 0x9159015a3070dd17ULL,
+                                        0x152fecd8f70e5939ULL, 0x67332667ffc00b31ULL, 0x8eb44a8768581511ULL,
+                                        0xdb0c2e0d64f98fa7ULL, 0x47b5481dbefa4fa4ULL};
+
+/* Sha384HashChunks(B) sha384/sha384HashChunks.circom:8-47 (O = 384) / Sha512HashChunks(B) sha512/sha512HashChunks.circom
+ * (O = 512): out[O] | in[1024B] | states[B+1][8][64] | iv, (sch, rds)[B] */
+static size_t ck_sha5chunks(ck_t *c, size_t b, int B, int O) {
+  const char *T = O == 384 ? "Sha384HashChunks hasher/sha2/sha384/sha384HashChunks.circom"
+                           : "Sha512HashChunks hasher/sha2/sha512/sha512HashChunks.circom";
+  const int d = O == 384 ? 1 : 0;  /* Sha512HashChunks' lines are one above Sha384HashChunks' */
+  size_t out = b, in = b + O, st = in + 1024 * (size_t)B, o = st + (size_t)(B + 1) * 512;
+  size_t iv = o;
+  const uint64_t *IV = O == 384 ? SHA384_IV64 : SHA512_IV64;
+  for (int k = 0; k < 8; k++)
+    for (int i = 0; i < 64; i++)
+      req(c, S(c, iv + 64 * k + i), KC((IV[k] >> i) & 1),
+          O == 384 ? "Sha384InitialValues sha384InitialValue.circom" : "Sha512InitialValues sha512InitialValue.circom", 24, iv);
+  o += 512;
+  for (int q = 0; q < 512; q++) EQ(S(c, st + q), S(c, iv + q), T, 19 + d);
+  for (int m = 0; m < B; m++) {
+    size_t sch = o;
+    o += ck_schedule512(c, sch);
+    size_t rds = o;
+    o += ck_rounds512(c, rds);
+    for (int k = 0; k < 16; k++)
+      for (int i = 0; i < 64; i++)
+        EQ(S(c, sch + 80 + 64 * k + i), S(c, in + 1024 * (size_t)m + 64 * k + 63 - i), T, 31 + d);
+    for (int q = 0; q < 80; q++) EQ(S(c, rds + 512 + q), S(c, sch + q), T, 35 + d);
+    for (int q = 0; q < 512; q++) {
+      EQ(S(c, rds + 592 + q), S(c, st + 512 * (size_t)m + q), T, 37 + d);
+      EQ(S(c, st + 512 * (size_t)(m + 1) + q), S(c, rds + q), T, 38 + d);
+    }
+  }
+  for (int j = 0; j < O / 64; j++)
+    for (int i = 0; i < 64; i++) EQ(S(c, out + 64 * j + i), S(c, st + 512 * (size_t)B + 64 * j + 63 - i), T, 43 + d);
+  return o - b;
+}
+
 /* ============================================================ SHA-1 (hasher/sha1) */
 /* RotL(32, L) rotate.circom: out[32] | in[32] */
 static size_t ck_rotl(ck_t *c, size_t b, int L) {
@@ -1244,40 +1476,43 @@ static size_t ck_rsa_pkcs256(ck_t *c, size_t b, int K, uint32_t EXP) {
 
 /* ============================================================ RSA-PSS (signatures/rsaPss.circom, mgf1.circom) */
 static size_t ck_shahash(ck_t *c, size_t b, int B, int algo);
-/* Mgf1Sha256(SEED_LEN, MASK_LEN) mgf1.circom:70-127: out[8 MASK] | seed[8 SEED] | hashed[256 ITER] | (sha256[i] num2Bits[i])[ITER] */
-static size_t ck_mgf1(ck_t *c, size_t b, int SEED, int MASK) {
-  const char *T = "Mgf1Sha256 signatures/mgf1.circom";
-  int SB = SEED * 8, MB = MASK * 8, IT = MASK / 32 + 1;
-  size_t out = b, seed = b + MB, hs = seed + SB, o = hs + 256 * (size_t)IT;
+/* Mgf1Sha256 / Mgf1Sha384(SEED_LEN, MASK_LEN) mgf1.circom:5-133 (H = 256 / 384):
+ * out[8 MASK] | seed[8 SEED] | hashed[H ITER] | (shaH[i] num2Bits[i])[ITER], ITER = MASK / (H/8) + 1; block i hashes
+ * seed | counter i (MSB first) | the padding of an (8 SEED + 32)-bit message to one BS-bit block */
+static size_t ck_mgf1(ck_t *c, size_t b, int SEED, int MASK, int H) {
+  const int h384 = H == 384;
+  const char *T = h384 ? "Mgf1Sha384 signatures/mgf1.circom" : "Mgf1Sha256 signatures/mgf1.circom";
+  int SB = SEED * 8, MB = MASK * 8, IT = MASK / (H / 8) + 1, BS = H > 256 ? 1024 : 512, LM = SB + 32;
+  size_t out = b, seed = b + MB, hs = seed + SB, o = hs + (size_t)H * IT;
   for (int i = 0; i < IT; i++) {
     size_t sh = o;
-    o += ck_shahash(c, sh, 1, 256);
+    o += ck_shahash(c, sh, 1, H);
     size_t nb = o;
     o += ck_num2bits(c, nb, 32);
-    EQ(S(c, nb + 32), KC((uint64_t)i), T, 99);
-    size_t in = sh + 256;
-    for (int j = 0; j < 512; j++) {
+    EQ(S(c, nb + 32), KC((uint64_t)i), T, h384 ? 35 : 99);
+    size_t in = sh + H;
+    for (int j = 0; j < BS; j++) {
       fr_t v;
       if (j < SB) v = S(c, seed + j);
-      else if (j < SB + 32) v = S(c, nb + 31 - (j - SB));
-      else v = KC(j == 288 || j == 503 || j == 506);  /* padding of the 288-bit message (:106-117) */
-      EQ(S(c, in + j), v, T, 120);
+      else if (j < LM) v = S(c, nb + 31 - (j - SB));
+      else v = KC(j == LM || (j >= BS - 11 && ((LM >> (BS - 1 - j)) & 1)));  /* padding (:42-55, :106-117) */
+      EQ(S(c, in + j), v, T, h384 ? 58 : 120);
     }
-    for (int j = 0; j < 256; j++) EQ(S(c, hs + (size_t)i * 256 + j), S(c, sh + j), T, 123);
+    for (int j = 0; j < H; j++) EQ(S(c, hs + (size_t)i * H + j), S(c, sh + j), T, h384 ? 61 : 123);
   }
-  for (int i = 0; i < MB; i++) EQ(S(c, out + i), S(c, hs + i), T, 128);
+  for (int i = 0; i < MB; i++) EQ(S(c, out + i), S(c, hs + i), T, h384 ? 66 : 128);
   return o - b;
 }
 
 /* VerifyRsaPssSig(64, K, SALT, EXP, 256) rsaPss.circom:18-254: pubkey[K] signature[K] hashed[256] |
  * eM[EM] eMsgInBits[8 EM] encoded[K] dbMask db salt maskedDB hash mDash[1024] |
  * powerMod num2Bits[K] bits2Num[EM] MGF1_256 xor hDash256 */
-static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP) {
+static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP, int H) {
   const char *T = "VerifyRsaPssSig signatures/rsaPss.circom";
-  const int EM = 8 * K, EMB = 64 * K, HL = 32, DBL = EM - HL - 1, SB = SALT * 8;
-  size_t pk = b, sig = b + K, hd = sig + K, eM = hd + 256, bits = eM + EM, enc = bits + EMB, dbm = enc + K,
+  const int EM = 8 * K, EMB = 64 * K, HL = H / 8, DBL = EM - HL - 1, SB = SALT * 8, h384 = H == 384;
+  size_t pk = b, sig = b + K, hd = sig + K, eM = hd + H, bits = eM + EM, enc = bits + EMB, dbm = enc + K,
          db = dbm + 8 * (size_t)DBL, salt = db + 8 * (size_t)DBL, mdb = salt + SB, hash = mdb + 8 * (size_t)DBL,
-         md = hash + 256, o = md + 1024;
+         md = hash + H, o = md + 1024;
   size_t pm = o;
   o += ck_powermod(c, pm, K, EXP);
   for (int i = 0; i < K; i++) {
@@ -1298,11 +1533,11 @@ static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP) {
     EQ(S(c, eM + EM - i - 1), S(c, bn), T, 66);
   }
   for (int i = 0; i < 8 * DBL; i++) EQ(S(c, mdb + i), S(c, bits + i), T, 86);
-  for (int i = 0; i < 256; i++) EQ(S(c, hash + i), S(c, bits + EMB - 256 - 8 + i), T, 93);
+  for (int i = 0; i < H; i++) EQ(S(c, hash + i), S(c, bits + EMB - H - 8 + i), T, 89);
   size_t mg = o;
-  o += ck_mgf1(c, mg, HL, DBL);
-  for (int i = 0; i < 256; i++) EQ(S(c, mg + 8 * (size_t)DBL + i), S(c, hash + i), T, 100);
-  for (int i = 0; i < 8 * DBL; i++) EQ(S(c, dbm + i), S(c, mg + i), T, 103);
+  o += ck_mgf1(c, mg, HL, DBL, H);
+  for (int i = 0; i < H; i++) EQ(S(c, mg + 8 * (size_t)DBL + i), S(c, hash + i), T, h384 ? 105 : 96);
+  for (int i = 0; i < 8 * DBL; i++) EQ(S(c, dbm + i), S(c, mg + i), T, h384 ? 108 : 99);
   size_t xr = o;  /* Xor2(n) bitify/bitGates.circom:232-240: out[n] | in1[n] in2[n] */
   o += 3 * 8 * (size_t)DBL;
   for (int i = 0; i < 8 * DBL; i++) {
@@ -1314,20 +1549,22 @@ static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP) {
     EQ(S(c, db + i), i == 0 ? fr_zero() : S(c, xr + i), T, i == 0 ? 135 : 137);
   }
   for (int i = 0; i < SB; i++) EQ(S(c, salt + SB - 1 - i), S(c, db + 8 * (size_t)DBL - 1 - i), T, 143);
-  for (int i = 0; i < 64; i++) EQ(S(c, md + i), fr_zero(), T, 155);
-  for (int i = 0; i < 256; i++) EQ(S(c, md + 64 + i), S(c, hd + i), T, 159);
-  for (int i = 0; i < SB; i++) EQ(S(c, md + 64 + 256 + i), S(c, salt + i), T, 163);
-  /* SHA-256 padding of M' (576 bits for salt 32, 832 for salt 64) */
-  int L = 64 + 256 + SB;
+  for (int i = 0; i < 64; i++) EQ(S(c, md + i), fr_zero(), T, 149);
+  for (int i = 0; i < H; i++) EQ(S(c, md + 64 + i), S(c, hd + i), T, 153);
+  for (int i = 0; i < SB; i++) EQ(S(c, md + 64 + H + i), S(c, salt + i), T, 157);
+  /* padding of M' to 1024 bits (576 bits for salt 32, 832 for SHA-256 salt 64 and SHA-384 salt 48): two SHA-256
+   * blocks (64-bit length) or one SHA-384 block (128-bit length); the length fits the last 11 bits */
+  int L = 64 + H + SB;
+  const int lp = h384 ? 210 : SALT == 32 ? 167 : 188;
   for (int i = L; i < 1024; i++) {
     int v = (i == L);
-    if (i >= 960) v = (((uint64_t)L >> (1023 - i)) & 1);
-    EQ(S(c, md + i), KC((uint64_t)v), T, SALT == 32 ? 170 : 196);
+    if (i >= 1013) v = (L >> (1023 - i)) & 1;  /* the length field: L < 2^11 */
+    EQ(S(c, md + i), KC((uint64_t)v), T, lp);
   }
   size_t hh = o;
-  o += ck_shahash(c, hh, 2, 256);
-  for (int i = 0; i < 1024; i++) EQ(S(c, hh + 256 + i), S(c, md + i), T, SALT == 32 ? 185 : 209);
-  for (int i = 0; i < 256; i++) EQ(S(c, hh + i), S(c, hash + i), T, SALT == 32 ? 186 : 210);
+  o += ck_shahash(c, hh, h384 ? 1 : 2, H);
+  for (int i = 0; i < 1024; i++) EQ(S(c, hh + H + i), S(c, md + i), T, h384 ? 224 : SALT == 32 ? 181 : 200);
+  for (int i = 0; i < H; i++) EQ(S(c, hh + i), S(c, hash + i), T, h384 ? 225 : SALT == 32 ? 182 : 201);
   return o - b;
 }
 
@@ -1859,13 +2096,15 @@ static size_t ck_flow(ck_t *c, size_t b, int ECS, int H, int EHT, int DG1S, int 
   return o - b;
 }
 
-/* ShaHashChunks(B, ALGO) hasher/hash.circom:32-68 (ALGO 160 / 224 / 256): out[ALGO] | in[512B] | hashALGO */
+/* ShaHashChunks(B, ALGO) hasher/hash.circom:32-68: out[ALGO] | in[BS x B] | hashALGO (BS = 512, or 1024 above 256) */
 static size_t ck_shahash(ck_t *c, size_t b, int B, int algo) {
   const char *T = "ShaHashChunks hasher/hash.circom";
-  size_t out = b, in = b + algo, h = in + 512 * (size_t)B;
-  size_t sz = (size_t)algo + 512 * (size_t)B + (algo == 160 ? ck_sha1chunks(c, h, B) : ck_sha2chunks(c, h, B, algo));
-  int l0 = algo == 160 ? 46 : algo == 224 ? 51 : 56;
-  for (int i = 0; i < 512 * B; i++) EQ(S(c, h + algo + i), S(c, in + i), T, l0);
+  const size_t BS = algo > 256 ? 1024 : 512;
+  size_t out = b, in = b + algo, h = in + BS * (size_t)B;
+  size_t sz = (size_t)algo + BS * (size_t)B +
+              (algo == 160 ? ck_sha1chunks(c, h, B) : algo > 256 ? ck_sha5chunks(c, h, B, algo) : ck_sha2chunks(c, h, B, algo));
+  int l0 = algo == 160 ? 46 : algo == 224 ? 51 : algo == 256 ? 56 : algo == 384 ? 60 : 65;
+  for (size_t i = 0; i < BS * B; i++) EQ(S(c, h + algo + i), S(c, in + i), T, l0);
   for (int i = 0; i < algo; i++) EQ(S(c, out + i), S(c, h + i), T, l0 + 1);
   return sz;
 }
@@ -1904,6 +2143,8 @@ static size_t ck_rsa_pkcs160(ck_t *c, size_t b, int K, uint32_t EXP) {
 typedef struct { int sig, dg_hash, doc, ec_blocks, ec_shift, dg1_shift, aa, dg15_shift, dg15_blocks, aa_shift; } ck_params;
 
 static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : sig >= 20 ? 4 : 32; }
+/* HASH_TYPE of the EC / SA hashers (passportVerificationBuilder.circom:16-59) */
+static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : sig == 13 ? 384 : 256; }
 
 /* PassportVerificationBuilder(...) passportVerificationBuilder.circom:11-246 (RSA PKCS#1 v1.5 over SHA-2):
  * passportHash | encapsulatedContent dg1 dg15 signedAttributes signature pubkey slaveMerkleInclusionBranches[80]
@@ -1912,21 +2153,22 @@ static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 
  * signatureVerification signedAttributesNum pubkeyHasherRsa smtVerifier signedAttributesHashHasher */
 static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "PassportVerificationBuilder passportVerification/passportVerificationBuilder.circom";
-  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = (P->sig == 3 || P->sig == 4) ? 160 : 256,
-            ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512, ecdsa = P->sig >= 20, PKL = ecdsa ? 2 * K : K;
+  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = sig_hash(P->sig), HBS = HT > 256 ? 1024 : 512,
+            DBS = DGH > 256 ? 1024 : 512, ECL = P->ec_blocks * HBS, D15L = P->dg15_blocks * HBS, ecdsa = P->sig >= 20,
+            PKL = ecdsa ? 2 * K : K;
   size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + PKL,
          br = pk + PKL, root = br + 80;
   /* intermediates: ..., pubkeyHash, then tempModulus[5] (RSA, :170) or ecBitsX[256] ecBitsY[256] (ECDSA, :188-189) */
   size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1,
          ebx = pkh + 1, eby = ebx + 256, o = ecdsa ? eby + 256 : tmod + 5;
   size_t hs = o;
-  o += ck_shahash(c, hs, 2, DGH);
-  for (int j = 0; j < 1024; j++) EQ(S(c, hs + DGH + j), S(c, dg1 + j), T, 97);
+  o += ck_shahash(c, hs, 1024 / DBS, DGH);
+  for (int j = 0; j < 1024; j++) EQ(S(c, hs + DGH + j), S(c, dg1 + j), T, 104);
   for (int j = 0; j < DGH; j++) EQ(S(c, d1h + j), S(c, hs + j), T, 98);
   if (P->aa) {
     hs = o;
     o += ck_shahash(c, hs, P->dg15_blocks, DGH);
-    for (int j = 0; j < D15L; j++) EQ(S(c, hs + DGH + j), S(c, dg15 + j), T, 111);
+    for (int j = 0; j < DBS * P->dg15_blocks; j++) EQ(S(c, hs + DGH + j), S(c, dg15 + j), T, 119);
     for (int j = 0; j < DGH; j++) EQ(S(c, d15h + j), S(c, hs + j), T, 113);
   } else {
     for (int j = 0; j < DGH; j++) EQ(S(c, d15h + j), fr_zero(), T, 118);
@@ -1936,8 +2178,8 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   for (int j = 0; j < ECL; j++) EQ(S(c, hs + HT + j), S(c, ec + j), T, 124);
   for (int j = 0; j < HT; j++) EQ(S(c, ech + j), S(c, hs + j), T, 126);
   hs = o;
-  o += ck_shahash(c, hs, 2, HT);
-  for (int j = 0; j < 1024; j++) EQ(S(c, hs + HT + j), S(c, sa + j), T, 129);
+  o += ck_shahash(c, hs, 1024 / HBS, HT);
+  for (int j = 0; j < 1024; j++) EQ(S(c, hs + HT + j), S(c, sa + j), T, 137);
   for (int j = 0; j < HT; j++) EQ(S(c, sah + j), S(c, hs + j), T, 130);
   size_t fl = o;
   o += ck_flow(c, fl, ECL, DGH, HT, P->dg1_shift, P->aa ? P->dg15_shift : DGH, P->ec_shift, P->aa);
@@ -1961,7 +2203,7 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
       req(c, S(c, rsa + 8 + i), S(c, sv + PK + i), TV, 186, sv);
     }
   } else if (pss) {  /* VerifyRsaPssSig: pubkey, signature, hashed */
-    o += 2 * (size_t)K + HT + ck_pss(c, rsa, K, P->sig == 12 ? 64 : 32, P->sig == 10 ? 3 : 65537);
+    o += 2 * (size_t)K + HT + ck_pss(c, rsa, K, P->sig == 12 ? 64 : P->sig == 13 ? 48 : 32, P->sig == 10 ? 3 : 65537, HT);
     for (int i = 0; i < K; i++) {
       req(c, S(c, rsa + i), S(c, sv + i), TV, 147, sv);
       req(c, S(c, rsa + K + i), S(c, sv + K + i), TV, 148, sv);
@@ -2036,7 +2278,7 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
  * dg1Hasher dg1Chunking[4] skIndentityHasher pkIdentityCalc pkIdentityHasher */
 static size_t ck_regid(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "RegisterIdentity identityManagement/identity.circom";
-  const int D15L = P->dg15_blocks * 512;
+  const int D15L = P->dg15_blocks * (P->dg_hash > 256 ? 1024 : 512);  /* DG15_SIZE x DG_HASH_BLOCK_SIZE */
   size_t d15ph = b, d1c = b + 1, pkih = b + 2, dg1 = b + 3, dg15 = dg1 + 1024, sk = dg15 + D15L, o = sk + 1;
   if (P->aa && P->aa < 20) {
     size_t ch[5];
@@ -2102,7 +2344,8 @@ static size_t ck_regid(ck_t *c, size_t b, const ck_params *P) {
  * passportVerifier registerIdentity */
 static size_t ck_builder(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "RegisterIdentityBuilder identityManagement/registerIdentityBuilder.circom";
-  const int K = sig_K(P->sig) * (P->sig >= 20 ? 2 : 1), ECL = P->ec_blocks * 512, D15L = P->dg15_blocks * 512;
+  const int HBS = sig_hash(P->sig) > 256 ? 1024 : 512;
+  const int K = sig_K(P->sig) * (P->sig >= 20 ? 2 : 1), ECL = P->ec_blocks * HBS, D15L = P->dg15_blocks * HBS;
   size_t d15ph = b, ph = b + 1, d1c = b + 2, pkih = b + 3, root = b + 4, ec = b + 5, dg1 = ec + ECL, dg15 = dg1 + 1024,
          sa = dg15 + D15L, sig = sa + 1024, pk = sig + K, br = pk + K, sk = br + 80, o = sk + 1;
   size_t pv = o;
@@ -2196,12 +2439,12 @@ int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r) {
   return ck_end(&c, walked, r);
 }
 
-/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-12, 14), ECDSA P-256 / brainpoolP256r1
- * (SIG 20 / 21), DG hash 160 / 224 / 256 */
+/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-14), ECDSA P-256 / brainpoolP256r1
+ * (SIG 20 / 21), DG hash 160 / 224 / 256 / 384 */
 int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r) {
   if (!pos_loaded) return -1;
-  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 12) || P->sig == 14 || P->sig == 20 || P->sig == 21) ||
-      !(P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160))
+  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 14) || P->sig == 20 || P->sig == 21) ||
+      !(P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160 || P->dg_hash == 384))
     return -2;
   if (P->sig >= 20) {
     CV = &EC[P->sig - 20];
@@ -2210,6 +2453,12 @@ int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r)
   ck_t c = ck_begin(wit, nw);
   size_t walked = 1 + ck_builder(&c, 1, P);
   req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);
+  return ck_end(&c, walked, r);
+}
+
+int ck_sha512(int B, int O, const uint8_t *wit, size_t n, ck_report *r) {
+  ck_t c = ck_begin(wit, n);
+  size_t walked = 1 + ck_sha5chunks(&c, 1, B, O);
   return ck_end(&c, walked, r);
 }
 

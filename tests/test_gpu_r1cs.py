@@ -37,8 +37,26 @@ def test_config2_sha256_device_witnesses():
         _ok(pyr1cs.check_sha256(w, 6), 0)
 
 
+@pytest.mark.parametrize("out_bits,blocks", [(384, 2), (512, 1)])
+def test_sha512_device_witnesses(out_bits, blocks):
+    """Sha384HashChunks / Sha512HashChunks device witnesses (k_emit_sha512) satisfy every constraint."""
+    rng = np.random.default_rng(out_bits + blocks)
+    rows = []
+    for _ in range(6):
+        m = rng.integers(0, 256, int(rng.integers(128 * blocks - 120, 128 * blocks - 17)), dtype=np.uint8).tobytes()
+        r = np.zeros((1024 * blocks, 32), np.uint8)
+        r[:, 0] = I.bits_msb_first(I.sha_pad(m, 1024))
+        rows.append(r)
+    circ = native.PZK_CIRCUIT_SHA384 if out_bits == 384 else native.PZK_CIRCUIT_SHA512
+    wit, st = native.Instance(circ, blocks).witness_batch_host(np.stack(rows))
+    assert (st == 0).all()
+    for w in wit:
+        _ok(pyr1cs.check_sha512(w, blocks, out_bits), 0)
+
+
 @pytest.mark.parametrize("sig,depths", [(1, [0, 1, 2, 40, 79, 0, 5, 17]), (2, [0, 9, 33]), (3, [0, 4]), (4, [2]),
-                                        (10, [0, 3]), (11, [0, 6]), (12, [1]), (14, [0]), (20, [0, 2]), (21, [1])])
+                                        (10, [0, 3]), (11, [0, 6]), (12, [1]), (13, [0, 3]), (14, [0]), (20, [0, 2]),
+                                        (21, [1])])
 def test_config3_4_register_device_witnesses(sig, depths):
     """Config 3 (canonical, SMT root of the one-leaf tree) and config 4 (depth-k SMT paths), the
     RSA-4096 flow of config 5 and the SHA-1 / RSA-3072 / RSA-PSS instances: every device witness

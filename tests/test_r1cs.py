@@ -22,7 +22,7 @@ pyr1cs = pytest.importorskip("pyr1cs")
 UNASSIGNED_PER_BMM = {32: 992, 64: 4032, 48: 4512}
 # BigMultModP instances per PowerMod (exp_to_bits, bigIntFunc.circom:590-616): 65537 -> 16 squarings + 1,
 # 3 -> 1 + 1, 37187 -> 15 + 5; SIG 3 / 4 add the two never-assigned hashed_chunks of rsa.circom:81
-N_BMM = {1: 17, 2: 17, 3: 17, 4: 20, 10: 2, 11: 17, 12: 17, 14: 17}
+N_BMM = {1: 17, 2: 17, 3: 17, 4: 20, 10: 2, 11: 17, 12: 17, 13: 17, 14: 17}
 EXTRA = {3: 2, 4: 2}
 # ECDSA (verifyECDSABits over 4 x 64-bit limbs): every BigMultNonEqualOverflow(G, 4) leaves 4 * 3 tmpResult entries
 # unassigned; 3,164 of them per witness = 260 EllipticCurveDouble x 9 + 102 EllipticCurveAdd x 8 + 4 BigMultModP x 2
@@ -63,6 +63,26 @@ def test_sha1_circuit(oracle):
         _ok(pyr1cs.check_sha1(w, blocks), 0)
 
 
+@pytest.mark.parametrize("out_bits", [384, 512])
+def test_sha512_circuits(oracle, out_bits):
+    """Sha384HashChunks / Sha512HashChunks (sha2/sha384, sha512/*.circom): every constraint of the schedule,
+    the 80 compression rounds (64-bit GetLastNBits decompositions of sums up to 67 bits) and the chunk
+    wiring holds on oracle witnesses; one flipped round bit breaks one."""
+    rng = np.random.default_rng(out_bits)
+    for blocks in (1, 2):
+        m = rng.integers(0, 256, 128 * blocks - 40, dtype=np.uint8).tobytes()
+        r = np.zeros((1024 * blocks, 32), np.uint8)
+        r[:, 0] = I.bits_msb_first(I.sha_pad(m, 1024))
+        rc, w = oracle.sha512_witness(r, blocks, out_bits)
+        assert rc == 0
+        _ok(pyr1cs.check_sha512(w, blocks, out_bits), 0)
+    w = w.copy()
+    k = 1 + out_bits + 2048 + 512 * 3 + 512 + 94480 + 5000  # inside block 0's rounds
+    w[k, 0] ^= 1
+    rc, rep = pyr1cs.check_sha512(w, blocks, out_bits)
+    assert rc != 0 and rep["n_failed"] > 0
+
+
 def test_sha256_config2(oracle):
     _, rows = I.sha256_config2_batch(3, seed=2, blocks=6)
     for r in rows:
@@ -85,6 +105,8 @@ REGISTER_CASES = [
     ("sig10_pss_e3", I.instance_params(10), 4),
     ("sig11_pss", I.instance_params(11), 0),
     ("sig12_pss_salt64", I.instance_params(12), 0),
+    ("sig13_pss_sha384", I.instance_params(13), 0),
+    ("sig13_dg256_no_dg15", dict(I.instance_params(13), dg_hash=256, aa=0, dg15_blocks=0), 2),
     ("sig14_pss3072", I.instance_params(14), 1),
     ("sig20_ecdsa_p256", I.instance_params(20), 0),
     ("sig21_ecdsa_brainpool", I.instance_params(21), 3),

@@ -46,7 +46,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
     """Passports first .. first + batch - 1 of the synthetic stream, packed."""
     from pzkwit import inputs as I
     workers = workers or max(1, min(16, os.cpu_count() or 1))
-    I.PassportGen.shared(seed, n_keys, sig)  # keys generated once (parallel inside)
+    keys = I.PassportGen.shared(seed, n_keys, sig).keys  # keys generated once (parallel inside), handed to workers
     step = (batch + workers * 4 - 1) // (workers * 4)
     jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig) for lo in range(0, batch, step)]
     n_in = I.PassportGen.shared(seed, n_keys, sig).n_inputs
@@ -55,7 +55,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
         for lo, arr in map(_gen_slice, jobs):
             buf[lo - first: lo - first + len(arr)] = arr
     else:
-        with I.process_pool(workers) as ex:
+        with I.process_pool(workers, I.PassportGen.install_shared, (seed, n_keys, sig, keys)) as ex:
             for lo, arr in ex.map(_gen_slice, jobs):
                 buf[lo - first: lo - first + len(arr)] = arr
     return buf

@@ -13,13 +13,14 @@ import numpy as np
 
 from .field import P, SplitMix64, poseidon
 
-def process_pool(workers):
+def process_pool(workers, initializer=None, initargs=()):
     """Worker pool for input generation. Spawned, not forked: a fork of a process that has
     initialised HIP (torch, libpzkwit) hands the children a runtime they cannot use, and the
     parent's device state must not be touched by them either."""
     import multiprocessing
     from concurrent.futures import ProcessPoolExecutor
-    return ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn"))
+    return ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn"), initializer=initializer,
+                               initargs=initargs)
 
 
 # ----------------------------------------------------------- process_passport.js
@@ -337,10 +338,14 @@ class PassportGen:
 
     _shared = {}
 
-    def __init__(self, seed=3, n_keys=64, key_bits=2048, params=None, workers=None):
+    def __init__(self, seed=3, n_keys=64, key_bits=2048, params=None, workers=None, keys=None):
         self.seed = seed
         self.rng = SplitMix64(seed)
         self.params = dict(CANONICAL if params is None else params)
+        self._pkhash = {}
+        if keys is not None:  # signer keys made elsewhere (worker processes get the parent's)
+            self.keys = list(keys)
+            return
         if self.params["sig"] >= 20:
             key_bits = "bp256" if self.params["sig"] == 21 else "p256"
         elif self.params["sig"] == 2 and key_bits == 2048:
@@ -355,7 +360,6 @@ class PassportGen:
                 self.keys = list(ex.map(_keygen, jobs))
         else:
             self.keys = [_keygen(j) for j in jobs]
-        self._pkhash = {}
 
     @classmethod
     def shared(cls, seed=3, n_keys=64, sig=1):
@@ -363,6 +367,11 @@ class PassportGen:
         if key not in cls._shared:
             cls._shared[key] = cls(seed, n_keys, params=instance_params(sig))
         return cls._shared[key]
+
+    @classmethod
+    def install_shared(cls, seed, n_keys, sig, keys):
+        """Pool initializer: the parent's signer keys, so workers do not regenerate them."""
+        cls._shared[(seed, n_keys, sig)] = cls(seed, n_keys, params=instance_params(sig), keys=keys)
 
     @property
     def n_inputs(self):

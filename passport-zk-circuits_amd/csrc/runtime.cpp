@@ -20,6 +20,9 @@ using namespace pzk;
 
 static thread_local std::string g_err;
 static int fail(int code, const std::string& msg) { g_err = msg; return code; }
+namespace pzk {
+int api_fail(int code, const std::string& msg) { return fail(code, msg); }  // passport.cpp
+}
 #define HIPCHK(x)                                                                              \
   do {                                                                                         \
     hipError_t e_ = (x);                                                                       \

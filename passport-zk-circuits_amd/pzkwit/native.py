@@ -16,11 +16,11 @@ PZK_CIRCUIT_REGISTER, PZK_CIRCUIT_POSEIDON, PZK_CIRCUIT_SHA256, PZK_CIRCUIT_SHA1
 PZK_CIRCUIT_SHA384, PZK_CIRCUIT_SHA512 = 4, 5
 PZK_EXEC_SYNC = 1
 
-# C-ABI entry points declared in include/pzkwit.h (checked by tests/test_capi.py)
+# C-ABI entry points declared in include/pzkwit.h and include/pzkpassport.h (checked by tests/test_capi.py)
 EXPORTS = ("pzk_instance_create", "pzk_instance_destroy", "pzk_instance_info", "pzk_instance_input",
            "pzk_wtns_header", "pzk_witness_batch", "pzk_witness_batch_host", "pzk_instance_sync",
            "pzk_instance_create_mapped", "pzk_sym_check", "pzk_timing", "pzk_phase_info", "pzk_last_error",
-           "pzk_version")
+           "pzk_version", "pzk_passport_parse", "pzk_passport_inputs")
 
 STATUS_NAMES = {
     0: "OK", 1: "Num2Bits (bitify.circom:26)", 2: "AliasCheck (aliascheck.circom:14)",

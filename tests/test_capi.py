@@ -1,6 +1,7 @@
-"""CPU: the C-ABI library loads, exports every entry point include/pzkwit.h declares, and its
+"""CPU: the C-ABI library loads, exports every entry point include/*.h declares, and its
 host-side layout (no device needed) agrees with the oracle's independently derived sizes."""
 import ctypes
+import glob
 import os
 import re
 
@@ -8,11 +9,11 @@ import pytest
 
 from pzkwit import inputs as I, native
 
-HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pzkwit.h")
+HDRS = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "*.h")))
 
 
 def declared_functions():
-    src = open(HDR).read()
+    src = "".join(open(h).read() for h in HDRS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pzk_\w+)\s*\(", src)))
 

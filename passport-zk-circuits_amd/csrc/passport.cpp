@@ -6,6 +6,8 @@
 // :3593-3606), so every walk the reference makes over `decoded(json.sod)` lands on the same element.
 // Pinned by tests/golden/sod_vectors.json: the reference's processPassport itself, run on Node 12 over
 // synthetic EF.SOD files (tools/gen_sod_fixtures.*).
+#include <sched.h>
+
 #include <algorithm>
 #include <array>
 #include <cstdint>
@@ -982,7 +984,12 @@ extern "C" int pzk_passport_inputs(const pzk_params* params, const pzk_passport_
       status[i] = PZK_PP_PARSE;
     }
   };
-  int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nt = threads;
+  if (nt <= 0) {  // the CPUs this process may run on (a container's share, not the machine's count)
+    cpu_set_t cs;
+    nt = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : (int)std::thread::hardware_concurrency();
+    nt = std::max(nt, 1);
+  }
   nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(n, 1));
   if (nt <= 1) {
     for (size_t i = 0; i < n; i++) work(i);

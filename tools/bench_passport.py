@@ -48,7 +48,7 @@ def main():
     rows = __import__("numpy").zeros((a.n,) + rows.shape[1:], dtype=rows.dtype)
     rows.fill(1)  # fault the pages in: the timed calls write rows into resident (e.g. pinned) memory
     srcs = PP.sources(batch)
-    for th in (1, os.cpu_count() or 1):
+    for th in (1, int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))):  # the box's CPU share
         t = time.perf_counter()
         rows, st = PP.input_rows(params, srcs, threads=th, out=rows)
         dt = time.perf_counter() - t

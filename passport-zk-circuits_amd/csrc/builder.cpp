@@ -109,12 +109,13 @@ void pos_program(int t, std::vector<uint16_t>& P) {
   const PosImg I(t);
   const int n = t - 1, RP = I.rp;
   P.clear();
-  auto C = [&](int idx) { P.push_back(pos_desc(idx, POS_D_COPY)); };
-  // GetSumOfNElements(t) over a prefix-sum row: out | in[t] | sum[t-1]
+  auto C = [&](int idx) { P.push_back(pos_desc(idx)); };
+  // GetSumOfNElements(t) over a prefix-sum row: out | in[t] (the products) | sum[t-1]
   auto getsum = [&](int row) {
+    const int r = row < I.ps ? (row - I.fs) / t : 7 * t + 1 + (row - I.ps) / t;  // phase-B row number
     C(row + t - 1);
     C(row);
-    for (int j = 1; j < t; j++) P.push_back(pos_desc(row + j, POS_D_DIFF));
+    for (int j = 1; j < t; j++) C(I.prod(r, j));
     for (int q = 1; q < t; q++) C(row + q);
   };
   C(I.hash);

@@ -274,15 +274,10 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
   for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
   pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
-  // two lanes per element (16 B each, 1 KiB contiguous per wave store); DIFF rows are the
-  // products of a GetSum row, recovered from its prefix sums
+  // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
   uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
-  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) {
-    const uint32_t d = prog[h >> 1], idx = d & 2047;
-    fr v = img[idx];
-    if (d >> 11) v = fr_sub(v, img[idx - 1]);
-    out[h] = (h & 1) ? make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]) : make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
-  }
+  const uint4* im = reinterpret_cast<const uint4*>(img);
+  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = im[2u * prog[h >> 1] + (h & 1)];
 }
 
 // ------------------------------------------------------------------- emit: generic small regions

@@ -177,9 +177,9 @@ __device__ __forceinline__ void pos_core_group(const PosConsts& K, const PosTask
 //  A: per S-box (8t full-layer elements, RP partial rounds): x, x^2, x^4, x^5 and the Ark output
 //     from the Montgomery layer state of the core; the remaining partial-round states; inputs,
 //     hash, zero.
-//  B: per GetSum row (7t full, 1 last, RP partial): t products constant*value as prefix sums.
-//     mont_mul(c * R, v) = c * v, so products of Montgomery constants with normal-form values
-//     come out in normal form.
+//  B: per GetSum row (7t full, 1 last, RP partial): t products constant*value, kept (products
+//     1..t-1, the row's `in` signals) and turned into prefix sums. mont_mul(c * R, v) = c * v, so
+//     products of Montgomery constants with normal-form values come out in normal form.
 template <int T>
 __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const fr* core, const ValueStore& vs,
                                              const PosTask& task, uint32_t w) {
@@ -245,7 +245,9 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
       v = k == 0 ? img[I.pin0 + r] : img[I.pin + r * t + k];
       dst = I.ps + r * t + k;
     }
-    img[dst] = fr_mul_fast(c, v);
+    const fr pr = fr_mul_fast(c, v);
+    img[dst] = pr;
+    if (k) img[I.prod(row, k)] = pr;
   }
   __syncthreads();
   // prefix sums along each row

@@ -363,9 +363,9 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
+            hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess;
+  ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+       hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_pos, &I->ev_tab})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t& e : I->ev_gather) {
@@ -718,11 +718,12 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     HIPCHK(hipEventRecord(I->ev_pos, st));
     // BabyJubJub emitter behind the SHA emitters; of the chain's tail emitters, the Poseidon blocks go
     // behind the signature emitters and the small regions / flow / checks behind the SHA emitters
-    // (default, "split": 70.7k vs 68.3k / 69.0k witnesses/s for all-on-sha / all-on-emit, tuning switch
-    // PZK_TAIL=sha|emit|split, profiles/README.md)
+    // (default, "split": 70.7k vs 68.3k / 69.0k witnesses/s for all-on-sha / all-on-emit; "rsa", the tail on
+    // the RSA stream, equals split; tuning switch PZK_TAIL=sha|emit|split|rsa, profiles/README.md)
     static const char* tail_env = getenv("PZK_TAIL");
-    static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0 : 2;
-    hipStream_t s_tail = tail_mode == 1 ? s_emit : s_sha, s_pos = tail_mode == 0 ? s_sha : s_emit;
+    static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0
+                                 : !strcmp(tail_env, "rsa") ? 3 : 2;
+    hipStream_t s_tail = tail_mode == 1 ? s_emit : tail_mode == 3 ? s_rsa : s_sha, s_pos = tail_mode == 0 ? s_sha : s_emit;
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_sha))) return rc;
     HIPCHK(hipStreamWaitEvent(s_pos, I->ev_pos, 0));

@@ -18,8 +18,20 @@ same files to pin it. Layout of the DER (ICAO 9303-10 §4.6.2, RFC 5652):
 import hashlib
 
 from .field import SplitMix64
-from .inputs import (BP256, P256, EcKey, RsaKey, _dg15_rsa1024, _mrz_dg1, pkcs1v15_sha1_sign, pkcs1v15_sha256_sign,
-                     pss_sign)
+from .inputs import (BP256, P256, Curve, EcKey, RsaKey, _dg15_rsa1024, _mrz_dg1, pkcs1v15_sha1_sign,
+                     pkcs1v15_sha256_sign, pss_sign)
+
+# secp521r1 (SEC 2 2.6.1): a named-curve key the reference recognises by name (getSigType :230, 66-bit chunks)
+P521 = Curve("secp521r1", p=2 ** 521 - 1, a=2 ** 521 - 4,
+             b=int("0051953EB9618E1C9A1F929A21A0B68540EEA2DA725B99B315F3B8B489918EF109E156193951EC7E937B1652C0BD3BB1BF07"
+                   "3573DF883D2C34F1EF451FD46B503F00", 16),
+             n=int("01FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFA51868783BF2F966B7FCC0148F709A5D03BB5C9B8"
+                   "899C47AEBB6FB71E91386409", 16),
+             g=(int("00C6858E06B70404E9CD9E3ECB662395B4429C648139053FB521F828AF606B4D3DBAA14B5E77EFE75928FE1DC127A2FFA8DE3348"
+                    "B3C1856A429BF97E7E31C2E5BD66", 16),
+                int("011839296A789A3BC0045C8A5FB42C7D1BD998F54449579B446817AFBD17273E662C97EE72995EF42640C550B9013FAD0761353C"
+                    "7086A272C24088BE94769FD16650", 16)))
+CURVE_OID = {"prime256v1": "1.2.840.10045.3.1.7", "secp521r1": "1.3.132.0.35"}
 
 OID = {
     "sha1": "1.3.14.3.2.26", "sha224": "2.16.840.1.101.3.4.2.4", "sha256": "2.16.840.1.101.3.4.2.1",
@@ -132,6 +144,13 @@ def ec_spki(curve, q):
     return seq(seq(oid(OID["ecPublicKey"]), params), bitstring(point(q)))
 
 
+def ec_spki_named(curve_name, curve, q):
+    """Named-curve EC key: the parameters are an OID (extract_ecdsa_pubkey then takes the OID's name, :449-451)."""
+    L = (curve.p.bit_length() + 7) // 8
+    return seq(seq(oid(OID["ecPublicKey"]), oid(CURVE_OID[curve_name])),
+               bitstring(b"\x04" + _fixed(q[0], L) + _fixed(q[1], L)))
+
+
 def certificate(spki, sig_alg, rng):
     tbs = seq(ctx(0, integer(2)), integer(1 + rng.below(1 << 62)), sig_alg, name_(b"CSCA"),
               seq(tlv(0x17, b"230101000000Z"), tlv(0x17, b"330101000000Z")), name_(b"DS"), spki)
@@ -157,7 +176,7 @@ SIG_KIND = {  # SIGNATURE_TYPE -> (key, sa / ec hash bits, scheme, salt)
     1: ("rsa2048", 256, "pkcs1", 0), 2: ("rsa4096", 256, "pkcs1", 0), 3: ("rsa2048", 160, "pkcs1", 0),
     10: ("rsa2048e3", 256, "pss", 32), 11: ("rsa2048", 256, "pss", 32), 12: ("rsa2048", 256, "pss", 64),
     13: ("rsa2048", 384, "pss", 48), 14: ("rsa3072", 256, "pss", 32), 20: ("p256", 256, "ecdsa", 0),
-    21: ("bp256", 256, "ecdsa", 0),
+    21: ("bp256", 256, "ecdsa", 0), 27: ("p521", 256, "ecdsa", 0),
 }
 
 
@@ -168,13 +187,19 @@ def signer_key(sig, seed=5, k=0):
         return EcKey(rng, P256)
     if kind == "bp256":
         return EcKey(rng, BP256)
+    if kind == "p521":
+        return EcKey(rng, P521)
     bits = {"rsa2048": 2048, "rsa2048e3": 2048, "rsa4096": 4096, "rsa3072": 3072}[kind]
     return RsaKey(bits, rng, 3 if kind == "rsa2048e3" else 65537)
 
 
-def make_passport(sig, key, index, seed=5, dg_hash=None, n_dgs=5, dg15=True, td1=False, signing_time=True):
+def make_passport(sig, key, index, seed=5, dg_hash=None, n_dgs=5, dg15=True, td1=False, signing_time=True,
+                  named_curve=None, pss_salt_param=True, odd_dg1=False):
     """One synthetic passport: {dg1, dg15, sod} bytes plus the values the SOD carries (for checks).
-    DG1 is hashed first in the LDS object and DG15 (when present) last, DGs 2, 11, 12, 14 between."""
+    DG1 is hashed first in the LDS object and DG15 (when present) last, DGs 2, 11, 12, 14 between.
+    Edge layouts: named_curve (an EC key named by OID), pss_salt_param=False (RSASSA-PSS parameters
+    without saltLength), odd_dg1 (a DG11 hash first, then a DG2 entry whose 33-byte value holds DG1's
+    digest one hex digit in: the reference's string search finds it there, a half-byte shift)."""
     _, hbits, scheme, salt = SIG_KIND[sig]
     dg_hash = dg_hash or hbits
     rng = SplitMix64((seed << 40) ^ (0x534F4450 + index))
@@ -185,16 +210,24 @@ def make_passport(sig, key, index, seed=5, dg_hash=None, n_dgs=5, dg15=True, td1
     others = [(n, rng.bytes(64 + rng.below(64))) for n in (2, 11, 12, 14)][:max(0, n_dgs - 1 - (1 if dg15 else 0))]
     dgs = [(1, dg1)] + others + ([(15, d15)] if dg15 else [])
     ec = lds_security_object(dg_hash, dgs)
+    if odd_dg1:
+        h = HASH_NAME[dg_hash]
+        crafted = bytes.fromhex("0" + hashlib.new(h, dg1).hexdigest() + "0")
+        rows = [seq(integer(11), octets(hashlib.new(h, others[0][1] if others else b"").digest())),
+                seq(integer(2), octets(crafted))] + [seq(integer(n), octets(hashlib.new(h, d).digest())) for n, d in dgs]
+        ec = seq(integer(0), alg(h), seq(*rows))
     sa = signed_attributes(ec, hbits, b"240101120000Z" if signing_time else None)
     hf = getattr(hashlib, HASH_NAME[hbits])
     if scheme == "ecdsa":
         r, s = key.sign(sa, rng)
-        sig_field, spki, sig_alg = seq(integer(r), integer(s)), ec_spki(key.curve, key.q), alg("ecdsaWithSHA256", b"")
+        spki = ec_spki_named(named_curve, key.curve, key.q) if named_curve else ec_spki(key.curve, key.q)
+        sig_field, sig_alg = seq(integer(r), integer(s)), alg("ecdsaWithSHA256", b"")
         signature = (r, s)
     else:
         if scheme == "pss":
             signature = pss_sign(key, sa, rng.bytes(salt), hf)
-            sig_alg = pss_alg(hbits, salt)
+            sig_alg = pss_alg(hbits, salt) if pss_salt_param else alg("rsassaPss", seq(
+                ctx(0, alg(HASH_NAME[hbits])), ctx(1, alg("mgf1", alg(HASH_NAME[hbits])))))
         else:
             signature = (pkcs1v15_sha1_sign if hbits == 160 else pkcs1v15_sha256_sign)(key, sa)
             sig_alg = alg("sha1WithRSAEncryption" if hbits == 160 else "sha256WithRSAEncryption")

@@ -24,6 +24,10 @@ CASES = [
     (1, 0, {}), (1, 1, {"n_dgs": 4}), (1, 2, {"dg15": False, "n_dgs": 3}), (1, 3, {"signing_time": False}),
     (1, 4, {"td1": True}), (1, 5, {"dg_hash": 224}), (3, 0, {}), (10, 0, {}), (11, 0, {}), (12, 0, {}),
     (13, 0, {"n_dgs": 3}), (20, 0, {}), (21, 0, {}), (20, 1, {"dg15": False}),
+    # quirk paths: a key named by OID (P-256: getSigType 0; secp521r1: SIG 27, 66-bit chunks), PSS parameters
+    # without saltLength (the salt reads "(2 elem)": SIG 0), a digest found at an odd hex digit, RSA-4096 / 3072
+    (20, 2, {"named_curve": "prime256v1"}), (27, 0, {"named_curve": "secp521r1"}), (11, 1, {"pss_salt_param": False}),
+    (1, 6, {"odd_dg1": True}), (2, 0, {}), (14, 0, {}),
 ]
 
 

@@ -395,6 +395,8 @@ def report(args, r, world):
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
         "phases": phases,
     }
+    if world == 1 and not args.no_cpu and args.workload.startswith("register") and sig in (1, 3, 10, 11, 12, 20, 21):
+        out["input_side"] = input_side(sig)
     if world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
         procs = max(1, min(CPU_SHARE, os.cpu_count() or 1))
         if args.workload.startswith("register"):
@@ -422,6 +424,30 @@ def report(args, r, world):
             "cores_note": "%d = the host CPU share of a one-GPU job on the GPU box (its OMP_NUM_THREADS); "
                           "the box's nproc counts the whole machine" % CPU_SHARE}
     return out
+
+
+def input_side(sig, distinct=128, n=8192):
+    """The input step before the hot path, on the host: EF.SOD files -> this instance's
+    input rows with the bulk preprocessor (pzk_passport_inputs) on the host CPU share, rows written into
+    resident memory. Reported beside the line; the reference's per-passport processPassport takes ~22 ms
+    (Node 12, profiles/r2_passport_preprocessor.json)."""
+    from pzkwit import passport as PP, sodgen
+    t0 = time.perf_counter()
+    key = sodgen.signer_key(sig)
+    uniq = [sodgen.make_passport(sig, key, i) for i in range(distinct)]
+    gen_s = time.perf_counter() - t0
+    params = PP.parse(uniq[0])["params"]
+    src = PP.sources([uniq[i % distinct] for i in range(n)])
+    rows, _ = PP.input_rows(params, uniq[:1])
+    rows = np.ones((n,) + rows.shape[1:], dtype=np.uint8)  # resident pages
+    t0 = time.perf_counter()
+    rows, st = PP.input_rows(params, src, threads=CPU_SHARE, out=rows)
+    dt = time.perf_counter() - t0
+    return {"what": "EF.SOD + DG1 + DG15 -> input rows (pzk_passport_inputs, include/pzkpassport.h)",
+            "passports_per_s": round(n / dt, 1), "threads": CPU_SHARE, "passports": n, "ok": int((st == 0).sum()),
+            "row_bytes": int(rows[0].nbytes), "params": params,
+            "sample": "%d distinct synthetic SOD passports (pzkwit/sodgen.py, SIGNATURE_TYPE %d; %.1fs to make) repeated"
+                      % (distinct, sig, gen_s)}
 
 
 # ----------------------------------------------------------------------------- config 5

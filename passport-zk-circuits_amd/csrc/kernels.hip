@@ -486,14 +486,18 @@ hipError_t launch_bjj_table(fr* table, hipStream_t st) {
 
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st) {
-  const uint32_t lanes = vs.batch * BJJ_SEGS;
-  hipLaunchKernelGGL(k_bjj_core, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
+  // PZK_BJJ_SEGS (8 / 16 / 32): lanes per witness, for tuning runs (runtime.cpp validates the value)
+  static const int segs = getenv("PZK_BJJ_SEGS") ? atoi(getenv("PZK_BJJ_SEGS")) : BJJ_SEGS_DEFAULT;
+  const uint32_t lanes = vs.batch * segs;
+  auto kern = segs == 8 ? k_bjj_core<8> : segs == 32 ? k_bjj_core<32> : k_bjj_core<16>;
+  hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
   return hipGetLastError();
 }
 
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st) {
-  hipLaunchKernelGGL(k_smt_prep, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, inputs, vs, smt_core, status, vs.batch);
+  hipLaunchKernelGGL(k_smt_prep, dim3((vs.batch * SMT_PREP_LANES + 63) / 64), dim3(64), 0, st, L, inputs, vs, smt_core, status,
+                     vs.batch);
   return hipGetLastError();
 }
 

@@ -188,11 +188,13 @@ struct RegInfo {
 constexpr int MM_CORE_WORDS(int K) { return 12 * K - 3; }  // x[K] y[K] q[K+1] r[K] inv[K](4 words) carry[2K-2](2 words)
 constexpr int BJJ_STEPS = 254;
 constexpr int BJJ_EMIT_STEPS = 32;                           // ladder steps per k_emit_bjj work item
-constexpr int BJJ_SEGS = 8, BJJ_SEG_LEN = 32;                // k_bjj_core: 8 lanes per witness, 32 steps each
+constexpr int BJJ_SCRATCH_STEPS = 256;                       // k_bjj_core: SEGS lanes per witness x 256 / SEGS steps
+constexpr int BJJ_SEGS_DEFAULT = 32;                        // A/B 8 / 16 / 32: 2.00 / 1.47 / 1.22 ms per 2048 witnesses
 constexpr int BJJ_TABLE_WINDOWS = 32;                        // fixed-base table: 32 windows x 256 x (x, y, t2d)
-constexpr int BJJ_SCRATCH_FR = 9 * BJJ_SEG_LEN * BJJ_SEGS;   // per witness
+constexpr int BJJ_SCRATCH_FR = 9 * BJJ_SCRATCH_STEPS;        // per witness, for any segment count
 constexpr int BJJ_CORE_FR = 5 * BJJ_STEPS;                  // per step: Dx, Dy, Ax, Ay, inv(Dx)   (Montgomery)
 constexpr int SMT_LEVELS = 80;
+constexpr int SMT_PREP_LANES = 8;                           // k_smt_prep: lanes per witness (10 levels each)
 constexpr int SMT_CORE_FR = 3 * SMT_LEVELS + 2;             // inv(sibling), root, flags per level; j; inv(root-root0)
 
 constexpr int POS_MAX_T = 6;

@@ -498,20 +498,25 @@ __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
 
 // BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171): MSB-first double-and-add over
 // the 254 bits of sk with the (0,0) sentinel for "no point yet". The ladder is cut into BJJ_SEGS
-// segments of BJJ_SEG_LEN steps, one lane each (8 adjacent lanes = one witness): a segment
+// segments of BJJ_SEG_LEN steps, one lane each (BJJ_SEGS adjacent lanes = one witness): a segment
 // starts from A_{i0-1} = (sk >> (254 - i0)) * Base8, summed from the fixed-base table, so the
 // segments run in parallel. The affine outputs need 1/Z of every point (and 1/x of every D):
 // one batched inversion per witness, whose single Fr inversion is shared by the 8 lanes
 // through wave shuffles.
-// scratch: SoA [elem][lane], 9 * BJJ_SEG_LEN elements per lane (X,Y,Z of D and A, 3 prefixes)
+// scratch: SoA [elem][lane], 9 * SEG_LEN elements per lane (X,Y,Z of D and A, 3 prefixes).
+// SEGS (8 / 16 / 32 lanes per witness, SEG_LEN = 256 / SEGS steps each) trades the segment-start
+// table sums (up to i0 / 8 affine additions) against ladder length and occupancy.
+template <int BJJ_SEGS>
 __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, const fr* table, fr* bjj_core,
                                                 fr* scratch, uint32_t batch) {
+  constexpr int BJJ_SEG_LEN = BJJ_SCRATCH_STEPS / BJJ_SEGS;
+  static_assert(64 % BJJ_SEGS == 0 && BJJ_SEG_LEN * BJJ_SEGS >= BJJ_STEPS, "segments must cover the ladder");
   core_priority();
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nlanes = batch * BJJ_SEGS;
   const uint32_t w = tid / BJJ_SEGS;
   const int seg = (int)(tid % BJJ_SEGS);
-  if (w >= batch) return;  // whole 8-lane groups only (64 % BJJ_SEGS == 0)
+  if (w >= batch) return;  // whole lane groups only (64 % BJJ_SEGS == 0)
   BjjConsts C;
   C.init();
   const int NS = BJJ_STEPS;
@@ -551,7 +556,7 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
     if (have) { S(o) = A.X; S(o + 1) = A.Y; S(o + 2) = A.Z; }
     else { S(o) = fr_zero(); S(o + 1) = fr_zero(); S(o + 2) = fr_zero(); }
   }
-  // batched inversion of Z(D_i), Z(A_i), X(D_i) over the segment, then across the 8 lanes
+  // batched inversion of Z(D_i), Z(A_i), X(D_i) over the segment, then across the BJJ_SEGS lanes
   auto elem = [&](int qi) -> fr {
     int j = qi / 3, kind = qi - 3 * j;
     return kind == 0 ? S(3 * j + 2) : kind == 1 ? S(3 * BJJ_SEG_LEN + 3 * j + 2) : S(3 * j);
@@ -590,63 +595,101 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
 // ============================================================================ SMT
 // flags per level (u32 in the SMT core): bit0 levIns, bit1 done, bit2 st_top, bit3 st_inew, bit4 lrbit, bit5 isZero
 // SMT core (Fr): [inv(sibling) normal][80] [root Montgomery][80] [flags][80] [j, inv(root_in - root_0)]
-__global__ void __launch_bounds__(64, 1) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
-                           uint32_t batch) {
+// SMT_PREP_LANES lanes per witness, SMT_LEVELS / SMT_PREP_LANES levels each: the sibling inverses
+// are one batched inversion per witness (segment prefix products per lane, the segment totals
+// combined by shuffles, one Fr inversion shared by the group, as in k_bjj_core); the SMTLevIns /
+// SMTVerifierSM chains are integer recurrences over the 80 isZero bits, which every lane of the
+// group rebuilds from the gathered bit mask and writes for its own levels.
+__global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core,
+                                                int32_t* status, uint32_t batch) {
   core_priority();
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= batch) return;
+  constexpr int G = SMT_PREP_LANES, NL = SMT_LEVELS / SMT_PREP_LANES;
+  static_assert(SMT_LEVELS % SMT_PREP_LANES == 0 && 64 % SMT_PREP_LANES == 0 && NL <= 32, "level split");
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = tid / G;
+  const int seg = (int)(tid % G), i0 = seg * NL;
+  if (w >= batch) return;  // whole lane groups only
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;
   uint32_t* flags = reinterpret_cast<uint32_t*>(core + 2 * SMT_LEVELS);
-  fr key = fr_from_mont(vs.at(R.v_pkhash, w));
-  int iz[SMT_LEVELS];
+  const fr key = fr_from_mont(vs.at(R.v_pkhash, w));
   // inverses of the siblings (SMTLevIns isZero, SMTVerifier.circom:47-50), batched
+  fr sm[NL];
+  uint32_t zmask = 0;  // bit k: sibling i0 + k is zero
   fr acc = fr_mont_one();
-  for (int i = 0; i < SMT_LEVELS; i++) {
-    fr s = load_fr(row + 32ull * (R.in_br + i));
-    iz[i] = fr_is_zero(s);
-    core[i] = acc;
-    if (!iz[i]) acc = fr_mul(acc, fr_to_mont(s));
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    const fr sn = load_fr(row + 32ull * (R.in_br + i0 + k));
+    const bool z = fr_is_zero(sn);
+    zmask |= (uint32_t)z << k;
+    sm[k] = fr_to_mont(sn);
+    core[i0 + k] = acc;
+    if (!z) acc = fr_mul(acc, sm[k]);
   }
-  fr inv = fr_inv(acc);
-  for (int i = SMT_LEVELS - 1; i >= 0; i--) {
+  fr others = fr_mont_one(), total = fr_mont_one();
+#pragma unroll
+  for (int t = 0; t < G; t++) {
+    const fr pt = fr_shfl(acc, t, G);
+    total = fr_mul(total, pt);
+    if (t != seg) others = fr_mul(others, pt);
+  }
+  fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
+#pragma unroll
+  for (int k = NL - 1; k >= 0; k--) {
     fr r = fr_zero();
-    if (!iz[i]) {
-      fr sm = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
-      r = fr_mul(inv, core[i]);
-      inv = fr_mul(inv, sm);
+    if (!((zmask >> k) & 1)) { r = fr_mul(inv, core[i0 + k]); inv = fr_mul(inv, sm[k]); }
+    core[i0 + k] = fr_from_mont(r);
+  }
+  // the group's isZero bits, levels 0..79
+  uint32_t zm[G];
+#pragma unroll
+  for (int t = 0; t < G; t++) zm[t] = (uint32_t)__shfl((int)zmask, t, G);
+  auto iz = [&](int i) -> int {
+    int r = 0;
+#pragma unroll
+    for (int t = 0; t < G; t++) r |= (i / NL == t) ? (int)((zm[t] >> (i - t * NL)) & 1u) : 0;
+    return r;
+  };
+  if (seg == G - 1 && !iz(SMT_LEVELS - 1)) set_status(status ? status + w : nullptr, ST_SMT_LAST);
+  // SMTLevIns (SMTVerifier.circom:39-65): done[i-1] = lev[i] + done[i], from the top
+  uint32_t levm[3] = {0, 0, 0}, donem[3] = {0, 0, 0};
+  auto setb = [](uint32_t* m, int i, int v) { m[i >> 5] |= (uint32_t)(v & 1) << (i & 31); };
+  auto getb = [](const uint32_t* m, int i) -> int { return (int)((m[i >> 5] >> (i & 31)) & 1u); };
+  {
+    int lev = 1 - iz(SMT_LEVELS - 2), done = lev;  // lev[79], done[78]
+    setb(levm, SMT_LEVELS - 1, lev);
+    setb(donem, SMT_LEVELS - 2, done);
+    for (int i = SMT_LEVELS - 2; i > 0; i--) {
+      lev = (1 - done) * (1 - iz(i - 1));
+      setb(levm, i, lev);
+      done = lev + done;  // done[i - 1]
+      setb(donem, i - 1, done);
     }
-    core[i] = fr_from_mont(r);
+    setb(levm, 0, 1 - done);
   }
-  if (!iz[SMT_LEVELS - 1]) set_status(status ? status + w : nullptr, ST_SMT_LAST);
-  // SMTLevIns (SMTVerifier.circom:39-65)
-  int lev[SMT_LEVELS], done[SMT_LEVELS];
-  lev[SMT_LEVELS - 1] = 1 - iz[SMT_LEVELS - 2];
-  done[SMT_LEVELS - 2] = lev[SMT_LEVELS - 1];
-  done[SMT_LEVELS - 1] = 0;
-  for (int i = SMT_LEVELS - 2; i > 0; i--) {
-    lev[i] = (1 - done[i]) * (1 - iz[i - 1]);
-    done[i - 1] = lev[i] + done[i];
-  }
-  lev[0] = 1 - done[0];
   // SMTVerifierSM chain and the insertion level j
   int prev_top = 1, j = SMT_LEVELS;
   for (int i = 0; i < SMT_LEVELS; i++) {
-    int st_inew = prev_top * lev[i], st_top = prev_top - st_inew;
+    const int lv = getb(levm, i), st_inew = prev_top * lv, st_top = prev_top - st_inew;
     if (st_inew) j = i;
-    int lr = (key.v[i >> 5] >> (i & 31)) & 1;
-    flags[i] = (uint32_t)(lev[i] & 1) | ((uint32_t)(done[i] & 1) << 1) | ((uint32_t)(st_top & 1) << 2) |
-               ((uint32_t)(st_inew & 1) << 3) | ((uint32_t)lr << 4) | ((uint32_t)iz[i] << 5);
+    if (i >= i0 && i < i0 + NL) {
+      const int lr = (key.v[i >> 5] >> (i & 31)) & 1;
+      flags[i] = (uint32_t)lv | ((uint32_t)getb(donem, i) << 1) | ((uint32_t)(st_top & 1) << 2) |
+                 ((uint32_t)(st_inew & 1) << 3) | ((uint32_t)lr << 4) | ((uint32_t)iz(i) << 5);
+    }
     prev_top = st_top;
   }
-  reinterpret_cast<uint32_t*>(core + 3 * SMT_LEVELS)[0] = (uint32_t)j;
+  if (seg == 0) reinterpret_cast<uint32_t*>(core + 3 * SMT_LEVELS)[0] = (uint32_t)j;
   // level hashes whose child is 0 (i >= j): inputs known now
-  for (int i = (j < SMT_LEVELS ? j : 0); i < SMT_LEVELS; i++) {
-    fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
-    int lr = (flags[i] >> 4) & 1;
-    vs.at(R.v_smt_lr + 2 * i, w) = lr ? sib : fr_zero();
-    vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? fr_zero() : sib;
+  const int from = j < SMT_LEVELS ? j : 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    const int i = i0 + k;
+    if (i < from) continue;
+    const int lr = (key.v[i >> 5] >> (i & 31)) & 1;
+    vs.at(R.v_smt_lr + 2 * i, w) = lr ? sm[k] : fr_zero();
+    vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? fr_zero() : sm[k];
   }
 }
 

@@ -314,6 +314,10 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
     int v = atoi(u);
     if (v != 8 && v != 16 && v != 32) return fail(PZK_E_ARG, std::string("PZK_SHA_U=") + u + ": valid values are 8, 16, 32");
   }
+  if (const char* u = getenv("PZK_BJJ_SEGS")) {  // tuning switch of k_bjj_core (kernels.hip)
+    int v = atoi(u);
+    if (v != 8 && v != 16 && v != 32) return fail(PZK_E_ARG, std::string("PZK_BJJ_SEGS=") + u + ": valid values are 8, 16, 32");
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(PZK_E_NODEVICE, "no HIP device visible: pzkwit has no CPU fallback");

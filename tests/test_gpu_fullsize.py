@@ -1,6 +1,7 @@
-"""GPU, full size: the config-3 workload (BASELINE.json configs[1]) of 4096 canonical
+"""GPU, full size: the config-3 workload (BASELINE.json configs[2]) of 4096 canonical
 RegisterIdentityBuilder passports, run through the device-resident C-ABI path the way bench.py runs it
-(sub-batches into one reused output slab), here with a ragged sub-batch of 1500 (1500, 1500, 1096 rows:
+(sub-batches into one reused output slab), and one GPU's 4096-row shard of config 4 (deep SMT
+proofs), here with a ragged sub-batch of 1500 (1500, 1500, 1096 rows:
 none a multiple of the 16-witness RSA groups or the 64-lane waves). The oracle cannot check 4096 rows of
 72 MB in seconds, so the full batch is checked through size-independent properties:
 
@@ -24,12 +25,19 @@ pytestmark = pytest.mark.gpu
 
 BATCH, DISTINCT, SUB = 4096, 1024, 1500
 
+# config 3: shallow SMT proofs (depth 0..8); config 4 (BASELINE.json configs[3], "registerIdentity +
+# depth-80 Sparse Merkle inclusion, batch 32768 over 8 GPUs"): one GPU's 4096-row shard of it, with
+# proofs of depth 40..79, so every lane walks the upper half of SMTVerifier(80) up to its last level
+FULLSIZE = {"config3": (3, lambda i: i % 9), "config4_shard": (4, lambda i: 40 + i % 40)}
 
-def test_config3_fullsize_properties(oracle):
+
+@pytest.mark.parametrize("config", sorted(FULLSIZE))
+def test_fullsize_properties(oracle, config):
     import torch
     params = I.CANONICAL
-    g = I.PassportGen(seed=3, n_keys=8, params=params, workers=1)
-    pps = [g.passport_at(i, smt_depth=i % 9) for i in range(DISTINCT)]
+    seed, depth = FULLSIZE[config]
+    g = I.PassportGen(seed=seed, n_keys=8, params=params, workers=1)
+    pps = [g.passport_at(i, smt_depth=depth(i)) for i in range(DISTINCT)]
     rows = np.stack([I.pack_register_inputs(pp, params) for pp in pps])
     inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params)
     W, NIN = inst.witness_size, inst.n_inputs

@@ -503,7 +503,7 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, hipStream_t st) {
-  hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
+  hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
                      smt_core, vs.batch);
   return hipGetLastError();
 }

@@ -194,6 +194,7 @@ constexpr int BJJ_TABLE_WINDOWS = 32;                        // fixed-base table
 constexpr int BJJ_SCRATCH_FR = 9 * BJJ_SCRATCH_STEPS;        // per witness, for any segment count
 constexpr int BJJ_CORE_FR = 5 * BJJ_STEPS;                  // per step: Dx, Dy, Ax, Ay, inv(Dx)   (Montgomery)
 constexpr int SMT_LEVELS = 80;
+constexpr int SMT_CHAIN_LANES = 4;                          // k_smt_chain: lanes per witness (one PoseidonHash(2) group)
 constexpr int SMT_PREP_LANES = 8;                           // k_smt_prep: lanes per witness (10 levels each)
 constexpr int SMT_CORE_FR = 3 * SMT_LEVELS + 2;             // inv(sibling), root, flags per level; j; inv(root-root0)
 

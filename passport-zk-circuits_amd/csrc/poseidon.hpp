@@ -104,7 +104,8 @@ __device__ __forceinline__ void pos_core_lane(const PosConsts& K, const PosTask&
   vs.at(task.out_slot, w) = h;
 }
 
-// Cooperative permutation: G lanes per (witness, task), lane j < t holds state element j
+// Cooperative permutation: G lanes per (witness, task), lane j < t holds state element j; returns
+// the hash to every lane of the group
 // (G = 4 for t <= 4, 8 otherwise; the lanes j >= t carry zeros). A full round is one S-box per
 // lane and a t-term mix gathered with shuffles; a partial round is lane 0's S-box, one product
 // per lane and a butterfly sum. Same core output as pos_core_lane (Montgomery layer states,
@@ -112,7 +113,7 @@ __device__ __forceinline__ void pos_core_lane(const PosConsts& K, const PosTask&
 // one lane per permutation and ~70 VGPRs instead of 256, so the kernel can be placed next to
 // the emitters.
 template <int T, int G>
-__device__ __forceinline__ void pos_core_group(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
+__device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
                                                fr* core /* this witness's Poseidon core */, int j) {
   constexpr int t = T;
   const int RP = pos_nrp(t);
@@ -170,6 +171,7 @@ __device__ __forceinline__ void pos_core_group(const PosConsts& K, const PosTask
   if (act) out[o + j] = st;  // Z3
   fr h = group_sum(act ? fr_mul(K.M(t, jj, 0), pow5(st)) : fr_zero());
   if (j == 0) vs.at(task.out_slot, w) = h;
+  return h;  // every lane of the group holds the hash (Montgomery)
 }
 
 // ------------------------------------------------------------------------------ emit

@@ -693,27 +693,35 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
   }
 }
 
-// sequential part: levels j-1 .. 0, then all roots and the isEqual inverse
-__global__ void __launch_bounds__(64, 1) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs, ValueStore vs,
-                            fr* pos_core, fr* smt_core, uint32_t batch) {
+// sequential part: levels j-1 .. 0, then all roots and the isEqual inverse. SMT_CHAIN_LANES lanes per
+// witness run each level hash as a cooperative permutation (pos_core_group: lane k < 3 holds state
+// element k); every lane writes the level's two hash inputs itself, so the permutation's input loads
+// read the lane's own stores, and the hash comes back to every lane of the group by its butterfly.
+__global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
+                                                 ValueStore vs, fr* pos_core, fr* smt_core, uint32_t batch) {
   core_priority();
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= batch) return;
+  constexpr int G = SMT_CHAIN_LANES;
+  static_assert(G == 4 && 64 % G == 0, "PoseidonHash(2) groups are 4 lanes (t = 3)");
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = tid / G;
+  const int jl = (int)(tid % G);
+  if (w >= batch) return;  // whole lane groups only
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;
   const uint32_t* flags = reinterpret_cast<const uint32_t*>(core + 2 * SMT_LEVELS);
-  int j = (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0];
-  fr leaf = vs.at(R.v_leaf, w);
+  const int j = (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0];
+  const fr leaf = vs.at(R.v_leaf, w);
   fr child = leaf;  // root_j = leaf
+  fr* pcore = pos_core + (size_t)w * L.pos_core_elems;
   for (int i = (j < SMT_LEVELS ? j : SMT_LEVELS) - 1; i >= 0; i--) {
-    fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
-    int lr = (flags[i] >> 4) & 1;
+    const fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
+    const int lr = (flags[i] >> 4) & 1;
     vs.at(R.v_smt_lr + 2 * i, w) = lr ? sib : child;
     vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? child : sib;
-    pos_core_lane<3>(K, L.pos[level_task[i]], vs, w, pos_core + (size_t)w * L.pos_core_elems);
-    child = vs.at(R.v_smt_h + i, w);  // root_i = H_i (st_top = 1 below the insertion level)
+    child = pos_core_group<3, G>(K, L.pos[level_task[i]], vs, w, pcore, jl);  // root_i = H_i (st_top = 1 below j)
   }
+  if (jl != 0) return;  // lane 0 wrote every level hash this kernel made (pos_core_group's out_slot store)
   // roots of every level: root_i = st_top_i * H_i + st_inew_i * leaf (SMTVerifier.circom:104-106)
   fr* roots = core + SMT_LEVELS;
   for (int i = 0; i < SMT_LEVELS; i++) {

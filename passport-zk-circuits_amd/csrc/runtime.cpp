@@ -699,10 +699,13 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if ((rc = emit(E_SHA, s_sha))) return rc;
     if ((rc = emit(E_SHA1, s_sha))) return rc;  // SHA-1 hashers (SIGNATURE_TYPE 3, DG_HASH_TYPE 160)
     if ((rc = emit(E_SHA5, s_sha))) return rc;  // SHA-384/512 hashers (standalone circuits)
-    // signature emitters: BigMultModP blocks / EC table blocks, PSS derived hashers, on the RSA stream right
-    // behind the chain they read, so they overlap the SHA emitters instead of queueing behind the previous
-    // call's Poseidon emitters (config 3: 71.21k vs 70.75k witnesses/s; tuning switch PZK_SIGEMIT=emit)
-    static const bool sig_on_rsa = !(getenv("PZK_SIGEMIT") && !strcmp(getenv("PZK_SIGEMIT"), "emit"));
+    // signature emitters: BigMultModP blocks / EC table blocks, PSS derived hashers. RSA instances: on the
+    // RSA stream right behind the chain they read, so they overlap the SHA emitters instead of queueing
+    // behind the previous call's Poseidon emitters (config 3: 71.21k vs 70.75k witnesses/s). ECDSA
+    // instances: on the emit stream, because there the next call's EC core (a long chain) would queue
+    // behind this call's EC table emitter. Tuning switch PZK_SIGEMIT=rsa|emit forces one placement.
+    static const char* se_env = getenv("PZK_SIGEMIT");
+    const bool sig_on_rsa = se_env ? strcmp(se_env, "emit") != 0 : !lay.is_ecdsa;
     hipStream_t s_sig = sig_on_rsa ? s_rsa : s_emit;
     HIPCHK(hipStreamWaitEvent(s_sig, I->ev_rsa, 0));
     if ((rc = emit(E_MM, s_sig))) return rc;

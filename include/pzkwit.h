@@ -40,9 +40,12 @@ enum {
 typedef struct pzk_params {
   int32_t circuit;            /* PZK_CIRCUIT_* */
   int32_t size_arg;           /* n for POSEIDON, blocks for SHA256 / SHA1 / SHA384 / SHA512; ignored for REGISTER */
-  int32_t signature_type;     /* SIGNATURE_TYPE (1 = RSA-2048/SHA-256/65537, 2 = RSA-4096, 10-12 = RSA-2048
-                                 PSS/SHA-256 (10: e = 3), 20 = ECDSA secp256r1/SHA-256) */
-  int32_t dg_hash_type;       /* DG_HASH_TYPE (256) */
+  int32_t signature_type;     /* SIGNATURE_TYPE (signatureVerification.circom:9-127): 1 = RSA-2048 PKCS#1 v1.5
+                                 SHA-256 e = 65537, 2 = RSA-4096, 3 = RSA-2048 SHA-1, 4 = RSA-3072 SHA-1
+                                 e = 37187; 10-12 = RSA-2048 PSS SHA-256 (10: e = 3; 12: salt 64), 13 = RSA-2048
+                                 PSS SHA-384 (salt 48), 14 = RSA-3072 PSS SHA-256; 20 = ECDSA secp256r1,
+                                 21 = ECDSA brainpoolP256r1 (SHA-256). Others: PZK_E_PARAMS */
+  int32_t dg_hash_type;       /* DG_HASH_TYPE (160, 224, 256, 384) */
   int32_t document_type;      /* DOCUMENT_TYPE (1 = TD1, 3 = TD3) */
   int32_t ec_block_number;    /* EC_BLOCK_NUMBER */
   int32_t ec_shift;           /* EC_SHIFT (bits) */
@@ -59,7 +62,8 @@ typedef struct pzk_info {
   uint32_t n_outputs;      /* main outputs (witness[1 .. n_outputs]) */
   uint32_t n_public_inputs;/* public inputs, right after the outputs */
   uint32_t n_input_groups; /* named input signals (see pzk_instance_input) */
-  uint32_t reserved;
+  uint32_t pipeline_depth; /* calls in flight with a NULL stream: call k + pipeline_depth starts after call k
+                              has completed (pzk_witness_batch) */
 } pzk_info;
 
 typedef struct pzk_exec {
@@ -146,8 +150,11 @@ int pzk_wtns_header(const pzk_instance* inst, uint8_t header[76]);
  *              multiple of 16), device pointer
  *   d_status : batch x int32 lane status (PZK_ST_*), device pointer (may be NULL)
  * The buffers must stay untouched until the call has completed (see pzk_exec.stream). With a NULL
- * stream consecutive calls overlap: call k + 1's cores run beside call k's emitters (two scratch
- * sets); call k + 2 starts after call k has completed.
+ * stream consecutive calls overlap: the instance keeps pzk_info.pipeline_depth (3) scratch sets, call
+ * k uses set k mod 3, so calls k, k + 1 and k + 2 may run at the same time (call k + 1's cores beside
+ * call k's emitters) and call k + 3 starts after call k has completed. A caller that reuses call k's
+ * d_inputs / d_wtns / d_status for a later call must therefore either give the later call an index
+ * >= k + 3 or synchronise first (pzk_instance_sync, PZK_EXEC_SYNC, or a stream).
  * Replaces: for (input of inputs) await wc.calculateWitness(input) (automatisationTest.js:24-50). */
 int pzk_witness_batch(pzk_instance* inst, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns,
                       size_t wtns_stride, int32_t* d_status, const pzk_exec* exec);

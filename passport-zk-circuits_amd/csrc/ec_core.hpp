@@ -182,9 +182,9 @@ struct EcTabCtx {
     if (t.w[0] | t.w[1]) fail(ST_BIGISZERO);
     return i_shr64(t);
   }
-  __device__ V inv_fr(const V& d) const {
-    fr x = fr_to_mont(i_as_fr(i_to_fr(d)));
-    fr y = fr_from_mont(fr_inv(x));
+  __device__ V inv_fr(const V& d) const {  // FIPS products: 64 independent lanes per wave, one op each
+    fr x = fr_mul_fast(i_as_fr(i_to_fr(d)), fr_const(R2_));
+    fr y = fr_from_mont_fast(fr_inv<true>(x));
     I256 r;
     for (int i = 0; i < 8; i++) r.w[i] = y.v[i];
     return r;
@@ -808,7 +808,7 @@ __global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_i
   } else {
     d = fr_diff_u64(dx, C[ECC_SM_AP + 8 * (j - ECI_SM_ZA + 1)]);
   }
-  ec_inv[(size_t)w * EC_N_INV + j] = fr_is_zero(d) ? d : fr_from_mont(fr_inv(fr_to_mont(d)));
+  ec_inv[(size_t)w * EC_N_INV + j] = fr_is_zero(d) ? d : fr_from_mont_fast(fr_inv<true>(fr_mul_fast(d, fr_const(R2_))));
 }
 
 // ============================================================ k_ec_table: lane per (witness, op)

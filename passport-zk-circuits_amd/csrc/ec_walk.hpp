@@ -18,20 +18,28 @@
 namespace pzk {
 inline namespace PZK_EC_NS {
 
+// Every walker function is force-inlined, so on the device each k_ec_table<TYPE> holds only its own
+// type's walk and no callable function exists. A callable walker (what hipcc chose on its own: one
+// ~46 k-instruction function shared by the three types) needs long branches, and ROCm 7.2's branch
+// relaxation may expand them with s[30:31] — the function's unsaved return address — as the scratch
+// pair; the walker then "returns" into its own body (the round-2 P-256 hang / brainpool fault,
+// DESIGN.md §4.8; tools/check_code_objects.py checks every built code object for this).
+#define PZK_WALK __host__ __device__ __attribute__((always_inline)) inline
+
 template <class C>
 struct EcWalk {
   using V = typename C::V;
   C& c;
-  __host__ __device__ explicit EcWalk(C& ctx) : c(ctx) {}
+  PZK_WALK explicit EcWalk(C& ctx) : c(ctx) {}
 
   // Num2Bits(L) bitify.circom:10-32: out[L] | in | sum[L]   (v already in the table)
-  __host__ __device__ void n2b(uint32_t b, const V& v, int L) {
+  PZK_WALK void n2b(uint32_t b, const V& v, int L) {
     c.bits(b, v, L);
     c.cp(b + L, v);
     c.masks(b + L + 1, v, L);
   }
   // Num2Bits(L) whose input is a fresh value
-  __host__ __device__ V n2b_new(uint32_t b, const V& x, int L) {
+  PZK_WALK V n2b_new(uint32_t b, const V& x, int L) {
     V v = c.put(b + L, x);
     c.bits(b, v, L);
     c.masks(b + L + 1, v, L);
@@ -44,7 +52,7 @@ struct EcWalk {
   // in the column that consumes it.
   // f(i, out[i]) is called per output column, so callers can consume columns without an array
   template <class F>
-  __host__ __device__ void bmneq_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
+  PZK_WALK void bmneq_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
     const uint32_t i1 = b + G + L - 1, i2 = i1 + G, tm = i2 + L, tr = tm + G * L;
     for (int i = 0; i < G; i++) c.cp(i1 + i, in1[i]);
     for (int j = 0; j < L; j++) c.cp(i2 + j, in2[j]);
@@ -61,28 +69,28 @@ struct EcWalk {
       f(i, s);
     }
   }
-  __host__ __device__ void bmneq(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+  PZK_WALK void bmneq(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
     bmneq_cb(b, G, L, in1, in2, [&](int i, const V& s) { out[i] = s; });
   }
   // BigMultOverflow(G,L) bigIntOverflow.circom:38-72 (schoolbook for these sizes):
   // out[G+L-1] | in1[G], in2[L] | mult
   template <class F>
-  __host__ __device__ void bmo_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
+  PZK_WALK void bmo_cb(uint32_t b, int G, int L, const V* in1, const V* in2, F f) {
     for (int i = 0; i < G; i++) c.cp(b + G + L - 1 + i, in1[i]);
     for (int j = 0; j < L; j++) c.cp(b + 2 * G + L - 1 + j, in2[j]);
     bmneq_cb(b + 2 * G + 2 * L - 1, G, L, in1, in2, [&](int i, const V& s) { c.cp(b + i, s); f(i, s); });
   }
-  __host__ __device__ void bmo(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+  PZK_WALK void bmo(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
     bmo_cb(b, G, L, in1, in2, [&](int i, const V& s) { out[i] = s; });
   }
   // ScalarMultOverflow(N) bigIntOverflow.circom:101-111: out[N] | in[N], scalar
-  __host__ __device__ void smo(uint32_t b, int N, const V* in, uint64_t k, V* out) {
+  PZK_WALK void smo(uint32_t b, int N, const V* in, uint64_t k, V* out) {
     for (int i = 0; i < N; i++) c.cp(b + N + i, in[i]);
     V kv = c.put(b + 2 * N, c.u64(k));
     for (int i = 0; i < N; i++) out[i] = c.put(b + i, c.mul(kv, in[i]));
   }
   // BigAddOverflow(G,L) bigIntOverflow.circom:22-35: out[G] | in1[G], in2[L]
-  __host__ __device__ void bao(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
+  PZK_WALK void bao(uint32_t b, int G, int L, const V* in1, const V* in2, V* out) {
     for (int i = 0; i < G; i++) c.cp(b + G + i, in1[i]);
     for (int j = 0; j < L; j++) c.cp(b + 2 * G + j, in2[j]);
     for (int i = 0; i < G; i++) {
@@ -91,7 +99,7 @@ struct EcWalk {
     }
   }
   // BigSubModOverflow(N) bigIntOverflow.circom:78-98: out[N] | in1[N], in2[N], modulus[N]
-  __host__ __device__ void bsmo(uint32_t b, const V* in1, const V* in2, const V* mod, V* out) {
+  PZK_WALK void bsmo(uint32_t b, const V* in1, const V* in2, const V* mod, V* out) {
     for (int i = 0; i < 4; i++) { c.cp(b + 4 + i, in1[i]); c.cp(b + 8 + i, in2[i]); c.cp(b + 12 + i, mod[i]); }
     for (int i = 0; i < 4; i++) {
       V v = c.sub(c.add(mod[i], in1[i]), in2[i]);
@@ -101,13 +109,13 @@ struct EcWalk {
     }
   }
   // materialise 4 constant limbs
-  __host__ __device__ void consts4(const uint64_t* k, V* out) {
+  PZK_WALK void consts4(const uint64_t* k, V* out) {
     for (int i = 0; i < 4; i++) out[i] = c.put_hidden(c.u64(k[i]));
   }
 
   // BigIntIsZero(64,MAX,K) bigIntComparators.circom:105-129: in[K] | carry[K-1] | carryRangeChecks[K-1]
   // (in already placed by the caller)
-  __host__ __device__ void bisz(uint32_t b, int MAX, int K, const V* in) {
+  PZK_WALK void bisz(uint32_t b, int MAX, int K, const V* in) {
     const int L = MAX + 3 - 64;
     const uint32_t carry = b + K, sub = carry + K - 1;
     V cy{};
@@ -123,7 +131,7 @@ struct EcWalk {
   // in[CN], modulus[4] | sign, k[DIV] | kRangeChecks[DIV], mult, isZero, swicher[CN]
   // The columns of mult = k * modulus feed the switchers, isZero.in and the carry chain of
   // BigIntIsZero (bigIntComparators.circom:105-129) as they are produced (no column arrays).
-  __host__ __device__ void bizmp(uint32_t b, int MAX, int CN, int MCN, const V* in, const V* mod) {
+  PZK_WALK void bizmp(uint32_t b, int MAX, int CN, int MCN, const V* in, const V* mod) {
     const int DIV = MCN - 3, LB = MAX + 3 - 64;
     const uint32_t o_mod = b + CN, o_sign = o_mod + 4, o_k = o_sign + 1, o_krc = o_k + DIV,
                    o_mult = o_krc + DIV * ec_n2b(64), o_isz = o_mult + ec_bmo(DIV, 4), o_sw = o_isz + ec_bisz(MAX, MCN);
@@ -163,7 +171,7 @@ struct EcWalk {
   }
 
   // PointOnCurve curve.circom:110-138: in[2][4] | squareX, cubeX, squareY, coefMult, isZeroModP
-  __host__ __device__ void poncurve(uint32_t b, const V* pt) {
+  PZK_WALK void poncurve(uint32_t b, const V* pt) {
     for (int i = 0; i < 8; i++) c.cp(b + i, pt[i]);
     const uint32_t sx = b + 8, cx = sx + ec_bmo(4, 4), sy = cx + ec_bmo(7, 4), cm = sy + ec_bmo(4, 4),
                    iz = cm + ec_bmo(4, 4);
@@ -186,7 +194,7 @@ struct EcWalk {
   }
   // PointOnTangent curve.circom:145-197: in1[2][4], in2[2][4] | squareX, scalarMult, bigAdd, bigSub,
   // rightMult, scalarMult2, bigAdd2, leftMult, isZeroModP
-  __host__ __device__ void pontangent(uint32_t b, const V* p1, const V* p2) {
+  PZK_WALK void pontangent(uint32_t b, const V* p1, const V* p2) {
     for (int i = 0; i < 8; i++) { c.cp(b + i, p1[i]); c.cp(b + 8 + i, p2[i]); }
     const uint32_t sx = b + 16, sm = sx + ec_bmo(4, 4), ba = sm + 15, bs = ba + 18, rm = bs + 16, sm2 = rm + ec_bmo(7, 4),
                    ba2 = sm2 + 9, lm = ba2 + 12, iz = lm + ec_bmo(4, 4);
@@ -207,7 +215,7 @@ struct EcWalk {
   }
   // PointOnLine curve.circom:204-245: in1, in2, in3 | bigAdd, bigSub, bigSub2, bigSub3, leftMult,
   // rightMult, isZeroModP
-  __host__ __device__ void ponline(uint32_t b, const V* p1, const V* p2, const V* p3) {
+  PZK_WALK void ponline(uint32_t b, const V* p1, const V* p2, const V* p3) {
     for (int i = 0; i < 8; i++) { c.cp(b + i, p1[i]); c.cp(b + 8 + i, p2[i]); c.cp(b + 16 + i, p3[i]); }
     const uint32_t ba = b + 24, s1 = ba + 12, s2 = s1 + 16, s3 = s2 + 16, lm = s3 + 16, rm = lm + ec_bmo(4, 4),
                    iz = rm + ec_bmo(4, 4);
@@ -223,7 +231,7 @@ struct EcWalk {
   }
 
   // EllipticCurveDouble curve.circom:281-310: out[2][4] | in[2][4] | onTangentCheck, onCurveCheck
-  __host__ __device__ void dbl() {
+  PZK_WALK void dbl() {
     V in[8], out[8];
     for (int i = 0; i < 8; i++) in[i] = c.put(8 + i, c.rec(i));
     for (int i = 0; i < 8; i++) out[i] = c.put(i, c.rec(16 + i));
@@ -231,7 +239,7 @@ struct EcWalk {
     poncurve(16 + EC_SZ_PONTANGENT, out);
   }
   // EllipticCurveAdd curve.circom:314-345: out[2][4] | in1[2][4], in2[2][4] | onCurveCheck, onLineCheck
-  __host__ __device__ void add() {
+  PZK_WALK void add() {
     V in1[8], in2[8], out[8];
     for (int i = 0; i < 8; i++) in1[i] = c.put(8 + i, c.rec(i));
     for (int i = 0; i < 8; i++) in2[i] = c.put(16 + i, c.rec(8 + i));
@@ -241,7 +249,7 @@ struct EcWalk {
   }
 
   // IsEqual comparators.circom:24-33: out | in[2] | IsZero(out, in, inv)
-  __host__ __device__ V isequal(uint32_t b, const V& a, const V& bb) {
+  PZK_WALK V isequal(uint32_t b, const V& a, const V& bb) {
     c.cp(b + 1, a);
     c.cp(b + 2, bb);
     V d = c.put(b + 4, c.sub(bb, a));
@@ -252,7 +260,7 @@ struct EcWalk {
   }
   // BigMultModP(64,4,4,4) bigInt.circom:206-272:
   // div[5], mod[4] | in1[4], in2[4], modulus[4] | mult, modChecks[4], greaterThan, mult2, isZero
-  __host__ __device__ void mm() {
+  PZK_WALK void mm() {
     V x[4], y[4], n[4];
     for (int i = 0; i < 4; i++) x[i] = c.put(9 + i, c.rec(i));
     for (int i = 0; i < 4; i++) y[i] = c.put(13 + i, c.rec(4 + i));
@@ -293,7 +301,7 @@ struct EcWalk {
     bisz(o_isz, 132, 7, iz);
   }
 
-  __host__ __device__ void run(int type) {
+  PZK_WALK void run(int type) {
     if (type == ECT_DBL) dbl();
     else if (type == ECT_ADD) add();
     else mm();

@@ -142,14 +142,15 @@ __device__ __forceinline__ fr fr_from_mont_fast(const fr& a) {
   }
   return fr_reduce_once(r);
 }
-// The general fr_mul / fr_sqr / fr_from_mont below stay operand-scanning CIOS: with the FIPS
-// product inlined, the EC table walker (ec_walk.hpp, EcWalk<EcTabCtx>::run, a ~50 k-instruction
-// callable function) did not terminate on MI355X and the brainpoolP256r1 path faulted, although
-// the FIPS product equals the CIOS one on every input of tools/fieldbench's stress kernel
-// (divergent lanes; product, square, inverse chains). Cause not isolated;
-// the _fast forms are used only where GPU parity tests cover every output element.
+// The general fr_mul / fr_sqr / fr_from_mont below stay operand-scanning CIOS: the latency-bound cores
+// (one wave per SIMD on a dependent chain) run them faster than the FIPS form. (The round-2 "FIPS hang"
+// of the EC table walker was not this product: the walker had become a callable function whose far
+// branches the compiler expanded through its unsaved return-address registers)
 // Montgomery product a*b*2^-256 mod p
 __device__ __forceinline__ fr fr_mul(const fr& a, const fr& b) {
+#ifdef PZK_FR_FIPS_ALL
+  return fr_mul_fast(a, b);
+#endif
   uint32_t t[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) t[j] = 0;
@@ -180,6 +181,9 @@ __device__ __forceinline__ fr fr_mul(const fr& a, const fr& b) {
 // Montgomery square: 28 cross products (doubled) + 8 squares, then REDC — 100 instead of 128
 // 32x32 products (measured 12 % faster than fr_mul(a, a) on MI355X, tools/fieldbench)
 __device__ __forceinline__ fr fr_sqr(const fr& a) {
+#ifdef PZK_FR_FIPS_ALL
+  return fr_mul_fast(a, a);
+#endif
   uint32_t t[16];
 #pragma unroll
   for (int j = 0; j < 16; j++) t[j] = 0;
@@ -224,8 +228,12 @@ __device__ __forceinline__ fr fr_sqr(const fr& a) {
 __device__ __forceinline__ fr fr_to_mont(const fr& a) { return fr_mul(a, fr_const(R2_)); }
 __device__ __forceinline__ fr fr_from_mont(const fr& a) { fr one = fr_zero(); one.v[0] = 1; return fr_mul(a, one); }
 
-// a^(p-2) in Montgomery form; inverse of 0 is 0 (IsZero semantics, comparators.circom:17)
+// a^(p-2) in Montgomery form; inverse of 0 is 0 (IsZero semantics, comparators.circom:17).
+// FAST = the FIPS product (throughput form, for kernels with many independent lanes per SIMD)
+template <bool FAST = false>
 __device__ __forceinline__ fr fr_inv(const fr& a) {
+  auto mul = [](const fr& x, const fr& y) { return FAST ? fr_mul_fast(x, y) : fr_mul(x, y); };
+  auto sqr = [](const fr& x) { return FAST ? fr_mul_fast(x, x) : fr_sqr(x); };
   // exponent p-2, scanned MSB->LSB with a 4-bit fixed window (wave-uniform control flow)
   constexpr uint32_t E[8] = {0xefffffffu, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
                              0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
@@ -233,18 +241,18 @@ __device__ __forceinline__ fr fr_inv(const fr& a) {
   tbl[0] = fr_mont_one();
   tbl[1] = a;
 #pragma unroll
-  for (int i = 2; i < 16; i++) tbl[i] = fr_mul(tbl[i - 1], a);
+  for (int i = 2; i < 16; i++) tbl[i] = mul(tbl[i - 1], a);
   fr r = fr_mont_one();
   bool started = false;
   for (int w = 63; w >= 0; w--) {
     uint32_t nib = (E[w >> 3] >> ((w & 7) * 4)) & 15u;
-    if (started) { r = fr_sqr(r); r = fr_sqr(r); r = fr_sqr(r); r = fr_sqr(r); }
+    if (started) { r = sqr(r); r = sqr(r); r = sqr(r); r = sqr(r); }
     if (nib) {
       // select tbl[nib] without dynamic indexing into a register array
       fr s = tbl[0];
 #pragma unroll
       for (int q = 1; q < 16; q++) if ((uint32_t)q == nib) s = tbl[q];
-      r = started ? fr_mul(r, s) : s;
+      r = started ? mul(r, s) : s;
       started = true;
     }
   }

@@ -6,7 +6,6 @@
 #include "poseidon.hpp"
 #include "regcore.hpp"
 #include "pss.hpp"
-#include "rsa_coop.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
 #include "sha1.hpp"
@@ -15,8 +14,6 @@
 #include "kernels.hpp"
 
 namespace pzk {
-
-constexpr int EMIT_THREADS = 256;
 
 // ------------------------------------------------------------------- value loads
 // value-store slot <- input element (normal form -> Montgomery)
@@ -43,42 +40,6 @@ __global__ void __launch_bounds__(64, 1) k_sha_core(const ShaJob* jobs, int n_jo
   if (J.algo == 1) sha1_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
   else if (J.algo >= 3) sha512_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
   else sha_core_lane(row, J, sha_core + (size_t)w * core_words, status ? status + w : nullptr);
-}
-
-// ------------------------------------------------------------------- Poseidon core
-// wave = 64 witnesses of one task. SMT level tasks below the insertion level depend on the
-// chain and are left to k_smt_chain.
-// lane per permutation: for launches with many tasks (the 80 SMT level hashes), where the
-// batch x tasks lanes already fill the chip and the cooperative form only adds shuffles
-template <int T>
-__global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
-                                                  uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
-  core_priority();
-  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= vs.batch) return;
-  const PosTask& task = tasks[blockIdx.y];
-  if (task.smt_level >= 0) {
-    int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
-    if (task.smt_level < jl) return;
-  }
-  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
-}
-
-template <int T>
-__global__ void __launch_bounds__(256) k_pos_core(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
-                                                  uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
-  core_priority();
-  constexpr int G = T <= 4 ? 4 : 8;
-  const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / G;  // (witness) of this lane group
-  const int j = threadIdx.x & (G - 1);
-  const uint32_t w = gid;
-  if (w >= vs.batch) return;  // whole groups (batch rows are group-aligned)
-  const PosTask& task = tasks[blockIdx.y];
-  if (task.smt_level >= 0) {
-    int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
-    if (task.smt_level < jl) return;  // whole group: same witness
-  }
-  pos_core_group<T, G>(K, task, vs, w, pos_core + (size_t)w * core_elems, j);
 }
 
 // ------------------------------------------------------------------- emit: SHA regions
@@ -259,27 +220,6 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha512(DevLayout L, const
   }
 }
 
-// ------------------------------------------------------------------- emit: Poseidon
-template <int T>
-__global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
-                                                          const fr* pos_core, uint8_t* wtns, size_t stride) {
-  constexpr PosImg I(T);
-  __shared__ fr img[I.size];
-  const Work wk = work[blockIdx.x];
-  const uint32_t w = blockIdx.y;
-  const Region R = L.regions[wk.region];
-  const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
-  // the block's descriptors go to LDS first: a global load inside the store loop would wait for
-  // every store in flight (gfx9 vmcnt counts stores too)
-  __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
-  for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
-  pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
-  // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
-  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
-  const uint4* im = reinterpret_cast<const uint4*>(img);
-  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = im[2u * prog[h >> 1] + (h & 1)];
-}
-
 // ------------------------------------------------------------------- emit: generic small regions
 // A work item packs up to GEN_PACK signals from up to GEN_MAX_PIECES region slices (most generic
 // regions are a handful of signals: SMT levels, switchers, IsZero blocks). Thread q finds its
@@ -376,46 +316,6 @@ hipError_t launch_pss(const DevLayout& L, int stage, const uint64_t* rsa_core, c
   return hipGetLastError();
 }
 
-hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
-                           uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, const fr* smt_core,
-                           uint32_t smt_core_fr, hipStream_t st) {
-  // group consecutive tasks of equal t into one launch (blockIdx.y = task)
-  uint32_t i = 0;
-  while (i < count) {
-    int t = h_tasks[first + i].n + 1;
-    uint32_t j = i;
-    while (j < count && h_tasks[first + j].n + 1 == t) j++;
-    const PosTask* tp = d_tasks + first + i;
-    if (j - i >= 8) {  // many tasks: one lane per permutation
-      dim3 g1((vs.batch + 63) / 64, j - i);
-      switch (t) {
-        case 2: hipLaunchKernelGGL(k_pos_core1<2>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-        case 3: hipLaunchKernelGGL(k_pos_core1<3>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-        case 4: hipLaunchKernelGGL(k_pos_core1<4>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-        case 5: hipLaunchKernelGGL(k_pos_core1<5>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-        case 6: hipLaunchKernelGGL(k_pos_core1<6>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-        default: return hipErrorInvalidValue;
-      }
-      HIP_TRY(hipGetLastError());
-      i = j;
-      continue;
-    }
-    const uint32_t G = t <= 4 ? 4 : 8;
-    dim3 g((vs.batch * G + 255) / 256, j - i);
-    switch (t) {
-      case 2: hipLaunchKernelGGL(k_pos_core<2>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 3: hipLaunchKernelGGL(k_pos_core<3>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 4: hipLaunchKernelGGL(k_pos_core<4>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 5: hipLaunchKernelGGL(k_pos_core<5>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      case 6: hipLaunchKernelGGL(k_pos_core<6>, g, dim3(256), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
-      default: return hipErrorInvalidValue;
-    }
-    HIP_TRY(hipGetLastError());
-    i = j;
-  }
-  return hipSuccess;
-}
-
 hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
                        int32_t* status, hipStream_t st) {
   hipLaunchKernelGGL(k_prep, dim3(vs.batch), dim3(64), 0, st, L, inputs, sha_core, vs, status);
@@ -427,55 +327,6 @@ hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uin
   if (!status) return hipSuccess;
   hipLaunchKernelGGL(k_rsa_check, dim3((batch + 63) / 64), dim3(64), 0, st, L, inputs, sha_core, rsa_core, status,
                      batch);
-  return hipGetLastError();
-}
-
-// RSA core: the cooperative Barrett kernel (rsa_coop.hpp) by default; PZK_RSA_CORE=lane selects
-// the one-lane-per-witness Knuth D kernel (regcore.hpp) for A/B measurements.
-template <int K, int G>
-static hipError_t launch_rsa_core2(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, int32_t* status,
-                                   uint32_t batch, hipStream_t st) {
-  constexpr int WPB = 64 / G;
-  const size_t lds = sizeof(uint64_t) * rsa2_lds_words<K>() * WPB;
-  HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core2<K, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((k_rsa_core2<K, G>), dim3((batch + WPB - 1) / WPB), dim3(64), lds, st, L, inputs, rsa_core, status,
-                     batch);
-  return hipGetLastError();
-}
-
-template <int K, int NL>
-static hipError_t launch_rsa_lane(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
-                                  int32_t* status, uint32_t batch, hipStream_t st) {
-  const size_t lds = sizeof(uint64_t) * rsa_lds_words<K>() * NL;
-  HIP_TRY(hipFuncSetAttribute((const void*)k_rsa_core<K, NL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((k_rsa_core<K, NL>), dim3((batch + NL - 1) / NL), dim3(NL), lds, st, L, inputs, rsa_core, colsum,
-                     status, batch);
-  return hipGetLastError();
-}
-
-static bool rsa_core_lane() {
-  static const int v = [] {
-    const char* e = getenv("PZK_RSA_CORE");
-    return e && e[0] == 'l' ? 1 : 0;
-  }();
-  return v;
-}
-
-hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* rsa_core, uint64_t* colsum,
-                           int32_t* status, uint32_t batch, hipStream_t st) {
-  const bool lane = rsa_core_lane() && colsum;
-  if (L.reg.K == 48) {  // RSA-3072 (SIGNATURE_TYPE 14): cooperative core only
-    HIP_TRY((launch_rsa_core2<48, 16>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<48>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
-  } else if (L.reg.K == 32) {
-    HIP_TRY((lane ? launch_rsa_lane<32, 64>(L, inputs, rsa_core, colsum, status, batch, st)
-                  : launch_rsa_core2<32, 8>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<32>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
-  } else {
-    HIP_TRY((lane ? launch_rsa_lane<64, 32>(L, inputs, rsa_core, colsum, status, batch, st)
-                  : launch_rsa_core2<64, 16>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<64>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
-  }
   return hipGetLastError();
 }
 
@@ -532,23 +383,10 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
                          B.stride, 1);
       break;
     }
-    case E_POS:  // one launch per width (runtime.cpp groups the work by t); max_t = that width
-      switch (max_t) {
-        case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-        case 3: hipLaunchKernelGGL(k_emit_pos<3>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-        case 4: hipLaunchKernelGGL(k_emit_pos<4>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-        case 5: hipLaunchKernelGGL(k_emit_pos<5>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-        case 6: hipLaunchKernelGGL(k_emit_pos<6>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-        default: return hipErrorInvalidValue;
-      }
-      break;
+    case E_POS: return launch_emit_pos(L, work, n_work, K, B, batch, max_t, st);  // one launch per width (kernels_pos.hip)
     case E_BITS: hipLaunchKernelGGL(k_emit_bits, g, blk, 0, st, L, work, B); break;
     case E_FLOW: hipLaunchKernelGGL(k_emit_flow, g, blk, 0, st, L, work, B); break;
-    case E_MM:
-      if (L.reg.K == 32) hipLaunchKernelGGL(k_emit_mm<32>, g, blk, 0, st, L, work, B);
-      else if (L.reg.K == 48) hipLaunchKernelGGL(k_emit_mm<48>, g, blk, 0, st, L, work, B);
-      else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
-      break;
+    case E_MM: return launch_emit_mm(L, work, n_work, B, batch, st);  // kernels_rsa.hip
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
     case E_SHA5:
     case E_SHA5D:

@@ -8,6 +8,8 @@
 
 namespace pzk {
 
+constexpr int EMIT_THREADS = 256;  // emit kernels' workgroup size
+
 struct ValueLoad {
   int32_t slot;    // value-store slot
   int32_t in_off;  // input element offset
@@ -50,6 +52,10 @@ hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uin
 hipError_t launch_inv_small(fr* out, hipStream_t st);
 hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st);
+hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,
+                           uint32_t batch, int t, hipStream_t st);
+hipError_t launch_emit_mm(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                          hipStream_t st);
 hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,
                        const Bufs& B, uint32_t batch, int max_t, hipStream_t st);
 

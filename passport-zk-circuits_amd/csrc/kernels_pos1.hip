@@ -1,0 +1,42 @@
+// Poseidon permutation core, one lane per permutation (launches with many tasks of one width: the SMT
+// level hashes), and its launcher; own translation unit so it compiles in parallel with kernels_pos.hip.
+#include <hip/hip_runtime.h>
+
+#define PZK_TEMPLATE_KERNELS_ONLY
+#include "bufs.hpp"
+#include "poseidon.hpp"
+#include "kernels.hpp"
+
+namespace pzk {
+
+// lane per permutation: for launches with many tasks (the 80 SMT level hashes), where the
+// batch x tasks lanes already fill the chip and the cooperative form only adds shuffles
+template <int T>
+__global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
+                                                  uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
+  core_priority();
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= vs.batch) return;
+  const PosTask& task = tasks[blockIdx.y];
+  if (task.smt_level >= 0) {
+    int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
+    if (task.smt_level < jl) return;
+  }
+  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
+}
+
+hipError_t launch_pos_core1(int t, const PosConsts& K, const PosTask* tp, uint32_t n_tasks, ValueStore vs, fr* pos_core,
+                            uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr, hipStream_t st) {
+  dim3 g1((vs.batch + 63) / 64, n_tasks);
+  switch (t) {
+    case 2: hipLaunchKernelGGL(k_pos_core1<2>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+    case 3: hipLaunchKernelGGL(k_pos_core1<3>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+    case 4: hipLaunchKernelGGL(k_pos_core1<4>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+    case 5: hipLaunchKernelGGL(k_pos_core1<5>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+    case 6: hipLaunchKernelGGL(k_pos_core1<6>, g1, dim3(64), 0, st, K, tp, vs, pos_core, core_elems, smt_core, smt_core_fr); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pzk

@@ -1,0 +1,49 @@
+// PoseidonHash block emitter (k_emit_pos<t>, t = 2..6) and its launcher. Own translation unit (template
+// kernels only from the shared headers), so it compiles in parallel with the other kernel units.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#define PZK_TEMPLATE_KERNELS_ONLY
+#include "bufs.hpp"
+#include "poseidon.hpp"
+#include "kernels.hpp"
+
+namespace pzk {
+
+// ------------------------------------------------------------------- emit: Poseidon
+template <int T>
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
+                                                          const fr* pos_core, uint8_t* wtns, size_t stride) {
+  constexpr PosImg I(T);
+  __shared__ fr img[I.size];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
+  // the block's descriptors go to LDS first: a global load inside the store loop would wait for
+  // every store in flight (gfx9 vmcnt counts stores too)
+  __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
+  for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
+  pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+  // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
+  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
+  const uint4* im = reinterpret_cast<const uint4*>(img);
+  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = im[2u * prog[h >> 1] + (h & 1)];
+}
+
+hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,
+                           uint32_t batch, int t, hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  dim3 g(n_work, batch), blk(EMIT_THREADS);
+  switch (t) {
+    case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 3: hipLaunchKernelGGL(k_emit_pos<3>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 4: hipLaunchKernelGGL(k_emit_pos<4>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 5: hipLaunchKernelGGL(k_emit_pos<5>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 6: hipLaunchKernelGGL(k_emit_pos<6>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pzk

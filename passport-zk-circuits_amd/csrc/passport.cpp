@@ -328,7 +328,13 @@ struct Tree {
     return true;
   }
   int bad(const char* why) { err = why; return -1; }
-  int decode(int64_t& pos) {
+  // Nesting cap: the input is untrusted DER, and every walk over the tree (decode, content_ok, the key
+  // and digest searches) recurses per level. asn1.js has no cap of its own (it throws a RangeError when
+  // the JS stack runs out); real EF.SOD files nest < 20 levels, so anything past 64 is rejected here
+  // instead of overflowing a host thread's stack.
+  static constexpr int MAX_DEPTH = 64;
+  int decode(int64_t& pos, int depth = 0) {
+    if (depth > MAX_DEPTH) return bad("ASN.1 nesting deeper than 64 levels");
     Node x{};
     x.start = pos;
     uint8_t t;
@@ -371,14 +377,14 @@ struct Tree {
         const int64_t end = start + len;
         if (end > n) { err = "Container has a length past the end of the stream"; return false; }
         while (pos < end) {
-          const int s = decode(pos);
+          const int s = decode(pos, depth + 1);
           if (s < 0) return false;
           sub.push_back(s);
         }
         if (pos != end) { err = "Content size is not correct for container"; return false; }
       } else {
         for (;;) {
-          const int s = decode(pos);
+          const int s = decode(pos, depth + 1);
           if (s < 0) return false;
           if (is_eoc(nodes[s])) break;
           sub.push_back(s);

@@ -84,6 +84,7 @@ __device__ __forceinline__ PssView pss_view(const DevLayout& L, const uint64_t* 
 }
 
 // derived row of a witness: MGF1 block c at elements [BS c, BS c + BS), M' at [BS n_mgf, + 1024)
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_pss_mgf(DevLayout L, const uint64_t* rsa_core, const uint32_t* sha_core,
                                                  uint8_t* derived) {
   const uint32_t w = blockIdx.y;
@@ -93,7 +94,9 @@ __global__ void __launch_bounds__(256) k_pss_mgf(DevLayout L, const uint64_t* rs
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x)
     store_u64(row + 32ull * e, P.mgf_msg_bit(e / bs, e % bs));
 }
+#endif
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_pss_mdash(DevLayout L, const uint64_t* rsa_core, const uint32_t* sha_core,
                                                    uint8_t* derived) {
   const uint32_t w = blockIdx.y;
@@ -102,6 +105,7 @@ __global__ void __launch_bounds__(256) k_pss_mdash(DevLayout L, const uint64_t* 
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 1024; e += gridDim.x * blockDim.x)
     store_u64(row + 32ull * e, P.mdash_bit(e));
 }
+#endif
 
 // lane checks of VerifyRsaPssSig (called from k_rsa_check)
 __device__ __forceinline__ void pss_check(const PssView& P, int32_t* status) {

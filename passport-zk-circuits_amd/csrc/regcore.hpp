@@ -43,6 +43,7 @@ __device__ __forceinline__ fr wave_bits_fr(const uint8_t* row, int base, int L, 
   return v;
 }
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs, int32_t* status) {
   core_priority();
   const uint32_t w = blockIdx.x;
@@ -107,6 +108,7 @@ __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs,
   }
   if (__ballot(bad) && lane == 0) set_status(status ? status + w : nullptr, ST_INPUT_RANGE);
 }
+#endif
 
 // ============================================================================ RSA core
 
@@ -380,6 +382,7 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
 constexpr uint64_t RSA_EM4 = 217300885422736416ull, RSA_EM5 = 938447882527703397ull;  // rsa.circom:53-54
 constexpr uint64_t RSA_EM6 = 0xFFFFFFFF00303130ull;  // num2bits_6: remainsBits (rsa.circom:59-62), ones (:65-67)
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
                                                   const uint64_t* rsa_core, int32_t* status, uint32_t batch) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -426,6 +429,7 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
   }
   if (gt_bad) lane_status(status + w, ST_BIGMOD_GT);
 }
+#endif
 
 // ============================================================================ BabyJubJub core
 // twisted Edwards a x^2 + y^2 = 1 + d x^2 y^2, a = 168700, d = 168696 (babyjubjub/curve.circom:62-70)
@@ -475,6 +479,7 @@ __device__ __forceinline__ ExtPt bjj_add(const ExtPt& P, const ExtPt& Q, const B
   return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
 }
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (w, v)
   if (idx >= BJJ_TABLE_WINDOWS * 256) return;
@@ -494,6 +499,7 @@ __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
   fr x = fr_mul(acc.X, zi), y = fr_mul(acc.Y, zi);
   out[0] = x; out[1] = y; out[2] = fr_mul(fr_mul(C.D, x), y);
 }
+#endif
 
 
 // BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171): MSB-first double-and-add over
@@ -600,6 +606,7 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
 // combined by shuffles, one Fr inversion shared by the group, as in k_bjj_core); the SMTLevIns /
 // SMTVerifierSM chains are integer recurrences over the 80 isZero bits, which every lane of the
 // group rebuilds from the gathered bit mask and writes for its own levels.
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core,
                                                 int32_t* status, uint32_t batch) {
   core_priority();
@@ -692,11 +699,13 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
     vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? fr_zero() : sm[k];
   }
 }
+#endif
 
 // sequential part: levels j-1 .. 0, then all roots and the isEqual inverse. SMT_CHAIN_LANES lanes per
 // witness run each level hash as a cooperative permutation (pos_core_group: lane k < 3 holds state
 // element k); every lane writes the level's two hash inputs itself, so the permutation's input loads
 // read the lane's own stores, and the hash comes back to every lane of the group by its butterfly.
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
                                                  ValueStore vs, fr* pos_core, fr* smt_core, uint32_t batch) {
   core_priority();
@@ -736,5 +745,6 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
   fr dlt = fr_sub(rin, roots[0]);
   core[3 * SMT_LEVELS + 1] = fr_inv(dlt);
 }
+#endif
 
 }  // namespace pzk

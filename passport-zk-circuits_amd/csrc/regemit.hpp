@@ -227,6 +227,7 @@ __device__ __forceinline__ W256 alias_sig(const W256& V, const uint64_t* sout, u
   return w_mask(so, (int)s - 135);
 }
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint32_t val[8];
   __shared__ uint64_t sout[3];
@@ -299,8 +300,10 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
     return el_w(w_mask(V, (int)(s - Lb)));
   });
 }
+#endif
 
 // ------------------------------------------------------------------ PassportVerificationFlow
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint8_t eq[3 * 512 + 8], chain[3 * 512 + 8];  // 3 DG + 8 IsEqual, DG <= 512
   __shared__ fr invV;  // 1 / DG15_VERIFICATION (normal form): IsZero inverses of the scaled DG15 checks
@@ -362,6 +365,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
     return d >= 0 ? el_fr(m) : el_fr(fr_sub(fr_zero(), m));
   });
 }
+#endif
 
 // ------------------------------------------------------------------ BigMultModP
 // Karatsuba input table (K = 32): the in1/in2 values of every non-root KaratsubaOverflow node
@@ -744,6 +748,7 @@ enum BjjRec { BR_X1, BR_Y1, BR_OX, BR_OY, BR_INV, BR_X1Y2, BR_Y1X2, BR_DELTA, BR
 __device__ __forceinline__ uint32_t bjj_step_of(uint32_t s) { return s < 46 ? 0 : 1 + (s - 46) / 60; }
 __device__ __forceinline__ uint32_t bjj_sig_of(uint32_t i) { return i == 0 ? 0 : 46 + 60 * (i - 1); }
 
+#ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
   __shared__ fr rec[(BJJ_EMIT_STEPS + 1) * BR_N];
   __shared__ uint32_t bits[BJJ_EMIT_STEPS + 1];
@@ -860,5 +865,6 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
     return el_fr(res);
   });
 }
+#endif
 
 }  // namespace pzk

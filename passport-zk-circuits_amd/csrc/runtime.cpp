@@ -303,6 +303,26 @@ static void free_all(pzk_instance* I) {
   I->timing.destroy();
 }
 
+// The caller's current device is switched to the instance's for the duration of a call and
+// restored on return (every stream, event and buffer of an instance lives on its device).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// wait until every stream of the instance has drained (all calls issued so far are complete)
+static int sync_all(pzk_instance* I) {
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit})
+    if (s) HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
 extern "C" {
 
 const char* pzk_last_error(void) { return g_err.c_str(); }
@@ -390,7 +410,8 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
 
 // circom .sym text ("signal_idx,witness_idx,component_idx,name" per line; witness_idx -1 = eliminated)
 // -> inv[k] = O0 index of output witness element k (inv[0] = 0, the constant 1). Signal indices are the
-// --O0 numbering (1 .. o0_size - 1); witness indices must cover 1 .. max exactly once.
+// --O0 numbering (1 .. o0_size - 1); witness indices must cover 1 .. max, each by one or
+// more signals (several signals on one index: the lowest signal index is emitted).
 static bool parse_sym(const char* text, size_t len, uint64_t o0_size, std::vector<uint32_t>& inv, std::string& why) {
   std::vector<int64_t> w_of;  // witness index -> signal index
   size_t i = 0;
@@ -420,8 +441,9 @@ static bool parse_sym(const char* text, size_t len, uint64_t o0_size, std::vecto
     if (wit == -1) continue;
     if (wit < 1) { why = "sym line " + std::to_string(line) + ": bad witness index"; return false; }
     if ((uint64_t)wit >= w_of.size()) w_of.resize(wit + 1, -1);
-    if (w_of[wit] != -1) { why = "sym: witness index " + std::to_string(wit) + " assigned twice"; return false; }
-    w_of[wit] = sig;
+    // circom's simplification can merge equal signals onto one witness index (snarkjs loadSymbols joins
+    // their names with '|'): they carry one value, so the lowest signal index stands for all of them
+    if (w_of[wit] == -1 || sig < w_of[wit]) w_of[wit] = sig;
   }
   if (w_of.size() < 2) { why = "sym: no signal is kept"; return false; }
   inv.assign(w_of.size(), 0);
@@ -491,7 +513,14 @@ int pzk_layout_region(const pzk_params* params, uint32_t i, uint64_t* off, uint3
 
 void pzk_instance_destroy(pzk_instance* inst) {
   if (!inst) return;
-  free_all(inst);
+  {
+    // calls are asynchronous across the instance's streams: wait for a concurrent caller to leave and
+    // for every call in flight to drain, on the instance's device, before anything is freed
+    std::lock_guard<std::mutex> lock(inst->mu);
+    DeviceGuard dg(inst->device);
+    (void)sync_all(inst);
+    free_all(inst);
+  }
   delete inst;
 }
 
@@ -503,6 +532,7 @@ int pzk_instance_info(const pzk_instance* I, pzk_info* info) {
   info->n_outputs = I->lay.n_outputs;
   info->n_public_inputs = I->lay.n_public;
   info->n_input_groups = (uint32_t)I->lay.inputs.size();
+  info->pipeline_depth = NSETS;
   return 0;
 }
 
@@ -557,29 +587,10 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
   return 0;
 }
 
-// The caller's current device is switched to the instance's for the duration of a call and
-// restored on return (every stream, event and buffer of an instance lives on its device).
-struct DeviceGuard {
-  int prev = -1;
-  hipError_t err = hipSuccess;
-  explicit DeviceGuard(int dev) {
-    err = hipGetDevice(&prev);
-    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
-    else prev = -1;
-  }
-  ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
-};
-
 static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
   if (exec && exec->device >= 0 && exec->device != I->device)
     return fail(PZK_E_ARG, "pzk_exec.device " + std::to_string(exec->device) + " != the instance's device " +
                                std::to_string(I->device) + " (create one instance per device)");
-  return 0;
-}
-
-// wait until every stream of the instance has drained (all calls issued so far are complete)
-static int sync_all(pzk_instance* I) {
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit}) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 

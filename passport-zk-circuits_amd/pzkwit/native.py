@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libpzkwit.so")
+# PZK_LIB selects another build of the same library (A/B builds under tools/gpu); default: the in-tree one
+LIB_PATH = os.environ.get("PZK_LIB") or os.path.join(PKG, "lib", "libpzkwit.so")
 
 PZK_CIRCUIT_REGISTER, PZK_CIRCUIT_POSEIDON, PZK_CIRCUIT_SHA256, PZK_CIRCUIT_SHA1 = 0, 1, 2, 3
 PZK_CIRCUIT_SHA384, PZK_CIRCUIT_SHA512 = 4, 5
@@ -45,7 +46,7 @@ class PzkParams(ctypes.Structure):
 class PzkInfo(ctypes.Structure):
     _fields_ = [("witness_size", ctypes.c_uint64), ("n_inputs", ctypes.c_uint64), ("n_outputs", ctypes.c_uint32),
                 ("n_public_inputs", ctypes.c_uint32), ("n_input_groups", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("pipeline_depth", ctypes.c_uint32)]
 
 
 class PzkExec(ctypes.Structure):

@@ -9,13 +9,19 @@ can be dropped in where circom is available (none is here: SURVEY.md §8c).
 import numpy as np
 
 
-def sym_text(keep, names=None):
+def sym_text(keep, names=None, merged=None):
     """keep: bool array over the O0 signals (index 0 = the constant 1, ignored). Kept signals get
-    witness indices 1, 2, ... in O0 order."""
+    witness indices 1, 2, ... in O0 order. merged: optional bool array; a merged signal that is not kept
+    shares the witness index of the closest kept signal before it (circom's simplification maps equal
+    signals onto one witness index; snarkjs loadSymbols joins their names with '|')."""
     keep = np.asarray(keep, dtype=bool)
     wit = np.full(keep.shape[0], -1, dtype=np.int64)
     idx = np.flatnonzero(keep[1:]) + 1
     wit[idx] = np.arange(1, idx.size + 1)
+    if merged is not None:
+        last = np.maximum.accumulate(np.where(keep, np.arange(keep.shape[0]), 0))
+        m = np.asarray(merged, dtype=bool) & ~keep & (last > 0)
+        wit[m] = wit[last[m]]
     lines = ["%d,%d,0,%s" % (s, wit[s], names[s] if names else "s%d" % s) for s in range(1, keep.shape[0])]
     return "\n".join(lines) + "\n"
 
@@ -27,10 +33,8 @@ def parse_sym(text):
         if not ln.strip():
             continue
         sig, wit = (int(x) for x in ln.split(",")[:2])
-        if wit >= 0:
-            if wit in pairs:
-                raise ValueError("witness index %d assigned twice" % wit)
-            pairs[wit] = sig
+        if wit >= 0:  # several signals on one index: the lowest signal index stands for them (runtime.cpp parse_sym)
+            pairs[wit] = min(sig, pairs.get(wit, sig))
     n = max(pairs) + 1
     inv = np.zeros(n, dtype=np.int64)
     for k in range(1, n):

@@ -145,3 +145,16 @@ def test_wtns_header_layout():
     # construct expected with a host-side writer and compare against the library's layout rules
     assert struct.calcsize("<4sII") + struct.calcsize("<IQI32sI") + struct.calcsize("<IQ") == 76
     assert P.to_bytes(32, "little")[:4] == bytes([0x01, 0x00, 0x00, 0xF0])
+
+
+def test_code_objects_keep_return_addresses():
+    """Every gfx950 code object in libpzkwit.so: no callable device function overwrites its return
+    address (s[30:31]) before saving it. ROCm 7.2's branch relaxation can expand a far branch of a large
+    callable function through those registers; the function then returns into its own body. This was the
+    round-2 EC table walker hang / illegal access: the walker is force-inlined now, and
+    this check keeps any later large callable function from reintroducing it."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import check_code_objects
+    assert os.path.exists(native.LIB_PATH)
+    assert check_code_objects.check(native.LIB_PATH) == []

@@ -216,7 +216,14 @@ def test_sym_map_validation():
     assert native.sym_check(I.CANONICAL, txt) == int(keep[1:].sum()) + 1
     inv = symmap.parse_sym(txt)
     assert inv.shape[0] == int(keep[1:].sum()) + 1 and (np.diff(inv[1:]) > 0).all()
-    for bad, msg in [("1,1,0,a\n2,1,0,b\n", "assigned twice"), ("1,2,0,a\n", "not assigned"),
+    # signals merged onto one witness index (circom --O1/--O2): accepted, the size is the number of indices
+    merged = symmap.synthetic_keep(n_o0, 0, fraction=3, salt=0x77)
+    txt2 = symmap.sym_text(keep, merged=merged)
+    assert native.sym_check(I.CANONICAL, txt2) == int(keep[1:].sum()) + 1
+    inv2 = symmap.parse_sym(txt2)
+    assert (inv2 == inv).all()  # each index keeps its lowest signal
+    assert native.sym_check(I.CANONICAL, "1,1,0,a\n2,1,0,b\n3,2,0,c\n") == 3
+    for bad, msg in [("1,2,0,a\n", "not assigned"),
                      ("%d,1,0,a\n" % n_o0, "outside"), ("x,1,0,a\n", "expected"), ("1,-1,0,a\n", "no signal")]:
         with pytest.raises(native.PzkError, match=msg):
             native.sym_check(I.CANONICAL, bad)

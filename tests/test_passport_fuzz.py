@@ -72,3 +72,40 @@ def test_mutated_sods_under_sanitizers(fuzz_bin):
         if want is not None:
             assert got == want
     assert sum(x == "err" for x in lines) > len(lines) // 4  # the mutations do reach the rejection paths
+
+
+def _der_len(n):
+    if n < 0x80:
+        return bytes([n])
+    b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([0x80 | len(b)]) + b
+
+
+def test_deeply_nested_der_is_rejected(fuzz_bin):
+    """Untrusted DER nested far past any real EF.SOD (definite and indefinite lengths, nested
+    constructed BIT STRINGs / OCTET STRINGs, and an encapsulation chain of primitive OCTET STRINGs
+    each holding the next) must be rejected by the nesting cap, not overflow the parser's stack."""
+    blobs = []
+    for depth in (100, 5000, 50000):
+        blobs.append(b"\x30\x80" * depth + b"\x00\x00" * depth)          # indefinite SEQUENCEs
+        blobs.append(b"\x23\x80" * depth + b"\x00\x00" * depth)          # constructed BIT STRINGs
+        blobs.append(b"\x24\x80" * depth + b"\x00\x00" * depth)          # constructed OCTET STRINGs
+        inner = b"\x05\x00"
+        for _ in range(min(depth, 2000)):                                 # definite SEQUENCEs
+            inner = b"\x30" + _der_len(len(inner)) + inner
+        blobs.append(inner)
+        inner = b"\x05\x00"
+        for _ in range(min(depth, 2000)):                                 # encapsulated OCTET STRINGs
+            inner = b"\x04" + _der_len(len(inner)) + inner
+        blobs.append(inner)
+    c = CASES[0]
+    dg1 = base64.b64decode(c["dg1"])
+    data = b"".join(record(dg1, b"", sod) for sod in blobs) + b"".join(record(dg1, sod, base64.b64decode(c["sod"]))
+                                                                       for sod in blobs[:5])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([fuzz_bin], input=data, capture_output=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"runtime error" not in r.stderr and b"ERROR: AddressSanitizer" not in r.stderr, r.stderr.decode()[-3000:]
+    lines = r.stdout.decode().splitlines()
+    assert len(lines) == len(blobs) + 5
+    assert all(x == "err" for x in lines), lines

@@ -454,12 +454,60 @@ def input_side(sig, distinct=128, n=8192):
 MIX = ((1, 0.4), (2, 0.3), (20, 0.3))  # RSA-2048 / RSA-4096 / ECDSA secp256r1
 
 
+def _mixed_plan(per_gpu, world):
+    """Deterministic config-5 job (every rank derives the same): flow of each of the world x per_gpu
+    witnesses (seed 5), the flows' instance parameters, and each rank's cost-balanced contiguous shard."""
+    from pzkwit import inputs as I, mixed
+    total = per_gpu * world
+    rng = np.random.default_rng(5)
+    sigs = rng.choice([m[0] for m in MIX], size=total, p=[m[1] for m in MIX])
+    flows = {sg: dict(I.CANONICAL, sig=int(sg)) for sg, _ in MIX}
+    costs = [mixed.witness_cost(flows[int(sg)]) for sg in sigs]
+    shards = [mixed.shard_by_cost(costs, world, r) for r in range(world)]
+    return sigs, flows, costs, shards
+
+
+def _mixed_groups(sigs, lo, hi):
+    """A shard's witnesses grouped per flow (MIX order), each group in global order: {sig: [index]}"""
+    groups = {}
+    for sg, _ in MIX:
+        idx = [i for i in range(lo, hi) if int(sigs[i]) == sg]
+        if idx:
+            groups[sg] = idx
+    return groups
+
+
+def _mixed_host_rows(sigs, lo, hi, n_in_max, workers):
+    """Input rows of shard [lo, hi) on the host, grouped per flow (the _mixed_groups order), each row
+    zero-padded to n_in_max elements: [hi - lo, n_in_max, 32]"""
+    from pzkwit import inputs as I
+    n_keys = {1: 64, 2: 8, 20: 64}
+    out = np.zeros((hi - lo, n_in_max, 32), dtype=np.uint8)
+    pos = 0
+    for sg, idx in _mixed_groups(sigs, lo, hi).items():
+        where = {gi: pos + k for k, gi in enumerate(idx)}
+        n_in = I.PassportGen.shared(5, n_keys[sg], sg).n_inputs
+        step = max(1, (len(idx) + workers * 4 - 1) // (workers * 4))
+        # a flow's items are not contiguous in the global batch: generate each covering range, keep members
+        jobs = [(5, idx[a], idx[min(len(idx), a + step) - 1] + 1, n_keys[sg], sg) for a in range(0, len(idx), step)]
+        with I.process_pool(workers) as ex:
+            for first, arr in ex.map(_gen_slice, jobs):
+                for k in range(len(arr)):
+                    gi = first + k
+                    if gi in where:
+                        out[where[gi], :n_in] = arr[k]
+        pos += len(idx)
+    return out
+
+
 def bench_mixed(args):
     """Config 5: a mixed-flow batch (40 % RSA-2048, 30 % RSA-4096, 30 % ECDSA secp256r1, seed 5),
-    --batch witnesses per GPU on average, sharded across ranks by .wtns bytes (pzkwit.mixed),
-    each rank running its flows one instance at a time through a shared output slab."""
+    --batch witnesses per GPU on average, sharded across ranks by .wtns bytes (pzkwit.mixed). As in
+    run_rank: rank 0 makes every rank's input rows and scatters them over the process group; status and
+    public signals are all-gathered after the timed region. On a rank, each flow has its own instance and
+    its own output slot, so the flows' pipelined calls overlap (no synchronisation between instances)."""
     import torch
-    from pzkwit import native, inputs as I, mixed
+    from pzkwit import native, dist as D
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -472,71 +520,93 @@ def bench_mixed(args):
         dist.init_process_group("nccl", device_id=dev)
     per_gpu = args.batch or 4096
     total = per_gpu * world
-    rng = np.random.default_rng(5)
-    sigs = rng.choice([m[0] for m in MIX], size=total, p=[m[1] for m in MIX])
-    flows = {sg: dict(I.CANONICAL, sig=int(sg)) for sg, _ in MIX}
-    costs = [mixed.witness_cost(flows[int(sg)]) for sg in sigs]
-    lo, hi = mixed.shard_by_cost(costs, world, rank)
-    t0 = time.time()
-    groups = {}
-    for i in range(lo, hi):
-        groups.setdefault(int(sigs[i]), []).append(i)
-    n_keys = {1: 64, 2: 8, 20: 64}
-    host = {}
-    for sg, idx in groups.items():
-        workers = max(1, min(CPU_SHARE, os.cpu_count() or 1))
-        I.PassportGen.shared(5, n_keys[sg], sg)
-        n_in = I.PassportGen.shared(5, n_keys[sg], sg).n_inputs
-        buf = np.zeros((len(idx), n_in, 32), dtype=np.uint8)
-        step = max(1, (len(idx) + workers * 4 - 1) // (workers * 4))
-        jobs = [(5, idx[a], idx[min(len(idx), a + step) - 1] + 1, n_keys[sg], sg) for a in range(0, len(idx), step)]
-        # items of one flow are not contiguous in the global batch: generate the covering range, keep members
-        with I.process_pool(workers) as ex:
-            for first, arr in ex.map(_gen_slice, jobs):
-                for k in range(len(arr)):
-                    gi = first + k
-                    if gi < total and int(sigs[gi]) == sg:
-                        buf[idx.index(gi)] = arr[k]
-        host[sg] = buf
-    log("mixed inputs: %s generated in %.1fs" % ({k: len(v) for k, v in groups.items()}, time.time() - t0))
+    sigs, flows, costs, shards = _mixed_plan(per_gpu, world)
+    lo, hi = shards[rank]
+    groups = _mixed_groups(sigs, lo, hi)
     inst = {sg: native.Instance(native.PZK_CIRCUIT_REGISTER, 0, flows[sg]) for sg in groups}
-    d_in = {sg: torch.from_numpy(host[sg].reshape(-1)).to(dev) for sg in groups}
-    del host
+    n_in_max = max(native.layout_inputs(flows[sg]) for sg, _ in MIX)
+    row_bytes = n_in_max * 32
+    rows_max = max(h - l for l, h in shards)
+    # inputs: rank 0 makes every shard (grouped per flow, padded rows), scatters shard r to rank r
+    t0 = time.time()
+    recv = torch.zeros(rows_max * row_bytes, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        workers = max(1, min(CPU_SHARE * world, os.cpu_count() or 1))
+        parts = []
+        for r, (a, b) in enumerate(shards):
+            h = np.zeros((rows_max, n_in_max, 32), dtype=np.uint8)
+            h[: b - a] = _mixed_host_rows(sigs, a, b, n_in_max, workers)
+            parts.append(torch.from_numpy(h.reshape(-1)))
+        log("mixed inputs: %d x %d rows generated on rank 0 in %.1fs" % (world, rows_max, time.time() - t0))
+        if dist is None:
+            recv.copy_(parts[0])
+        else:
+            parts = [p.to(dev) for p in parts]
+    else:
+        parts = None
+    if dist is not None:
+        dist.scatter(recv, parts, src=0)
+    del parts
+    view = recv.view(rows_max, row_bytes)
+    d_in, first = {}, {}
+    pos = 0
+    for sg, idx in groups.items():  # per flow: compact rows of its own width
+        d_in[sg] = view[pos: pos + len(idx), : 32 * inst[sg].n_inputs].contiguous()
+        first[sg] = pos
+        pos += len(idx)
+    del recv, view
+    # one output slot per flow, sized so the slots and the instances' scratch fit beside each other
     free, _ = torch.cuda.mem_get_info(dev)
-    quarter = int(free * 0.8) // 4  # two output slots <= half; each instance's scratch grows with its sub-batch
-    scratch = {1: 1 << 20, 2: 2 << 20, 20: 10 << 20}
-    sub = {sg: max(1, min(len(groups[sg]), quarter // (32 * inst[sg].witness_size + scratch[sg]))) for sg in groups}
-    slot_bytes = max(sub[sg] * 32 * inst[sg].witness_size for sg in groups)
-    d_out = torch.empty(2 * slot_bytes, dtype=torch.uint8, device=dev)
+    scratch = {1: 1 << 20, 2: 2 << 20, 20: 10 << 20}  # per-witness core scratch of one set
+    budget = int(free * 0.85) // max(1, len(groups))
+    sub = {sg: max(1, min(len(groups[sg]), budget // (32 * inst[sg].witness_size + 3 * scratch[sg]))) for sg in groups}
+    d_out = {sg: torch.empty(sub[sg] * 32 * inst[sg].witness_size, dtype=torch.uint8, device=dev) for sg in groups}
     d_st = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
+    log("mixed rank %d: flows %s, sub-batches %s, slots %.1f GB" % (
+        rank, {k: len(v) for k, v in groups.items()}, sub, sum(t.numel() for t in d_out.values()) / 1e9))
     torch.cuda.synchronize(dev)  # the library's streams do not wait for torch's stream
 
     def step():
-        off = 0
         for sg, idx in groups.items():
             W, NIN = inst[sg].witness_size, inst[sg].n_inputs
-            for j, a in enumerate(range(0, len(idx), sub[sg])):
+            for a in range(0, len(idx), sub[sg]):
                 n = min(sub[sg], len(idx) - a)
-                inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n,
-                                              d_out.data_ptr() + (j % 2) * slot_bytes, 32 * W,
-                                              d_st.data_ptr() + 4 * (off + a))
-            inst[sg].sync()  # the next instance writes the same output slab
-            off += len(idx)
+                inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n, d_out[sg].data_ptr(), 32 * W,
+                                              d_st.data_ptr() + 4 * (first[sg] + a))
+
+    def sync():
+        for i in inst.values():
+            i.sync()
+        torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    bad = int((d_st != 0).sum().item())
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    bad = int((d_st != 0).sum().item())  # lanes failing in the last timed step
+    # untimed: status + public signals (witness[1 .. 5]) of every witness of the shard, for the gather
+    n_pub = 5
+    pub = torch.zeros((hi - lo, n_pub, 32), dtype=torch.uint8, device=dev)
+    st = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
+    for sg, idx in groups.items():
+        W, NIN = inst[sg].witness_size, inst[sg].n_inputs
+        out = d_out[sg].view(sub[sg], W, 32)
+        for a in range(0, len(idx), sub[sg]):
+            n = min(sub[sg], len(idx) - a)
+            inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n, d_out[sg].data_ptr(), 32 * W,
+                                          st.data_ptr() + 4 * (first[sg] + a))
+            inst[sg].sync()
+            pub[first[sg] + a: first[sg] + a + n] = out[:n, 1: 1 + n_pub]
+    torch.cuda.synchronize(dev)
     my_bytes = sum(costs[lo:hi])
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -545,6 +615,11 @@ def bench_mixed(args):
         bt = torch.tensor([bad], device=dev, dtype=torch.int64)
         dist.all_reduce(bt)
         bad = int(bt.item())
+        st, pub = D.gather_results(dist, st, pub, device=dev)
+    import hashlib
+    gathered = {"witnesses": int(st.shape[0]), "status_nonzero": int((st != 0).sum().item()),
+                "public_sha256": hashlib.sha256(pub.cpu().numpy().tobytes()).hexdigest()[:16],
+                "order": "rank-major; within a rank grouped per flow (SIG 1, 2, 20), global order inside a group"}
     value = total * args.steps / dt
     job_gbs = sum(costs) * args.steps / dt / 1e9
     out = {
@@ -554,7 +629,8 @@ def bench_mixed(args):
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": "mixed flows %s, %d per GPU, cost-sharded" % (dict(MIX), per_gpu),
                    "flows": {str(k): len(v) for k, v in groups.items()}, "rank0_bytes": my_bytes,
-                   "invalid_lanes": bad},
+                   "sub_batches": {str(k): v for k, v in sub.items()}, "invalid_lanes": bad,
+                   "inputs": "rank 0 generates every shard and scatters it (process group)", "gathered": gathered},
         "job_hbm": {"achieved": round(job_gbs, 1), "unit": "GB/s", "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
     }
     if rank == 0:

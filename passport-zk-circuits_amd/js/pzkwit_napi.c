@@ -6,13 +6,23 @@
  * primitives:
  *
  *   version()                              -> string
- *   createInstance(params)                 -> handle (napi external; destroyed by the GC)
+ *   createInstance(params [, sym])         -> handle (napi external; destroyed by the GC); sym: the circuit's
+ *                                             .sym text (string or Buffer) -> pzk_instance_create_mapped, the
+ *                                             witness in the layout circom --O1/--O2 writes (compile-circuit.sh:34)
  *   instanceInfo(handle)                   -> { witnessSize, nInputs, nOutputs, nPublicInputs,
  *                                               inputs: [{ name, offset, length }] }
  *   wtnsHeader(handle)                     -> Buffer(76)
  *   witnessBatch(handle, inputs, batch)    -> Promise<{ witness: Buffer, status: Int32Array }>
  *        inputs: Buffer of batch x nInputs x 32 B (LE normal form); runs pzk_witness_batch_host
  *        on a libuv worker thread (napi_create_async_work), so the event loop stays free.
+ *
+ *   passportParse({ dg1, dg15, sod })       -> { params, name, refAaShift, ... } (pzk_passport_parse)
+ *   passportInputs(params, passports, identity, threads)
+ *                                           -> Promise<{ rows: Buffer, status: Int32Array }>: the bulk SOD
+ *        preprocessor (include/pzkpassport.h, pzk_passport_inputs) on a libuv worker thread: replaces one
+ *        processPassport (test/process_passport.js:674-816) per passport with one call for the batch.
+ *        passports: [{ dg1: Buffer, dg15: Buffer | null, sod: Buffer }]; identity: Buffer of
+ *        n x 82 x 32 B (slaveMerkleRoot, skIdentity, 80 branches) or null.
  *
  * Errors: a failing pzk_* call throws (or rejects with) an Error carrying pzk_last_error().
  * N-API version 4 features only (Node >= 10.16 / 12.x).
@@ -24,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../../include/pzkpassport.h"
 #include "../../include/pzkwit.h"
 
 #define CHECK(call)                                                         \
@@ -75,26 +86,66 @@ static napi_value js_version(napi_env env, napi_callback_info info) {
 /* params: { circuit, sizeArg, SIGNATURE_TYPE, DG_HASH_TYPE, DOCUMENT_TYPE, EC_BLOCK_NUMBER, EC_SHIFT,
  *           DG1_SHIFT, AA_SIGNATURE_ALGO, DG15_SHIFT, DG15_BLOCK_NUMBER, AA_SHIFT } — the template
  * parameter names of registerIdentityBuilder.circom:41-52 */
-static napi_value js_create_instance(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1], ext;
-  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc < 1) { napi_throw_type_error(env, NULL, "createInstance(params)"); return NULL; }
+static void read_params(napi_env env, napi_value obj, pzk_params* pp) {
   pzk_params p;
-  p.circuit = get_i32_prop(env, argv[0], "circuit", PZK_CIRCUIT_REGISTER);
-  p.size_arg = get_i32_prop(env, argv[0], "sizeArg", 0);
-  p.signature_type = get_i32_prop(env, argv[0], "SIGNATURE_TYPE", 1);
-  p.dg_hash_type = get_i32_prop(env, argv[0], "DG_HASH_TYPE", 256);
-  p.document_type = get_i32_prop(env, argv[0], "DOCUMENT_TYPE", 3);
-  p.ec_block_number = get_i32_prop(env, argv[0], "EC_BLOCK_NUMBER", 4);
-  p.ec_shift = get_i32_prop(env, argv[0], "EC_SHIFT", 600);
-  p.dg1_shift = get_i32_prop(env, argv[0], "DG1_SHIFT", 248);
-  p.aa_signature_algo = get_i32_prop(env, argv[0], "AA_SIGNATURE_ALGO", 1);
-  p.dg15_shift = get_i32_prop(env, argv[0], "DG15_SHIFT", 1496);
-  p.dg15_block_number = get_i32_prop(env, argv[0], "DG15_BLOCK_NUMBER", 3);
-  p.aa_shift = get_i32_prop(env, argv[0], "AA_SHIFT", 256);
+  p.circuit = get_i32_prop(env, obj, "circuit", PZK_CIRCUIT_REGISTER);
+  p.size_arg = get_i32_prop(env, obj, "sizeArg", 0);
+  p.signature_type = get_i32_prop(env, obj, "SIGNATURE_TYPE", 1);
+  p.dg_hash_type = get_i32_prop(env, obj, "DG_HASH_TYPE", 256);
+  p.document_type = get_i32_prop(env, obj, "DOCUMENT_TYPE", 3);
+  p.ec_block_number = get_i32_prop(env, obj, "EC_BLOCK_NUMBER", 4);
+  p.ec_shift = get_i32_prop(env, obj, "EC_SHIFT", 600);
+  p.dg1_shift = get_i32_prop(env, obj, "DG1_SHIFT", 248);
+  p.aa_signature_algo = get_i32_prop(env, obj, "AA_SIGNATURE_ALGO", 1);
+  p.dg15_shift = get_i32_prop(env, obj, "DG15_SHIFT", 1496);
+  p.dg15_block_number = get_i32_prop(env, obj, "DG15_BLOCK_NUMBER", 3);
+  p.aa_shift = get_i32_prop(env, obj, "AA_SHIFT", 256);
+  *pp = p;
+}
+
+/* a string or Buffer argument as bytes (strings copied into malloc'd memory: *owned = 1) */
+static int get_bytes(napi_env env, napi_value v, const char** data, size_t* len, int* owned) {
+  napi_valuetype t;
+  bool is_buf = false;
+  *owned = 0;
+  if (napi_typeof(env, v, &t) != napi_ok) return -1;
+  if (t == napi_string) {
+    size_t n = 0;
+    if (napi_get_value_string_utf8(env, v, NULL, 0, &n) != napi_ok) return -1;
+    char* b = (char*)malloc(n + 1);
+    if (!b || napi_get_value_string_utf8(env, v, b, n + 1, &n) != napi_ok) { free(b); return -1; }
+    *data = b; *len = n; *owned = 1;
+    return 0;
+  }
+  if (napi_is_buffer(env, v, &is_buf) != napi_ok || !is_buf) return -1;
+  void* d = NULL;
+  if (napi_get_buffer_info(env, v, &d, len) != napi_ok) return -1;
+  *data = (const char*)d;
+  return 0;
+}
+
+static napi_value js_create_instance(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], ext;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 1) { napi_throw_type_error(env, NULL, "createInstance(params [, sym])"); return NULL; }
+  pzk_params p;
+  read_params(env, argv[0], &p);
+  const char* sym = NULL;
+  size_t sym_len = 0;
+  int owned = 0;
+  if (argc >= 2) {
+    napi_valuetype t;
+    CHECK(napi_typeof(env, argv[1], &t));
+    if (t != napi_undefined && t != napi_null && get_bytes(env, argv[1], &sym, &sym_len, &owned) != 0) {
+      napi_throw_type_error(env, NULL, "createInstance: sym must be a string or a Buffer");
+      return NULL;
+    }
+  }
   pzk_instance* inst = NULL;
-  if (pzk_instance_create(&p, &inst) != 0) return throw_pzk(env, "pzk_instance_create");
+  const int rc = sym ? pzk_instance_create_mapped(&p, sym, sym_len, &inst) : pzk_instance_create(&p, &inst);
+  if (owned) free((void*)sym);
+  if (rc != 0) return throw_pzk(env, sym ? "pzk_instance_create_mapped" : "pzk_instance_create");
   CHECK(napi_create_external(env, inst, finalize_instance, NULL, &ext));
   return ext;
 }
@@ -236,6 +287,190 @@ static napi_value js_witness_batch(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+/* ---------------------------------------------------------------- SOD preprocessor (pzkpassport.h) */
+static napi_value params_object(napi_env env, const pzk_params* p) {
+  napi_value o, v;
+  if (napi_create_object(env, &o) != napi_ok) return NULL;
+  const struct { const char* k; int32_t v; } f[] = {
+      {"circuit", p->circuit}, {"SIGNATURE_TYPE", p->signature_type}, {"DG_HASH_TYPE", p->dg_hash_type},
+      {"DOCUMENT_TYPE", p->document_type}, {"EC_BLOCK_NUMBER", p->ec_block_number}, {"EC_SHIFT", p->ec_shift},
+      {"DG1_SHIFT", p->dg1_shift}, {"AA_SIGNATURE_ALGO", p->aa_signature_algo}, {"DG15_SHIFT", p->dg15_shift},
+      {"DG15_BLOCK_NUMBER", p->dg15_block_number}, {"AA_SHIFT", p->aa_shift}};
+  for (size_t i = 0; i < sizeof f / sizeof f[0]; i++) {
+    if (napi_create_int32(env, f[i].v, &v) != napi_ok || napi_set_named_property(env, o, f[i].k, v) != napi_ok)
+      return NULL;
+  }
+  return o;
+}
+
+/* passport object { dg1, dg15, sod } of Buffers (dg15 may be null / absent) -> source */
+static int get_passport(napi_env env, napi_value obj, pzk_passport_src* src) {
+  const char* keys[3] = {"dg1", "dg15", "sod"};
+  const uint8_t** ptr[3] = {&src->dg1, &src->dg15, &src->sod};
+  size_t* len[3] = {&src->dg1_len, &src->dg15_len, &src->sod_len};
+  for (int i = 0; i < 3; i++) {
+    bool has = false, is_buf = false;
+    napi_value v;
+    *ptr[i] = NULL; *len[i] = 0;
+    if (napi_has_named_property(env, obj, keys[i], &has) != napi_ok) return -1;
+    if (!has) { if (i == 1) continue; return -1; }
+    if (napi_get_named_property(env, obj, keys[i], &v) != napi_ok) return -1;
+    napi_valuetype t;
+    if (napi_typeof(env, v, &t) != napi_ok) return -1;
+    if (i == 1 && (t == napi_null || t == napi_undefined)) continue;
+    if (napi_is_buffer(env, v, &is_buf) != napi_ok || !is_buf) return -1;
+    void* d = NULL;
+    if (napi_get_buffer_info(env, v, &d, len[i]) != napi_ok) return -1;
+    *ptr[i] = (const uint8_t*)d;
+  }
+  return 0;
+}
+
+static napi_value js_passport_parse(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], obj, v;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  pzk_passport_src src;
+  if (argc < 1 || get_passport(env, argv[0], &src) != 0) {
+    napi_throw_type_error(env, NULL, "passportParse({ dg1: Buffer, dg15: Buffer | null, sod: Buffer })");
+    return NULL;
+  }
+  pzk_passport_info pi;
+  if (pzk_passport_parse(&src, &pi) != 0) return throw_pzk(env, "pzk_passport_parse");
+  CHECK(napi_create_object(env, &obj));
+  napi_value po = params_object(env, &pi.params);
+  if (!po) { napi_throw_error(env, NULL, "pzkwit: params object"); return NULL; }
+  CHECK(napi_set_named_property(env, obj, "params", po));
+  CHECK(napi_create_string_utf8(env, pi.name, NAPI_AUTO_LENGTH, &v));
+  CHECK(napi_set_named_property(env, obj, "name", v));
+  const struct { const char* k; int32_t v; } f[] = {
+      {"refAaShift", pi.ref_aa_shift}, {"dgHashBytes", pi.dg_hash_bytes}, {"hashBytes", pi.hash_bytes},
+      {"dg1Len", pi.dg1_len}, {"dg15Len", pi.dg15_len}, {"ecLen", pi.ec_len}, {"saLen", pi.sa_len},
+      {"chunkNumber", pi.chunk_number}, {"chunkBits", pi.chunk_bits}, {"salt", pi.salt}};
+  for (size_t i = 0; i < sizeof f / sizeof f[0]; i++) {
+    CHECK(napi_create_int32(env, f[i].v, &v));
+    CHECK(napi_set_named_property(env, obj, f[i].k, v));
+  }
+  return obj;
+}
+
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref args_ref;  /* keeps the passports array and the identity Buffer alive */
+  pzk_params params;
+  pzk_passport_src* srcs;
+  size_t n;
+  const uint8_t* identity;
+  uint8_t* rows;
+  int32_t* status;
+  size_t row_bytes;
+  int threads, rc;
+  char err[512];
+} pp_job;
+
+static void pp_execute(napi_env env, void* data) {
+  (void)env;
+  pp_job* j = (pp_job*)data;
+  j->rc = pzk_passport_inputs(&j->params, j->srcs, j->n, j->identity, j->rows, j->status, j->threads);
+  if (j->rc) snprintf(j->err, sizeof j->err, "pzk_passport_inputs: %s", pzk_last_error());
+}
+
+static void pp_complete(napi_env env, napi_status st, void* data) {
+  pp_job* j = (pp_job*)data;
+  napi_value result, err_msg, err;
+  napi_delete_reference(env, j->args_ref);
+  free(j->srcs);
+  if (st != napi_ok || j->rc != 0) {
+    napi_create_string_utf8(env, j->rc ? j->err : "pzkwit: async work cancelled", NAPI_AUTO_LENGTH, &err_msg);
+    napi_create_error(env, NULL, err_msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+    free(j->rows);
+    free(j->status);
+  } else {
+    napi_value rbuf, sab, sarr;
+    napi_create_object(env, &result);
+    napi_create_external_buffer(env, j->n * j->row_bytes, j->rows, free_cb, NULL, &rbuf);
+    napi_create_external_arraybuffer(env, j->status, j->n * sizeof(int32_t), free_cb, NULL, &sab);
+    napi_create_typedarray(env, napi_int32_array, j->n, sab, 0, &sarr);
+    napi_set_named_property(env, result, "rows", rbuf);
+    napi_set_named_property(env, result, "status", sarr);
+    napi_resolve_deferred(env, j->deferred, result);
+  }
+  napi_delete_async_work(env, j->work);
+  free(j);
+}
+
+static napi_value js_passport_inputs(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4], promise, name, holder;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 2) { napi_throw_type_error(env, NULL, "passportInputs(params, passports [, identity, threads])"); return NULL; }
+  pzk_params p;
+  read_params(env, argv[0], &p);
+  bool is_arr = false;
+  CHECK(napi_is_array(env, argv[1], &is_arr));
+  if (!is_arr) { napi_throw_type_error(env, NULL, "passports must be an array"); return NULL; }
+  uint32_t n = 0;
+  CHECK(napi_get_array_length(env, argv[1], &n));
+  pzk_info li;
+  if (pzk_layout_query(&p, &li, NULL) != 0) return throw_pzk(env, "pzk_layout_query");
+  const uint8_t* ident = NULL;
+  if (argc >= 3) {
+    napi_valuetype t;
+    CHECK(napi_typeof(env, argv[2], &t));
+    if (t != napi_null && t != napi_undefined) {
+      void* d = NULL;
+      size_t len = 0;
+      if (napi_get_buffer_info(env, argv[2], &d, &len) != napi_ok || len != (size_t)n * 82 * 32) {
+        napi_throw_range_error(env, NULL, "identity must be a Buffer of n x 82 x 32 bytes");
+        return NULL;
+      }
+      ident = (const uint8_t*)d;
+    }
+  }
+  int32_t threads = 0;
+  if (argc >= 4) {
+    napi_valuetype t;
+    CHECK(napi_typeof(env, argv[3], &t));
+    if (t == napi_number) CHECK(napi_get_value_int32(env, argv[3], &threads));
+  }
+  pp_job* j = (pp_job*)calloc(1, sizeof(pp_job));
+  if (!j) { napi_throw_error(env, NULL, "pzkwit: host allocation failed"); return NULL; }
+  j->params = p;
+  j->n = n;
+  j->identity = ident;
+  j->threads = threads;
+  j->row_bytes = (size_t)li.n_inputs * 32;
+  j->srcs = (pzk_passport_src*)calloc(n ? n : 1, sizeof(pzk_passport_src));
+  j->rows = (uint8_t*)malloc(n ? (size_t)n * j->row_bytes : 1);
+  j->status = (int32_t*)calloc(n ? n : 1, sizeof(int32_t));
+  if (!j->srcs || !j->rows || !j->status) {
+    free(j->srcs); free(j->rows); free(j->status); free(j);
+    napi_throw_error(env, NULL, "pzkwit: host allocation failed");
+    return NULL;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value e;
+    if (napi_get_element(env, argv[1], i, &e) != napi_ok || get_passport(env, e, &j->srcs[i]) != 0) {
+      char msg[128];
+      snprintf(msg, sizeof msg, "passports[%u] must be { dg1: Buffer, dg15: Buffer | null, sod: Buffer }", i);
+      free(j->srcs); free(j->rows); free(j->status); free(j);
+      napi_throw_type_error(env, NULL, msg);
+      return NULL;
+    }
+  }
+  CHECK(napi_create_array_with_length(env, 2, &holder));  /* the job reads the Buffers on a worker thread */
+  CHECK(napi_set_element(env, holder, 0, argv[1]));
+  if (ident) CHECK(napi_set_element(env, holder, 1, argv[2]));
+  CHECK(napi_create_reference(env, holder, 1, &j->args_ref));
+  CHECK(napi_create_promise(env, &j->deferred, &promise));
+  CHECK(napi_create_string_utf8(env, "pzkwit.passportInputs", NAPI_AUTO_LENGTH, &name));
+  CHECK(napi_create_async_work(env, NULL, name, pp_execute, pp_complete, j, &j->work));
+  CHECK(napi_queue_async_work(env, j->work));
+  return promise;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"version", NULL, js_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -243,6 +478,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"instanceInfo", NULL, js_instance_info, NULL, NULL, NULL, napi_enumerable, NULL},
       {"wtnsHeader", NULL, js_wtns_header, NULL, NULL, NULL, napi_enumerable, NULL},
       {"witnessBatch", NULL, js_witness_batch, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"passportParse", NULL, js_passport_parse, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"passportInputs", NULL, js_passport_inputs, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   CHECK(napi_define_properties(env, exports, sizeof props / sizeof props[0], props));
   return exports;

@@ -1,7 +1,11 @@
 // Tests of the JS host layer (run by tests/test_js.py).
-//   node test_witness_calculator.js cpu                      addon loads, marshalling + error texts
-//   node test_witness_calculator.js gpu IN.json OUT.wtns     Poseidon KAT, then the register
-//                                                            witness of IN.json written as .wtns
+//   node test_witness_calculator.js cpu [PP.json ROWS.bin]   addon loads, marshalling + error texts; with
+//        PP.json ({ params, passports: [{dg1, dg15, sod} base64], names }) the bulk preprocessor binding:
+//        passportParse names and passportInputs rows == ROWS.bin (the C-ABI's rows, via Python)
+//   node test_witness_calculator.js gpu IN.json OUT.wtns [EXTRA.json]
+//        Poseidon KAT, then the register witness of IN.json written as .wtns; with EXTRA.json
+//        ({ inputs: [3 passports' JSON], sym: ".sym text" }) concurrent calls on different passports and a
+//        .sym-mapped instance
 "use strict";
 const assert = require("assert");
 const fs = require("fs");
@@ -40,10 +44,23 @@ async function cpu() {
   assert.ok(/Error in template verifyECDSABits line: 81/.test(wcmod.statusMessage(16)));
   assert.ok(/Error in template VerifyRsaPssSig line: 182/.test(wcmod.statusMessage(18)));
   assert.strictEqual(wcmod.CIRCUIT.SHA1, 3);
+  if (ppPath) {
+    const pp = JSON.parse(fs.readFileSync(ppPath, "utf8"));
+    const b64 = (x) => (x ? Buffer.from(x, "base64") : null);
+    const passports = pp.passports.map((p) => ({ dg1: b64(p.dg1), dg15: b64(p.dg15), sod: b64(p.sod) }));
+    passports.forEach((p, i) => assert.strictEqual(wcmod.passportParse(p).name, pp.names[i]));
+    assert.throws(() => wcmod.passportParse({ dg1: Buffer.from([0x61]), sod: Buffer.from([0x30, 0x80]) }),
+                  /pzk_passport_parse/);
+    const r = await wcmod.passportInputs(pp.params, passports, null, 2);
+    const want = fs.readFileSync(rowsPath);
+    assert.strictEqual(r.status.length, passports.length);
+    assert.ok(Buffer.compare(r.rows, want) === 0, "passportInputs rows differ from the C-ABI's");
+    assert.deepStrictEqual(Array.from(r.status), pp.status);
+  }
   console.log("js cpu ok");
 }
 
-async function gpu(inPath, outPath) {
+async function gpu(inPath, outPath, extraPath) {
   const { builder, CIRCUIT } = require("./witness_calculator.js");
   // Poseidon(2) KAT from the reference's test/poseidon.js (SURVEY.md §8c)
   const pc = await builder({ circuit: CIRCUIT.POSEIDON, sizeArg: 2 });
@@ -60,16 +77,43 @@ async function gpu(inPath, outPath) {
   assert.strictEqual(b.status.length, 2);
   assert.ok(Buffer.compare(Buffer.from(b.wtns[0]), Buffer.from(b.wtns[1])) === 0);
   assert.ok(Buffer.compare(Buffer.from(b.wtns[0]), Buffer.from(wtns)) === 0);
-  // concurrent, unawaited calls on one instance (libuv pool threads): serialised inside the
-  // library, each result equal to the serial one
-  const conc = await Promise.all([rc.calculateWTNSBin(input, true), rc.calculateWTNSBinBatch([input, input], true),
-                                  rc.calculateWTNSBin(input, true)]);
-  for (const x of [conc[0], conc[1].wtns[0], conc[1].wtns[1], conc[2]])
-    assert.ok(Buffer.compare(Buffer.from(x), Buffer.from(wtns)) === 0);
+  if (extraPath) {
+    const extra = JSON.parse(fs.readFileSync(extraPath, "utf8"));
+    const [a, b, c] = extra.inputs;
+    // serial results of three different passports
+    const ser = [];
+    for (const x of [a, b, c]) ser.push(Buffer.from(await rc.calculateWTNSBin(x, true)));
+    assert.ok(Buffer.compare(ser[0], ser[1]) !== 0 && Buffer.compare(ser[1], ser[2]) !== 0);
+    // concurrent, unawaited calls on one instance (libuv pool threads), each on its own passports: serialised
+    // inside the library; every result equals ITS passport's serial result (a cross-call buffer mix-up fails)
+    const conc = await Promise.all([rc.calculateWTNSBin(a, true), rc.calculateWTNSBinBatch([b, c], true),
+                                    rc.calculateWTNSBin(c, true), rc.calculateWTNSBinBatch([c, a], true),
+                                    rc.calculateWTNSBin(b, true)]);
+    const got = [[conc[0], 0], [conc[1].wtns[0], 1], [conc[1].wtns[1], 2], [conc[2], 2], [conc[3].wtns[0], 2],
+                 [conc[3].wtns[1], 0], [conc[4], 1]];
+    got.forEach(([x, k], i) => assert.ok(Buffer.compare(Buffer.from(x), ser[k]) === 0, `concurrent result ${i}`));
+    // a .sym-mapped instance: element k of its witness = O0 signal inv[k] of the unmapped one
+    const inv = [0];
+    for (const ln of extra.sym.split("\n")) {
+      if (!ln) continue;
+      const [sig, wi] = ln.split(",").map(Number);
+      if (wi >= 0 && (inv[wi] === undefined || sig < inv[wi])) inv[wi] = sig;
+    }
+    const mc = await builder({ circuit: CIRCUIT.REGISTER }, { sym: extra.sym });
+    assert.strictEqual(mc.witnessSize, inv.length);
+    const mw = Buffer.from(await mc.calculateWTNSBin(b, true));
+    assert.strictEqual(mw.length, 76 + 32 * inv.length);
+    assert.strictEqual(mw.readUInt32LE(60), inv.length);  // header witnessSize (after the prime)
+    const o0 = ser[1];
+    for (let k = 0; k < inv.length; k++)
+      if (Buffer.compare(mw.subarray(76 + 32 * k, 108 + 32 * k), o0.subarray(76 + 32 * inv[k], 108 + 32 * inv[k])) !== 0)
+        throw new Error(`mapped element ${k} (signal ${inv[k]}) differs`);
+  }
   console.log(`js gpu ok (witnessSize ${rc.witnessSize}, ${Date.now() - t0} ms)`);
 }
 
-(mode === "cpu" ? cpu() : gpu(process.argv[3], process.argv[4])).catch((e) => {
+const ppPath = mode === "cpu" ? process.argv[3] : null, rowsPath = process.argv[4];
+(mode === "cpu" ? cpu() : gpu(process.argv[3], process.argv[4], process.argv[5])).catch((e) => {
   console.error(e);
   process.exit(1);
 });

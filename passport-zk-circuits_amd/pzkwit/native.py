@@ -106,14 +106,24 @@ def lib():
     return _lib
 
 
-def layout_witness_size(params, circuit=None):
-    """Witness elements of a RegisterIdentityBuilder instance, from the host layout (no device)."""
+def layout_info(params, circuit=None):
+    """pzk_info of a RegisterIdentityBuilder instance, from the host layout (no device)."""
     p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit)
     for k, v in param_fields(params).items():
         setattr(p, k, v)
     info = PzkInfo()
     _check(lib().pzk_layout_query(ctypes.byref(p), ctypes.byref(info), None))
-    return int(info.witness_size)
+    return info
+
+
+def layout_witness_size(params, circuit=None):
+    """Witness elements of a RegisterIdentityBuilder instance, from the host layout (no device)."""
+    return int(layout_info(params, circuit).witness_size)
+
+
+def layout_inputs(params, circuit=None):
+    """Input elements (flat row length / 32) of a RegisterIdentityBuilder instance (no device)."""
+    return int(layout_info(params, circuit).n_inputs)
 
 
 def sym_check(params, sym, circuit=None):

@@ -126,6 +126,31 @@ def test_mixed_shard_by_cost_balances_bytes():
             assert abs(sum(costs[lo:hi]) - share) <= max(costs)
 
 
+def test_mixed_bench_rows_are_the_flow_groups():
+    """Config 5 in bench.py: rank 0 makes each shard's rows grouped per flow and padded to the widest
+    flow's row; a rank cuts its flows' compact rows back out (bench_mixed). The grouped rows equal the
+    flows' own packed inputs of the same global passports, and the shards tile the job."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from pzkwit import native
+    sigs, flows, costs, shards = bench._mixed_plan(24, 2)
+    assert shards[0][0] == 0 and shards[0][1] == shards[1][0] and shards[1][1] == 48
+    n_in_max = max(native.layout_inputs(flows[sg]) for sg, _ in bench.MIX)
+    lo, hi = shards[1]
+    rows = bench._mixed_host_rows(sigs, lo, hi, n_in_max, 1)
+    pos = 0
+    for sg, idx in bench._mixed_groups(sigs, lo, hi).items():
+        assert all(int(sigs[i]) == sg for i in idx) and idx == sorted(idx)
+        n_keys = {1: 64, 2: 8, 20: 64}[sg]
+        g = I.PassportGen.shared(5, n_keys, sg)
+        for k in (0, len(idx) - 1):
+            want = I.pack_register_inputs(g.passport_at(idx[k]), g.params)
+            assert (rows[pos + k, : g.n_inputs] == want).all()
+            assert not rows[pos + k, g.n_inputs:].any()
+        pos += len(idx)
+    assert pos == hi - lo
+
+
 class _StubInst:
     """timing / phase_info of a libpzkwit instance, for bench.report without a GPU"""
 

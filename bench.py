@@ -148,8 +148,13 @@ class GpuEngine:
                     sym = open(args.sym).read()
                     self.layout = ".sym map %s" % os.path.basename(args.sym)
             self.inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params, sym=sym)
-            if sym is not None:  # two O0 chunks of up to 1024 witnesses (runtime.cpp MAP_CHUNK)
-                self.o0_staging_bytes = 2 * 1024 * 32 * native.layout_witness_size(params)
+            if sym is not None:
+                inv = symmap.parse_sym(sym)
+                if (np.diff(inv) <= 0).any() or os.environ.get("PZK_SYM_GATHER"):  # two O0 staging chunks of <= 1024 witnesses
+                    self.o0_staging_bytes = 2 * 1024 * 32 * native.layout_witness_size(params)
+                    self.layout += "; staging + gather (non-monotone map)"
+                else:
+                    self.layout += "; emitted directly (monotone map, mapsink.hpp)"
         else:
             self.inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
         self.W, self.NIN = self.inst.witness_size, self.inst.n_inputs

@@ -166,6 +166,20 @@ int pzk_instance_sync(pzk_instance* inst);
 int pzk_witness_batch_host(pzk_instance* inst, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
                            int32_t* h_status, const pzk_exec* exec);
 
+/* Streamed delivery to host memory (replaces gen-witness.sh's one generate_witness.js + .wtns write per
+ * input, circuits/scripts/gen-witness.sh:25, for a whole batch): h_inputs = batch x n_inputs x 32 B (host);
+ * the batch runs in chunks of `chunk` witnesses (0: ~1 GiB of rows per chunk), and as each chunk's rows
+ * arrive in pinned host memory the calling thread passes them to
+ *   sink(user, first, n, rows, row_stride, status): rows[i * row_stride ..] is witness first + i (32 B
+ *   elements, witness_size of them; the .wtns section 2 payload), status[i] its lane status.
+ * The rows are valid only during the call (the buffer is reused two chunks later); a non-zero return stops
+ * the stream (PZK_E_ARG). Chunk c + 1 computes and chunk c copies down while the sink runs on chunk c - 1,
+ * so a sink that keeps up leaves the host link (PCIe) as the bound. */
+typedef int (*pzk_sink_fn)(void* user, size_t first, size_t n, const uint8_t* rows, size_t row_stride,
+                           const int32_t* status);
+int pzk_witness_stream(pzk_instance* inst, const uint8_t* h_inputs, size_t batch, size_t chunk, pzk_sink_fn sink,
+                       void* user, const pzk_exec* exec);
+
 /* Per-phase kernel time accumulated (ms) by calls made with PZK_EXEC_TIMING, and the number of
  * launches of each phase. On input *count is the capacity of the arrays; on output the number of
  * phases. Synchronises on the recorded events. reset != 0 clears the accumulators afterwards. */

@@ -6,6 +6,7 @@
 #include "fr.hpp"
 #include "layout.hpp"
 #include "core_util.hpp"
+#include "mapsink.hpp"
 
 namespace pzk {
 inline namespace PZK_EC_NS {
@@ -860,7 +861,7 @@ __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work,
   for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
   __syncthreads();
   const uint32_t* prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
-  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
+  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
   // ECT_U descriptors are loaded before the ECT_U stores that use them: a global load issued
   // after a store waits for it (gfx9 vmcnt counts both), which would put every element's store
   // latency in series under the saturated write path. Two lanes per element, 1 KiB per wave store.
@@ -876,7 +877,7 @@ __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work,
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
-      if (h < tot) out[h] = ect_value(tab, d[k], h & 1);
+      store_half(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
   }
 }

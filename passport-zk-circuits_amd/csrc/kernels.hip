@@ -11,6 +11,7 @@
 #include "sha1.hpp"
 #include "sha512.hpp"
 #include "sha_prog.hpp"
+#include "mapsink.hpp"
 #include "kernels.hpp"
 
 namespace pzk {
@@ -76,7 +77,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
   const Region R = L.regions[wk.region];
   const ShaJob job = L.sha[R.a[0]];
   const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
-  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
   if (R.kind == RK_SHA_BLOCK) {
     // stage 1: the word-table entries this chunk's signals read (base words, feed-forward sums,
     // and the derived words of the schedule / compress rounds the chunk overlaps)
@@ -122,7 +123,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
       for (int k = 0; k < SHA_U; k++) {
         const uint32_t h = base + k * blockDim.x;
         const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d[k], wt[d[k] & 2047]);
-        if (h < tot) reinterpret_cast<uint4*>(out)[h] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+        store_half(out, h, make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), h < tot);
       }
     }
   } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha1(DevLayout L, const W
   const Region R = L.regions[wk.region];
   const ShaJob job = L.sha[R.a[0]];
   const uint32_t* wc = sha_core + (size_t)w * L.sha_core_words + job.core_off;
-  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
   if (R.kind == RK_SHA1_BLOCK) {
     const uint32_t* bc = wc + R.a[1] * SHA1_BLOCK_CORE;
     for (int i = threadIdx.x; i < SHA1_BLOCK_CORE; i += blockDim.x) wd[i < 85 ? i : i + 5] = bc[i];
@@ -195,7 +196,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha512(DevLayout L, const
   const Region R = L.regions[wk.region];
   const ShaJob job = L.sha[R.a[0]];
   const uint64_t* wc = reinterpret_cast<const uint64_t*>(sha_core + (size_t)w * L.sha_core_words + job.core_off);
-  uint8_t* out = wtns + (size_t)w * stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
   if (R.kind == RK_SHA5_BLOCK) {
     const uint64_t* bc = wc + (size_t)R.a[1] * (SHA5_BLOCK_CORE / 2);  // Hin[8] W[80] A[1..80] E[1..80]
     for (int i = threadIdx.x; i < 8 + 80; i += blockDim.x) wd[i] = bc[i];
@@ -235,7 +236,8 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
   uint8_t* row = B.wtns + (size_t)w * B.stride;
   // two passes: every load of the thread's elements first, then every store. A load issued after
   // a store waits for that store (gfx9 vmcnt counts both), which under a saturated write path
-  // would serialise each element on the store latency.
+  // would serialise each element on the store latency. Mapped (mapsink.hpp): the element's keep bit
+  // and mapped index are loaded in the first pass too; a dropped element is not evaluated.
   constexpr int PER = GEN_PACK / EMIT_THREADS;
   El val[PER];
   uint64_t dst[PER];
@@ -252,8 +254,10 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
       const GenPiece p = pc[lo];
       const Region& R = L.regions[p.region];
       const uint32_t s = p.start + (q - cum[lo]);
+      uint32_t rank = 0;
+      if (L.keep.bits && !map_keep_lane(L.keep, R.off + s, rank)) continue;
       val[k] = emit_small(L, B, R, w, s);
-      dst[k] = R.off + s;
+      dst[k] = L.keep.bits ? rank : R.off + s;
     }
   }
 #pragma unroll

@@ -6,6 +6,7 @@
 #define PZK_TEMPLATE_KERNELS_ONLY
 #include "bufs.hpp"
 #include "poseidon.hpp"
+#include "mapsink.hpp"
 #include "kernels.hpp"
 
 namespace pzk {
@@ -26,9 +27,13 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
   pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
   // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
-  uint4* out = reinterpret_cast<uint4*>(wtns + (size_t)w * stride + 32ull * (R.off + wk.start));
+  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
   const uint4* im = reinterpret_cast<const uint4*>(img);
-  for (uint32_t h = threadIdx.x; h < 2 * wk.count; h += blockDim.x) out[h] = im[2u * prog[h >> 1] + (h & 1)];
+  const uint32_t tot = 2 * wk.count;
+  for (uint32_t h0 = threadIdx.x & ~63u; h0 < tot; h0 += blockDim.x) {  // wave-uniform loop: store_half's map window
+    const uint32_t h = h0 + (threadIdx.x & 63);
+    store_half(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
+  }
 }
 
 hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,

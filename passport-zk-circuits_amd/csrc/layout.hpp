@@ -225,6 +225,13 @@ struct PosParamIndex {
   int32_t s_off[POS_MAX_T + 1];
 };
 
+// .sym-mapped output (mapsink.hpp): keep bitmap over the O0 signal indices and the number of kept
+// signals below every 64-signal boundary; bits == nullptr: the O0 layout
+struct KeepMap {
+  const uint64_t* bits;
+  const uint32_t* rank;
+};
+
 // everything the kernels need about an instance (device copy lives in Instance)
 struct DevLayout {
   uint64_t wit_size;      // elements per witness
@@ -253,6 +260,7 @@ struct DevLayout {
   uint32_t ec_prog_off[3], ec_tab_n[3];
   const uint32_t* ec_tab_off;       // entry offset of table op t inside a witness's tables
   uint32_t ec_tab_entries;          // table entries per witness
+  KeepMap keep;                     // direct emission into a .sym-mapped witness (mapsink.hpp)
 };
 
 }  // namespace pzk

@@ -1,0 +1,116 @@
+// Witness stores of the emit kernels, O0 or .sym-mapped.
+//
+// An emitter produces O0 elements: element q of a run is the signal with O0 index g + q. Without a map it
+// is stored at row[g + q]. With a monotone map (pzk_instance_create_mapped, every kept signal's witness
+// index increasing with its O0 index — the order circom gives the kept signals) the kept elements of any
+// run are CONSECUTIVE in the mapped row, so the emitter writes the mapped witness directly: element
+// g goes to row[rank(g)], rank(g) = number of kept signals below g, and dropped elements are not
+// stored (emit_run skips the evaluation of a wave with no kept element). The map is a keep bitmap over the O0 indices (one u64 per 64
+// signals) and the rank at every 64-signal boundary (one u32), read per wave with SCALAR loads: a wave's
+// 64 consecutive elements span at most two bitmap words, the address is wave-uniform, and scalar loads
+// are counted by lgkmcnt, so unlike a vector load they never wait for the wave's stores in flight (gfx9
+// vmcnt counts loads and stores together; DESIGN.md §4.2 rule 1).
+#pragma once
+#include "fr.hpp"
+#include "layout.hpp"
+
+namespace pzk {
+
+typedef __attribute__((address_space(4))) const uint64_t cu64_t;
+typedef __attribute__((address_space(4))) const uint32_t cu32_t;
+
+// bitmap words [i, i + 1] and their ranks: covers O0 indices [64 i, 64 i + 128)
+struct MapWin {
+  uint64_t w0, w1;
+  uint32_t r0, r1;
+  uint64_t base;
+};
+// g0: a wave-uniform O0 index (every lane passes the same value)
+__device__ __forceinline__ MapWin map_win(const KeepMap& M, uint64_t g0) {
+  const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(g0 >> 6));
+  cu64_t* b = (cu64_t*)M.bits;
+  cu32_t* r = (cu32_t*)M.rank;
+  MapWin m;
+  m.w0 = b[i];
+  m.w1 = b[i + 1];
+  m.r0 = r[i];
+  m.r1 = r[i + 1];
+  m.base = (uint64_t)i << 6;
+  return m;
+}
+__device__ __forceinline__ bool map_keep(const MapWin& m, uint64_t g) {  // g in [base, base + 128)
+  const uint32_t d = (uint32_t)(g - m.base);
+  return ((d < 64 ? m.w0 : m.w1) >> (d & 63)) & 1;
+}
+__device__ __forceinline__ uint32_t map_rank(const MapWin& m, uint64_t g) {  // kept signals below g
+  const uint32_t d = (uint32_t)(g - m.base);
+  const uint64_t w = d < 64 ? m.w0 : m.w1;
+  return (d < 64 ? m.r0 : m.r1) + (uint32_t)__popcll(w & ((1ull << (d & 63)) - 1));
+}
+// per-lane form (vector loads: only where no store of the wave is in flight yet, e.g. k_emit_gen's load pass)
+__device__ __forceinline__ bool map_keep_lane(const KeepMap& M, uint64_t g, uint32_t& rank) {
+  const uint64_t w = M.bits[g >> 6];
+  rank = M.rank[g >> 6] + (uint32_t)__popcll(w & ((1ull << (g & 63)) - 1));
+  return (w >> (g & 63)) & 1;
+}
+
+// One emitter run's destination: O0 element g + q of the witness row `row`.
+struct OutRow {
+  uint8_t* row;  // the witness row (mapped: the compact row)
+  uint64_t g;    // O0 index of element 0 of the run
+  KeepMap map;   // map.bits == nullptr: O0, the identity
+  __device__ OutRow at(uint64_t q) const { return OutRow{row, g + q, map}; }
+};
+__device__ __forceinline__ OutRow out_row(const DevLayout& L, uint8_t* wtns, size_t stride, uint32_t w, uint64_t g) {
+  return OutRow{wtns + (size_t)w * stride, g, L.keep};
+}
+
+// Half h of element h / 2 of the run (16 B; the "two lanes per element" store shape: with all lanes of a
+// wave storing consecutive halves, every wave store is 1 KiB contiguous; mapped, the kept halves of a wave
+// are still consecutive). Called with a wave's 64 lanes on 64 consecutive h (h - lane wave-uniform); lanes
+// with valid = false store nothing but take part.
+__device__ __forceinline__ void store_half(const OutRow& o, uint32_t h, const uint4& v, bool valid) {
+  if (!o.map.bits) {
+    if (valid) reinterpret_cast<uint4*>(o.row + 32ull * o.g)[h] = v;
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  const MapWin m = map_win(o.map, o.g + ((h - lane) >> 1));
+  const uint64_t e = o.g + (h >> 1);
+  if (valid && map_keep(m, e)) reinterpret_cast<uint4*>(o.row)[2ull * map_rank(m, e) + (h & 1)] = v;
+}
+
+// for (q < count) out[q] = f(q), wave-contiguous (fr.hpp emit_run); mapped: the kept elements of a wave
+// are compacted through the LDS stage and stored as one contiguous run of the mapped row. A wave with no
+// kept element skips its evaluation; otherwise f runs on every valid lane as in the O0 path (element
+// functions may scan across the wave's lanes, regemit.hpp bmneq_tmpr)
+template <typename F>
+__device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4* stage_block, F f) {
+  if (!o.map.bits) {
+    emit_run(o.row + 32ull * o.g, count, stage_block, f);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  uint4* stage = stage_block + (threadIdx.x >> 6) * 128;
+  for (uint32_t q0 = threadIdx.x - lane; q0 < count; q0 += blockDim.x) {
+    const uint32_t q = q0 + lane;
+    const MapWin m = map_win(o.map, o.g + q0);
+    const bool keep = q < count && map_keep(m, o.g + q);
+    const uint64_t mask = __ballot(keep);
+    if (mask == 0) continue;  // wave-uniform
+    const El e = q < count ? f(q) : el_zero();
+    const uint32_t pos = (uint32_t)__popcll(mask & ((1ull << lane) - 1)), nk = (uint32_t)__popcll(mask);
+    if (keep) {
+      stage[2 * pos] = e.lo;
+      stage[2 * pos + 1] = e.hi;
+    }
+    wave_sync();
+    const uint4 a = stage[lane], b = stage[64 + lane];
+    uint4* d = reinterpret_cast<uint4*>(o.row + 32ull * map_rank(m, o.g + q0));
+    if (lane < 2 * nk) d[lane] = a;
+    if (64 + lane < 2 * nk) d[64 + lane] = b;
+    wave_sync();
+  }
+}
+
+}  // namespace pzk

@@ -13,6 +13,7 @@
 #include "mm_prog.hpp"
 #include "ec_emit.hpp"
 #include "pss.hpp"
+#include "mapsink.hpp"
 
 namespace pzk {
 
@@ -281,7 +282,7 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
     }
     __syncthreads();
   }
-  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     uint32_t s = wk.start + q;
@@ -340,7 +341,7 @@ __global__ void __launch_bounds__(256) k_emit_flow(DevLayout L, const Work* work
     if (!c && B.status) lane_status(B.status + w, ST_FLOW);
   }
   __syncthreads();
-  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   const uint32_t o_d1 = 1, o_d15 = 1 + H, o_ec = 1 + 2 * H, o_eh = o_ec + ecLen, o_sa = o_eh + EH, o_v = o_sa + 1024,
                  o_eq = o_v + NC;
   __shared__ uint4 stage[2 * 256];
@@ -660,11 +661,11 @@ __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
 }
 
 template <int K, int SEC>
-__device__ __forceinline__ void mm_sections(const MMCore C, uint8_t* out, uint4* stage) {
+__device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, uint4* stage) {
   if constexpr (SEC < (int)MM_SECTIONS) {
     constexpr MMStarts S = mm_starts(K);
     constexpr uint32_t a = S.v[SEC], n = S.v[SEC + 1] - S.v[SEC];
-    emit_run(out + 32ull * a, n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    emit_run(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
     mm_sections<K, SEC + 1>(C, out, stage);
   }
 }
@@ -729,7 +730,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   }
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
            cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
-  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never
@@ -803,7 +804,7 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
   }
   __syncthreads();
   const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);
-  uint8_t* out = B.wtns + (size_t)w * B.stride + 32ull * (R.off + wk.start);
+  const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     const uint32_t s = wk.start + q, i = bjj_step_of(s), t = s - bjj_sig_of(i);

@@ -167,6 +167,11 @@ struct pzk_instance {
   // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
   // --O0 witness of a chunk into d_o0[slot]; k_wtns_gather compacts it into the caller's rows
   uint64_t out_size = 0;          // elements per output witness (= lay.wit_size without a map)
+  // monotone map (every .sym map circom writes): the emitters write the mapped witness directly
+  // (mapsink.hpp): keep bitmap over the O0 indices + the kept count below every 64-signal boundary
+  uint64_t* d_keep_bits = nullptr;
+  uint32_t* d_keep_rank = nullptr;
+  // any other map: O0 chunks into staging slots, then k_wtns_gather
   uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
   uint8_t* d_o0[2] = {};
   size_t o0_cap = 0;
@@ -174,6 +179,13 @@ struct pzk_instance {
   size_t host_cap = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
   int32_t* d_status = nullptr;
+  // streamed delivery (pzk_witness_stream): two chunk slots of device inputs / rows / statuses and
+  // their pinned host copies, an input+compute stream and a device->host copy stream
+  size_t st_cap = 0;
+  uint8_t *st_din[2] = {}, *st_dout[2] = {}, *st_hout[2] = {};
+  int32_t *st_dst[2] = {}, *st_hst[2] = {};
+  hipStream_t s_in = nullptr, s_d2h = nullptr;
+  hipEvent_t ev_comp[2] = {}, ev_d2h[2] = {};
   DevLayout dev_layout() const {
     DevLayout L{};
     L.wit_size = lay.wit_size;
@@ -202,6 +214,7 @@ struct pzk_instance {
     for (int t = 0; t < 3; t++) { L.ec_prog_off[t] = lay.ec_prog_off[t]; L.ec_tab_n[t] = lay.ec_tab_n[t]; }
     L.ec_tab_off = d_ec_tab_off;
     L.ec_tab_entries = lay.ec_tab_entries;
+    L.keep = KeepMap{d_keep_bits, d_keep_rank};
     return L;
   }
 };
@@ -281,12 +294,24 @@ static void free_scratch(pzk_instance* I) {
   for (Scratch& s : I->scr) s.free_all();
 }
 
+static void free_stream_bufs(pzk_instance* I) {
+  for (int k = 0; k < 2; k++) {
+    for (void* p : {(void*)I->st_din[k], (void*)I->st_dout[k], (void*)I->st_dst[k]})
+      if (p) (void)hipFree(p);
+    for (void* p : {(void*)I->st_hout[k], (void*)I->st_hst[k]})
+      if (p) (void)hipHostFree(p);
+    I->st_din[k] = I->st_dout[k] = I->st_hout[k] = nullptr;
+    I->st_dst[k] = I->st_hst[k] = nullptr;
+  }
+  I->st_cap = 0;
+}
+
 static void free_all(pzk_instance* I) {
   free_scratch(I);
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
                   I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small, I->d_map,
-                  I->d_o0[0], I->d_o0[1]};
+                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
@@ -300,6 +325,12 @@ static void free_all(pzk_instance* I) {
       if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : I->ev_gather)
     if (e) (void)hipEventDestroy(e);
+  free_stream_bufs(I);
+  for (hipStream_t st : {I->s_in, I->s_d2h})
+    if (st) (void)hipStreamDestroy(st);
+  for (int k = 0; k < 2; k++)
+    for (hipEvent_t e : {I->ev_comp[k], I->ev_d2h[k]})
+      if (e) (void)hipEventDestroy(e);
   I->timing.destroy();
 }
 
@@ -474,8 +505,22 @@ int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t
   std::vector<uint32_t> inv;
   std::string why;
   if (!parse_sym(sym, sym_len, I->lay.wit_size, inv, why)) { pzk_instance_destroy(I); return fail(PZK_E_ARG, why); }
-  if (hipMalloc(&I->d_map, 4 * inv.size()) != hipSuccess ||
-      hipMemcpy(I->d_map, inv.data(), 4 * inv.size(), hipMemcpyHostToDevice) != hipSuccess) {
+  bool monotone = true;
+  for (size_t k = 1; k < inv.size() && monotone; k++) monotone = inv[k] > inv[k - 1];
+  static const bool force_gather = getenv("PZK_SYM_GATHER") != nullptr;  // A/B: the staging + gather path
+  bool ok;
+  if (monotone && !force_gather) {
+    // direct emission: keep bitmap (+ 2 zero words past the end: a wave's window reads words i, i + 1)
+    const size_t nw = I->lay.wit_size / 64 + 3;
+    std::vector<uint64_t> bits(nw, 0);
+    std::vector<uint32_t> rank(nw, 0);
+    for (uint32_t g : inv) bits[g >> 6] |= 1ull << (g & 63);
+    for (size_t i = 1; i < nw; i++) rank[i] = rank[i - 1] + (uint32_t)__builtin_popcountll(bits[i - 1]);
+    ok = upload(&I->d_keep_bits, bits) == 0 && upload(&I->d_keep_rank, rank) == 0;
+  } else {
+    ok = upload(&I->d_map, inv) == 0;
+  }
+  if (!ok) {
     pzk_instance_destroy(I);
     return fail(PZK_E_NOMEM, "device allocation of the signal map failed");
   }
@@ -839,7 +884,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   DeviceGuard dg(I->device);
   if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
   if (I->d_map) return batch_mapped(I, d_inputs, batch, d_wtns, stride, d_status, exec);
-  return batch_locked(I, d_inputs, batch, d_wtns, stride, d_status, exec);
+  return batch_locked(I, d_inputs, batch, d_wtns, stride, d_status, exec);  // O0, or a monotone map emitted directly
 }
 
 int pzk_instance_sync(pzk_instance* I) {
@@ -883,6 +928,74 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
   HIPCHK(hipMemcpy(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost));
   if (h_status) HIPCHK(hipMemcpy(h_status, I->d_status, 4 * batch, hipMemcpyDeviceToHost));
   return 0;
+}
+
+// Streamed delivery: chunk c's inputs go up and its witnesses are computed on s_in (the
+// call joined into it), then copied down on s_d2h into pinned slot c % 2 while chunk c + 1 computes; the
+// calling thread hands chunk c - 1's pinned rows to the sink meanwhile. Chunk c + 2 reuses slot c % 2:
+// its upload waits for the device->host copy of chunk c (ev_d2h), and its copy down is issued only after
+// the sink of chunk c has returned.
+int pzk_witness_stream(pzk_instance* I, const uint8_t* h_inputs, size_t batch, size_t chunk, pzk_sink_fn sink,
+                       void* user, const pzk_exec* exec) {
+  if (!I || !h_inputs || !sink) return fail(PZK_E_ARG, "null argument");
+  if (batch == 0) return 0;
+  int rc = check_exec_device(I, exec);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(I->mu);
+  DeviceGuard dg(I->device);
+  if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
+  const size_t in_row = 32ull * I->lay.n_inputs, out_row = 32ull * I->out_size;
+  if (chunk == 0) chunk = std::max<size_t>(1, (size_t(1) << 30) / out_row);  // ~1 GiB of rows per copy
+  chunk = std::min({chunk, batch, size_t(65535)});
+  if ((rc = sync_all(I))) return rc;
+  if (!I->s_in) {
+    bool ok = hipStreamCreateWithFlags(&I->s_in, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&I->s_d2h, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < 2 && ok; k++)
+      ok = hipEventCreateWithFlags(&I->ev_comp[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&I->ev_d2h[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) return fail(PZK_E_HIP, "stream / event creation failed");
+  }
+  if (chunk > I->st_cap) {
+    free_stream_bufs(I);
+    for (int k = 0; k < 2; k++) {
+      if (hipMalloc(&I->st_din[k], in_row * chunk) != hipSuccess || hipMalloc(&I->st_dout[k], out_row * chunk) != hipSuccess ||
+          hipMalloc(&I->st_dst[k], 4 * chunk) != hipSuccess ||
+          hipHostMalloc(&I->st_hout[k], out_row * chunk, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(&I->st_hst[k], 4 * chunk, hipHostMallocDefault) != hipSuccess) {
+        free_stream_bufs(I);
+        (void)hipGetLastError();
+        return fail(PZK_E_NOMEM, "stream buffers (device rows or pinned host rows) could not be allocated");
+      }
+    }
+    I->st_cap = chunk;
+  }
+  const size_t n_chunks = (batch + chunk - 1) / chunk;
+  pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, I->s_in};
+  auto deliver = [&](size_t c) -> int {
+    const int k = (int)(c & 1);
+    const size_t first = c * chunk, n = std::min(chunk, batch - first);
+    HIPCHK(hipEventSynchronize(I->ev_d2h[k]));
+    if (sink(user, first, n, I->st_hout[k], out_row, I->st_hst[k]) != 0)
+      return fail(PZK_E_ARG, "the sink returned non-zero for chunk at " + std::to_string(first));
+    return 0;
+  };
+  for (size_t c = 0; c < n_chunks; c++) {
+    const int k = (int)(c & 1);
+    const size_t first = c * chunk, n = std::min(chunk, batch - first);
+    HIPCHK(hipStreamWaitEvent(I->s_in, I->ev_d2h[k], 0));  // chunk c - 2's rows have left slot k
+    HIPCHK(hipMemcpyAsync(I->st_din[k], h_inputs + in_row * first, in_row * n, hipMemcpyHostToDevice, I->s_in));
+    rc = I->d_map ? batch_mapped(I, I->st_din[k], n, I->st_dout[k], out_row, I->st_dst[k], &ex)
+                  : batch_locked(I, I->st_din[k], n, I->st_dout[k], out_row, I->st_dst[k], &ex);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(I->ev_comp[k], I->s_in));
+    if (c > 0 && (rc = deliver(c - 1))) return rc;  // chunk c - 1 to the sink while chunk c computes
+    HIPCHK(hipStreamWaitEvent(I->s_d2h, I->ev_comp[k], 0));
+    HIPCHK(hipMemcpyAsync(I->st_hout[k], I->st_dout[k], out_row * n, hipMemcpyDeviceToHost, I->s_d2h));
+    HIPCHK(hipMemcpyAsync(I->st_hst[k], I->st_dst[k], 4 * n, hipMemcpyDeviceToHost, I->s_d2h));
+    HIPCHK(hipEventRecord(I->ev_d2h[k], I->s_d2h));
+  }
+  return deliver(n_chunks - 1);
 }
 
 int pzk_timing(pzk_instance* I, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset) {

@@ -53,6 +53,10 @@ class PzkExec(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_int32), ("stream", ctypes.c_void_p)]
 
 
+SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                           ctypes.c_size_t, ctypes.c_void_p)
+
+
 class PzkError(RuntimeError):
     pass
 
@@ -88,6 +92,8 @@ def lib():
         L.pzk_witness_batch_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(PzkExec)]
         L.pzk_instance_sync.argtypes = [ctypes.c_void_p]
+        L.pzk_witness_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, SINK_FN,
+                                         ctypes.c_void_p, ctypes.POINTER(PzkExec)]
         L.pzk_instance_create_mapped.argtypes = [ctypes.POINTER(PzkParams), ctypes.c_char_p, ctypes.c_size_t,
                                                  ctypes.POINTER(ctypes.c_void_p)]
         L.pzk_sym_check.argtypes = [ctypes.POINTER(PzkParams), ctypes.c_char_p, ctypes.c_size_t,
@@ -222,6 +228,29 @@ class Instance:
                 break
             out.append((nm.value.decode(), kn.value.decode(), int(b.value)))
         return out
+
+    def witness_stream(self, inputs, sink, chunk=0):
+        """Streamed delivery (pzk_witness_stream): sink(first, rows, status) gets numpy views of each chunk's
+        pinned host rows ((n, W, 32) uint8) and statuses, valid only during the call; a truthy return stops."""
+        a = np.ascontiguousarray(inputs, dtype=np.uint8)
+        assert a.ndim == 3 and a.shape[1:] == (self.n_inputs, 32), a.shape
+        W = self.witness_size
+        err = []
+
+        def _cb(user, first, n, rows, stride, status):
+            try:
+                r = np.ctypeslib.as_array(ctypes.cast(rows, ctypes.POINTER(ctypes.c_uint8)), shape=(n * stride,))
+                s = np.ctypeslib.as_array(ctypes.cast(status, ctypes.POINTER(ctypes.c_int32)), shape=(n,))
+                return 1 if sink(first, r.reshape(n, stride)[:, : 32 * W].reshape(n, W, 32), s) else 0
+            except Exception as e:  # noqa: BLE001  (reported after the call)
+                err.append(e)
+                return 1
+        cb = SINK_FN(_cb)
+        ex = PzkExec(device=-1, flags=0, stream=None)
+        rc = lib().pzk_witness_stream(self._h, a.ctypes.data, a.shape[0], chunk, cb, None, ctypes.byref(ex))
+        if err:
+            raise err[0]
+        _check(rc)
 
     def witness_batch_host(self, inputs):
         """inputs: (batch, n_inputs, 32) uint8 -> (witness (batch, W, 32) uint8, status (batch,) int32)."""

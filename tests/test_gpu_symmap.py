@@ -64,3 +64,58 @@ def test_mapped_batch_equals_o0_batch_on_device():
     finally:
         del out0, outm, d_in
         torch.cuda.empty_cache()
+
+
+def _host_pair(params, txt, rows):
+    o0 = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params)
+    mp = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params, sym=txt)
+    w0, s0 = o0.witness_batch_host(rows)
+    wm, sm = mp.witness_batch_host(rows)
+    return w0, s0, wm, sm
+
+
+@pytest.mark.parametrize("sig", [20, 13, 3, 11, 2])
+def test_direct_mapped_emission_every_emitter(sig):
+    """Monotone maps are emitted directly by every emitter (mapsink.hpp): ECDSA table blocks (k_emit_ect),
+    SHA-384 (k_emit_sha512), SHA-1 (k_emit_sha1), RSA-PSS derived hashers, RSA-4096 BigMultModP (K = 64),
+    plus the common SHA-256 / Poseidon / BigMultModP / BabyJubJub / small-region emitters. The map also
+    merges signals onto shared witness indices (circom --O1/--O2). Mapped rows == the O0 rows at the kept
+    indices, element for element."""
+    params = I.instance_params(sig)
+    keep = _keep(params, 3)
+    merged = symmap.synthetic_keep(keep.shape[0], 0, fraction=7, salt=0x41)
+    txt = symmap.sym_text(keep, merged=merged)
+    inv = symmap.parse_sym(txt)
+    g = I.PassportGen(seed=0x70 + sig, n_keys=1, params=params, workers=1)
+    rows = np.stack([I.pack_register_inputs(g.passport_at(i, smt_depth=2 * i), params) for i in range(3)])
+    w0, s0, wm, sm = _host_pair(params, txt, rows)
+    assert (s0 == 0).all() and (sm == 0).all()
+    assert wm.shape[1] == inv.shape[0]
+    for b in range(rows.shape[0]):
+        bad = np.nonzero((wm[b] != w0[b][inv]).any(axis=1))[0]
+        assert bad.size == 0, "sig %d row %d: %d mapped elements differ (first k=%d, O0 %d)" % (
+            sig, b, bad.size, bad[0], inv[bad[0]])
+
+
+def test_keep_all_map_is_o0_and_nonmonotone_map_gathers():
+    """A map that keeps every signal in order reproduces the O0 witness through the direct path; a map that
+    is not monotone (two kept signals with swapped witness indices) takes the staging + gather path and is
+    still the O0 witness at its indices."""
+    params = I.CANONICAL
+    n_o0 = native.layout_witness_size(params)
+    g = I.PassportGen(seed=0x63, n_keys=1, workers=1)
+    rows = np.stack([I.pack_register_inputs(g.passport_at(i, smt_depth=i)) for i in range(2)])
+    w0, _, wm, sm = _host_pair(params, symmap.sym_text(np.ones(n_o0, dtype=bool)), rows)
+    assert (sm == 0).all() and wm.shape == w0.shape and (wm == w0).all()
+    keep = _keep(params, 5)
+    lines = symmap.sym_text(keep).splitlines()
+    kept = [i for i, ln in enumerate(lines) if int(ln.split(",")[1]) > 100]
+    a, b = kept[10], kept[5000]
+    la, lb = lines[a].split(","), lines[b].split(",")
+    la[1], lb[1] = lb[1], la[1]
+    lines[a], lines[b] = ",".join(la), ",".join(lb)
+    txt = "\n".join(lines) + "\n"
+    inv = symmap.parse_sym(txt)
+    assert (np.diff(inv[1:]) < 0).any()
+    _, _, wm2, sm2 = _host_pair(params, txt, rows)
+    assert (sm2 == 0).all() and (wm2 == w0[:, inv]).all()

@@ -305,6 +305,8 @@ def main():
     ap.add_argument("--sym", default=None, help="signal -> witness map: a circom .sym file, or synthetic[:N]")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
+    ap.add_argument("--host-sample", type=int, default=None, help="witnesses streamed for host_delivered")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)  # before torch / any GPU call
@@ -400,6 +402,8 @@ def report(args, r, world):
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
         "phases": phases,
     }
+    if world == 1 and not args.no_host and args.workload.startswith("register"):
+        out["host_delivered"] = host_delivered(args, r["engine"].inst, sig)
     if world == 1 and not args.no_cpu and args.workload.startswith("register") and sig in (1, 3, 10, 11, 12, 20, 21):
         out["input_side"] = input_side(sig)
     if world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
@@ -429,6 +433,35 @@ def report(args, r, world):
             "cores_note": "%d = the host CPU share of a one-GPU job on the GPU box (its OMP_NUM_THREADS); "
                           "the box's nproc counts the whole machine" % CPU_SHARE}
     return out
+
+
+def host_delivered(args, inst, sig, n=None):
+    """Witnesses delivered into host memory (pzk_witness_stream, include/pzkwit.h): host input rows up, each
+    chunk's rows computed, then copied down into pinned host memory while the next chunk computes; the sink
+    (this process) checks witness[0] == 1 and the lane status of every row. Reported beside the line, never
+    as `value` (which keeps the device-resident definition): it measures the host link, not the kernels."""
+    n = n or args.host_sample or max(64, min(512, int(36e9 // (32 * inst.witness_size))))
+    rows = make_register_inputs(n, 2 * 10 ** 6, workers=max(1, min(CPU_SHARE, os.cpu_count() or 1)),
+                                seed=SIG_SEED[sig], sig=sig)
+    seen = {"n": 0, "bad": 0, "one": 0}
+
+    def sink(first, w, st):
+        seen["n"] += w.shape[0]
+        seen["bad"] += int((st != 0).sum())
+        seen["one"] += int((w[:, 0, 0] == 1).sum())
+
+    inst.witness_stream(rows[:16], sink)  # warm: stream buffers and pinned memory allocated once per instance
+    seen.update(n=0, bad=0, one=0)
+    t0 = time.perf_counter()
+    inst.witness_stream(rows, sink)
+    dt = time.perf_counter() - t0
+    assert seen["n"] == n, seen
+    row_bytes = 32 * inst.witness_size
+    return {"what": "pzk_witness_stream: inputs from host memory, witnesses into pinned host memory (device->host "
+                    "copy of chunk c beside the compute of chunk c + 1), every row handed to a host sink",
+            "value": round(n / dt, 2), "unit": "witnesses/s", "witnesses": n, "seconds": round(dt, 3),
+            "row_bytes": row_bytes, "gb_per_s": round(n * row_bytes / dt / 1e9, 2),
+            "sink_checks": {"rows": seen["n"], "status_nonzero": seen["bad"], "witness0_is_one": seen["one"]}}
 
 
 def input_side(sig, distinct=128, n=8192):

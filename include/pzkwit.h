@@ -168,7 +168,7 @@ int pzk_witness_batch_host(pzk_instance* inst, const uint8_t* h_inputs, size_t b
 
 /* Streamed delivery to host memory (replaces gen-witness.sh's one generate_witness.js + .wtns write per
  * input, circuits/scripts/gen-witness.sh:25, for a whole batch): h_inputs = batch x n_inputs x 32 B (host);
- * the batch runs in chunks of `chunk` witnesses (0: ~1 GiB of rows per chunk), and as each chunk's rows
+ * the batch runs in chunks of `chunk` witnesses (0: ~4 GiB of rows per chunk), and as each chunk's rows
  * arrive in pinned host memory the calling thread passes them to
  *   sink(user, first, n, rows, row_stride, status): rows[i * row_stride ..] is witness first + i (32 B
  *   elements, witness_size of them; the .wtns section 2 payload), status[i] its lane status.

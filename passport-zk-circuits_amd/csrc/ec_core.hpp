@@ -849,6 +849,7 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
   return make_uint4(mw(q.x, 0), mw(q.y, 1), mw(q.z, 2), mw(q.w, 3));
 }
 
+template <int MM>  // store mode (mapsink.hpp)
 __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
                                                   size_t stride) {
   __shared__ uint4 tab[2 * EC_TABLE_MAX];
@@ -877,7 +878,7 @@ __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work,
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
-      store_half(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
+      store_half<MM>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
   }
 }

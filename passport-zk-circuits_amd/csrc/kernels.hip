@@ -64,7 +64,7 @@ __device__ __forceinline__ uint64_t sha_own_sig(const Region& R, const uint32_t*
   return ((O == 224 ? SHA224_IV[s >> 5] : SHA_IV[s >> 5]) >> (s & 31)) & 1;
 }
 
-template <int SHA_U>  // descriptors loaded ahead of their stores (see stage 2)
+template <int SHA_U, int MM>  // descriptors loaded ahead of their stores (see stage 2); MM: store mode (mapsink.hpp)
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Work* work, const uint8_t* inputs,
                                                           const uint8_t* derived, const uint32_t* sha_core,
                                                           uint8_t* wtns, size_t stride, int wit_major) {
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
       for (int k = 0; k < SHA_U; k++) {
         const uint32_t h = base + k * blockDim.x;
         const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d[k], wt[d[k] & 2047]);
-        store_half(out, h, make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), h < tot);
+        store_half<MM>(out, h, make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), h < tot);
       }
     }
   } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     __syncthreads();
     const uint8_t* in_row = job.src ? derived + 32ull * (uint64_t)w * L.n_derived : inputs + 32ull * (uint64_t)w * L.n_inputs;
     uint4* stage = reinterpret_cast<uint4*>(wt);  // the word table is not used on this path
-    emit_run(out, wk.count, stage, [&](uint32_t q) {
+    emit_run<MM>(out, wk.count, stage, [&](uint32_t q) {
       bool cp; uint64_t src = 0;
       uint64_t v = sha_own_sig(R, core, wk.start + q, cp, src);
       return cp ? el_load(in_row + 32ull * src) : el_u64(v);
@@ -382,7 +382,8 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
     case E_SHA: case E_SHAD:  // witness-major grid (see k_emit_sha)
     {  // PZK_SHA_U (8 / 16 / 32): prefetch depth, for tuning runs
       static const int u = getenv("PZK_SHA_U") ? atoi(getenv("PZK_SHA_U")) : 16;
-      auto kern = u == 8 ? k_emit_sha<8> : u == 32 ? k_emit_sha<32> : k_emit_sha<16>;
+      auto kern = L.keep.bits ? k_emit_sha<16, MAP_DIRECT>
+                  : u == 8 ? k_emit_sha<8, MAP_O0> : u == 32 ? k_emit_sha<32, MAP_O0> : k_emit_sha<16, MAP_O0>;
       hipLaunchKernelGGL(kern, dim3(batch, n_work), blk, 0, st, L, work, B.inputs, B.derived, B.sha_core, B.wtns,
                          B.stride, 1);
       break;

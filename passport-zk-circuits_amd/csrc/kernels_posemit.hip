@@ -12,7 +12,7 @@
 namespace pzk {
 
 // ------------------------------------------------------------------- emit: Poseidon
-template <int T>
+template <int T, int MM>
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
                                                           const fr* pos_core, uint8_t* wtns, size_t stride) {
   constexpr PosImg I(T);
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   const uint32_t tot = 2 * wk.count;
   for (uint32_t h0 = threadIdx.x & ~63u; h0 < tot; h0 += blockDim.x) {  // wave-uniform loop: store_half's map window
     const uint32_t h = h0 + (threadIdx.x & 63);
-    store_half(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
+    store_half<MM>(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
   }
 }
 
@@ -41,11 +41,11 @@ hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work
   if (n_work == 0) return hipSuccess;
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (t) {
-    case 2: hipLaunchKernelGGL(k_emit_pos<2>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 3: hipLaunchKernelGGL(k_emit_pos<3>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 4: hipLaunchKernelGGL(k_emit_pos<4>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 5: hipLaunchKernelGGL(k_emit_pos<5>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 6: hipLaunchKernelGGL(k_emit_pos<6>, g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 2: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<2, MAP_DIRECT> : k_emit_pos<2, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 3: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<3, MAP_DIRECT> : k_emit_pos<3, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 4: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<4, MAP_DIRECT> : k_emit_pos<4, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 5: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<5, MAP_DIRECT> : k_emit_pos<5, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 6: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<6, MAP_DIRECT> : k_emit_pos<6, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -66,9 +66,11 @@ hipError_t launch_emit_mm(const DevLayout& L, const Work* work, uint32_t n_work,
                           hipStream_t st) {
   if (n_work == 0) return hipSuccess;
   dim3 g(n_work, batch), blk(EMIT_THREADS);
-  if (L.reg.K == 32) hipLaunchKernelGGL(k_emit_mm<32>, g, blk, 0, st, L, work, B);
-  else if (L.reg.K == 48) hipLaunchKernelGGL(k_emit_mm<48>, g, blk, 0, st, L, work, B);
-  else hipLaunchKernelGGL(k_emit_mm<64>, g, blk, 0, st, L, work, B);
+  const bool m = L.keep.bits != nullptr;  // store mode (mapsink.hpp)
+  auto kern = L.reg.K == 32 ? (m ? k_emit_mm<32, MAP_DIRECT> : k_emit_mm<32, MAP_O0>)
+            : L.reg.K == 48 ? (m ? k_emit_mm<48, MAP_DIRECT> : k_emit_mm<48, MAP_O0>)
+                            : (m ? k_emit_mm<64, MAP_DIRECT> : k_emit_mm<64, MAP_O0>);
+  hipLaunchKernelGGL(kern, g, blk, 0, st, L, work, B);
   return hipGetLastError();
 }
 

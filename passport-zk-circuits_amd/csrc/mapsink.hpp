@@ -54,6 +54,10 @@ __device__ __forceinline__ bool map_keep_lane(const KeepMap& M, uint64_t g, uint
   return (w >> (g & 63)) & 1;
 }
 
+// Store modes: the hot emitters are compiled per mode (O0 / direct), so their O0 code is the plain store
+// loop; the rest check the instance's map at run time (a wave-uniform branch).
+enum { MAP_O0 = 0, MAP_DIRECT = 1, MAP_ANY = 2 };
+
 // One emitter run's destination: O0 element g + q of the witness row `row`.
 struct OutRow {
   uint8_t* row;  // the witness row (mapped: the compact row)
@@ -69,8 +73,9 @@ __device__ __forceinline__ OutRow out_row(const DevLayout& L, uint8_t* wtns, siz
 // wave storing consecutive halves, every wave store is 1 KiB contiguous; mapped, the kept halves of a wave
 // are still consecutive). Called with a wave's 64 lanes on 64 consecutive h (h - lane wave-uniform); lanes
 // with valid = false store nothing but take part.
+template <int MM = MAP_ANY>
 __device__ __forceinline__ void store_half(const OutRow& o, uint32_t h, const uint4& v, bool valid) {
-  if (!o.map.bits) {
+  if (MM == MAP_O0 || (MM == MAP_ANY && !o.map.bits)) {
     if (valid) reinterpret_cast<uint4*>(o.row + 32ull * o.g)[h] = v;
     return;
   }
@@ -84,9 +89,9 @@ __device__ __forceinline__ void store_half(const OutRow& o, uint32_t h, const ui
 // are compacted through the LDS stage and stored as one contiguous run of the mapped row. A wave with no
 // kept element skips its evaluation; otherwise f runs on every valid lane as in the O0 path (element
 // functions may scan across the wave's lanes, regemit.hpp bmneq_tmpr)
-template <typename F>
+template <int MM = MAP_ANY, typename F>
 __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4* stage_block, F f) {
-  if (!o.map.bits) {
+  if (MM == MAP_O0 || (MM == MAP_ANY && !o.map.bits)) {
     emit_run(o.row + 32ull * o.g, count, stage_block, f);
     return;
   }

@@ -660,17 +660,17 @@ __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
   }
 }
 
-template <int K, int SEC>
+template <int K, int SEC, int MM>
 __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, uint4* stage) {
   if constexpr (SEC < (int)MM_SECTIONS) {
     constexpr MMStarts S = mm_starts(K);
     constexpr uint32_t a = S.v[SEC], n = S.v[SEC + 1] - S.v[SEC];
-    emit_run(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
-    mm_sections<K, SEC + 1>(C, out, stage);
+    emit_run<MM>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    mm_sections<K, SEC + 1, MM>(C, out, stage);
   }
 }
 
-template <int K>
+template <int K, int MM>
 __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint64_t lds[MM_CORE_WORDS(K) + K + 3 * (4 * K - 1)];
   const Work wk = work[blockIdx.x];
@@ -735,7 +735,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never
   // straddles the start of a wave (K = 32: two rows per wave; K = 64: one)
-  mm_sections<K, 0>(C, out, stage);
+  mm_sections<K, 0, MM>(C, out, stage);
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps

@@ -173,6 +173,12 @@ struct pzk_instance {
   uint32_t* d_keep_rank = nullptr;
   // any other map: O0 chunks into staging slots, then k_wtns_gather
   uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
+  std::vector<uint32_t> kept;     // mapped instances: the kept O0 indices, sorted (pzk_phase_info's bytes)
+  uint64_t kept_in(uint64_t off, uint64_t len) const {  // kept signals in [off, off + len) (all without a map)
+    if (kept.empty()) return len;
+    return (uint64_t)(std::lower_bound(kept.begin(), kept.end(), (uint32_t)(off + len)) -
+                      std::lower_bound(kept.begin(), kept.end(), (uint32_t)off));
+  }
   uint8_t* d_o0[2] = {};
   size_t o0_cap = 0;
   // staging for the host-buffer path
@@ -525,6 +531,8 @@ int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t
     return fail(PZK_E_NOMEM, "device allocation of the signal map failed");
   }
   I->out_size = inv.size();
+  I->kept = inv;
+  std::sort(I->kept.begin(), I->kept.end());
   *out = I;
   return 0;
 }
@@ -945,7 +953,9 @@ int pzk_witness_stream(pzk_instance* I, const uint8_t* h_inputs, size_t batch, s
   DeviceGuard dg(I->device);
   if (dg.err != hipSuccess) return fail(PZK_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dg.err));
   const size_t in_row = 32ull * I->lay.n_inputs, out_row = 32ull * I->out_size;
-  if (chunk == 0) chunk = std::max<size_t>(1, (size_t(1) << 30) / out_row);  // ~1 GiB of rows per copy
+  // default: ~4 GiB of rows per chunk, so a chunk's compute (whose chains cost the same for few witnesses
+  // as for many) stays short against its device->host copy also for small (mapped) rows
+  if (chunk == 0) chunk = std::max<size_t>(1, (size_t(4) << 30) / out_row);
   chunk = std::min({chunk, batch, size_t(65535)});
   if ((rc = sync_all(I))) return rc;
   if (!I->s_in) {
@@ -1035,7 +1045,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
     uint64_t b = 0;
     for (const Region& r : L.regions) {
       if (EMIT_PHASE[emitter_of(r.kind)] != (int)phase) continue;
-      b += 32ull * r.len;
+      b += 32ull * I->kept_in(r.off, r.len);  // the elements the phase writes (a .sym map: the kept ones)
       if (r.kind == RK_SHA_OWN) b += 32ull * 512 * r.a[1] * (r.a[3] ? 2 : 1);  // message bits copied
       if (r.kind == RK_SHA_BLOCK) b += 4ull * SHA_BLOCK_CORE;
       if (r.kind == RK_SHA1_OWN) b += 32ull * 512 * r.a[1];  // message bits copied

@@ -194,6 +194,7 @@ def _bench_rank(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     args = argparse.Namespace(workload="sha256", batch=6, sub=None, slots=1, steps=2, warmup=1, sig_eff=0, no_cpu=True,
+                              no_host=True,
                               gpus=world)
     r = bench.run_rank(args, rank, world, 0, dist, engine_cls=_StubEngine, device="cpu")
     if rank == 0:

@@ -373,6 +373,8 @@ def report(args, r, world):
     # PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per witness, tools/pmc_summary.py) committed under
     # profiles/pmc_*/traffic.json for the workload this line measures; none -> null
     for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
+        if not r["engine"].layout.startswith("O0"):
+            break  # the committed PMC passes measured the O0 layout
         tj = json.load(open(tf))
         ks = [tj["kernels"].get(k) for k in info[dom][0].split("+")]
         if tj.get("workload") == workload and all(ks):
@@ -440,7 +442,7 @@ def host_delivered(args, inst, sig, n=None):
     chunk's rows computed, then copied down into pinned host memory while the next chunk computes; the sink
     (this process) checks witness[0] == 1 and the lane status of every row. Reported beside the line, never
     as `value` (which keeps the device-resident definition): it measures the host link, not the kernels."""
-    n = n or args.host_sample or max(64, min(512, int(36e9 // (32 * inst.witness_size))))
+    n = n or args.host_sample or max(64, min(4096, int(36e9 // (32 * inst.witness_size))))  # ~36 GB of rows
     rows = make_register_inputs(n, 2 * 10 ** 6, workers=max(1, min(CPU_SHARE, os.cpu_count() or 1)),
                                 seed=SIG_SEED[sig], sig=sig)
     seen = {"n": 0, "bad": 0, "one": 0}
@@ -450,7 +452,7 @@ def host_delivered(args, inst, sig, n=None):
         seen["bad"] += int((st != 0).sum())
         seen["one"] += int((w[:, 0, 0] == 1).sum())
 
-    inst.witness_stream(rows[:16], sink)  # warm: stream buffers and pinned memory allocated once per instance
+    inst.witness_stream(rows, sink)  # warm: the stream's device slots and pinned host rows are allocated once
     seen.update(n=0, bad=0, one=0)
     t0 = time.perf_counter()
     inst.witness_stream(rows, sink)

@@ -14,8 +14,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "build", "liboracle.so")
 POSEIDON_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "poseidon_t2_6.bin")
-P256_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "p256_gpow8.bin")
-BP256_BIN = os.path.join(REPO, "passport-zk-circuits_amd", "data", "bp256_gpow8.bin")
+# generator tables by curve index (SIGNATURE_TYPE 20, 21, 24, 25)
+EC_TABLES = [os.path.join(REPO, "passport-zk-circuits_amd", "data", n) for n in
+             ("p256_gpow8.bin", "bp256_gpow8.bin", "p224_gpow8.bin", "bp384_gpow8.bin")]
+P256_BIN, BP256_BIN = EC_TABLES[0], EC_TABLES[1]
 
 P = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
@@ -59,7 +61,7 @@ def lib():
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
         L.orc_load_ec_table.argtypes = [ctypes.c_int, ctypes.c_char_p]
-        for curve, path in enumerate((P256_BIN, BP256_BIN)):
+        for curve, path in enumerate(EC_TABLES):
             rc = L.orc_load_ec_table(curve, path.encode())
             if rc != 0:
                 raise RuntimeError("oracle: cannot load the generator table %s (%d)" % (path, rc))

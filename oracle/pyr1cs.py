@@ -87,7 +87,7 @@ def _load_poseidon():
         if rc:
             raise RuntimeError("r1cs_check: cannot load Poseidon constants (%d)" % rc)
         data = os.path.join(os.path.dirname(HERE), "passport-zk-circuits_amd", "data")
-        for curve, name in ((0, "p256_gpow8.bin"), (1, "bp256_gpow8.bin")):
+        for curve, name in enumerate(("p256_gpow8.bin", "bp256_gpow8.bin", "p224_gpow8.bin", "bp384_gpow8.bin")):
             rc = lib().ck_load_ec_table(curve, os.path.join(data, name).encode())
             if rc:
                 raise RuntimeError("r1cs_check: cannot load %s (%d)" % (name, rc))

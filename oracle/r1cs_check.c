@@ -1274,13 +1274,17 @@ static size_t ck_bmneq(ck_t *c, size_t b, int G, int L) {
 
 static int karatsuba_path(int G, int L) {
   /* BigMultOverflow bigIntOverflow.circom:43-53: power-of-two G and is_karatsuba_optimal(G, L)
-   * (bigIntFunc.circom:617-629 with get_a_coeff, dontOpenPlease.circom); the instances here use
-   * G = L in {32, 48, 64} and, for the 4-limb EC templates, G in {4, 5, 6, 7, 9, 10} x L = 4: optimal for
-   * 32 and 64 (2.5 G^1.6 <= G L), never below G = 8; 48, 5..10 are no powers of two */
-  int pow2 = (G & (G - 1)) == 0;
-  if ((G == L && (G == 32 || G == 48 || G == 64)) || (L == 4 && G >= 4 && G <= 10 && G != 8)) return pow2 && G >= 32;
-  fprintf(stderr, "r1cs_check: BigMultOverflow(%d,%d) unsupported\n", G, L);
-  abort();
+   * (bigIntFunc.circom:617-629: G >= 8 and get_a_coeff(G) <= G L, dontOpenPlease.circom: 70, 211, 640, 1940 for
+   * G = 8, 16, 32, 64). The instances here: G = L in {32, 48, 64} (RSA; optimal for 32 and 64), and the EC
+   * templates' G in {N, N+2, 2N-1, 2N+1, 2N+2} x L = N for N = 4, 6, 7 (G = 8 x 6 and 16 x 7 are powers of two
+   * but not optimal) */
+  if ((G & (G - 1)) != 0 || G < 8) return 0;
+  const int a = G == 8 ? 70 : G == 16 ? 211 : G == 32 ? 640 : G == 64 ? 1940 : -1;
+  if (a < 0) {
+    fprintf(stderr, "r1cs_check: BigMultOverflow(%d,%d) unsupported\n", G, L);
+    abort();
+  }
+  return a <= G * L;
 }
 
 /* BigMultOverflow(n, G, L) bigIntOverflow.circom:38-72: out[G+L-1] | in1[G] in2[L] | karatsuba or mult */
@@ -1353,9 +1357,9 @@ static int log_ceil(int n) { int i = 0; while (n) { n /= 2; i++; } return i; }  
 
 /* BigMultModP(n, K, K, K) bigInt.circom:206-272: div[K+1] mod[K] | in1[K] in2[K] modulus[K] |
  * mult modChecks[K] greaterThan mult2 isZero */
-static size_t ck_bmm(ck_t *c, size_t b, int K) {
+static size_t ck_bmm_n(ck_t *c, size_t b, int n, int K) {
   const char *T = "BigMultModP bigInt/bigInt.circom";
-  const int n = 64, BASE = 2 * K, DIV = K + 1;
+  const int BASE = 2 * K, DIV = K + 1;
   size_t div = b, mod = b + DIV, in1 = mod + K, in2 = in1 + K, md = in2 + K, o = md + K;
   size_t mult = o;
   o += ck_bmo(c, mult, K, K);
@@ -1387,6 +1391,8 @@ static size_t ck_bmm(ck_t *c, size_t b, int K) {
   }
   return o - b;
 }
+
+static size_t ck_bmm(ck_t *c, size_t b, int K) { return ck_bmm_n(c, b, 64, K); }
 
 /* exp_to_bits bigIntFunc.circom:590-616 (result_counter starts at 0, circom's default for a var) */
 static void exp_to_bits(uint32_t e, int *idx) {
@@ -1569,35 +1575,62 @@ static size_t ck_pss(ck_t *c, size_t b, int K, int SALT, uint32_t EXP, int H) {
 }
 
 /* ============================================================ ECDSA (signatures/ecdsa.circom, ec/curve.circom, ec/get.circom) */
-/* curve constants, 4 x 64-bit limbs little-endian (signatureVerification.circom:177-196, ec/get.circom) */
-typedef struct { uint64_t A[4], B[4], P[4], order[4], dummy[2][4]; uint64_t *gpow; } ec_curve_t;
-static ec_curve_t EC[2] = {
-    {{18446744073709551612ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
+/* curve constants as EK chunks of EB bits, little-endian (signatureVerification.circom:177-263, ec/get.circom):
+ * SIG 20 secp256r1 and 21 brainpoolP256r1 (4 x 64), 24 secp224r1 (7 x 32), 25 brainpoolP384r1 (6 x 64) */
+typedef struct { int nl, cs; uint64_t A[7], B[7], P[7], order[7], dummy[2][7]; uint64_t *gpow; } ec_curve_t;
+static ec_curve_t EC[4] = {
+    {4, 64,
+     {18446744073709551612ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
      {4309448131093880907ULL, 7285987128567378166ULL, 12964664127075681980ULL, 6540974713487397863ULL},
      {18446744073709551615ULL, 4294967295ULL, 0ULL, 18446744069414584321ULL},
      {17562291160714782033ULL, 13611842547513532036ULL, 18446744073709551615ULL, 18446744069414584320ULL},
      {{4148137498610012746ULL, 51237685452122967ULL, 6555942389409504868ULL, 799804747332166731ULL},
       {13395177781894339167ULL, 1107697421929919296ULL, 6228258783500845564ULL, 11862546499924939746ULL}}, NULL},
-    {{16810331318623712729ULL, 18122579188607900780ULL, 17219079075415130087ULL, 9032542404991529047ULL},
+    {4, 64,
+     {16810331318623712729ULL, 18122579188607900780ULL, 17219079075415130087ULL, 9032542404991529047ULL},
      {7767825457231955894ULL, 10773760575486288334ULL, 17523706096862592191ULL, 2800214691157789508ULL},
      {2311270323689771895ULL, 7943213001558335528ULL, 4496292894210231666ULL, 12248480212390422972ULL},
      {10384753744809580199ULL, 10104242082523752183ULL, 4496292894210231665ULL, 12248480212390422972ULL},
      {{5870538370169240658ULL, 13064052279558318326ULL, 1032222391323187885ULL, 10478252910764369874ULL},
-      {9125809427693782222ULL, 4479624720887462683ULL, 4313457861005768495ULL, 11848267593595748038ULL}}, NULL}};
+      {9125809427693782222ULL, 4479624720887462683ULL, 4313457861005768495ULL, 11848267593595748038ULL}}, NULL},
+    {7, 32,
+     {4294967294ULL, 4294967295ULL, 4294967295ULL, 4294967294ULL, 4294967295ULL, 4294967295ULL, 4294967295ULL},
+     {592838580ULL, 655046979ULL, 3619674298ULL, 1346678967ULL, 4114690646ULL, 201634731ULL, 3020229253ULL},
+     {1ULL, 0ULL, 0ULL, 4294967295ULL, 4294967295ULL, 4294967295ULL, 4294967295ULL},
+     {1549543997ULL, 333261125ULL, 3770216510ULL, 4294907554ULL, 4294967295ULL, 4294967295ULL, 4294967295ULL},
+     {{2477436510ULL, 406882550ULL, 2884834286ULL, 2269163287ULL, 3636783260ULL, 3699382582ULL, 912817446ULL},
+      {582933619ULL, 1778719645ULL, 3780674687ULL, 3008581200ULL, 3586474874ULL, 866709652ULL, 3566930607ULL}}, NULL},
+    {6, 64,
+     {335737924824737830ULL, 9990533504564909291ULL, 1410020238645393679ULL, 14032832221039175559ULL,
+      4355552632119865248ULL, 8918115475071440140ULL},
+     {4230998357940653073ULL, 8985869839777909140ULL, 3352946025465340629ULL, 3438355245973688998ULL,
+      10032249017711215740ULL, 335737924824737830ULL},
+     {9747760000893709395ULL, 12453481191562877553ULL, 1347097566612230435ULL, 1526563086152259252ULL,
+      1107163671716839903ULL, 10140169582434348328ULL},
+     {4289733633151100261ULL, 14932448379039367952ULL, 2240099277684876711ULL, 1526563086152259251ULL,
+      1107163671716839903ULL, 10140169582434348328ULL},
+     {{522720248942821492ULL, 13227018843434759032ULL, 17067096815187998133ULL, 8957183796380674257ULL,
+       7544165743263758981ULL, 6159107397665645433ULL},
+      {9174881270872499347ULL, 7148726877058227897ULL, 1584493337432922624ULL, 1438582915076653591ULL,
+       16161625210166602047ULL, 946254366129831718ULL}}, NULL}};
+static int ec_curve_of(int sig) { return sig == 20 ? 0 : sig == 21 ? 1 : sig == 24 ? 2 : sig == 25 ? 3 : -1; }
 static const ec_curve_t *CV;  /* the curve of the witness being checked */
+static int EK = 4, EB = 64;   /* its CHUNK_NUMBER, CHUNK_SIZE */
 
 int ck_load_ec_table(int curve, const char *path) {
+  if (curve < 0 || curve > 3) return -3;
+  const size_t n = (size_t)(EC[curve].nl * EC[curve].cs / 8) * 256 * 2 * EC[curve].nl;
   FILE *fp = fopen(path, "rb");
   if (!fp) return -1;
-  uint64_t *t = malloc(8ull * 32 * 256 * 2 * 4);
-  size_t n = fread(t, 8, 32 * 256 * 2 * 4, fp);
+  uint64_t *t = malloc(8 * n);
+  size_t got = fread(t, 8, n, fp);
   fclose(fp);
-  if (n != 32 * 256 * 2 * 4) { free(t); return -2; }
+  if (got != n) { free(t); return -2; }
   free(EC[curve].gpow);
   EC[curve].gpow = t;
   return 0;
 }
-#define GPOW(i, j, a, k) CV->gpow[((((size_t)(i) * 256 + (j)) * 2 + (a)) * 4) + (k)]
+#define GPOW(i, j, a, k) CV->gpow[((((size_t)(i) * 256 + (j)) * 2 + (a)) * EK) + (k)]
 
 /* ScalarMultOverflow(N) bigIntOverflow.circom:101-110: out[N] | in[N] scalar */
 static size_t ck_smo(ck_t *c, size_t b, int N) {
@@ -1612,26 +1645,26 @@ static size_t ck_bao(ck_t *c, size_t b, int G, int L) {
        i < L ? 30 : 33);
   return 2 * (size_t)G + L;
 }
-/* BigSubModOverflow(K) bigIntOverflow.circom:78-98: out[K] | in1[K] in2[K] modulus[K] */
+/* BigSubModOverflow(EB, K) bigIntOverflow.circom:78-98: out[K] | in1[K] in2[K] modulus[K] */
 static size_t ck_bsmo(ck_t *c, size_t b, int K) {
   const char *T = "BigSubModOverflow bigInt/bigIntOverflow.circom";
   for (int i = 0; i < K; i++) {
     fr_t v = SUB(ADD(S(c, b + 3 * K + i), S(c, b + K + i)), S(c, b + 2 * K + i));
-    if (i == 0) v = ADD(v, P2[64]);
+    if (i == 0) v = ADD(v, P2[EB]);
     else if (i == K - 1) v = SUB(v, KC(1));
-    else v = SUB(ADD(v, P2[64]), KC(1));
+    else v = SUB(ADD(v, P2[EB]), KC(1));
     EQ(S(c, b + i), v, T, i == 0 ? 89 : i == K - 1 ? 92 : 94);
   }
   return 4 * (size_t)K;
 }
-/* BigIntIsZeroModP(n, MAX, N, MAXN, NM) bigIntComparators.circom:158-212:
+/* BigIntIsZeroModP(EB, MAX, N, MAXN, NM) bigIntComparators.circom:158-212:
  * in[N] modulus[NM] | sign k[DIV] | kRangeChecks[DIV] mult isZero swicher[N]  (kRangeChecks.in is set by `<--`) */
 static size_t ck_biszmp(ck_t *c, size_t b, int N, int MAX, int MAXN, int NM) {
   const char *T = "BigIntIsZeroModP bigInt/bigIntComparators.circom";
   const int DIV = MAXN - NM + 1;
   size_t in = b, md = b + N, sign = md + NM, k = sign + 1, o = k + DIV;
   EQ(MUL(S(c, sign), SUB(KC(1), S(c, sign))), fr_zero(), T, 167);
-  for (int i = 0; i < DIV; i++) o += ck_num2bits(c, o, 64);
+  for (int i = 0; i < DIV; i++) o += ck_num2bits(c, o, EB);
   size_t mult = o;
   int G = DIV >= NM ? DIV : NM, L = DIV >= NM ? NM : DIV;
   o += ck_bmo(c, mult, G, L);
@@ -1639,7 +1672,7 @@ static size_t ck_biszmp(ck_t *c, size_t b, int N, int MAX, int MAXN, int NM) {
   for (int i = 0; i < NM; i++) EQ(S(c, (DIV >= NM ? m2 : m1) + i), S(c, md + i), T, DIV >= NM ? 185 : 189);
   for (int i = 0; i < DIV; i++) EQ(S(c, (DIV >= NM ? m1 : m2) + i), S(c, k + i), T, DIV >= NM ? 186 : 190);
   size_t iz = o;
-  o += ck_bisz(c, iz, 64, MAX, MAXN);
+  o += ck_bisz(c, iz, EB, MAX, MAXN);
   for (int i = 0; i < N; i++) {
     size_t sw = o;
     o += ck_switcher(c, sw);
@@ -1654,107 +1687,109 @@ static size_t ck_biszmp(ck_t *c, size_t b, int N, int MAX, int MAXN, int NM) {
 
 static fr_t L64(uint64_t v) { return fr_u64(v); }
 
-/* PointOnCurve curve.circom:107-138: in[2][K] | squareX cubeX squareY coefMult isZeroModP */
+/* PointOnCurve curve.circom:107-138: in[2][K] | squareX cubeX squareY coefMult isZeroModP(EB, 3 EB + 2K, 3K - 2, 3K, K) */
 static size_t ck_ponc(ck_t *c, size_t b) {
   const char *T = "PointOnCurve ec/curve.circom";
-  const int K = 4;
+  const int K = EK, K2 = 2 * K - 1, K3 = 3 * K - 2;
   size_t x = b, y = b + K, o = b + 2 * K;
-  size_t sx = o; o += ck_bmo(c, sx, 4, 4);
-  size_t cx = o; o += ck_bmo(c, cx, 7, 4);
-  size_t sy = o; o += ck_bmo(c, sy, 4, 4);
-  size_t cm = o; o += ck_bmo(c, cm, 4, 4);
-  size_t iz = o; o += ck_biszmp(c, iz, 10, 200, 12, 4);
+  size_t sx = o; o += ck_bmo(c, sx, K, K);
+  size_t cx = o; o += ck_bmo(c, cx, K2, K);
+  size_t sy = o; o += ck_bmo(c, sy, K, K);
+  size_t cm = o; o += ck_bmo(c, cm, K, K);
+  size_t iz = o; o += ck_biszmp(c, iz, K3, 3 * EB + 2 * K, 3 * K, K);
   for (int i = 0; i < K; i++) {
-    EQ(S(c, sx + 7 + i), S(c, x + i), T, 111); EQ(S(c, sx + 11 + i), S(c, x + i), T, 112);
-    EQ(S(c, cx + 10 + 7 + i), S(c, x + i), T, 116);
-    EQ(S(c, sy + 7 + i), S(c, y + i), T, 119); EQ(S(c, sy + 11 + i), S(c, y + i), T, 120);
-    EQ(S(c, cm + 7 + i), S(c, x + i), T, 123); EQ(S(c, cm + 11 + i), L64(CV->A[i]), T, 124);
-    EQ(S(c, iz + 10 + i), L64(CV->P[i]), T, 137);
+    EQ(S(c, sx + K2 + i), S(c, x + i), T, 111); EQ(S(c, sx + K2 + K + i), S(c, x + i), T, 112);
+    EQ(S(c, cx + K3 + K2 + i), S(c, x + i), T, 116);
+    EQ(S(c, sy + K2 + i), S(c, y + i), T, 119); EQ(S(c, sy + K2 + K + i), S(c, y + i), T, 120);
+    EQ(S(c, cm + K2 + i), S(c, x + i), T, 123); EQ(S(c, cm + K2 + K + i), L64(CV->A[i]), T, 124);
+    EQ(S(c, iz + K3 + i), L64(CV->P[i]), T, 137);
   }
-  for (int i = 0; i < 7; i++) EQ(S(c, cx + 10 + i), S(c, sx + i), T, 115);
-  for (int i = 0; i < 10; i++) {
+  for (int i = 0; i < K2; i++) EQ(S(c, cx + K3 + i), S(c, sx + i), T, 115);
+  for (int i = 0; i < K3; i++) {
     fr_t v = S(c, cx + i);
-    if (i < 7) v = SUB(ADD(v, S(c, cm + i)), S(c, sy + i));
+    if (i < K2) v = SUB(ADD(v, S(c, cm + i)), S(c, sy + i));
     if (i < K) v = ADD(v, L64(CV->B[i]));
-    EQ(S(c, iz + i), v, T, i < K ? 128 : i < 7 ? 131 : 134);
+    EQ(S(c, iz + i), v, T, i < K ? 128 : i < K2 ? 131 : 134);
   }
   return o - b;
 }
 
 /* PointOnTangent curve.circom:144-190: in1[2][K] in2[2][K] | squareX scalarMult bigAdd bigSub rightMult scalarMult2
- * bigAdd2 leftMult isZeroModP */
+ * bigAdd2 leftMult isZeroModP(EB, 3 EB + 2K, 3K - 2, 3K + 1, K) */
 static size_t ck_pont(ck_t *c, size_t b) {
   const char *T = "PointOnTangent ec/curve.circom";
-  const int K = 4;
-  size_t x1 = b, y1 = b + 4, x3 = b + 8, y3 = b + 12, o = b + 16;
-  size_t sx = o; o += ck_bmo(c, sx, 4, 4);
-  size_t sm = o; o += ck_smo(c, sm, 7);
-  size_t ba = o; o += ck_bao(c, ba, 7, 4);
-  size_t bs = o; o += ck_bsmo(c, bs, 4);
-  size_t rm = o; o += ck_bmo(c, rm, 7, 4);
-  size_t sm2 = o; o += ck_smo(c, sm2, 4);
-  size_t ba2 = o; o += ck_bao(c, ba2, 4, 4);
-  size_t lm = o; o += ck_bmo(c, lm, 4, 4);
-  size_t iz = o; o += ck_biszmp(c, iz, 10, 200, 13, 4);
+  const int K = EK, K2 = 2 * K - 1, K3 = 3 * K - 2;
+  size_t x1 = b, y1 = b + K, x3 = b + 2 * K, y3 = b + 3 * K, o = b + 4 * K;
+  size_t sx = o; o += ck_bmo(c, sx, K, K);
+  size_t sm = o; o += ck_smo(c, sm, K2);
+  size_t ba = o; o += ck_bao(c, ba, K2, K);
+  size_t bs = o; o += ck_bsmo(c, bs, K);
+  size_t rm = o; o += ck_bmo(c, rm, K2, K);
+  size_t sm2 = o; o += ck_smo(c, sm2, K);
+  size_t ba2 = o; o += ck_bao(c, ba2, K, K);
+  size_t lm = o; o += ck_bmo(c, lm, K, K);
+  size_t iz = o; o += ck_biszmp(c, iz, K3, 3 * EB + 2 * K, 3 * K + 1, K);
   for (int i = 0; i < K; i++) {
-    EQ(S(c, sx + 7 + i), S(c, x1 + i), T, 148); EQ(S(c, sx + 11 + i), S(c, x1 + i), T, 149);
-    EQ(S(c, ba + 14 + i), L64(CV->A[i]), T, 157);
-    EQ(S(c, bs + 4 + i), S(c, x1 + i), T, 161); EQ(S(c, bs + 8 + i), S(c, x3 + i), T, 162);
-    EQ(S(c, bs + 12 + i), L64(CV->P[i]), T, 163);
-    EQ(S(c, rm + 10 + 7 + i), S(c, bs + i), T, 167);
-    EQ(S(c, sm2 + 4 + i), S(c, y1 + i), T, 170);
-    EQ(S(c, ba2 + 4 + i), S(c, y1 + i), T, 174); EQ(S(c, ba2 + 8 + i), S(c, y3 + i), T, 175);
-    EQ(S(c, lm + 7 + i), S(c, ba2 + i), T, 178); EQ(S(c, lm + 11 + i), S(c, sm2 + i), T, 179);
-    EQ(S(c, iz + 10 + i), L64(CV->P[i]), T, 189);
+    EQ(S(c, sx + K2 + i), S(c, x1 + i), T, 148); EQ(S(c, sx + K2 + K + i), S(c, x1 + i), T, 149);
+    EQ(S(c, ba + 2 * K2 + i), L64(CV->A[i]), T, 157);
+    EQ(S(c, bs + K + i), S(c, x1 + i), T, 161); EQ(S(c, bs + 2 * K + i), S(c, x3 + i), T, 162);
+    EQ(S(c, bs + 3 * K + i), L64(CV->P[i]), T, 163);
+    EQ(S(c, rm + K3 + K2 + i), S(c, bs + i), T, 167);
+    EQ(S(c, sm2 + K + i), S(c, y1 + i), T, 170);
+    EQ(S(c, ba2 + K + i), S(c, y1 + i), T, 174); EQ(S(c, ba2 + 2 * K + i), S(c, y3 + i), T, 175);
+    EQ(S(c, lm + K2 + i), S(c, ba2 + i), T, 178); EQ(S(c, lm + K2 + K + i), S(c, sm2 + i), T, 179);
+    EQ(S(c, iz + K3 + i), L64(CV->P[i]), T, 189);
   }
-  for (int i = 0; i < 7; i++) {
-    EQ(S(c, sm + 7 + i), S(c, sx + i), T, 152);
-    EQ(S(c, ba + 7 + i), S(c, sm + i), T, 156);
-    EQ(S(c, rm + 10 + i), S(c, ba + i), T, 166);
+  for (int i = 0; i < K2; i++) {
+    EQ(S(c, sm + K2 + i), S(c, sx + i), T, 152);
+    EQ(S(c, ba + K2 + i), S(c, sm + i), T, 156);
+    EQ(S(c, rm + K3 + i), S(c, ba + i), T, 166);
   }
-  EQ(S(c, sm + 14), KC(3), T, 153);
-  EQ(S(c, sm2 + 8), KC(2), T, 171);
-  for (int i = 0; i < 10; i++) EQ(S(c, iz + i), i < 7 ? SUB(S(c, rm + i), S(c, lm + i)) : S(c, rm + i), T, i < 7 ? 182 : 185);
+  EQ(S(c, sm + 2 * K2), KC(3), T, 153);
+  EQ(S(c, sm2 + 2 * K), KC(2), T, 171);
+  for (int i = 0; i < K3; i++) EQ(S(c, iz + i), i < K2 ? SUB(S(c, rm + i), S(c, lm + i)) : S(c, rm + i), T, i < K2 ? 182 : 185);
   return o - b;
 }
 
-/* PointOnLine curve.circom:198-238: in1 in2 in3 [2][K] | bigAdd bigSub bigSub2 bigSub3 leftMult rightMult isZeroModP */
+/* PointOnLine curve.circom:198-238: in1 in2 in3 [2][K] | bigAdd bigSub bigSub2 bigSub3 leftMult rightMult
+ * isZeroModP(EB, 2 EB + 2K, 2K - 1, 2K + 1, K) */
 static size_t ck_ponl(ck_t *c, size_t b) {
   const char *T = "PointOnLine ec/curve.circom";
-  const int K = 4;
-  size_t x1 = b, y1 = b + 4, x2 = b + 8, y2 = b + 12, x3 = b + 16, y3 = b + 20, o = b + 24;
-  size_t ba = o; o += ck_bao(c, ba, 4, 4);
-  size_t s1 = o; o += ck_bsmo(c, s1, 4);
-  size_t s2 = o; o += ck_bsmo(c, s2, 4);
-  size_t s3 = o; o += ck_bsmo(c, s3, 4);
-  size_t lm = o; o += ck_bmo(c, lm, 4, 4);
-  size_t rm = o; o += ck_bmo(c, rm, 4, 4);
-  size_t iz = o; o += ck_biszmp(c, iz, 7, 136, 9, 4);
+  const int K = EK, K2 = 2 * K - 1;
+  size_t x1 = b, y1 = b + K, x2 = b + 2 * K, y2 = b + 3 * K, x3 = b + 4 * K, y3 = b + 5 * K, o = b + 6 * K;
+  size_t ba = o; o += ck_bao(c, ba, K, K);
+  size_t s1 = o; o += ck_bsmo(c, s1, K);
+  size_t s2 = o; o += ck_bsmo(c, s2, K);
+  size_t s3 = o; o += ck_bsmo(c, s3, K);
+  size_t lm = o; o += ck_bmo(c, lm, K, K);
+  size_t rm = o; o += ck_bmo(c, rm, K, K);
+  size_t iz = o; o += ck_biszmp(c, iz, K2, 2 * EB + 2 * K, 2 * K + 1, K);
   for (int i = 0; i < K; i++) {
-    EQ(S(c, ba + 4 + i), S(c, y1 + i), T, 204); EQ(S(c, ba + 8 + i), S(c, y3 + i), T, 205);
-    EQ(S(c, s1 + 4 + i), S(c, x2 + i), T, 208); EQ(S(c, s1 + 8 + i), S(c, x1 + i), T, 209);
-    EQ(S(c, s2 + 4 + i), S(c, y2 + i), T, 213); EQ(S(c, s2 + 8 + i), S(c, y1 + i), T, 214);
-    EQ(S(c, s3 + 4 + i), S(c, x1 + i), T, 218); EQ(S(c, s3 + 8 + i), S(c, x3 + i), T, 219);
-    EQ(S(c, s1 + 12 + i), L64(CV->P[i]), T, 210); EQ(S(c, s2 + 12 + i), L64(CV->P[i]), T, 215);
-    EQ(S(c, s3 + 12 + i), L64(CV->P[i]), T, 220);
-    EQ(S(c, lm + 7 + i), S(c, ba + i), T, 223); EQ(S(c, lm + 11 + i), S(c, s1 + i), T, 224);
-    EQ(S(c, rm + 7 + i), S(c, s2 + i), T, 227); EQ(S(c, rm + 11 + i), S(c, s3 + i), T, 228);
-    EQ(S(c, iz + 7 + i), L64(CV->P[i]), T, 236);
+    EQ(S(c, ba + K + i), S(c, y1 + i), T, 204); EQ(S(c, ba + 2 * K + i), S(c, y3 + i), T, 205);
+    EQ(S(c, s1 + K + i), S(c, x2 + i), T, 208); EQ(S(c, s1 + 2 * K + i), S(c, x1 + i), T, 209);
+    EQ(S(c, s2 + K + i), S(c, y2 + i), T, 213); EQ(S(c, s2 + 2 * K + i), S(c, y1 + i), T, 214);
+    EQ(S(c, s3 + K + i), S(c, x1 + i), T, 218); EQ(S(c, s3 + 2 * K + i), S(c, x3 + i), T, 219);
+    EQ(S(c, s1 + 3 * K + i), L64(CV->P[i]), T, 210); EQ(S(c, s2 + 3 * K + i), L64(CV->P[i]), T, 215);
+    EQ(S(c, s3 + 3 * K + i), L64(CV->P[i]), T, 220);
+    EQ(S(c, lm + K2 + i), S(c, ba + i), T, 223); EQ(S(c, lm + K2 + K + i), S(c, s1 + i), T, 224);
+    EQ(S(c, rm + K2 + i), S(c, s2 + i), T, 227); EQ(S(c, rm + K2 + K + i), S(c, s3 + i), T, 228);
+    EQ(S(c, iz + K2 + i), L64(CV->P[i]), T, 236);
   }
-  for (int i = 0; i < 7; i++) EQ(S(c, iz + i), SUB(S(c, lm + i), S(c, rm + i)), T, 233);
+  for (int i = 0; i < K2; i++) EQ(S(c, iz + i), SUB(S(c, lm + i), S(c, rm + i)), T, 233);
   return o - b;
 }
 
 /* EllipticCurveDouble curve.circom:281-313: out[2][K] | in[2][K] | onTangentCheck onCurveCheck */
 static size_t ck_ecdbl(ck_t *c, size_t b) {
   const char *T = "EllipticCurveDouble ec/curve.circom";
-  size_t o = b + 16, tg = o;
+  const int PT = 2 * EK;
+  size_t o = b + 2 * PT, tg = o;
   o += ck_pont(c, tg);
   size_t oc = o;
   o += ck_ponc(c, oc);
-  for (int i = 0; i < 8; i++) {
-    EQ(S(c, tg + i), S(c, b + 8 + i), T, 301);
-    EQ(S(c, tg + 8 + i), S(c, b + i), T, 302);
+  for (int i = 0; i < PT; i++) {
+    EQ(S(c, tg + i), S(c, b + PT + i), T, 301);
+    EQ(S(c, tg + PT + i), S(c, b + i), T, 302);
     EQ(S(c, oc + i), S(c, b + i), T, 305);
   }
   return o - b;
@@ -1762,83 +1797,87 @@ static size_t ck_ecdbl(ck_t *c, size_t b) {
 /* EllipticCurveAdd curve.circom:316-350: out[2][K] | in1 in2 | onCurveCheck onLineCheck */
 static size_t ck_ecadd(ck_t *c, size_t b) {
   const char *T = "EllipticCurveAdd ec/curve.circom";
-  size_t o = b + 24, oc = o;
+  const int PT = 2 * EK;
+  size_t o = b + 3 * PT, oc = o;
   o += ck_ponc(c, oc);
   size_t ln = o;
   o += ck_ponl(c, ln);
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < PT; i++) {
     EQ(S(c, oc + i), S(c, b + i), T, 339);
-    EQ(S(c, ln + i), S(c, b + 8 + i), T, 342);
-    EQ(S(c, ln + 8 + i), S(c, b + 16 + i), T, 343);
-    EQ(S(c, ln + 16 + i), S(c, b + i), T, 344);
+    EQ(S(c, ln + i), S(c, b + PT + i), T, 342);
+    EQ(S(c, ln + PT + i), S(c, b + 2 * PT + i), T, 343);
+    EQ(S(c, ln + 2 * PT + i), S(c, b + i), T, 344);
   }
   return o - b;
 }
 /* EllipticCurveGetDummy ec/get.circom:79-140: dummyPoint[2][K] */
 static size_t ck_getdummy(ck_t *c, size_t b) {
   for (int a = 0; a < 2; a++)
-    for (int i = 0; i < 4; i++) EQ(S(c, b + 4 * a + i), L64(CV->dummy[a][i]), "EllipticCurveGetDummy ec/get.circom", 92 + a);
-  return 8;
+    for (int i = 0; i < EK; i++) EQ(S(c, b + EK * a + i), L64(CV->dummy[a][i]), "EllipticCurveGetDummy ec/get.circom", 92 + a);
+  return 2 * (size_t)EK;
 }
 
 /* EllipticCurvePrecomputePipinger(.., 4) curve.circom:242-278: out[16][2][K] | in[2][K] | getDummy (doublers, adders) */
 static size_t ck_precompute(ck_t *c, size_t b) {
   const char *T = "EllipticCurvePrecomputePipinger ec/curve.circom";
-  size_t out = b, in = b + 128, o = b + 136;
+  const size_t PT = 2 * (size_t)EK;
+  size_t out = b, in = b + 16 * PT, o = in + PT;
   size_t gd = o;
   o += ck_getdummy(c, gd);
-  for (int i = 0; i < 8; i++) {
+  for (size_t i = 0; i < PT; i++) {
     EQ(S(c, out + i), S(c, gd + i), T, 253);
-    EQ(S(c, out + 8 + i), S(c, in + i), T, 255);
+    EQ(S(c, out + PT + i), S(c, in + i), T, 255);
   }
   for (int i = 2; i < 16; i++) {
     size_t x = o;
     if (i % 2 == 0) {
       o += ck_ecdbl(c, x);
-      for (int q = 0; q < 8; q++) {
-        EQ(S(c, x + 8 + q), S(c, out + 8 * (size_t)(i / 2) + q), T, 263);
-        EQ(S(c, out + 8 * (size_t)i + q), S(c, x + q), T, 264);
+      for (size_t q = 0; q < PT; q++) {
+        EQ(S(c, x + PT + q), S(c, out + PT * (size_t)(i / 2) + q), T, 263);
+        EQ(S(c, out + PT * (size_t)i + q), S(c, x + q), T, 264);
       }
     } else {
       o += ck_ecadd(c, x);
-      for (int q = 0; q < 8; q++) {
-        EQ(S(c, x + 8 + q), S(c, out + 8 + q), T, 269);
-        EQ(S(c, x + 16 + q), S(c, out + 8 * (size_t)(i - 1) + q), T, 270);
-        EQ(S(c, out + 8 * (size_t)i + q), S(c, x + q), T, 271);
+      for (size_t q = 0; q < PT; q++) {
+        EQ(S(c, x + PT + q), S(c, out + PT + q), T, 269);
+        EQ(S(c, x + 2 * PT + q), S(c, out + PT * (size_t)(i - 1) + q), T, 270);
+        EQ(S(c, out + PT * (size_t)i + q), S(c, x + q), T, 271);
       }
     }
   }
   return o - b;
 }
 
-/* EllipticCurveScalarMult(.., 4) curve.circom:359-512: out[2][K] | in[2][K] scalar[K] |
- * scalarBits[256] resultingPoints[65][2][K] additionPoints[64][2][K] | precompute getDummy num2Bits[4], then per
- * window: bits2Num isZeroResult [doublers (doubleSwitcher x8 after the first) ] getSum x8 partsEqual x16
- * [adders isZeroAddition (resultSwitcherAddition resultSwitcherDoubling) x8] */
+/* EllipticCurveScalarMult(.., 4) curve.circom:359-512 (F = K EB bits, F / 4 windows): out[2][K] | in[2][K] scalar[K] |
+ * scalarBits[F] resultingPoints[F/4+1][2][K] additionPoints[F/4][2][K] | precompute getDummy num2Bits[K], then per
+ * window: bits2Num isZeroResult [doublers (doubleSwitcher x2K after the first) ] getSum x2K partsEqual x16
+ * [adders isZeroAddition (resultSwitcherAddition resultSwitcherDoubling) x2K] */
 static size_t ck_ecmul(ck_t *c, size_t b) {
   const char *T = "EllipticCurveScalarMult ec/curve.circom";
-  size_t out = b, in = b + 8, sc = b + 16, bits = b + 20, rp = bits + 256, ap = rp + 65 * 8, o = ap + 64 * 8;
+  const int F = EK * EB, NW = F / 4;
+  const size_t PT = 2 * (size_t)EK;
+  size_t out = b, in = b + PT, sc = in + PT, bits = sc + EK, rp = bits + F, ap = rp + (NW + 1) * PT, o = ap + NW * PT;
   size_t pc = o;
   o += ck_precompute(c, pc);
-  for (int i = 0; i < 8; i++) EQ(S(c, pc + 128 + i), S(c, in + i), T, 368);
+  for (size_t i = 0; i < PT; i++) EQ(S(c, pc + 16 * PT + i), S(c, in + i), T, 368);
   size_t gd = o;
   o += ck_getdummy(c, gd);
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < EK; i++) {
     size_t nb = o;
-    o += ck_num2bits(c, nb, 64);
-    EQ(S(c, nb + 64), S(c, sc + i), T, 387);
-    for (int j = 0; j < 64; j++) EQ(S(c, bits + 256 - 64 * (i + 1) + j), S(c, nb + 63 - j), T, 389);
+    o += ck_num2bits(c, nb, EB);
+    EQ(S(c, nb + EB), S(c, sc + i), T, 387);
+    for (int j = 0; j < EB; j++) EQ(S(c, bits + F - EB * (i + 1) + j), S(c, nb + EB - 1 - j), T, 389);
   }
-  for (int q = 0; q < 8; q++) EQ(S(c, rp + q), S(c, pc + q), T, 409);
-  size_t dbl_at[256];
-  for (int i = 0; i < 256; i += 4) {
+  for (size_t q = 0; q < PT; q++) EQ(S(c, rp + q), S(c, pc + q), T, 409);
+  size_t *dbl_at = malloc(sizeof(size_t) * F);
+  for (int i = 0; i < F; i += 4) {
     int w = i / 4;
     size_t bn = o;
     o += ck_bits2num(c, bn, 4);
     for (int j = 0; j < 4; j++) EQ(S(c, bn + 1 + j), S(c, bits + i + 3 - j), T, 414);
     size_t izr = o;
     o += ck_isequal(c, izr);
-    EQ(S(c, izr + 1), S(c, rp + 8 * (size_t)w), T, 418);
+    EQ(S(c, izr + 1), S(c, rp + PT * (size_t)w), T, 418);
     EQ(S(c, izr + 2), S(c, gd), T, 419);
     if (i != 0) {
       for (int j = 0; j < 4; j++) {
@@ -1846,43 +1885,43 @@ static size_t ck_ecmul(ck_t *c, size_t b) {
         dbl_at[i + j - 4] = d;
         o += ck_ecdbl(c, d);
         if (j == 0) {
-          for (int q = 0; q < 8; q++) {
+          for (size_t q = 0; q < PT; q++) {
             size_t sw = o;
             o += ck_switcher(c, sw);
             EQ(S(c, sw + 2), S(c, izr), T, 431);
             EQ(S(c, sw + 3), S(c, gd + q), T, 432);
-            EQ(S(c, sw + 4), S(c, rp + 8 * (size_t)w + q), T, 433);
-            EQ(S(c, d + 8 + q), S(c, sw + 1), T, 435);
+            EQ(S(c, sw + 4), S(c, rp + PT * (size_t)w + q), T, 433);
+            EQ(S(c, d + PT + q), S(c, sw + 1), T, 435);
           }
         } else {
-          for (int q = 0; q < 8; q++) EQ(S(c, d + 8 + q), S(c, dbl_at[i + j - 5] + q), T, 440);
+          for (size_t q = 0; q < PT; q++) EQ(S(c, d + PT + q), S(c, dbl_at[i + j - 5] + q), T, 440);
         }
       }
     }
     size_t gs = o;
-    for (int q = 0; q < 8; q++) o += ck_getsum(c, o, 16);
+    for (size_t q = 0; q < PT; q++) o += ck_getsum(c, o, 16);
     for (int pt = 0; pt < 16; pt++) {
       size_t pe = o;
       o += ck_isequal(c, pe);
       EQ(S(c, pe + 1), KC((uint64_t)pt), T, 457);
       EQ(S(c, pe + 2), S(c, bn), T, 458);
-      for (int q = 0; q < 8; q++) EQ(S(c, gs + 32 * (size_t)q + 1 + pt), MUL(S(c, pe), S(c, pc + 8 * (size_t)pt + q)), T, 461);
+      for (size_t q = 0; q < PT; q++) EQ(S(c, gs + 32 * q + 1 + pt), MUL(S(c, pe), S(c, pc + PT * (size_t)pt + q)), T, 461);
     }
-    for (int q = 0; q < 8; q++) EQ(S(c, ap + 8 * (size_t)w + q), S(c, gs + 32 * (size_t)q), T, 470);
+    for (size_t q = 0; q < PT; q++) EQ(S(c, ap + PT * (size_t)w + q), S(c, gs + 32 * q), T, 470);
     if (i == 0) {
-      for (int q = 0; q < 8; q++) EQ(S(c, rp + 8 + q), S(c, ap + q), T, 476);
+      for (size_t q = 0; q < PT; q++) EQ(S(c, rp + PT + q), S(c, ap + q), T, 476);
     } else {
       size_t ad = o;
       o += ck_ecadd(c, ad);
-      for (int q = 0; q < 8; q++) {
-        EQ(S(c, ad + 8 + q), S(c, dbl_at[i - 1] + q), T, 482);
-        EQ(S(c, ad + 16 + q), S(c, ap + 8 * (size_t)w + q), T, 483);
+      for (size_t q = 0; q < PT; q++) {
+        EQ(S(c, ad + PT + q), S(c, dbl_at[i - 1] + q), T, 482);
+        EQ(S(c, ad + 2 * PT + q), S(c, ap + PT * (size_t)w + q), T, 483);
       }
       size_t iza = o;
       o += ck_isequal(c, iza);
-      EQ(S(c, iza + 1), S(c, ap + 8 * (size_t)w), T, 486);
+      EQ(S(c, iza + 1), S(c, ap + PT * (size_t)w), T, 486);
       EQ(S(c, iza + 2), S(c, gd), T, 487);
-      for (int q = 0; q < 8; q++) {
+      for (size_t q = 0; q < PT; q++) {
         size_t sa = o, sd = o + 6;
         o += 12;
         ck_switcher(c, sa);
@@ -1891,64 +1930,65 @@ static size_t ck_ecmul(ck_t *c, size_t b) {
         EQ(S(c, sa + 3), S(c, ad + q), T, 501);
         EQ(S(c, sa + 4), S(c, dbl_at[i - 1] + q), T, 502);
         EQ(S(c, sd + 2), S(c, izr), T, 504);
-        EQ(S(c, sd + 3), S(c, ap + 8 * (size_t)w + q), T, 505);
+        EQ(S(c, sd + 3), S(c, ap + PT * (size_t)w + q), T, 505);
         EQ(S(c, sd + 4), S(c, sa), T, 506);
-        EQ(S(c, rp + 8 * (size_t)(w + 1) + q), S(c, sd + 1), T, 508);
+        EQ(S(c, rp + PT * (size_t)(w + 1) + q), S(c, sd + 1), T, 508);
       }
     }
   }
-  for (int q = 0; q < 8; q++) EQ(S(c, out + q), S(c, rp + 64 * 8 + q), T, 513);
+  free(dbl_at);
+  for (size_t q = 0; q < PT; q++) EQ(S(c, out + q), S(c, rp + (size_t)NW * PT + q), T, 513);
   return o - b;
 }
 
-/* EllipicCurveScalarGeneratorMult curve.circom:680-906: out[2][K] | scalar[K] | resultCoordinateComputation[32][256][2][K]
- * additionPoints[32][2][K] resultingPointsLeft/Left2/Right/Right2 (never assigned) resultingPoints[32][2][K] |
- * num2bits[4] bits2num[32] getDummy getSecondDummy equal[32][256] getSumOfNElements[32][2][4]
- * (adders isFirstDummyLeft isSecondDummyLeft isFirstDummyRight isSecondDummyRight (switcherRight switcherLeft) x8)[31] */
+/* EllipicCurveScalarGeneratorMult curve.circom:680-906 (NP = K EB / 8 parts): out[2][K] | scalar[K] |
+ * resultCoordinateComputation[NP][256][2][K] additionPoints[NP][2][K] resultingPointsLeft/Left2/Right/Right2 (never
+ * assigned) resultingPoints[NP][2][K] | num2bits[K] bits2num[NP] getDummy getSecondDummy equal[NP][256]
+ * getSumOfNElements[NP][2][K] (adders isFirstDummyLeft isSecondDummyLeft isFirstDummyRight isSecondDummyRight
+ * (switcherRight switcherLeft) x2K)[NP-1] */
 static size_t ck_ecgen(ck_t *c, size_t b) {
   const char *T = "EllipicCurveScalarGeneratorMult ec/curve.circom";
-  const size_t NP = 32, PT = 8;
-  size_t out = b, sc = b + 8, rcc = b + 12, ap = rcc + NP * 256 * PT, unused = ap + NP * PT, rp = unused + 4 * NP * PT,
+  const size_t NP = (size_t)EK * EB / 8, PT = 2 * (size_t)EK;
+  size_t out = b, sc = b + PT, rcc = sc + EK, ap = rcc + NP * 256 * PT, unused = ap + NP * PT, rp = unused + 4 * NP * PT,
          o = rp + NP * PT;
-  size_t n2b[4];
-  for (int i = 0; i < 4; i++) {
+  size_t n2b[7];
+  for (int i = 0; i < EK; i++) {
     n2b[i] = o;
-    o += ck_num2bits(c, o, 64);
-    EQ(S(c, n2b[i] + 64), S(c, sc + i), T, 733);
+    o += ck_num2bits(c, o, EB);
+    EQ(S(c, n2b[i] + EB), S(c, sc + i), T, 733);
   }
-  size_t b2n[32];
-  for (int i = 0; i < 32; i++) {
+  size_t *b2n = malloc(sizeof(size_t) * NP);
+  for (size_t i = 0; i < NP; i++) {
     b2n[i] = o;
     o += ck_bits2num(c, o, 8);
-    for (int j = 0; j < 8; j++) EQ(S(c, b2n[i] + 1 + j), S(c, n2b[(i * 8 + j) / 64] + (i * 8 + j) % 64), T, 739);
+    for (int j = 0; j < 8; j++) EQ(S(c, b2n[i] + 1 + j), S(c, n2b[(i * 8 + j) / EB] + (i * 8 + j) % EB), T, 739);
   }
   size_t gd = o;
   o += ck_getdummy(c, gd);
   size_t g2 = o;
   o += ck_ecdbl(c, g2);
-  for (int q = 0; q < 8; q++) EQ(S(c, g2 + 8 + q), S(c, gd + q), T, 745);
+  for (size_t q = 0; q < PT; q++) EQ(S(c, g2 + PT + q), S(c, gd + q), T, 745);
   for (size_t i = 0; i < NP; i++)
     for (int j = 0; j < 256; j++) {
       size_t e = o;
       o += ck_isequal(c, e);
       EQ(S(c, e + 1), KC((uint64_t)j), T, 751);
       EQ(S(c, e + 2), S(c, b2n[i]), T, 752);
-      for (int q = 0; q < 8; q++) {
+      for (size_t q = 0; q < PT; q++) {
         fr_t v;
         if (j == 0) v = (i % 2 == 0) ? S(c, gd + q) : S(c, g2 + q);
-        else v = L64(GPOW(i, j, q / 4, q % 4));
+        else v = L64(GPOW(i, j, q / EK, q % EK));
         EQ(S(c, rcc + (i * 256 + j) * PT + q), MUL(S(c, e), v), T, j == 0 ? (i % 2 == 0 ? 756 : 764) : 772);
       }
     }
-  size_t gs = o;
   for (size_t i = 0; i < NP; i++)
-    for (int q = 0; q < 8; q++) {
+    for (size_t q = 0; q < PT; q++) {
       size_t g = o;
       o += ck_getsum(c, g, 256);
       for (int j = 0; j < 256; j++) EQ(S(c, g + 1 + j), S(c, rcc + (i * 256 + j) * PT + q), T, 787);
       EQ(S(c, ap + i * PT + q), S(c, g), T, 797);
     }
-  (void)gs;
+  free(b2n);
   for (size_t i = 0; i + 1 < NP; i++) {
     size_t ad = o;
     o += ck_ecadd(c, ad);
@@ -1964,11 +2004,11 @@ static size_t ck_ecgen(ck_t *c, size_t b) {
     EQ(S(c, sl + 2), left0, T, i == 0 ? 839 : 867);
     EQ(S(c, fr + 2), S(c, ap + (i + 1) * PT), T, i == 0 ? 840 : 868);
     EQ(S(c, sr + 2), S(c, ap + (i + 1) * PT), T, i == 0 ? 841 : 869);
-    for (int q = 0; q < 8; q++) {
-      EQ(S(c, ad + 8 + q), i == 0 ? S(c, ap + q) : S(c, rp + (i - 1) * PT + q), T, i == 0 ? 842 : 871);
-      EQ(S(c, ad + 16 + q), S(c, ap + (i + 1) * PT + q), T, i == 0 ? 843 : 872);
+    for (size_t q = 0; q < PT; q++) {
+      EQ(S(c, ad + PT + q), i == 0 ? S(c, ap + q) : S(c, rp + (i - 1) * PT + q), T, i == 0 ? 842 : 871);
+      EQ(S(c, ad + 2 * PT + q), S(c, ap + (i + 1) * PT + q), T, i == 0 ? 843 : 872);
     }
-    for (int q = 0; q < 8; q++) {
+    for (size_t q = 0; q < PT; q++) {
       size_t swr = o, swl = o + 6;
       o += 12;
       ck_switcher(c, swr);
@@ -1982,15 +2022,15 @@ static size_t ck_ecgen(ck_t *c, size_t b) {
       EQ(S(c, rp + i * PT + q), S(c, swl + 1), T, 862);
     }
   }
-  for (int q = 0; q < 8; q++) EQ(S(c, out + q), S(c, rp + (NP - 2) * PT + q), T, 905);
+  for (size_t q = 0; q < PT; q++) EQ(S(c, out + q), S(c, rp + (NP - 2) * PT + q), T, 905);
   return o - b;
 }
 
-/* BigModInv(n, K) bigInt.circom:344-368: out[K] | in[K] modulus[K] | mult */
+/* BigModInv(EB, K) bigInt.circom:344-368: out[K] | in[K] modulus[K] | mult */
 static size_t ck_bminv(ck_t *c, size_t b, int K) {
   const char *T = "BigModInv bigInt/bigInt.circom";
   size_t m = b + 3 * (size_t)K;
-  size_t sz = 3 * (size_t)K + ck_bmm(c, m, K);
+  size_t sz = 3 * (size_t)K + ck_bmm_n(c, m, EB, K);
   size_t md_out = m + K + 1, in1 = md_out + K, in2 = in1 + K, modl = in2 + K;
   for (int i = 0; i < K; i++) {
     EQ(S(c, in1 + i), S(c, b + K + i), T, 357);
@@ -2001,18 +2041,18 @@ static size_t ck_bminv(ck_t *c, size_t b, int K) {
   return sz;
 }
 
-/* verifyECDSABits(64, 4, A, B, P, 256) signatures/ecdsa.circom:18-87: pubkey[2][K] signature[2][K] hashed[256] |
+/* verifyECDSABits(EB, K, A, B, P, K EB) signatures/ecdsa.circom:18-87: pubkey[2][K] signature[2][K] hashed[K EB] |
  * hashedChunked[K] one[K] order[K] sinv[K] | bits2Num[K] getOrder modInv mult mult2 scalarMult1 scalarMult2 add modOrder */
 static size_t ck_ecdsa(ck_t *c, size_t b) {
   const char *T = "verifyECDSABits signatures/ecdsa.circom";
-  const int K = 4;
-  size_t pk = b, sig = b + 8, hs = b + 16, hc = hs + 256, one = hc + K, ord = one + K, sinv = ord + K, o = sinv + K;
+  const int K = EK, PT = 2 * EK;
+  size_t pk = b, sig = b + PT, hs = sig + PT, hc = hs + (size_t)K * EB, one = hc + K, ord = one + K, sinv = ord + K, o = sinv + K;
   EQ(S(c, one), KC(1), T, 27);
   for (int i = 1; i < K; i++) EQ(S(c, one + i), fr_zero(), T, 29);
   for (int i = 0; i < K; i++) {
     size_t bn = o;
-    o += ck_bits2num(c, bn, 64);
-    for (int j = 0; j < 64; j++) EQ(S(c, bn + 1 + 63 - j), S(c, hs + i * 64 + j), T, 36);
+    o += ck_bits2num(c, bn, EB);
+    for (int j = 0; j < EB; j++) EQ(S(c, bn + 1 + EB - 1 - j), S(c, hs + (size_t)i * EB + j), T, 36);
     EQ(S(c, hc + K - 1 - i), S(c, bn), T, 38);
   }
   size_t go = o;  /* EllipicCurveGetOrder ec/get.circom:146: order[K] */
@@ -2027,9 +2067,9 @@ static size_t ck_ecdsa(ck_t *c, size_t b) {
     EQ(S(c, sinv + i), S(c, mi + i), T, 52);
   }
   size_t m1 = o;
-  o += ck_bmm(c, m1, K);
+  o += ck_bmm_n(c, m1, EB, K);
   size_t m2 = o;
-  o += ck_bmm(c, m2, K);
+  o += ck_bmm_n(c, m2, EB, K);
 #define BI1(m) ((m) + 2 * (size_t)K + 1)
   for (int i = 0; i < K; i++) {
     EQ(S(c, BI1(m1) + i), S(c, sinv + i), T, 56);
@@ -2041,19 +2081,19 @@ static size_t ck_ecdsa(ck_t *c, size_t b) {
   }
   size_t g = o;
   o += ck_ecgen(c, g);
-  for (int i = 0; i < K; i++) EQ(S(c, g + 8 + i), S(c, m1 + K + 1 + i), T, 68);
+  for (int i = 0; i < K; i++) EQ(S(c, g + PT + i), S(c, m1 + K + 1 + i), T, 68);
   size_t sm = o;
   o += ck_ecmul(c, sm);
-  for (int i = 0; i < K; i++) EQ(S(c, sm + 16 + i), S(c, m2 + K + 1 + i), T, 72);
-  for (int i = 0; i < 8; i++) EQ(S(c, sm + 8 + i), S(c, pk + i), T, 73);
+  for (int i = 0; i < K; i++) EQ(S(c, sm + 2 * PT + i), S(c, m2 + K + 1 + i), T, 72);
+  for (int i = 0; i < PT; i++) EQ(S(c, sm + PT + i), S(c, pk + i), T, 73);
   size_t ad = o;
   o += ck_ecadd(c, ad);
-  for (int i = 0; i < 8; i++) {
-    EQ(S(c, ad + 8 + i), S(c, g + i), T, 77);
-    EQ(S(c, ad + 16 + i), S(c, sm + i), T, 78);
+  for (int i = 0; i < PT; i++) {
+    EQ(S(c, ad + PT + i), S(c, g + i), T, 77);
+    EQ(S(c, ad + 2 * PT + i), S(c, sm + i), T, 78);
   }
   size_t mo = o;
-  o += ck_bmm(c, mo, K);
+  o += ck_bmm_n(c, mo, EB, K);
   for (int i = 0; i < K; i++) {
     EQ(S(c, BI1(mo) + i), S(c, ad + i), T, 83);
     EQ(S(c, BI1(mo) + K + i), S(c, one + i), T, 84);
@@ -2142,9 +2182,13 @@ static size_t ck_rsa_pkcs160(ck_t *c, size_t b, int K, uint32_t EXP) {
 
 typedef struct { int sig, dg_hash, doc, ec_blocks, ec_shift, dg1_shift, aa, dg15_shift, dg15_blocks, aa_shift; } ck_params;
 
-static int sig_K(int sig) { return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : sig >= 20 ? 4 : 32; }
-/* HASH_TYPE of the EC / SA hashers (passportVerificationBuilder.circom:16-59) */
-static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : sig == 13 ? 384 : 256; }
+static int sig_K(int sig) {
+  return sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : sig >= 20 ? (ec_curve_of(sig) >= 0 ? EC[ec_curve_of(sig)].nl : 4) : 32;
+}
+/* HASH_TYPE of the SA hasher (passportVerificationBuilder.circom:16-59) and EC_HASH_TYPE of the EC hasher (:53: the
+ * HASH_TYPE before SIG 24 sets 224) */
+static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : (sig == 13 || sig == 25) ? 384 : sig == 24 ? 224 : 256; }
+static int ec_hash_t(int sig) { return sig == 24 ? 256 : sig_hash(sig); }
 
 /* PassportVerificationBuilder(...) passportVerificationBuilder.circom:11-246 (RSA PKCS#1 v1.5 over SHA-2):
  * passportHash | encapsulatedContent dg1 dg15 signedAttributes signature pubkey slaveMerkleInclusionBranches[80]
@@ -2153,14 +2197,15 @@ static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : sig == 13 ?
  * signatureVerification signedAttributesNum pubkeyHasherRsa smtVerifier signedAttributesHashHasher */
 static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
   const char *T = "PassportVerificationBuilder passportVerification/passportVerificationBuilder.circom";
-  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = sig_hash(P->sig), HBS = HT > 256 ? 1024 : 512,
+  const int K = sig_K(P->sig), DGH = P->dg_hash, HT = sig_hash(P->sig), EHT = ec_hash_t(P->sig), HBS = HT > 256 ? 1024 : 512,
             DBS = DGH > 256 ? 1024 : 512, ECL = P->ec_blocks * HBS, D15L = P->dg15_blocks * HBS, ecdsa = P->sig >= 20,
             PKL = ecdsa ? 2 * K : K;
   size_t ph = b, ec = b + 1, dg1 = ec + ECL, dg15 = dg1 + 1024, sa = dg15 + D15L, sig = sa + 1024, pk = sig + PKL,
          br = pk + PKL, root = br + 80;
-  /* intermediates: ..., pubkeyHash, then tempModulus[5] (RSA, :170) or ecBitsX[256] ecBitsY[256] (ECDSA, :188-189) */
-  size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + HT, pkh = sah + HT, tmod = pkh + 1,
-         ebx = pkh + 1, eby = ebx + 256, o = ecdsa ? eby + 256 : tmod + 5;
+  /* intermediates: ..., pubkeyHash, then tempModulus[5] (RSA, :170) or ecBitsX[F] ecBitsY[F] (ECDSA, :188-189) */
+  const int EF = ecdsa ? K * EB : 0;
+  size_t d1h = root + 1, d15h = d1h + DGH, ech = d15h + DGH, sah = ech + EHT, pkh = sah + HT, tmod = pkh + 1,
+         ebx = pkh + 1, eby = ebx + EF, o = ecdsa ? eby + EF : tmod + 5;
   size_t hs = o;
   o += ck_shahash(c, hs, 1024 / DBS, DGH);
   for (int j = 0; j < 1024; j++) EQ(S(c, hs + DGH + j), S(c, dg1 + j), T, 104);
@@ -2174,33 +2219,33 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
     for (int j = 0; j < DGH; j++) EQ(S(c, d15h + j), fr_zero(), T, 118);
   }
   hs = o;
-  o += ck_shahash(c, hs, P->ec_blocks, HT);
-  for (int j = 0; j < ECL; j++) EQ(S(c, hs + HT + j), S(c, ec + j), T, 124);
-  for (int j = 0; j < HT; j++) EQ(S(c, ech + j), S(c, hs + j), T, 126);
+  o += ck_shahash(c, hs, P->ec_blocks, EHT);
+  for (int j = 0; j < ECL; j++) EQ(S(c, hs + EHT + j), S(c, ec + j), T, 124);
+  for (int j = 0; j < EHT; j++) EQ(S(c, ech + j), S(c, hs + j), T, 126);
   hs = o;
   o += ck_shahash(c, hs, 1024 / HBS, HT);
   for (int j = 0; j < 1024; j++) EQ(S(c, hs + HT + j), S(c, sa + j), T, 137);
   for (int j = 0; j < HT; j++) EQ(S(c, sah + j), S(c, hs + j), T, 130);
   size_t fl = o;
-  o += ck_flow(c, fl, ECL, DGH, HT, P->dg1_shift, P->aa ? P->dg15_shift : DGH, P->ec_shift, P->aa);
+  o += ck_flow(c, fl, ECL, DGH, EHT, P->dg1_shift, P->aa ? P->dg15_shift : DGH, P->ec_shift, P->aa);
   for (int j = 0; j < DGH; j++) {
     EQ(S(c, fl + 1 + j), S(c, d1h + j), T, 140);
     EQ(S(c, fl + 1 + DGH + j), S(c, d15h + j), T, 141);
   }
   for (int j = 0; j < ECL; j++) EQ(S(c, fl + 1 + 2 * DGH + j), S(c, ec + j), T, 142);
-  for (int j = 0; j < HT; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + j), S(c, ech + j), T, 143);
-  for (int j = 0; j < 1024; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + HT + j), S(c, sa + j), T, 144);
+  for (int j = 0; j < EHT; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + j), S(c, ech + j), T, 143);
+  for (int j = 0; j < 1024; j++) EQ(S(c, fl + 1 + 2 * DGH + ECL + EHT + j), S(c, sa + j), T, 144);
   EQ(S(c, fl), KC(1), T, 146);
   size_t sv = o;  /* VerifySignature(SIG) signatureVerification.circom: pubkey[PK] signature[PK] hashed[HT] | verifier */
   const char *TV = "VerifySignature signatureVerifier/signatureVerification.circom";
   const int PK = ecdsa ? 2 * K : K;
   size_t rsa = sv + 2 * (size_t)PK + HT;
   const int pss = P->sig >= 10 && P->sig <= 14;
-  if (ecdsa) {    /* verifyECDSABits: pubkey[2][4], signature[2][4], hashed */
+  if (ecdsa) {    /* verifyECDSABits: pubkey[2][K], signature[2][K], hashed */
     o += 2 * (size_t)PK + HT + ck_ecdsa(c, rsa);
     for (int i = 0; i < 2 * K; i++) {
       req(c, S(c, rsa + i), S(c, sv + i), TV, 184, sv);
-      req(c, S(c, rsa + 8 + i), S(c, sv + PK + i), TV, 186, sv);
+      req(c, S(c, rsa + 2 * K + i), S(c, sv + PK + i), TV, 186, sv);
     }
   } else if (pss) {  /* VerifyRsaPssSig: pubkey, signature, hashed */
     o += 2 * (size_t)K + HT + ck_pss(c, rsa, K, P->sig == 12 ? 64 : P->sig == 13 ? 48 : 32, P->sig == 10 ? 3 : 65537, HT);
@@ -2237,22 +2282,27 @@ static size_t ck_pvb(ck_t *c, size_t b, const ck_params *P) {
       EQ(S(c, pkr + 1 + i), ADD(S(c, tmod + i), S(c, pk + 3 * i + 2)), T, 177);
     }
     EQ(S(c, pkh), S(c, pkr), T, 179);
-  } else {  /* :184-218, EC_FIELD_SIZE 256, DIFF 8 */
+  } else {  /* :184-218, EC_FIELD_SIZE EF = K x EB, DIFF = EF - 248 above 248 bits */
+    const int DF = EF > 248 ? EF - 248 : 0, NB = EF - DF;
     for (int i = 0; i < K; i++) {
-      size_t nx = o, ny = o + 129;
-      o += ck_num2bits(c, nx, 64) + ck_num2bits(c, ny, 64);
-      EQ(S(c, nx + 64), S(c, pk + i), T, 195);
-      EQ(S(c, ny + 64), S(c, pk + i + K), T, 196);
-      for (int j = 0; j < 64; j++) {
-        EQ(S(c, ebx + 255 - j - 64 * i), S(c, nx + j), T, 199);
-        EQ(S(c, eby + 255 - j - 64 * i), S(c, ny + j), T, 200);
+      size_t nx = o;
+      o += ck_num2bits(c, nx, EB);
+      size_t ny = o;
+      o += ck_num2bits(c, ny, EB);
+      EQ(S(c, nx + EB), S(c, pk + i), T, 195);
+      EQ(S(c, ny + EB), S(c, pk + i + K), T, 196);
+      for (int j = 0; j < EB; j++) {
+        EQ(S(c, ebx + EF - 1 - j - EB * i), S(c, nx + j), T, 199);
+        EQ(S(c, eby + EF - 1 - j - EB * i), S(c, ny + j), T, 200);
       }
     }
-    size_t xn = o, yn = o + 497;
-    o += ck_bits2num(c, xn, 248) + ck_bits2num(c, yn, 248);
-    for (int i = 0; i < 248; i++) {
-      EQ(S(c, xn + 1 + 247 - i), S(c, ebx + i + 8), T, 212);
-      EQ(S(c, yn + 1 + 247 - i), S(c, eby + i + 8), T, 213);
+    size_t xn = o;
+    o += ck_bits2num(c, xn, NB);
+    size_t yn = o;
+    o += ck_bits2num(c, yn, NB);
+    for (int i = 0; i < NB; i++) {
+      EQ(S(c, xn + 1 + NB - 1 - i), S(c, ebx + i + DF), T, 212);
+      EQ(S(c, yn + 1 + NB - 1 - i), S(c, eby + i + DF), T, 213);
     }
     size_t h = o;
     o += ck_poseidon(c, h, 2);
@@ -2439,15 +2489,16 @@ int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r) {
   return ck_end(&c, walked, r);
 }
 
-/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-14), ECDSA P-256 / brainpoolP256r1
- * (SIG 20 / 21), DG hash 160 / 224 / 256 / 384 */
+/* RegisterIdentityBuilder as main: RSA PKCS#1 v1.5 (SIG 1-4), RSA-PSS (SIG 10-14), ECDSA P-256 / brainpoolP256r1 /
+ * P-224 / brainpoolP384r1 (SIG 20 / 21 / 24 / 25), DG hash 160 / 224 / 256 / 384 */
 int ck_register(const ck_params *P, const uint8_t *wit, size_t nw, ck_report *r) {
   if (!pos_loaded) return -1;
-  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 14) || P->sig == 20 || P->sig == 21) ||
+  if (!((P->sig >= 1 && P->sig <= 4) || (P->sig >= 10 && P->sig <= 14) || ec_curve_of(P->sig) >= 0) ||
       !(P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160 || P->dg_hash == 384))
     return -2;
   if (P->sig >= 20) {
-    CV = &EC[P->sig - 20];
+    CV = &EC[ec_curve_of(P->sig)];
+    EK = CV->nl; EB = CV->cs;
     if (!CV->gpow) return -3;
   }
   ck_t c = ck_begin(wit, nw);

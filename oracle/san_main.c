@@ -50,10 +50,10 @@ int ck_poseidon_circuit(int n, const uint8_t *wit, size_t nw, ck_report *r);
 
 static int load_all(const char *dir) {
   char path[4096];
-  static const char *ec[2] = {"p256_gpow8.bin", "bp256_gpow8.bin"};
+  static const char *ec[4] = {"p256_gpow8.bin", "bp256_gpow8.bin", "p224_gpow8.bin", "bp384_gpow8.bin"};
   snprintf(path, sizeof path, "%s/poseidon_t2_6.bin", dir);
   if (orc_load_poseidon(path) || ck_load_poseidon(path)) return 1;
-  for (int c = 0; c < 2; c++) {
+  for (int c = 0; c < 4; c++) {
     snprintf(path, sizeof path, "%s/%s", dir, ec[c]);
     if (orc_load_ec_table(c, path) || ck_load_ec_table(c, path)) return 2;
   }

@@ -1143,11 +1143,12 @@ static void run_bgt(ctx_t *c, size_t b, int n, int K) {
 
 /* BigIntIsZero(n,MAX,K) bigIntComparators.circom:105-129: in[K] | carry[K-1] | carryRangeChecks[K-1] */
 static size_t sz_bisz(int n, int MAX, int K) { return (size_t)K + (K - 1) + (size_t)(K - 1) * sz_num2bits(MAX + 3 - n); }
-static fr_t INV2_64;
+static fr_t INV2_64, INV2_N[65];
 static void run_bisz(ctx_t *c, size_t b, int n, int MAX, int K) {
   int L = MAX + 3 - n;
   size_t in = b, carry = b + K, sub = carry + K - 1, per = sz_num2bits(L);
-  fr_t inv = (n == 64) ? INV2_64 : fr_inv(POW2[n]);
+  if (n != 64 && fr_is_zero(INV2_N[n])) INV2_N[n] = fr_inv(POW2[n]);
+  fr_t inv = (n == 64) ? INV2_64 : INV2_N[n];
   for (int i = 0; i < K - 1; i++) {
     fr_t v = i == 0 ? W(in) : fr_add(W(in + i), W(carry + i - 1));
     W(carry + i) = fr_mul(v, inv);
@@ -1215,6 +1216,34 @@ static void mp_divmod(const uint64_t *a, int na, const uint64_t *b, int nb, uint
   for (int i = 0; i < nb; i++) r[i] = (u[i] >> s) | (s && i + 1 <= nb ? u[i + 1] << (64 - s) : 0);
 }
 
+/* acc (AW words, two's complement) += / -= mag (4 words) << sh bits */
+static void acc_shifted(uint64_t *acc, int AW, const uint64_t *mag, int sh, int neg) {
+  uint64_t t[6] = {0};
+  int s = sh & 63, w0 = sh >> 6;
+  for (int w = 0; w < 4; w++) {
+    t[w] |= mag[w] << s;
+    if (s) t[w + 1] |= mag[w] >> (64 - s);
+  }
+  uint64_t cy = 0;
+  for (int w = 0; w + w0 < AW; w++) {
+    uint64_t v = w < 6 ? t[w] : 0;
+    if (!neg) {
+      u128 x = (u128)acc[w + w0] + v + cy;
+      acc[w + w0] = (uint64_t)x; cy = (uint64_t)(x >> 64);
+    } else {
+      u128 x = (u128)acc[w + w0] - v - cy;
+      acc[w + w0] = (uint64_t)x; cy = (uint64_t)(x >> 64) & 1;
+    }
+  }
+}
+/* chunk j (n bits) of the word array a */
+static uint64_t word_chunk(const uint64_t *a, int n, int j) {
+  int off = n * j;
+  uint64_t v = a[off >> 6] >> (off & 63);
+  if ((off & 63) + n > 64) v |= a[(off >> 6) + 1] << (64 - (off & 63));
+  return n == 64 ? v : v & ((1ULL << n) - 1);
+}
+
 /* BigMultModP(n,G,L,M) bigInt.circom:206-272:
  * div[DIV], mod[M] | in1[G], in2[L], modulus[M] | mult, modChecks[M], greaterThan, mult2, isZero */
 static size_t sz_bmmp(int n, int G, int L, int M) {
@@ -1235,14 +1264,27 @@ static void run_bmmp(ctx_t *c, size_t b, int n, int G, int L, int M) {
   run_bmo(c, mult, G, L);
   /* witness-time reduce_overflow + long_div (unconstrained) */
   uint64_t red[160], modl[80], q[90], r[80];
-  reduce_overflow(&W(mult), BASE - 1, BASE, red);
-  for (int i = 0; i < M; i++) modl[i] = W(mo + i).l[0];
-  int nb = M;
-  while (nb > 1 && modl[nb - 1] == 0) nb--;
   memset(q, 0, sizeof q); memset(r, 0, sizeof r);
-  mp_divmod(red, BASE, modl, nb, q, r);
+  if (n == 64) {
+    reduce_overflow(&W(mult), BASE - 1, BASE, red);
+    for (int i = 0; i < M; i++) modl[i] = W(mo + i).l[0];
+    int nb = M;
+    while (nb > 1 && modl[nb - 1] == 0) nb--;
+    mp_divmod(red, BASE, modl, nb, q, r);
+  } else { /* n < 64 chunks: the same quotient / remainder computed on words, then re-chunked */
+    uint64_t qw[90] = {0}, rw[80] = {0};
+    int aw = (n * BASE + 63) / 64 + 4;
+    memset(red, 0, sizeof red); memset(modl, 0, sizeof modl);
+    for (int i = 0; i < BASE - 1; i++) acc_shifted(red, aw, W(mult + i).l, n * i, 0);
+    for (int i = 0; i < M; i++) modl[(n * i) >> 6] |= W(mo + i).l[0] << ((n * i) & 63);
+    int nb = (n * M + 63) / 64;
+    while (nb > 1 && modl[nb - 1] == 0) nb--;
+    mp_divmod(red, aw, modl, nb, qw, rw);
+    for (int i = 0; i < DIV; i++) q[i] = word_chunk(qw, n, i);
+    for (int i = 0; i < M; i++) r[i] = word_chunk(rw, n, i);
+  }
   for (int i = 0; i < DIV; i++) W(dv + i) = fr_u64(q[i]);
-  for (int i = 0; i < M; i++) W(md + i) = fr_u64(i < nb ? r[i] : 0);
+  for (int i = 0; i < M; i++) W(md + i) = fr_u64(r[i]);
   for (int i = 0; i < M; i++) {
     size_t nc = mchk + (size_t)i * sz_num2bits(n);
     W(nc + n) = W(md + i);
@@ -1497,7 +1539,7 @@ static void run_verifysig_pss(ctx_t *c, size_t b, int K, int sig) {
   run_pss(c, v, K, pss_salt(sig), sig_exp(sig), H);
 }
 
-#include "ecdsa_p256.inc.c"
+#include "ecdsa.inc.c"
 
 /* ======================================================== SMT (depth 80) */
 static size_t sz_smthash1(void) { return 3 + sz_poseidon(3); }
@@ -1605,41 +1647,49 @@ static void run_flow(ctx_t *c, size_t b, int ecLen, int H, int EH, int dg1s, int
 
 /* ============================================ PassportVerificationBuilder */
 static int sig_chunks(int sig) { return sig == 2 ? 64 : (sig == 14 || sig == 4) ? 48 : 32; }
-/* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x 4 limbs for ECDSA */
-static int sig_len(int sig) { return sig >= 20 ? 8 : sig_chunks(sig); }
+/* signature / pubkey input lengths (registerIdentityBuilder.circom:131-140): 2 x CHUNK_NUMBER chunks for ECDSA */
+static int sig_len(int sig) { return sig >= 20 ? 2 * (ec_index(sig) >= 0 ? EC_CURVES[ec_index(sig)].nl : 4) : sig_chunks(sig); }
 
-/* HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:19-50): 160 for
- * SIG 3 / 4, 384 for SIG 13; inputs hashed with it come in HASH_BLOCK_SIZE = 512 / 1024-bit blocks (:61-68) */
-static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : sig == 13 ? 384 : 256; }
+/* HASH_TYPE of the signed attributes (passportVerificationBuilder.circom:16-59): 160 for SIG 3 / 4, 384 for SIG 13 / 25,
+ * 224 for SIG 24; inputs hashed with it come in HASH_BLOCK_SIZE = 512 / 1024-bit blocks (:65-68) */
+static int sig_hash(int sig) { return (sig == 3 || sig == 4) ? 160 : (sig == 13 || sig == 25) ? 384 : sig == 24 ? 224 : 256; }
+/* EC_HASH_TYPE, the encapsulated content's hash (:53-59): HASH_TYPE before SIG 24 sets it to 224, so 256 there */
+static int ec_hash(int sig) { return sig == 24 ? 256 : sig_hash(sig); }
+/* EC_FIELD_SIZE = CHUNK_NUMBER x CHUNK_SIZE bits of the ECDSA pubkey hash (:196), and its DIFF (:214-217) */
+static int ec_field(int sig) { const ec_curve_t *C = &EC_CURVES[ec_index(sig)]; return C->nl * C->cs; }
+static int ec_diff(int sig) { return ec_field(sig) > 248 ? ec_field(sig) - 248 : 0; }
 static int hblock(int algo) { return algo > 256 ? 1024 : 512; }
 static size_t sz_pvb(const orc_params *P) {
-  int DG = P->dg_hash, HT = sig_hash(P->sig);
+  int DG = P->dg_hash, HT = sig_hash(P->sig), EH = ec_hash(P->sig);
   int K = sig_len(P->sig), ecLen = P->ec_blocks * hblock(HT), dg15Len = P->dg15_blocks * hblock(HT), ec = P->sig >= 20;
-  /* own: ..., dg1Hash[DG], dg15Hash[DG], ecHash[HT], saHash[HT], pubkeyHash, then tempModulus[5] (RSA, :184) or
-   * ecBitsX[256], ecBitsY[256] (ECDSA, :197-198) */
-  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 2 * (size_t)DG + 2 * (size_t)HT + 1 + (ec ? 512 : 5);
-  size_t pkh = ec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
-  return own + sz_hashc(DG, 1024 / hblock(DG)) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(HT, P->ec_blocks) +
+  /* own: ..., dg1Hash[DG], dg15Hash[DG], ecHash[EH], saHash[HT], pubkeyHash, then tempModulus[5] (RSA, :184) or
+   * ecBitsX[F], ecBitsY[F] (ECDSA, :197-198) */
+  const int F = ec ? ec_field(P->sig) : 0;
+  size_t own = 1 + (size_t)ecLen + 1024 + dg15Len + 1024 + K + K + 80 + 1 + 2 * (size_t)DG + EH + HT + 1 + (ec ? 2 * (size_t)F : 5);
+  size_t pkh = ec ? (size_t)K * sz_num2bits(EC_CURVES[ec_index(P->sig)].cs) + 2 * sz_bits2num(F - ec_diff(P->sig)) + sz_poseidon(2)
+                  : sz_poseidon(5);
+  return own + sz_hashc(DG, 1024 / hblock(DG)) + (P->aa ? sz_hashc(DG, P->dg15_blocks) : 0) + sz_hashc(EH, P->ec_blocks) +
          sz_hashc(HT, 1024 / hblock(HT)) +
-         sz_flow(ecLen, DG, HT) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig))) +
+         sz_flow(ecLen, DG, EH) + (ec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig))) +
          sz_bits2num(252) + pkh + sz_smt(80) + sz_poseidon(1);
 }
 static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
-  int DG = P->dg_hash, HT = sig_hash(P->sig);
+  int DG = P->dg_hash, HT = sig_hash(P->sig), EH = ec_hash(P->sig);
   int K = sig_len(P->sig), ecLen = P->ec_blocks * hblock(HT), dg15Len = P->dg15_blocks * hblock(HT), isec = P->sig >= 20;
   const int dg1B = 1024 / hblock(DG), saB = 1024 / hblock(HT), dg15HB = P->dg15_blocks * hblock(DG);
   size_t ec = b + 1, dg1 = ec + ecLen, dg15 = dg1 + 1024, sa = dg15 + dg15Len, sig = sa + 1024, pk = sig + K,
-         br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + DG, ecH = dg15H + DG, saH = ecH + HT,
+         br = pk + K, root = br + 80, dg1H = root + 1, dg15H = dg1H + DG, ecH = dg15H + DG, saH = ecH + EH,
          pkHash = saH + HT, tmpMod = pkHash + 1;
-  size_t p = tmpMod + (isec ? 512 : 5);
+  const int F = isec ? ec_field(P->sig) : 0, FD = isec ? F - ec_diff(P->sig) : 0, CS = isec ? F / (K / 2) : 64;
+  size_t p = tmpMod + (isec ? 2 * (size_t)F : 5);
   size_t hDg1 = p; p += sz_hashc(DG, dg1B);
   size_t hDg15 = 0; if (P->aa) { hDg15 = p; p += sz_hashc(DG, P->dg15_blocks); }
-  size_t hEc = p; p += sz_hashc(HT, P->ec_blocks);
+  size_t hEc = p; p += sz_hashc(EH, P->ec_blocks);
   size_t hSa = p; p += sz_hashc(HT, saB);
-  size_t flow = p; p += sz_flow(ecLen, DG, HT);
+  size_t flow = p; p += sz_flow(ecLen, DG, EH);
   size_t vs = p; p += isec ? sz_verifysig_ec() : is_pss(P->sig) ? sz_verifysig_pss(K, P->sig) : sz_verifysig(K, HT, sig_exp(P->sig));
   size_t saNum = p; p += sz_bits2num(252);
-  size_t pkH = p; p += isec ? 8 * sz_num2bits(64) + 2 * sz_bits2num(248) + sz_poseidon(2) : sz_poseidon(5);
+  size_t pkH = p; p += isec ? (size_t)K * sz_num2bits(CS) + 2 * sz_bits2num(FD) + sz_poseidon(2) : sz_poseidon(5);
   size_t smt = p; p += sz_smt(80);
   size_t saHH = p;
   /* hashes */
@@ -1654,21 +1704,21 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
   } else {
     for (int i = 0; i < DG; i++) W(dg15H + i) = fr_zero();
   }
-  for (int i = 0; i < ecLen; i++) W(hEc + HT + i) = W(ec + i);
-  run_hashc(c, hEc, HT, P->ec_blocks);
-  for (int i = 0; i < HT; i++) W(ecH + i) = W(hEc + i);
+  for (int i = 0; i < ecLen; i++) W(hEc + EH + i) = W(ec + i);
+  run_hashc(c, hEc, EH, P->ec_blocks);
+  for (int i = 0; i < EH; i++) W(ecH + i) = W(hEc + i);
   for (int i = 0; i < 1024; i++) W(hSa + HT + i) = W(sa + i);
   run_hashc(c, hSa, HT, saB);
   for (int i = 0; i < HT; i++) W(saH + i) = W(hSa + i);
   /* flow */
   {
-    size_t h1 = flow + 1, h15 = h1 + DG, fec = h15 + DG, fech = fec + ecLen, fsa = fech + HT;
+    size_t h1 = flow + 1, h15 = h1 + DG, fec = h15 + DG, fech = fec + ecLen, fsa = fech + EH;
     for (int i = 0; i < DG; i++) { W(h1 + i) = W(dg1H + i); W(h15 + i) = W(dg15H + i); }
-    for (int i = 0; i < HT; i++) W(fech + i) = W(ecH + i);
+    for (int i = 0; i < EH; i++) W(fech + i) = W(ecH + i);
     for (int i = 0; i < ecLen; i++) W(fec + i) = W(ec + i);
     for (int i = 0; i < 1024; i++) W(fsa + i) = W(sa + i);
     int dg15shift = P->aa ? P->dg15_shift : DG;
-    run_flow(c, flow, ecLen, DG, HT, P->dg1_shift, dg15shift, P->ec_shift, P->aa);
+    run_flow(c, flow, ecLen, DG, EH, P->dg1_shift, dg15shift, P->ec_shift, P->aa);
     if (!fr_eq(W(flow), ONE()) && !c->err) c->err = S_FLOW;
   }
   /* signature */
@@ -1687,17 +1737,18 @@ static void run_pvb(ctx_t *c, size_t b, const orc_params *P) {
     }
     run_poseidon(c, pkH, 5);
     W(pkHash) = W(pkH);
-  } else { /* ECDSA pubkey hash (:193-230): Poseidon2 of the low 248 bits of x and y */
-    size_t bx = tmpMod, by = bx + 256, n2b = pkH, per = sz_num2bits(64);
-    size_t xn = n2b + 8 * per, yn = xn + sz_bits2num(248), ph = yn + sz_bits2num(248);
-    for (int i = 0; i < 4; i++) {
+  } else { /* ECDSA pubkey hash (:193-230): Poseidon2 of the low F - DIFF = min(F, 248) bits of x and y */
+    const int N = K / 2, D = F - FD;
+    size_t bx = tmpMod, by = bx + F, n2b = pkH, per = sz_num2bits(CS);
+    size_t xn = n2b + (size_t)K * per, yn = xn + sz_bits2num(FD), ph = yn + sz_bits2num(FD);
+    for (int i = 0; i < N; i++) {
       size_t nx = n2b + (size_t)(2 * i) * per, ny = nx + per;
-      W(nx + 64) = W(pk + i); run_num2bits(c, nx, 64);
-      W(ny + 64) = W(pk + 4 + i); run_num2bits(c, ny, 64);
-      for (int j = 0; j < 64; j++) { W(bx + 255 - j - 64 * i) = W(nx + j); W(by + 255 - j - 64 * i) = W(ny + j); }
+      W(nx + CS) = W(pk + i); run_num2bits(c, nx, CS);
+      W(ny + CS) = W(pk + N + i); run_num2bits(c, ny, CS);
+      for (int j = 0; j < CS; j++) { W(bx + F - 1 - j - CS * i) = W(nx + j); W(by + F - 1 - j - CS * i) = W(ny + j); }
     }
-    for (int i = 0; i < 248; i++) { W(xn + 1 + 247 - i) = W(bx + i + 8); W(yn + 1 + 247 - i) = W(by + i + 8); }
-    run_bits2num(c, xn, 248); run_bits2num(c, yn, 248);
+    for (int i = 0; i < FD; i++) { W(xn + 1 + FD - 1 - i) = W(bx + i + D); W(yn + 1 + FD - 1 - i) = W(by + i + D); }
+    run_bits2num(c, xn, FD); run_bits2num(c, yn, FD);
     W(ph + 1) = W(xn); W(ph + 2) = W(yn);
     run_poseidon(c, ph, 2);
     W(pkHash) = W(ph);
@@ -1791,13 +1842,13 @@ static void orc_init(void) {
   orc_init_done = 1;
 }
 
-/* The flow reads encapsulatedContentHash[i] for i < DG_HASH_TYPE (passportVerificationFlow.circom:36-40), so DG <= HT;
+/* The flow reads encapsulatedContentHash[i] for i < DG_HASH_TYPE (passportVerificationFlow.circom:36-40), so DG <= EC_HASH_TYPE;
  * RegisterIdentity's dg15 (DG15_SIZE x DG_HASH_BLOCK_SIZE) is assigned from an input of DG15_BLOCK_NUMBER x
  * HASH_BLOCK_SIZE (registerIdentityBuilder.circom:151), so the block sizes agree or there is no dg15 */
 static int params_ok(const orc_params *P) {
   const int HT = sig_hash(P->sig);
-  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || ((P->sig == 20 || P->sig == 21) && EC_GPOW_T[P->sig - 20])) &&
-         (P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160 || P->dg_hash == 384) && P->dg_hash <= HT &&
+  return ((P->sig >= 1 && P->sig <= 4) || is_pss(P->sig) || (ec_index(P->sig) >= 0 && EC_GPOW_T[ec_index(P->sig)])) &&
+         (P->dg_hash == 256 || P->dg_hash == 224 || P->dg_hash == 160 || P->dg_hash == 384) && P->dg_hash <= ec_hash(P->sig) &&
          (hblock(P->dg_hash) == hblock(HT) || P->dg15_blocks == 0) && (P->doc == 1 || P->doc == 3) && (P->aa >= 0 && P->aa <= 25) &&
          P->ec_blocks > 0 && P->ec_blocks <= 16 && P->dg15_blocks >= 0 && P->dg15_blocks <= 16;
 }
@@ -1810,6 +1861,7 @@ size_t orc_register_n_inputs(const orc_params *P) {
 size_t orc_register_witness_size(const orc_params *P) {
   if (!pos_loaded || !params_ok(P)) return 0;
   orc_init();
+  if (P->sig >= 20) ec_select(ec_index(P->sig));
   return 1 + 4 + orc_register_n_inputs(P) + sz_pvb(P) + sz_regid(P);
 }
 
@@ -1819,7 +1871,7 @@ int orc_register_witness(const orc_params *P, const uint8_t *inputs, uint8_t *wi
   if (!pos_loaded || !params_ok(P)) return -1;
   orc_init();
   ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
-  if (P->sig >= 20) ec_select(P->sig - 20);
+  if (P->sig >= 20) ec_select(ec_index(P->sig));
   size_t nIn = orc_register_n_inputs(P), nW = orc_register_witness_size(P);
   memset(wit, 0, nW * 32);
   W(0) = ONE();

@@ -225,7 +225,27 @@ BP256 = Curve("brainpoolP256r1",
               n=0xA9FB57DBA1EEA9BC3E660A909D838D718C397AA3B561A6F7901E0E82974856A7,
               g=(0x8BD2AEB9CB7E57CB2C4B482FFC81B7AFB9DE27E1E3BD23C23A4453BD9ACE3262,
                  0x547EF835C3DAC4FD97F8461A14611DC9C27745132DED8E545C1D54C72F046997))
-EC_CURVES = {20: P256, 21: BP256}  # SIGNATURE_TYPE -> curve
+# secp224r1, FIPS 186-4 D.1.2.2 (SIGNATURE_TYPE 24: 7 x 32-bit chunks, signatureVerification.circom:230-243)
+P224 = Curve("secp224r1",
+             p=0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFF000000000000000000000001,
+             a=0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFFFFFFFFFFFFFFFFFFFE,
+             b=0xB4050A850C04B3ABF54132565044B0B7D7BFD8BA270B39432355FFB4,
+             n=0xFFFFFFFFFFFFFFFFFFFFFFFFFFFF16A2E0B8F03E13DD29455C5C2A3D,
+             g=(0xB70E0CBD6BB4BF7F321390B94A03C1D356C21122343280D6115C1D21,
+                0xBD376388B5F723FB4C22DFE6CD4375A05A07476444D5819985007E34))
+# brainpoolP384r1, RFC 5639 3.6 (SIGNATURE_TYPE 25: 6 x 64-bit chunks, signatureVerification.circom:245-258)
+BP384 = Curve("brainpoolP384r1",
+              p=0x8CB91E82A3386D280F5D6F7E50E641DF152F7109ED5456B412B1DA197FB71123ACD3A729901D1A71874700133107EC53,
+              a=0x7BC382C63D8C150C3C72080ACE05AFA0C2BEA28E4FB22787139165EFBA91F90F8AA5814A503AD4EB04A8C7DD22CE2826,
+              b=0x04A8C7DD22CE28268B39B55416F0447C2FB77DE107DCD2A62E880EA53EEB62D57CB4390295DBC9943AB78696FA504C11,
+              n=0x8CB91E82A3386D280F5D6F7E50E641DF152F7109ED5456B31F166E6CAC0425A7CF3AB6AF6B7FC3103B883202E9046565,
+              g=(0x1D1C64F068CF45FFA2A63A81B7C13F6B8847A3E77EF14FE3DB7FCAFE0CBD10E8E826E03436D646AAEF87B2E247D4AF1E,
+                 0x8ABE1D7520F9C2A45CB1EB8E95CFD55262B70B29FEEC5864E19C054FF99129280E4646217791811142820341263C5315))
+EC_CURVES = {20: P256, 21: BP256, 24: P224, 25: BP384}  # SIGNATURE_TYPE -> curve
+# SIGNATURE_TYPE -> (CHUNK_NUMBER, CHUNK_SIZE) of the ECDSA inputs and templates (registerIdentityBuilder.circom:81-99).
+# 22 (brainpoolP320r1, 5 x 64) and 23 (secp192r1, 3 x 64) read hashed[] out of bounds in verifyECDSABits
+# (ecdsa.circom:31-37: CHUNK_NUMBER x CHUNK_SIZE = 320 / 192 bits of a 256 / 160-bit hash): no circuit compiles.
+EC_CHUNKS = {20: (4, 64), 21: (4, 64), 24: (7, 32), 25: (6, 64)}
 
 P256_P, P256_A, P256_N, P256_G = P256.p, P256.a, P256.n, P256.g
 
@@ -239,18 +259,20 @@ def p256_mul(k, pt=P256_G):
 
 
 class EcKey:
-    """ECDSA signer key (SIG 20: P-256, SIG 21: brainpoolP256r1)."""
+    """ECDSA signer key (SIG 20: P-256, 21: brainpoolP256r1, 24: P-224 with SHA-224, 25: brainpoolP384r1 with SHA-384)."""
 
-    def __init__(self, rng, curve=P256):
+    def __init__(self, rng, curve=P256, hash_fn=None):
         self.curve = curve
+        self.hash_fn = hash_fn or hashlib.sha256
         self.d = 1 + rng.below(curve.n - 1)
         self.q = curve.mul(self.d)
         self.n = self.q  # the "pubkey" of the passport dict: (x, y)
 
     def sign(self, msg: bytes, rng):
-        """ECDSA-SHA256 (r, s); h = the digest as an integer, not reduced (ecdsa.circom:30-38)."""
+        """ECDSA (r, s) over the instance's hash; h = the digest as an integer, not reduced (ecdsa.circom:30-38:
+        its CHUNK_NUMBER x CHUNK_SIZE bits are exactly the hash's)."""
         c = self.curve
-        h = int.from_bytes(hashlib.sha256(msg).digest(), "big")
+        h = int.from_bytes(self.hash_fn(msg).digest(), "big")
         while True:
             k = 1 + rng.below(c.n - 1)
             r = c.mul(k)[0] % c.n
@@ -259,15 +281,21 @@ class EcKey:
                 return r, s
 
 
-def ecdsa_pk_hash(q):
-    """Poseidon2 of the low 248 bits of x and y (passportVerificationBuilder.circom:193-230)."""
-    m = (1 << 248) - 1
+def ecdsa_pk_hash(q, field_bits=256):
+    """Poseidon2 of the low min(EC_FIELD_SIZE, 248) bits of x and y (passportVerificationBuilder.circom:193-230)."""
+    m = (1 << min(field_bits, 248)) - 1
     return poseidon([q[0] & m, q[1] & m])
 
 
 def sig_hash_type(sig):
-    """HASH_TYPE of the signed attributes / encapsulated content (passportVerificationBuilder.circom:16-59)."""
-    return 160 if sig in (3, 4) else 384 if sig == 13 else 256
+    """HASH_TYPE of the signed attributes / encapsulated content (registerIdentityBuilder.circom:54-99)."""
+    return 160 if sig in (3, 4) else 384 if sig in (13, 25) else 224 if sig == 24 else 256
+
+
+def ec_hash_type(sig):
+    """EC_HASH_TYPE, the encapsulated content's hash (passportVerificationBuilder.circom:53-59): HASH_TYPE as set
+    before SIG 24 switches it to 224, so SHA-256 for SIG 24."""
+    return 256 if sig == 24 else sig_hash_type(sig)
 
 
 def hash_block(algo):
@@ -280,13 +308,15 @@ HASHES = {160: hashlib.sha1, 224: hashlib.sha224, 256: hashlib.sha256, 384: hash
 
 def sig_input_len(sig):
     """signature / pubkey input lengths (registerIdentityBuilder.circom:131-140)."""
-    return 8 if sig >= 20 else 64 if sig == 2 else 48 if sig in (4, 14) else 32
+    return 2 * EC_CHUNKS[sig][0] if sig >= 20 else 64 if sig == 2 else 48 if sig in (4, 14) else 32
 
 
 def sig_limbs(v, sig):
-    """RSA: integer -> K limbs; ECDSA: (a, b) -> 4 + 4 limbs (process_passport.js:125-135)."""
+    """RSA: integer -> K 64-bit limbs; ECDSA: (a, b) -> 2 x CHUNK_NUMBER chunks of CHUNK_SIZE bits
+    (process_passport.js:125-135)."""
     if sig >= 20:
-        return chunk_limbs(v[0], 64, 4) + chunk_limbs(v[1], 64, 4)
+        k, n = EC_CHUNKS[sig]
+        return chunk_limbs(v[0], n, k) + chunk_limbs(v[1], n, k)
     return chunk_limbs(v, 64, sig_input_len(sig))
 
 
@@ -299,9 +329,9 @@ def instance_params(sig):
     """The canonical instance with SIGNATURE_TYPE sig (SIG 3 / 4 hash with SHA-1 and need DG_HASH_TYPE 160).
     SIG 13 hashes with SHA-384 in 1024-bit blocks: DG_HASH_TYPE 384, and the block counts / EC_SHIFT the
     synthetic messages fit (EC and the RSA-1024 DG15 pad to 2 blocks; the SA, one block, holds at most 111 bytes)."""
-    if sig == 13:
-        return dict(CANONICAL, sig=13, dg_hash=384, ec_blocks=2, dg15_blocks=2, ec_shift=336)
-    return dict(CANONICAL, sig=sig, dg_hash=160 if sig in (3, 4) else 256)
+    if sig in (13, 25):  # SHA-384 EC / SA hashers (SIG 25: ECDSA brainpoolP384r1)
+        return dict(CANONICAL, sig=sig, dg_hash=384, ec_blocks=2, dg15_blocks=2, ec_shift=336)
+    return dict(CANONICAL, sig=sig, dg_hash=160 if sig in (3, 4) else 224 if sig == 24 else 256)
 
 _MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789<"
 _DG15_PREFIX = bytes.fromhex("6f81a230819f300d06092a864886f70d010101050003818d00308189028181")
@@ -327,6 +357,10 @@ def _keygen(args):
         return EcKey(rng)
     if bits == "bp256":
         return EcKey(rng, BP256)
+    if bits == "p224":
+        return EcKey(rng, P224, hashlib.sha224)
+    if bits == "bp384":
+        return EcKey(rng, BP384, hashlib.sha384)
     return RsaKey(bits, rng, e)
 
 
@@ -347,7 +381,7 @@ class PassportGen:
             self.keys = list(keys)
             return
         if self.params["sig"] >= 20:
-            key_bits = "bp256" if self.params["sig"] == 21 else "p256"
+            key_bits = {20: "p256", 21: "bp256", 24: "p224", 25: "bp384"}[self.params["sig"]]
         elif self.params["sig"] == 2 and key_bits == 2048:
             key_bits = 4096
         elif self.params["sig"] in (4, 14) and key_bits == 2048:
@@ -395,7 +429,7 @@ class PassportGen:
         h = self._pkhash.get(key.n)
         if h is None:
             if isinstance(key, EcKey):
-                h = ecdsa_pk_hash(key.q)
+                h = ecdsa_pk_hash(key.q, key.curve.p.bit_length())  # EC_FIELD_SIZE = CHUNK_NUMBER x CHUNK_SIZE
             else:
                 a = chunk_limbs(key.n, 64, 15)
                 h = poseidon([(a[3 * i] << 128) + (a[3 * i + 1] << 64) + a[3 * i + 2] for i in range(5)])
@@ -415,7 +449,7 @@ class PassportGen:
         bs = hash_block(ht) // 8
         ec_len = 219 + rng.below(pr["ec_blocks"] * bs - (bs // 8 + 1) - 219 + 1)
         ec = bytearray(rng.bytes(ec_len))
-        dgh, sah = HASHES[pr["dg_hash"]], HASHES[ht]
+        dgh, sah, ech = HASHES[pr["dg_hash"]], HASHES[ht], HASHES[ec_hash_type(pr["sig"])]
         h1, h15 = dgh(dg1).digest(), dgh(dg15).digest()
         d1 = pr["dg1_shift"] // 8
         ec[d1 - 7:d1] = bytes.fromhex("302502010104") + bytes([max(32, len(h1))])
@@ -430,7 +464,7 @@ class PassportGen:
         sa_len = sa_shift + hl + rng.below(sa_max - (sa_shift + hl) + 1)
         sa = bytearray(rng.bytes(sa_len))
         sa[sa_shift - 2:sa_shift] = bytes([0x04, hl])
-        sa[sa_shift:sa_shift + hl] = (sah(ec).digest() + bytes(32))[:hl]
+        sa[sa_shift:sa_shift + hl] = (ech(ec).digest() + bytes(32))[:hl]
         sa = bytes(sa)
         if isinstance(key, EcKey):
             sig = key.sign(sa, rng)

@@ -1,6 +1,6 @@
 """GPU parity for RegisterIdentityBuilder with SIGNATURE_TYPE 20 (ECDSA secp256r1 + SHA-256,
 SURVEY.md §8d config 5 and §8f rows f1/f2): every witness element of the 5.49 M-element O0
-witness equals the CPU oracle's (oracle/ecdsa_p256.inc.c), the lane status is OK, the public
+witness equals the CPU oracle's (oracle/ecdsa.inc.c), the lane status is OK, the public
 outputs equal independent computations, and lanes whose signature does not verify carry the
 check-site code of ecdsa.circom:81-83."""
 import numpy as np

@@ -130,9 +130,11 @@ def ec_passports():
 def _pk_hash_offset(params):
     """PassportVerificationBuilder.pubkeyHash: after its passportHash, inputs (ec, dg1, dg15, sa,
     signature, pubkey, branches, root) and dg1/dg15/ec/sa hashes (passportVerificationBuilder.circom:89-109)."""
-    nin = 1 + params["ec_blocks"] * 512 + 1024 + params["dg15_blocks"] * 512 + 1024 + 16 + 80 + 1
+    sig = params["sig"]
+    hb = I.hash_block(I.sig_hash_type(sig))
+    nin = 1 + params["ec_blocks"] * hb + 1024 + params["dg15_blocks"] * hb + 1024 + 2 * I.sig_input_len(sig) + 80 + 1
     pvb = 5 + nin
-    return pvb + 1 + (nin - 1) + 4 * 256
+    return pvb + 1 + (nin - 1) + 2 * params["dg_hash"] + I.ec_hash_type(sig) + I.sig_hash_type(sig)
 
 
 def test_p256_generator_table_is_pinned():
@@ -373,3 +375,54 @@ def test_sha1_instances_oracle(oracle, params):
     bad = dict(pp)
     bad["sig"] = pp["sig"] + 1
     assert oracle.register_witness(prm, I.pack_register_inputs(bad, params))[0] == 8
+
+
+# ------------------------------------- ECDSA secp224r1 / brainpoolP384r1 (SIGNATURE_TYPE 24 / 25)
+@pytest.mark.parametrize("sig,name,parts", [(24, "p224", 28), (25, "bp384", 48)])
+def test_p224_bp384_generator_tables_are_pinned(sig, name, parts):
+    """data/<name>_gpow8.bin (tools/gen_ec_tables.py, checked there against ec/powers/secp224r1pows.circom /
+    brainpoolP384r1pows.circom) = j * 2^(8i) * G in CHUNK_NUMBER chunks of CHUNK_SIZE bits."""
+    k, n = I.EC_CHUNKS[sig]
+    t = np.fromfile(os.path.join(os.path.dirname(__file__), "..", "passport-zk-circuits_amd", "data",
+                                 "%s_gpow8.bin" % name), dtype="<u8").reshape(parts, 256, 2, k)
+    rng = np.random.default_rng(sig)
+    for i, j in [(0, 1), (parts - 1, 255)] + [tuple(int(v) for v in x) for x in rng.integers([0, 1], [parts, 256], (4, 2))]:
+        pt = I.EC_CURVES[sig].mul(j << (8 * i))
+        assert [sum(int(t[i, j, a, c]) << (n * c) for c in range(k)) for a in range(2)] == list(pt), (i, j)
+    assert not t[:, 0].any() and int(t.max()) < (1 << n)
+
+
+@pytest.mark.parametrize("sig", [24, 25])
+def test_ecdsa_p224_bp384_oracle(oracle, sig):
+    """SIGNATURE_TYPE 24 (secp224r1, 7 x 32-bit chunks, SHA-224 signed attributes over a SHA-256 encapsulated
+    content hash) and 25 (brainpoolP384r1, 6 x 64, SHA-384 in 1024-bit blocks): a valid signature from an
+    independent signer (pzkwit.inputs.EcKey) passes every check of the generic restatement (oracle/ecdsa.inc.c:
+    BigModInv, x1 mod n === r, every PointOnCurve / Tangent / Line BigIntIsZeroModP and their range checks),
+    the public outputs match independent math (passportHash of the 224 / 384-bit SA digest, the pubkey hash
+    of x, y's low min(EC_FIELD_SIZE, 248) bits), and s + 1 fails x1 mod n === r (ecdsa.circom:81-83)."""
+    from refmath import dg1_commitment
+    params = I.instance_params(sig)
+    prm = oracle.register_params(**params)
+    g = I.PassportGen(seed=17, n_keys=1, params=params, workers=1)
+    pp = g.passport_at(0)
+    rows = I.pack_register_inputs(pp, params)
+    nin, nw = oracle.register_sizes(prm)
+    assert rows.shape[0] == nin == {24: 5742, 25: 6250}[sig]
+    rc, w = oracle.register_witness(prm, rows)
+    assert rc == 0
+    v = [oracle.from_elem(w[i]) for i in range(6)]
+    ht = I.sig_hash_type(sig)
+    sah = I.HASHES[ht](pp["sa"]).digest()
+    hb = [(sah[i // 8] >> (7 - i % 8)) & 1 for i in range(ht)]
+    bits = hb[:252] if ht >= 252 else [0] * (252 - ht) + hb
+    assert v[2] == field.poseidon([sum(bits[i] << i for i in range(252))])
+    assert v[3] == dg1_commitment(pp["dg1"], pp["sk"])
+    assert oracle.from_elem(w[_pk_hash_offset(params)]) == I.ecdsa_pk_hash(pp["n"], {24: 224, 25: 384}[sig]) == pp["pk_hash"]
+    assert v[5] == pp["root"] == field.poseidon([pp["pk_hash"]] * 2 + [1])
+    bad = dict(pp)
+    r, s_ = pp["sig"]
+    bad["sig"] = (r, (s_ + 1) % I.EC_CURVES[sig].n)
+    assert oracle.register_witness(prm, I.pack_register_inputs(bad, params))[0] == 16
+    if sig == 24:  # SIG 24 hashes the encapsulated content with SHA-256: DG_HASH_TYPE may be 256, not 384
+        assert oracle.register_sizes(oracle.register_params(**dict(params, dg_hash=256)))[1] > 0
+        assert oracle.register_sizes(oracle.register_params(**dict(params, dg_hash=384)))[1] == 0

@@ -24,16 +24,26 @@ UNASSIGNED_PER_BMM = {32: 992, 64: 4032, 48: 4512}
 # 3 -> 1 + 1, 37187 -> 15 + 5; SIG 3 / 4 add the two never-assigned hashed_chunks of rsa.circom:81
 N_BMM = {1: 17, 2: 17, 3: 17, 4: 20, 10: 2, 11: 17, 12: 17, 13: 17, 14: 17}
 EXTRA = {3: 2, 4: 2}
-# ECDSA (verifyECDSABits over 4 x 64-bit limbs): every BigMultNonEqualOverflow(G, 4) leaves 4 * 3 tmpResult entries
-# unassigned; 3,164 of them per witness = 260 EllipticCurveDouble x 9 + 102 EllipticCurveAdd x 8 + 4 BigMultModP x 2
-# (PointOnCurve 5, PointOnTangent 4, PointOnLine 3 products); plus EllipicCurveScalarGeneratorMult's never-assigned
-# resultingPointsLeft/Left2/Right/Right2 (4 x 32 x 8) and resultingPoints[31] (8) (ec/curve.circom:812-816, 904)
-ECDSA_UNCOVERED = 12 * (260 * 9 + 102 * 8 + 4 * 2) + 4 * 32 * 8 + 8
+# ECDSA (verifyECDSABits over N chunks): every BigMultNonEqualOverflow(G, N) leaves N (N - 1) tmpResult entries
+# unassigned, per EllipticCurveDouble 9 products, per EllipticCurveAdd 8, per BigMultModP 2 (PointOnCurve 5,
+# PointOnTangent 4, PointOnLine 3); P-256: 260 doubles (precompute 7, scalar mult 4 x 63, second dummy 1) and 102 adds
+# (precompute 7, scalar mult 63, generator mult 31, final 1) and 4 BigMultModP; plus EllipicCurveScalarGeneratorMult's
+# never-assigned resultingPointsLeft/Left2/Right/Right2 (4 x PARTS x 2N) and resultingPoints[PARTS - 1] (2N)
+# (ec/curve.circom:812-816, 904)
+def ecdsa_uncovered(sig):
+    n, cs = I.EC_CHUNKS[sig]
+    wins, parts = n * cs // 4, n * cs // 8
+    dbl, add = 8 + 4 * (wins - 1), 7 + (wins - 1) + (parts - 1) + 1
+    return n * (n - 1) * (9 * dbl + 8 * add + 4 * 2) + 4 * parts * 2 * n + 2 * n
+
+
+ECDSA_UNCOVERED = ecdsa_uncovered(20)
+assert ECDSA_UNCOVERED == 12 * (260 * 9 + 102 * 8 + 4 * 2) + 4 * 32 * 8 + 8
 
 
 def expected_uncovered(sig):
     if sig >= 20:
-        return ECDSA_UNCOVERED
+        return ecdsa_uncovered(sig)
     return N_BMM[sig] * UNASSIGNED_PER_BMM[I.sig_input_len(sig)] + EXTRA.get(sig, 0)
 
 
@@ -110,6 +120,9 @@ REGISTER_CASES = [
     ("sig14_pss3072", I.instance_params(14), 1),
     ("sig20_ecdsa_p256", I.instance_params(20), 0),
     ("sig21_ecdsa_brainpool", I.instance_params(21), 3),
+    ("sig24_ecdsa_p224", I.instance_params(24), 2),
+    ("sig24_dg256", dict(I.instance_params(24), dg_hash=256), 0),
+    ("sig25_ecdsa_brainpool384", I.instance_params(25), 0),
 ]
 
 

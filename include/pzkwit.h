@@ -44,7 +44,10 @@ typedef struct pzk_params {
                                  SHA-256 e = 65537, 2 = RSA-4096, 3 = RSA-2048 SHA-1, 4 = RSA-3072 SHA-1
                                  e = 37187; 10-12 = RSA-2048 PSS SHA-256 (10: e = 3; 12: salt 64), 13 = RSA-2048
                                  PSS SHA-384 (salt 48), 14 = RSA-3072 PSS SHA-256; 20 = ECDSA secp256r1,
-                                 21 = ECDSA brainpoolP256r1 (SHA-256). Others: PZK_E_PARAMS */
+                                 21 = ECDSA brainpoolP256r1 (SHA-256), 24 = ECDSA secp224r1 (7 x 32-bit chunks;
+                                 SHA-224 signed attributes, SHA-256 encapsulated content), 25 = ECDSA
+                                 brainpoolP384r1 (6 x 64-bit chunks, SHA-384). 22 / 23 do not compile in the
+                                 reference (ecdsa.circom:31-37 reads past hashed[]). Others: PZK_E_PARAMS */
   int32_t dg_hash_type;       /* DG_HASH_TYPE (160, 224, 256, 384) */
   int32_t document_type;      /* DOCUMENT_TYPE (1 = TD1, 3 = TD3) */
   int32_t ec_block_number;    /* EC_BLOCK_NUMBER */

@@ -1,7 +1,7 @@
-// ECDSA secp256r1 layout (SIGNATURE_TYPE 20): the VerifySignature(20) subtree
-// (signatureVerification.circom:177-191 -> signatures/ecdsa.circom:18-87) as regions, and the
+// ECDSA layout (SIGNATURE_TYPE 20, 21, 24, 25): the VerifySignature(SIG) subtree
+// (signatureVerification.circom:177-263 -> signatures/ecdsa.circom:18-87) as regions, and the
 // descriptor programs of the table blocks (EllipticCurveDouble / EllipticCurveAdd /
-// BigMultModP(64,4,4,4)), produced by running the shared walkers (ec_walk.hpp) symbolically.
+// BigMultModP(CS,N,N,N)), produced by running the shared walkers (ec_walk.hpp) symbolically.
 #include "builder_impl.hpp"
 #include "ec_walk.hpp"
 
@@ -47,45 +47,60 @@ struct EcProgCtx {
   V sel(const V&, const V&, const V&) const { return {}; }
   V is_zero(const V&) const { return {}; }
   V bit(const V&, int) const { return {}; }
-  V shr64_exact(const V&) const { return {}; }
+  V shr_exact(const V&, int) const { return {}; }
   V inv_fr(const V&) const { return {}; }
   void check_zero(const V&) const {}
   void check_one(const V&) const {}
+  int nl = 4;
   void div_signed(const V*, int, int MCN, V& sign, V* k) const {
     sign = {};
-    for (int i = 0; i < MCN - 3; i++) k[i] = {};
+    for (int i = 0; i < MCN - nl + 1; i++) k[i] = {};
   }
   void divmod_n(const V*, V* q, V* r) const {
-    for (int i = 0; i < 5; i++) q[i] = {};
-    for (int i = 0; i < 4; i++) r[i] = {};
+    for (int i = 0; i < nl + 1; i++) q[i] = {};
+    for (int i = 0; i < nl; i++) r[i] = {};
   }
 };
+
+template <int CV>
+bool ec_program(int t, std::vector<uint32_t>& P, uint32_t& n) {
+  const uint32_t size = ec_type_size(EC_GEO[CV], t);
+  P.assign(size, ecd(ECD_ZERO, 0));
+  EcProgCtx c{P.data(), size};
+  c.nl = EC_GEO[CV].nl;
+  EcWalk<EcProgCtx, CV> walk(c);
+  walk.run(t);
+  n = c.n;
+  return !c.bad;
+}
 
 uint32_t sz_n2b(int L) { return 2 * L + 1; }
 
 }  // namespace
 
 bool ec_programs(Layout& L, std::string& why) {
+  const int cv = L.reg.ec_curve;
+  const EcGeo& G = EC_GEO[cv];
   L.ec_prog.clear();
   for (int t = 0; t < ECT_N; t++) {
-    const uint32_t size = ec_type_size(t);
-    std::vector<uint32_t> P(size, ecd(ECD_ZERO, 0));
-    EcProgCtx c{P.data(), size};
-    EcWalk<EcProgCtx> walk(c);
-    walk.run(t);
-    if (c.bad || c.n > EC_TABLE_MAX) {
-      why = "internal: ECDSA table program " + std::to_string(t) + (c.bad ? " addresses a signal outside its block" : " too large");
+    std::vector<uint32_t> P;
+    uint32_t n = 0;
+    const bool ok = cv == 0 ? ec_program<0>(t, P, n) : cv == 1 ? ec_program<1>(t, P, n) : cv == 2 ? ec_program<2>(t, P, n)
+                                                                                         : ec_program<3>(t, P, n);
+    if (!ok || n > EC_TABLE_MAX[cv]) {
+      why = "internal: ECDSA table program " + std::to_string(t) +
+            (!ok ? " addresses a signal outside its block" : " too large (" + std::to_string(n) + " entries)");
       return false;
     }
     L.ec_prog_off[t] = (uint32_t)L.ec_prog.size();
-    L.ec_tab_n[t] = c.n;
+    L.ec_tab_n[t] = n;
     L.ec_prog.insert(L.ec_prog.end(), P.begin(), P.end());
   }
   L.ec_tab_off.clear();
   for (int i = 0; i < ECT_N; i++) L.ec_ops[i].clear();
   uint32_t off = 0;
-  for (int t = 0; t < EC_N_OPS + EC_N_MM; t++) {
-    const int type = t >= EC_N_OPS ? ECT_MM : ec_op_is_dbl(t) ? ECT_DBL : ECT_ADD;
+  for (int t = 0; t < G.n_ops + EC_N_MM; t++) {
+    const int type = t >= G.n_ops ? ECT_MM : ec_op_is_dbl(G, t) ? ECT_DBL : ECT_ADD;
     L.ec_tab_off.push_back(off);
     L.ec_ops[type].push_back(t);
     off += L.ec_tab_n[type];
@@ -94,78 +109,80 @@ bool ec_programs(Layout& L, std::string& why) {
   return true;
 }
 
-// VerifySignature(20): pubkey[8], signature[8], hashed[256] | verifyECDSABits(64,4,A,B,P,256)
-void ec_verify_regions(Builder& b, int IN_PK, int IN_SIG, int J_SA) {
-  auto ect = [&](int t, int type) { b.region(RK_ECT, ec_type_size(type), {t, type}); };
-  auto ecop = [&](int op) { ect(op, ec_op_is_dbl(op) ? ECT_DBL : ECT_ADD); };
-  b.region(RK_INCOPY, 8, {IN_PK});
-  b.region(RK_INCOPY, 8, {IN_SIG});
-  b.region(RK_DIGEST, 256, {J_SA});
-  // verifyECDSABits own: pubkey[2][4], signature[2][4], hashed[256] | hashedChunked[4], one[4], order[4], sinv[4]
-  b.region(RK_INCOPY, 8, {IN_PK});
-  b.region(RK_INCOPY, 8, {IN_SIG});
-  b.region(RK_DIGEST, 256, {J_SA});
-  b.region(RK_HCHUNK, 4, {J_SA});
-  b.region(RK_EC_CONST, 4, {EC_K_ONE});
-  b.region(RK_EC_CONST, 4, {EC_K_ORDER});
-  b.region(RK_EC_U64, 4, {ECC_SINV});
-  // bits2Num[i].in[63-j] = hashed[64 i + j] (ecdsa.circom:31-37)
-  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_n2b(64), {64, 1, i * 64 + 63, -1, J_SA});
-  b.region(RK_EC_CONST, 4, {EC_K_ORDER});  // getOrder
-  // modInv (BigModInv): out[4] | in[4], modulus[4] | mult
-  b.region(RK_EC_U64, 4, {ECC_SINV});
-  b.region(RK_INCOPY, 4, {IN_SIG + 4});
-  b.region(RK_EC_CONST, 4, {EC_K_ORDER});
-  ect(EC_N_OPS + EC_MM_INV, ECT_MM);
-  ect(EC_N_OPS + EC_MM_U1, ECT_MM);
-  ect(EC_N_OPS + EC_MM_U2, ECT_MM);
-  // scalarMult1 = EllipicCurveScalarGeneratorMult (curve.circom:672-906)
-  b.region(RK_EC_U64, 8, {ECC_GM_RP + 8 * 30});  // out = resultingPoints[30]
-  b.region(RK_EC_U64, 4, {ECC_U1});
-  b.region(RK_EC_GM_RCC, 32 * 256 * 8);
-  b.region(RK_EC_U64, 256, {ECC_GM_AP});
-  b.region(RK_VALUE, 4 * 256, {-2});  // resultingPointsLeft/Left2/Right/Right2: declared, never assigned
-  b.region(RK_EC_U64, 248, {ECC_GM_RP});
-  b.region(RK_VALUE, 8, {-2});        // resultingPoints[31]
-  for (int i = 0; i < 4; i++) b.region(RK_EC_N2B, sz_n2b(64), {0, ECC_U1 + i});
-  b.region(RK_EC_B2N8, 32 * 17, {ECC_U1});
-  b.region(RK_EC_CONST, 8, {EC_K_DUMMY});
+// VerifySignature(SIG): pubkey[2N], signature[2N], hashed[N CS] | verifyECDSABits(CS,N,A,B,P,N CS)
+void ec_verify_regions(Builder& b, int cv, int IN_PK, int IN_SIG, int J_SA) {
+  const EcGeo& G = EC_GEO[cv];
+  const int N = G.nl, CS = G.cs, F = G.fb, P2 = 2 * N;
+  auto ect = [&](int t, int type) { b.region(RK_ECT, ec_type_size(G, type), {t, type}); };
+  auto ecop = [&](int op) { ect(op, ec_op_is_dbl(G, op) ? ECT_DBL : ECT_ADD); };
+  b.region(RK_INCOPY, P2, {IN_PK});
+  b.region(RK_INCOPY, P2, {IN_SIG});
+  b.region(RK_DIGEST, F, {J_SA});
+  // verifyECDSABits own: pubkey[2][N], signature[2][N], hashed[F] | hashedChunked[N], one[N], order[N], sinv[N]
+  b.region(RK_INCOPY, P2, {IN_PK});
+  b.region(RK_INCOPY, P2, {IN_SIG});
+  b.region(RK_DIGEST, F, {J_SA});
+  b.region(RK_HCHUNK, N, {J_SA, N, CS});
+  b.region(RK_EC_CONST, N, {EC_K_ONE});
+  b.region(RK_EC_CONST, N, {EC_K_ORDER});
+  b.region(RK_EC_U64, N, {G.c_sinv});
+  // bits2Num[i].in[CS-1-j] = hashed[CS i + j] (ecdsa.circom:31-37)
+  for (int i = 0; i < N; i++) b.region(RK_BITS2NUM, sz_n2b(CS), {CS, 1, i * CS + CS - 1, -1, J_SA});
+  b.region(RK_EC_CONST, N, {EC_K_ORDER});  // getOrder
+  // modInv (BigModInv): out[N] | in[N], modulus[N] | mult
+  b.region(RK_EC_U64, N, {G.c_sinv});
+  b.region(RK_INCOPY, N, {IN_SIG + N});
+  b.region(RK_EC_CONST, N, {EC_K_ORDER});
+  ect(G.n_ops + EC_MM_INV, ECT_MM);
+  ect(G.n_ops + EC_MM_U1, ECT_MM);
+  ect(G.n_ops + EC_MM_U2, ECT_MM);
+  // scalarMult1 = EllipicCurveScalarGeneratorMult (curve.circom:680-906)
+  b.region(RK_EC_U64, P2, {G.c_gm_rp + P2 * (G.parts - 2)});  // out = resultingPoints[PARTS-2]
+  b.region(RK_EC_U64, N, {G.c_u1});
+  b.region(RK_EC_GM_RCC, (uint64_t)G.parts * 256 * P2);
+  b.region(RK_EC_U64, G.parts * P2, {G.c_gm_ap});
+  b.region(RK_VALUE, 4 * G.parts * P2, {-2});  // resultingPointsLeft/Left2/Right/Right2: declared, never assigned
+  b.region(RK_EC_U64, (G.parts - 1) * P2, {G.c_gm_rp});
+  b.region(RK_VALUE, P2, {-2});                 // resultingPoints[PARTS-1]
+  for (int i = 0; i < N; i++) b.region(RK_EC_N2B, sz_n2b(CS), {0, G.c_u1 + i, CS});
+  b.region(RK_EC_B2N8, G.parts * 17, {G.c_u1});
+  b.region(RK_EC_CONST, P2, {EC_K_DUMMY});
   ecop(EC_OP_SD);
-  b.region(RK_EC_GM_EQ, 32 * 256 * 6);
-  b.region(RK_EC_GM_SUM, 32 * 8 * 512);
-  for (int i = 0; i < 31; i++) {
+  b.region(RK_EC_GM_EQ, (uint64_t)G.parts * 256 * 6);
+  b.region(RK_EC_GM_SUM, (uint64_t)G.parts * P2 * 512);
+  for (int i = 0; i < G.parts - 1; i++) {
     ecop(ec_op_gm_add(i));
-    b.region(RK_EC_GM_STEP, 4 * 6 + 16 * 6, {i});
+    b.region(RK_EC_GM_STEP, 4 * 6 + 2 * P2 * 6, {i});
   }
   // scalarMult2 = EllipticCurveScalarMult(…,4) (curve.circom:356-494)
-  b.region(RK_EC_U64, 8, {ECC_SM_RP + 8 * 64});
-  b.region(RK_INCOPY, 8, {IN_PK});
-  b.region(RK_EC_U64, 4, {ECC_U2});
-  b.region(RK_EC_SBITS, 256, {ECC_U2});
-  b.region(RK_EC_U64, 65 * 8, {ECC_SM_RP});
-  b.region(RK_EC_U64, 64 * 8, {ECC_SM_AP});
-  //   precompute (EllipticCurvePrecomputePipinger): out[16][2][4] | in[2][4] | getDummy, ops i = 2..15
-  b.region(RK_EC_U64, 128, {ECC_PRE});
-  b.region(RK_INCOPY, 8, {IN_PK});
-  b.region(RK_EC_CONST, 8, {EC_K_DUMMY});
-  for (int i = 2; i < 16; i++) ecop(ec_op_pre(i));
-  b.region(RK_EC_CONST, 8, {EC_K_DUMMY});  // getDummy
-  for (int i = 0; i < 4; i++) b.region(RK_EC_N2B, sz_n2b(64), {0, ECC_U2 + i});
-  for (int w = 0; w < 64; w++) {
+  b.region(RK_EC_U64, P2, {G.c_sm_rp + P2 * G.wins});
+  b.region(RK_INCOPY, P2, {IN_PK});
+  b.region(RK_EC_U64, N, {G.c_u2});
+  b.region(RK_EC_SBITS, F, {G.c_u2});
+  b.region(RK_EC_U64, (G.wins + 1) * P2, {G.c_sm_rp});
+  b.region(RK_EC_U64, G.wins * P2, {G.c_sm_ap});
+  //   precompute (EllipticCurvePrecomputePipinger): out[16][2][N] | in[2][N] | getDummy, ops i = 2..15
+  b.region(RK_EC_U64, 16 * P2, {G.c_pre});
+  b.region(RK_INCOPY, P2, {IN_PK});
+  b.region(RK_EC_CONST, P2, {EC_K_DUMMY});
+  for (int i = 2; i < 16; i++) ecop(ec_op_pre(G, i));
+  b.region(RK_EC_CONST, P2, {EC_K_DUMMY});  // getDummy
+  for (int i = 0; i < N; i++) b.region(RK_EC_N2B, sz_n2b(CS), {0, G.c_u2 + i, CS});
+  for (int w = 0; w < G.wins; w++) {
     b.region(RK_EC_SM_W0, sz_n2b(4) + 6, {w});
     if (w > 0) {
-      ecop(ec_op_sm_dbl(4 * w - 4));
-      b.region(RK_EC_SM_DSW, 8 * 6, {w});
-      for (int j = 1; j < 4; j++) ecop(ec_op_sm_dbl(4 * w - 4 + j));
+      ecop(ec_op_sm_dbl(G, 4 * w - 4));
+      b.region(RK_EC_SM_DSW, P2 * 6, {w});
+      for (int j = 1; j < 4; j++) ecop(ec_op_sm_dbl(G, 4 * w - 4 + j));
     }
-    b.region(RK_EC_SM_SEL, 8 * 32 + 16 * 6, {w});
+    b.region(RK_EC_SM_SEL, P2 * 32 + 16 * 6, {w});
     if (w > 0) {
-      ecop(ec_op_sm_add(w - 1));
-      b.region(RK_EC_SM_RSW, 6 + 16 * 6, {w});
+      ecop(ec_op_sm_add(G, w - 1));
+      b.region(RK_EC_SM_RSW, 6 + 2 * P2 * 6, {w});
     }
   }
-  ecop(EC_OP_FINAL);
-  ect(EC_N_OPS + EC_MM_XN, ECT_MM);
+  ecop(G.op_final);
+  ect(G.n_ops + EC_MM_XN, ECT_MM);
 }
 
 }  // namespace pzk

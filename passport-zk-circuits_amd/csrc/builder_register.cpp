@@ -5,6 +5,7 @@
 // templates (cited inline); the CPU oracle derives them independently and the parity tests
 // compare every element.
 #include "builder_impl.hpp"
+#include "ec_common.hpp"
 #include "mm_prog.hpp"
 
 namespace pzk {
@@ -25,7 +26,7 @@ uint32_t sz_bmneq(int G, int L) { return (G + L - 1) + G + L + G * L + (G + L - 
 }  // namespace
 
 bool ec_programs(Layout& L, std::string& why);
-void ec_verify_regions(Builder& b, int IN_PK, int IN_SIG, int J_SA);
+void ec_verify_regions(Builder& b, int cv, int IN_PK, int IN_SIG, int J_SA);
 
 // BigMultModP(64,K,K,K) block size (bigInt.circom:206-272)
 uint32_t modmul_size(int K) {
@@ -43,24 +44,35 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool pss = p.signature_type >= 10 && p.signature_type <= 14;
   // RSA exponent (signatureVerification.circom:14-75): 3 for SIG 10, 37187 for SIG 4, else 65537
   const long EXP = p.signature_type == 10 ? 3 : p.signature_type == 4 ? 37187 : 65537;
-  if ((p.signature_type < 1 || p.signature_type > 4) && !pss && p.signature_type != 20 && p.signature_type != 21) {
+  const int cv = ec_curve_of_sig(p.signature_type);
+  if (p.signature_type == 22 || p.signature_type == 23) {
     why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
-          " not built yet (RSA PKCS#1 v1.5 types 1-4, RSA-PSS types 10-14, ECDSA secp256r1 20 and brainpoolP256r1 21 are)";
+          ": verifyECDSABits reads hashed[] past its end (ecdsa.circom:31-37, 5 x 64 / 3 x 64 chunks of a 256 / 160-bit "
+          "hash), so the reference circuit does not compile";
     return false;
   }
-  const bool ecdsa = p.signature_type == 20 || p.signature_type == 21;
-  // DG_HASH_TYPE 160, 224, 256 or 384. HASH_TYPE (EC / SA hashers, passportVerificationBuilder.circom:16-59): 160 for
-  // SIG 3 / 4, 384 for SIG 13, else 256. The flow's `encapsulatedContentHash[i], i < HASH_SIZE` loop
-  // (passportVerificationFlow.circom:36-40) runs over the DG hash bits, so DG <= HASH_TYPE or the reference cannot compile.
+  if ((p.signature_type < 1 || p.signature_type > 4) && !pss && cv < 0) {
+    why = "SIGNATURE_TYPE " + std::to_string(p.signature_type) +
+          " not supported (RSA PKCS#1 v1.5 types 1-4, RSA-PSS types 10-14, ECDSA 20, 21, 24, 25 are)";
+    return false;
+  }
+  const bool ecdsa = cv >= 0;
+  // DG_HASH_TYPE 160, 224, 256 or 384. HASH_TYPE (SA hasher, passportVerificationBuilder.circom:16-59): 160 for
+  // SIG 3 / 4, 384 for SIG 13 / 25, 224 for SIG 24, else 256; EC_HASH_TYPE (EC hasher, :53) is the HASH_TYPE before
+  // SIG 24 sets 224, so 256 there. The flow's `encapsulatedContentHash[i], i < HASH_SIZE` loop
+  // (passportVerificationFlow.circom:36-40) runs over the DG hash bits, so DG <= EC_HASH_TYPE or the reference cannot
+  // compile.
   if (p.dg_hash_type != 256 && p.dg_hash_type != 224 && p.dg_hash_type != 160 && p.dg_hash_type != 384) {
     why = "DG_HASH_TYPE must be 160, 224, 256 or 384";
     return false;
   }
   const bool sha1_sig = p.signature_type == 3 || p.signature_type == 4;
-  const int DG = p.dg_hash_type, HT = sha1_sig ? 160 : p.signature_type == 13 ? 384 : 256;
-  if (DG > HT) {
-    why = "DG_HASH_TYPE " + std::to_string(DG) + " is wider than this SIGNATURE_TYPE's hash (" + std::to_string(HT) +
-          "): passportVerificationFlow.circom:36-40 would read encapsulatedContentHash past its end";
+  const int DG = p.dg_hash_type,
+            HT = sha1_sig ? 160 : (p.signature_type == 13 || p.signature_type == 25) ? 384 : p.signature_type == 24 ? 224 : 256;
+  const int EHT = p.signature_type == 24 ? 256 : HT;
+  if (DG > EHT) {
+    why = "DG_HASH_TYPE " + std::to_string(DG) + " is wider than this SIGNATURE_TYPE's encapsulated-content hash (" +
+          std::to_string(EHT) + "): passportVerificationFlow.circom:36-40 would read encapsulatedContentHash past its end";
     return false;
   }
   // HASH_BLOCK_SIZE / DG_HASH_BLOCK_SIZE (registerIdentityBuilder.circom:95-102): 1024-bit blocks above 256-bit hashes
@@ -72,7 +84,8 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const bool aa_ec = p.aa_signature_algo >= 20;
   const int aa_f = p.aa_signature_algo == 22 ? 320 : p.aa_signature_algo == 23 ? 192 : 256;
   const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
-  const int K = ecdsa ? 8 : p.signature_type == 2 ? 64 : (p.signature_type == 14 || p.signature_type == 4) ? 48 : 32;  // signature / pubkey input length
+  // signature / pubkey input length: 2 x CHUNK_NUMBER for ECDSA (registerIdentityBuilder.circom:124-135)
+  const int K = ecdsa ? 2 * EC_GEO[cv].nl : p.signature_type == 2 ? 64 : (p.signature_type == 14 || p.signature_type == 4) ? 48 : 32;
   const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = HBS * ecB, d15Len = HBS * d15B;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
@@ -116,7 +129,9 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   L.reg.aa_f = aa_f;
   L.reg.aa_hs = aa_hs;
   L.reg.ecdsa = ecdsa ? 1 : 0;
-  L.reg.ec_curve = p.signature_type == 21 ? 1 : 0;
+  L.reg.ec_curve = ecdsa ? cv : 0;
+  L.reg.ec_nl = ecdsa ? EC_GEO[cv].nl : 0;
+  L.reg.ec_cs = ecdsa ? EC_GEO[cv].cs : 0;
   L.is_ecdsa = ecdsa;
   if (ecdsa && !ec_programs(L, why)) return false;
 
@@ -159,16 +174,16 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   // so reserve the job ids first (creation order dg1, dg15, ec, sa).
   const int J_DG1 = b.hash_job(DG, IN_DG1, 1024 / DBS);
   const int J_DG15 = aa ? b.hash_job(DG, IN_DG15, d15B) : -1;  // the first d15B x DG_HASH_BLOCK_SIZE bits (:117-120)
-  const int J_EC = b.hash_job(HT, IN_EC, ecB);
+  const int J_EC = b.hash_job(EHT, IN_EC, ecB);
   const int J_SA = b.hash_job(HT, IN_SA, 1024 / HBS);
   L.reg.j_dg1 = J_DG1; L.reg.j_dg15 = J_DG15; L.reg.j_ec = J_EC; L.reg.j_sa = J_SA;
   b.region(RK_DIGEST, DG, {J_DG1});
   if (aa) b.region(RK_DIGEST, DG, {J_DG15});
   else b.region(RK_VALUE, DG, {-2});  // dg15Hash <== 0 (zeros)
-  b.region(RK_DIGEST, HT, {J_EC});
+  b.region(RK_DIGEST, EHT, {J_EC});
   b.region(RK_DIGEST, HT, {J_SA});
   const uint32_t r_pkhash = b.region(RK_VALUE, 1, {-1});
-  if (ecdsa) b.region(RK_EC_PKBITS, 512, {IN_PK});  // ecBitsX[256], ecBitsY[256]
+  if (ecdsa) b.region(RK_EC_PKBITS, 2 * EC_GEO[cv].fb, {IN_PK, EC_GEO[cv].nl, EC_GEO[cv].cs});  // ecBitsX[F], ecBitsY[F]
   else b.region(RK_TEMPMOD, 5, {IN_PK});
   auto sha_blocks = [&](int job, int in_off, int blocks) {
     if (L.sha[job].algo == 1) { b.sha1_regions(job, in_off, blocks, true); return; }  // ShaHashChunks(B, 160)
@@ -182,13 +197,13 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   if (aa) sha_blocks(J_DG15, IN_DG15, d15B);
   sha_blocks(J_EC, IN_EC, ecB);
   sha_blocks(J_SA, IN_SA, 1024 / HBS);
-  // PassportVerificationFlow(ecLen, DG, HT, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA): 3 DG + 8 IsEqual
-  b.region(RK_FLOW, 1 + 2 * DG + ecLen + HT + 1024 + (3 * DG + 8) * (1 + SZ_ISEQUAL),
+  // PassportVerificationFlow(ecLen, DG, EHT, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA): 3 DG + 8 IsEqual
+  b.region(RK_FLOW, 1 + 2 * DG + ecLen + EHT + 1024 + (3 * DG + 8) * (1 + SZ_ISEQUAL),
            {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, p.aa_signature_algo});
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
   if (ecdsa) {
-    ec_verify_regions(b, IN_PK, IN_SIG, J_SA);
+    ec_verify_regions(b, cv, IN_PK, IN_SIG, J_SA);
   } else {
     // PowerMod(64,K,EXP): out[K] | base[K], modulus[K] | muls[], resultMuls[] (bigInt.circom:280-340).
     // exp_to_bits(65537) = [16, 2, 0, 16], exp_to_bits(3) = [1, 2, 0, 1]: muls[i] = muls[i-1]^2
@@ -239,7 +254,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
       b.region(RK_INCOPY, K, {IN_SIG});
       b.region(RK_INCOPY, K, {IN_PK});
       b.region(RK_DIGEST, 256, {J_SA});
-      b.region(RK_HCHUNK, 4, {J_SA});
+      b.region(RK_HCHUNK, 4, {J_SA, 4, 64});
       if (!power_mod()) return false;
       for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, sz_bits2num(64), {64, 1, i * 64 + 63, -1, J_SA});
       b.region(RK_NUM2BITS, sz_num2bits(64), {64, 1, 6});  // Num2Bits(64)(EM limb 6)
@@ -273,18 +288,19 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
       L.n_derived = (uint64_t)BS * IT + 1024;
     }
   }
-  // signedAttributesNum = Bits2Num(252)(saHash[0..251]), or of 92 zeros | saHash[0..159] for SHA-1
-  b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, HT == 160 ? -92 : 0, 1, J_SA});
+  // signedAttributesNum = Bits2Num(252)(saHash[0..251]), or of 252 - HT zeros | saHash[0..HT-1] for HT < 252
+  b.region(RK_BITS2NUM, sz_bits2num(252), {252, 1, HT < 252 ? HT - 252 : 0, 1, J_SA});
   int S_PKH;
   if (ecdsa) {
-    // num2bitsX[i], num2bitsY[i] (Num2Bits(64)), xToNum, yToNum (Bits2Num(248)), PoseidonHash(2)
-    // (passportVerificationBuilder.circom:193-230)
-    for (int i = 0; i < 4; i++) {
-      b.region(RK_EC_N2B, sz_num2bits(64), {1, IN_PK + i});
-      b.region(RK_EC_N2B, sz_num2bits(64), {1, IN_PK + 4 + i});
+    // num2bitsX[i], num2bitsY[i] (Num2Bits(CS)), xToNum, yToNum (Bits2Num(F - DIFF), F - DIFF = min(F, 248)),
+    // PoseidonHash(2) (passportVerificationBuilder.circom:193-230)
+    const int N = EC_GEO[cv].nl, CS = EC_GEO[cv].cs, F = EC_GEO[cv].fb, FD = F > 248 ? 248 : F;
+    for (int i = 0; i < N; i++) {
+      b.region(RK_EC_N2B, sz_num2bits(CS), {1, IN_PK + i, CS});
+      b.region(RK_EC_N2B, sz_num2bits(CS), {1, IN_PK + N + i, CS});
     }
-    b.region(RK_EC_B2N248, sz_bits2num(248), {IN_PK});
-    b.region(RK_EC_B2N248, sz_bits2num(248), {IN_PK + 4});
+    b.region(RK_EC_B2N248, sz_bits2num(FD), {IN_PK, N, CS, FD});
+    b.region(RK_EC_B2N248, sz_bits2num(FD), {IN_PK + N, N, CS, FD});
     S_PKH = b.poseidon(2, {V_PKX, V_PKY}, 0);
   } else {
     // pubkeyHasherRsa = PoseidonHash(5)

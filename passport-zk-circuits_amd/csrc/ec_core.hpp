@@ -1,5 +1,6 @@
-// ECDSA secp256r1 kernels (SIGNATURE_TYPE 20): k_ec_core, k_ec_table, k_emit_ect.
-// See ec_common.hpp for the split and the per-witness layouts.
+// ECDSA kernels (SIGNATURE_TYPE 20, 21, 24, 25): k_ec_scalars / k_ec_chain / k_ec_final / k_ec_affine /
+// k_ec_link / k_ec_inv (the EC core), k_ec_table, k_emit_ect. Compiled once per curve (PZK_EC_CURVE, see
+// ec_common.hpp for the split, the per-curve geometry ECG and the per-witness layouts).
 #pragma once
 #include "ec_common.hpp"
 #include "ec_walk.hpp"
@@ -10,6 +11,11 @@
 
 namespace pzk {
 inline namespace PZK_EC_NS {
+
+// this curve's chunking: NL chunks of CS bits; field elements as NW 32-bit words, JW 64-bit words
+static constexpr int NL = ECG.nl, CS = ECG.cs, P2 = 2 * ECG.nl;
+static constexpr int NW = (ECG.fb + 31) / 32, JW = ECG.jw;
+static constexpr uint64_t CS_MASK = CS == 64 ? ~0ull : (1ull << CS) - 1;
 
 // ============================================================ signed 256-bit integers
 struct I256 { uint32_t w[8]; };
@@ -90,38 +96,39 @@ __device__ __forceinline__ I256 i_to_fr(const I256& a) {
 }
 __device__ __forceinline__ fr i_as_fr(const I256& a) { fr r; for (int i = 0; i < 8; i++) r.v[i] = a.w[i]; return r; }
 
-// ============================================================ multiprecision division (64-bit limbs)
-// floor(a / b), b = 4 limbs with b[3] != 0 (P-256 p and n); q[na-3], r[4]. Knuth D with the
-// 128/64 step of regcore.hpp (divlu). Same unique quotient/remainder long_div
-// (bigIntFunc.circom:190-232) produces.
-__device__ __forceinline__ void mp_divmod4(const uint64_t* a, int na, const uint64_t* b, uint64_t* q, uint64_t* r) {
-  const int s = __clzll((long long)b[3]);
-  uint64_t v[4], u[16];
+// ============================================================ multiprecision division (64-bit words)
+// floor(a / b), b = NB words with b[NB-1] != 0 (this curve's p or n); q[na-NB+1], r[NB]. Knuth D with the
+// 128/64 step of core_util.hpp (divlu). Same unique quotient/remainder long_div (bigIntFunc.circom:190-232)
+// produces.
+template <int NB>
+__device__ __forceinline__ void mp_divmod(const uint64_t* a, int na, const uint64_t* b, uint64_t* q, uint64_t* r) {
+  const int s = __clzll((long long)b[NB - 1]);
+  uint64_t v[NB], u[32];
 #pragma unroll
-  for (int i = 3; i > 0; i--) v[i] = (b[i] << s) | (s ? b[i - 1] >> (64 - s) : 0);
+  for (int i = NB - 1; i > 0; i--) v[i] = (b[i] << s) | (s ? b[i - 1] >> (64 - s) : 0);
   v[0] = b[0] << s;
   u[na] = s ? a[na - 1] >> (64 - s) : 0;
   for (int i = na - 1; i > 0; i--) u[i] = (a[i] << s) | (s ? a[i - 1] >> (64 - s) : 0);
   u[0] = a[0] << s;
-  for (int j = na - 4; j >= 0; j--) {
+  for (int j = na - NB; j >= 0; j--) {
     uint64_t qhat, rhat;
     bool big = false;
-    if (u[j + 4] >= v[3]) {
+    if (u[j + NB] >= v[NB - 1]) {
       qhat = ~0ull;
-      rhat = u[j + 3] + v[3];
-      big = rhat < v[3];
+      rhat = u[j + NB - 1] + v[NB - 1];
+      big = rhat < v[NB - 1];
     } else {
-      qhat = divlu(u[j + 4], u[j + 3], v[3], &rhat);
+      qhat = divlu(u[j + NB], u[j + NB - 1], v[NB - 1], &rhat);
     }
     while (!big) {
-      uint64_t ph = __umul64hi(qhat, v[2]), pl = qhat * v[2];
-      if (ph > rhat || (ph == rhat && pl > u[j + 2])) {
-        qhat--; rhat += v[3]; big = rhat < v[3];
+      uint64_t ph = __umul64hi(qhat, v[NB - 2]), pl = qhat * v[NB - 2];
+      if (ph > rhat || (ph == rhat && pl > u[j + NB - 2])) {
+        qhat--; rhat += v[NB - 1]; big = rhat < v[NB - 1];
       } else break;
     }
     uint64_t carry = 0, borrow = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < NB; i++) {
       uint64_t pl = qhat * v[i], ph = __umul64hi(qhat, v[i]);
       pl += carry; ph += pl < carry;
       uint64_t t = u[i + j] - pl;
@@ -130,24 +137,47 @@ __device__ __forceinline__ void mp_divmod4(const uint64_t* a, int na, const uint
       b1 += t < borrow;
       u[i + j] = t2; borrow = b1; carry = ph;
     }
-    uint64_t t = u[j + 4] - carry, b1 = u[j + 4] < carry;
+    uint64_t t = u[j + NB] - carry, b1 = u[j + NB] < carry;
     uint64_t t2 = t - borrow; b1 += t < borrow;
-    u[j + 4] = t2;
+    u[j + NB] = t2;
     if (b1) {  // add back
       qhat--;
       uint64_t c = 0;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
+      for (int i = 0; i < NB; i++) {
         uint64_t s1 = u[i + j] + v[i], c1 = s1 < v[i];
         uint64_t s2 = s1 + c; c1 += s2 < c;
         u[i + j] = s2; c = c1;
       }
-      u[j + 4] += c;
+      u[j + NB] += c;
     }
     q[j] = qhat;
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++) r[i] = (u[i] >> s) | (s ? u[i + 1] << (64 - s) : 0);
+  for (int i = 0; i < NB; i++) r[i] = (u[i] >> s) | (s ? u[i + 1] << (64 - s) : 0);
+}
+// chunks (one per u64, CS bits) <-> 64-bit words of the integer they spell
+__device__ __forceinline__ void chunks_to_words(const uint64_t* ch, int n, uint64_t* w, int nw) {
+  for (int i = 0; i < nw; i++) w[i] = 0;
+  for (int i = 0; i < n; i++) w[(CS * i) >> 6] |= ch[i] << ((CS * i) & 63);
+}
+__device__ __forceinline__ uint64_t word_chunk(const uint64_t* w, int i) {
+  return (w[(CS * i) >> 6] >> ((CS * i) & 63)) & CS_MASK;
+}
+// words (32-bit) of p and n for the divisions
+static constexpr int PWORDS = (ECG.fb + 63) / 64;
+__device__ __forceinline__ void const_words(const uint64_t* ch, uint64_t* w) { chunks_to_words(ch, NL, w, PWORDS); }
+
+// two's-complement accumulation of signed I256 values shifted by CS i bits (32-bit words)
+template <int AW32>
+__device__ __forceinline__ void acc_signed(uint32_t* acc, const I256& v, int i) {
+  const int off = (CS / 32) * i;
+  const uint32_t ext = i_is_neg(v) ? ~0u : 0u;
+  uint64_t c = 0;
+  for (int j = 0; off + j < AW32; j++) {
+    const uint64_t s = (uint64_t)acc[off + j] + (j < 8 ? v.w[j] : ext) + c;
+    acc[off + j] = (uint32_t)s; c = s >> 32;
+  }
 }
 
 // ============================================================ table context (device walker)
@@ -178,10 +208,17 @@ struct EcTabCtx {
   __device__ V sel(const V& c, const V& a, const V& b) const { return c.w[0] ? a : b; }
   __device__ V is_zero(const V& a) const { return i_u64(i_is_zero(a) ? 1 : 0); }
   __device__ V bit(const V& a, int b) const { return i_u64(i_bit(a, b)); }
-  // carry = (in + carry') / 2^64, field division (bigIntComparators.circom:119-122): exact for a passing witness
-  __device__ V shr64_exact(const V& t) {
-    if (t.w[0] | t.w[1]) fail(ST_BIGISZERO);
-    return i_shr64(t);
+  // carry = (in + carry') / 2^CS, field division (bigIntComparators.circom:119-122): exact for a passing witness
+  __device__ V shr_exact(const V& t, int) {
+    I256 r; const uint32_t s = i_is_neg(t) ? ~0u : 0u;
+    if (CS == 64) {
+      if (t.w[0] | t.w[1]) fail(ST_BIGISZERO);
+      return i_shr64(t);
+    }
+    if (t.w[0]) fail(ST_BIGISZERO);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = i + 1 < 8 ? t.w[i + 1] : s;
+    return r;
   }
   __device__ V inv_fr(const V& d) const {  // FIPS products: 64 independent lanes per wave, one op each
     fr x = fr_mul_fast(i_as_fr(i_to_fr(d)), fr_const(R2_));
@@ -195,353 +232,369 @@ struct EcTabCtx {
     if (!i_is_zero(i_sub(v, i_u64(1)))) fail(ST_BIGMOD_GT);
   }
   // reduce_overflow_signed (bigIntFunc.circom:646-694) + long_div by P (:190-232): the signed sum
-  // S = sum in[i] 2^(64 i); sign = S >= 0; k = |S| / p (MCN - 3 digits)
+  // S = sum in[i] 2^(CS i); sign = S >= 0; k = |S| / p (MCN - NL + 1 chunks)
   __device__ void div_signed(const V* in, int CN, int MCN, V& sign, V* k) {
-    uint64_t acc[14];
-    for (int i = 0; i < 14; i++) acc[i] = 0;
-    for (int i = 0; i < CN; i++) {
-      const uint64_t ext = i_is_neg(in[i]) ? ~0ull : 0ull;
-      uint64_t c = 0;
-      for (int j = 0; i + j < 14; j++) {
-        uint64_t x = j < 4 ? ((uint64_t)in[i].w[2 * j + 1] << 32 | in[i].w[2 * j]) : ext;
-        uint64_t s1 = acc[i + j] + x, c1 = s1 < x;
-        uint64_t s2 = s1 + c; c1 += s2 < c;
-        acc[i + j] = s2; c = c1;
-      }
-    }
-    const bool pos = !(acc[13] >> 63);
+    constexpr int AW = ((3 * NL + 1) * CS + 63) / 64 + 2, AW32 = 2 * AW;
+    uint32_t acc[AW32];
+    for (int i = 0; i < AW32; i++) acc[i] = 0;
+    for (int i = 0; i < CN; i++) acc_signed<AW32>(acc, in[i], i);
+    const bool pos = !(acc[AW32 - 1] >> 31);
     if (!pos) {
       uint64_t c = 1;
-      for (int i = 0; i < 14; i++) { uint64_t x = ~acc[i] + c; c = (c && x == 0) ? 1 : 0; acc[i] = x; }
+      for (int i = 0; i < AW32; i++) { const uint64_t x = (uint64_t)(uint32_t)~acc[i] + c; acc[i] = (uint32_t)x; c = x >> 32; }
     }
-    uint64_t q[12], r[4];
-    mp_divmod4(acc, MCN, EC_P, q, r);
+    uint64_t a[AW], pw[PWORDS], q[AW], r[PWORDS];
+    for (int i = 0; i < AW; i++) { a[i] = (uint64_t)acc[2 * i + 1] << 32 | acc[2 * i]; q[i] = 0; }
+    const_words(EC_P, pw);
+    const int na = (MCN * CS + 63) / 64;
+    mp_divmod<PWORDS>(a, na < PWORDS ? PWORDS : na, pw, q, r);
     sign = i_u64(pos ? 1 : 0);
-    for (int i = 0; i < MCN - 3; i++) k[i] = i_u64(q[i]);
+    for (int i = 0; i < MCN - NL + 1; i++) k[i] = i_u64(word_chunk(q, i));
   }
-  // reduce_overflow(64, 7, 8) (bigIntFunc.circom:570-588) + long_div by n
+  // reduce_overflow(CS, 2N-1, 2N) (bigIntFunc.circom:570-588) + long_div by n
   __device__ void divmod_n(const V* mo, V* q, V* r) {
-    uint64_t red[9];
-    for (int i = 0; i < 9; i++) red[i] = 0;
-    for (int i = 0; i < 7; i++) {
-      uint64_t c = 0;
-      for (int j = 0; j < 3 && i + j < 9; j++) {
-        uint64_t x = (uint64_t)mo[i].w[2 * j + 1] << 32 | mo[i].w[2 * j];
-        uint64_t s1 = red[i + j] + x, c1 = s1 < x;
-        uint64_t s2 = s1 + c; c1 += s2 < c;
-        red[i + j] = s2; c = c1;
-      }
-      for (int j = i + 3; j < 9 && c; j++) { red[j] += c; c = red[j] == 0; }
-    }
-    uint64_t qq[5], rr[4];
-    mp_divmod4(red, 8, EC_N, qq, rr);
-    for (int i = 0; i < 5; i++) q[i] = i_u64(qq[i]);
-    for (int i = 0; i < 4; i++) r[i] = i_u64(rr[i]);
+    constexpr int AW = (2 * NL * CS + 63) / 64 + 2, AW32 = 2 * AW;
+    uint32_t acc[AW32];
+    for (int i = 0; i < AW32; i++) acc[i] = 0;
+    for (int i = 0; i < 2 * NL - 1; i++) acc_signed<AW32>(acc, mo[i], i);
+    uint64_t a[AW], nw[PWORDS], qq[AW], rr[PWORDS + 1];
+    for (int i = 0; i < AW; i++) { a[i] = (uint64_t)acc[2 * i + 1] << 32 | acc[2 * i]; qq[i] = 0; }
+    rr[PWORDS] = 0;
+    const_words(EC_N, nw);
+    mp_divmod<PWORDS>(a, AW - 1, nw, qq, rr);
+    for (int i = 0; i < NL + 1; i++) q[i] = i_u64(word_chunk(qq, i));
+    for (int i = 0; i < NL; i++) r[i] = i_u64(word_chunk(rr, i));
   }
   __device__ V rec(int k) const { return i_u64(rp[k]); }
 };
 
-// ============================================================ P-256 Montgomery fields (p and n)
-struct e8 { uint32_t v[8]; };
+// ============================================================ Montgomery fields (p and n of this curve)
+// NW 32-bit words; m, R^2 mod m, R mod m, m - 2 (Fermat exponent), -m^-1 mod 2^32, R = 2^(32 NW); aR = A R mod p
+struct eW { uint32_t v[NW]; };
 #if PZK_EC_CURVE == 0
+static constexpr bool EC_A_M3 = true;  // A = p - 3
 struct ModP {
-  static constexpr uint32_t m[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u,
-                                    0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
-  static constexpr uint32_t r2[8] = {0x00000003u, 0x00000000u, 0xffffffffu, 0xfffffffbu,
-                                     0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u};
-  static constexpr uint32_t r1[8] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu,
-                                     0xffffffffu, 0xffffffffu, 0xfffffffeu, 0x00000000u};
-  static constexpr uint32_t e[8] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0x00000000u,
-                                    0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
+  static constexpr uint32_t m[NW] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u,
+                                     0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
+  static constexpr uint32_t r2[NW] = {0x00000003u, 0x00000000u, 0xffffffffu, 0xfffffffbu,
+                                      0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u};
+  static constexpr uint32_t r1[NW] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu,
+                                      0xffffffffu, 0xffffffffu, 0xfffffffeu, 0x00000000u};
+  static constexpr uint32_t e[NW] = {0xfffffffdu, 0xffffffffu, 0xffffffffu, 0x00000000u,
+                                     0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu};
   static constexpr uint32_t minv = 1u;
   static constexpr bool is_p = true;
 };
 struct ModN {
-  static constexpr uint32_t m[8] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
-                                    0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
-  static constexpr uint32_t r2[8] = {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu,
-                                     0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u};
-  static constexpr uint32_t r1[8] = {0x039cdaafu, 0x0c46353du, 0x58e8617bu, 0x43190552u,
-                                     0x00000000u, 0x00000000u, 0xffffffffu, 0x00000000u};
-  static constexpr uint32_t e[8] = {0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
-                                    0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+  static constexpr uint32_t m[NW] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                     0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+  static constexpr uint32_t r2[NW] = {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu,
+                                      0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u};
+  static constexpr uint32_t r1[NW] = {0x039cdaafu, 0x0c46353du, 0x58e8617bu, 0x43190552u,
+                                      0x00000000u, 0x00000000u, 0xffffffffu, 0x00000000u};
+  static constexpr uint32_t e[NW] = {0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                     0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
   static constexpr uint32_t minv = 0xee00bc4fu;
   static constexpr bool is_p = false;
 };
-#else
-// brainpoolP256r1 (RFC 5639 3.4): m, R^2 mod m, R mod m, m - 2 (Fermat exponent), -m^-1 mod 2^32; aR = A R mod p
+#elif PZK_EC_CURVE == 1
+// brainpoolP256r1 (RFC 5639 3.4)
+static constexpr bool EC_A_M3 = false;
 struct ModP {
-  static constexpr uint32_t m[8] = {0x1f6e5377u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
-                                    0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
-  static constexpr uint32_t r2[8] = {0xa6465b6cu, 0x8cfedf7bu, 0x614d4f4du, 0x5cce4c26u,
-                                     0x6b1ac807u, 0xa1ecdacdu, 0xe5957fa8u, 0x4717aa21u};
-  static constexpr uint32_t r1[8] = {0xe091ac89u, 0xdfecb7e2u, 0x2ad9dfd7u, 0x91c409dcu,
-                                     0x627c728du, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
-  static constexpr uint32_t e[8] = {0x1f6e5375u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
-                                    0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t m[NW] = {0x1f6e5377u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
+                                     0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t r2[NW] = {0xa6465b6cu, 0x8cfedf7bu, 0x614d4f4du, 0x5cce4c26u,
+                                      0x6b1ac807u, 0xa1ecdacdu, 0xe5957fa8u, 0x4717aa21u};
+  static constexpr uint32_t r1[NW] = {0xe091ac89u, 0xdfecb7e2u, 0x2ad9dfd7u, 0x91c409dcu,
+                                      0x627c728du, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
+  static constexpr uint32_t e[NW] = {0x1f6e5375u, 0x2013481du, 0xd5262028u, 0x6e3bf623u,
+                                     0x9d838d72u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
   static constexpr uint32_t minv = 0xcefd89b9u;
   static constexpr bool is_p = true;
-  static constexpr uint32_t aR[8] = {0x69696261u, 0xd5d18edfu, 0xc1d20c64u, 0xa68123f1u,
-                                     0x6398556eu, 0x95ec1e5eu, 0xd666bc17u, 0x1e4676abu};
+  static constexpr uint32_t aR[NW] = {0x69696261u, 0xd5d18edfu, 0xc1d20c64u, 0xa68123f1u,
+                                      0x6398556eu, 0x95ec1e5eu, 0xd666bc17u, 0x1e4676abu};
 };
 struct ModN {
-  static constexpr uint32_t m[8] = {0x974856a7u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
-                                    0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
-  static constexpr uint32_t r2[8] = {0x3312fca6u, 0xe1d8d8deu, 0x1134e4a0u, 0xf35d176au,
-                                     0x6c815cb0u, 0x9b7f25e7u, 0xc3236762u, 0x0b25f1b9u};
-  static constexpr uint32_t r1[8] = {0x68b7a959u, 0x6fe1f17du, 0x4a9e5908u, 0x73c6855cu,
-                                     0x627c728eu, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
-  static constexpr uint32_t e[8] = {0x974856a5u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
-                                    0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t m[NW] = {0x974856a7u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
+                                     0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
+  static constexpr uint32_t r2[NW] = {0x3312fca6u, 0xe1d8d8deu, 0x1134e4a0u, 0xf35d176au,
+                                      0x6c815cb0u, 0x9b7f25e7u, 0xc3236762u, 0x0b25f1b9u};
+  static constexpr uint32_t r1[NW] = {0x68b7a959u, 0x6fe1f17du, 0x4a9e5908u, 0x73c6855cu,
+                                      0x627c728eu, 0xc199f56fu, 0x5e115643u, 0x5604a824u};
+  static constexpr uint32_t e[NW] = {0x974856a5u, 0x901e0e82u, 0xb561a6f7u, 0x8c397aa3u,
+                                     0x9d838d71u, 0x3e660a90u, 0xa1eea9bcu, 0xa9fb57dbu};
   static constexpr uint32_t minv = 0xcbb40ee9u;
+  static constexpr bool is_p = false;
+};
+#elif PZK_EC_CURVE == 2
+// secp224r1 (FIPS 186-4 D.1.2.2), 7 words
+static constexpr bool EC_A_M3 = true;
+struct ModP {
+  static constexpr uint32_t m[NW] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  static constexpr uint32_t r2[NW] = {0x00000001u, 0x00000000u, 0x00000000u, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0x00000000u};
+  static constexpr uint32_t r1[NW] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u};
+  static constexpr uint32_t e[NW] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  static constexpr uint32_t minv = 0xffffffffu;
+  static constexpr bool is_p = true;
+};
+struct ModN {
+  static constexpr uint32_t m[NW] = {0x5c5c2a3du, 0x13dd2945u, 0xe0b8f03eu, 0xffff16a2u, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  static constexpr uint32_t r2[NW] = {0x3ad01289u, 0x6bdaae6cu, 0x97a54552u, 0x6ad09d91u, 0xb1e97961u, 0x1822bc47u, 0xd4baa4cfu};
+  static constexpr uint32_t r1[NW] = {0xa3a3d5c3u, 0xec22d6bau, 0x1f470fc1u, 0x0000e95du, 0x00000000u, 0x00000000u, 0x00000000u};
+  static constexpr uint32_t e[NW] = {0x5c5c2a3bu, 0x13dd2945u, 0xe0b8f03eu, 0xffff16a2u, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  static constexpr uint32_t minv = 0x6a1fc2ebu;
+  static constexpr bool is_p = false;
+};
+#else
+// brainpoolP384r1 (RFC 5639 3.6), 12 words
+static constexpr bool EC_A_M3 = false;
+struct ModP {
+  static constexpr uint32_t m[NW] = {0x3107ec53u, 0x87470013u, 0x901d1a71u, 0xacd3a729u, 0x7fb71123u, 0x12b1da19u,
+                                     0xed5456b4u, 0x152f7109u, 0x50e641dfu, 0x0f5d6f7eu, 0xa3386d28u, 0x8cb91e82u};
+  static constexpr uint32_t r2[NW] = {0x40b64bdeu, 0x087cefffu, 0x3d7fd965u, 0x53528334u, 0xc9940899u, 0x8e28f99cu,
+                                      0x9918d5afu, 0x62140191u, 0xa57e052cu, 0xd5c6ef3bu, 0x178df842u, 0x36bf6883u};
+  static constexpr uint32_t r1[NW] = {0xcef813adu, 0x78b8ffecu, 0x6fe2e58eu, 0x532c58d6u, 0x8048eedcu, 0xed4e25e6u,
+                                      0x12aba94bu, 0xead08ef6u, 0xaf19be20u, 0xf0a29081u, 0x5cc792d7u, 0x7346e17du};
+  static constexpr uint32_t e[NW] = {0x3107ec51u, 0x87470013u, 0x901d1a71u, 0xacd3a729u, 0x7fb71123u, 0x12b1da19u,
+                                     0xed5456b4u, 0x152f7109u, 0x50e641dfu, 0x0f5d6f7eu, 0xa3386d28u, 0x8cb91e82u};
+  static constexpr uint32_t minv = 0xea9ec825u;
+  static constexpr bool is_p = true;
+  static constexpr uint32_t aR[NW] = {0x466c3c99u, 0xdb26b895u, 0xf157b07bu, 0x75d7f3feu, 0xd7f10db4u, 0x936771b9u,
+                                      0x35529374u, 0xe7ffe9e5u, 0x42b00c60u, 0x400a8fdfu, 0xa2e8c0d1u, 0x7c338021u};
+};
+struct ModN {
+  static constexpr uint32_t m[NW] = {0xe9046565u, 0x3b883202u, 0x6b7fc310u, 0xcf3ab6afu, 0xac0425a7u, 0x1f166e6cu,
+                                     0xed5456b3u, 0x152f7109u, 0x50e641dfu, 0x0f5d6f7eu, 0xa3386d28u, 0x8cb91e82u};
+  static constexpr uint32_t r2[NW] = {0xde771c8eu, 0xac4ed3a2u, 0x2f2b6b6eu, 0x37264e20u, 0x9802688au, 0x2a927e3bu,
+                                      0x52d748ffu, 0x574a74cbu, 0x65165fdbu, 0x8f886dc9u, 0x614e97c2u, 0x0ce8941au};
+  static constexpr uint32_t r1[NW] = {0x16fb9a9bu, 0xc477cdfdu, 0x94803cefu, 0x30c54950u, 0x53fbda58u, 0xe0e99193u,
+                                      0x12aba94cu, 0xead08ef6u, 0xaf19be20u, 0xf0a29081u, 0x5cc792d7u, 0x7346e17du};
+  static constexpr uint32_t e[NW] = {0xe9046563u, 0x3b883202u, 0x6b7fc310u, 0xcf3ab6afu, 0xac0425a7u, 0x1f166e6cu,
+                                     0xed5456b3u, 0x152f7109u, 0x50e641dfu, 0x0f5d6f7eu, 0xa3386d28u, 0x8cb91e82u};
+  static constexpr uint32_t minv = 0x5cb5bb93u;
   static constexpr bool is_p = false;
 };
 #endif
 using ModPFwd = ModP;
 using ModNFwd = ModN;
 
-template <class M> __device__ __forceinline__ e8 m_const(const uint32_t (&c)[8]) { e8 r; for (int i = 0; i < 8; i++) r.v[i] = c[i]; return r; }
+template <class M> __device__ __forceinline__ eW m_const(const uint32_t (&c)[NW]) { eW r; for (int i = 0; i < NW; i++) r.v[i] = c[i]; return r; }
 // r = t - m if t >= m (t < 2m, t given with a carry word)
-template <class M> __device__ __forceinline__ e8 m_reduce(const uint32_t* t, uint32_t top) {
-  e8 d; uint64_t br = 0;
+template <class M> __device__ __forceinline__ eW m_reduce(const uint32_t* t, uint32_t top) {
+  eW d; uint64_t br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) { uint64_t x = (uint64_t)t[i] - M::m[i] - br; d.v[i] = (uint32_t)x; br = (x >> 32) & 1; }
+  for (int i = 0; i < NW; i++) { uint64_t x = (uint64_t)t[i] - M::m[i] - br; d.v[i] = (uint32_t)x; br = (x >> 32) & 1; }
   if (top || !br) return d;
-  e8 r;
+  eW r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  for (int i = 0; i < NW; i++) r.v[i] = t[i];
   return r;
 }
-template <class M> __device__ __forceinline__ e8 m_mul_inl(const e8& a, const e8& b) {
-  uint32_t t[10];
+template <class M> __device__ __forceinline__ eW m_mul_inl(const eW& a, const eW& b) {
+  uint32_t t[NW + 2];
 #pragma unroll
-  for (int j = 0; j < 10; j++) t[j] = 0;
+  for (int j = 0; j < NW + 2; j++) t[j] = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < NW; i++) {
     uint64_t C = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) { uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + C; t[j] = (uint32_t)s; C = s >> 32; }
-    uint64_t s = (uint64_t)t[8] + C; t[8] = (uint32_t)s; t[9] = (uint32_t)(s >> 32);
+    for (int j = 0; j < NW; j++) { uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + C; t[j] = (uint32_t)s; C = s >> 32; }
+    uint64_t s = (uint64_t)t[NW] + C; t[NW] = (uint32_t)s; t[NW + 1] = (uint32_t)(s >> 32);
     const uint32_t m = t[0] * M::minv;
     s = (uint64_t)m * M::m[0] + t[0]; C = s >> 32;
 #pragma unroll
-    for (int j = 1; j < 8; j++) { s = (uint64_t)m * M::m[j] + t[j] + C; t[j - 1] = (uint32_t)s; C = s >> 32; }
-    s = (uint64_t)t[8] + C; t[7] = (uint32_t)s; t[8] = t[9] + (uint32_t)(s >> 32);
+    for (int j = 1; j < NW; j++) { s = (uint64_t)m * M::m[j] + t[j] + C; t[j - 1] = (uint32_t)s; C = s >> 32; }
+    s = (uint64_t)t[NW] + C; t[NW - 1] = (uint32_t)s; t[NW] = t[NW + 1] + (uint32_t)(s >> 32);
   }
-  return m_reduce<M>(t, t[8]);
+  return m_reduce<M>(t, t[NW]);
 }
 // Out of line: the point chains are long straight-line sequences of products; inlining every
-// 128-mad product makes k_ec_chain ~40 k instructions and instruction-fetch bound.
-__device__ __noinline__ e8 m_mul_p(e8 a, e8 b) { return m_mul_inl<ModPFwd>(a, b); }
-__device__ __noinline__ e8 m_mul_n(e8 a, e8 b) { return m_mul_inl<ModNFwd>(a, b); }
-template <class M> __device__ __forceinline__ e8 m_mul(const e8& a, const e8& b) {
+// product makes k_ec_chain ~40 k instructions and instruction-fetch bound.
+__device__ __noinline__ eW m_mul_p(eW a, eW b) { return m_mul_inl<ModPFwd>(a, b); }
+__device__ __noinline__ eW m_mul_n(eW a, eW b) { return m_mul_inl<ModNFwd>(a, b); }
+template <class M> __device__ __forceinline__ eW m_mul(const eW& a, const eW& b) {
   if constexpr (M::is_p) return m_mul_p(a, b); else return m_mul_n(a, b);
 }
-template <class M> __device__ __forceinline__ e8 m_add(const e8& a, const e8& b) {
-  uint32_t t[8]; uint64_t c = 0;
+template <class M> __device__ __forceinline__ eW m_add(const eW& a, const eW& b) {
+  uint32_t t[NW]; uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)a.v[i] + b.v[i] + c; t[i] = (uint32_t)s; c = s >> 32; }
+  for (int i = 0; i < NW; i++) { uint64_t s = (uint64_t)a.v[i] + b.v[i] + c; t[i] = (uint32_t)s; c = s >> 32; }
   return m_reduce<M>(t, (uint32_t)c);
 }
-template <class M> __device__ __forceinline__ e8 m_sub(const e8& a, const e8& b) {
-  e8 r; uint64_t br = 0;
+template <class M> __device__ __forceinline__ eW m_sub(const eW& a, const eW& b) {
+  eW r; uint64_t br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) { uint64_t d = (uint64_t)a.v[i] - b.v[i] - br; r.v[i] = (uint32_t)d; br = (d >> 32) & 1; }
+  for (int i = 0; i < NW; i++) { uint64_t d = (uint64_t)a.v[i] - b.v[i] - br; r.v[i] = (uint32_t)d; br = (d >> 32) & 1; }
   if (br) {
     uint64_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) { uint64_t s = (uint64_t)r.v[i] + M::m[i] + c; r.v[i] = (uint32_t)s; c = s >> 32; }
+    for (int i = 0; i < NW; i++) { uint64_t s = (uint64_t)r.v[i] + M::m[i] + c; r.v[i] = (uint32_t)s; c = s >> 32; }
   }
   return r;
 }
-template <class M> __device__ __forceinline__ e8 m_to(const e8& a) { return m_mul<M>(a, m_const<M>(M::r2)); }
-template <class M> __device__ __forceinline__ e8 m_from(const e8& a) { e8 one{}; for (int i = 0; i < 8; i++) one.v[i] = i == 0; return m_mul<M>(a, one); }
-template <class M> __device__ __forceinline__ bool m_is_zero(const e8& a) { uint32_t o = 0; for (int i = 0; i < 8; i++) o |= a.v[i]; return o == 0; }
+template <class M> __device__ __forceinline__ eW m_to(const eW& a) { return m_mul<M>(a, m_const<M>(M::r2)); }
+template <class M> __device__ __forceinline__ eW m_from(const eW& a) { eW one{}; for (int i = 0; i < NW; i++) one.v[i] = i == 0; return m_mul<M>(a, one); }
+template <class M> __device__ __forceinline__ bool m_is_zero(const eW& a) { uint32_t o = 0; for (int i = 0; i < NW; i++) o |= a.v[i]; return o == 0; }
 // a^(m-2) (Montgomery in/out), 4-bit fixed window; 0 -> 0 (mod_inv, bigIntFunc.circom:430-466)
-template <class M> __device__ e8 m_inv(const e8& a) {
-  e8 tbl[16];
+template <class M> __device__ eW m_inv(const eW& a) {
+  eW tbl[16];
   tbl[0] = m_const<M>(M::r1);
   tbl[1] = a;
   for (int i = 2; i < 16; i++) tbl[i] = m_mul<M>(tbl[i - 1], a);
-  e8 r = tbl[0];
-  for (int w = 63; w >= 0; w--) {
-    if (w != 63) for (int k = 0; k < 4; k++) r = m_mul<M>(r, r);
+  eW r = tbl[0];
+  for (int w = 8 * NW - 1; w >= 0; w--) {
+    if (w != 8 * NW - 1) for (int k = 0; k < 4; k++) r = m_mul<M>(r, r);
     const uint32_t nib = (M::e[w >> 3] >> ((w & 7) * 4)) & 15u;
-    e8 s = tbl[0];
+    eW s = tbl[0];
 #pragma unroll
     for (int q = 1; q < 16; q++) if ((uint32_t)q == nib) s = tbl[q];
     if (nib) r = m_mul<M>(r, s);
   }
   return r;
 }
-__device__ __forceinline__ e8 e8_from_u64(const uint64_t* x) {
-  e8 r;
-  for (int i = 0; i < 4; i++) { r.v[2 * i] = (uint32_t)x[i]; r.v[2 * i + 1] = (uint32_t)(x[i] >> 32); }
+// chunks (NL x CS bits, one per u64) / 64-bit scratch words <-> field words
+__device__ __forceinline__ eW ew_from_chunks(const uint64_t* x) {
+  eW r;
+  if (CS == 64) {
+#pragma unroll
+    for (int i = 0; i < NW / 2; i++) { r.v[2 * i] = (uint32_t)x[i]; r.v[2 * i + 1] = (uint32_t)(x[i] >> 32); }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NW; i++) r.v[i] = (uint32_t)x[i];
+  }
   return r;
 }
-__device__ __forceinline__ void e8_to_u64(const e8& a, uint64_t* x) {
-  for (int i = 0; i < 4; i++) x[i] = (uint64_t)a.v[2 * i + 1] << 32 | a.v[2 * i];
+__device__ __forceinline__ void ew_to_chunks(const eW& a, uint64_t* x) {
+  if (CS == 64) {
+#pragma unroll
+    for (int i = 0; i < NW / 2; i++) x[i] = (uint64_t)a.v[2 * i + 1] << 32 | a.v[2 * i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NW; i++) x[i] = a.v[i];
+  }
+}
+__device__ __forceinline__ eW ew_from_words(const uint64_t* x) {
+  eW r;
+#pragma unroll
+  for (int i = 0; i < NW; i++) r.v[i] = (uint32_t)(x[i >> 1] >> (32 * (i & 1)));
+  return r;
+}
+__device__ __forceinline__ void ew_to_words(const eW& a, uint64_t* x) {
+#pragma unroll
+  for (int i = 0; i < JW; i++) x[i] = (2 * i + 1 < NW ? (uint64_t)a.v[2 * i + 1] << 32 : 0ull) | a.v[2 * i];
 }
 
 // Jacobian points (Montgomery mod p)
-struct Jac { e8 x, y, z; };
-#if PZK_EC_CURVE == 0
-// dbl-2001-b, a = -3 (P-256: A = p - 3)
+struct Jac { eW x, y, z; };
+template <class M = ModP>  // a template so the general-a branch (M::aR) is discarded for a = -3 curves
 __device__ Jac jac_dbl(const Jac& P) {
-  using M = ModP;
-  e8 delta = m_mul<M>(P.z, P.z), gamma = m_mul<M>(P.y, P.y), beta = m_mul<M>(P.x, gamma);
-  e8 t = m_mul<M>(m_sub<M>(P.x, delta), m_add<M>(P.x, delta));
-  e8 alpha = m_add<M>(m_add<M>(t, t), t);
-  e8 b4 = m_add<M>(beta, beta); b4 = m_add<M>(b4, b4);
-  Jac R;
-  R.x = m_sub<M>(m_mul<M>(alpha, alpha), m_add<M>(b4, b4));
-  e8 yz = m_add<M>(P.y, P.z);
-  R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), gamma), delta);
-  e8 g2 = m_mul<M>(gamma, gamma);
-  e8 g8 = m_add<M>(g2, g2); g8 = m_add<M>(g8, g8); g8 = m_add<M>(g8, g8);
-  R.y = m_sub<M>(m_mul<M>(alpha, m_sub<M>(b4, R.x)), g8);
-  return R;
+  if constexpr (EC_A_M3) {  // dbl-2001-b, a = -3 (P-256, P-224: A = p - 3)
+    eW delta = m_mul<M>(P.z, P.z), gamma = m_mul<M>(P.y, P.y), beta = m_mul<M>(P.x, gamma);
+    eW t = m_mul<M>(m_sub<M>(P.x, delta), m_add<M>(P.x, delta));
+    eW alpha = m_add<M>(m_add<M>(t, t), t);
+    eW b4 = m_add<M>(beta, beta); b4 = m_add<M>(b4, b4);
+    Jac R;
+    R.x = m_sub<M>(m_mul<M>(alpha, alpha), m_add<M>(b4, b4));
+    eW yz = m_add<M>(P.y, P.z);
+    R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), gamma), delta);
+    eW g2 = m_mul<M>(gamma, gamma);
+    eW g8 = m_add<M>(g2, g2); g8 = m_add<M>(g8, g8); g8 = m_add<M>(g8, g8);
+    R.y = m_sub<M>(m_mul<M>(alpha, m_sub<M>(b4, R.x)), g8);
+    return R;
+  } else {  // dbl-2007-bl, general a (brainpool)
+    eW xx = m_mul<M>(P.x, P.x), yy = m_mul<M>(P.y, P.y), zz = m_mul<M>(P.z, P.z), yyyy = m_mul<M>(yy, yy);
+    eW xyy = m_add<M>(P.x, yy);
+    eW s = m_sub<M>(m_sub<M>(m_mul<M>(xyy, xyy), xx), yyyy);
+    s = m_add<M>(s, s);
+    eW mm = m_add<M>(m_add<M>(xx, xx), xx);
+    mm = m_add<M>(mm, m_mul<M>(m_const<M>(M::aR), m_mul<M>(zz, zz)));
+    Jac R;
+    R.x = m_sub<M>(m_mul<M>(mm, mm), m_add<M>(s, s));
+    eW y8 = m_add<M>(yyyy, yyyy); y8 = m_add<M>(y8, y8); y8 = m_add<M>(y8, y8);
+    R.y = m_sub<M>(m_mul<M>(mm, m_sub<M>(s, R.x)), y8);
+    eW yz = m_add<M>(P.y, P.z);
+    R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), yy), zz);
+    return R;
+  }
 }
-#else
-// dbl-2007-bl, general a (brainpoolP256r1)
-__device__ Jac jac_dbl(const Jac& P) {
-  using M = ModP;
-  e8 xx = m_mul<M>(P.x, P.x), yy = m_mul<M>(P.y, P.y), zz = m_mul<M>(P.z, P.z), yyyy = m_mul<M>(yy, yy);
-  e8 xyy = m_add<M>(P.x, yy);
-  e8 s = m_sub<M>(m_sub<M>(m_mul<M>(xyy, xyy), xx), yyyy);
-  s = m_add<M>(s, s);
-  e8 mm = m_add<M>(m_add<M>(xx, xx), xx);
-  mm = m_add<M>(mm, m_mul<M>(m_const<M>(M::aR), m_mul<M>(zz, zz)));
-  Jac R;
-  R.x = m_sub<M>(m_mul<M>(mm, mm), m_add<M>(s, s));
-  e8 y8 = m_add<M>(yyyy, yyyy); y8 = m_add<M>(y8, y8); y8 = m_add<M>(y8, y8);
-  R.y = m_sub<M>(m_mul<M>(mm, m_sub<M>(s, R.x)), y8);
-  e8 yz = m_add<M>(P.y, P.z);
-  R.z = m_sub<M>(m_sub<M>(m_mul<M>(yz, yz), yy), zz);
-  return R;
-}
-#endif
 // add-2007-bl (P != +-Q; H = 0 gives Z3 = 0, flagged by the caller)
 __device__ Jac jac_add(const Jac& P, const Jac& Q) {
   using M = ModP;
-  e8 z1z1 = m_mul<M>(P.z, P.z), z2z2 = m_mul<M>(Q.z, Q.z);
-  e8 u1 = m_mul<M>(P.x, z2z2), u2 = m_mul<M>(Q.x, z1z1);
-  e8 s1 = m_mul<M>(m_mul<M>(P.y, Q.z), z2z2), s2 = m_mul<M>(m_mul<M>(Q.y, P.z), z1z1);
-  e8 h = m_sub<M>(u2, u1), h2 = m_add<M>(h, h);
-  e8 i = m_mul<M>(h2, h2), j = m_mul<M>(h, i);
-  e8 r = m_sub<M>(s2, s1); r = m_add<M>(r, r);
-  e8 v = m_mul<M>(u1, i);
+  eW z1z1 = m_mul<M>(P.z, P.z), z2z2 = m_mul<M>(Q.z, Q.z);
+  eW u1 = m_mul<M>(P.x, z2z2), u2 = m_mul<M>(Q.x, z1z1);
+  eW s1 = m_mul<M>(m_mul<M>(P.y, Q.z), z2z2), s2 = m_mul<M>(m_mul<M>(Q.y, P.z), z1z1);
+  eW h = m_sub<M>(u2, u1), h2 = m_add<M>(h, h);
+  eW i = m_mul<M>(h2, h2), j = m_mul<M>(h, i);
+  eW r = m_sub<M>(s2, s1); r = m_add<M>(r, r);
+  eW v = m_mul<M>(u1, i);
   Jac R;
   R.x = m_sub<M>(m_sub<M>(m_mul<M>(r, r), j), m_add<M>(v, v));
-  e8 s1j = m_mul<M>(s1, j);
+  eW s1j = m_mul<M>(s1, j);
   R.y = m_sub<M>(m_mul<M>(r, m_sub<M>(v, R.x)), m_add<M>(s1j, s1j));
-  e8 zz = m_add<M>(P.z, Q.z);
+  eW zz = m_add<M>(P.z, Q.z);
   R.z = m_mul<M>(m_sub<M>(m_sub<M>(m_mul<M>(zz, zz), z1z1), z2z2), h);
   return R;
 }
 
 // madd-2007-bl: Q affine (Z2 = 1), 7M + 4S
-__device__ Jac jac_add_aff(const Jac& P, const e8& x2, const e8& y2) {
+__device__ Jac jac_add_aff(const Jac& P, const eW& x2, const eW& y2) {
   using M = ModP;
-  e8 z1z1 = m_mul<M>(P.z, P.z);
-  e8 u2 = m_mul<M>(x2, z1z1), s2 = m_mul<M>(m_mul<M>(y2, P.z), z1z1);
-  e8 h = m_sub<M>(u2, P.x), hh = m_mul<M>(h, h);
-  e8 i = m_add<M>(hh, hh); i = m_add<M>(i, i);
-  e8 j = m_mul<M>(h, i);
-  e8 r = m_sub<M>(s2, P.y); r = m_add<M>(r, r);
-  e8 v = m_mul<M>(P.x, i);
+  eW z1z1 = m_mul<M>(P.z, P.z);
+  eW u2 = m_mul<M>(x2, z1z1), s2 = m_mul<M>(m_mul<M>(y2, P.z), z1z1);
+  eW h = m_sub<M>(u2, P.x), hh = m_mul<M>(h, h);
+  eW i = m_add<M>(hh, hh); i = m_add<M>(i, i);
+  eW j = m_mul<M>(h, i);
+  eW r = m_sub<M>(s2, P.y); r = m_add<M>(r, r);
+  eW v = m_mul<M>(P.x, i);
   Jac R;
   R.x = m_sub<M>(m_sub<M>(m_mul<M>(r, r), j), m_add<M>(v, v));
-  e8 yj = m_mul<M>(P.y, j);
+  eW yj = m_mul<M>(P.y, j);
   R.y = m_sub<M>(m_mul<M>(r, m_sub<M>(v, R.x)), m_add<M>(yj, yj));
-  e8 zh = m_add<M>(P.z, h);
+  eW zh = m_add<M>(P.z, h);
   R.z = m_sub<M>(m_sub<M>(m_mul<M>(zh, zh), z1z1), hh);
   return R;
 }
 
-// ============================================================ k_ec_core
+// ============================================================ the EC core
 // handles of points: >= 0 op output; H_D dummy point; H_Q public key; <= -1000 fixed-base table entry
 constexpr int H_D = -1, H_Q = -2;
 __host__ __device__ constexpr int h_tab(int i, int j) { return -(1000 + i * 256 + j); }
 enum { PT_GM_AP, PT_GM_RP, PT_PRE, PT_SM_AP, PT_SM_RP };
-
-// The data flow of verifyECDSABits' two scalar multiplications (ec/curve.circom:356-494, 672-906):
-// calls on_op(op, in1, in2) for every point operation in op order and on_pt(kind, index, handle)
-// for every point the selection logic forwards (additionPoints / resultingPoints / precompute).
-// The isZero/isDummy decisions compare handles: a forwarded dummy is the dummy itself, and a
-// curve point equal in x[0] to a dummy by chance has probability ~2^-64.
-template <class OnOp, class OnPt>
-__device__ void ec_plan(const uint64_t* u1, const uint64_t* u2, OnOp on_op, OnPt on_pt) {
-  auto gm_ap = [&](int i) {
-    int b = (int)((u1[i >> 3] >> (8 * (i & 7))) & 255);
-    return b ? h_tab(i, b) : (i % 2 == 0 ? H_D : EC_OP_SD);
-  };
-  on_op(EC_OP_SD, H_D, 0);
-  for (int i = 0; i < 32; i++) on_pt(PT_GM_AP, i, gm_ap(i));
-  int left = gm_ap(0);
-  for (int i = 0; i < 31; i++) {
-    const int right = gm_ap(i + 1);
-    on_op(ec_op_gm_add(i), left, right);
-    const bool ld = left == H_D || left == EC_OP_SD, rd = right == H_D || right == EC_OP_SD;
-    const int rp = ld ? right : rd ? left : ec_op_gm_add(i);
-    on_pt(PT_GM_RP, i, rp);
-    left = rp;
-  }
-  const int gm_out = left;
-  auto pre = [](int i) { return i == 0 ? H_D : i == 1 ? H_Q : ec_op_pre(i); };
-  on_pt(PT_PRE, 0, H_D);
-  on_pt(PT_PRE, 1, H_Q);
-  for (int i = 2; i < 16; i++) {
-    if (i % 2 == 0) on_op(ec_op_pre(i), pre(i / 2), 0);
-    else on_op(ec_op_pre(i), H_Q, pre(i - 1));
-    on_pt(PT_PRE, i, ec_op_pre(i));
-  }
-  auto nib = [&](int w) { int b = 252 - 4 * w; return (int)((u2[b >> 6] >> (b & 63)) & 15); };
-  on_pt(PT_SM_RP, 0, H_D);
-  int rp = pre(nib(0));
-  on_pt(PT_SM_AP, 0, rp);
-  on_pt(PT_SM_RP, 1, rp);
-  for (int w = 1; w < 64; w++) {
-    const int ap = pre(nib(w));
-    on_pt(PT_SM_AP, w, ap);
-    const bool izr = rp == H_D, iza = ap == H_D;
-    for (int j = 0; j < 4; j++) {
-      const int op = ec_op_sm_dbl(4 * w - 4 + j);
-      on_op(op, j == 0 ? (izr ? H_D : rp) : op - 1, 0);
-    }
-    const int dl = ec_op_sm_dbl(4 * w - 1), ad = ec_op_sm_add(w - 1);
-    on_op(ad, dl, ap);
-    rp = izr ? ap : iza ? dl : ad;
-    on_pt(PT_SM_RP, w + 1, rp);
-  }
-  on_op(EC_OP_FINAL, gm_out, rp);
-}
 
 // Fr (BN254) of a - b for 64-bit a, b
 __device__ __forceinline__ fr fr_diff_u64(uint64_t a, uint64_t b) {
   return a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
 }
 
-// ---- k_ec_core scratch per witness (u64): per op X, Y, Z (Montgomery) + input handles; then the
-// handles of the forwarded points (gm_ap[32], gm_rp[31], pre[16], sm_ap[64], sm_rp[65])
-constexpr int ECJ_OP = 16, ECJ_PTS = EC_N_OPS * ECJ_OP, EC_N_PTS = 32 + 31 + 16 + 64 + 65;
+// forwarded points (additionPoints / resultingPoints / precompute) of the two scalar multiplications:
+// index into the chain's handle list, and the EC core word of the affine point
 __host__ __device__ constexpr int ec_pt_index(int kind, int i) {
-  return kind == PT_GM_AP ? i : kind == PT_GM_RP ? 32 + i : kind == PT_PRE ? 63 + i : kind == PT_SM_AP ? 79 + i : 143 + i;
+  return kind == PT_GM_AP ? i : kind == PT_GM_RP ? ECG.parts + i : kind == PT_PRE ? 2 * ECG.parts - 1 + i
+       : kind == PT_SM_AP ? 2 * ECG.parts + 15 + i : 2 * ECG.parts + 15 + ECG.wins + i;
 }
-__host__ __device__ constexpr int ec_pt_base(int idx) {  // EC core word of forwarded point idx
-  return idx < 32 ? ECC_GM_AP + 8 * idx : idx < 63 ? ECC_GM_RP + 8 * (idx - 32) : idx < 79 ? ECC_PRE + 8 * (idx - 63)
-       : idx < 143 ? ECC_SM_AP + 8 * (idx - 79) : ECC_SM_RP + 8 * (idx - 143);
+__host__ __device__ constexpr int ec_pt_base(int idx) {
+  return idx < ECG.parts ? ECG.c_gm_ap + P2 * idx
+       : idx < 2 * ECG.parts - 1 ? ECG.c_gm_rp + P2 * (idx - ECG.parts)
+       : idx < 2 * ECG.parts + 15 ? ECG.c_pre + P2 * (idx - (2 * ECG.parts - 1))
+       : idx < 2 * ECG.parts + 15 + ECG.wins ? ECG.c_sm_ap + P2 * (idx - (2 * ECG.parts + 15))
+       : ECG.c_sm_rp + P2 * (idx - (2 * ECG.parts + 15 + ECG.wins));
 }
-static_assert(EC_JAC_WORDS >= ECJ_PTS + (EC_N_PTS + 1) / 2, "EC Jacobian scratch");
+static_assert(ec_pt_index(PT_SM_RP, ECG.wins) + 1 == ECG.n_pts, "EC forwarded points");
+
+// byte i / nibble at bit b of a chunked scalar
+__device__ __forceinline__ int sc_byte(const uint64_t* s, int i) { return (int)((s[(8 * i) / CS] >> ((8 * i) % CS)) & 255); }
+__device__ __forceinline__ int sc_nib(const uint64_t* s, int b) { return (int)((s[b / CS] >> (b % CS)) & 15); }
 
 __device__ __forceinline__ void ec_aff_const(const DevLayout& L, const uint8_t* row, int hd, uint64_t* xy) {
-  if (hd == H_D) { for (int i = 0; i < 8; i++) xy[i] = EC_D[i]; }
-  else if (hd == H_Q) { for (int i = 0; i < 8; i++) xy[i] = *reinterpret_cast<const uint64_t*>(row + 32ull * (L.reg.in_pk + i)); }
+  if (hd == H_D) { for (int i = 0; i < P2; i++) xy[i] = EC_D[i]; }
+  else if (hd == H_Q) { for (int i = 0; i < P2; i++) xy[i] = *reinterpret_cast<const uint64_t*>(row + 32ull * (L.reg.in_pk + i)); }
   else {
-    const uint64_t* T = L.ec_gpow + (size_t)(-hd - 1000) * 8;
-    for (int i = 0; i < 8; i++) xy[i] = T[i];
+    const uint64_t* T = L.ec_gpow + (size_t)(-hd - 1000) * P2;
+    for (int i = 0; i < P2; i++) xy[i] = T[i];
   }
 }
+// an input chunk: < 2^CS
+__device__ __forceinline__ bool in_is_chunk(const uint8_t* e) { return in_is_u64(e) && (in_u64(e) & ~CS_MASK) == 0; }
 
 // Phase 0, lane = witness: the scalars mod n and the BigMultModP records
 __global__ void __launch_bounds__(64) k_ec_scalars(DevLayout L, const uint8_t* inputs, const uint32_t* sha_core,
@@ -551,63 +604,67 @@ __global__ void __launch_bounds__(64) k_ec_scalars(DevLayout L, const uint8_t* i
   if (w >= batch) return;
   const RegInfo& G = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
-  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  uint64_t* C = ec_core + (size_t)w * ECG.core_words;
   int32_t* st = status ? status + w : nullptr;
   bool bad = false;
-  uint64_t r[4], s[4], h[4];
-  for (int i = 0; i < 4; i++) {
+  uint64_t r[NL], s[NL], h[NL];
+  for (int i = 0; i < NL; i++) {
     const uint8_t* a = row + 32ull * (G.in_sig + i);
-    const uint8_t* b = row + 32ull * (G.in_sig + 4 + i);
-    bad |= !in_is_u64(a) || !in_is_u64(b);
+    const uint8_t* b = row + 32ull * (G.in_sig + NL + i);
+    bad |= !in_is_chunk(a) || !in_is_chunk(b);
     r[i] = in_u64(a); s[i] = in_u64(b);
   }
-  for (int i = 0; i < 8; i++) bad |= !in_is_u64(row + 32ull * (G.in_pk + i));
+  for (int i = 0; i < P2; i++) bad |= !in_is_chunk(row + 32ull * (G.in_pk + i));
   if (bad) set_status(st, ST_INPUT_RANGE);
-  {  // hashedChunked[j] (ecdsa.circom:30-38): 64-bit big-endian digest words, least significant first
+  {  // hashedChunked[N-1-i] = digest bits [CS i, CS i + CS) (ecdsa.circom:30-38); the digest as big-endian u32 words
     const ShaJob job = L.sha[G.j_sa];
     const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.hout;
-    for (int j = 0; j < 4; j++) h[j] = ((uint64_t)H[2 * (3 - j)] << 32) | H[2 * (3 - j) + 1];
+    for (int j = 0; j < NL; j++) {
+      const int i = NL - 1 - j;
+      h[j] = CS == 64 ? ((uint64_t)H[2 * i] << 32) | H[2 * i + 1] : H[i];
+    }
   }
   // sinv = s^-1 (BigModInv, bigInt.circom:344-368), u1 = sinv h, u2 = sinv r (mod n)
   using N = ModN;
-  auto red_n = [&](const uint64_t* x) { e8 a = e8_from_u64(x); return m_reduce<N>(a.v, 0); };
-  const e8 sm = m_to<N>(red_n(s)), sinv_m = m_inv<N>(sm);
-  const e8 u1 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(h))));
-  const e8 u2 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(r))));
-  const e8 one_chk = m_from<N>(m_mul<N>(sm, sinv_m));
+  auto red_n = [&](const uint64_t* x) { eW a = ew_from_chunks(x); return m_reduce<N>(a.v, 0); };
+  const eW sm = m_to<N>(red_n(s)), sinv_m = m_inv<N>(sm);
+  const eW u1 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(h))));
+  const eW u2 = m_from<N>(m_mul<N>(sinv_m, m_to<N>(red_n(r))));
+  const eW one_chk = m_from<N>(m_mul<N>(sm, sinv_m));
   {
     uint32_t o = one_chk.v[0] ^ 1u;
-    for (int i = 1; i < 8; i++) o |= one_chk.v[i];
+    for (int i = 1; i < NW; i++) o |= one_chk.v[i];
     if (o) set_status(st, ST_ECDSA_INV);  // bigInt.circom:364-368
   }
-  uint64_t sinv[4], U1[4], U2[4];
-  e8_to_u64(m_from<N>(sinv_m), sinv);
-  e8_to_u64(u1, U1);
-  e8_to_u64(u2, U2);
-  for (int i = 0; i < 4; i++) {
-    C[ECC_SINV + i] = sinv[i]; C[ECC_U1 + i] = U1[i]; C[ECC_U2 + i] = U2[i]; C[ECC_H + i] = h[i];
-    C[ECC_MM + 8 * EC_MM_INV + i] = s[i];    C[ECC_MM + 8 * EC_MM_INV + 4 + i] = sinv[i];
-    C[ECC_MM + 8 * EC_MM_U1 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U1 + 4 + i] = h[i];
-    C[ECC_MM + 8 * EC_MM_U2 + i] = sinv[i];  C[ECC_MM + 8 * EC_MM_U2 + 4 + i] = r[i];
+  uint64_t sinv[NL], U1[NL], U2[NL];
+  ew_to_chunks(m_from<N>(sinv_m), sinv);
+  ew_to_chunks(u1, U1);
+  ew_to_chunks(u2, U2);
+  for (int i = 0; i < NL; i++) {
+    C[ECG.c_sinv + i] = sinv[i]; C[ECG.c_u1 + i] = U1[i]; C[ECG.c_u2 + i] = U2[i]; C[ECG.c_h + i] = h[i];
+    C[ECG.c_mm + P2 * EC_MM_INV + i] = s[i];    C[ECG.c_mm + P2 * EC_MM_INV + NL + i] = sinv[i];
+    C[ECG.c_mm + P2 * EC_MM_U1 + i] = sinv[i];  C[ECG.c_mm + P2 * EC_MM_U1 + NL + i] = h[i];
+    C[ECG.c_mm + P2 * EC_MM_U2 + i] = sinv[i];  C[ECG.c_mm + P2 * EC_MM_U2 + NL + i] = r[i];
   }
 }
 
 __device__ __forceinline__ void jac_store(uint64_t* d, const Jac& R, int h1, int h2) {
-  e8_to_u64(R.x, d); e8_to_u64(R.y, d + 4); e8_to_u64(R.z, d + 8);
-  d[12] = (uint64_t)(uint32_t)h1 | ((uint64_t)(uint32_t)h2 << 32);
+  ew_to_words(R.x, d); ew_to_words(R.y, d + JW); ew_to_words(R.z, d + 2 * JW);
+  d[3 * JW] = (uint64_t)(uint32_t)h1 | ((uint64_t)(uint32_t)h2 << 32);
 }
 __device__ __forceinline__ Jac jac_load(const uint64_t* s0) {
-  Jac P; P.x = e8_from_u64(s0); P.y = e8_from_u64(s0 + 4); P.z = e8_from_u64(s0 + 8); return P;
+  Jac P; P.x = ew_from_words(s0); P.y = ew_from_words(s0 + JW); P.z = ew_from_words(s0 + 2 * JW); return P;
 }
 __device__ __forceinline__ Jac jac_of_aff(const uint64_t* xy) {
-  Jac P; P.x = m_to<ModP>(e8_from_u64(xy)); P.y = m_to<ModP>(e8_from_u64(xy + 4)); P.z = m_const<ModP>(ModP::r1); return P;
+  Jac P; P.x = m_to<ModP>(ew_from_chunks(xy)); P.y = m_to<ModP>(ew_from_chunks(xy + NL)); P.z = m_const<ModP>(ModP::r1); return P;
 }
 
-// Phase 1, lane = (witness, chain): chain 0 = the generator multiplication (ops 0..31,
-// curve.circom:672-906), chain 1 = precompute + the window-4 scalar multiplication of the public
-// key (ops 32..360, curve.circom:249-494). Jacobian coordinates, the running point in registers,
-// mixed additions for affine operands; every op's result and input handles go to the scratch.
-// The isDummy decisions compare handles (see ec_plan).
+// Phase 1, lane = (witness, chain): chain 0 = the generator multiplication (ops 0 .. PARTS-1,
+// curve.circom:680-906), chain 1 = precompute + the window-4 scalar multiplication of the public
+// key (curve.circom:249-494). Jacobian coordinates, the running point in registers, mixed additions
+// for affine operands; every op's result and input handles go to the scratch. The isZero / isDummy
+// decisions compare handles: a forwarded dummy is the dummy itself, and a curve point equal in x[0]
+// to a dummy by chance has probability ~2^-CS.
 __global__ void __launch_bounds__(64) k_ec_chain(DevLayout L, const uint8_t* inputs, const uint64_t* ec_core,
                                                  uint64_t* ec_jac, uint32_t batch) {
   core_priority();
@@ -615,40 +672,40 @@ __global__ void __launch_bounds__(64) k_ec_chain(DevLayout L, const uint8_t* inp
   const uint32_t w = gid >> 1, chain = gid & 1;
   if (w >= batch) return;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
-  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
-  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
-  int32_t* pts = reinterpret_cast<int32_t*>(J + ECJ_PTS);
+  const uint64_t* C = ec_core + (size_t)w * ECG.core_words;
+  uint64_t* J = ec_jac + (size_t)w * ECG.jac_words;
+  int32_t* pts = reinterpret_cast<int32_t*>(J + ECG.j_pts);
   using M = ModP;
   if (chain == 0) {
-    uint64_t u1[4];
-    for (int i = 0; i < 4; i++) u1[i] = C[ECC_U1 + i];
+    uint64_t u1[NL];
+    for (int i = 0; i < NL; i++) u1[i] = C[ECG.c_u1 + i];
     auto gm_ap = [&](int i) {
-      int b = (int)((u1[i >> 3] >> (8 * (i & 7))) & 255);
+      int b = sc_byte(u1, i);
       return b ? h_tab(i, b) : (i % 2 == 0 ? H_D : EC_OP_SD);
     };
-    uint64_t dxy[8];
-    for (int i = 0; i < 8; i++) dxy[i] = EC_D[i];
+    uint64_t dxy[P2];
+    for (int i = 0; i < P2; i++) dxy[i] = EC_D[i];
     const Jac D = jac_of_aff(dxy);
     const Jac SD = jac_dbl(D);
-    jac_store(J + ECJ_OP * EC_OP_SD, SD, H_D, 0);
-    for (int i = 0; i < 32; i++) pts[ec_pt_index(PT_GM_AP, i)] = gm_ap(i);
+    jac_store(J + ECG.j_op * EC_OP_SD, SD, H_D, 0);
+    for (int i = 0; i < ECG.parts; i++) pts[ec_pt_index(PT_GM_AP, i)] = gm_ap(i);
     auto point = [&](int hd) -> Jac {  // D, 2D or a table entry
       if (hd == H_D) return D;
       if (hd == EC_OP_SD) return SD;
-      return jac_of_aff(L.ec_gpow + (size_t)(-hd - 1000) * 8);
+      return jac_of_aff(L.ec_gpow + (size_t)(-hd - 1000) * P2);
     };
     int left = gm_ap(0);
     Jac acc = point(left);
-    for (int i = 0; i < 31; i++) {
+    for (int i = 0; i < ECG.parts - 1; i++) {
       const int right = gm_ap(i + 1);
       Jac R;
       if (right <= -1000) {
-        const uint64_t* T = L.ec_gpow + (size_t)(-right - 1000) * 8;
-        R = jac_add_aff(acc, m_to<M>(e8_from_u64(T)), m_to<M>(e8_from_u64(T + 4)));
+        const uint64_t* T = L.ec_gpow + (size_t)(-right - 1000) * P2;
+        R = jac_add_aff(acc, m_to<M>(ew_from_chunks(T)), m_to<M>(ew_from_chunks(T + NL)));
       } else {
         R = jac_add(acc, right == H_D ? D : SD);
       }
-      jac_store(J + ECJ_OP * ec_op_gm_add(i), R, left, right);
+      jac_store(J + ECG.j_op * ec_op_gm_add(i), R, left, right);
       const bool ld = left == H_D || left == EC_OP_SD, rd = right == H_D || right == EC_OP_SD;
       const int rp = ld ? right : rd ? left : ec_op_gm_add(i);
       if (ld) acc = point(right);
@@ -657,43 +714,43 @@ __global__ void __launch_bounds__(64) k_ec_chain(DevLayout L, const uint8_t* inp
       left = rp;
     }
   } else {
-    uint64_t u2[4], qxy[8], dxy[8];
-    for (int i = 0; i < 4; i++) u2[i] = C[ECC_U2 + i];
+    uint64_t u2[NL], qxy[P2], dxy[P2];
+    for (int i = 0; i < NL; i++) u2[i] = C[ECG.c_u2 + i];
     ec_aff_const(L, row, H_Q, qxy);
-    for (int i = 0; i < 8; i++) dxy[i] = EC_D[i];
+    for (int i = 0; i < P2; i++) dxy[i] = EC_D[i];
     const Jac Q = jac_of_aff(qxy), D = jac_of_aff(dxy);
-    const e8 qx = Q.x, qy = Q.y;
-    auto pre = [](int i) { return i == 0 ? H_D : i == 1 ? H_Q : ec_op_pre(i); };
-    auto pre_jac = [&](int i) -> Jac { return i == 0 ? D : i == 1 ? Q : jac_load(J + ECJ_OP * ec_op_pre(i)); };
+    const eW qx = Q.x, qy = Q.y;
+    auto pre = [](int i) { return i == 0 ? H_D : i == 1 ? H_Q : ec_op_pre(ECG, i); };
+    auto pre_jac = [&](int i) -> Jac { return i == 0 ? D : i == 1 ? Q : jac_load(J + ECG.j_op * ec_op_pre(ECG, i)); };
     pts[ec_pt_index(PT_PRE, 0)] = H_D;
     pts[ec_pt_index(PT_PRE, 1)] = H_Q;
     for (int i = 2; i < 16; i++) {
       Jac R;
-      if (i % 2 == 0) { R = jac_dbl(pre_jac(i / 2)); jac_store(J + ECJ_OP * ec_op_pre(i), R, pre(i / 2), 0); }
-      else { R = jac_add_aff(pre_jac(i - 1), qx, qy); jac_store(J + ECJ_OP * ec_op_pre(i), R, H_Q, pre(i - 1)); }
-      pts[ec_pt_index(PT_PRE, i)] = ec_op_pre(i);
+      if (i % 2 == 0) { R = jac_dbl(pre_jac(i / 2)); jac_store(J + ECG.j_op * ec_op_pre(ECG, i), R, pre(i / 2), 0); }
+      else { R = jac_add_aff(pre_jac(i - 1), qx, qy); jac_store(J + ECG.j_op * ec_op_pre(ECG, i), R, H_Q, pre(i - 1)); }
+      pts[ec_pt_index(PT_PRE, i)] = ec_op_pre(ECG, i);
     }
-    auto nib = [&](int w4) { int b = 252 - 4 * w4; return (int)((u2[b >> 6] >> (b & 63)) & 15); };
+    auto nib = [&](int w4) { return sc_nib(u2, ECG.fb - 4 - 4 * w4); };
     pts[ec_pt_index(PT_SM_RP, 0)] = H_D;
     int rp = pre(nib(0));
     Jac rpv = pre_jac(nib(0));
     pts[ec_pt_index(PT_SM_AP, 0)] = rp;
     pts[ec_pt_index(PT_SM_RP, 1)] = rp;
-    for (int w4 = 1; w4 < 64; w4++) {
+    for (int w4 = 1; w4 < ECG.wins; w4++) {
       const int n = nib(w4), ap = pre(n);
       pts[ec_pt_index(PT_SM_AP, w4)] = ap;
       const bool izr = rp == H_D, iza = ap == H_D;
       Jac d = izr ? D : rpv;
       int hin = izr ? H_D : rp;
       for (int j = 0; j < 4; j++) {
-        const int op = ec_op_sm_dbl(4 * w4 - 4 + j);
+        const int op = ec_op_sm_dbl(ECG, 4 * w4 - 4 + j);
         d = jac_dbl(d);
-        jac_store(J + ECJ_OP * op, d, hin, 0);
+        jac_store(J + ECG.j_op * op, d, hin, 0);
         hin = op;
       }
-      const int dl = ec_op_sm_dbl(4 * w4 - 1), ad = ec_op_sm_add(w4 - 1);
+      const int dl = ec_op_sm_dbl(ECG, 4 * w4 - 1), ad = ec_op_sm_add(ECG, w4 - 1);
       Jac R = n == 1 ? jac_add_aff(d, qx, qy) : jac_add(d, pre_jac(n));
-      jac_store(J + ECJ_OP * ad, R, dl, ap);
+      jac_store(J + ECG.j_op * ad, R, dl, ap);
       if (izr) { rp = ap; rpv = pre_jac(n); }
       else if (iza) { rp = dl; rpv = d; }
       else { rp = ad; rpv = R; }
@@ -702,56 +759,56 @@ __global__ void __launch_bounds__(64) k_ec_chain(DevLayout L, const uint8_t* inp
   }
 }
 
-// Phase 1b, lane = witness: verifyECDSABits.add (op 361) of the two chains' results
+// Phase 1b, lane = witness: verifyECDSABits.add (the last op) of the two chains' results
 __global__ void __launch_bounds__(64) k_ec_final(uint64_t* ec_jac, uint32_t batch) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
-  uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
-  const int32_t* pts = reinterpret_cast<const int32_t*>(J + ECJ_PTS);
-  const int h1 = pts[ec_pt_index(PT_GM_RP, 30)], h2 = pts[ec_pt_index(PT_SM_RP, 64)];
+  uint64_t* J = ec_jac + (size_t)w * ECG.jac_words;
+  const int32_t* pts = reinterpret_cast<const int32_t*>(J + ECG.j_pts);
+  const int h1 = pts[ec_pt_index(PT_GM_RP, ECG.parts - 2)], h2 = pts[ec_pt_index(PT_SM_RP, ECG.wins)];
   // both are op outputs (a forwarded dummy would need an all-zero scalar, which fails BigModInv /
   // the final check anyway): fall back to zero points otherwise
-  Jac P = h1 >= 0 ? jac_load(J + ECJ_OP * h1) : Jac{}, Q = h2 >= 0 ? jac_load(J + ECJ_OP * h2) : Jac{};
-  jac_store(J + ECJ_OP * EC_OP_FINAL, jac_add(P, Q), h1, h2);
+  Jac P = h1 >= 0 ? jac_load(J + ECG.j_op * h1) : Jac{}, Q = h2 >= 0 ? jac_load(J + ECG.j_op * h2) : Jac{};
+  jac_store(J + ECG.j_op * ECG.op_final, jac_add(P, Q), h1, h2);
 }
 
 // Phase 2, lane = (witness, group of 8 ops): affine out = (X / Z^2, Y / Z^3), one inversion per group
-constexpr int EC_AFF_GROUP = 8, EC_AFF_GROUPS = (EC_N_OPS + EC_AFF_GROUP - 1) / EC_AFF_GROUP;
+constexpr int EC_AFF_GROUP = 8, EC_AFF_GROUPS = (ECG.n_ops + EC_AFF_GROUP - 1) / EC_AFF_GROUP;
 __global__ void __launch_bounds__(64) k_ec_affine(uint64_t* ec_core, const uint64_t* ec_jac, int32_t* status, uint32_t batch) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t w = gid / EC_AFF_GROUPS, g = gid % EC_AFF_GROUPS;
   if (w >= batch) return;
   using M = ModP;
-  const uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
-  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
-  const int op0 = g * EC_AFF_GROUP, n = min(EC_AFF_GROUP, EC_N_OPS - op0);
-  e8 pre[EC_AFF_GROUP];
-  e8 acc = m_const<M>(M::r1);
+  const uint64_t* J = ec_jac + (size_t)w * ECG.jac_words;
+  uint64_t* C = ec_core + (size_t)w * ECG.core_words;
+  const int op0 = g * EC_AFF_GROUP, n = min(EC_AFF_GROUP, ECG.n_ops - op0);
+  eW pre[EC_AFF_GROUP];
+  eW acc = m_const<M>(M::r1);
   bool degenerate = false;
   for (int k = 0; k < n; k++) {
     pre[k] = acc;
-    e8 z = e8_from_u64(J + ECJ_OP * (op0 + k) + 8);
+    eW z = ew_from_words(J + ECG.j_op * (op0 + k) + 2 * JW);
     if (m_is_zero<M>(z)) degenerate = true;
     else acc = m_mul<M>(acc, z);
   }
   if (degenerate && status) lane_status(status + w, ST_BIGISZERO);  // dx = 0 or y = 0: the affine formulas divide by 0
-  e8 inv = m_inv<M>(acc);
+  eW inv = m_inv<M>(acc);
   for (int k = n - 1; k >= 0; k--) {
-    const uint64_t* d = J + ECJ_OP * (op0 + k);
-    uint64_t* o = C + ECC_REC + ECC_REC_WORDS * (op0 + k) + 16;
-    e8 z = e8_from_u64(d + 8);
-    if (m_is_zero<M>(z)) { for (int i = 0; i < 8; i++) o[i] = 0; continue; }
-    e8 zi = m_mul<M>(inv, pre[k]);
+    const uint64_t* d = J + ECG.j_op * (op0 + k);
+    uint64_t* o = C + ECG.c_rec + ECG.rec_words * (op0 + k) + 2 * P2;
+    eW z = ew_from_words(d + 2 * JW);
+    if (m_is_zero<M>(z)) { for (int i = 0; i < P2; i++) o[i] = 0; continue; }
+    eW zi = m_mul<M>(inv, pre[k]);
     inv = m_mul<M>(inv, z);
-    e8 zi2 = m_mul<M>(zi, zi), zi3 = m_mul<M>(zi2, zi);
-    e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d), zi2)), o);
-    e8_to_u64(m_from<M>(m_mul<M>(e8_from_u64(d + 4), zi3)), o + 4);
+    eW zi2 = m_mul<M>(zi, zi), zi3 = m_mul<M>(zi2, zi);
+    ew_to_chunks(m_from<M>(m_mul<M>(ew_from_words(d), zi2)), o);
+    ew_to_chunks(m_from<M>(m_mul<M>(ew_from_words(d + JW), zi3)), o + NL);
   }
 }
 
-// Phase 3, lane = (witness, item): op records' inputs (items < 362), forwarded points (next 208),
+// Phase 3, lane = (witness, item): op records' inputs (items < n_ops), forwarded points (next n_pts),
 // and the final x1 mod n === r check + modOrder record (last item)
-constexpr int EC_LINK_ITEMS = EC_N_OPS + EC_N_PTS + 1;
+constexpr int EC_LINK_ITEMS = ECG.n_ops + ECG.n_pts + 1;
 __global__ void __launch_bounds__(64) k_ec_link(DevLayout L, const uint8_t* inputs, uint64_t* ec_core, const uint64_t* ec_jac,
                                                 int32_t* status, uint32_t batch) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -759,31 +816,31 @@ __global__ void __launch_bounds__(64) k_ec_link(DevLayout L, const uint8_t* inpu
   const int it = (int)(gid % EC_LINK_ITEMS);
   if (w >= batch) return;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
-  const uint64_t* J = ec_jac + (size_t)w * EC_JAC_WORDS;
-  uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  const uint64_t* J = ec_jac + (size_t)w * ECG.jac_words;
+  uint64_t* C = ec_core + (size_t)w * ECG.core_words;
   auto aff = [&](int hd, uint64_t* xy) {
-    if (hd >= 0) { const uint64_t* o = C + ECC_REC + ECC_REC_WORDS * hd + 16; for (int i = 0; i < 8; i++) xy[i] = o[i]; }
+    if (hd >= 0) { const uint64_t* o = C + ECG.c_rec + ECG.rec_words * hd + 2 * P2; for (int i = 0; i < P2; i++) xy[i] = o[i]; }
     else ec_aff_const(L, row, hd, xy);
   };
-  if (it < EC_N_OPS) {
-    const uint64_t hh = J[ECJ_OP * it + 12];
-    uint64_t* rc = C + ECC_REC + ECC_REC_WORDS * it;
+  if (it < ECG.n_ops) {
+    const uint64_t hh = J[ECG.j_op * it + 3 * JW];
+    uint64_t* rc = C + ECG.c_rec + ECG.rec_words * it;
     aff((int32_t)(uint32_t)hh, rc);
-    if (ec_op_is_dbl(it)) { for (int i = 0; i < 8; i++) rc[8 + i] = 0; }
-    else aff((int32_t)(uint32_t)(hh >> 32), rc + 8);
-  } else if (it < EC_N_OPS + EC_N_PTS) {
-    const int idx = it - EC_N_OPS;
-    aff(reinterpret_cast<const int32_t*>(J + ECJ_PTS)[idx], C + ec_pt_base(idx));
+    if (ec_op_is_dbl(ECG, it)) { for (int i = 0; i < P2; i++) rc[P2 + i] = 0; }
+    else aff((int32_t)(uint32_t)(hh >> 32), rc + P2);
+  } else if (it < ECG.n_ops + ECG.n_pts) {
+    const int idx = it - ECG.n_ops;
+    aff(reinterpret_cast<const int32_t*>(J + ECG.j_pts)[idx], C + ec_pt_base(idx));
   } else {  // x1 mod n === r (ecdsa.circom:81-83); modOrder record
-    const uint64_t* x1 = C + ECC_REC + ECC_REC_WORDS * EC_OP_FINAL + 16;
-    e8 xm = m_reduce<ModN>(e8_from_u64(x1).v, 0);
-    uint64_t xr[4];
-    e8_to_u64(xm, xr);
+    const uint64_t* x1 = C + ECG.c_rec + ECG.rec_words * ECG.op_final + 2 * P2;
+    eW xm = m_reduce<ModN>(ew_from_chunks(x1).v, 0);
+    uint64_t xr[NL];
+    ew_to_chunks(xm, xr);
     bool ok = true;
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < NL; i++) {
       ok &= xr[i] == *reinterpret_cast<const uint64_t*>(row + 32ull * (L.reg.in_sig + i));
-      C[ECC_MM + 8 * EC_MM_XN + i] = x1[i];
-      C[ECC_MM + 8 * EC_MM_XN + 4 + i] = i == 0 ? 1 : 0;
+      C[ECG.c_mm + P2 * EC_MM_XN + i] = x1[i];
+      C[ECG.c_mm + P2 * EC_MM_XN + NL + i] = i == 0 ? 1 : 0;
     }
     if (!ok && status) lane_status(status + w, ST_ECDSA_R);
   }
@@ -793,23 +850,23 @@ __global__ void __launch_bounds__(64) k_ec_link(DevLayout L, const uint8_t* inpu
 // isZeroAddition) of the differences in[1] - in[0]; 0 -> 0 (comparators.circom:17)
 __global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_inv, uint32_t batch) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t w = gid / EC_N_INV;
-  const int j = (int)(gid % EC_N_INV);
+  const uint32_t w = gid / ECG.n_inv;
+  const int j = (int)(gid % ECG.n_inv);
   if (w >= batch) return;
-  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
+  const uint64_t* C = ec_core + (size_t)w * ECG.core_words;
   const uint64_t dx = EC_D[0];
   fr d;
-  if (j < ECI_SM_ZR) {
+  if (j < ECG.i_sm_zr) {
     const int i = j >> 2, k = j & 3;
-    const uint64_t lx = i == 0 ? C[ECC_GM_AP] : C[ECC_GM_RP + 8 * (i - 1)], rx = C[ECC_GM_AP + 8 * (i + 1)];
-    const uint64_t sdx = C[ECC_REC + ECC_REC_WORDS * EC_OP_SD + 16];
+    const uint64_t lx = i == 0 ? C[ECG.c_gm_ap] : C[ECG.c_gm_rp + P2 * (i - 1)], rx = C[ECG.c_gm_ap + P2 * (i + 1)];
+    const uint64_t sdx = C[ECG.c_rec + ECG.rec_words * EC_OP_SD + 2 * P2];
     d = fr_diff_u64(k < 2 ? lx : rx, (k & 1) ? sdx : dx);
-  } else if (j < ECI_SM_ZA) {
-    d = fr_diff_u64(dx, C[ECC_SM_RP + 8 * (j - ECI_SM_ZR)]);
+  } else if (j < ECG.i_sm_za) {
+    d = fr_diff_u64(dx, C[ECG.c_sm_rp + P2 * (j - ECG.i_sm_zr)]);
   } else {
-    d = fr_diff_u64(dx, C[ECC_SM_AP + 8 * (j - ECI_SM_ZA + 1)]);
+    d = fr_diff_u64(dx, C[ECG.c_sm_ap + P2 * (j - ECG.i_sm_za + 1)]);
   }
-  ec_inv[(size_t)w * EC_N_INV + j] = fr_is_zero(d) ? d : fr_from_mont_fast(fr_inv<true>(fr_mul_fast(d, fr_const(R2_))));
+  ec_inv[(size_t)w * ECG.n_inv + j] = fr_is_zero(d) ? d : fr_from_mont_fast(fr_inv<true>(fr_mul_fast(d, fr_const(R2_))));
 }
 
 // ============================================================ k_ec_table: lane per (witness, op)
@@ -819,11 +876,11 @@ __global__ void __launch_bounds__(64) k_ec_table(DevLayout L, const int32_t* ops
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= batch) return;
   const int t = ops[blockIdx.y];
-  const uint64_t* C = ec_core + (size_t)w * EC_CORE_WORDS;
-  const uint64_t* rec = t < EC_N_OPS ? C + ECC_REC + ECC_REC_WORDS * t : C + ECC_MM + 8 * (t - EC_N_OPS);
+  const uint64_t* C = ec_core + (size_t)w * ECG.core_words;
+  const uint64_t* rec = t < ECG.n_ops ? C + ECG.c_rec + ECG.rec_words * t : C + ECG.c_mm + P2 * (t - ECG.n_ops);
   uint4* tab = reinterpret_cast<uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
   EcTabCtx c{tab, 0, rec, 0};
-  EcWalk<EcTabCtx> walk(c);
+  EcWalk<EcTabCtx, EC_CV> walk(c);
   walk.run(TYPE);
   if (c.err && status) lane_status(status + w, c.err);
 }
@@ -852,7 +909,7 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
 template <int MM>  // store mode (mapsink.hpp)
 __global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
                                                   size_t stride) {
-  __shared__ uint4 tab[2 * EC_TABLE_MAX];
+  __shared__ uint4 tab[2 * EC_TABLE_MAX[EC_CV]];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];

@@ -1,7 +1,8 @@
 // ECDSA kernels (ec_core.hpp) and their launchers; a separate translation unit from kernels.hip so the
 // two compile in parallel. Compiled once per curve: this file for PZK_EC_CURVE 0 (secp256r1), and
-// kernels_ec_bp.hip includes it with PZK_EC_CURVE 1 (brainpoolP256r1). The curve-0 unit also defines
-// the public launchers, which dispatch on the instance's curve.
+// kernels_ec_bp.hip / kernels_ec_p224.hip / kernels_ec_bp384.hip include it with PZK_EC_CURVE 1 / 2 / 3
+// (brainpoolP256r1 / secp224r1 / brainpoolP384r1). The curve-0 unit also defines the public launchers,
+// which dispatch on the instance's curve.
 #include <hip/hip_runtime.h>
 
 #include "bufs.hpp"
@@ -27,7 +28,7 @@ hipError_t launch_ec_core_cv(const DevLayout& L, const uint8_t* inputs, const ui
   hipLaunchKernelGGL(k_ec_link, dim3((batch * EC_LINK_ITEMS + 63) / 64), dim3(64), 0, st, L, inputs, ec_core, ec_jac,
                      status, batch);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_ec_inv, dim3((batch * EC_N_INV + 63) / 64), dim3(64), 0, st, ec_core, ec_inv, batch);
+  hipLaunchKernelGGL(k_ec_inv, dim3((batch * ECG.n_inv + 63) / 64), dim3(64), 0, st, ec_core, ec_inv, batch);
   return hipGetLastError();
 }
 
@@ -54,29 +55,40 @@ hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_w
 }  // namespace PZK_EC_NS
 
 #if PZK_EC_CURVE == 0
-namespace ec_c1 {
-hipError_t launch_ec_core_cv(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
-                             uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st);
-hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
-                              uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st);
-hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
-                              hipStream_t st);
-}  // namespace ec_c1
+#define PZK_EC_DECL(ns)                                                                                                   \
+  namespace ns {                                                                                                        \
+  hipError_t launch_ec_core_cv(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,  \
+                               uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st);          \
+  hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops,                       \
+                                const uint64_t* ec_core, uint8_t* ec_tab, int32_t* status, uint32_t batch,              \
+                                hipStream_t st);                                                                        \
+  hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,   \
+                                hipStream_t st);                                                                        \
+  }
+PZK_EC_DECL(ec_c1)
+PZK_EC_DECL(ec_c2)
+PZK_EC_DECL(ec_c3)
+#undef PZK_EC_DECL
 
+#define PZK_EC_DISPATCH(call)                         \
+  switch (L.reg.ec_curve) {                           \
+    case 1: return ec_c1::call;                       \
+    case 2: return ec_c2::call;                       \
+    case 3: return ec_c3::call;                       \
+    default: return ec_c0::call;                      \
+  }
 hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
                           uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st) {
-  return L.reg.ec_curve ? ec_c1::launch_ec_core_cv(L, inputs, sha_core, ec_core, ec_jac, ec_inv, status, batch, st)
-                        : ec_c0::launch_ec_core_cv(L, inputs, sha_core, ec_core, ec_jac, ec_inv, status, batch, st);
+  PZK_EC_DISPATCH(launch_ec_core_cv(L, inputs, sha_core, ec_core, ec_jac, ec_inv, status, batch, st))
 }
 hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
                            uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st) {
-  return L.reg.ec_curve ? ec_c1::launch_ec_table_cv(L, type, ops, n_ops, ec_core, ec_tab, status, batch, st)
-                        : ec_c0::launch_ec_table_cv(L, type, ops, n_ops, ec_core, ec_tab, status, batch, st);
+  PZK_EC_DISPATCH(launch_ec_table_cv(L, type, ops, n_ops, ec_core, ec_tab, status, batch, st))
 }
 hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st) {
-  return L.reg.ec_curve ? ec_c1::launch_emit_ect_cv(L, work, n_work, B, batch, st)
-                        : ec_c0::launch_emit_ect_cv(L, work, n_work, B, batch, st);
+  PZK_EC_DISPATCH(launch_emit_ect_cv(L, work, n_work, B, batch, st))
 }
+#undef PZK_EC_DISPATCH
 #endif
 }  // namespace pzk

@@ -33,7 +33,7 @@ enum RegionKind : uint32_t {
   RK_DIGEST = 9,     // 256 digest bits (MSB first) of SHA job a0
   RK_TEMPMOD = 10,   // tempModulus[5] = pk[3i]*2^128 + pk[3i+1]*2^64; a0 = pubkey input offset
   RK_FLOW = 11,      // PassportVerificationFlow (passportVerificationFlow.circom:6-109), whole block
-  RK_HCHUNK = 12,    // RsaVerifyPkcs1v15.hashed_chunks[4]; a0 = SHA job
+  RK_HCHUNK = 12,    // hashed_chunks[N] (RsaVerifyPkcs1v15 4 x 64, verifyECDSABits N x CS); a0 = SHA job, a1 = N, a2 = CS
   RK_RSA_OUT = 13,   // PowerMod.out[K] = EM limbs (RSA core)
   RK_SMT_OWN = 14,   // SMTVerifier own signals
   RK_SMTHASH = 15,   // SMTHash1/2 own (out, key/L, value/R); a0 = level (-1 = hash1New)
@@ -45,23 +45,23 @@ enum RegionKind : uint32_t {
   RK_BJJ_OWN = 21,   // BabyjubjubBase8Multiplication own (out[2], scalar) + GetBabyjubjubBase8
   RK_BJJ_STEPS = 22, // adders[0], (adders[i], doublers[i-1]) i = 1..253
   RK_SIG_OWN = 23,   // VerifySignature / RsaVerifyPkcs1v15 / PowerMod input copies (a0 = sub-kind)
-  // ---- ECDSA secp256r1 (ec_common.hpp, ec_emit.hpp)
+  // ---- ECDSA (ec_common.hpp, ec_emit.hpp); chunked values have CHUNK_SIZE bits, points 2 x CHUNK_NUMBER chunks
   RK_ECT = 24,        // table block: a0 = table op (EC op, or EC_N_OPS + BigMultModP index), a1 = EcType
   RK_EC_U64 = 25,     // w[off+i] = EC core word a0 + i
   RK_EC_CONST = 26,   // curve constant a0 (ec_k ids)
-  RK_EC_GM_RCC = 27,  // generator mult resultCoordinateComputation[32][256][2][4]
-  RK_EC_GM_EQ = 28,   // generator mult equal[32][256] (IsEqual)
-  RK_EC_GM_SUM = 29,  // generator mult getSumOfNElements[32][2][4] (GetSum(256))
+  RK_EC_GM_RCC = 27,  // generator mult resultCoordinateComputation[PARTS][256][2][N]
+  RK_EC_GM_EQ = 28,   // generator mult equal[PARTS][256] (IsEqual)
+  RK_EC_GM_SUM = 29,  // generator mult getSumOfNElements[PARTS][2][N] (GetSum(256))
   RK_EC_GM_STEP = 30, // generator mult step a0: 4 IsEqual dummy tests + 16 switchers
-  RK_EC_N2B = 31,     // Num2Bits(64): a0 = 0 EC core word a1 / 1 input element a1
-  RK_EC_B2N8 = 32,    // generator mult bits2num[32] (Bits2Num(8)) of the scalar at core word a0
-  RK_EC_SBITS = 33,   // scalarMult scalarBits[256] of the scalar at core word a0
+  RK_EC_N2B = 31,     // Num2Bits(a2 = CS): a0 = 0 EC core word a1 / 1 input element a1
+  RK_EC_B2N8 = 32,    // generator mult bits2num[PARTS] (Bits2Num(8)) of the scalar at core word a0
+  RK_EC_SBITS = 33,   // scalarMult scalarBits[N CS] of the scalar at core word a0
   RK_EC_SM_W0 = 34,   // scalarMult window a0: bits2Num(4) + isZeroResult
-  RK_EC_SM_DSW = 35,  // scalarMult window a0: doubleSwitcher[8]
-  RK_EC_SM_SEL = 36,  // scalarMult window a0: getSum[8] (GetSum(16)) + partsEqual[16]
-  RK_EC_SM_RSW = 37,  // scalarMult window a0: isZeroAddition + (resultSwitcherAddition, resultSwitcherDoubling)[8]
-  RK_EC_PKBITS = 38,  // PassportVerificationBuilder ecBitsX[256], ecBitsY[256] of pubkey input a0
-  RK_EC_B2N248 = 39,  // Bits2Num(248) of the 4-limb input at a0 (xToNum / yToNum)
+  RK_EC_SM_DSW = 35,  // scalarMult window a0: doubleSwitcher[2N]
+  RK_EC_SM_SEL = 36,  // scalarMult window a0: getSum[2N] (GetSum(16)) + partsEqual[16]
+  RK_EC_SM_RSW = 37,  // scalarMult window a0: isZeroAddition + (resultSwitcherAddition, resultSwitcherDoubling)[2N]
+  RK_EC_PKBITS = 38,  // PassportVerificationBuilder ecBitsX[F], ecBitsY[F] of pubkey input a0 (a1 = N, a2 = CS)
+  RK_EC_B2N248 = 39,  // Bits2Num(a3 = min(F, 248)) of the N-chunk input at a0 (xToNum / yToNum; a1 = N, a2 = CS)
   // ---- RSA-PSS (SIGNATURE_TYPE 10-12, rsaPss.circom:18-204; pss.hpp)
   RK_PSS_OWN = 40,    // VerifyRsaPssSig eM .. mDash (after its pubkey/signature/hashed inputs); a0 = salt bits
   RK_PSS_B2N8 = 41,   // bits2Num[8K] (Bits2Num(8)) of the EM bytes
@@ -176,8 +176,9 @@ struct RegInfo {
   int8_t mm_x[32], mm_y[32];
   uint32_t modmul_size;
   int32_t ecdsa;                   // SIGNATURE_TYPE >= 20 (ECDSA)
-  int32_t ec_curve;                // 0: secp256r1 (20), 1: brainpoolP256r1 (21) (ec_common.hpp)
-  int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^248)
+  int32_t ec_curve;                // 0..3: SIG 20, 21, 24, 25 (ec_common.hpp)
+  int32_t ec_nl, ec_cs;            // its CHUNK_NUMBER, CHUNK_SIZE
+  int32_t v_pkx, v_pky;            // ECDSA pubkey hash inputs (x, y mod 2^min(N CS, 248))
   int32_t aa_ec, aa_f, aa_hs;      // EC active-authentication key: field bits, hashed bits (identity.circom:51-84)
   int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)
   int32_t pss_h;                   // RSA-PSS hash bits (256 or 384)
@@ -255,7 +256,7 @@ struct DevLayout {
   uint32_t rsa_core_words;          // u64 per witness
   uint32_t bjj_core_fr, smt_core_fr;
   // ECDSA (ec_common.hpp)
-  const uint64_t* ec_gpow;          // P-256 fixed-base table [32][256][2][4]
+  const uint64_t* ec_gpow;          // fixed-base table [PARTS][256][2][N] chunks (ec_common.hpp)
   const uint32_t* ec_prog;          // table-block descriptor programs, at ec_prog_off[type]
   uint32_t ec_prog_off[3], ec_tab_n[3];
   const uint32_t* ec_tab_off;       // entry offset of table op t inside a witness's tables

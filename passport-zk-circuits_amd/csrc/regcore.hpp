@@ -56,16 +56,20 @@ __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs,
   // pubkeyHasherRsa inputs: tempModulus[i] + pk[3i+2] = pk[3i]*2^128 + pk[3i+1]*2^64 + pk[3i+2]
   // (passportVerificationBuilder.circom:182-191), in field arithmetic; lane i computes input i
   if (R.ecdsa) {
-    // ECDSA: pubkeyHasher = Poseidon2(x mod 2^248, y mod 2^248) (passportVerificationBuilder.circom:193-230)
+    // ECDSA: pubkeyHasher = Poseidon2(x mod 2^FD, y mod 2^FD), FD = min(N CS, 248) (passportVerificationBuilder.circom:193-230)
     if (lane < 2) {
-      const int a = lane;
+      const int a = lane, N = R.ec_nl, CS = R.ec_cs, FD = N * CS > 248 ? 248 : N * CS;
       fr v = fr_zero();
-      for (int j = 0; j < 4; j++) {
-        const uint8_t* e = row + 32ull * (R.in_pk + 4 * a + j);
-        bad |= !in_is_u64(e);
-        uint64_t x = in_u64(e);
-        if (j == 3) x &= (1ull << 56) - 1;
-        v.v[2 * j] = (uint32_t)x; v.v[2 * j + 1] = (uint32_t)(x >> 32);
+      for (int j = 0; j < N; j++) {
+        const uint8_t* e = row + 32ull * (R.in_pk + N * a + j);
+        bad |= !in_is_u64(e) || (CS < 64 && (in_u64(e) >> CS) != 0);
+        const uint64_t x = in_u64(e);
+        for (int k = 0; k < CS && CS * j + k < FD; k += 32) {  // 32-bit pieces of the chunk below bit FD
+          const int bit = CS * j + k;
+          uint32_t piece = (uint32_t)(x >> k);
+          if (bit + 32 > FD) piece &= (1u << (FD - bit)) - 1u;
+          v.v[bit >> 5] = piece;
+        }
       }
       vs.at(a ? R.v_pky : R.v_pkx, w) = fr_to_mont(v);
     }
@@ -101,8 +105,9 @@ __global__ void __launch_bounds__(64) k_prep(DevLayout L, const uint8_t* inputs,
   if (lane == 0) {
     const ShaJob job = L.sha[R.j_sa];
     const uint32_t* H = sha_core + (size_t)w * L.sha_core_words + job.hout;
-    // the hash's first 252 bits, or a 160-bit SHA-1 hash shifted up by 92 (passportVerificationBuilder.circom:164-177)
-    const int sh = job.algo == 1 ? 92 : 0;
+    // the hash's first 252 bits, or an HT < 252-bit hash shifted up by 252 - HT: 92 for SHA-1, 28 for SHA-224
+    // (passportVerificationBuilder.circom:164-177)
+    const int sh = job.algo == 1 ? 92 : job.algo == 2 ? 28 : 0;
     fr sn = bits_to_fr(252, [&](int k) { return k < sh ? 0u : (H[(k - sh) >> 5] >> (31 - ((k - sh) & 31))) & 1u; });
     vs.at(R.v_sanum, w) = fr_to_mont(sn);
   }

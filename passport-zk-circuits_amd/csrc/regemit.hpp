@@ -95,10 +95,10 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
         return el_fr(fr_from_mont_fast(v));
       }
     }
-    case RK_HCHUNK: {
+    case RK_HCHUNK: {  // chunk s = digest bits [cs (n-1-s), cs (n-s)) as a number (rsa.circom:84-91, ecdsa.circom:30-38)
       const uint32_t* H = sha_hout(L, B, w, R.a[0]);
-      int wd = 3 - (int)s;
-      return el_u64(((uint64_t)H[2 * wd] << 32) | H[2 * wd + 1]);
+      const int n = R.a[1], cs = R.a[2], i = n - 1 - (int)s;
+      return el_u64(cs == 64 ? ((uint64_t)H[2 * i] << 32) | H[2 * i + 1] : H[i]);
     }
     case RK_RSA_OUT: {
       const uint64_t* mc = B.rsa_core + (size_t)w * L.rsa_core_words + (size_t)(G.n_modmul - 1) * MM_CORE_WORDS(G.K);

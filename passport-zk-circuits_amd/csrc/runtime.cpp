@@ -403,8 +403,10 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
       rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
   }
   if (!rc && I->lay.is_ecdsa) {
-    std::string path = data_dir() + (I->lay.reg.ec_curve ? "/bp256_gpow8.bin" : "/p256_gpow8.bin");
-    std::vector<uint64_t> tab(32 * 256 * 8);
+    static const char* const names[EC_N_CURVES] = {"/p256_gpow8.bin", "/bp256_gpow8.bin", "/p224_gpow8.bin", "/bp384_gpow8.bin"};
+    const EcGeo& G = EC_GEO[I->lay.reg.ec_curve];
+    std::string path = data_dir() + names[I->lay.reg.ec_curve];
+    std::vector<uint64_t> tab((size_t)G.parts * 256 * 2 * G.nl);  // [PARTS][256][2][N] chunks
     FILE* fp = fopen(path.c_str(), "rb");
     size_t got = fp ? fread(tab.data(), 8, tab.size(), fp) : 0;
     if (fp) fclose(fp);
@@ -625,9 +627,9 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
       {(void**)&S.d_bjj_core, 32ull * L.bjj_core_fr * batch},
       {(void**)&S.d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&S.d_smt_core, 32ull * L.smt_core_fr * batch},
-      {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_CORE_WORDS * batch : 0},
-      {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_JAC_WORDS * batch : 0},
-      {(void**)&S.d_ec_inv, L.is_ecdsa ? 32ull * EC_N_INV * batch : 0},
+      {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].core_words * batch : 0},
+      {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].jac_words * batch : 0},
+      {(void**)&S.d_ec_inv, L.is_ecdsa ? 32ull * EC_GEO[L.reg.ec_curve].n_inv * batch : 0},
       {(void**)&S.d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
       {(void**)&S.d_derived, 32ull * L.n_derived * batch},
   };

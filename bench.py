@@ -64,7 +64,7 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
 WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
-SIG_SEED = {1: 3, 2: 4, 3: 11, 4: 12, 10: 6, 11: 7, 12: 8, 13: 13, 14: 10, 20: 5, 21: 9}
+SIG_SEED = {1: 3, 2: 4, 3: 11, 4: 12, 10: 6, 11: 7, 12: 8, 13: 13, 14: 10, 20: 5, 21: 9, 24: 14, 25: 15}
 CPU_SHARE = 16  # host CPUs a one-GPU job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
 
 
@@ -244,7 +244,8 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
         sub = min(args.sub, batch)
     elif device == "cuda":
         free, _ = torch.cuda.mem_get_info(dev)
-        scratch_pw = 10 << 20 if args.sig_eff >= 20 else 1 << 20  # per-witness core scratch, two sets
+        # per-witness core scratch (EC value tables dominate: 11 / 15 / 20 MB for P-256 / P-224 / brainpoolP384r1), two sets
+        scratch_pw = {24: 16 << 20, 25: 22 << 20}.get(args.sig_eff, 10 << 20 if args.sig_eff >= 20 else 1 << 20)
         staging = getattr(engine, "o0_staging_bytes", 0)  # mapped layouts: the library's O0 chunk slots
         fit = max(1, int((free * 0.85 - staging) // (slots * stride + 2 * scratch_pw)))
         parts_n = 1
@@ -406,7 +407,7 @@ def report(args, r, world):
     }
     if world == 1 and not args.no_host and args.workload.startswith("register"):
         out["host_delivered"] = host_delivered(args, r["engine"].inst, sig)
-    if world == 1 and not args.no_cpu and args.workload.startswith("register") and sig in (1, 3, 10, 11, 12, 20, 21):
+    if world == 1 and not args.no_cpu and args.workload.startswith("register") and sig in (1, 3, 10, 11, 12, 20, 21, 24, 25):
         out["input_side"] = input_side(sig)
     if world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
         procs = max(1, min(CPU_SHARE, os.cpu_count() or 1))
@@ -474,7 +475,8 @@ def input_side(sig, distinct=128, n=8192):
     from pzkwit import passport as PP, sodgen
     t0 = time.perf_counter()
     key = sodgen.signer_key(sig)
-    uniq = [sodgen.make_passport(sig, key, i) for i in range(distinct)]
+    # SHA-384 signed attributes fit the circuit's one 1024-bit block only without signingTime (sodgen.make_passport)
+    uniq = [sodgen.make_passport(sig, key, i, signing_time=sig not in (13, 25)) for i in range(distinct)]
     gen_s = time.perf_counter() - t0
     params = PP.parse(uniq[0])["params"]
     src = PP.sources([uniq[i % distinct] for i in range(n)])

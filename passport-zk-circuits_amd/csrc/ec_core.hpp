@@ -906,8 +906,11 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
   return make_uint4(mw(q.x, 0), mw(q.y, 1), mw(q.z, 2), mw(q.w, 3));
 }
 
+// workgroup size: a big table (P-224 51 KB, brainpoolP384r1 39 KB of LDS) caps the workgroups per CU at 3-4, so
+// those curves run 8 waves per workgroup to keep ~24-32 waves per CU in flight
+constexpr int ECT_NT = EC_TABLE_MAX[EC_CV] > 1024 ? 512 : 256;
 template <int MM>  // store mode (mapsink.hpp)
-__global__ void __launch_bounds__(256) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
+__global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
                                                   size_t stride) {
   __shared__ uint4 tab[2 * EC_TABLE_MAX[EC_CV]];
   const Work wk = work[blockIdx.x];

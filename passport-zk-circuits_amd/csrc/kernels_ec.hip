@@ -47,7 +47,7 @@ hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, 
 hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st) {
   if (n_work == 0) return hipSuccess;
-  hipLaunchKernelGGL((L.keep.bits ? k_emit_ect<MAP_DIRECT> : k_emit_ect<MAP_O0>), dim3(n_work, batch), dim3(256), 0, st, L, work,
+  hipLaunchKernelGGL((L.keep.bits ? k_emit_ect<MAP_DIRECT> : k_emit_ect<MAP_O0>), dim3(n_work, batch), dim3(ECT_NT), 0, st, L, work,
                      B.ec_tab, B.wtns, B.stride);
   return hipGetLastError();
 }

@@ -944,8 +944,10 @@ extern "C" int pzk_passport_inputs(const pzk_params* params, const pzk_passport_
   uint32_t nreg = 0;
   if (int rc = pzk_layout_query(params, &li, &nreg)) return rc;
   const int sig = params->signature_type;
-  const int K = sig >= 20 ? 4 : sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : 32;  // limbs per coordinate
-  const int hb = (sig == 13) ? 1024 : 512;  // HASH_BLOCK_SIZE (registerIdentityBuilder.circom:104-111)
+  // limbs per coordinate: CHUNK_NUMBER of the circuit (registerIdentityBuilder.circom:59-99; 7 x 32 bits for SIG 24,
+  // where processPassport's getChunkedParams (:590-626) makes 4 x 64: such rows get PZK_PP_LIMBS)
+  const int K = sig == 24 ? 7 : sig == 25 ? 6 : sig >= 20 ? 4 : sig == 2 ? 64 : (sig == 4 || sig == 14) ? 48 : 32;
+  const int hb = (sig == 13 || sig == 25) ? 1024 : 512;  // HASH_BLOCK_SIZE (registerIdentityBuilder.circom:104-111)
   const size_t ecL = (size_t)params->ec_block_number * hb, d15L = (size_t)params->dg15_block_number * hb;
   const size_t n_in = 1 + ecL + 1024 + d15L + 1024 + 2 * (size_t)(sig >= 20 ? 2 * K : K) + 80 + 1;
   if (n_in != li.n_inputs) return pzk::api_fail(PZK_E_PARAMS, "pzk_passport_inputs: input layout mismatch");
@@ -960,7 +962,7 @@ extern "C" int pzk_passport_inputs(const pzk_params* params, const pzk_passport_
       want.size_arg = got.size_arg = 0;
       if (std::memcmp(&want, &got, sizeof want)) { status[i] = PZK_PP_PARAMS; return; }
       const int coords = sig >= 20 ? 2 : 1;
-      if (P.info.chunk_bits != 64 || P.info.chunk_number != K || (int)P.pk_limbs.size() != coords * K) {
+      if (P.info.chunk_bits != (sig == 24 ? 32 : 64) || P.info.chunk_number != K || (int)P.pk_limbs.size() != coords * K) {
         status[i] = PZK_PP_LIMBS;
         return;
       }

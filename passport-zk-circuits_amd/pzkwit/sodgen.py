@@ -18,7 +18,7 @@ same files to pin it. Layout of the DER (ICAO 9303-10 §4.6.2, RFC 5652):
 import hashlib
 
 from .field import SplitMix64
-from .inputs import (BP256, P256, Curve, EcKey, RsaKey, _dg15_rsa1024, _mrz_dg1, pkcs1v15_sha1_sign,
+from .inputs import (BP256, BP384, P224, P256, Curve, EcKey, RsaKey, _dg15_rsa1024, _mrz_dg1, pkcs1v15_sha1_sign,
                      pkcs1v15_sha256_sign, pss_sign)
 
 # secp521r1 (SEC 2 2.6.1): a named-curve key the reference recognises by name (getSigType :230, 66-bit chunks)
@@ -39,7 +39,8 @@ OID = {
     "rsaEncryption": "1.2.840.113549.1.1.1", "sha1WithRSAEncryption": "1.2.840.113549.1.1.5",
     "sha256WithRSAEncryption": "1.2.840.113549.1.1.11", "rsassaPss": "1.2.840.113549.1.1.10",
     "mgf1": "1.2.840.113549.1.1.8", "ecPublicKey": "1.2.840.10045.2.1", "primeField": "1.2.840.10045.1.1",
-    "ecdsaWithSHA256": "1.2.840.10045.4.3.2", "signedData": "1.2.840.113549.1.7.2",
+    "ecdsaWithSHA224": "1.2.840.10045.4.3.1", "ecdsaWithSHA256": "1.2.840.10045.4.3.2",
+    "ecdsaWithSHA384": "1.2.840.10045.4.3.3", "signedData": "1.2.840.113549.1.7.2",
     "ldsSecurityObject": "2.23.136.1.1.1", "contentType": "1.2.840.113549.1.9.3",
     "messageDigest": "1.2.840.113549.1.9.4", "signingTime": "1.2.840.113549.1.9.5",
     "countryName": "2.5.4.6", "commonName": "2.5.4.3",
@@ -176,7 +177,8 @@ SIG_KIND = {  # SIGNATURE_TYPE -> (key, sa / ec hash bits, scheme, salt)
     1: ("rsa2048", 256, "pkcs1", 0), 2: ("rsa4096", 256, "pkcs1", 0), 3: ("rsa2048", 160, "pkcs1", 0),
     10: ("rsa2048e3", 256, "pss", 32), 11: ("rsa2048", 256, "pss", 32), 12: ("rsa2048", 256, "pss", 64),
     13: ("rsa2048", 384, "pss", 48), 14: ("rsa3072", 256, "pss", 32), 20: ("p256", 256, "ecdsa", 0),
-    21: ("bp256", 256, "ecdsa", 0), 27: ("p521", 256, "ecdsa", 0),
+    21: ("bp256", 256, "ecdsa", 0), 24: ("p224", 224, "ecdsa", 0), 25: ("bp384", 384, "ecdsa", 0),
+    27: ("p521", 256, "ecdsa", 0),
 }
 
 
@@ -189,6 +191,10 @@ def signer_key(sig, seed=5, k=0):
         return EcKey(rng, BP256)
     if kind == "p521":
         return EcKey(rng, P521)
+    if kind == "p224":
+        return EcKey(rng, P224, hashlib.sha224)
+    if kind == "bp384":
+        return EcKey(rng, BP384, hashlib.sha384)
     bits = {"rsa2048": 2048, "rsa2048e3": 2048, "rsa4096": 4096, "rsa3072": 3072}[kind]
     return RsaKey(bits, rng, 3 if kind == "rsa2048e3" else 65537)
 
@@ -221,7 +227,7 @@ def make_passport(sig, key, index, seed=5, dg_hash=None, n_dgs=5, dg15=True, td1
     if scheme == "ecdsa":
         r, s = key.sign(sa, rng)
         spki = ec_spki_named(named_curve, key.curve, key.q) if named_curve else ec_spki(key.curve, key.q)
-        sig_field, sig_alg = seq(integer(r), integer(s)), alg("ecdsaWithSHA256", b"")
+        sig_field, sig_alg = seq(integer(r), integer(s)), alg("ecdsaWithSHA%d" % hbits, b"")
         signature = (r, s)
     else:
         if scheme == "pss":

@@ -14,7 +14,7 @@ def _batch(sig, n, **opt):
     key = sodgen.signer_key(sig)
     pps = [sodgen.make_passport(sig, key, i, **opt) for i in range(n)]
     if isinstance(key, I.EcKey):
-        pkh = I.ecdsa_pk_hash(key.q)
+        pkh = I.ecdsa_pk_hash(key.q, key.curve.p.bit_length())
     else:
         a = I.chunk_limbs(key.n, 64, 15)
         pkh = I.poseidon([(a[3 * i] << 128) + (a[3 * i + 1] << 64) + a[3 * i + 2] for i in range(5)])
@@ -25,8 +25,8 @@ def _batch(sig, n, **opt):
     return pps, np.stack(ident)
 
 
-@pytest.mark.parametrize("sig,opt", [(1, {}), (11, {}), (20, {}), (1, {"dg15": False, "n_dgs": 3})],
-                         ids=["sig1", "sig11", "sig20", "sig1_noaa"])
+@pytest.mark.parametrize("sig,opt", [(1, {}), (11, {}), (20, {}), (25, {"signing_time": False}), (1, {"dg15": False, "n_dgs": 3})],
+                         ids=["sig1", "sig11", "sig20", "sig25", "sig1_noaa"])
 def test_sod_to_witness(oracle, sig, opt):
     pps, ident = _batch(sig, 24, **opt)
     params = PP.parse(pps[0])["params"]

@@ -110,3 +110,24 @@ def test_parse_errors_are_reported():
         PP.parse(dict(src(canon), sod=base64.b64encode(b"\x30\x03\x02\x01").decode()))
     with pytest.raises(native.PzkError):
         PP.parse(dict(src(canon), sod=""))
+
+
+def test_ecdsa_p224_bp384_sods(oracle):
+    """EF.SOD of ECDSA signers the reference classifies as SIGNATURE_TYPE 24 / 25 (process_passport.js getSigType by the
+    key's curve parameter a). brainpoolP384r1 (SHA-384 throughout; signed attributes without signingTime, so they fit
+    the circuit's one 1024-bit block): the rows verify in the CPU restatement (every check of the circuit passes on
+    a signature made over real DER). secp224r1: processPassport's getChunkedParams (:590-626) cuts the key and the
+    signature into 4 x 64-bit chunks where the circuit takes 7 x 32 (registerIdentityBuilder.circom:90-94), so no
+    input the reference pipeline writes fits the SIG 24 circuit: status PZK_PP_LIMBS."""
+    from pzkwit import sodgen
+    pp = sodgen.make_passport(25, sodgen.signer_key(25), 0, signing_time=False)
+    info = PP.parse(pp)
+    assert info["params"]["sig"] == 25 and info["chunk_number"] == 6 and info["chunk_bits"] == 64
+    rows, st = PP.input_rows(info["params"], [pp])
+    assert st[0] == 0
+    assert oracle.register_witness(oracle.register_params(**info["params"]), rows[0])[0] == 0
+    pp = sodgen.make_passport(24, sodgen.signer_key(24), 0)
+    info = PP.parse(pp)
+    assert info["params"]["sig"] == 24 and (info["chunk_number"], info["chunk_bits"]) == (4, 64)
+    _, st = PP.input_rows(info["params"], [pp])
+    assert PP.PP_STATUS[int(st[0])] == "limbs"

@@ -8,6 +8,8 @@
 #include "layout.hpp"
 #include "core_util.hpp"
 #include "mapsink.hpp"
+#include "bufs.hpp"
+#include "ec_emit.hpp"
 
 namespace pzk {
 inline namespace PZK_EC_NS {
@@ -940,6 +942,57 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
       const uint32_t h = base + k * blockDim.x;
       store_half<MM>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
+  }
+}
+
+// ============================================================ k_emit_ecr: the generator multiplication's selection tables
+// EllipicCurveScalarGeneratorMult (curve.circom:750-797): resultCoordinateComputation[PARTS][256][2][N],
+// equal[PARTS][256] (IsEqual) and getSumOfNElements[PARTS][2][N] (GetSum(256)) — 245 k signals per P-256 witness,
+// every one a function of a part's scalar byte b_i and its additionPoints row. Work item = a chunk of one region;
+// the chunk's parts (<= 4), their bytes and the 1/(b - j) table go to LDS first, so the store loop issues no
+// global load (a load behind the wave's stores would wait for them: gfx9 vmcnt counts both).
+template <int MM>
+__global__ void __launch_bounds__(256) k_emit_ecr(DevLayout L, const Work* work, Bufs B) {
+  constexpr int MAXP = 4;
+  __shared__ uint64_t ap[MAXP][P2];
+  __shared__ uint32_t bt[MAXP];
+  __shared__ fr inv[256];
+  __shared__ uint4 stage[2 * 256];
+  const Work wk = work[blockIdx.x];
+  const uint32_t w = blockIdx.y;
+  const Region R = L.regions[wk.region];
+  const uint64_t* C = B.ec_core + (size_t)w * ECG.core_words;
+  const uint32_t per = R.kind == RK_EC_GM_RCC ? 256u * P2 : R.kind == RK_EC_GM_EQ ? 256u * 6 : 512u * P2;
+  const uint32_t i0 = wk.start / per;
+  for (uint32_t t = threadIdx.x; t < MAXP * P2; t += blockDim.x) {
+    const uint32_t k = t / P2, q = t % P2, i = i0 + k;
+    if (i < (uint32_t)ECG.parts) ap[k][q] = C[ECG.c_gm_ap + P2 * i + q];
+  }
+  if (threadIdx.x < MAXP && i0 + threadIdx.x < (uint32_t)ECG.parts) {
+    uint64_t u1[NL];
+    for (int k = 0; k < NL; k++) u1[k] = C[ECG.c_u1 + k];
+    bt[threadIdx.x] = (uint32_t)sc_byte(u1, (int)(i0 + threadIdx.x));
+  }
+  if (R.kind == RK_EC_GM_EQ) inv[threadIdx.x] = B.inv_small[threadIdx.x];
+  __syncthreads();
+  const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
+  if (R.kind == RK_EC_GM_RCC) {  // = equal[i][j] * (point j of part i): the part's additionPoints row where j == b_i
+    emit_run<MM>(out, wk.count, stage, [&](uint32_t q0) -> El {
+      const uint32_t s = wk.start + q0, k = s / (256u * P2) - i0, j = (s / P2) % 256u, q = s % P2;
+      return el_u64(bt[k] == j ? ap[k][q] : 0ull);
+    });
+  } else if (R.kind == RK_EC_GM_EQ) {  // IsEqual(j, b_i): out | in[2] | IsZero(out, b_i - j, 1 / (b_i - j))
+    emit_run<MM>(out, wk.count, stage, [&](uint32_t q0) -> El {
+      const uint32_t s = wk.start + q0, blk = s / 6, e = s % 6, k = (blk >> 8) - i0, j = blk & 255u, b = bt[k];
+      const int d = (int)b - (int)j;
+      return iseq_sig((int)e, j, b, d == 0 ? fr_zero() : d > 0 ? inv[d] : fr_sub(fr_zero(), inv[-d]));
+    });
+  } else {  // GetSumOfNElements(256) of column (i, a, k): out | in[256] | sum[255]
+    emit_run<MM>(out, wk.count, stage, [&](uint32_t q0) -> El {
+      const uint32_t s = wk.start + q0, blk = s >> 9, m = s & 511u, k = blk / P2 - i0, q = blk % P2, b = bt[k];
+      const uint64_t v = ap[k][q];
+      return el_u64(m == 0 ? v : m <= 256 ? (b == m - 1 ? v : 0ull) : (b <= m - 256 ? v : 0ull));
+    });
   }
 }
 

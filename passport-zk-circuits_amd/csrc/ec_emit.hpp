@@ -64,8 +64,10 @@ __device__ __forceinline__ El switcher_sig(int e, uint64_t bl, uint64_t in0, uin
   }
 }
 
+// The small ECDSA regions (one instance for every curve: the geometry comes from EC_GEO[curve]; the three big
+// selection tables of the generator multiplication have their own per-curve emitter, k_emit_ecr in ec_core.hpp)
 __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint32_t w, uint32_t s) {
-  const int cv = L.reg.ec_curve;  // this TU is curve-generic: geometry and constants by run-time curve id
+  const int cv = L.reg.ec_curve;
   const EcGeo& G = EC_GEO[cv];
   const int N = G.nl, CS = G.cs, P2 = 2 * N;
   const uint64_t* C = B.ec_core + (size_t)w * G.core_words;
@@ -76,24 +78,6 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
   switch (R.kind) {
     case RK_EC_U64: return el_u64(C[R.a[0] + s]);
     case RK_EC_CONST: return el_u64(ec_k(cv, R.a[0], (int)s));
-    case RK_EC_GM_RCC: {  // resultCoordinateComputation[i][j][a][k] = equal[i][j] * point  (curve.circom:750-776)
-      const uint32_t i = s / (256 * P2), j = (s / P2) % 256, q = s % P2;
-      const uint32_t b = sc8(C + G.c_u1, CS, (int)i);
-      return el_u64(b == j ? C[G.c_gm_ap + P2 * i + q] : 0);
-    }
-    case RK_EC_GM_EQ: {  // equal[i][j]: in = (j, byte_i)
-      const uint32_t blk = s / 6, e = s % 6, i = blk >> 8, j = blk & 255u;
-      const uint32_t b = sc8(C + G.c_u1, CS, (int)i);
-      return iseq_sig((int)e, j, b, inv_small_signed(B.inv_small, (int)b - (int)j));
-    }
-    case RK_EC_GM_SUM: {  // GetSumOfNElements(256) of column (i, a, k): out | in[256] | sum[255]
-      const uint32_t blk = s >> 9, m = s & 511u, i = blk / P2, q = blk % P2;
-      const uint32_t b = sc8(C + G.c_u1, CS, (int)i);
-      const uint64_t v = C[G.c_gm_ap + P2 * i + q];
-      if (m == 0) return el_u64(v);
-      if (m <= 256) return el_u64(b == m - 1 ? v : 0);
-      return el_u64(b <= m - 256 ? v : 0);
-    }
     case RK_EC_GM_STEP: {  // isFirst/SecondDummyLeft/Right[i], then (switcherRight, switcherLeft)[a][k]
       const int i = R.a[0];
       const uint64_t* left = i == 0 ? C + G.c_gm_ap : C + G.c_gm_rp + P2 * (i - 1);
@@ -183,5 +167,4 @@ __device__ El ec_small(const DevLayout& L, const Bufs& B, const Region& R, uint3
     default: return el_u64(0);
   }
 }
-
 }  // namespace pzk

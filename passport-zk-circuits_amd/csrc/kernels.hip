@@ -392,6 +392,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
     case E_BITS: hipLaunchKernelGGL(k_emit_bits, g, blk, 0, st, L, work, B); break;
     case E_FLOW: hipLaunchKernelGGL(k_emit_flow, g, blk, 0, st, L, work, B); break;
     case E_MM: return launch_emit_mm(L, work, n_work, B, batch, st);  // kernels_rsa.hip
+    case E_ECR: return launch_emit_ecr(L, work, n_work, B, batch, st);  // kernels_ec*.hip
     case E_BJJ: hipLaunchKernelGGL(k_emit_bjj, g, blk, 0, st, L, work, B); break;
     case E_SHA5:
     case E_SHA5D:

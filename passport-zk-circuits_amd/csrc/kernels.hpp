@@ -47,6 +47,8 @@ hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_
                             ValueStore vs, fr* pos_core, fr* smt_core, hipStream_t st);
 hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,
                           uint64_t* ec_jac, fr* ec_inv, int32_t* status, uint32_t batch, hipStream_t st);
+hipError_t launch_emit_ecr(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                           hipStream_t st);
 hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uint32_t n_ops, const uint64_t* ec_core,
                            uint8_t* ec_tab, int32_t* status, uint32_t batch, hipStream_t st);
 hipError_t launch_inv_small(fr* out, hipStream_t st);

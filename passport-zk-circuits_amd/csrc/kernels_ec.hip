@@ -52,6 +52,13 @@ hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_w
   return hipGetLastError();
 }
 
+hipError_t launch_emit_ecr_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                              hipStream_t st) {
+  if (n_work == 0) return hipSuccess;
+  hipLaunchKernelGGL((L.keep.bits ? k_emit_ecr<MAP_DIRECT> : k_emit_ecr<MAP_O0>), dim3(n_work, batch), dim3(256), 0, st, L, work, B);
+  return hipGetLastError();
+}
+
 }  // namespace PZK_EC_NS
 
 #if PZK_EC_CURVE == 0
@@ -63,6 +70,8 @@ hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_w
                                 const uint64_t* ec_core, uint8_t* ec_tab, int32_t* status, uint32_t batch,              \
                                 hipStream_t st);                                                                        \
   hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,   \
+                                hipStream_t st);                                                                        \
+  hipError_t launch_emit_ecr_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,   \
                                 hipStream_t st);                                                                        \
   }
 PZK_EC_DECL(ec_c1)
@@ -88,6 +97,10 @@ hipError_t launch_ec_table(const DevLayout& L, int type, const int32_t* ops, uin
 hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st) {
   PZK_EC_DISPATCH(launch_emit_ect_cv(L, work, n_work, B, batch, st))
+}
+hipError_t launch_emit_ecr(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
+                           hipStream_t st) {
+  PZK_EC_DISPATCH(launch_emit_ecr_cv(L, work, n_work, B, batch, st))
 }
 #undef PZK_EC_DISPATCH
 #endif

@@ -12,42 +12,65 @@
 namespace pzk {
 
 // ------------------------------------------------------------------- emit: Poseidon
+// A workgroup emits one PoseidonHash block (a Work item) for WPB consecutive witnesses: per witness it
+// fills the permutation's value image in LDS (pos_img_fill), then stores the block's signals from it. The
+// stores of witness k are still in flight while the image of witness k + 1 is computed, so one workgroup
+// overlaps its own compute with its store drain; the block's descriptors are loaded once per WPB witnesses.
 template <int T, int MM>
 __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
-                                                          const fr* pos_core, uint8_t* wtns, size_t stride) {
+                                                          const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch,
+                                                          uint32_t wpb) {
   constexpr PosImg I(T);
   __shared__ fr img[I.size];
   const Work wk = work[blockIdx.x];
-  const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
   const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
   // the block's descriptors go to LDS first: a global load inside the store loop would wait for
   // every store in flight (gfx9 vmcnt counts stores too)
   __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
   for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
-  pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
-  // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
-  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
-  const uint4* im = reinterpret_cast<const uint4*>(img);
-  const uint32_t tot = 2 * wk.count;
-  for (uint32_t h0 = threadIdx.x & ~63u; h0 < tot; h0 += blockDim.x) {  // wave-uniform loop: store_half's map window
-    const uint32_t h = h0 + (threadIdx.x & 63);
-    store_half<MM>(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
+  const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
+  for (uint32_t w = w0; w < w1; w++) {
+    if (w != w0) __syncthreads();  // every lane has read the previous witness's image
+    pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+    // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
+    const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
+    const uint4* im = reinterpret_cast<const uint4*>(img);
+    const uint32_t tot = 2 * wk.count;
+    for (uint32_t h0 = threadIdx.x & ~63u; h0 < tot; h0 += blockDim.x) {  // wave-uniform loop: store_half's map window
+      const uint32_t h = h0 + (threadIdx.x & 63);
+      store_half<MM>(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
+    }
   }
+}
+
+// witnesses per workgroup (A/B: PZK_POS_WPB, default 1)
+static uint32_t pos_wpb() {
+  static const uint32_t v = [] {
+    const char* e = getenv("PZK_POS_WPB");
+    const int x = e ? atoi(e) : 1;
+    return (uint32_t)(x < 1 ? 1 : x > 64 ? 64 : x);
+  }();
+  return v;
 }
 
 hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,
                            uint32_t batch, int t, hipStream_t st) {
   if (n_work == 0) return hipSuccess;
-  dim3 g(n_work, batch), blk(EMIT_THREADS);
+  const uint32_t wpb = pos_wpb();
+  dim3 g(n_work, (batch + wpb - 1) / wpb), blk(EMIT_THREADS);
+#define PZK_POS_LAUNCH(T_)                                                                                              \
+  hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<T_, MAP_DIRECT> : k_emit_pos<T_, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, \
+                     B.pos_core, B.wtns, B.stride, batch, wpb)
   switch (t) {
-    case 2: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<2, MAP_DIRECT> : k_emit_pos<2, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 3: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<3, MAP_DIRECT> : k_emit_pos<3, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 4: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<4, MAP_DIRECT> : k_emit_pos<4, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 5: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<5, MAP_DIRECT> : k_emit_pos<5, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
-    case 6: hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<6, MAP_DIRECT> : k_emit_pos<6, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride); break;
+    case 2: PZK_POS_LAUNCH(2); break;
+    case 3: PZK_POS_LAUNCH(3); break;
+    case 4: PZK_POS_LAUNCH(4); break;
+    case 5: PZK_POS_LAUNCH(5); break;
+    case 6: PZK_POS_LAUNCH(6); break;
     default: return hipErrorInvalidValue;
   }
+#undef PZK_POS_LAUNCH
   return hipGetLastError();
 }
 

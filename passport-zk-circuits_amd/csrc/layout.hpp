@@ -80,11 +80,12 @@ enum RegionKind : uint32_t {
 
 // emit kernels (one work list each)
 // E_GENR = generic regions that read the RSA core (they run after it, off the main chain)
-// E_ECT = ECDSA table blocks (k_emit_ect)
+// E_ECT = ECDSA table blocks (k_emit_ect); E_ECR = the generator multiplication's selection tables (k_emit_ecr:
+// resultCoordinateComputation, equal[][], getSumOfNElements, ec_core.hpp)
 // E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
 // E_SHA1 = SHA-1 hasher regions (k_emit_sha1); E_SHA5 = SHA-384/512 hasher regions (k_emit_sha512); E_SHA5D = the
 // SHA-384 hashers of derived messages (RSA-PSS SHA-384 MGF1 / M'), emitted after the PSS chain like E_SHAD
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_SHA5D, E_COUNT };
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_SHA5D, E_ECR, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -97,6 +98,7 @@ __host__ __device__ inline int emitter_of(uint32_t kind) {
     case RK_BJJ_STEPS: return E_BJJ;
     case RK_RSA_OUT: return E_GENR;
     case RK_ECT: return E_ECT;
+    case RK_EC_GM_RCC: case RK_EC_GM_EQ: case RK_EC_GM_SUM: return E_ECR;
     default: return kind >= RK_EC_U64 && kind <= RK_PSS_XOR ? E_GENR : E_GEN;
   }
 }

@@ -33,21 +33,21 @@ int api_fail(int code, const std::string& msg) { return fail(code, msg); }  // p
 enum Phase {
   PH_LOAD, PH_SHA_CORE, PH_PREP, PH_RSA_CORE, PH_BJJ_CORE, PH_POS_CORE, PH_SMT,
   PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ,
-  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_PSS, PH_COUNT
+  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_PSS, PH_EMIT_ECR, PH_COUNT
 };
 static const char* PHASE_NAMES[PH_COUNT] = {"load_values", "sha_core", "prep",     "rsa_core",  "bjj_core",
                                             "pos_core",    "smt",      "emit_gen", "emit_sha",  "emit_pos",
                                             "emit_bits",   "emit_flow", "emit_mm", "emit_bjj",
-                                            "ec_core",     "ec_table",  "emit_ect", "pss"};
+                                            "ec_core",     "ec_table",  "emit_ect", "pss",       "emit_ecr"};
 static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k_prep",      "k_rsa_core",
                                               "k_bjj_core",    "k_pos_core",  "k_smt_prep+k_smt_chain",
                                               "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
                                               "k_emit_flow",   "k_emit_mm",   "k_emit_bjj",
                                               "k_ec_core",     "k_ec_table",  "k_emit_ect",
-                                              "k_pss_mgf+k_sha_core+k_pss_mdash"};
+                                              "k_pss_mgf+k_sha_core+k_pss_mdash", "k_emit_ecr"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
                                         PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
-                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA};
+                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_ECR};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -158,10 +158,11 @@ struct pzk_instance {
   // cores can run while call k's emitters still read set k % 2
   Scratch scr[NSETS];
   uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
-  // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit)
-  hipEvent_t ev_done[NSETS][4] = {};
+  // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit, tail)
+  hipEvent_t ev_done[NSETS][5] = {};
   hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
+  hipStream_t s_tail = nullptr;  // the small tail emitters (PZK_TAIL=own), so the next call's SHA emitter never queues behind them
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
   // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
@@ -322,7 +323,7 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail})
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_pos, I->ev_tab})
     if (e) (void)hipEventDestroy(e);
@@ -355,7 +356,7 @@ struct DeviceGuard {
 
 // wait until every stream of the instance has drained (all calls issued so far are complete)
 static int sync_all(pzk_instance* I) {
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
@@ -428,7 +429,8 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess;
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
+       hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+       hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_pos, &I->ev_tab})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t& e : I->ev_gather) {
@@ -706,7 +708,8 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   };
   // PZK_SERIAL=1 (profiling): every phase on the main stream, so kernel times are standalone
   static const bool serial = getenv("PZK_SERIAL") != nullptr;
-  hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha, s_emit = serial ? st : I->s_emit;
+  hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha, s_emit = serial ? st : I->s_emit,
+              s_own = serial ? st : I->s_tail;
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
     HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, S.d_values, B, st)); }
@@ -716,7 +719,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
     for (int e = 0; e < E_COUNT; e++)
       if ((rc = emit(e, st))) return rc;
-    s_rsa = s_sha = s_emit = st;
+    s_rsa = s_sha = s_emit = s_own = st;
   } else {
     // Four streams. The dependency chains get the high-priority streams: the
     // signature core (rsa) depends only on the inputs; the Poseidon/SMT/BabyJubJub chain (main)
@@ -778,6 +781,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if ((rc = emit(E_SHAD, s_sig))) return rc;
     if ((rc = emit(E_SHA5D, s_sig))) return rc;  // SHA-384 PSS hashers (SIGNATURE_TYPE 13)
     if (lay.is_ecdsa) {
+      if ((rc = emit(E_ECR, s_sig))) return rc;  // the generator multiplication's selection tables (EC core only)
       HIPCHK(hipStreamWaitEvent(s_sig, I->ev_tab, 0));
       if ((rc = emit(E_ECT, s_sig))) return rc;
     }
@@ -799,10 +803,11 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // the RSA stream, equals split; tuning switch PZK_TAIL=sha|emit|split|rsa, profiles/README.md)
     static const char* tail_env = getenv("PZK_TAIL");
     static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0
-                                 : !strcmp(tail_env, "rsa") ? 3 : 2;
-    hipStream_t s_tail = tail_mode == 1 ? s_emit : tail_mode == 3 ? s_rsa : s_sha, s_pos = tail_mode == 0 ? s_sha : s_emit;
-    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
-    if ((rc = emit(E_BJJ, s_sha))) return rc;
+                                 : !strcmp(tail_env, "rsa") ? 3 : !strcmp(tail_env, "own") ? 4 : 2;
+    hipStream_t s_tail = tail_mode == 1 ? s_emit : tail_mode == 3 ? s_rsa : tail_mode == 4 ? s_own : s_sha,
+                s_pos = tail_mode == 0 ? s_sha : s_emit, s_bjj = tail_mode == 4 ? s_own : s_sha;
+    HIPCHK(hipStreamWaitEvent(s_bjj, I->ev_bjj, 0));
+    if ((rc = emit(E_BJJ, s_bjj))) return rc;
     HIPCHK(hipStreamWaitEvent(s_pos, I->ev_pos, 0));
     if ((rc = emit(E_POS, s_pos))) return rc;
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_pos, 0));
@@ -816,8 +821,8 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if ((rc = emit(E_BITS, s_tail))) return rc;
     if ((rc = emit(E_GENR, s_tail))) return rc;
   }
-  hipStream_t streams[4] = {st, s_rsa, s_sha, s_emit};
-  for (int i = 0; i < 4; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
+  hipStream_t streams[5] = {st, s_rsa, s_sha, s_emit, s_own};
+  for (int i = 0; i < 5; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));
   }
@@ -866,7 +871,7 @@ static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[slot], o0_stride,
                           d_status ? d_status + lo : nullptr, &ex);
     if (rc) return rc;
-    for (int i = 1; i < 4; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
+    for (int i = 1; i < 5; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
     HIPCHK(launch_wtns_gather(I->d_o0[slot], o0_stride, I->d_map, I->out_size, d_wtns + stride * lo, stride, (uint32_t)n,
                               I->stream));
     HIPCHK(hipEventRecord(I->ev_done[set][0], I->stream));

@@ -911,9 +911,9 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
 // workgroup size: a big table (P-224 51 KB, brainpoolP384r1 39 KB of LDS) caps the workgroups per CU at 3-4, so
 // those curves run 8 waves per workgroup to keep ~24-32 waves per CU in flight
 constexpr int ECT_NT = EC_TABLE_MAX[EC_CV] > 1024 ? 512 : 256;
-template <int MM>  // store mode (mapsink.hpp)
+template <int MM, int ECT_U>  // store mode (mapsink.hpp), descriptors per batch
 __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
-                                                  size_t stride) {
+                                                  size_t stride, int prefetch) {
   __shared__ uint4 tab[2 * EC_TABLE_MAX[EC_CV]];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
@@ -925,23 +925,29 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
   __syncthreads();
   const uint32_t* prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
   const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
-  // ECT_U descriptors are loaded before the ECT_U stores that use them: a global load issued
-  // after a store waits for it (gfx9 vmcnt counts both), which would put every element's store
-  // latency in series under the saturated write path. Two lanes per element, 1 KiB per wave store.
-  constexpr int ECT_U = 8;
-  const uint32_t tot = 2 * wk.count;
-  for (uint32_t base = threadIdx.x; base < tot; base += ECT_U * blockDim.x) {
-    uint32_t d[ECT_U];
+  // ECT_U descriptors per batch, loaded before the batch's stores (a global load issued after a store waits for it:
+  // gfx9 vmcnt counts both, in order); with prefetch the next batch's descriptors are loaded ahead of this batch's
+  // stores (PZK_ECT_PREFETCH, PZK_ECT_U: tuning knobs). Two lanes per element, 1 KiB per wave store.
+  const uint32_t tot = 2 * wk.count, step = ECT_U * blockDim.x;
+  uint32_t d[ECT_U], dn[ECT_U];
+  auto load = [&](uint32_t base, uint32_t* dd) {
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
-      d[k] = h < tot ? prog[h >> 1] : 0u;
+      dd[k] = h < tot ? prog[h >> 1] : 0u;
     }
+  };
+  load(threadIdx.x, dn);
+  for (uint32_t base = threadIdx.x; base < tot; base += step) {
+#pragma unroll
+    for (int k = 0; k < ECT_U; k++) d[k] = dn[k];
+    if (prefetch && base + step < tot) load(base + step, dn);
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
       store_half<MM>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
+    if (!prefetch && base + step < tot) load(base + step, dn);
   }
 }
 

@@ -4,6 +4,7 @@
 // (brainpoolP256r1 / secp224r1 / brainpoolP384r1). The curve-0 unit also defines the public launchers,
 // which dispatch on the instance's curve.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "bufs.hpp"
 #include "ec_core.hpp"
@@ -47,8 +48,11 @@ hipError_t launch_ec_table_cv(const DevLayout& L, int type, const int32_t* ops, 
 hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                            hipStream_t st) {
   if (n_work == 0) return hipSuccess;
-  hipLaunchKernelGGL((L.keep.bits ? k_emit_ect<MAP_DIRECT> : k_emit_ect<MAP_O0>), dim3(n_work, batch), dim3(ECT_NT), 0, st, L, work,
-                     B.ec_tab, B.wtns, B.stride);
+  static const int prefetch = getenv("PZK_ECT_PREFETCH") ? atoi(getenv("PZK_ECT_PREFETCH")) : 1;
+  static const int u = getenv("PZK_ECT_U") ? atoi(getenv("PZK_ECT_U")) : 16;  // isolated P-256: 8 / 16 / 32 = 22.6 / 21.7 / 41.0 ms
+  auto kern = L.keep.bits ? k_emit_ect<MAP_DIRECT, 16>
+              : u == 16 ? k_emit_ect<MAP_O0, 16> : u == 32 ? k_emit_ect<MAP_O0, 32> : k_emit_ect<MAP_O0, 8>;
+  hipLaunchKernelGGL(kern, dim3(n_work, batch), dim3(ECT_NT), 0, st, L, work, B.ec_tab, B.wtns, B.stride, prefetch);
   return hipGetLastError();
 }
 

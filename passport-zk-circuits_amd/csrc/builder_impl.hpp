@@ -127,10 +127,10 @@ struct Builder {
     int i = 0;
     for (int s : in_slots) t.in_slot[i++] = s;
     t.out_slot = out_slot >= 0 ? out_slot : value();
-    t.core_off = (int)L.pos_core_elems;
+    t.core_off = (int)L.pos_core_elems;  // a multiple of 4 Fr: each task's slice starts on a 128-byte line
     t.level = level;
     t.smt_level = -1;
-    L.pos_core_elems += pos_core_len(n + 1);
+    L.pos_core_elems += (pos_core_len(n + 1) + 3) & ~3u;  // (k_pos_core1 writes whole lines, poseidon.hpp)
     L.max_t = std::max(L.max_t, n + 1);
     L.pos.push_back(t);
     region(RK_POSEIDON, pos_hash_size(n), {(int32_t)L.pos.size() - 1, n});

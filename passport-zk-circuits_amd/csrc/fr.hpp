@@ -33,6 +33,14 @@ __device__ __forceinline__ fr fr_u64(uint64_t x) {
 __device__ __forceinline__ fr fr_const(const uint32_t (&c)[8]) { fr r; for (int i = 0; i < 8; i++) r.v[i] = c[i]; return r; }
 __device__ __forceinline__ fr fr_mont_one() { return fr_const(R1_); }
 
+// bit i of a's limbs (a run-time a.v[i >> 5] puts `a` in scratch: select by AND/OR masks instead)
+__device__ __forceinline__ uint32_t fr_bit(const fr& a, int i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r |= a.v[k] & (0u - (uint32_t)((i >> 5) == k));
+  return (r >> (i & 31)) & 1u;
+}
+
 __device__ __forceinline__ bool fr_is_zero(const fr& a) {
   uint32_t o = 0; for (int i = 0; i < 8; i++) o |= a.v[i]; return o == 0;
 }
@@ -48,7 +56,11 @@ __device__ __forceinline__ fr fr_reduce_once(const fr& a) {
     uint64_t d = (uint64_t)a.v[i] - P_[i] - br;
     t.v[i] = (uint32_t)d; br = (d >> 32) & 1;
   }
-  return br ? a : t;
+  // per-limb selects: `br ? a : t` on the structs is a select between two addresses, which keeps a
+  // caller's fr array (pos_core_lane's state) from being promoted to registers (scratch)
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.v[i] = br ? a.v[i] : t.v[i];
+  return t;
 }
 
 __device__ __forceinline__ fr fr_add(const fr& a, const fr& b) {
@@ -234,26 +246,17 @@ template <bool FAST = false>
 __device__ __forceinline__ fr fr_inv(const fr& a) {
   auto mul = [](const fr& x, const fr& y) { return FAST ? fr_mul_fast(x, y) : fr_mul(x, y); };
   auto sqr = [](const fr& x) { return FAST ? fr_mul_fast(x, x) : fr_sqr(x); };
-  // exponent p-2, scanned MSB->LSB with a 4-bit fixed window (wave-uniform control flow)
-  constexpr uint32_t E[8] = {0xefffffffu, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
-                             0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
-  fr tbl[16];
-  tbl[0] = fr_mont_one();
-  tbl[1] = a;
-#pragma unroll
-  for (int i = 2; i < 16; i++) tbl[i] = mul(tbl[i - 1], a);
-  fr r = fr_mont_one();
-  bool started = false;
-  for (int w = 63; w >= 0; w--) {
-    uint32_t nib = (E[w >> 3] >> ((w & 7) * 4)) & 15u;
-    if (started) { r = sqr(r); r = sqr(r); r = sqr(r); r = sqr(r); }
-    if (nib) {
-      // select tbl[nib] without dynamic indexing into a register array
-      fr s = tbl[0];
-#pragma unroll
-      for (int q = 1; q < 16; q++) if ((uint32_t)q == nib) s = tbl[q];
-      r = started ? mul(r, s) : s;
-      started = true;
+  // exponent p-2 (254 bits, 127 ones), square-and-multiply MSB->LSB on a wave-uniform bit: 253 squarings +
+  // 126 products. A 4-bit window table saves ~50 products, but a fr[16] selected by a run-time nibble is
+  // lowered to a 512-byte scratch array (every kernel calling this got 528 B of scratch per lane, whose
+  // spills reached HBM: 6.9x the algorithmic traffic of k_bjj_core, 1.5x of k_emit_flow)
+  fr r = a;
+  for (int wi = 7; wi >= 0; wi--) {
+    const uint32_t e = wi == 7 ? 0x30644e72u : wi == 6 ? 0xe131a029u : wi == 5 ? 0xb85045b6u : wi == 4 ? 0x8181585du
+                     : wi == 3 ? 0x2833e848u : wi == 2 ? 0x79b97091u : wi == 1 ? 0x43e1f593u : 0xefffffffu;
+    for (int b = wi == 7 ? 28 : 31; b >= 0; b--) {  // bit 253 (word 7, bit 29) is the leading one: r = a
+      r = sqr(r);
+      if ((e >> b) & 1u) r = mul(r, a);
     }
   }
   return r;

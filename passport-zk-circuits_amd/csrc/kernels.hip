@@ -237,8 +237,11 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
   // two passes: every load of the thread's elements first, then every store. A load issued after
   // a store waits for that store (gfx9 vmcnt counts both), which under a saturated write path
   // would serialise each element on the store latency. Mapped (mapsink.hpp): the element's keep bit
-  // and mapped index are loaded in the first pass too; a dropped element is not evaluated.
+  // and mapped index are loaded in the first pass too; a dropped element is not evaluated. PER stays small
+  // enough for the loop to unroll: at 8 (GEN_PACK 2048) it did not, val[] / dst[] went to 272 B of scratch
+  // per lane, and the spills doubled the kernel's HBM traffic.
   constexpr int PER = GEN_PACK / EMIT_THREADS;
+  static_assert(PER <= 2, "k_emit_gen keeps PER elements per lane in registers");
   El val[PER];
   uint64_t dst[PER];
 #pragma unroll

@@ -15,6 +15,7 @@ template <int T>
 __global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* tasks, ValueStore vs, fr* pos_core,
                                                   uint32_t core_elems, const fr* smt_core, uint32_t smt_core_fr) {
   core_priority();
+  __shared__ fr lines[4 * 64];
   uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= vs.batch) return;
   const PosTask& task = tasks[blockIdx.y];
@@ -22,7 +23,8 @@ __global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* ta
     int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
     if (task.smt_level < jl) return;
   }
-  pos_core_lane<T>(K, task, vs, w, pos_core + (size_t)w * core_elems);
+  const PosLineSink out{pos_core + (size_t)w * core_elems + task.core_off, lines + threadIdx.x};
+  pos_core_lane<T>(K, task, vs, w, out);
 }
 
 hipError_t launch_pos_core1(int t, const PosConsts& K, const PosTask* tp, uint32_t n_tasks, ValueStore vs, fr* pos_core,

@@ -129,7 +129,7 @@ struct GenPiece {
   uint32_t cum;
   uint32_t pad;
 };
-constexpr uint32_t GEN_PACK = 2048;        // signals per packed work item
+constexpr uint32_t GEN_PACK = 512;         // signals per packed work item (2 per k_emit_gen lane, in registers)
 constexpr uint32_t GEN_MAX_PIECES = 256;   // pieces per packed work item
 
 // SHA hasher job: one (witness, hasher) lane of the SHA core kernel

@@ -9,6 +9,7 @@
 //           every constant-times-state product into LDS in parallel, then writes the
 //           PoseidonHash(n) block (1 + n + |PoseidonEx|) as consecutive 32-byte elements.
 #pragma once
+#include <type_traits>
 #include "fr.hpp"
 #include "layout.hpp"
 #include "pos_prog.hpp"
@@ -35,72 +36,75 @@ struct ValueStore {
   __device__ __forceinline__ fr& at(int slot, uint32_t w) const { return v[(size_t)slot * batch + w]; }
 };
 
+// Round-state sink of pos_core_lane. Each lane's core slice starts on a 128-byte line (the builder aligns
+// task.core_off and the per-witness core to 4 Fr); element k is parked in the lane's 4-element line in LDS
+// and the line leaves as one whole 128-byte write when its last element arrives. Writing the 32-byte
+// elements as they come (one partial line per lane per round, 64 lanes on 64 different lines) let L2 evict
+// most lines half-written under the emitters' store stream: 2.2x the algorithmic write bytes.
+struct PosLineSink {
+  fr* out;   // the lane's task slice (128-byte aligned)
+  fr* line;  // the wave's LDS lines, element i of lane l at line[i * 64 + l]
+  __device__ __forceinline__ void flush(int k0, int n) const {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i < n) out[k0 + i] = line[i * 64];
+  }
+  __device__ __forceinline__ void put(int k, const fr& v) const {
+    line[(k & 3) * 64] = v;
+    if ((k & 3) == 3) flush(k - 3, 4);  // k is wave-uniform
+  }
+  __device__ __forceinline__ void finish(int k_end) const {
+    if (k_end & 3) flush(k_end & ~3, k_end & 3);
+  }
+};
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+// (every index into st[] / nx[] is a constant expression from the start, so the arrays are registers: with
+// `#pragma unroll` loops the state of t <= 6 stayed a 96-400 B scratch array)
 template <int T>
 __device__ __forceinline__ void pos_core_lane(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
-                                              fr* core /* this witness's Poseidon core */) {
+                                              const PosLineSink& out) {
   constexpr int t = T;
   const int RP = pos_nrp(t);
   fr st[t], nx[t];
-  fr* out = core + task.core_off;
-  st[0] = fr_zero();
-#pragma unroll
-  for (int j = 1; j < t; j++) st[j] = vs.at(task.in_slot[j - 1], w);
-#pragma unroll
-  for (int j = 0; j < t; j++) st[j] = fr_add(st[j], K.C(t, j));
+  st[0] = K.C(t, 0);
+  sfor<1, t>([&](auto J) { st[J] = fr_add(vs.at(task.in_slot[J - 1], w), K.C(t, J)); });
   int o = 0;
-  // full rounds 0..3 (round 3 mixes with P)
-  for (int r = 0; r < 4; r++) {
-#pragma unroll
-    for (int j = 0; j < t; j++) out[o + j] = st[j];
+  auto full = [&](int c0, bool use_p) __attribute__((always_inline)) {  // S-box layer (Ark constants from c0), then the t x t mix
+    sfor<0, t>([&](auto J) { out.put(o + J, st[J]); });
     o += t;
-#pragma unroll
-    for (int j = 0; j < t; j++) st[j] = fr_add(pow5(st[j]), K.C(t, (r + 1) * t + j));
-#pragma unroll
-    for (int i = 0; i < t; i++) {
+    sfor<0, t>([&](auto J) { st[J] = fr_add(pow5(st[J]), K.C(t, c0 + J)); });
+    sfor<0, t>([&](auto I) {
       fr acc = fr_zero();
-#pragma unroll
-      for (int j = 0; j < t; j++) acc = fr_add(acc, fr_mul(r == 3 ? K.Pm(t, j, i) : K.M(t, j, i), st[j]));
-      nx[i] = acc;
-    }
-#pragma unroll
-    for (int j = 0; j < t; j++) st[j] = nx[j];
-  }
-  // partial rounds
-  for (int r = 0; r < RP; r++) {
-#pragma unroll
-    for (int j = 0; j < t; j++) out[o + j] = st[j];
+      sfor<0, t>([&](auto J) { acc = fr_add(acc, fr_mul(use_p ? K.Pm(t, J, I) : K.M(t, J, I), st[J])); });
+      nx[I] = acc;
+    });
+    sfor<0, t>([&](auto J) { st[J] = nx[J]; });
+  };
+  for (int r = 0; r < 4; r++) full((r + 1) * t, r == 3);  // full rounds 0..3 (round 3 mixes with P)
+  for (int r = 0; r < RP; r++) {                          // partial rounds
+    sfor<0, t>([&](auto J) { out.put(o + J, st[J]); });
     o += t;
-    fr s0 = fr_add(pow5(st[0]), K.C(t, 5 * t + r));
+    const fr s0 = fr_add(pow5(st[0]), K.C(t, 5 * t + r));
     const int sb = (2 * t - 1) * r;
     fr acc = fr_mul(K.S(t, sb), s0);
-#pragma unroll
-    for (int i = 1; i < t; i++) acc = fr_add(acc, fr_mul(K.S(t, sb + i), st[i]));
-#pragma unroll
-    for (int i = 1; i < t; i++) st[i] = fr_add(st[i], fr_mul(s0, K.S(t, sb + t + i - 1)));
+    sfor<1, t>([&](auto I) { acc = fr_add(acc, fr_mul(K.S(t, sb + I), st[I])); });
+    sfor<1, t>([&](auto I) { st[I] = fr_add(st[I], fr_mul(s0, K.S(t, sb + t + I - 1))); });
     st[0] = acc;
   }
-  // full rounds 4..6
-  for (int r = 0; r < 3; r++) {
-#pragma unroll
-    for (int j = 0; j < t; j++) out[o + j] = st[j];
-    o += t;
-#pragma unroll
-    for (int j = 0; j < t; j++) st[j] = fr_add(pow5(st[j]), K.C(t, 5 * t + RP + r * t + j));
-#pragma unroll
-    for (int i = 0; i < t; i++) {
-      fr acc = fr_zero();
-#pragma unroll
-      for (int j = 0; j < t; j++) acc = fr_add(acc, fr_mul(K.M(t, j, i), st[j]));
-      nx[i] = acc;
-    }
-#pragma unroll
-    for (int j = 0; j < t; j++) st[j] = nx[j];
-  }
-#pragma unroll
-  for (int j = 0; j < t; j++) out[o + j] = st[j];  // Z3
+  for (int r = 0; r < 3; r++) full(5 * t + RP + r * t, false);  // full rounds 4..6
+  sfor<0, t>([&](auto J) { out.put(o + J, st[J]); });         // Z3
+  out.finish(o + t);
   fr h = fr_zero();
-#pragma unroll
-  for (int j = 0; j < t; j++) h = fr_add(h, fr_mul(K.M(t, j, 0), pow5(st[j])));
+  sfor<0, t>([&](auto J) { h = fr_add(h, fr_mul(K.M(t, J, 0), pow5(st[J]))); });
   vs.at(task.out_slot, w) = h;
 }
 

@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
   const int i0 = seg * BJJ_SEG_LEN, i1 = i0 + BJJ_SEG_LEN < NS ? i0 + BJJ_SEG_LEN : NS, ns = i1 - i0;
   auto S = [&](int e) -> fr& { return scratch[(size_t)e * nlanes + tid]; };
   const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
-  auto sk_bit = [&](int k) -> uint32_t { return (sk.v[k >> 5] >> (k & 31)) & 1u; };  // bit k of sk
+  auto sk_bit = [&](int k) -> uint32_t { return fr_bit(sk, k); };  // bit k of sk
   // segment start: A_{i0-1} = p * Base8, p = sk >> (254 - i0) (an i0-bit prefix)
   bool have = false;
   ExtPt A;
@@ -686,7 +686,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
     const int lv = getb(levm, i), st_inew = prev_top * lv, st_top = prev_top - st_inew;
     if (st_inew) j = i;
     if (i >= i0 && i < i0 + NL) {
-      const int lr = (key.v[i >> 5] >> (i & 31)) & 1;
+      const int lr = (int)fr_bit(key, i);
       flags[i] = (uint32_t)lv | ((uint32_t)getb(donem, i) << 1) | ((uint32_t)(st_top & 1) << 2) |
                  ((uint32_t)(st_inew & 1) << 3) | ((uint32_t)lr << 4) | ((uint32_t)iz(i) << 5);
     }
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
   for (int k = 0; k < NL; k++) {
     const int i = i0 + k;
     if (i < from) continue;
-    const int lr = (key.v[i >> 5] >> (i & 31)) & 1;
+    const int lr = (int)fr_bit(key, i);
     vs.at(R.v_smt_lr + 2 * i, w) = lr ? sm[k] : fr_zero();
     vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? fr_zero() : sm[k];
   }

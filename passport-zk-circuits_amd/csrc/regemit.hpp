@@ -191,8 +191,9 @@ __device__ __forceinline__ void u192_add(uint64_t* a, uint64_t lo, uint64_t hi) 
 
 // CompConstant(p-1) part i (compconstant.circom:28-46): a = 2^i, b = 2^128 - 2^i
 __device__ __forceinline__ void alias_part(const W256& bits, int i, uint64_t& lo, uint64_t& hi) {
-  fr pm1 = fr_const(P_); pm1.v[0] -= 1;
-  uint32_t cl = (pm1.v[(2 * i) >> 5] >> ((2 * i) & 31)) & 1, cm = (pm1.v[(2 * i + 1) >> 5] >> ((2 * i + 1) & 31)) & 1;
+  W256 pm1; for (int k = 0; k < 8; k++) pm1.v[k] = P_[k];
+  pm1.v[0] -= 1;
+  const uint32_t cl = w_bit(pm1, 2 * i), cm = w_bit(pm1, 2 * i + 1);  // (pm1.v[run-time index] went to scratch)
   uint32_t sl = w_bit(bits, 2 * i), sm = w_bit(bits, 2 * i + 1);
   // which of {0, a, b}
   int sel;
@@ -765,7 +766,7 @@ __global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work,
     fr sk = fr_from_mont_fast(skm);
     for (int j = threadIdx.x; j < nrec; j += blockDim.x) {
       int i = base + j;
-      bits[j] = (sk.v[(253 - i) >> 5] >> ((253 - i) & 31)) & 1;
+      bits[j] = fr_bit(sk, 253 - i);
     }
   }
   __syncthreads();

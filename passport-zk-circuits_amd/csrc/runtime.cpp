@@ -1067,7 +1067,17 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       for (const ShaJob& j : L.sha)
         b += j.algo >= 3 ? 32ull * 1024 * j.blocks + 4ull * (j.blocks * SHA5_BLOCK_CORE + 32)
                          : 32ull * 512 * j.blocks + 4ull * (j.blocks * (j.algo == 1 ? SHA1_BLOCK_CORE : SHA_BLOCK_CORE) + 8);
-    if (phase == PH_POS_CORE) b += 32ull * L.pos_core_elems;
+    if (phase == PH_POS_CORE)  // the round states written (not the line padding between task slices)
+      for (const PosTask& t : L.pos) b += 32ull * pos_core_len(t.n + 1);
+    if (phase == PH_PREP && L.is_register) {  // k_prep: the input elements it reads (one 32-byte
+      const RegInfo& G = L.reg;                                     // element per key / DG1 bit) + the SA digest
+      uint64_t el = G.ecdsa ? 2ull * G.ec_nl : 15;
+      if (G.aa && G.aa_ec) el += 2ull * G.aa_hs;
+      else if (G.aa) el += 4 * 200 + 224;
+      b += 32ull * (el + 4ull * G.dg1_chunk) + 32;
+    }
+    if (phase == PH_SMT && L.is_register)  // siblings, root and key read; SMT core and the
+      b += 32ull * (SMT_LEVELS + 2) + 32ull * SMT_CORE_FR + 32ull * 2 * SMT_LEVELS;  // level hash inputs written
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;
     if (phase == PH_LOAD) b += 64ull * L.loads.size();

@@ -2,6 +2,7 @@
 // kernels only from the shared headers), so it compiles in parallel with the other kernel units.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <stdio.h>
 
 #define PZK_TEMPLATE_KERNELS_ONLY
 #include "bufs.hpp"
@@ -10,6 +11,15 @@
 #include "kernels.hpp"
 
 namespace pzk {
+
+#ifdef PZK_MM_PROF  // profiling build only: image fill / store clocks of wave 0 of every workgroup
+static __device__ unsigned long long g_pos_prof[2];
+#define PZK_POS_CLK(v) const long long v = clock64()
+#define PZK_POS_ACC(i, t0) do { const long long t1_ = clock64(); if (threadIdx.x == 0) atomicAdd(&g_pos_prof[i], (unsigned long long)(t1_ - (t0))); } while (0)
+#else
+#define PZK_POS_CLK(v)
+#define PZK_POS_ACC(i, t0)
+#endif
 
 // ------------------------------------------------------------------- emit: Poseidon
 // A workgroup emits one PoseidonHash block (a Work item) for WPB consecutive witnesses: per witness it
@@ -32,7 +42,10 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
   for (uint32_t w = w0; w < w1; w++) {
     if (w != w0) __syncthreads();  // every lane has read the previous witness's image
+    PZK_POS_CLK(t0);
     pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+    PZK_POS_ACC(0, t0);
+    PZK_POS_CLK(t1);
     // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
     const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
     const uint4* im = reinterpret_cast<const uint4*>(img);
@@ -41,6 +54,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
       const uint32_t h = h0 + (threadIdx.x & 63);
       store_half<MM>(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
+    PZK_POS_ACC(1, t1);
   }
 }
 
@@ -56,6 +70,14 @@ static uint32_t pos_wpb() {
 
 hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,
                            uint32_t batch, int t, hipStream_t st) {
+#ifdef PZK_MM_PROF
+  {
+    static int n = 0;
+    unsigned long long h[2];
+    if (++n > 1 && hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pos_prof), sizeof h) == hipSuccess)
+      fprintf(stderr, "pos_prof launches=%d fill %llu store %llu\n", n - 1, h[0], h[1]);
+  }
+#endif
   if (n_work == 0) return hipSuccess;
   const uint32_t wpb = pos_wpb();
   dim3 g(n_work, (batch + wpb - 1) / wpb), blk(EMIT_THREADS);

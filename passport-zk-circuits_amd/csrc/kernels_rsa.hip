@@ -2,6 +2,7 @@
 // inversions, and the BigMultModP block emitter, with their launchers. Own translation unit (template
 // kernels only from the shared headers), so it compiles in parallel with kernels.hip.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #define PZK_TEMPLATE_KERNELS_ONLY
@@ -64,6 +65,19 @@ hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* 
 
 hipError_t launch_emit_mm(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                           hipStream_t st) {
+#ifdef PZK_MM_PROF
+  {  // cumulative per-section clocks (wave 0 of each workgroup), printed at every launch after a sync
+    static int n = 0;
+    if (++n > 1) {
+      unsigned long long h[MM_SECTIONS + 2];
+      if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mm_prof), sizeof h) == hipSuccess) {
+        fprintf(stderr, "mm_prof launches=%d", n - 1);
+        for (int i = 0; i <= (int)MM_SECTIONS; i++) fprintf(stderr, " %llu", h[i]);
+        fprintf(stderr, "\n");
+      }
+    }
+  }
+#endif
   if (n_work == 0) return hipSuccess;
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   const bool m = L.keep.bits != nullptr;  // store mode (mapsink.hpp)

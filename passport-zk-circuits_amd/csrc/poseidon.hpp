@@ -25,6 +25,7 @@ struct PosConsts {
   __device__ __forceinline__ const fr& M(int t, int i, int j) const { return base[ix.m_off[t] + i * t + j]; }
   __device__ __forceinline__ const fr& Pm(int t, int i, int j) const { return base[ix.p_off[t] + i * t + j]; }
   __device__ __forceinline__ const fr& S(int t, int i) const { return base[ix.s_off[t] + i]; }
+  __device__ __forceinline__ const fr& Sn(int t, int i) const { return nbase[ix.s_off[t] + i]; }
 };
 
 __device__ __forceinline__ fr pow5(const fr& x) { fr x2 = fr_sqr(x), x4 = fr_sqr(x2); return fr_mul(x4, x); }
@@ -179,86 +180,149 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
 }
 
 // ------------------------------------------------------------------------------ emit
-// Image fill (pos_prog.hpp layout, normal form), two phases:
-//  A: per S-box (8t full-layer elements, RP partial rounds): x, x^2, x^4, x^5 and the Ark output
-//     from the Montgomery layer state of the core; the remaining partial-round states; inputs,
-//     hash, zero.
-//  B: per GetSum row (7t full, 1 last, RP partial): t products constant*value, kept (products
-//     1..t-1, the row's `in` signals) and turned into prefix sums. mont_mul(c * R, v) = c * v, so
-//     products of Montgomery constants with normal-form values come out in normal form.
+// Image fill (pos_prog.hpp layout, normal form). Mixed forms give normal-form results straight from the FIPS product:
+// mont_mul(aR, b) = ab, so a Montgomery core value times a normal-form constant (or the reverse) is a normal-form
+// product. The work: NS = 8t + RP S-box chains (x^2 = sqr(xR) -> x^2 = from_mont(x^2 R) -> x^4 = (x^2 R) x^2 ->
+// x^5 = x^4 (xR), + the Ark constant), NA = RP (t-1) partial-round products S * Y_r[k] (k >= 1, from the core, no
+// dependency), the format conversions (S-box inputs, the other partial-round states, hash inputs / output), and the
+// GetSum products that need an S-box output (full mixes, mixLast, the partial rounds' k = 0 term).
+// Scheduled so that every wave runs ONE operation per step on all its lanes: thread q < NS keeps S-box q's chain
+// in registers across steps 1-4, and the lanes of a step beyond NS take independent products (steps 1, 3, 4) or
+// conversions (step 2), with operands and destinations selected per lane around a single product call. (The
+// previous fill gave each lane one S-box chain OR one conversion in a branchy loop: waves holding both ran both, and
+// the 81 S-box chains of t = 3 occupied two waves for 4 product times while the others idled: 14.5 product-times
+// of wave work per block against 10.5 here.)
 template <int T>
 __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const fr* core, const ValueStore& vs,
                                              const PosTask& task, uint32_t w) {
   constexpr int t = T;
   constexpr PosImg I(T);
   constexpr int RP = I.rp;
-  const int tid = threadIdx.x, nt = blockDim.x;
   // core order: X0..X3 (4t), Y0..Y_RP ((RP+1)t), Z1..Z3 (3t), all Montgomery
-  constexpr int NA = 8 * t + RP, NC = RP * (t - 1) + t;
-  for (int q = tid; q < NA + NC + 7; q += nt) {
+  constexpr int NS = 8 * t + RP, NA = RP * (t - 1), NC = RP * (t - 1) + t, NF = NS + NC + 7;
+  constexpr int PAD = (NS + 63) / 64 * 64 - NS;  // lanes left in the S-box waves of a product step
+  constexpr int A1 = NA < PAD ? NA : PAD, A3 = NA - A1 < PAD ? NA - A1 : PAD, A4 = NA - A1 - A3;
+  static_assert(NS <= 256, "one S-box chain per thread of a 256-thread workgroup");
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // S-box q: core index, image slots of x, x^2, x^4, x^5 and of the Ark output (-1: none), its Ark constant index
+  auto sbox = [&](int q, int& ci, int& din, int& d2, int& d4, int& d5, int& dark, int& cidx) {
     if (q < 8 * t) {
       const int f = q / t, j = q - f * t;
-      const int ci = f < 4 ? f * t + j : f == 4 ? 4 * t + RP * t + j : 4 * t + (RP + 1) * t + (f - 5) * t + j;
-      // mixed forms: mont_mul(aR, b) = ab, so normal-form powers come straight out of products
-      // with the Montgomery-form x and x^2 (3.4 products per S-box instead of 5.3)
-      const fr xm = core[ci], x2m = fr_sqr_fast(xm), x2 = fr_from_mont_fast(x2m), x4 = fr_mul_fast(x2m, x2), x5 = fr_mul_fast(x4, xm);
-      img[I.in + q] = fr_from_mont_fast(xm); img[I.p2 + q] = x2;
-      img[I.p4 + q] = x4; img[I.p5 + q] = x5;
-      if (f < 7) {
-        const int cidx = f < 4 ? (f + 1) * t + j : 5 * t + RP + (f - 4) * t + j;
-        img[I.ark + q] = fr_add(x5, K.Cn(t, cidx));
-      }
-    } else if (q < NA) {
-      const int r = q - 8 * t;
-      const fr xm = core[4 * t + r * t], x2m = fr_sqr_fast(xm), x2 = fr_from_mont_fast(x2m), x4 = fr_mul_fast(x2m, x2),
-               x5 = fr_mul_fast(x4, xm);
-      img[I.pin + r * t] = fr_from_mont_fast(xm); img[I.pp2 + r] = x2;
-      img[I.pp4 + r] = x4; img[I.pp5 + r] = x5;
-      img[I.pin0 + r] = fr_add(x5, K.Cn(t, 5 * t + r));
-    } else if (q < NA + NC) {
-      const int c = q - NA;
-      int r, i;
-      if (c < RP * (t - 1)) { r = c / (t - 1); i = 1 + (c - r * (t - 1)); }
-      else { r = RP; i = c - RP * (t - 1); }
-      img[I.pin + r * t + i] = fr_from_mont_fast(core[4 * t + r * t + i]);
+      ci = f < 4 ? f * t + j : f == 4 ? 4 * t + RP * t + j : 4 * t + (RP + 1) * t + (f - 5) * t + j;
+      din = I.in + q; d2 = I.p2 + q; d4 = I.p4 + q; d5 = I.p5 + q;
+      dark = f < 7 ? I.ark + q : -1;
+      cidx = f < 4 ? (f + 1) * t + j : 5 * t + RP + (f - 4) * t + j;
     } else {
-      const int k = q - NA - NC;
-      if (k < task.n) img[I.inp + k] = fr_from_mont_fast(vs.at(task.in_slot[k], w));
-      else if (k == 5) img[I.hash] = fr_from_mont_fast(vs.at(task.out_slot, w));
-      else if (k == 6) img[I.zero] = fr_zero();
+      const int r = q - 8 * t;
+      ci = 4 * t + r * t;
+      din = I.pin + r * t; d2 = I.pp2 + r; d4 = I.pp4 + r; d5 = I.pp5 + r;
+      dark = I.pin0 + r;
+      cidx = 5 * t + r;
     }
+  };
+  // independent product a: S[(2t-1) r + k] * Y_r[k] (k >= 1) -> the row's prefix-sum slot and its product slot
+  auto aprod = [&](int a, fr& x, fr& y, int& d1, int& d2) {
+    const int r = a / (t - 1), k = 1 + (a - r * (t - 1));
+    x = K.Sn(t, (2 * t - 1) * r + k);
+    y = core[4 * t + r * t + k];
+    d1 = I.ps + r * t + k;
+    d2 = I.prod(7 * t + 1 + r, k);
+  };
+  const bool chain = tid < NS;
+  int ci = 0, din = 0, d2 = 0, d4 = 0, d5 = 0, dark = -1, cidx = 0;
+  if (chain) sbox(tid, ci, din, d2, d4, d5, dark, cidx);
+  fr xm = chain ? core[ci] : fr_zero(), x2m = xm, x2 = xm, x4 = xm;
+  // step 1 (product): x^2 R = sqr(x R) | independent products [0, A1)
+  for (int q = tid; q < NS + A1; q += nt) {
+    fr x = xm, y = xm;
+    int e1 = -1, e2 = -1;
+    if (q >= NS) aprod(q - NS, x, y, e1, e2);
+    const fr r = fr_mul_fast(x, y);
+    if (q < NS) x2m = r;
+    else { img[e1] = r; img[e2] = r; }
+  }
+  // step 2 (conversion): x^2 | S-box inputs, partial-round states, hash inputs / output, zero
+  for (int q = tid; q < NS + NF; q += nt) {
+    fr x = x2m;
+    int e = q < NS ? d2 : -1;
+    if (q >= NS) {
+      const int f = q - NS;
+      if (f < NS) {  // S-box input x
+        int c_, i_, a_, b_, g_, h_, k_;
+        sbox(f, c_, i_, a_, b_, g_, h_, k_);
+        x = core[c_]; e = i_;
+      } else if (f < NS + NC) {
+        const int c = f - NS;
+        int r, i;
+        if (c < RP * (t - 1)) { r = c / (t - 1); i = 1 + (c - r * (t - 1)); }
+        else { r = RP; i = c - RP * (t - 1); }
+        x = core[4 * t + r * t + i]; e = I.pin + r * t + i;
+      } else {
+        const int k = f - NS - NC;
+        x = fr_zero();
+        if (k < task.n) { x = vs.at(task.in_slot[k], w); e = I.inp + k; }
+        else if (k == 5) { x = vs.at(task.out_slot, w); e = I.hash; }
+        else if (k == 6) e = I.zero;  // from_mont(0) = 0
+      }
+    }
+    const fr r = fr_from_mont_fast(x);
+    if (q < NS) x2 = r;
+    if (e >= 0) img[e] = r;
+  }
+  // step 3 (product): x^4 = (x^2 R) x^2 | independent products [A1, A1 + A3)
+  for (int q = tid; q < NS + A3; q += nt) {
+    fr x = x2m, y = x2;
+    int e1 = d4, e2 = -1;
+    if (q >= NS) aprod(A1 + q - NS, x, y, e1, e2);
+    const fr r = fr_mul_fast(x, y);
+    if (q < NS) x4 = r;
+    img[e1] = r;
+    if (e2 >= 0) img[e2] = r;
+  }
+  // step 4 (product): x^5 = x^4 (x R), Ark output | independent products [A1 + A3, NA)
+  for (int q = tid; q < NS + A4; q += nt) {
+    fr x = x4, y = xm;
+    int e1 = d5, e2 = -1;
+    if (q >= NS) aprod(A1 + A3 + q - NS, x, y, e1, e2);
+    const fr r = fr_mul_fast(x, y);
+    img[e1] = r;
+    if (e2 >= 0) img[e2] = r;
+    if (q < NS && dark >= 0) img[dark] = fr_add(r, K.Cn(t, cidx));
   }
   __syncthreads();
-  constexpr int NF = 7 * t, NR = NF + 1 + RP;
-  // products, one per thread: row r, term k (full mix f, output i: Mat_f[k][i] * ark[f][k];
-  // mixLast: M[k][0] * x5[7][k]; partial r: S[(2t-1)r + k] * in_k, in_0 = the S-box's Ark output)
-  for (int q = tid; q < NR * t; q += nt) {
-    const int row = q / t, k = q - row * t;
+  // step 5 (product): the GetSum terms of an S-box output (full mix f, output i: Mat_f[k][i] * ark[f][k]; mixLast:
+  // M[k][0] * x5[7][k]; partial r, k = 0: S[(2t-1) r] * (S-box output + Ark))
+  constexpr int NFR = 7 * t;
+  for (int q = tid; q < NFR * t + t + RP; q += nt) {
     fr c, v;
-    int dst;
-    if (row < NF) {
-      const int f = row / t, i = row - f * t;
+    int e1, e2 = -1;
+    if (q < NFR * t) {
+      const int row = q / t, k = q - row * t, f = row / t, i = row - f * t;
       c = f == 3 ? K.Pm(t, k, i) : K.M(t, k, i);
       v = img[I.ark + f * t + k];
-      dst = I.fs + row * t + k;
-    } else if (row == NF) {
+      e1 = I.fs + row * t + k;
+      if (k) e2 = I.prod(row, k);
+    } else if (q < NFR * t + t) {
+      const int k = q - NFR * t;
       c = K.M(t, k, 0);
       v = img[I.p5 + 7 * t + k];
-      dst = I.ls + k;
+      e1 = I.ls + k;
+      if (k) e2 = I.prod(NFR, k);
     } else {
-      const int r = row - NF - 1;
-      c = K.S(t, (2 * t - 1) * r + k);
-      v = k == 0 ? img[I.pin0 + r] : img[I.pin + r * t + k];
-      dst = I.ps + r * t + k;
+      const int r = q - NFR * t - t;
+      c = K.S(t, (2 * t - 1) * r);
+      v = img[I.pin0 + r];
+      e1 = I.ps + r * t;
     }
     const fr pr = fr_mul_fast(c, v);
-    img[dst] = pr;
-    if (k) img[I.prod(row, k)] = pr;
+    img[e1] = pr;
+    if (e2 >= 0) img[e2] = pr;
   }
   __syncthreads();
-  // prefix sums along each row
+  // prefix sums along each row (7t full, mixLast, RP partial)
+  constexpr int NR = NFR + 1 + RP;
   for (int row = tid; row < NR; row += nt) {
-    const int base = row < NF ? I.fs + row * t : row == NF ? I.ls : I.ps + (row - NF - 1) * t;
+    const int base = row < NFR ? I.fs + row * t : row == NFR ? I.ls : I.ps + (row - NFR - 1) * t;
     fr acc = img[base];
 #pragma unroll
     for (int k = 1; k < t; k++) { acc = fr_add(acc, img[base + k]); img[base + k] = acc; }

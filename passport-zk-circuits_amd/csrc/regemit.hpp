@@ -383,6 +383,7 @@ struct MMCore {
   bool kara;                                      // x*y by KaratsubaOverflow (K = 2^m), else schoolbook
   const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32; else null)
   const uint8_t* kt_hi;
+  const uint64_t* ko;                             // LDS node outputs of Karatsuba levels 1..KO_LEVELS (K = 32; else null)
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
 };
 __device__ __forceinline__ U192 u192_at(const uint64_t* a, int i) { U192 r; r.a0 = a[3 * i]; r.a1 = a[3 * i + 1]; r.a2 = a[3 * i + 2]; return r; }
@@ -620,6 +621,48 @@ __device__ __forceinline__ El el_num2bits(uint64_t lo, uint64_t hi, uint32_t L, 
   return el_u128_low(lo, hi, t - L);
 }
 
+// KaratsubaOverflow(32) signal from tables (K = KT_K): the node is found by a fixed five-step descent over the
+// compile-time subtree sizes (no size switch, no loop), its inputs are Karatsuba table entries and the outputs of
+// levels 1..KO_LEVELS come precomputed from LDS (ko, filled once per workgroup by k_emit_mm), so only the two
+// deepest levels (<= 2 products per signal) are multiplied here. kara_sig walked the tree and formed each output
+// as a convolution of up to 16 products per lane, the dominant VALU cost of the K = 32 emitter.
+constexpr int KO_LEVELS = 3, KO_VALUES = 456;  // 3 x 32 + 9 x 16 + 27 x 8 node outputs (2N per node)
+__device__ __forceinline__ int kt_level_base(int l) {  // first table entry of level l >= 1 (2N entries per node)
+  return l == 1 ? 0 : l == 2 ? 96 : l == 3 ? 240 : l == 4 ? 456 : 780;
+}
+__device__ __forceinline__ El kara_el32(const MMCore& C, const uint64_t* ko, uint32_t s) {
+  constexpr uint32_t SZ[6] = {mm_kara_size(32), mm_kara_size(16), mm_kara_size(8), mm_kara_size(4), mm_kara_size(2),
+                              mm_kara_size(1)};
+  int lvl = 0, m = 0;
+  uint32_t p = s;
+#pragma unroll
+  for (int L = 0; L < 5; L++) {  // node at level L has 4 N_L own signals, then its 3 child subtrees of SZ[L + 1]
+    const uint32_t own = 4u * (32u >> L);
+    if (lvl == L && p >= own) {
+      p -= own;
+      const uint32_t c = (p >= SZ[L + 1] ? 1u : 0u) + (p >= 2 * SZ[L + 1] ? 1u : 0u);
+      p -= c * SZ[L + 1];
+      m = 3 * m + (int)c;
+      lvl = L + 1;
+    }
+  }
+  const int N = 32 >> lvl;
+  if (p >= 2u * N) {  // in1[N] | in2[N]
+    const int k = (int)p - 2 * N;
+    if (lvl == 0) return el_u64(k < N ? C.x[k] : C.y[k - N]);
+    const int i = kt_level_base(lvl) + m * 2 * N + k;
+    return el_u128(C.kt_lo[i], C.kt_hi[i]);
+  }
+  if (p == 2u * N - 1) return el_zero();  // top coefficient (K(1).out[1] never assigned)
+  if (lvl == 0) return el_w(u192w(u192_at(C.cxy, (int)p)));
+  if (lvl <= KO_LEVELS) return el_w(u192w(u192_at(ko, kt_level_base(lvl) + m * 2 * N + (int)p)));
+  const int tb = kt_level_base(lvl) + m * 2 * N, lo = (int)p < N ? 0 : (int)p - N + 1, hi = (int)p < N ? (int)p : N - 1;
+  U192 acc;
+  for (int u = lo; u <= hi; u++)  // <= 2 terms (N <= 2)
+    mac2(acc, C.kt_lo[tb + u], C.kt_hi[tb + u], C.kt_lo[tb + N + (int)p - u], C.kt_hi[tb + N + (int)p - u]);
+  return el_w(u192w(acc));
+}
+
 template <int K, int SEC>
 __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
   if constexpr (SEC == MM_MODCHK) {  // Num2Bits(64)(mod_i): out[64] | in | sum[64]
@@ -647,6 +690,8 @@ __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
     const uint32_t i = s / PER, t = s - PER * i;
     const uint64_t lo = C.cr[2 * i], hi = C.cr[2 * i + 1] + (1ull << (RL - 1 - 64));
     return el_num2bits(lo, hi, RL, t);
+  } else if constexpr (SEC == MM_KARA && K == KT_K) {
+    return kara_el32(C, C.ko, s);
   } else if constexpr (SEC == MM_Q) {
     return el_u64(C.q[s]);
   } else if constexpr (SEC == MM_R) {
@@ -661,12 +706,23 @@ __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
   }
 }
 
+#ifdef PZK_MM_PROF  // profiling build only (make EXTRA=-DPZK_MM_PROF): per-section clocks of wave 0 of every workgroup
+static __device__ unsigned long long g_mm_prof[MM_SECTIONS + 2];
+#define PZK_MM_CLK(v) const long long v = clock64()
+#define PZK_MM_ACC(i, t0) do { const long long t1_ = clock64(); if (threadIdx.x == 0) atomicAdd(&g_mm_prof[i], (unsigned long long)(t1_ - (t0))); } while (0)
+#else
+#define PZK_MM_CLK(v)
+#define PZK_MM_ACC(i, t0)
+#endif
+
 template <int K, int SEC, int MM>
 __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, uint4* stage) {
   if constexpr (SEC < (int)MM_SECTIONS) {
     constexpr MMStarts S = mm_starts(K);
     constexpr uint32_t a = S.v[SEC], n = S.v[SEC + 1] - S.v[SEC];
+    PZK_MM_CLK(t0);
     emit_run<MM>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    PZK_MM_ACC(SEC, t0);
     mm_sections<K, SEC + 1, MM>(C, out, stage);
   }
 }
@@ -674,6 +730,7 @@ __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, u
 template <int K, int MM>
 __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint64_t lds[MM_CORE_WORDS(K) + K + 3 * (4 * K - 1)];
+  PZK_MM_CLK(tp);
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
@@ -729,10 +786,28 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
       nodes *= 3;
     }
   }
+  // outputs of the Karatsuba nodes of levels 1..KO_LEVELS (K = 32): out[s] = sum_u in1[u] in2[s - u] over the
+  // node's table inputs, once per workgroup (kara_el32 reads them)
+  constexpr int KON = K == KT_K ? 3 * KO_VALUES : 1;
+  __shared__ uint64_t ko[KON];
+  if (K == KT_K) {
+    for (int r = threadIdx.x; r < KO_VALUES; r += blockDim.x) {
+      const int l = r < 96 ? 1 : r < 240 ? 2 : 3, N = K >> l, rr = r - kt_level_base(l), m = rr / (2 * N);
+      const int p = rr - m * 2 * N, tb = kt_level_base(l) + m * 2 * N;
+      U192 acc;
+      if (p < 2 * N - 1)
+        for (int u = p < N ? 0 : p - N + 1; u <= (p < N ? p : N - 1); u++)
+          mac2(acc, kt_lo[tb + u], kt_hi[tb + u], kt_lo[tb + N + p - u], kt_hi[tb + N + p - u]);
+      ko[3 * r] = acc.a0; ko[3 * r + 1] = acc.a1; ko[3 * r + 2] = acc.a2;
+    }
+    __syncthreads();
+  }
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
-           cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr};
+           cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr,
+           K == KT_K ? ko : nullptr};
   const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
+  PZK_MM_ACC(MM_SECTIONS, tp);  // prologue: core loads, column sums, Karatsuba input table
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never
   // straddles the start of a wave (K = 32: two rows per wave; K = 64: one)

@@ -32,7 +32,10 @@ enum {
   PZK_CIRCUIT_SHA256 = 2,   /* Sha256HashChunks(blocks)      sha256HashChunks.circom:8 (config 2) */
   PZK_CIRCUIT_SHA1 = 3,     /* Sha1HashChunks(blocks)        hasher/sha1/sha1.circom:7 */
   PZK_CIRCUIT_SHA384 = 4,   /* Sha384HashChunks(blocks)      hasher/sha2/sha384/sha384HashChunks.circom:8 */
-  PZK_CIRCUIT_SHA512 = 5    /* Sha512HashChunks(blocks)      hasher/sha2/sha512/sha512HashChunks.circom */
+  PZK_CIRCUIT_SHA512 = 5,   /* Sha512HashChunks(blocks)      hasher/sha2/sha512/sha512HashChunks.circom */
+  PZK_CIRCUIT_QUERY = 6     /* QueryIdentity(idTreeDepth = size_arg, 80)  identityManagement/queryIdentity.circom:37;
+                               BabyPbk (undefined in the snapshot) is the reference's BabyjubjubBase8Multiplication,
+                               DESIGN.md §11 */
 };
 
 /* Template parameters of RegisterIdentityBuilder (registerIdentityBuilder.circom:41-52),
@@ -103,6 +106,11 @@ enum {
   PZK_ST_ECDSA_R = 16,    /* ecdsa.circom:81-83 (x1 mod n === r) */
   PZK_ST_PSS_TRAILER = 17,/* rsaPss.circom:73 (assert eM[0] == 188) */
   PZK_ST_PSS_HASH = 18,   /* rsaPss.circom:182,201 (hDash256.out === hash) */
+  PZK_ST_QUERY = 19,      /* comparators.circom:42 ((1 - isEqual.out) * enabled === 0: a selected query bound fails) */
+  PZK_ST_DATE = 20,       /* dateDecoder.circom:22 (encoded === dateEncoded: not a "YYMMDD" digit string) */
+  PZK_ST_CIT_BLACKLIST = 21, /* citizenshipCheck.circom:271 (the citizenship is in the mask) */
+  PZK_ST_CIT_LIST = 22,   /* citizenshipCheck.circom:274 (the citizenship is not in COUNTRY_ARR) */
+  PZK_ST_ISV_ROOT = 23,   /* identityStateVerifier.circom:46 (smtVerifier.isVerified === 1) */
   PZK_ST_INPUT_RANGE = 64 /* an input outside the domain the GPU path evaluates (e.g. a non-bit
                              SHA input, a limb >= 2^64); see DESIGN.md §5 */
 };

@@ -1,0 +1,295 @@
+/* oracle/query.inc.c — QueryIdentity(80) part of the CPU restatement.
+ *
+ * TEST INFRASTRUCTURE ONLY (included by witness_oracle.c; see its header). Restates, in the O0 layout of
+ * DESIGN.md §2, the selective-disclosure circuit
+ *   QueryIdentity(idTreeDepth)         identityManagement/queryIdentity.circom:37-229
+ *   DG1DataExtractor                   identityManagement/dg1DataExtractor.circom:5-97
+ *   IdentityStateVerifier(80)          identityManagement/identityStateVerifier.circom:8-46
+ *   CitizenshipCheck                   identityManagement/citizenshipCheck.circom:6-275
+ *   EncodedDateIsLess / ...Normalized  dateUtilities/dateComparisonEncoded.circom:6-29, dateComparisonEncodedNormalized.circom:13-53
+ *   DateDecoder / DateEncoder / DateIsLess  dateUtilities/dateDecoder.circom:6-23, dateEncoder.circom:4-32, dateComparison.circom:5-58
+ *   GreaterEqThan / LessThan / GreaterThan / ForceEqualIfEnabled  lib/circuits/bitify/comparators.circom:36-91
+ * with main = QueryIdentity(80) {public [eventID .. citizenshipMask]} (the reference declares no main; its
+ * 14 public signals are the inputs declared before the private ones, queryIdentity.circom:51-69, so the
+ * witness order is the declaration order).
+ *
+ * BabyPbk: identityStateVerifier.circom:19 instantiates BabyPbk, which the snapshot does not define (it is
+ * circomlib's, package.json "circomlib": "^2.0.5", not vendored). circomlib's file defines Num2Bits,
+ * Edwards2Montgomery, MontgomeryAdd / Double and Montgomery2Edwards as well, names the reference defines
+ * itself with other signatures (lib/circuits/bitify/bitify.circom, babyjubjub/montogomery.circom), so no
+ * compilable reading of the snapshot exists. This restatement substitutes the reference's own
+ * BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171), which RegisterIdentity uses for the same
+ * key (identity.circom:113-117): Ax, Ay = skIdentity * Base8 either way, so pkIdentityHash, the tree
+ * position and every signal outside that block are the same as with circomlib's template; the block's own
+ * intermediate signals follow the reference's ladder (parity of that block against circomlib: unpinned).
+ */
+
+static const uint32_t QY_COUNTRY[240] = {
+#include "../passport-zk-circuits_amd/data/citizenship_codes.inc"
+};
+
+#define QY_DEPTH 80
+#define QY_NIN 842  /* main inputs */
+
+/* DateEncoder dateEncoder.circom:4-32: encoded | day, month, year | dayDecimals, dayRest, monthDecimals,
+ * monthRest, yearDecimals, yearRest, dayEncoded, monthEncoded, yearEncoded */
+static void run_dateencoder(ctx_t *c, size_t b) {
+  uint64_t v[3] = {small(W(b + 1)), small(W(b + 2)), small(W(b + 3))};  /* day, month, year (< 2^64 here) */
+  fr_t enc[3];
+  for (int k = 0; k < 3; k++) {
+    W(b + 4 + 2 * k) = fr_u64(v[k] / 10);
+    W(b + 5 + 2 * k) = fr_u64(v[k] % 10);
+    enc[k] = fr_add(fr_add(fr_mul(W(b + 4 + 2 * k), fr_u64(256)), W(b + 5 + 2 * k)), fr_u64(12336)); /* 2^4+2^5+2^12+2^13 */
+    W(b + 10 + k) = enc[k];
+  }
+  W(b) = fr_add(fr_add(fr_mul(enc[2], POW2[32]), fr_mul(enc[1], POW2[16])), enc[0]);
+}
+/* DateDecoder dateDecoder.circom:6-23: day, month, year | dateEncoded | DateEncoder (17 signals) */
+static void run_datedecoder(ctx_t *c, size_t b) {
+  const uint64_t e = small(W(b + 3));  /* the nibbles read sit in the low 48 bits */
+  W(b) = fr_u64(((e >> 8) & 15) * 10 + (e & 15));
+  W(b + 1) = fr_u64(((e >> 24) & 15) * 10 + ((e >> 16) & 15));
+  W(b + 2) = fr_u64(((e >> 40) & 15) * 10 + ((e >> 32) & 15));
+  size_t de = b + 4;
+  W(de + 1) = W(b); W(de + 2) = W(b + 1); W(de + 3) = W(b + 2);
+  run_dateencoder(c, de);
+  if (!fr_eq(W(de), W(b + 3)) && !c->err) c->err = S_DATE;
+}
+#define SZ_DATEDEC 17
+/* GreaterThan(L) comparators.circom:72-80: out | in[2] | LessThan(L)(in[1], in[0]) */
+static size_t sz_greaterthan(int L) { return 3 + sz_lessthan(L); }
+static void run_greaterthan(ctx_t *c, size_t b, int L) {
+  size_t lt = b + 3;
+  W(lt + 1) = W(b + 2); W(lt + 2) = W(b + 1);
+  run_lessthan(c, lt, L);
+  W(b) = W(lt);
+}
+/* GreaterEqThan(L) comparators.circom:83-91: out | in[2] | LessThan(L)(in[1], in[0] + 1) */
+static size_t sz_greatereq(int L) { return 3 + sz_lessthan(L); }
+static void run_greatereq(ctx_t *c, size_t b, int L) {
+  size_t lt = b + 3;
+  W(lt + 1) = W(b + 2); W(lt + 2) = fr_add(W(b + 1), ONE());
+  run_lessthan(c, lt, L);
+  W(b) = W(lt);
+}
+/* DateIsLess dateComparison.circom:5-58: out | firstDay, secondDay, firstMonth, secondMonth, firstYear,
+ * secondYear | isYearLess, isMonthLess, isDayLess, isYearEqual, isMonthEqual, isLess1, isLess2, temp, isLess3
+ * | yearLess, monthLess, dayLess (LessThan(8)), yearEqual, monthEqual (IsEqual), greaterThen (GreaterThan(3)) */
+#define SZ_DATEISLESS (16 + 3 * (3 + 19) + 2 * 6 + (3 + 3 + 9))
+static void run_dateisless(ctx_t *c, size_t b) {
+  size_t yl = b + 16, ml = yl + 22, dl = ml + 22, ye = dl + 22, me = ye + 6, gt = me + 6;
+  const int fi[3] = {5, 3, 1};  /* year, month, day: first at b + fi, second at b + fi + 1 */
+  size_t lts[3] = {yl, ml, dl};
+  for (int k = 0; k < 3; k++) {
+    W(lts[k] + 1) = W(b + fi[k]); W(lts[k] + 2) = W(b + fi[k] + 1);
+    run_lessthan(c, lts[k], 8);
+  }
+  W(ye + 1) = W(b + 5); W(ye + 2) = W(b + 6); run_isequal(c, ye);
+  W(me + 1) = W(b + 3); W(me + 2) = W(b + 4); run_isequal(c, me);
+  W(b + 7) = W(yl); W(b + 8) = W(ml); W(b + 9) = W(dl); W(b + 10) = W(ye); W(b + 11) = W(me);
+  W(b + 12) = W(b + 7);
+  W(b + 13) = mulg(W(b + 10), W(b + 8));
+  W(b + 14) = mulg(W(b + 10), W(b + 11));
+  W(b + 15) = mulg(W(b + 14), W(b + 9));
+  W(gt + 1) = fr_add(fr_add(W(b + 12), W(b + 13)), W(b + 15));
+  W(gt + 2) = fr_zero();
+  run_greaterthan(c, gt, 3);
+  W(b) = W(gt);
+}
+/* EncodedDateIsLess dateComparisonEncoded.circom:6-29: out | first, second | firstDateDecoder,
+ * secondDateDecoder, dateIsLess */
+#define SZ_EDIL (3 + 2 * SZ_DATEDEC + SZ_DATEISLESS)
+static void run_edil(ctx_t *c, size_t b) {
+  size_t d1 = b + 3, d2 = d1 + SZ_DATEDEC, dl = d2 + SZ_DATEDEC;
+  W(d1 + 3) = W(b + 1); run_datedecoder(c, d1);
+  W(d2 + 3) = W(b + 2); run_datedecoder(c, d2);
+  W(dl + 1) = W(d1); W(dl + 2) = W(d2);          /* days */
+  W(dl + 3) = W(d1 + 1); W(dl + 4) = W(d2 + 1);  /* months */
+  W(dl + 5) = W(d1 + 2); W(dl + 6) = W(d2 + 2);  /* years */
+  run_dateisless(c, dl);
+  W(b) = W(dl);
+}
+/* EncodedDateIsLessNormalized dateComparisonEncodedNormalized.circom:13-53: out | first, second, currentDate |
+ * CENTURY | firstDateDecoder, secondDateDecoder, firstDateNormalization, secondDateNormalization, dateIsLess */
+#define SZ_EDILN (5 + 2 * SZ_DATEDEC + 2 * SZ_EDIL + SZ_DATEISLESS)
+static void run_ediln(ctx_t *c, size_t b) {
+  size_t d1 = b + 5, d2 = d1 + SZ_DATEDEC, n1 = d2 + SZ_DATEDEC, n2 = n1 + SZ_EDIL, dl = n2 + SZ_EDIL;
+  W(b + 4) = fr_u64(100);
+  W(d1 + 3) = W(b + 1); run_datedecoder(c, d1);
+  W(d2 + 3) = W(b + 2); run_datedecoder(c, d2);
+  W(n1 + 1) = W(b + 1); W(n1 + 2) = W(b + 3); run_edil(c, n1);
+  W(n2 + 1) = W(b + 2); W(n2 + 2) = W(b + 3); run_edil(c, n2);
+  W(dl + 1) = W(d1); W(dl + 2) = W(d2);
+  W(dl + 3) = W(d1 + 1); W(dl + 4) = W(d2 + 1);
+  W(dl + 5) = fr_add(W(d1 + 2), mulg(W(b + 4), W(n1)));
+  W(dl + 6) = fr_add(W(d2 + 2), mulg(W(b + 4), W(n2)));
+  run_dateisless(c, dl);
+  W(b) = W(dl);
+}
+/* ForceEqualIfEnabled comparators.circom:36-43: enabled, in[2] | IsEqual; (1 - isEqual.out) * enabled === 0 */
+#define SZ_FEIE 9
+static void run_feie(ctx_t *c, size_t b, fr_t enabled, fr_t in0, fr_t in1) {
+  W(b) = enabled; W(b + 1) = in0; W(b + 2) = in1;
+  W(b + 4) = in0; W(b + 5) = in1;
+  run_isequal(c, b + 3);
+  if (!fr_is_zero(mulg(fr_sub(ONE(), W(b + 3)), enabled)) && !c->err) c->err = S_QUERY;
+}
+/* DG1DataExtractor dg1DataExtractor.circom:5-97: birthDate, expirationDate, name, nameResidual, nationality,
+ * citizenship, sex, documentNumber | dg1[744] | Bits2Num encoders, in[L-1-i] = dg1[SHIFT + i] */
+static const int QY_DGX_L[8] = {48, 48, 248, 64, 24, 24, 8, 72};
+static const int QY_DGX_SHIFT[8] = {496, 560, 80, 328, 472, 56, 552, 392};
+static size_t sz_dgx(void) {
+  size_t s = 8 + 744;
+  for (int k = 0; k < 8; k++) s += sz_bits2num(QY_DGX_L[k]);
+  return s;
+}
+static void run_dgx(ctx_t *c, size_t b) {
+  size_t p = b + 8 + 744;
+  for (int k = 0; k < 8; k++) {
+    const int L = QY_DGX_L[k];
+    for (int i = 0; i < L; i++) W(p + 1 + L - 1 - i) = W(b + 8 + QY_DGX_SHIFT[k] + i);
+    run_bits2num(c, p, L);
+    W(b + k) = W(p);
+    p += sz_bits2num(L);
+  }
+}
+/* CitizenshipCheck citizenshipCheck.circom:6-275: citizenship, blacklist | validCheck[241], bitmask[240] |
+ * num2bits (Num2Bits(240)), (isEqual[i], isEqual2[i]) i < 240 */
+static size_t sz_citizenship(void) { return 2 + 241 + 240 + sz_num2bits(240) + 240 * 12; }
+static void run_citizenship(ctx_t *c, size_t b) {
+  size_t vc = b + 2, bm = vc + 241, nb = bm + 240, eq = nb + sz_num2bits(240);
+  W(nb + 240) = W(b + 1);
+  run_num2bits(c, nb, 240);
+  W(vc) = fr_zero();
+  for (int i = 0; i < 240; i++) {
+    W(bm + i) = W(nb + 239 - i);
+    size_t e1 = eq + 12 * (size_t)i, e2 = e1 + 6;
+    W(e1 + 1) = fr_u64(QY_COUNTRY[i]); W(e1 + 2) = W(b);
+    run_isequal(c, e1);
+    W(e2 + 1) = ONE(); W(e2 + 2) = W(bm + i);
+    run_isequal(c, e2);
+    if (!fr_is_zero(mulg(W(e1), W(e2))) && !c->err) c->err = S_CIT_BLACKLIST;
+    W(vc + i + 1) = fr_add(W(e1), W(vc + i));
+  }
+  if (!fr_eq(W(vc + 240), ONE()) && !c->err) c->err = S_CIT_LIST;
+}
+/* IdentityStateVerifier(80) identityStateVerifier.circom:8-46: skIdentity, pkPassHash, dgCommit, identityCounter,
+ * timestamp, idStateRoot, idStateSiblings[80] | treePosition | babyPbk (BabyjubjubBase8Multiplication, see the
+ * header), pkIdentityHasher, positionHasher (PoseidonHash(2)), valueHasher (PoseidonHash(3)), smtVerifier */
+static size_t sz_isv(void) {
+  return 6 + QY_DEPTH + 1 + sz_bjjmul() + 2 * sz_poseidon(2) + sz_poseidon(3) + sz_smt(QY_DEPTH);
+}
+static void run_isv(ctx_t *c, size_t b) {
+  size_t bjj = b + 6 + QY_DEPTH + 1, pkh = bjj + sz_bjjmul(), posh = pkh + sz_poseidon(2), valh = posh + sz_poseidon(2),
+         smt = valh + sz_poseidon(3);
+  W(bjj + 2) = W(b);
+  run_bjjmul(c, bjj);
+  W(pkh + 1) = W(bjj); W(pkh + 2) = W(bjj + 1); run_poseidon(c, pkh, 2);
+  W(posh + 1) = W(b + 1); W(posh + 2) = W(pkh); run_poseidon(c, posh, 2);
+  W(b + 6 + QY_DEPTH) = W(posh);
+  W(valh + 1) = W(b + 2); W(valh + 2) = W(b + 3); W(valh + 3) = W(b + 4); run_poseidon(c, valh, 3);
+  /* SMTVerifier: isVerified | root, leaf, key, siblings[80] | ... */
+  W(smt + 1) = W(b + 5); W(smt + 2) = W(valh); W(smt + 3) = W(b + 6 + QY_DEPTH);
+  for (int i = 0; i < QY_DEPTH; i++) W(smt + 4 + i) = W(b + 6 + i);
+  run_smt(c, smt, QY_DEPTH);
+  if (!fr_eq(W(smt), ONE()) && !c->err) c->err = S_ISV_ROOT;
+}
+
+static size_t sz_query_main(void) {
+  return 9 + QY_NIN + 1 + sz_num2bits(18) + sz_dgx() + sz_poseidon(1) + sz_poseidon(3) + 2 * sz_greatereq(64) +
+         2 * sz_lessthan(64) + 8 * SZ_FEIE + 2 * SZ_EDIL + 2 * SZ_EDILN + sz_poseidon(5) + 4 * sz_bits2num(186) +
+         sz_poseidon(1) + sz_isv() + sz_citizenship();
+}
+size_t orc_query_n_inputs(void) { return QY_NIN; }
+size_t orc_query_witness_size(void) {
+  if (!pos_loaded) return 0;
+  orc_init();
+  return 1 + sz_query_main();
+}
+
+/* inputs: 842 x 32 B LE in declaration order (eventID, eventData, idStateRoot, selector, currentDate,
+ * timestampLowerbound, timestampUpperbound, identityCounterLowerbound, identityCounterUpperbound,
+ * birthDateLowerbound, birthDateUpperbound, expirationDateLowerbound, expirationDateUpperbound, citizenshipMask,
+ * skIdentity, pkPassportHash, dg1[744], idStateSiblings[80], timestamp, identityCounter). Returns check-site id. */
+int orc_query_witness(const uint8_t *inputs, uint8_t *wit) {
+  if (!pos_loaded) return -1;
+  orc_init();
+  ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
+  const size_t nW = orc_query_witness_size();
+  memset(wit, 0, nW * 32);
+  W(0) = ONE();
+  const size_t m = 1, in = m + 9;
+  memcpy(&W(in), inputs, QY_NIN * 32);
+  enum { EVID, EVDATA, ROOT, SEL, CUR, TSLO, TSHI, ICLO, ICHI, BDLO, BDHI, EDLO, EDHI, CMASK, SK, PKPASS, DG1,
+         SIB = DG1 + 744, TS = SIB + QY_DEPTH, IC };
+#define IN(k) W(in + (k))
+  W(in + QY_NIN) = mulg(IN(EVDATA), IN(EVDATA));  /* eventDataSquare (queryIdentity.circom:205) */
+  size_t p = in + QY_NIN + 1;
+  /* selectorBits = Num2Bits(18)(selector) */
+  size_t selb = p; p += sz_num2bits(18);
+  W(selb + 18) = IN(SEL);
+  run_num2bits(c, selb, 18);
+#define SEL_BIT(k) W(selb + (k))
+  /* dg1DataExtractor */
+  size_t dgx = p; p += sz_dgx();
+  for (int i = 0; i < 744; i++) W(dgx + 8 + i) = IN(DG1 + i);
+  run_dgx(c, dgx);
+  for (int k = 0; k < 8; k++) W(m + 1 + k) = mulg(W(dgx + k), SEL_BIT(k == 0 ? 1 : k == 1 ? 2 : k <= 3 ? 3 : k));
+  /* nullifier = Poseidon3(sk, Poseidon1(sk), eventID) * selector[0] */
+  size_t skh = p; p += sz_poseidon(1);
+  W(skh + 1) = IN(SK); run_poseidon(c, skh, 1);
+  size_t nul = p; p += sz_poseidon(3);
+  W(nul + 1) = IN(SK); W(nul + 2) = W(skh); W(nul + 3) = IN(EVID); run_poseidon(c, nul, 3);
+  W(m) = mulg(W(nul), SEL_BIT(0));
+  /* timestamp / identity counter bounds: GreaterEqThan(64) / LessThan(64) + ForceEqualIfEnabled */
+  const int cmp_x[4] = {TS, TS, IC, IC}, cmp_y[4] = {TSLO, TSHI, ICLO, ICHI};
+  for (int k = 0; k < 4; k++) {
+    size_t cb = p; p += (k & 1) ? sz_lessthan(64) : sz_greatereq(64);
+    W(cb + 1) = IN(cmp_x[k]); W(cb + 2) = IN(cmp_y[k]);
+    if (k & 1) run_lessthan(c, cb, 64); else run_greatereq(c, cb, 64);
+    size_t fe = p; p += SZ_FEIE;
+    run_feie(c, fe, SEL_BIT(8 + k), W(cb), ONE());
+  }
+  /* expiration date bounds (EncodedDateIsLess), birth date bounds (EncodedDateIsLessNormalized) */
+  for (int k = 0; k < 2; k++) {
+    size_t eb = p; p += SZ_EDIL;
+    W(eb + 1) = k ? W(dgx + 1) : IN(EDLO); W(eb + 2) = k ? IN(EDHI) : W(dgx + 1);
+    run_edil(c, eb);
+    size_t fe = p; p += SZ_FEIE;
+    run_feie(c, fe, SEL_BIT(12 + k), W(eb), ONE());
+  }
+  for (int k = 0; k < 2; k++) {
+    size_t eb = p; p += SZ_EDILN;
+    W(eb + 1) = k ? W(dgx) : IN(BDLO); W(eb + 2) = k ? IN(BDHI) : W(dgx); W(eb + 3) = IN(CUR);
+    run_ediln(c, eb);
+    size_t fe = p; p += SZ_FEIE;
+    run_feie(c, fe, SEL_BIT(14 + k), W(eb), ONE());
+  }
+  /* DG commitment: dg1Hasher = Poseidon5(Bits2Num(186) x 4 of dg1, Poseidon1(sk)); dg1Hasher is created
+   * before dg1Chunking[i] (queryIdentity.circom:192-198) */
+  size_t dgh = p; p += sz_poseidon(5);
+  for (int i = 0; i < 4; i++) {
+    size_t ch = p; p += sz_bits2num(186);
+    for (int j = 0; j < 186; j++) W(ch + 1 + j) = IN(DG1 + i * 186 + j);
+    run_bits2num(c, ch, 186);
+    W(dgh + 1 + i) = W(ch);
+  }
+  size_t skh2 = p; p += sz_poseidon(1);
+  W(skh2 + 1) = IN(SK); run_poseidon(c, skh2, 1);
+  W(dgh + 5) = W(skh2);
+  run_poseidon(c, dgh, 5);
+  /* identityStateVerifier */
+  size_t isv = p; p += sz_isv();
+  W(isv) = IN(SK); W(isv + 1) = IN(PKPASS); W(isv + 2) = W(dgh); W(isv + 3) = IN(IC); W(isv + 4) = IN(TS);
+  W(isv + 5) = IN(ROOT);
+  for (int i = 0; i < QY_DEPTH; i++) W(isv + 6 + i) = IN(SIB + i);
+  run_isv(c, isv);
+  /* citizenshipCheck(dg1DataExtractor.citizenship, citizenshipMask) */
+  size_t cit = p; p += sz_citizenship();
+  W(cit) = W(dgx + 5); W(cit + 1) = IN(CMASK);
+  run_citizenship(c, cit);
+#undef IN
+#undef SEL_BIT
+  if (p != nW) return -2;  /* layout bookkeeping */
+  return c->err;
+}

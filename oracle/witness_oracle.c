@@ -55,6 +55,11 @@ enum {
   S_ECDSA_R = 16,        /* ecdsa.circom:81-83  x1 mod n === r */
   S_PSS_TRAILER = 17,    /* rsaPss.circom:73  assert(eM[0] == 188) */
   S_PSS_HASH = 18,       /* rsaPss.circom:182,201  hDash256.out === hash */
+  S_QUERY = 19,          /* comparators.circom:42  (1 - isEqual.out) * enabled === 0 (QueryIdentity bounds) */
+  S_DATE = 20,           /* dateDecoder.circom:22  dateEncoder.encoded === dateEncoded */
+  S_CIT_BLACKLIST = 21,  /* citizenshipCheck.circom:271  isEqual[i].out * isEqual2[i].out === 0 */
+  S_CIT_LIST = 22,       /* citizenshipCheck.circom:274  validCheck[COUNTRY_COUNT] === 1 */
+  S_ISV_ROOT = 23,       /* identityStateVerifier.circom:46  smtVerifier.isVerified === 1 */
 };
 
 /* ------------------------------------------------------------- fr helpers */
@@ -1899,6 +1904,8 @@ int orc_register_witness(const orc_params *P, const uint8_t *inputs, uint8_t *wi
   W(1) = W(rid); W(3) = W(rid + 1); W(4) = W(rid + 2);
   return c->err;
 }
+
+#include "query.inc.c"
 
 /* ----- standalone circuits for configs 1 and 2 ----- */
 /* config 1: component main = PoseidonHash(n): [1, out, in[n], pEx...] */

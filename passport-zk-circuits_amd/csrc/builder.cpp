@@ -219,6 +219,7 @@ bool build_layout(const pzk_params& p, Layout& L, std::string& why) {
     case PZK_CIRCUIT_SHA384: ok = build_sha512(p, L, why, 384); break;
     case PZK_CIRCUIT_SHA512: ok = build_sha512(p, L, why, 512); break;
     case PZK_CIRCUIT_REGISTER: ok = build_register(p, L, why); break;
+    case PZK_CIRCUIT_QUERY: ok = build_query(p, L, why); break;
     default: why = "unknown circuit family"; return false;
   }
   if (ok && !L.pos.empty()) {

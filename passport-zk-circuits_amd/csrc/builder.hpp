@@ -47,6 +47,8 @@ struct Layout {
   pzk_params params{};
   std::vector<int> out_slots;
   uint32_t rsa_core_words = 0, bjj_core_fr = 0, smt_core_fr = 0;
+  // QueryIdentity(80) (builder_query.cpp, query.hpp)
+  bool is_query = false;
   // ECDSA (SIGNATURE_TYPE 20)
   bool is_ecdsa = false;
   std::vector<uint32_t> ec_prog;      // per-type descriptor programs (ec_walk.hpp)
@@ -57,6 +59,7 @@ struct Layout {
 };
 
 bool build_layout(const pzk_params& p, Layout& L, std::string& why);
+bool build_query(const pzk_params& p, Layout& L, std::string& why);
 
 // chunk size of one emit workgroup (signals)
 constexpr uint32_t EMIT_CHUNK = 4096;

@@ -325,6 +325,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   }
   b.region(RK_ISEQ_ROOT, SZ_ISEQUAL, {IN_ROOT});
   L.reg.v_pkhash = S_PKH; L.reg.v_leaf = S_LEAF; L.reg.v_smt_h = S_H[0];
+  L.reg.v_smt_key = L.reg.v_smt_val = S_PKH;  // SMTVerifier key = leaf = the pubkey hash (passportVerificationBuilder.circom:232-239)
   for (int i = 1; i < 80; i++)
     if (S_H[i] != S_H[0] + i) { why = "internal: SMT hash slots not contiguous"; return false; }
   // signedAttributesHashHasher = PoseidonHash(1)(signedAttributesNum)

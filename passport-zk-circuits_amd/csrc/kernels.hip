@@ -225,7 +225,8 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha512(DevLayout L, const
 // A work item packs up to GEN_PACK signals from up to GEN_MAX_PIECES region slices (most generic
 // regions are a handful of signals: SMT levels, switchers, IsZero blocks). Thread q finds its
 // piece by binary search over the piece prefix sums staged in LDS.
-__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
+template <bool QRY>
+__device__ __forceinline__ void emit_gen_body(const DevLayout& L, const Work* work, const Bufs& B) {
   __shared__ uint32_t cum[GEN_MAX_PIECES];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
       const uint32_t s = p.start + (q - cum[lo]);
       uint32_t rank = 0;
       if (L.keep.bits && !map_keep_lane(L.keep, R.off + s, rank)) continue;
-      val[k] = emit_small(L, B, R, w, s);
+      val[k] = QRY ? query_small(L, B, R, w, s) : emit_small(L, B, R, w, s);
       dst[k] = L.keep.bits ? rank : R.off + s;
     }
   }
@@ -269,6 +270,16 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Wo
       uint4* d = reinterpret_cast<uint4*>(row + 32ull * dst[k]);
       d[0] = val[k].lo; d[1] = val[k].hi;
     }
+}
+
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
+  emit_gen_body<false>(L, work, B);
+}
+// QueryIdentity's small regions (query.hpp): the same packed emitter with its own element function, so
+// k_emit_gen keeps its register budget (one kernel for both took 192 VGPRs and 208 B of scratch per lane,
+// against 112 and none)
+__global__ void __launch_bounds__(EMIT_THREADS) k_emit_qry(DevLayout L, const Work* work, Bufs B) {
+  emit_gen_body<true>(L, work, B);
 }
 
 // ------------------------------------------------------------------- signal map (.sym) gather
@@ -329,6 +340,11 @@ hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t
   return hipGetLastError();
 }
 
+hipError_t launch_qry_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, int32_t* status, hipStream_t st) {
+  hipLaunchKernelGGL(k_qry_prep, dim3(vs.batch), dim3(64), 0, st, L, inputs, vs, status);
+  return hipGetLastError();
+}
+
 hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core,
                             const uint64_t* rsa_core, int32_t* status, uint32_t batch, hipStream_t st) {
   if (!status) return hipSuccess;
@@ -360,9 +376,9 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 }
 
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
-                            ValueStore vs, fr* pos_core, fr* smt_core, hipStream_t st) {
+                            ValueStore vs, fr* pos_core, fr* smt_core, int32_t* status, hipStream_t st) {
   hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
-                     smt_core, vs.batch);
+                     smt_core, status, vs.batch);
   return hipGetLastError();
 }
 
@@ -382,6 +398,7 @@ hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32
   dim3 g(n_work, batch), blk(EMIT_THREADS);
   switch (emitter) {
     case E_GEN: case E_GENR: hipLaunchKernelGGL(k_emit_gen, g, blk, 0, st, L, work, B); break;
+    case E_QRY: hipLaunchKernelGGL(k_emit_qry, g, blk, 0, st, L, work, B); break;
     case E_SHA: case E_SHAD:  // witness-major grid (see k_emit_sha)
     {  // PZK_SHA_U (8 / 16 / 32): prefetch depth, for tuning runs
       static const int u = getenv("PZK_SHA_U") ? atoi(getenv("PZK_SHA_U")) : 16;

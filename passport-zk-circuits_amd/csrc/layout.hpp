@@ -15,7 +15,8 @@ namespace pzk {
 constexpr int32_t ST_NUM2BITS = 1, ST_ALIAS = 2, ST_ISZERO = 3, ST_FLOW = 7, ST_RSA_HASH = 8,
                   ST_RSA_PREFIX = 9, ST_RSA_PAD = 10, ST_BIGMOD_GT = 11, ST_BIGISZERO = 12,
                   ST_SMT_LAST = 13, ST_ECDSA_INV = 15, ST_ECDSA_R = 16, ST_PSS_TRAILER = 17,
-                  ST_PSS_HASH = 18, ST_INPUT_RANGE = 64;
+                  ST_PSS_HASH = 18, ST_QUERY = 19, ST_DATE = 20, ST_CIT_BLACKLIST = 21, ST_CIT_LIST = 22,
+                  ST_ISV_ROOT = 23, ST_INPUT_RANGE = 64;
 
 // ---- emit regions: a contiguous run of witness signals with one closed-form generator
 enum RegionKind : uint32_t {
@@ -75,6 +76,15 @@ enum RegionKind : uint32_t {
   RK_SHA5_OWN = 47,   // [ShaHashChunks out[O] | in[1024B] (a4 = 1)] Sha384/512HashChunks out[O] | in[1024B] | states | iv;
                       // a0 = sha slot, a1 = blocks, a2 = input offset, a3 = O
   RK_SHA5_BLOCK = 48, // Sha2_384_512Schedule + Sha2_384_512Rounds(80) of one block; a0 = sha slot, a1 = block
+  // ---- QueryIdentity(80) (identityManagement/queryIdentity.circom; query.hpp), all from the input row + value store
+  RK_Q_OUT = 49,      // main outputs: nullifier, birthDate .. documentNumber (selector-masked)
+  RK_Q_SQ = 50,       // eventDataSquare
+  RK_Q_CMP = 51,      // GreaterEqThan(64) / LessThan(64) block a0 = 0..3 (timestamp / identity counter bounds)
+  RK_Q_FEIE = 52,     // ForceEqualIfEnabled block a0 = 0..7 (condition a0, enabled = selector bit 8 + a0)
+  RK_Q_EDIL = 53,     // EncodedDateIsLess block a0 = 0 (expirationDateLowerbound, exp) / 1 (exp, expirationDateUpperbound)
+  RK_Q_EDILN = 54,    // EncodedDateIsLessNormalized block a0 = 0 (birthDateLowerbound, birth) / 1 (birth, birthDateUpperbound)
+  RK_Q_CIT = 55,      // CitizenshipCheck own: citizenship, blacklist | validCheck[241], bitmask[240]
+  RK_Q_CITEQ = 56,    // CitizenshipCheck (isEqual[i], isEqual2[i]) i < 240
   RK_COUNT
 };
 
@@ -85,7 +95,8 @@ enum RegionKind : uint32_t {
 // E_SHAD = SHA regions of hashers fed by derived messages (RSA-PSS MGF1 / M'), emitted after the PSS chain
 // E_SHA1 = SHA-1 hasher regions (k_emit_sha1); E_SHA5 = SHA-384/512 hasher regions (k_emit_sha512); E_SHA5D = the
 // SHA-384 hashers of derived messages (RSA-PSS SHA-384 MGF1 / M'), emitted after the PSS chain like E_SHAD
-enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_SHA5D, E_ECR, E_COUNT };
+// E_QRY = QueryIdentity's small regions (k_emit_qry, query.hpp)
+enum Emitter { E_GEN = 0, E_SHA, E_POS, E_BITS, E_FLOW, E_MM, E_BJJ, E_GENR, E_ECT, E_SHAD, E_SHA1, E_SHA5, E_SHA5D, E_ECR, E_QRY, E_COUNT };
 __host__ __device__ inline int emitter_of(uint32_t kind) {
   switch (kind) {
     case RK_SHA_OWN: case RK_SHA_BLOCK: return E_SHA;
@@ -99,13 +110,15 @@ __host__ __device__ inline int emitter_of(uint32_t kind) {
     case RK_RSA_OUT: return E_GENR;
     case RK_ECT: return E_ECT;
     case RK_EC_GM_RCC: case RK_EC_GM_EQ: case RK_EC_GM_SUM: return E_ECR;
+    case RK_Q_OUT: case RK_Q_SQ: case RK_Q_CMP: case RK_Q_FEIE: case RK_Q_EDIL: case RK_Q_EDILN: case RK_Q_CIT:
+    case RK_Q_CITEQ: return E_QRY;
     default: return kind >= RK_EC_U64 && kind <= RK_PSS_XOR ? E_GENR : E_GEN;
   }
 }
 // regions whose emit workgroup needs the whole region (LDS pre-pass over all of it)
 __host__ __device__ inline bool emitter_whole(int e) { return e == E_POS || e == E_BITS || e == E_FLOW; }
 // emitters whose work items pack many small regions (Work.region = first GenPiece, Work.pad = pieces)
-__host__ __device__ inline bool emitter_packed(int e) { return e == E_GEN || e == E_GENR; }
+__host__ __device__ inline bool emitter_packed(int e) { return e == E_GEN || e == E_GENR || e == E_QRY; }
 
 constexpr int REGION_ARGS = 10;
 struct Region {
@@ -185,6 +198,12 @@ struct RegInfo {
   int32_t pss_s8;                  // RSA-PSS salt bits (0: not PSS)
   int32_t pss_h;                   // RSA-PSS hash bits (256 or 384)
   int32_t j_mgf, n_mgf, j_hd;      // RSA-PSS SHA jobs: MGF1 blocks [j_mgf, j_mgf + n_mgf), M' hasher
+  // SMTVerifier key / value slots (RegisterIdentityBuilder: both the pubkey hash; QueryIdentity: treePosition and
+  // the identity-state value hash); smt_check: isVerified === 1 is a constraint (identityStateVerifier.circom:46)
+  int32_t v_smt_key, v_smt_val, smt_check;
+  // QueryIdentity: first of the 8 DG1DataExtractor outputs, first of the 240 CitizenshipCheck IsEqual inverses
+  // (Montgomery), the citizenship's index in COUNTRY_ARR (raw u32 in limb 0; 240 = absent), the nullifier hash
+  int32_t q_dgf, q_cinv, q_cidx, q_nul;
 };
 
 // per-witness core sizes of the register-circuit kernels

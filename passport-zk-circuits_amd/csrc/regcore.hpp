@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;
   uint32_t* flags = reinterpret_cast<uint32_t*>(core + 2 * SMT_LEVELS);
-  const fr key = fr_from_mont(vs.at(R.v_pkhash, w));
+  const fr key = fr_from_mont(vs.at(R.v_smt_key, w));
   // inverses of the siblings (SMTLevIns isZero, SMTVerifier.circom:47-50), batched
   fr sm[NL];
   uint32_t zmask = 0;  // bit k: sibling i0 + k is zero
@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 // read the lane's own stores, and the hash comes back to every lane of the group by its butterfly.
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
-                                                 ValueStore vs, fr* pos_core, fr* smt_core, uint32_t batch) {
+                                                 ValueStore vs, fr* pos_core, fr* smt_core, int32_t* status, uint32_t batch) {
   core_priority();
   constexpr int G = SMT_CHAIN_LANES;
   static_assert(G == 4 && 64 % G == 0, "PoseidonHash(2) groups are 4 lanes (t = 3)");
@@ -749,6 +749,9 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
   fr rin = fr_to_mont(load_fr(row + 32ull * R.in_root));
   fr dlt = fr_sub(rin, roots[0]);
   core[3 * SMT_LEVELS + 1] = fr_inv(dlt);
+  // smtVerifier.isVerified === 1 where the circuit asserts it (identityStateVerifier.circom:46; the register
+  // circuit leaves it commented out, passportVerificationBuilder.circom:240)
+  if (R.smt_check && !fr_is_zero(dlt)) set_status(status ? status + w : nullptr, ST_ISV_ROOT);
 }
 #endif
 

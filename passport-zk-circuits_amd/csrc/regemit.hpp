@@ -14,6 +14,7 @@
 #include "ec_emit.hpp"
 #include "pss.hpp"
 #include "mapsink.hpp"
+#include "query.hpp"
 
 namespace pzk {
 
@@ -109,12 +110,13 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
         fr r0 = fr_from_mont_fast(smt[SMT_LEVELS]);
         return el_u64(fr_eq(r0, load_fr(row + 32ull * R.a[0])) ? 1 : 0);
       } else if (s == 1) return el_load(row + 32ull * R.a[0]);
-      else if (s == 2 || s == 3 || s == 84) return el_fr(V(G.v_pkhash));
+      else if (s == 3) return el_fr(V(G.v_smt_key));
+      else if (s == 2 || s == 84) return el_fr(V(G.v_smt_val));
       else return el_load(row + 32ull * (R.a[1] + s - 4));
     }
     case RK_SMTHASH: {
       int lv = R.a[0];
-      if (lv < 0) return el_fr(s == 0 ? V(G.v_leaf) : V(G.v_pkhash));
+      if (lv < 0) return el_fr(s == 0 ? V(G.v_leaf) : s == 1 ? V(G.v_smt_key) : V(G.v_smt_val));
       else return el_fr(s == 0 ? V(G.v_smt_h + lv) : V(G.v_smt_lr + 2 * lv + (int)s - 1));
     }
     case RK_LEVINS: {  // levIns[80] | siblings[80] | done[79] | isZero[80] (out, in, inv)

@@ -33,21 +33,23 @@ int api_fail(int code, const std::string& msg) { return fail(code, msg); }  // p
 enum Phase {
   PH_LOAD, PH_SHA_CORE, PH_PREP, PH_RSA_CORE, PH_BJJ_CORE, PH_POS_CORE, PH_SMT,
   PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS, PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ,
-  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_PSS, PH_EMIT_ECR, PH_COUNT
+  PH_EC_CORE, PH_EC_TABLE, PH_EMIT_ECT, PH_PSS, PH_EMIT_ECR, PH_EMIT_QRY, PH_COUNT
 };
 static const char* PHASE_NAMES[PH_COUNT] = {"load_values", "sha_core", "prep",     "rsa_core",  "bjj_core",
                                             "pos_core",    "smt",      "emit_gen", "emit_sha",  "emit_pos",
                                             "emit_bits",   "emit_flow", "emit_mm", "emit_bjj",
-                                            "ec_core",     "ec_table",  "emit_ect", "pss",       "emit_ecr"};
+                                            "ec_core",     "ec_table",  "emit_ect", "pss",       "emit_ecr",
+                                            "emit_qry"};
 static const char* PHASE_KERNELS[PH_COUNT] = {"k_load_values", "k_sha_core",  "k_prep",      "k_rsa_core",
                                               "k_bjj_core",    "k_pos_core",  "k_smt_prep+k_smt_chain",
                                               "k_emit_gen",    "k_emit_sha",  "k_emit_pos",  "k_emit_bits",
                                               "k_emit_flow",   "k_emit_mm",   "k_emit_bjj",
                                               "k_ec_core",     "k_ec_table",  "k_emit_ect",
-                                              "k_pss_mgf+k_sha_core+k_pss_mdash", "k_emit_ecr"};
+                                              "k_pss_mgf+k_sha_core+k_pss_mdash", "k_emit_ecr", "k_emit_qry"};
 static const int EMIT_PHASE[E_COUNT] = {PH_EMIT_GEN, PH_EMIT_SHA, PH_EMIT_POS, PH_EMIT_BITS,
                                         PH_EMIT_FLOW, PH_EMIT_MM, PH_EMIT_BJJ, PH_EMIT_GEN, PH_EMIT_ECT,
-                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_ECR};
+                                        PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_SHA, PH_EMIT_ECR,
+                                        PH_EMIT_QRY};
 
 // Per-phase HIP-event timing. A phase may be bracketed several times per batch (e.g. Poseidon
 // levels before and after the SMT prep); its time is the sum of its brackets, each bracket
@@ -397,8 +399,9 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   if (!rc) rc = upload(&I->d_sha, I->lay.sha);
   if (!rc) rc = upload(&I->d_pos, I->lay.pos);
   if (!rc) rc = upload(&I->d_loads, I->lay.loads);
-  if (!rc && I->lay.is_register) rc = upload(&I->d_level_task, level_task);
-  if (!rc && I->lay.is_register) {
+  const bool chains = I->lay.is_register || I->lay.is_query;  // SMT / BabyJubJub chains
+  if (!rc && chains) rc = upload(&I->d_level_task, level_task);
+  if (!rc && chains) {
     if (hipMalloc(&I->d_bjj_table, sizeof(fr) * 3 * BJJ_TABLE_WINDOWS * 256) != hipSuccess ||
         launch_bjj_table(I->d_bjj_table, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
       rc = fail(PZK_E_HIP, "BabyJubJub table setup failed");
@@ -420,6 +423,10 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
                 launch_inv_small(I->d_inv_small, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
       rc = fail(PZK_E_HIP, "ECDSA constant setup failed");
   }
+  if (!rc && I->lay.is_query &&
+      (hipMalloc(&I->d_inv_small, sizeof(fr) * 256) != hipSuccess ||
+       launch_inv_small(I->d_inv_small, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+    rc = fail(PZK_E_HIP, "QueryIdentity constant setup failed");
   if (rc) { free_all(I); delete I; return rc; }
   // The dependency chains (main stream: Poseidon/SMT/BJJ cores; s_rsa: RSA core) get the
   // highest queue priority, the bulk SHA emitter the lowest: when the chip is full of emitter
@@ -627,7 +634,7 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
       {(void**)&S.d_rsa_core, 8ull * L.rsa_core_words * batch},
       {(void**)&S.d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
       {(void**)&S.d_bjj_core, 32ull * L.bjj_core_fr * batch},
-      {(void**)&S.d_bjj_scratch, L.is_register ? 32ull * BJJ_SCRATCH_FR * batch : 0},
+      {(void**)&S.d_bjj_scratch, (L.is_register || L.is_query) ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&S.d_smt_core, 32ull * L.smt_core_fr * batch},
       {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].core_words * batch : 0},
       {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].jac_words * batch : 0},
@@ -713,7 +720,30 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
     HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, S.d_values, B, st)); }
-  if (!lay.is_register) {
+  if (lay.is_query) {
+    // QueryIdentity(80) (query.hpp): one chain on the main stream — prep, the BabyJubJub key, Poseidon levels
+    // 0-3 (sk hashes, nullifier, dg1 commitment, pk / position / value hashes), the SMT prep (needs the tree
+    // position), levels 4-5 (the new-leaf hash and the level hashes above the insertion level), the SMT chain;
+    // then the emitters on the two emitter streams
+    { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_qry_prep(L, d_inputs, vs, d_status, st)); }
+    { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
+      HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
+    HIPCHK(hipEventRecord(I->ev_bjj, st));
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
+    if ((rc = emit(E_BJJ, s_sha))) return rc;
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 4))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st);
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, d_status, st)); }
+    HIPCHK(hipEventRecord(I->ev_pos, st));
+    HIPCHK(hipStreamWaitEvent(s_emit, I->ev_pos, 0));
+    if ((rc = emit(E_POS, s_emit))) return rc;
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_pos, 0));
+    if ((rc = emit(E_GEN, s_sha))) return rc;
+    if ((rc = emit(E_QRY, s_sha))) return rc;
+    if ((rc = emit(E_BITS, s_sha))) return rc;  // Num2Bits(254) of the tree position reads level 3
+  } else if (!lay.is_register) {
     { PhaseScope ps(T, slot, PH_SHA_CORE, st);
       HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, 0, L.n_sha, S.d_sha_core, d_status, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
@@ -791,7 +821,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, st)); }
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
     HIPCHK(hipEventRecord(I->ev_bjj, st));

@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("PZK_LIB") or os.path.join(PKG, "lib", "libpzkwit.so")
 
 PZK_CIRCUIT_REGISTER, PZK_CIRCUIT_POSEIDON, PZK_CIRCUIT_SHA256, PZK_CIRCUIT_SHA1 = 0, 1, 2, 3
-PZK_CIRCUIT_SHA384, PZK_CIRCUIT_SHA512 = 4, 5
+PZK_CIRCUIT_SHA384, PZK_CIRCUIT_SHA512, PZK_CIRCUIT_QUERY = 4, 5, 6
 PZK_EXEC_SYNC = 1
 
 # C-ABI entry points declared in include/pzkwit.h and include/pzkpassport.h (checked by tests/test_capi.py)

@@ -1,0 +1,61 @@
+"""QueryIdentity(80) on the GPU: every element of every witness bit-exact against the
+CPU oracle (oracle/query.inc.c), lane statuses equal to the oracle's check sites, and a full 4096-witness
+batch with its public outputs checked against independent math."""
+import numpy as np
+import pytest
+
+from pzkwit import native, query as Q
+from pzkwit.field import SplitMix64
+
+from test_query import FAIL_KINDS, _fail_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def inst():
+    return native.Instance(native.PZK_CIRCUIT_QUERY, 80)
+
+
+def _compare(oracle, rows, wit, st, codes):
+    for b in range(rows.shape[0]):
+        rc, ref = oracle.query_witness(rows[b])
+        assert rc == codes[b] == st[b], (b, rc, codes[b], st[b])
+        bad = np.nonzero((ref != wit[b]).any(axis=1))[0]
+        assert bad.size == 0, "row %d: %d mismatching signals, first %d" % (b, bad.size, bad[0])
+
+
+def test_query_matches_oracle(oracle, inst):
+    assert inst.witness_size == oracle.query_sizes()[1] and inst.n_inputs == Q.N_INPUTS
+    rng = SplitMix64(0x5151)
+    rows, codes = [], []
+    for k in range(40):
+        sel = [0, (1 << 18) - 1, None, None][k % 4]
+        depth = [0, 1, 79, 40, None][k % 5]
+        inp, _ = Q.make_query(rng, selector=sel, depth=depth)
+        rows.append(Q.pack(inp))
+        codes.append(0)
+    for i, kind in enumerate(FAIL_KINDS):  # one failing lane per check site, between valid ones
+        inp, code = _fail_case(kind, SplitMix64(0x77 + i))
+        rows.insert(3 * i + 1, Q.pack(inp))
+        codes.insert(3 * i + 1, code)
+    rows = np.stack(rows)
+    wit, st = inst.witness_batch_host(rows)
+    _compare(oracle, rows, wit, st, codes)
+
+
+def test_query_full_batch(oracle, inst):
+    """4096 witnesses (64 distinct queries tiled) in one call: every lane passes, every lane's public outputs
+    equal independent math, repeated rows are identical, and rows at the batch edges equal the oracle."""
+    rng = SplitMix64(0x4096)
+    uniq = [Q.make_query(rng) for _ in range(64)]
+    rows = np.stack([Q.pack(inp) for inp, _ in uniq])
+    batch = np.concatenate([rows] * 64)
+    wit, st = inst.witness_batch_host(batch)
+    assert (st == 0).all()
+    for i in range(4096):
+        inp, info = uniq[i % 64]
+        got = [int.from_bytes(wit[i, 1 + k].tobytes(), "little") for k in range(9)]
+        assert got == Q.public_outputs(inp, info), i
+    assert (wit[:64] == wit[4032:]).all()
+    _compare(oracle, batch[[0, 63, 4095]], wit[[0, 63, 4095]], st[[0, 63, 4095]], [0, 0, 0])

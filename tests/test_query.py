@@ -1,0 +1,91 @@
+"""QueryIdentity(80) on the CPU: the oracle restatement (oracle/query.inc.c) against
+independent math on generated queries, its check sites, and the host layout (builder_query.cpp) against the
+oracle's sizes. No device is needed."""
+import numpy as np
+import pytest
+
+from pzkwit import native, query as Q
+from pzkwit.field import P, SplitMix64, poseidon
+
+
+def test_layout_matches_oracle_sizes(oracle):
+    nin, nw = oracle.query_sizes()
+    assert nin == Q.N_INPUTS == native.layout_inputs({}, circuit=native.PZK_CIRCUIT_QUERY)
+    assert nw == native.layout_witness_size({}, circuit=native.PZK_CIRCUIT_QUERY) == 141169
+    with pytest.raises(native.PzkError):
+        native.layout_info({"size_arg": 40}, circuit=native.PZK_CIRCUIT_QUERY)
+
+
+def test_country_table_is_the_packed_alpha3_codes():
+    C = Q.countries()
+    assert len(set(C)) == 240 and C[0] == int.from_bytes(b"ABW", "big") and C[-1] == int.from_bytes(b"ZWE", "big")
+    assert C == sorted(C)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_valid_queries_pass_and_outputs_match_math(oracle, seed):
+    rng = SplitMix64(0x51 + seed)
+    for k in range(4):
+        sel = [0, (1 << 18) - 1, None, 1 | (1 << 5)][k]
+        inp, info = Q.make_query(rng, selector=sel, depth=[0, 1, 79, None][k])
+        rc, w = oracle.query_witness(Q.pack(inp))
+        assert rc == 0
+        got = [oracle.from_elem(w[1 + i]) for i in range(9)]
+        assert got == Q.public_outputs(inp, info)
+        # independent recomputations: BabyJubJub key, nullifier, the identity-state SMT root
+        ax, ay = info["pk_identity"]
+        assert (ax * ax * Q.A_BJJ + ay * ay - 1 - Q.D_BJJ * ax * ax * ay * ay) % P == 0
+        assert info["nullifier"] == poseidon([inp["skIdentity"], poseidon([inp["skIdentity"]]), inp["eventID"]])
+        assert w[0, 0] == 1 and (w[0, 1:] == 0).all()
+        # main inputs are copied after the 9 outputs, eventDataSquare after them
+        assert (w[10:10 + 842] == Q.pack(inp)).all()
+        assert oracle.from_elem(w[852]) == inp["eventData"] ** 2 % P
+
+
+def _fail_case(kind, rng):
+    if kind == "bound":        # selected timestamp lower bound above the timestamp
+        inp, _ = Q.make_query(rng, selector=1 << 8)
+        inp["timestampLowerbound"] = inp["timestamp"] + 5
+        return inp, 19
+    if kind == "date":         # expirationDateLowerbound not a digit string ("24A101"), its check not selected
+        inp, _ = Q.make_query(rng, selector=0)
+        inp["expirationDateLowerbound"] = int.from_bytes(b"24A101", "big")
+        return inp, 20
+    if kind == "blacklist":
+        inp, info = Q.make_query(rng, selector=0)
+        inp["citizenshipMask"] |= 1 << (239 - info["citizenship_index"])
+        return inp, 21
+    if kind == "unlisted":
+        inp, _ = Q.make_query(rng, selector=0, cit_code=b"XXX")
+        return inp, 22
+    if kind == "root":
+        inp, _ = Q.make_query(rng, selector=0)
+        inp["idStateRoot"] = (inp["idStateRoot"] + 1) % P
+        return inp, 23
+    if kind == "smt_last":     # a non-zero last sibling (SMTVerifier.circom:54) before the root check
+        inp, _ = Q.make_query(rng, selector=0, depth=3)
+        inp["idStateSiblings"][79] = 7
+        return inp, 13
+    if kind == "selector":     # selector >= 2^18: Num2Bits(18)
+        inp, _ = Q.make_query(rng, selector=0)
+        inp["selector"] = 1 << 20
+        return inp, 1
+    raise ValueError(kind)
+
+
+FAIL_KINDS = ["bound", "date", "blacklist", "unlisted", "root", "smt_last", "selector"]
+
+
+@pytest.mark.parametrize("kind", FAIL_KINDS)
+def test_check_sites(oracle, kind):
+    inp, code = _fail_case(kind, SplitMix64(0x77 + FAIL_KINDS.index(kind)))
+    rc, _ = oracle.query_witness(Q.pack(inp))
+    assert rc == code
+
+
+def test_unselected_bounds_do_not_fail(oracle):
+    rng = SplitMix64(0x99)
+    inp, _ = Q.make_query(rng, selector=(1 << 18) - 1 - (1 << 8))
+    inp["timestampLowerbound"] = inp["timestamp"] + 5
+    rc, w = oracle.query_witness(Q.pack(inp))
+    assert rc == 0

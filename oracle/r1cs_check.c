@@ -2424,6 +2424,8 @@ static size_t ck_builder(ck_t *c, size_t b, const ck_params *P) {
   return o - b;
 }
 
+#include "r1cs_query.inc.c"
+
 /* ============================================================ entry points */
 static int ck_ready = 0;
 static void ck_init(void) {
@@ -2516,5 +2518,14 @@ int ck_sha512(int B, int O, const uint8_t *wit, size_t n, ck_report *r) {
 int ck_sha1(int B, const uint8_t *wit, size_t n, ck_report *r) {
   ck_t c = ck_begin(wit, n);
   size_t walked = 1 + ck_sha1chunks(&c, 1, B);
+  return ck_end(&c, walked, r);
+}
+
+/* QueryIdentity(80) as main (oracle/r1cs_query.inc.c) */
+int ck_query(const uint8_t *wit, size_t nw, ck_report *r) {
+  if (!pos_loaded) return -1;
+  ck_t c = ck_begin(wit, nw);
+  size_t walked = 1 + ck_queryid(&c, 1);
+  req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);
   return ck_end(&c, walked, r);
 }

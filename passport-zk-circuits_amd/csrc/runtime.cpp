@@ -673,7 +673,18 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   if (rc) return rc;
   I->calls++;
   hipStream_t user = (exec && exec->stream) ? (hipStream_t)exec->stream : nullptr;
+  // PZK_SERIAL=1 (profiling): every phase on the main stream, so kernel times are standalone
+  static const bool serial = getenv("PZK_SERIAL") != nullptr;
+  // QueryIdentity: the whole per-call chain (prep .. SMT chain) is one latency-bound dependency chain whose
+  // length is the SMT proof depth (k_smt_chain: 0.5 ms per level for 4096 witnesses, one wave per CU), so
+  // consecutive calls rotate over PZK_QRY_CHAINS (1 / 2 / 3) chain streams — the two high-priority streams,
+  // then the fifth stream — and their chains run side by side
+  static const int qry_chains = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 2;
   hipStream_t st = I->stream;
+  if (I->lay.is_query && !serial && qry_chains > 1) {
+    const int c = qry_chains >= 3 ? set : set & 1;  // NSETS = 3 calls in flight
+    st = c == 0 ? I->stream : c == 1 ? I->s_rsa : I->s_tail;
+  }
   for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(st, e, 0));
   if (user) {
     HIPCHK(hipEventRecord(I->ev_entry, user));
@@ -713,15 +724,13 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     return 0;
   };
-  // PZK_SERIAL=1 (profiling): every phase on the main stream, so kernel times are standalone
-  static const bool serial = getenv("PZK_SERIAL") != nullptr;
   hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha, s_emit = serial ? st : I->s_emit,
               s_own = serial ? st : I->s_tail;
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
     HIPCHK(launch_load_values(I->d_loads, (int)lay.loads.size(), d_inputs, lay.n_inputs, S.d_values, B, st)); }
   if (lay.is_query) {
-    // QueryIdentity(80) (query.hpp): one chain on the main stream — prep, the BabyJubJub key, Poseidon levels
+    // QueryIdentity(80) (query.hpp): one chain on the call's chain stream — prep, the BabyJubJub key, Poseidon levels
     // 0-3 (sk hashes, nullifier, dg1 commitment, pk / position / value hashes), the SMT prep (needs the tree
     // position), levels 4-5 (the new-leaf hash and the level hashes above the insertion level), the SMT chain;
     // then the emitters on the two emitter streams

@@ -59,3 +59,17 @@ def test_query_full_batch(oracle, inst):
         assert got == Q.public_outputs(inp, info), i
     assert (wit[:64] == wit[4032:]).all()
     _compare(oracle, batch[[0, 63, 4095]], wit[[0, 63, 4095]], st[[0, 63, 4095]], [0, 0, 0])
+
+
+def test_query_device_witnesses_satisfy_constraints(inst):
+    """Device witnesses through the independent constraint checker (oracle/r1cs_query.inc.c): 140,542
+    constraints hold and every signal is read by one."""
+    import pyr1cs
+    rng = SplitMix64(0xC1)
+    rows = np.stack([Q.pack(Q.make_query(rng, selector=s, depth=d)[0])
+                     for s, d in ((0, 0), ((1 << 18) - 1, 79), (None, 40), (None, None))])
+    wit, st = inst.witness_batch_host(rows)
+    assert (st == 0).all()
+    for b in range(rows.shape[0]):
+        rc, rep = pyr1cs.check_query(wit[b])
+        assert rc == 0 and rep["n_failed"] == 0 and rep["n_uncovered"] == 0, (b, rep)

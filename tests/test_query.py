@@ -89,3 +89,37 @@ def test_unselected_bounds_do_not_fail(oracle):
     inp["timestampLowerbound"] = inp["timestamp"] + 5
     rc, w = oracle.query_witness(Q.pack(inp))
     assert rc == 0
+
+
+# the constraint that each check site violates (template, reference line), as the checker names it
+FAIL_CONSTRAINT = {"bound": ("ForceEqualIfEnabled", 42), "date": ("DateDecoder", 22),
+                   "blacklist": ("CitizenshipCheck", 271), "unlisted": ("CitizenshipCheck", 274),
+                   "root": ("IdentityStateVerifier", 46), "smt_last": ("SMTLevIns", None), "selector": ("Num2Bits", 26)}
+
+
+def test_constraints_hold_on_oracle_witnesses(oracle):
+    """The independent constraint checker (oracle/r1cs_query.inc.c, restated from the .circom constraints, never
+    computing a witness) accepts oracle witnesses: every constraint holds and every signal is read by one."""
+    import pyr1cs
+    rng = SplitMix64(0xC0)
+    for sel, depth in ((0, 0), ((1 << 18) - 1, 79), (None, None)):
+        inp, _ = Q.make_query(rng, selector=sel, depth=depth)
+        rc, w = oracle.query_witness(Q.pack(inp))
+        assert rc == 0
+        crc, rep = pyr1cs.check_query(w)
+        assert crc == 0 and rep["n_failed"] == 0 and rep["n_uncovered"] == 0, rep
+        assert rep["size_walked"] == w.shape[0] and rep["n_constraints"] == 140542
+
+
+@pytest.mark.parametrize("kind", FAIL_KINDS)
+def test_checker_names_the_failing_constraint(oracle, kind):
+    import pyr1cs
+    inp, code = _fail_case(kind, SplitMix64(0x77 + FAIL_KINDS.index(kind)))
+    rc, w = oracle.query_witness(Q.pack(inp))
+    assert rc == code
+    crc, rep = pyr1cs.check_query(w)
+    assert crc == 1 and rep["n_failed"] >= 1
+    tmpl, line = FAIL_CONSTRAINT[kind]
+    assert rep["first_template"].startswith(tmpl), rep
+    if line is not None:
+        assert rep["first_line"] == line, rep

@@ -155,17 +155,21 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
     fr a = act ? fr_add(pow5(st), K.C(t, (r + 1) * t + jj)) : fr_zero();
     st = mix(a, r == 3);
   }
-  for (int r = 0; r < RP; r++) {  // partial rounds
+  for (int r = 0; r < RP; r++) {  // partial rounds: 4 product times per round (was 5)
     if (act) out[o + j] = st;
     o += t;
-    fr s0 = fr_zero();
-    if (j == 0) s0 = fr_add(pow5(st), K.C(t, 5 * t + r));
-    s0 = fr_shfl(s0, gb, 64);
     const int sb = (2 * t - 1) * r;
-    fr term = act ? fr_mul(K.S(t, sb + jj), j == 0 ? s0 : st) : fr_zero();
-    fr sum = group_sum(term);
+    // one product on every lane: lane 0 squares its state (the S-box's first step), lanes 1..t-1 take their
+    // sparse-matrix terms S[k] * st_k, which do not depend on the S-box
+    const fr p = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
+    fr s0 = fr_zero();
+    if (j == 0) s0 = fr_add(fr_mul(fr_sqr(p), st), K.C(t, 5 * t + r));
+    s0 = fr_shfl(s0, gb, 64);
+    // one product on every lane: lane 0's term S[0] * s0, the others' updates s0 * S'[k]
+    const fr q = fr_mul(j == 0 ? K.S(t, sb) : K.S(t, sb + t + jj - 1), s0);
+    const fr sum = group_sum(j == 0 ? q : act ? p : fr_zero());
     if (j == 0) st = sum;
-    else if (act) st = fr_add(st, fr_mul(s0, K.S(t, sb + t + j - 1)));
+    else if (act) st = fr_add(st, q);
   }
   for (int r = 0; r < 3; r++) {  // full rounds 4..6
     if (act) out[o + j] = st;

@@ -73,3 +73,15 @@ def test_query_device_witnesses_satisfy_constraints(inst):
     for b in range(rows.shape[0]):
         rc, rep = pyr1cs.check_query(wit[b])
         assert rc == 0 and rep["n_failed"] == 0 and rep["n_uncovered"] == 0, (b, rep)
+
+
+def test_query_witness_calculator_json(oracle):
+    """The reference-shaped surface (WitnessCalculator.calculateWitness over the circuit's JSON signal names)
+    on a query: equals the oracle's witness."""
+    from pzkwit import witness_calculator
+    wc = witness_calculator.WitnessCalculator(native.PZK_CIRCUIT_QUERY, 80)
+    inp, _ = Q.make_query(SplitMix64(0x3E), selector=(1 << 18) - 1)
+    w = wc.calculateWitness({k: (v if isinstance(v, list) else str(v)) for k, v in inp.items()}, True)
+    rc, ref = oracle.query_witness(Q.pack(inp))
+    assert rc == 0 and len(w) == ref.shape[0]
+    assert all(w[i] == int.from_bytes(ref[i].tobytes(), "little") for i in range(len(w)))

@@ -376,9 +376,38 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 }
 
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
-                            ValueStore vs, fr* pos_core, fr* smt_core, int32_t* status, hipStream_t st) {
+                            ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
+                            hipStream_t st) {
   hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
-                     smt_core, status, vs.batch);
+                     smt_core, order, status, vs.batch);
+  return hipGetLastError();
+}
+
+// Counting sort of the batch by SMT insertion level j (0..80, written by k_smt_prep), deepest first: one workgroup.
+// k_smt_chain's lane groups then take witnesses in this order, so a wave holds proofs of (nearly) one depth and
+// finishes after its own depth, not after the deepest of 16 random ones (with uniform depths 0-79 that halves the
+// chain's SIMD time; the kernel itself still lasts as long as the deepest proof).
+__global__ void __launch_bounds__(1024) k_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order,
+                                                    uint32_t batch) {
+  constexpr int NB = SMT_LEVELS + 1;
+  __shared__ uint32_t cnt[NB], at[NB];
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  auto level = [&](uint32_t w) -> uint32_t {
+    const uint32_t j = reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
+    return j < (uint32_t)SMT_LEVELS ? j : (uint32_t)SMT_LEVELS;  // no insertion level: the chain walks all 80
+  };
+  for (uint32_t w = threadIdx.x; w < batch; w += blockDim.x) atomicAdd(&cnt[level(w)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sum = 0;
+    for (int k = NB - 1; k >= 0; k--) { at[k] = sum; sum += cnt[k]; }  // deepest first
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < batch; w += blockDim.x) order[atomicAdd(&at[level(w)], 1u)] = w;
+}
+hipError_t launch_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order, uint32_t batch, hipStream_t st) {
+  hipLaunchKernelGGL(k_smt_order, dim3(1), dim3(1024), 0, st, smt_core, smt_core_fr, order, batch);
   return hipGetLastError();
 }
 

@@ -44,7 +44,10 @@ hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, f
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st);
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
-                            ValueStore vs, fr* pos_core, fr* smt_core, int32_t* status, hipStream_t st);
+                            ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
+                            hipStream_t st);
+// witnesses ordered by SMT insertion level (the chain's length), deepest first, for k_smt_chain's lane groups
+hipError_t launch_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order, uint32_t batch, hipStream_t st);
 // QueryIdentity prep (query.hpp): DG1 fields, dg1 chunks, citizenship inverses, the query checks
 hipError_t launch_qry_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, int32_t* status, hipStream_t st);
 hipError_t launch_ec_core(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, uint64_t* ec_core,

@@ -712,14 +712,16 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 // read the lane's own stores, and the hash comes back to every lane of the group by its butterfly.
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
-                                                 ValueStore vs, fr* pos_core, fr* smt_core, int32_t* status, uint32_t batch) {
+                                                 ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order,
+                                                 int32_t* status, uint32_t batch) {
   core_priority();
   constexpr int G = SMT_CHAIN_LANES;
   static_assert(G == 4 && 64 % G == 0, "PoseidonHash(2) groups are 4 lanes (t = 3)");
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t w = tid / G;
+  const uint32_t g = tid / G;
   const int jl = (int)(tid % G);
-  if (w >= batch) return;  // whole lane groups only
+  if (g >= batch) return;  // whole lane groups only
+  const uint32_t w = order ? order[g] : g;  // k_smt_order: lane groups by proof depth, deepest first
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;

@@ -115,9 +115,10 @@ struct Scratch {
   fr* d_ec_inv = nullptr;
   uint8_t* d_ec_tab = nullptr;
   uint8_t* d_derived = nullptr;  // RSA-PSS derived SHA messages
+  uint32_t* d_smt_order = nullptr;  // witnesses by SMT insertion level, deepest first (k_smt_order)
   void free_all() {
     void* ptrs[] = {d_sha_core, d_pos_core, d_values, d_rsa_core, d_rsa_colsum, d_bjj_core, d_bjj_scratch,
-                    d_smt_core, d_ec_core, d_ec_jac, d_ec_inv, d_ec_tab, d_derived};
+                    d_smt_core, d_ec_core, d_ec_jac, d_ec_inv, d_ec_tab, d_derived, d_smt_order};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
     *this = Scratch();
@@ -641,6 +642,7 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
       {(void**)&S.d_ec_inv, L.is_ecdsa ? 32ull * EC_GEO[L.reg.ec_curve].n_inv * batch : 0},
       {(void**)&S.d_ec_tab, L.is_ecdsa ? 32ull * L.ec_tab_entries * batch : 0},
       {(void**)&S.d_derived, 32ull * L.n_derived * batch},
+      {(void**)&S.d_smt_order, (L.is_register || L.is_query) ? 4ull * batch : 0},
   };
   for (auto& r : req)
     if (r.bytes && hipMalloc(r.p, r.bytes) != hipSuccess) {
@@ -679,7 +681,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   // length is the SMT proof depth (k_smt_chain: 0.5 ms per level for 4096 witnesses, one wave per CU), so
   // consecutive calls rotate over PZK_QRY_CHAINS (1 / 2 / 3) chain streams — the two high-priority streams,
   // then the fifth stream — and their chains run side by side
-  static const int qry_chains = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 2;
+  static const int qry_chains = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 3;
   hipStream_t st = I->stream;
   if (I->lay.is_query && !serial && qry_chains > 1) {
     const int c = qry_chains >= 3 ? set : set & 1;  // NSETS = 3 calls in flight
@@ -744,10 +746,16 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, d_status, st)); }
+      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st));
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
+                              st)); }
     HIPCHK(hipEventRecord(I->ev_pos, st));
-    HIPCHK(hipStreamWaitEvent(s_emit, I->ev_pos, 0));
-    if ((rc = emit(E_POS, s_emit))) return rc;
+    // PZK_QRY_EMIT1=1: every emitter on one stream (with 3 chain streams that is 4 streams in use = the
+    // hardware queues a process gets by default)
+    static const bool emit1 = getenv("PZK_QRY_EMIT1") != nullptr;
+    hipStream_t s_pe = emit1 ? s_sha : s_emit;
+    HIPCHK(hipStreamWaitEvent(s_pe, I->ev_pos, 0));
+    if ((rc = emit(E_POS, s_pe))) return rc;
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_pos, 0));
     if ((rc = emit(E_GEN, s_sha))) return rc;
     if ((rc = emit(E_QRY, s_sha))) return rc;
@@ -830,7 +838,9 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, d_status, st)); }
+      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st));
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
+                              st)); }
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
     HIPCHK(hipEventRecord(I->ev_bjj, st));

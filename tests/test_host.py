@@ -167,7 +167,8 @@ class _StubEngine:
 
     def __init__(self, args, workload, dev):
         import torch
-        self.torch, self.NIN, self.W, self.n_pub, self.inst = torch, 3072, 3072 + 300, 4, _StubInst()
+        nin = 842 if workload == "query" else 3072
+        self.torch, self.NIN, self.W, self.n_pub, self.inst = torch, nin, nin + 300, 4, _StubInst()
         self.layout = "stub"
 
     def setup(self, d_in, batch, sub, slots, steps):
@@ -187,13 +188,13 @@ class _StubEngine:
         return self.rows[:, 0, 0].to(self.torch.int32).clone(), self.rows[:, : self.n_pub].clone()
 
 
-def _bench_rank(rank, world, port, q):
+def _bench_rank(rank, world, port, q, workload="sha256"):
     import argparse
     import torch.distributed as dist
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    args = argparse.Namespace(workload="sha256", batch=6, sub=None, slots=1, steps=2, warmup=1, sig_eff=0, no_cpu=True,
+    args = argparse.Namespace(workload=workload, batch=6, sub=None, slots=1, steps=2, warmup=1, sig_eff=0, no_cpu=True,
                               no_host=True,
                               gpus=world)
     r = bench.run_rank(args, rank, world, 0, dist, engine_cls=_StubEngine, device="cpu")
@@ -202,10 +203,11 @@ def _bench_rank(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_bench_two_ranks_gloo_scatter_gather():
+@pytest.mark.parametrize("workload", ["sha256", "query"])
+def test_bench_two_ranks_gloo_scatter_gather(workload):
     """bench.run_rank over a 2-rank gloo group with the GPU path stubbed: rank 0 generates the job's
     inputs and scatters the shards, the ranks' statuses and public rows are gathered in global order,
-    and the record reports n_gpus = 2."""
+    and the record reports n_gpus = 2. Also for the QueryIdentity workload (its rows)."""
     import hashlib
     import socket
     import torch.multiprocessing as mp
@@ -217,7 +219,7 @@ def test_bench_two_ranks_gloo_scatter_gather():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_bench_rank, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_bench_rank, args=(r, 2, port, q, workload)) for r in range(2)]
     for p in ps:
         p.start()
     out = q.get(timeout=180)
@@ -225,7 +227,11 @@ def test_bench_two_ranks_gloo_scatter_gather():
         p.join(60)
     assert out["n_gpus"] == 2 and out["value"] > 0
     g = out["config"]["gathered"]
-    _, rows = I.sha256_config2_batch(12, seed=2, blocks=6)
+    if workload == "query":
+        from pzkwit import query as Q
+        rows = Q.batch_rows(12, seed=0x9, distinct=64)
+    else:
+        _, rows = I.sha256_config2_batch(12, seed=2, blocks=6)
     assert g["witnesses"] == 12
     assert g["status_nonzero"] == int((rows[:, 0, 0] != 0).sum())
     assert g["public_sha256"] == hashlib.sha256(rows[:, :4].tobytes()).hexdigest()[:16]

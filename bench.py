@@ -79,10 +79,11 @@ def _cpu_work(args):
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
             pyoracle.register_witness(prm, r, out=w)
-    elif kind == "query":
-        w = np.zeros((pyoracle.query_sizes()[1], 32), dtype=np.uint8)
+    elif kind.startswith("query"):
+        td1 = kind == "query-td1"
+        w = np.zeros((pyoracle.query_sizes(td1)[1], 32), dtype=np.uint8)
         for r in rows:
-            pyoracle.query_witness(r, out=w)
+            pyoracle.query_witness(r, out=w, td1=td1)
     else:
         for r in rows:
             pyoracle.sha256_witness(r, 6)
@@ -159,8 +160,8 @@ class GpuEngine:
                     self.layout += "; staging + gather (non-monotone map)"
                 else:
                     self.layout += "; emitted directly (monotone map, mapsink.hpp)"
-        elif workload == "query":
-            self.inst = native.Instance(native.PZK_CIRCUIT_QUERY, 80)
+        elif workload.startswith("query"):
+            self.inst = native.Instance(native.PZK_CIRCUIT_QUERY, 80, {"doc": 1} if workload == "query-td1" else None)
         else:
             self.inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
         self.W, self.NIN = self.inst.witness_size, self.inst.n_inputs
@@ -217,7 +218,7 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
     from pzkwit import dist as D, inputs as I
     dev = torch.device(device, local) if device == "cuda" else torch.device(device)
     register = args.workload.startswith("register")
-    batch = args.batch or (4096 if register or args.workload == "query" else 1024)
+    batch = args.batch or (4096 if register or args.workload.startswith("query") else 1024)
     engine = engine_cls(args, args.workload, dev)
     NIN, W = engine.NIN, engine.W
     # inputs: rank 0 makes all world x batch rows, scatters shard r to rank r
@@ -228,9 +229,9 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
         if register:
             host = make_register_inputs(batch * world, 0, seed=SIG_SEED[args.sig_eff], sig=args.sig_eff,
                                         workers=workers)
-        elif args.workload == "query":
+        elif args.workload.startswith("query"):
             from pzkwit import query as Q
-            host = Q.batch_rows(batch * world, seed=0x9, distinct=64)
+            host = Q.batch_rows(batch * world, seed=0x9, distinct=64, td1=args.workload == "query-td1")
         else:
             _, host = I.sha256_config2_batch(batch * world, seed=2, blocks=6)
         full = torch.from_numpy(host.reshape(world, -1))
@@ -307,7 +308,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "sha256", "mixed", "query"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "sha256", "mixed", "query", "query-td1"], default="register")
     ap.add_argument("--sig", type=int, default=None, help="SIGNATURE_TYPE of a register workload (overrides --workload's)")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slot) size")
@@ -363,9 +364,10 @@ def report(args, r, world):
             workload = "RegisterIdentityBuilder(%d,%d,%d,%d,%d,%d,%d,%d,%d,%d) synthetic passports" % tuple(
                 q[k] for k in ("sig", "dg_hash", "doc", "ec_blocks", "ec_shift", "dg1_shift", "aa", "dg15_shift",
                                "dg15_blocks", "aa_shift"))
-    elif args.workload == "query":
-        metric = "QueryIdentity(80) witnesses/sec, batch=4096 (SURVEY.md row f4)"
-        workload = "QueryIdentity(80) synthetic queries (64 distinct, SMT proofs of depth 0-79)"
+    elif args.workload.startswith("query"):
+        td1 = args.workload == "query-td1"
+        metric = "QueryIdentity%s(80) witnesses/sec, batch=4096 (SURVEY.md row f4)" % ("TD1" if td1 else "")
+        workload = "QueryIdentity%s(80) synthetic queries (64 distinct, SMT proofs of depth 0-79)" % ("TD1" if td1 else "")
     else:
         metric = "Sha256HashChunks(6) witnesses/sec, batch=1024 (config 2)"
         workload = "Sha256HashChunks(6) synthetic 312-375 B messages (config 2)"
@@ -427,11 +429,11 @@ def report(args, r, world):
             ns = args.cpu_sample or (48 if sig >= 20 else 96 if sig == 11 else 128) * procs
             rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=SIG_SEED[sig], sig=sig)
             kind = "register:%d" % sig
-        elif args.workload == "query":
+        elif args.workload.startswith("query"):
             from pzkwit import query as Q
             ns = args.cpu_sample or 64 * procs
-            rows = Q.batch_rows(ns, seed=99, distinct=64)
-            kind = "query"
+            rows = Q.batch_rows(ns, seed=99, distinct=64, td1=args.workload == "query-td1")
+            kind = args.workload
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)

@@ -58,8 +58,10 @@ def lib():
         L.orc_sha512_witness_size.argtypes = [ctypes.c_int, ctypes.c_int]
         L.orc_sha512_witness.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_query_witness_size.restype = ctypes.c_size_t
+        L.orc_query_witness_size.argtypes = [ctypes.c_int]
         L.orc_query_n_inputs.restype = ctypes.c_size_t
-        L.orc_query_witness.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_query_n_inputs.argtypes = [ctypes.c_int]
+        L.orc_query_witness.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         rc = L.orc_load_poseidon(POSEIDON_BIN.encode())
         if rc != 0:
             raise RuntimeError("oracle: cannot load Poseidon constants (%d)" % rc)
@@ -153,18 +155,18 @@ def sha512_witness(in_elems, blocks, out_bits=512):
     return rc, w
 
 
-def query_sizes():
-    """QueryIdentity(80): (inputs, witness elements)."""
+def query_sizes(td1=False):
+    """QueryIdentity(80) (td1: QueryIdentityTD1): (inputs, witness elements)."""
     L = lib()
-    return L.orc_query_n_inputs(), L.orc_query_witness_size()
+    return L.orc_query_n_inputs(int(td1)), L.orc_query_witness_size(int(td1))
 
 
-def query_witness(inputs, out=None):
-    """QueryIdentity(80) witness; inputs (842, 32) uint8 in declaration order. Returns (rc, (nWit, 32) uint8)."""
+def query_witness(inputs, out=None, td1=False):
+    """QueryIdentity(80) witness; inputs (842 | 858, 32) uint8 in declaration order. Returns (rc, (nWit, 32) uint8)."""
     L = lib()
-    nin, nw = query_sizes()
+    nin, nw = query_sizes(td1)
     a = np.ascontiguousarray(inputs, dtype=np.uint8)
     assert a.shape == (nin, 32), (a.shape, nin)
     w = out if out is not None else np.zeros((nw, 32), dtype=np.uint8)
-    rc = L.orc_query_witness(a.ctypes.data, w.ctypes.data)
+    rc = L.orc_query_witness(int(td1), a.ctypes.data, w.ctypes.data)
     return rc, w

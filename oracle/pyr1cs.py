@@ -38,7 +38,7 @@ def lib():
         L.ck_load_poseidon.argtypes = [ctypes.c_char_p]
         L.ck_load_ec_table.argtypes = [ctypes.c_int, ctypes.c_char_p]
         L.ck_register.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
-        L.ck_query.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
+        L.ck_query.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Report)]
         _lib = L
     return _lib
 
@@ -112,11 +112,11 @@ def check_register(wit, **params):
     return rc, r.as_dict()
 
 
-def check_query(wit):
-    """QueryIdentity(80) witness (oracle/r1cs_query.inc.c) -> (rc, report dict)."""
+def check_query(wit, td1=False):
+    """QueryIdentity(80) witness (oracle/r1cs_query.inc.c; td1: QueryIdentityTD1) -> (rc, report dict)."""
     import numpy as np
     _load_poseidon()
     w = np.ascontiguousarray(wit, dtype=np.uint8)
     r = Report()
-    rc = lib().ck_query(w.ctypes.data, w.shape[0], ctypes.byref(r))
+    rc = lib().ck_query(int(td1), w.ctypes.data, w.shape[0], ctypes.byref(r))
     return rc, r.as_dict()

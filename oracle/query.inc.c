@@ -29,7 +29,13 @@ static const uint32_t QY_COUNTRY[240] = {
 };
 
 #define QY_DEPTH 80
-#define QY_NIN 842  /* main inputs */
+/* variant: TD3 = QueryIdentity (queryIdentity.circom, dg1[744], DG1DataExtractor); TD1 = queryIdentityTD1.circom
+ * (dg1[760], DG1TD1DataExtractor dg1TD1DataExtractor.circom:5-107, PoseidonHash(1) of documentNumber and
+ * personalNumber, 10 outputs) */
+static int QY_TD1 = 0;
+#define QY_DG1 (QY_TD1 ? 760 : 744)
+#define QY_NIN (98 + QY_DG1)  /* main inputs */
+#define QY_NOUT (QY_TD1 ? 10 : 9)
 
 /* DateEncoder dateEncoder.circom:4-32: encoded | day, month, year | dayDecimals, dayRest, monthDecimals,
  * monthRest, yearDecimals, yearRest, dayEncoded, monthEncoded, yearEncoded */
@@ -138,16 +144,24 @@ static void run_feie(ctx_t *c, size_t b, fr_t enabled, fr_t in0, fr_t in1) {
  * citizenship, sex, documentNumber | dg1[744] | Bits2Num encoders, in[L-1-i] = dg1[SHIFT + i] */
 static const int QY_DGX_L[8] = {48, 48, 248, 64, 24, 24, 8, 72};
 static const int QY_DGX_SHIFT[8] = {496, 560, 80, 328, 472, 56, 552, 392};
+/* TD1: birthDate, expirationDate, name, nationality, citizenship, sex, documentNumber, personalNumber, documentType
+ * (dg1TD1DataExtractor.circom:20-107; sex at bit 336, not byte) */
+static const int QY1_DGX_L[9] = {48, 48, 240, 24, 24, 8, 72, 88, 16};
+static const int QY1_DGX_SHIFT[9] = {280, 344, 520, 400, 56, 336, 80, 160, 40};
+#define QY_NF (QY_TD1 ? 9 : 8)
+#define QY_FL(k) (QY_TD1 ? QY1_DGX_L[k] : QY_DGX_L[k])
+#define QY_FS(k) (QY_TD1 ? QY1_DGX_SHIFT[k] : QY_DGX_SHIFT[k])
+#define QY_FCIT (QY_TD1 ? 4 : 5)
 static size_t sz_dgx(void) {
-  size_t s = 8 + 744;
-  for (int k = 0; k < 8; k++) s += sz_bits2num(QY_DGX_L[k]);
+  size_t s = (size_t)QY_NF + QY_DG1;
+  for (int k = 0; k < QY_NF; k++) s += sz_bits2num(QY_FL(k));
   return s;
 }
 static void run_dgx(ctx_t *c, size_t b) {
-  size_t p = b + 8 + 744;
-  for (int k = 0; k < 8; k++) {
-    const int L = QY_DGX_L[k];
-    for (int i = 0; i < L; i++) W(p + 1 + L - 1 - i) = W(b + 8 + QY_DGX_SHIFT[k] + i);
+  size_t p = b + QY_NF + QY_DG1;
+  for (int k = 0; k < QY_NF; k++) {
+    const int L = QY_FL(k);
+    for (int i = 0; i < L; i++) W(p + 1 + L - 1 - i) = W(b + QY_NF + QY_FS(k) + i);
     run_bits2num(c, p, L);
     W(b + k) = W(p);
     p += sz_bits2num(L);
@@ -195,33 +209,36 @@ static void run_isv(ctx_t *c, size_t b) {
   if (!fr_eq(W(smt), ONE()) && !c->err) c->err = S_ISV_ROOT;
 }
 
+static int qy_chunk(void) { return QY_TD1 ? 190 : 186; }
 static size_t sz_query_main(void) {
-  return 9 + QY_NIN + 1 + sz_num2bits(18) + sz_dgx() + sz_poseidon(1) + sz_poseidon(3) + 2 * sz_greatereq(64) +
-         2 * sz_lessthan(64) + 8 * SZ_FEIE + 2 * SZ_EDIL + 2 * SZ_EDILN + sz_poseidon(5) + 4 * sz_bits2num(186) +
-         sz_poseidon(1) + sz_isv() + sz_citizenship();
+  return QY_NOUT + QY_NIN + 1 + sz_num2bits(18) + sz_dgx() + (QY_TD1 ? 2 * sz_poseidon(1) : 0) + sz_poseidon(1) +
+         sz_poseidon(3) + 2 * sz_greatereq(64) + 2 * sz_lessthan(64) + 8 * SZ_FEIE + 2 * SZ_EDIL + 2 * SZ_EDILN +
+         sz_poseidon(5) + 4 * sz_bits2num(qy_chunk()) + sz_poseidon(1) + sz_isv() + sz_citizenship();
 }
-size_t orc_query_n_inputs(void) { return QY_NIN; }
-size_t orc_query_witness_size(void) {
+/* td1: 0 = QueryIdentity (TD3), 1 = QueryIdentityTD1 */
+size_t orc_query_n_inputs(int td1) { QY_TD1 = td1 != 0; return QY_NIN; }
+size_t orc_query_witness_size(int td1) {
   if (!pos_loaded) return 0;
   orc_init();
+  QY_TD1 = td1 != 0;
   return 1 + sz_query_main();
 }
 
-/* inputs: 842 x 32 B LE in declaration order (eventID, eventData, idStateRoot, selector, currentDate,
+/* inputs: 842 (TD1: 858) x 32 B LE in declaration order (eventID, eventData, idStateRoot, selector, currentDate,
  * timestampLowerbound, timestampUpperbound, identityCounterLowerbound, identityCounterUpperbound,
  * birthDateLowerbound, birthDateUpperbound, expirationDateLowerbound, expirationDateUpperbound, citizenshipMask,
  * skIdentity, pkPassportHash, dg1[744], idStateSiblings[80], timestamp, identityCounter). Returns check-site id. */
-int orc_query_witness(const uint8_t *inputs, uint8_t *wit) {
+int orc_query_witness(int td1, const uint8_t *inputs, uint8_t *wit) {
   if (!pos_loaded) return -1;
   orc_init();
   ctx_t cc = {(fr_t *)wit, 0}, *c = &cc;
-  const size_t nW = orc_query_witness_size();
+  const size_t nW = orc_query_witness_size(td1);
   memset(wit, 0, nW * 32);
   W(0) = ONE();
-  const size_t m = 1, in = m + 9;
+  const size_t m = 1, in = m + QY_NOUT;
   memcpy(&W(in), inputs, QY_NIN * 32);
-  enum { EVID, EVDATA, ROOT, SEL, CUR, TSLO, TSHI, ICLO, ICHI, BDLO, BDHI, EDLO, EDHI, CMASK, SK, PKPASS, DG1,
-         SIB = DG1 + 744, TS = SIB + QY_DEPTH, IC };
+  enum { EVID, EVDATA, ROOT, SEL, CUR, TSLO, TSHI, ICLO, ICHI, BDLO, BDHI, EDLO, EDHI, CMASK, SK, PKPASS, DG1 };
+  const int SIB = DG1 + QY_DG1, TS = SIB + QY_DEPTH, IC = TS + 1;
 #define IN(k) W(in + (k))
   W(in + QY_NIN) = mulg(IN(EVDATA), IN(EVDATA));  /* eventDataSquare (queryIdentity.circom:205) */
   size_t p = in + QY_NIN + 1;
@@ -232,9 +249,21 @@ int orc_query_witness(const uint8_t *inputs, uint8_t *wit) {
 #define SEL_BIT(k) W(selb + (k))
   /* dg1DataExtractor */
   size_t dgx = p; p += sz_dgx();
-  for (int i = 0; i < 744; i++) W(dgx + 8 + i) = IN(DG1 + i);
+  for (int i = 0; i < QY_DG1; i++) W(dgx + QY_NF + i) = IN(DG1 + i);
   run_dgx(c, dgx);
-  for (int k = 0; k < 8; k++) W(m + 1 + k) = mulg(W(dgx + k), SEL_BIT(k == 0 ? 1 : k == 1 ? 2 : k <= 3 ? 3 : k));
+  if (!QY_TD1) {
+    for (int k = 0; k < 8; k++) W(m + 1 + k) = mulg(W(dgx + k), SEL_BIT(k == 0 ? 1 : k == 1 ? 2 : k <= 3 ? 3 : k));
+  } else {
+    /* documentNumberHasher, personalNumberHasher (queryIdentityTD1.circom:89-95); outputs :97-105 */
+    size_t dnh = p; p += sz_poseidon(1);
+    W(dnh + 1) = W(dgx + 6); run_poseidon(c, dnh, 1);
+    size_t pnh = p; p += sz_poseidon(1);
+    W(pnh + 1) = W(dgx + 7); run_poseidon(c, pnh, 1);
+    for (int k = 0; k < 6; k++) W(m + 1 + k) = mulg(W(dgx + k), SEL_BIT(k + 1));
+    W(m + 7) = mulg(W(dnh), SEL_BIT(7));
+    W(m + 8) = mulg(W(pnh), SEL_BIT(16));
+    W(m + 9) = mulg(W(dgx + 8), SEL_BIT(17));
+  }
   /* nullifier = Poseidon3(sk, Poseidon1(sk), eventID) * selector[0] */
   size_t skh = p; p += sz_poseidon(1);
   W(skh + 1) = IN(SK); run_poseidon(c, skh, 1);
@@ -268,10 +297,11 @@ int orc_query_witness(const uint8_t *inputs, uint8_t *wit) {
   /* DG commitment: dg1Hasher = Poseidon5(Bits2Num(186) x 4 of dg1, Poseidon1(sk)); dg1Hasher is created
    * before dg1Chunking[i] (queryIdentity.circom:192-198) */
   size_t dgh = p; p += sz_poseidon(5);
+  const int CH = qy_chunk();
   for (int i = 0; i < 4; i++) {
-    size_t ch = p; p += sz_bits2num(186);
-    for (int j = 0; j < 186; j++) W(ch + 1 + j) = IN(DG1 + i * 186 + j);
-    run_bits2num(c, ch, 186);
+    size_t ch = p; p += sz_bits2num(CH);
+    for (int j = 0; j < CH; j++) W(ch + 1 + j) = IN(DG1 + i * CH + j);
+    run_bits2num(c, ch, CH);
     W(dgh + 1 + i) = W(ch);
   }
   size_t skh2 = p; p += sz_poseidon(1);
@@ -286,7 +316,7 @@ int orc_query_witness(const uint8_t *inputs, uint8_t *wit) {
   run_isv(c, isv);
   /* citizenshipCheck(dg1DataExtractor.citizenship, citizenshipMask) */
   size_t cit = p; p += sz_citizenship();
-  W(cit) = W(dgx + 5); W(cit + 1) = IN(CMASK);
+  W(cit) = W(dgx + QY_FCIT); W(cit + 1) = IN(CMASK);
   run_citizenship(c, cit);
 #undef IN
 #undef SEL_BIT

@@ -2521,9 +2521,10 @@ int ck_sha1(int B, const uint8_t *wit, size_t n, ck_report *r) {
   return ck_end(&c, walked, r);
 }
 
-/* QueryIdentity(80) as main (oracle/r1cs_query.inc.c) */
-int ck_query(const uint8_t *wit, size_t nw, ck_report *r) {
+/* QueryIdentity(80) as main (oracle/r1cs_query.inc.c); td1: QueryIdentityTD1 */
+int ck_query(int td1, const uint8_t *wit, size_t nw, ck_report *r) {
   if (!pos_loaded) return -1;
+  CKQ_TD1 = td1 != 0;
   ck_t c = ck_begin(wit, nw);
   size_t walked = 1 + ck_queryid(&c, 1);
   req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);

@@ -9,6 +9,8 @@
  * BabyjubjubBase8Multiplication, with BabyPbk's port names: in = scalar, Ax/Ay = out[0]/out[1].
  */
 
+static int CKQ_TD1 = 0;  /* 0: QueryIdentity (queryIdentity.circom), 1: QueryIdentityTD1 (queryIdentityTD1.circom) */
+
 static const uint32_t CKQ_COUNTRY[240] = {
 #include "../passport-zk-circuits_amd/data/citizenship_codes.inc"
 };
@@ -124,16 +126,22 @@ static size_t ck_ediln(ck_t *c, size_t b) {
   EQ(S(c, b), S(c, dl), T, 48);
   return sz;
 }
-/* DG1DataExtractor dg1DataExtractor.circom:5-97: 8 outputs | dg1[744] | Bits2Num encoders */
+/* DG1DataExtractor dg1DataExtractor.circom:5-97: 8 outputs | dg1[744] | Bits2Num encoders;
+ * DG1TD1DataExtractor dg1TD1DataExtractor.circom:5-107: 9 outputs | dg1[760] | Bits2Num encoders */
 static size_t ck_dgx(ck_t *c, size_t b) {
-  const char *T = "DG1DataExtractor identityManagement/dg1DataExtractor.circom";
-  static const int L[8] = {48, 48, 248, 64, 24, 24, 8, 72}, SH[8] = {496, 560, 80, 328, 472, 56, 552, 392},
-                   IN_LINE[8] = {27, 36, 49, 53, 64, 74, 84, 94}, OUT_LINE[8] = {29, 39, 55, 56, 66, 76, 86, 97};
-  size_t o = b + 8 + 744;
-  for (int k = 0; k < 8; k++) {
+  const char *T = CKQ_TD1 ? "DG1TD1DataExtractor identityManagement/dg1TD1DataExtractor.circom"
+                          : "DG1DataExtractor identityManagement/dg1DataExtractor.circom";
+  static const int L3[8] = {48, 48, 248, 64, 24, 24, 8, 72}, SH3[8] = {496, 560, 80, 328, 472, 56, 552, 392},
+                   IN3[8] = {27, 36, 49, 53, 64, 74, 84, 94}, OUT3[8] = {29, 39, 55, 56, 66, 76, 86, 97};
+  static const int L1[9] = {48, 48, 240, 24, 24, 8, 72, 88, 16}, SH1[9] = {280, 344, 520, 400, 56, 336, 80, 160, 40},
+                   IN1[9] = {26, 35, 45, 55, 65, 75, 85, 95, 105}, OUT1[9] = {28, 37, 47, 57, 67, 77, 87, 97, 107};
+  const int NF = CKQ_TD1 ? 9 : 8, DG = CKQ_TD1 ? 760 : 744;
+  const int *L = CKQ_TD1 ? L1 : L3, *SH = CKQ_TD1 ? SH1 : SH3, *IN_LINE = CKQ_TD1 ? IN1 : IN3, *OUT_LINE = CKQ_TD1 ? OUT1 : OUT3;
+  size_t o = b + NF + DG;
+  for (int k = 0; k < NF; k++) {
     size_t e = o;
     o += ck_bits2num(c, e, L[k]);
-    for (int i = 0; i < L[k]; i++) EQ(S(c, e + 1 + L[k] - 1 - i), S(c, b + 8 + SH[k] + i), T, IN_LINE[k]);
+    for (int i = 0; i < L[k]; i++) EQ(S(c, e + 1 + L[k] - 1 - i), S(c, b + NF + SH[k] + i), T, IN_LINE[k]);
     EQ(S(c, b + k), S(c, e), T, OUT_LINE[k]);
   }
   return o - b;
@@ -183,21 +191,36 @@ static size_t ck_isv(ck_t *c, size_t b) {
 /* QueryIdentity(80) queryIdentity.circom:37-229 as main: [1] nullifier birthDate expirationDate name nameResidual
  * nationality citizenship sex documentNumber | 842 inputs (declaration order) | eventDataSquare | subcomponents */
 static size_t ck_queryid(ck_t *c, size_t b) {
-  const char *T = "QueryIdentity identityManagement/queryIdentity.circom";
-  enum { EVID, EVDATA, ROOT, SEL, CUR, TSLO, TSHI, ICLO, ICHI, BDLO, BDHI, EDLO, EDHI, CMASK, SK, PKPASS, DG1,
-         SIB = DG1 + 744, TS = SIB + 80, IC };
-  const size_t in = b + 9;
+  const char *T = CKQ_TD1 ? "QueryIdentity identityManagement/queryIdentityTD1.circom"
+                          : "QueryIdentity identityManagement/queryIdentity.circom";
+  enum { EVID, EVDATA, ROOT, SEL, CUR, TSLO, TSHI, ICLO, ICHI, BDLO, BDHI, EDLO, EDHI, CMASK, SK, PKPASS, DG1 };
+  const int DGL = CKQ_TD1 ? 760 : 744, SIB = DG1 + DGL, TS = SIB + 80, IC = TS + 1, NIN = IC + 1, NOUT = CKQ_TD1 ? 10 : 9;
+  const int NF = CKQ_TD1 ? 9 : 8;
+  const size_t in = b + (size_t)NOUT;
 #define QIN(k) (in + (size_t)(k))
-  size_t o = in + 842 + 1;
-  EQ(S(c, in + 842), MUL(S(c, QIN(EVDATA)), S(c, QIN(EVDATA))), T, 209);
+  size_t o = in + (size_t)NIN + 1;
+  EQ(S(c, in + NIN), MUL(S(c, QIN(EVDATA)), S(c, QIN(EVDATA))), T, 209);
   size_t selb = o;
   o += ck_num2bits(c, selb, 18);
   EQ(S(c, selb + 18), S(c, QIN(SEL)), T, 81);
   size_t dgx = o;
   o += ck_dgx(c, dgx);
-  for (int i = 0; i < 744; i++) EQ(S(c, dgx + 8 + i), S(c, QIN(DG1 + i)), T, 86);
-  static const int OSEL[8] = {1, 2, 3, 3, 4, 5, 6, 7};
-  for (int k = 0; k < 8; k++) EQ(S(c, b + 1 + k), MUL(S(c, dgx + k), S(c, selb + OSEL[k])), T, 88 + k);
+  for (int i = 0; i < DGL; i++) EQ(S(c, dgx + NF + i), S(c, QIN(DG1 + i)), T, 86);
+  if (!CKQ_TD1) {
+    static const int OSEL[8] = {1, 2, 3, 3, 4, 5, 6, 7};
+    for (int k = 0; k < 8; k++) EQ(S(c, b + 1 + k), MUL(S(c, dgx + k), S(c, selb + OSEL[k])), T, 88 + k);
+  } else {  /* documentNumberHasher, personalNumberHasher (:89-95), outputs (:97-105) */
+    size_t dnh = o;
+    o += ck_poseidon(c, dnh, 1);
+    EQ(S(c, dnh + 1), S(c, dgx + 6), T, 91);
+    size_t pnh = o;
+    o += ck_poseidon(c, pnh, 1);
+    EQ(S(c, pnh + 1), S(c, dgx + 7), T, 95);
+    for (int k = 0; k < 6; k++) EQ(S(c, b + 1 + k), MUL(S(c, dgx + k), S(c, selb + 1 + k)), T, 97 + k);
+    EQ(S(c, b + 7), MUL(S(c, dnh), S(c, selb + 7)), T, 103);
+    EQ(S(c, b + 8), MUL(S(c, pnh), S(c, selb + 16)), T, 104);
+    EQ(S(c, b + 9), MUL(S(c, dgx + 8), S(c, selb + 17)), T, 105);
+  }
   size_t skh = o;
   o += ck_poseidon(c, skh, 1);
   EQ(S(c, skh + 1), S(c, QIN(SK)), T, 100);
@@ -207,7 +230,7 @@ static size_t ck_queryid(ck_t *c, size_t b) {
   EQ(S(c, nul + 2), S(c, skh), T, 104);
   EQ(S(c, nul + 3), S(c, QIN(EVID)), T, 105);
   EQ(S(c, b), MUL(S(c, nul), S(c, selb)), T, 107);
-  static const int CX[4] = {TS, TS, IC, IC}, CY[4] = {TSLO, TSHI, ICLO, ICHI}, CL[4] = {112, 122, 133, 143};
+  const int CX[4] = {TS, TS, IC, IC}, CY[4] = {TSLO, TSHI, ICLO, ICHI}, CL[4] = {112, 122, 133, 143};
   for (int k = 0; k < 4; k++) {
     size_t cb = o;
     o += (k & 1) ? ck_lessthan(c, cb, 64) : ck_greatereq(c, cb, 64);
@@ -244,10 +267,11 @@ static size_t ck_queryid(ck_t *c, size_t b) {
   }
   size_t dgh = o;  /* created before dg1Chunking[i] */
   o += ck_poseidon(c, dgh, 5);
+  const int CH = CKQ_TD1 ? 190 : 186;
   for (int i = 0; i < 4; i++) {
     size_t ch = o;
-    o += ck_bits2num(c, ch, 186);
-    for (int j = 0; j < 186; j++) EQ(S(c, ch + 1 + j), S(c, QIN(DG1 + i * 186 + j)), T, 199);
+    o += ck_bits2num(c, ch, CH);
+    for (int j = 0; j < CH; j++) EQ(S(c, ch + 1 + j), S(c, QIN(DG1 + i * CH + j)), T, 199);
     EQ(S(c, dgh + 1 + i), S(c, ch), T, 201);
   }
   size_t skh2 = o;
@@ -265,7 +289,7 @@ static size_t ck_queryid(ck_t *c, size_t b) {
   for (int i = 0; i < 80; i++) EQ(S(c, isv + 6 + i), S(c, QIN(SIB + i)), T, 220);
   size_t cit = o;
   o += ck_citizenship(c, cit);
-  EQ(S(c, cit), S(c, dgx + 5), T, 226);
+  EQ(S(c, cit), S(c, dgx + (CKQ_TD1 ? 4 : 5)), T, 226);
   EQ(S(c, cit + 1), S(c, QIN(CMASK)), T, 227);
   /* main's inputs are read by the wiring above; the 14 public inputs each feed some constraint */
 #undef QIN

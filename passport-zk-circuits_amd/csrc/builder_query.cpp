@@ -20,9 +20,18 @@ bool build_query(const pzk_params& p, Layout& L, std::string& why) {
     why = "QueryIdentity: idTreeDepth must be 80 (idStateSiblings[80] is fixed, queryIdentity.circom:75)";
     return false;
   }
+  if (p.document_type != 0 && p.document_type != 1 && p.document_type != 3) {
+    why = "QueryIdentity: document_type must be 3 (TD3, queryIdentity.circom) or 1 (TD1, queryIdentityTD1.circom)";
+    return false;
+  }
+  const bool td1 = p.document_type == 1;
+  const int NF = td1 ? 9 : 8, DG1L = q_dg1_len(td1), IN_SIB = q_in_sib(td1), IN_TS = q_in_ts(td1), IN_IC = q_in_ic(td1),
+            CH = q_chunk(td1);
+  auto fl = [&](int k) { return td1 ? Q1_DGX_L[k] : Q_DGX_L[k]; };
+  auto fs = [&](int k) { return td1 ? Q1_DGX_SHIFT[k] : Q_DGX_SHIFT[k]; };
   Builder b(L);
-  L.n_inputs = QI_N;
-  L.n_outputs = 9;
+  L.n_inputs = q_n_inputs(td1);
+  L.n_outputs = td1 ? 10 : 9;
   L.n_public = 14;
   L.inputs = {{"eventID", QI_EVID, 1},
               {"eventData", QI_EVDATA, 1},
@@ -40,49 +49,57 @@ bool build_query(const pzk_params& p, Layout& L, std::string& why) {
               {"citizenshipMask", QI_CMASK, 1},
               {"skIdentity", QI_SK, 1},
               {"pkPassportHash", QI_PKPASS, 1},
-              {"dg1", QI_DG1, 744},
-              {"idStateSiblings", QI_SIB, (uint64_t)Q_DEPTH},
-              {"timestamp", QI_TS, 1},
-              {"identityCounter", QI_IC, 1}};
+              {"dg1", QI_DG1, (uint64_t)DG1L},
+              {"idStateSiblings", (uint64_t)IN_SIB, (uint64_t)Q_DEPTH},
+              {"timestamp", (uint64_t)IN_TS, 1},
+              {"identityCounter", (uint64_t)IN_IC, 1}};
   L.is_query = true;
   L.params = p;
-  L.reg.in_br = QI_SIB;
+  L.reg.in_br = IN_SIB;
   L.reg.in_root = QI_ROOT;
   L.reg.smt_check = 1;
+  L.reg.q_td1 = td1 ? 1 : 0;
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
 
   // ---- value-store slots (Montgomery): loaded inputs, k_qry_prep outputs, chain outputs
   const int V_ONE = b.value(), V_SK = b.value(), V_EVID = b.value(), V_PKPASS = b.value(), V_IC = b.value(),
             V_TS = b.value(), V_SEL = b.value(), V_CMASK = b.value();
-  int V_DGF[8], V_DGC[4], V_L[Q_DEPTH], V_R[Q_DEPTH];
-  for (int k = 0; k < 8; k++) V_DGF[k] = b.value();
+  int V_DGF[9], V_DGC[4], V_L[Q_DEPTH], V_R[Q_DEPTH];
+  for (int k = 0; k < 9; k++) V_DGF[k] = b.value();
   for (int i = 0; i < 4; i++) V_DGC[i] = b.value();
   const int V_BJJ_X = b.value(), V_BJJ_Y = b.value();
   for (int i = 0; i < Q_DEPTH; i++) { V_L[i] = b.value(); V_R[i] = b.value(); }
   const int V_CIDX = b.value();
   const int V_CINV = b.value();
   for (int i = 1; i < 240; i++) b.value();
-  for (auto [slot, in] : {std::pair<int, int>{V_SK, QI_SK}, {V_EVID, QI_EVID}, {V_PKPASS, QI_PKPASS}, {V_IC, QI_IC},
-                          {V_TS, QI_TS}, {V_SEL, QI_SEL}, {V_CMASK, QI_CMASK}})
+  for (auto [slot, in] : {std::pair<int, int>{V_SK, QI_SK}, {V_EVID, QI_EVID}, {V_PKPASS, QI_PKPASS}, {V_IC, IN_IC},
+                          {V_TS, IN_TS}, {V_SEL, QI_SEL}, {V_CMASK, QI_CMASK}})
     L.loads.push_back(ValueLoad{slot, in});
   L.reg.v_one = V_ONE; L.reg.v_sk = V_SK; L.reg.v_dg1 = V_DGC[0]; L.reg.v_bjj = V_BJJ_X; L.reg.v_smt_lr = V_L[0];
   L.reg.q_dgf = V_DGF[0]; L.reg.q_cinv = V_CINV; L.reg.q_cidx = V_CIDX;
-  // Poseidon levels: 0 sk hashes; 1 nullifier, dg1 commitment; 2 (after the BabyJubJub core) pk identity hash,
-  // identity-state value; 3 tree position (the SMT key); 4 SMTHash1 of the new leaf; 5 SMT level hashes
+  // Poseidon levels: 0 sk hashes (and TD1's document / personal number hashes); 1 nullifier, dg1 commitment;
+  // 2 (after the BabyJubJub core) pk identity hash, identity-state value; 3 tree position (the SMT key);
+  // 4 SMTHash1 of the new leaf; 5 SMT level hashes
 
-  // =========================== main: [1 | outputs(9) | inputs(842) | eventDataSquare] ===========================
+  // =========================== main: [1 | outputs | inputs | eventDataSquare] ===========================
   b.region(RK_ONE, 1);
-  b.region(RK_Q_OUT, 9);
-  b.region(RK_INCOPY, QI_N, {0});
+  b.region(RK_Q_OUT, L.n_outputs);
+  b.region(RK_INCOPY, L.n_inputs, {0});
   b.region(RK_Q_SQ, 1);
   // selectorBits = Num2Bits(18)(selector)
   b.region(RK_NUM2BITS, q_num2bits(18), {18, 0, V_SEL});
-  // DG1DataExtractor: 8 outputs | dg1[744] | Bits2Num encoders (in[L-1-i] = dg1[SHIFT + i])
-  b.region(RK_VALUE, 8, {-3, V_DGF[0], V_DGF[1], V_DGF[2], V_DGF[3], V_DGF[4], V_DGF[5], V_DGF[6], V_DGF[7]});
-  b.region(RK_INCOPY, 744, {QI_DG1});
-  for (int k = 0; k < 8; k++)
-    b.region(RK_BITS2NUM, q_num2bits(Q_DGX_L[k]), {Q_DGX_L[k], 0, QI_DG1 + Q_DGX_SHIFT[k] + Q_DGX_L[k] - 1, -1});
+  // DG1DataExtractor / DG1TD1DataExtractor: fields | dg1 | Bits2Num encoders (in[L-1-i] = dg1[SHIFT + i])
+  if (td1)
+    b.region(RK_VALUE, 9, {-3, V_DGF[0], V_DGF[1], V_DGF[2], V_DGF[3], V_DGF[4], V_DGF[5], V_DGF[6], V_DGF[7], V_DGF[8]});
+  else
+    b.region(RK_VALUE, 8, {-3, V_DGF[0], V_DGF[1], V_DGF[2], V_DGF[3], V_DGF[4], V_DGF[5], V_DGF[6], V_DGF[7]});
+  b.region(RK_INCOPY, DG1L, {QI_DG1});
+  for (int k = 0; k < NF; k++) b.region(RK_BITS2NUM, q_num2bits(fl(k)), {fl(k), 0, QI_DG1 + fs(k) + fl(k) - 1, -1});
+  if (td1) {  // documentNumberHasher, personalNumberHasher (queryIdentityTD1.circom:89-95)
+    L.reg.q_doch = b.poseidon(1, {V_DGF[6]}, 0);
+    L.reg.q_persh = b.poseidon(1, {V_DGF[7]}, 0);
+  }
   // nullifier = Poseidon3(sk, Poseidon1(sk), eventID) (queryIdentity.circom:97-105)
   const int S_SKH = b.poseidon(1, {V_SK}, 0);
   const int S_NUL = b.poseidon(3, {V_SK, S_SKH, V_EVID}, 1);
@@ -100,10 +117,10 @@ bool build_query(const pzk_params& p, Layout& L, std::string& why) {
     b.region(RK_Q_EDILN, Q_SZ_EDILN, {k});
     b.region(RK_Q_FEIE, Q_SZ_FEIE, {6 + k});
   }
-  // dg1Hasher (created before dg1Chunking[i]) = Poseidon5(4 x Bits2Num(186), skIndentityHasher) (:191-202)
+  // dg1Hasher (created before dg1Chunking[i]) = Poseidon5(4 x Bits2Num(186 | 190), skIndentityHasher) (:191-202)
   const size_t dgh_task = L.pos.size();
   const int S_DGC = b.poseidon(5, {V_DGC[0], V_DGC[1], V_DGC[2], V_DGC[3], -1}, 1);
-  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, q_num2bits(186), {186, 0, QI_DG1 + 186 * i, 1});
+  for (int i = 0; i < 4; i++) b.region(RK_BITS2NUM, q_num2bits(CH), {CH, 0, QI_DG1 + CH * i, 1});
   const int S_SKH2 = b.poseidon(1, {V_SK}, 0);
   L.pos[dgh_task].in_slot[4] = S_SKH2;
 
@@ -111,10 +128,10 @@ bool build_query(const pzk_params& p, Layout& L, std::string& why) {
   // own: skIdentity, pkPassHash, dgCommit, identityCounter, timestamp, idStateRoot, idStateSiblings[80] | treePosition
   b.region(RK_INCOPY, 2, {QI_SK});  // skIdentity, pkPassportHash (adjacent inputs)
   b.region(RK_VALUE, 1, {S_DGC});
-  b.region(RK_INCOPY, 1, {QI_IC});
-  b.region(RK_INCOPY, 1, {QI_TS});
+  b.region(RK_INCOPY, 1, {IN_IC});
+  b.region(RK_INCOPY, 1, {IN_TS});
   b.region(RK_INCOPY, 1, {QI_ROOT});
-  b.region(RK_INCOPY, Q_DEPTH, {QI_SIB});
+  b.region(RK_INCOPY, Q_DEPTH, {IN_SIB});
   const uint32_t r_pos = b.region(RK_VALUE, 1, {-1, -1});  // treePosition (slot patched below)
   // babyPbk: BabyjubjubBase8Multiplication: out[2] | scalar | getBase8, num2Bits(254), adders/doublers
   b.region(RK_BJJ_OWN, 3 + 2);
@@ -125,20 +142,20 @@ bool build_query(const pzk_params& p, Layout& L, std::string& why) {
   const int S_VAL = b.poseidon(3, {S_DGC, V_IC, V_TS}, 2);
   // SMTVerifier(80): isVerified | root, leaf, key, siblings[80] | value | hash1New, n2bNew, smtLevIns, sm[80],
   // levels[79..0], isEqual
-  b.region(RK_SMT_OWN, 1 + 3 + Q_DEPTH + 1, {QI_ROOT, QI_SIB});
+  b.region(RK_SMT_OWN, 1 + 3 + Q_DEPTH + 1, {QI_ROOT, IN_SIB});
   b.region(RK_SMTHASH, 3, {-1});
   const int S_LEAF = b.poseidon(3, {S_POS, S_VAL, V_ONE}, 4);
   b.region(RK_NUM2BITS, q_num2bits(254), {254, 0, S_POS});
-  b.region(RK_LEVINS, Q_DEPTH + Q_DEPTH + (Q_DEPTH - 1) + Q_DEPTH * 3, {QI_SIB});
+  b.region(RK_LEVINS, Q_DEPTH + Q_DEPTH + (Q_DEPTH - 1) + Q_DEPTH * 3, {IN_SIB});
   b.region(RK_SM, Q_DEPTH * 4);
   int S_H[Q_DEPTH];
   for (int i = 0; i < Q_DEPTH; i++) S_H[i] = b.value();
   for (int i = Q_DEPTH - 1; i >= 0; i--) {
-    b.region(RK_SMT_LEVEL, 8, {i, QI_SIB});
+    b.region(RK_SMT_LEVEL, 8, {i, IN_SIB});
     b.region(RK_SMTHASH, 3, {i});
     b.poseidon(2, {V_L[i], V_R[i]}, 5, S_H[i]);
     L.pos.back().smt_level = i;
-    b.region(RK_SWITCHER, SZ_SWITCHER, {i, QI_SIB});
+    b.region(RK_SWITCHER, SZ_SWITCHER, {i, IN_SIB});
   }
   b.region(RK_ISEQ_ROOT, SZ_ISEQUAL, {QI_ROOT});
   for (int i = 1; i < Q_DEPTH; i++)

@@ -204,6 +204,8 @@ struct RegInfo {
   // QueryIdentity: first of the 8 DG1DataExtractor outputs, first of the 240 CitizenshipCheck IsEqual inverses
   // (Montgomery), the citizenship's index in COUNTRY_ARR (raw u32 in limb 0; 240 = absent), the nullifier hash
   int32_t q_dgf, q_cinv, q_cidx, q_nul;
+  // QueryIdentityTD1 (document_type 1): 9 DG1 fields, dg1[760]; PoseidonHash(1) of documentNumber / personalNumber
+  int32_t q_td1, q_doch, q_persh;
 };
 
 // per-witness core sizes of the register-circuit kernels

@@ -189,15 +189,20 @@ __device__ __forceinline__ El q_ediln_sig(int s, const fr* T, uint64_t e1, uint6
 // the dates and conditions of one witness (inputs < 2^64 in the evaluated domain)
 struct QView {
   const uint8_t* row;
+  int ts, ic;  // input offsets of timestamp / identityCounter (after dg1, whose length depends on TD1 / TD3)
   __device__ __forceinline__ uint64_t in(int k) const { return in_u64(row + 32ull * k); }
 };
+__device__ __forceinline__ QView q_view(const DevLayout& L, const uint8_t* inputs, uint32_t w) {
+  const bool td1 = L.reg.q_td1 != 0;
+  return QView{inputs + 32ull * (uint64_t)w * L.n_inputs, q_in_ts(td1), q_in_ic(td1)};
+}
 // condition k of the ForceEqualIfEnabled checks (queryIdentity.circom:109-188); exp / birth: DG1 dates
 __device__ __forceinline__ int q_cond(const QView& Q, int k, uint64_t exp, uint64_t birth) {
   switch (k) {
-    case 0: return Q.in(QI_TS) >= Q.in(QI_TSLO);
-    case 1: return Q.in(QI_TS) < Q.in(QI_TSHI);
-    case 2: return Q.in(QI_IC) >= Q.in(QI_ICLO);
-    case 3: return Q.in(QI_IC) < Q.in(QI_ICHI);
+    case 0: return Q.in(Q.ts) >= Q.in(QI_TSLO);
+    case 1: return Q.in(Q.ts) < Q.in(QI_TSHI);
+    case 2: return Q.in(Q.ic) >= Q.in(QI_ICLO);
+    case 3: return Q.in(Q.ic) < Q.in(QI_ICHI);
     case 4: return q_edil_out(Q.in(QI_EDLO), exp);
     case 5: return q_edil_out(exp, Q.in(QI_EDHI));
     case 6: { const uint64_t c = Q.in(QI_CUR), lo = Q.in(QI_BDLO);
@@ -212,7 +217,9 @@ __device__ __forceinline__ int q_cond(const QView& Q, int k, uint64_t exp, uint6
 // one signal of a query region (emit_small, regemit.hpp)
 __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, const Region& R, uint32_t w, uint32_t s) {
   const RegInfo& G = L.reg;
-  const QView Q{B.inputs + 32ull * (uint64_t)w * L.n_inputs};
+  const QView Q = q_view(L, B.inputs, w);
+  const bool td1 = G.q_td1 != 0;
+  const int fcit = q_f_cit(td1);
   auto V = [&](int slot) { return fr_from_mont_fast(B.vs.at(slot, w)); };
   auto IN = [&](int k) { return el_load(Q.row + 32ull * k); };
   auto dg_u64 = [&](int k) { const fr v = V(G.q_dgf + k); return (uint64_t)v.v[0] | ((uint64_t)v.v[1] << 32); };
@@ -221,7 +228,10 @@ __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, con
     case RK_Q_OUT: {
       if (s == 0) return (sel & 1) ? el_fr(V(G.q_nul)) : el_zero();
       const int k = (int)s - 1;
-      return ((sel >> Q_OUT_SEL[k]) & 1) ? el_fr(V(G.q_dgf + k)) : el_zero();
+      if (!td1) return ((sel >> Q_OUT_SEL[k]) & 1) ? el_fr(V(G.q_dgf + k)) : el_zero();
+      // TD1: fields 0-5, PoseidonHash(1) of documentNumber / personalNumber, documentType
+      const int slot = k == 6 ? G.q_doch : k == 7 ? G.q_persh : G.q_dgf + (k == 8 ? 8 : k);
+      return ((sel >> Q1_OUT_SEL[k]) & 1) ? el_fr(V(slot)) : el_zero();
     }
     case RK_Q_SQ: {
       const fr x = fr_to_mont(load_fr(Q.row + 32ull * QI_EVDATA));
@@ -229,7 +239,7 @@ __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, con
     }
     case RK_Q_CMP: {  // GreaterEqThan(64) (even) / LessThan(64) (odd) of (timestamp | identityCounter, bound)
       const int k = R.a[0];
-      const int xi = k < 2 ? QI_TS : QI_IC, yi = k == 0 ? QI_TSLO : k == 1 ? QI_TSHI : k == 2 ? QI_ICLO : QI_ICHI;
+      const int xi = k < 2 ? Q.ts : Q.ic, yi = k == 0 ? QI_TSLO : k == 1 ? QI_TSHI : k == 2 ? QI_ICLO : QI_ICHI;
       const uint64_t x = Q.in(xi), y = Q.in(yi);
       if (k & 1) return q_lt_sig((int)s, 64, IN(xi), IN(yi), q_v64(x, 0, y, 0));
       // out | in[2] | LessThan(64)(in[1], in[0] + 1)
@@ -260,7 +270,7 @@ __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, con
                          : q_ediln_sig((int)s, B.inv_small, birth, Q.in(QI_BDHI), cur);
     }
     case RK_Q_CIT: {  // citizenship, blacklist | validCheck[241], bitmask[240]
-      if (s == 0) return el_fr(V(G.q_dgf + 5));
+      if (s == 0) return el_fr(V(G.q_dgf + fcit));
       if (s == 1) return IN(QI_CMASK);
       if (s < 243) return el_u64((uint32_t)(s - 2) > B.vs.at(G.q_cidx, w).v[0]);
       const fr m = load_fr(Q.row + 32ull * QI_CMASK);
@@ -268,7 +278,7 @@ __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, con
     }
     default: {  // RK_Q_CITEQ: isEqual[i] (COUNTRY_ARR[i], citizenship), isEqual2[i] (1, bitmask[i])
       const uint32_t i = s / 12, r = s % 12;
-      if (r < 6) return iseq_sig((int)r, Q_COUNTRY[i], dg_u64(5), V(G.q_cinv + (int)i));
+      if (r < 6) return iseq_sig((int)r, Q_COUNTRY[i], dg_u64(fcit), V(G.q_cinv + (int)i));
       const fr m = load_fr(Q.row + 32ull * QI_CMASK);
       const uint32_t bm = q_bit(m, 239 - (int)i);
       const fr pm1 = fr_sub(fr_zero(), fr_u64(1));
@@ -293,22 +303,26 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
   if (w >= vs.batch) return;  // whole wave
   const int lane = threadIdx.x;
   const RegInfo& R = L.reg;
-  const QView Q{inputs + 32ull * (uint64_t)w * L.n_inputs};
+  const QView Q = q_view(L, inputs, w);
+  const bool td1 = R.q_td1 != 0;
   bool bad = false;
   if (lane == 0) vs.at(R.v_one, w) = fr_mont_one();
-  uint64_t f64[8];
+  uint64_t f64[9];
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const fr v = wave_bits_fr(Q.row, QI_DG1 + Q_DGX_SHIFT[k], Q_DGX_L[k], -1, bad);
+  for (int k = 0; k < 9; k++) {
+    if (k == 8 && !td1) { f64[k] = 0; continue; }
+    const int Lk = td1 ? Q1_DGX_L[k] : Q_DGX_L[k], Sk = td1 ? Q1_DGX_SHIFT[k] : Q_DGX_SHIFT[k];
+    const fr v = wave_bits_fr(Q.row, QI_DG1 + Sk, Lk, -1, bad);
     f64[k] = (uint64_t)v.v[0] | ((uint64_t)v.v[1] << 32);
     if (lane == 0) vs.at(R.q_dgf + k, w) = fr_to_mont(v);
   }
-  for (int i = 0; i < 4; i++) {  // dg1Chunking[i] = Bits2Num(186), in[j] = dg1[186 i + j] (queryIdentity.circom:192-198)
-    const fr v = wave_bits_fr(Q.row, QI_DG1 + 186 * i, 186, +1, bad);
+  const int CH = q_chunk(td1);
+  for (int i = 0; i < 4; i++) {  // dg1Chunking[i] = Bits2Num(186 | 190), in[j] = dg1[CH i + j] (queryIdentity.circom:192-198)
+    const fr v = wave_bits_fr(Q.row, QI_DG1 + CH * i, CH, +1, bad);
     if (lane == 0) vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
   }
   // CitizenshipCheck: index of the citizenship in COUNTRY_ARR and 1 / (citizenship - COUNTRY_ARR[i])
-  const uint64_t cit = f64[5];
+  const uint64_t cit = f64[q_f_cit(td1)];
   int first = 240;
   fr d[4], pre[4];
   fr acc = fr_mont_one();
@@ -341,7 +355,7 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
   { fr ix = fr_zero(); ix.v[0] = (uint32_t)first; vs.at(R.q_cidx, w) = ix; }
   int32_t* st = status ? status + w : nullptr;
   // inputs read as 64-bit integers: bounds, dates, timestamp, counter (the evaluated domain)
-  const int u64_in[11] = {QI_CUR, QI_TSLO, QI_TSHI, QI_ICLO, QI_ICHI, QI_BDLO, QI_BDHI, QI_EDLO, QI_EDHI, QI_TS, QI_IC};
+  const int u64_in[11] = {QI_CUR, QI_TSLO, QI_TSHI, QI_ICLO, QI_ICHI, QI_BDLO, QI_BDHI, QI_EDLO, QI_EDHI, Q.ts, Q.ic};
   for (int k = 0; k < 11; k++) bad |= !in_is_u64(Q.row + 32ull * u64_in[k]);
   if (bad) set_status(st, ST_INPUT_RANGE);
   const uint64_t exp = f64[1], birth = f64[0], cur = Q.in(QI_CUR);

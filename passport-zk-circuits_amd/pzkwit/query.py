@@ -22,12 +22,22 @@ NAMES = ["eventID", "eventData", "idStateRoot", "selector", "currentDate", "time
 LENGTHS = {"dg1": 744, "idStateSiblings": 80}
 N_INPUTS = 842
 DEPTH = 80
-OFF = {}
-_o = 0
-for _n in NAMES:
-    OFF[_n] = _o
-    _o += LENGTHS.get(_n, 1)
-assert _o == N_INPUTS
+# QueryIdentityTD1 (queryIdentityTD1.circom): dg1[760], the rest identical
+LENGTHS_TD1 = {"dg1": 760, "idStateSiblings": 80}
+N_INPUTS_TD1 = 858
+
+
+def _offsets(lengths):
+    off, o = {}, 0
+    for n in NAMES:
+        off[n] = o
+        o += lengths.get(n, 1)
+    return off, o
+
+
+OFF, _n3 = _offsets(LENGTHS)
+OFF_TD1, _n1 = _offsets(LENGTHS_TD1)
+assert _n3 == N_INPUTS and _n1 == N_INPUTS_TD1
 
 # CitizenshipCheck COUNTRY_ARR (data/citizenship_codes.inc, extracted from citizenshipCheck.circom)
 _INC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "citizenship_codes.inc")
@@ -89,10 +99,10 @@ def smt_root(key, value, siblings):
 _MRZ = b"ABCDEFGHIJKLMNOPQRSTUVWXYZ<"
 
 
-def make_query(rng, depth=None, selector=None, cit_code=None, **over):
+def make_query(rng, depth=None, selector=None, cit_code=None, td1=False, **over):
     """One valid query: -> (inputs dict of python ints / lists, info dict). `over` replaces inputs after
     generation (the SMT root is NOT recomputed for them); cit_code: a 3-byte issuing-state code for the DG1
-    (the identity state is built over that DG1)."""
+    (the identity state is built over that DG1); td1: a TD1 (ID card) DG1 for QueryIdentityTD1."""
     C = countries()
     cidx = rng.below(240)
     cit = C[cidx].to_bytes(3, "big") if cit_code is None else cit_code
@@ -102,19 +112,28 @@ def make_query(rng, depth=None, selector=None, cit_code=None, **over):
     name = bytes(_MRZ[rng.below(len(_MRZ))] for _ in range(39))
     docnum = bytes(b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"[rng.below(36)] for _ in range(9))
     sex = b"MF<"[rng.below(3):][:1]
-    line1 = b"P<" + cit + name
-    line2 = (docnum + b"0" + nat + b"%02d%02d%02d" % (by, bm, bd) + b"0" + sex + b"%02d%02d%02d" % (ey, em, ed) +
-             b"0" + b"<" * 14 + b"00")
-    assert len(line1) == 44 and len(line2) == 44
-    dg1 = bytes.fromhex("615b5f1f58") + line1 + line2
+    if not td1:
+        line1 = b"P<" + cit + name
+        line2 = (docnum + b"0" + nat + b"%02d%02d%02d" % (by, bm, bd) + b"0" + sex + b"%02d%02d%02d" % (ey, em, ed) +
+                 b"0" + b"<" * 14 + b"00")
+        assert len(line1) == 44 and len(line2) == 44
+        dg1 = bytes.fromhex("615b5f1f58") + line1 + line2
+    else:  # TD1: 3 x 30 MRZ characters (ICAO 9303-5): type, state, number, optional data | dates, sex, nationality | name
+        pers = bytes(b"0123456789"[rng.below(10)] for _ in range(11))
+        l1 = b"ID" + cit + docnum + b"0" + pers + b"<" * 4
+        l2 = b"%02d%02d%02d" % (by, bm, bd) + b"0" + sex + b"%02d%02d%02d" % (ey, em, ed) + b"0" + nat + b"<" * 11 + b"0"
+        l3 = name[:30]
+        assert len(l1) == 30 and len(l2) == 30 and len(l3) == 30
+        dg1 = bytes.fromhex("615d5f1f5a") + l1 + l2 + l3
     bits = np.unpackbits(np.frombuffer(dg1, dtype=np.uint8)).astype(int).tolist()
-    assert len(bits) == 744
+    assert len(bits) == (760 if td1 else 744)
     sk = rng.fr() >> 2
     pk_pass = rng.fr()
     ts = 1_700_000_000 + rng.below(100_000_000)
     ic = rng.below(1000)
     # identity state: value = Poseidon3(dgCommit, counter, timestamp), key = Poseidon2(pkPassHash, pkIdentityHash)
-    chunks = [int("".join(map(str, bits[186 * i:186 * (i + 1)]))[::-1] or "0", 2) for i in range(4)]
+    ch = 190 if td1 else 186
+    chunks = [int("".join(map(str, bits[ch * i:ch * (i + 1)]))[::-1] or "0", 2) for i in range(4)]
     sk_h = poseidon([sk])
     dg_commit = poseidon(chunks + [sk_h])
     ax, ay = bjj_mul(sk)
@@ -138,41 +157,50 @@ def make_query(rng, depth=None, selector=None, cit_code=None, **over):
         "timestamp": ts, "identityCounter": ic,
     }
     inp.update(over)
-    fields = [int.from_bytes(dg1[o // 8:o // 8 + n // 8], "big") for o, n in
-              ((496, 48), (560, 48), (80, 248), (328, 64), (472, 24), (56, 24), (552, 8), (392, 72))]
+    spec = (((280, 48), (344, 48), (520, 240), (400, 24), (56, 24), (336, 8), (80, 72), (160, 88), (40, 16)) if td1 else
+            ((496, 48), (560, 48), (80, 248), (328, 64), (472, 24), (56, 24), (552, 8), (392, 72)))
+    fields = [int.from_bytes(dg1[o // 8:o // 8 + n // 8], "big") for o, n in spec]
     info = {"fields": fields, "nullifier": poseidon([sk, sk_h, inp["eventID"]]), "dg_commit": dg_commit,
-            "pk_identity": (ax, ay), "key": key, "value": value, "depth": d, "citizenship_index": cidx}
+            "pk_identity": (ax, ay), "key": key, "value": value, "depth": d, "citizenship_index": cidx, "td1": td1}
     return inp, info
 
 
 def pack(inp, out=None):
-    """inputs dict -> (842, 32) uint8 row (normal form, little-endian)."""
-    row = out if out is not None else np.zeros((N_INPUTS, 32), dtype=np.uint8)
+    """inputs dict -> (842 | 858 (TD1), 32) uint8 row (normal form, little-endian)."""
+    td1 = len(inp["dg1"]) == 760
+    lengths, off = (LENGTHS_TD1, OFF_TD1) if td1 else (LENGTHS, OFF)
+    row = out if out is not None else np.zeros((N_INPUTS_TD1 if td1 else N_INPUTS, 32), dtype=np.uint8)
     for name in NAMES:
         v = inp[name]
         vals = v if isinstance(v, (list, tuple)) else [v]
-        assert len(vals) == LENGTHS.get(name, 1), name
+        assert len(vals) == lengths.get(name, 1), name
         for i, x in enumerate(vals):
-            row[OFF[name] + i] = np.frombuffer((int(x) % P).to_bytes(32, "little"), dtype=np.uint8)
+            row[off[name] + i] = np.frombuffer((int(x) % P).to_bytes(32, "little"), dtype=np.uint8)
     return row
 
 
 def public_outputs(inp, info):
     """Main outputs [nullifier, birthDate, expirationDate, name, nameResidual, nationality, citizenship, sex,
-    documentNumber], each masked by its selector bit (queryIdentity.circom:86-105)."""
+    documentNumber] (TD1: [nullifier, birthDate, expirationDate, name, nationality, citizenship, sex,
+    Poseidon1(documentNumber), Poseidon1(personalNumber), documentType]), each masked by its selector bit
+    (queryIdentity.circom:86-105, queryIdentityTD1.circom:97-105)."""
     sel = inp["selector"]
     bit = lambda k: (sel >> k) & 1  # noqa: E731
     out = [info["nullifier"] * bit(0)]
+    f = info["fields"]
+    if info.get("td1"):
+        out += [f[k] * bit(k + 1) for k in range(6)]
+        return out + [poseidon([f[6]]) * bit(7), poseidon([f[7]]) * bit(16), f[8] * bit(17)]
     for k, b in enumerate((1, 2, 3, 3, 4, 5, 6, 7)):
-        out.append(info["fields"][k] * bit(b))
+        out.append(f[k] * bit(b))
     return out
 
 
-def batch_rows(batch, seed=0x9, distinct=64, depth=None):
-    """(batch, 842, 32) rows: `distinct` generated queries repeated (generation is host Python, ~40 ms each)."""
+def batch_rows(batch, seed=0x9, distinct=64, depth=None, td1=False):
+    """(batch, 842 | 858, 32) rows: `distinct` generated queries repeated (generation is host Python, ~40 ms each)."""
     rng = SplitMix64(seed)
-    uniq = [pack(make_query(rng, depth=depth)[0]) for _ in range(min(batch, distinct))]
-    out = np.empty((batch, N_INPUTS, 32), dtype=np.uint8)
+    uniq = [pack(make_query(rng, depth=depth, td1=td1)[0]) for _ in range(min(batch, distinct))]
+    out = np.empty((batch, uniq[0].shape[0], 32), dtype=np.uint8)
     for i in range(batch):
         out[i] = uniq[i % len(uniq)]
     return out

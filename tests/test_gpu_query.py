@@ -17,31 +17,38 @@ def inst():
     return native.Instance(native.PZK_CIRCUIT_QUERY, 80)
 
 
-def _compare(oracle, rows, wit, st, codes):
+@pytest.fixture(scope="module")
+def inst_td1():
+    return native.Instance(native.PZK_CIRCUIT_QUERY, 80, {"doc": 1})
+
+
+def _compare(oracle, rows, wit, st, codes, td1=False):
     for b in range(rows.shape[0]):
-        rc, ref = oracle.query_witness(rows[b])
+        rc, ref = oracle.query_witness(rows[b], td1=td1)
         assert rc == codes[b] == st[b], (b, rc, codes[b], st[b])
         bad = np.nonzero((ref != wit[b]).any(axis=1))[0]
         assert bad.size == 0, "row %d: %d mismatching signals, first %d" % (b, bad.size, bad[0])
 
 
-def test_query_matches_oracle(oracle, inst):
-    assert inst.witness_size == oracle.query_sizes()[1] and inst.n_inputs == Q.N_INPUTS
-    rng = SplitMix64(0x5151)
+@pytest.mark.parametrize("td1", [False, True])
+def test_query_matches_oracle(oracle, inst, inst_td1, td1):
+    I = inst_td1 if td1 else inst
+    assert I.witness_size == oracle.query_sizes(td1)[1] and I.n_inputs == (Q.N_INPUTS_TD1 if td1 else Q.N_INPUTS)
+    rng = SplitMix64(0x5151 + td1)
     rows, codes = [], []
     for k in range(40):
         sel = [0, (1 << 18) - 1, None, None][k % 4]
         depth = [0, 1, 79, 40, None][k % 5]
-        inp, _ = Q.make_query(rng, selector=sel, depth=depth)
+        inp, _ = Q.make_query(rng, selector=sel, depth=depth, td1=td1)
         rows.append(Q.pack(inp))
         codes.append(0)
     for i, kind in enumerate(FAIL_KINDS):  # one failing lane per check site, between valid ones
-        inp, code = _fail_case(kind, SplitMix64(0x77 + i))
+        inp, code = _fail_case(kind, SplitMix64(0x77 + i), td1)
         rows.insert(3 * i + 1, Q.pack(inp))
         codes.insert(3 * i + 1, code)
     rows = np.stack(rows)
-    wit, st = inst.witness_batch_host(rows)
-    _compare(oracle, rows, wit, st, codes)
+    wit, st = I.witness_batch_host(rows)
+    _compare(oracle, rows, wit, st, codes, td1)
 
 
 def test_query_full_batch(oracle, inst):
@@ -61,17 +68,18 @@ def test_query_full_batch(oracle, inst):
     _compare(oracle, batch[[0, 63, 4095]], wit[[0, 63, 4095]], st[[0, 63, 4095]], [0, 0, 0])
 
 
-def test_query_device_witnesses_satisfy_constraints(inst):
-    """Device witnesses through the independent constraint checker (oracle/r1cs_query.inc.c): 140,542
-    constraints hold and every signal is read by one."""
+@pytest.mark.parametrize("td1", [False, True])
+def test_query_device_witnesses_satisfy_constraints(inst, inst_td1, td1):
+    """Device witnesses through the independent constraint checker (oracle/r1cs_query.inc.c): every constraint
+    holds and every signal is read by one."""
     import pyr1cs
     rng = SplitMix64(0xC1)
-    rows = np.stack([Q.pack(Q.make_query(rng, selector=s, depth=d)[0])
+    rows = np.stack([Q.pack(Q.make_query(rng, selector=s, depth=d, td1=td1)[0])
                      for s, d in ((0, 0), ((1 << 18) - 1, 79), (None, 40), (None, None))])
-    wit, st = inst.witness_batch_host(rows)
+    wit, st = (inst_td1 if td1 else inst).witness_batch_host(rows)
     assert (st == 0).all()
     for b in range(rows.shape[0]):
-        rc, rep = pyr1cs.check_query(wit[b])
+        rc, rep = pyr1cs.check_query(wit[b], td1=td1)
         assert rc == 0 and rep["n_failed"] == 0 and rep["n_uncovered"] == 0, (b, rep)
 
 

@@ -17,5 +17,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 tools/kstats.py $O/prof/run_kernel_stats.csv > $O/prof_stats.txt 2>&1; head -4 $O/prof_stats.txt
 timeout -k 10 300 python -u bench.py --workload query --steps 10 > $O/bench_query.json 2> $O/bench_query.err || { tail -20 $O/bench_query.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_query.json')); print('query', d['value'], d['cpu_baseline']['value'])"
+timeout -k 10 300 python -u bench.py --workload query-td1 --steps 10 --no-cpu > $O/bench_query_td1.json 2> $O/bench_query_td1.err || { tail -20 $O/bench_query_td1.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_query_td1.json')); print('query-td1', d['value'])"
 timeout -k 10 400 python -u bench.py --workload mixed --steps 3 --warmup 1 > $O/bench_mixed.json 2> $O/bench_mixed.err || { tail -20 $O/bench_mixed.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_mixed.json')); print('mixed', d['value'])"

@@ -303,6 +303,29 @@ __device__ __forceinline__ fr fr_shfl_down(const fr& a, unsigned d) {
   return r;
 }
 
+// Batched inversion across a G-lane group (G a power of two dividing 64): given each lane's product acc, return the
+// product of the OTHER lanes' values and the group total, by an inclusive prefix scan and suffix scan (2 log2 G + 1
+// products per lane; the gather-all loop it replaces took 2 G).
+template <int G>
+__device__ __forceinline__ void fr_group_others(const fr& acc, fr& others, fr& total) {
+  static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "G: a power of two <= 64");
+  const int l = (int)(threadIdx.x & (G - 1));
+  auto up = [](const fr& a, int d) { fr r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl_up((int)a.v[k], d, G); return r; };
+  auto down = [](const fr& a, int d) { fr r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, G); return r; };
+  fr p = acc, s = acc;
+#pragma unroll
+  for (int d = 1; d < G; d <<= 1) {
+    const fr u = up(p, d), v = down(s, d);
+    if (l >= d) p = fr_mul(p, u);
+    if (l + d < G) s = fr_mul(s, v);
+  }
+  fr pe = up(p, 1), se = down(s, 1);
+  if (l == 0) pe = fr_mont_one();
+  if (l == G - 1) se = fr_mont_one();
+  others = fr_mul(pe, se);
+  total = fr_shfl(p, G - 1, G);
+}
+
 // ---- wave-contiguous element stores
 // Emitters produce one 32-byte element per lane. Stored directly that is 32 B per lane per
 // store pair; staged through LDS it becomes two 1 KiB fully contiguous wave stores of 16 B per

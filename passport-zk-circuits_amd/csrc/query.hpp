@@ -337,12 +337,8 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
     pre[j] = acc;
     if (!fr_is_zero(d[j])) acc = fr_mul(acc, d[j]);
   }
-  fr others = fr_mont_one(), total = fr_mont_one();
-  for (int t = 0; t < 64; t++) {
-    const fr pt = fr_shfl(acc, t, 64);
-    total = fr_mul(total, pt);
-    if (t != lane) others = fr_mul(others, pt);
-  }
+  fr others, total;
+  fr_group_others<64>(acc, others, total);
   fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
 #pragma unroll
   for (int j = 3; j >= 0; j--) {

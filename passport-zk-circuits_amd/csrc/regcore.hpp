@@ -579,12 +579,8 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
     S(PRE + qi) = acc;
     if (!fr_is_zero(e)) acc = fr_mul(acc, e);
   }
-  fr others = fr_mont_one(), total = fr_mont_one();
-  for (int t = 0; t < BJJ_SEGS; t++) {
-    fr pt = fr_shfl(acc, t, BJJ_SEGS);
-    total = fr_mul(total, pt);
-    if (t != seg) others = fr_mul(others, pt);
-  }
+  fr others, total;
+  fr_group_others<BJJ_SEGS>(acc, others, total);
   fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
   fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
   for (int qi = NQ - 1; qi >= 0; qi--) {
@@ -639,13 +635,8 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
     core[i0 + k] = acc;
     if (!z) acc = fr_mul(acc, sm[k]);
   }
-  fr others = fr_mont_one(), total = fr_mont_one();
-#pragma unroll
-  for (int t = 0; t < G; t++) {
-    const fr pt = fr_shfl(acc, t, G);
-    total = fr_mul(total, pt);
-    if (t != seg) others = fr_mul(others, pt);
-  }
+  fr others, total;
+  fr_group_others<G>(acc, others, total);
   fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
 #pragma unroll
   for (int k = NL - 1; k >= 0; k--) {

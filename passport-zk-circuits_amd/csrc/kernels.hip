@@ -387,7 +387,7 @@ hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_
 // k_smt_chain's lane groups then take witnesses in this order, so a wave holds proofs of (nearly) one depth and
 // finishes after its own depth, not after the deepest of 16 random ones (with uniform depths 0-79 that halves the
 // chain's SIMD time; the kernel itself still lasts as long as the deepest proof).
-__global__ void __launch_bounds__(1024) k_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order,
+__global__ void __launch_bounds__(256) k_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order,
                                                     uint32_t batch) {
   constexpr int NB = SMT_LEVELS + 1;
   __shared__ uint32_t cnt[NB], at[NB];
@@ -407,7 +407,9 @@ __global__ void __launch_bounds__(1024) k_smt_order(const fr* smt_core, uint32_t
   for (uint32_t w = threadIdx.x; w < batch; w += blockDim.x) order[atomicAdd(&at[level(w)], 1u)] = w;
 }
 hipError_t launch_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order, uint32_t batch, hipStream_t st) {
-  hipLaunchKernelGGL(k_smt_order, dim3(1), dim3(1024), 0, st, smt_core, smt_core_fr, order, batch);
+  // 256 threads: one workgroup that fits beside the emitters' waves on any CU (a 1024-thread group waited
+  // ~1.7 ms for a CU with 16 free wave slots inside the concurrent config-3 run)
+  hipLaunchKernelGGL(k_smt_order, dim3(1), dim3(256), 0, st, smt_core, smt_core_fr, order, batch);
   return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ struct PosConsts {
   const fr* base;   // Montgomery-form constants
   const fr* nbase;  // the same constants in normal form
   PosParamIndex ix;
+  const fr* sbase;  // partial-round products S[i] * C[5t + r] (Montgomery) at S's indices (k_pos_sc, runtime.cpp)
+  __device__ __forceinline__ const fr& SC(int t, int i) const { return sbase[ix.s_off[t] + i]; }
   __device__ __forceinline__ const fr& Cn(int t, int i) const { return nbase[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& C(int t, int i) const { return base[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& M(int t, int i, int j) const { return base[ix.m_off[t] + i * t + j]; }
@@ -155,21 +157,37 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
     fr a = act ? fr_add(pow5(st), K.C(t, (r + 1) * t + jj)) : fr_zero();
     st = mix(a, r == 3);
   }
-  for (int r = 0; r < RP; r++) {  // partial rounds: 4 product times per round (was 5)
+  for (int r = 0; r < RP; r++) {  // partial rounds
     if (act) out[o + j] = st;
     o += t;
     const int sb = (2 * t - 1) * r;
-    // one product on every lane: lane 0 squares its state (the S-box's first step), lanes 1..t-1 take their
-    // sparse-matrix terms S[k] * st_k, which do not depend on the S-box
-    const fr p = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
-    fr s0 = fr_zero();
-    if (j == 0) s0 = fr_add(fr_mul(fr_sqr(p), st), K.C(t, 5 * t + r));
-    s0 = fr_shfl(s0, gb, 64);
-    // one product on every lane: lane 0's term S[0] * s0, the others' updates s0 * S'[k]
-    const fr q = fr_mul(j == 0 ? K.S(t, sb) : K.S(t, sb + t + jj - 1), s0);
-    const fr sum = group_sum(j == 0 ? q : act ? p : fr_zero());
-    if (j == 0) st = sum;
-    else if (act) st = fr_add(st, q);
+    if constexpr (G > T) {
+      // 3 product times per round, with the group's spare lane t: s0 = x^5 + C with x = st_0, and
+      //   lane 0:   st_0' = S[0] s0 + sum_k S[k] st_k      (S[0] s0 = x^3 (S[0] x^2) + S[0] C)
+      //   lane k:   st_k' = st_k + S'[k] s0                (S'[k] s0 = x^3 (S'[k] x^2) + S'[k] C)
+      // A: lane 0 x^2, lanes k their terms S[k] st_k | B: lane 0 x^3, lanes k S'[k] x^2, lane t S[0] x^2 |
+      // C: every lane x^3 times its B product. The S * C constants come precomputed (K.SC).
+      const fr a = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
+      const fr x2 = fr_shfl(a, gb, 64);
+      const fr b = fr_mul(j == 0 ? st : act ? K.S(t, sb + t + jj - 1) : K.S(t, sb), x2);
+      const fr x3 = fr_shfl(b, gb, 64), s0x2 = fr_shfl(b, gb + t, 64);
+      const fr c = fr_mul(x3, j == 0 ? s0x2 : b);
+      const fr sum = group_sum(j == 0 ? fr_add(c, K.SC(t, sb)) : act ? a : fr_zero());
+      if (j == 0) st = sum;
+      else if (act) st = fr_add(st, fr_add(c, K.SC(t, sb + t + jj - 1)));
+    } else {
+      // 4 product times (no spare lane: t = 4 on 4 lanes): one product on every lane: lane 0 squares its state
+      // (the S-box's first step), lanes 1..t-1 take their sparse-matrix terms S[k] * st_k
+      const fr p = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
+      fr s0 = fr_zero();
+      if (j == 0) s0 = fr_add(fr_mul(fr_sqr(p), st), K.C(t, 5 * t + r));
+      s0 = fr_shfl(s0, gb, 64);
+      // one product on every lane: lane 0's term S[0] * s0, the others' updates s0 * S'[k]
+      const fr q = fr_mul(j == 0 ? K.S(t, sb) : K.S(t, sb + t + jj - 1), s0);
+      const fr sum = group_sum(j == 0 ? q : act ? p : fr_zero());
+      if (j == 0) st = sum;
+      else if (act) st = fr_add(st, q);
+    }
   }
   for (int r = 0; r < 3; r++) {  // full rounds 4..6
     if (act) out[o + j] = st;

@@ -246,6 +246,16 @@ __global__ void k_to_mont_inplace(fr* a, int n) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) a[i] = fr_to_mont(a[i]);
 }
+// partial-round constant products for pos_core_group: sc[S index] = S[i] * C[5t + r] at i = (2t-1) r (the
+// S[0] term) and i = (2t-1) r + t + k - 1 (the S'[k] updates); Montgomery in, Montgomery out
+__global__ void k_pos_sc(const fr* m, fr* sc, PosParamIndex ix) {
+  const int t = blockIdx.x + 2, r = threadIdx.x;
+  if (t > POS_MAX_T || ix.nrp[t] == 0 || r >= ix.nrp[t]) return;
+  const fr c = m[ix.c_off[t] + 5 * t + r];
+  const int sb = ix.s_off[t] + (2 * t - 1) * r;
+  sc[sb] = fr_mul(m[sb], c);
+  for (int k = 1; k < t; k++) sc[sb + t + k - 1] = fr_mul(m[sb + t + k - 1], c);
+}
 
 static int load_poseidon(pzk_instance* I) {
   std::string path = data_dir() + "/poseidon_t2_6.bin";
@@ -281,12 +291,16 @@ static int load_poseidon(pzk_instance* I) {
     off += 32 * n_el;
   }
   int n = (int)(consts.size() / 32);
-  // two copies: Montgomery form (cores) and normal form (the emitters' round-constant adds)
-  HIPCHK(hipMalloc(&I->d_pos_consts, 2 * consts.size()));
+  // three copies: Montgomery form (cores), normal form (the emitters' round-constant adds), and the partial-round
+  // products S * C (k_pos_sc) at S's indices
+  HIPCHK(hipMalloc(&I->d_pos_consts, 3 * consts.size()));
   HIPCHK(hipMemcpy(I->d_pos_consts, consts.data(), consts.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(I->d_pos_consts + n, consts.data(), consts.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(I->d_pos_consts + 2 * n, 0, consts.size()));
   I->pos_consts_n = n;
   hipLaunchKernelGGL(k_to_mont_inplace, dim3((n + 255) / 256), dim3(256), 0, 0, I->d_pos_consts, n);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_pos_sc, dim3(POS_MAX_T - 1), dim3(64), 0, 0, I->d_pos_consts, I->d_pos_consts + 2 * n, I->pix);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   return 0;
@@ -696,7 +710,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
   ValueStore vs{S.d_values, B};
-  PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix};
+  PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix, I->d_pos_consts + 2 * I->pos_consts_n};
   Bufs bufs{d_inputs, S.d_sha_core, S.d_rsa_core, S.d_pos_core, S.d_bjj_core, S.d_smt_core, vs, d_wtns, stride,
             d_status, S.d_ec_core, S.d_ec_inv, S.d_ec_tab, I->d_inv_small, S.d_derived};
   Timing* T = nullptr;

@@ -186,11 +186,6 @@ __device__ __forceinline__ El emit_small(const DevLayout& L, const Bufs& B, cons
 
 // ------------------------------------------------------------------ Bits2Num / Num2Bits (+ AliasCheck)
 // one workgroup per (region, witness): the L-bit value is assembled in LDS first.
-__device__ __forceinline__ void u192_add(uint64_t* a, uint64_t lo, uint64_t hi) {
-  uint64_t s = a[0] + lo; uint64_t c = s < lo; a[0] = s;
-  uint64_t t = a[1] + hi; uint64_t c2 = t < hi; uint64_t t2 = t + c; c2 += t2 < t; a[1] = t2; a[2] += c2;
-}
-
 // CompConstant(p-1) part i (compconstant.circom:28-46): a = 2^i, b = 2^128 - 2^i
 __device__ __forceinline__ void alias_part(const W256& bits, int i, uint64_t& lo, uint64_t& hi) {
   W256 pm1; for (int k = 0; k < 8; k++) pm1.v[k] = P_[k];
@@ -276,9 +271,27 @@ __global__ void __launch_bounds__(256) k_emit_bits(DevLayout L, const Work* work
   __syncthreads();
   W256 V; for (int i = 0; i < 8; i++) V.v[i] = val[i];
   if (Lb == 254) {
+    // CompConstant's sum of its 127 parts: one part per thread, summed as four 32-bit columns in LDS (127 * 2^32
+    // fits 64 bits), then one carry pass (a serial 127-step loop on thread 0 held the whole workgroup)
+    __shared__ unsigned long long col[4];
+    if (threadIdx.x < 4) col[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x < 127) {
+      uint64_t lo, hi;
+      alias_part(V, threadIdx.x, lo, hi);
+      atomicAdd(&col[0], (unsigned long long)(uint32_t)lo);
+      atomicAdd(&col[1], (unsigned long long)(lo >> 32));
+      atomicAdd(&col[2], (unsigned long long)(uint32_t)hi);
+      atomicAdd(&col[3], (unsigned long long)(hi >> 32));
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-      uint64_t acc[3] = {0, 0, 0};
-      for (int i = 0; i < 127; i++) { uint64_t lo, hi; alias_part(V, i, lo, hi); u192_add(acc, lo, hi); }
+      uint32_t l[6];
+      uint64_t c = 0;
+      for (int k = 0; k < 4; k++) { c += col[k]; l[k] = (uint32_t)c; c >>= 32; }
+      l[4] = (uint32_t)c; l[5] = (uint32_t)(c >> 32);
+      uint64_t acc[3];
+      for (int k = 0; k < 3; k++) acc[k] = (uint64_t)l[2 * k] | ((uint64_t)l[2 * k + 1] << 32);
       sout[0] = acc[0]; sout[1] = acc[1]; sout[2] = acc[2];
       W256 so = u192_w(acc);
       if (w_bit(so, 127) && B.status) lane_status(B.status + w, ST_ALIAS);

@@ -15,6 +15,7 @@
 #include "bufs.hpp"
 #include "ec_common.hpp"
 #include "poseidon.hpp"
+#include "query_layout.hpp"
 
 using namespace pzk;
 
@@ -1101,6 +1102,7 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
   if (name) *name = PHASE_NAMES[phase];
   if (kernel) {
     *kernel = PHASE_KERNELS[phase];
+    if (phase == PH_PREP && I->lay.is_query) *kernel = "k_qry_prep";
     if (phase == PH_EMIT_SHA) {  // the SHA-2 and SHA-1 emitters share the phase: name the ones this instance runs
       const bool s2 = !I->lay.work[E_SHA].empty() || !I->lay.work[E_SHAD].empty(), s1 = !I->lay.work[E_SHA1].empty();
       const bool s5 = !I->lay.work[E_SHA5].empty() || !I->lay.work[E_SHA5D].empty();
@@ -1139,7 +1141,10 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
       else if (G.aa) el += 4 * 200 + 224;
       b += 32ull * (el + 4ull * G.dg1_chunk) + 32;
     }
-    if (phase == PH_SMT && L.is_register)  // siblings, root and key read; SMT core and the
+    if (phase == PH_PREP && L.is_query)  // k_qry_prep: the DG1 bits and the scalar inputs it reads (QI_EVID ..
+      b += 32ull * (q_dg1_len(L.reg.q_td1) + QI_DG1) +  // QI_PKPASS) + the value slots written: DG1 fields, dg1
+           32ull * (9 + 4 + 1 + 240);                   // chunks, citizenship index and its 240 IsEqual inverses
+    if (phase == PH_SMT && (L.is_register || L.is_query))  // siblings, root and key read; SMT core and the
       b += 32ull * (SMT_LEVELS + 2) + 32ull * SMT_CORE_FR + 32ull * 2 * SMT_LEVELS;  // level hash inputs written
     if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;

@@ -29,7 +29,7 @@ hipError_t launch_pss(const DevLayout& L, int stage, const uint64_t* rsa_core, c
                       uint8_t* derived, uint32_t batch, hipStream_t st);
 hipError_t launch_pos_core(const PosConsts& K, const PosTask* d_tasks, const PosTask* h_tasks, uint32_t first,
                            uint32_t count, ValueStore vs, fr* pos_core, uint32_t core_elems, const fr* smt_core,
-                           uint32_t smt_core_fr, hipStream_t st);
+                           uint32_t smt_core_fr, const uint32_t* order, hipStream_t st);  // order: k_smt_order's
 hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core, ValueStore vs,
                        int32_t* status, hipStream_t st);
 hipError_t launch_rsa_check(const DevLayout& L, const uint8_t* inputs, const uint32_t* sha_core,

@@ -723,11 +723,12 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     T->head = (T->head + 1) % Timing::RING;
     T->pending[slot] = true;
   }
-  auto pos_levels = [&](int lo, int hi) -> int {
+  // order: the SMT level hashes' witness order (k_smt_order, depth sorted), or null (witness order)
+  auto pos_levels = [&](int lo, int hi, const uint32_t* order = nullptr) -> int {
     for (int l = lo; l < hi && l + 1 < (int)lay.pos_level_start.size(); l++) {
       uint32_t a = lay.pos_level_start[l], b = lay.pos_level_start[l + 1];
       HIPCHK(launch_pos_core(K, I->d_pos, lay.pos.data(), a, b - a, vs, S.d_pos_core, lay.pos_core_elems,
-                             S.d_smt_core, lay.smt_core_fr, st));
+                             S.d_smt_core, lay.smt_core_fr, order, st));
     }
     return 0;
   };
@@ -758,10 +759,10 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     HIPCHK(hipStreamWaitEvent(s_sha, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_sha))) return rc;
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 4))) return rc; }
-    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
-    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st));
+      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6, S.d_smt_order))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st));
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
                               st)); }
     HIPCHK(hipEventRecord(I->ev_pos, st));
@@ -850,10 +851,10 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // main chain
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, S.d_sha_core, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 2))) return rc; }
-    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st)); }
-    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3))) return rc; }
+    { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st));
+      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st)); }
+    { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3, S.d_smt_order))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st));
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
                               st)); }
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);

@@ -262,6 +262,37 @@ __device__ __forceinline__ fr fr_inv(const fr& a) {
   return r;
 }
 
+// a^(p-2) by a 4-bit sliding window: the odd powers a^1 .. a^15 in registers, then 49 windows (252 squarings +
+// 49 products + 8 for the table = 309 products against fr_inv's 379). The windows are constants (a uniform loop) and
+// pick their table entry by masks: no run-time array indexing, so no scratch. Windows of p - 2 MSB first; the first
+// window is a^3.
+template <bool FAST = false>
+__device__ __forceinline__ fr fr_inv_sw(const fr& a) {
+  auto mul = [](const fr& x, const fr& y) { return FAST ? fr_mul_fast(x, y) : fr_mul(x, y); };
+  auto sqr = [](const fr& x) { return FAST ? fr_mul_fast(x, x) : fr_sqr(x); };
+  static constexpr uint8_t SQ[49] = {7, 3, 7, 2, 5, 6, 1, 8, 1, 7, 10, 6, 2, 7, 6, 7, 5, 3, 8, 9, 3, 8, 3, 5, 7,
+                                     6, 3, 8, 8, 6, 2, 6, 1, 8, 6, 8, 1, 8, 3, 3, 6, 4, 5, 4, 4, 4, 4, 4, 4};
+  static constexpr uint8_t WV[49] = {3, 1, 9, 3, 7, 11, 1, 9, 1, 13, 5, 13, 3, 5, 1, 11, 13, 5, 3, 5, 3, 11, 5, 5, 3,
+                                     15, 5, 9, 15, 13, 3, 11, 1, 9, 5, 15, 1, 15, 5, 3, 9, 15, 15, 15, 15, 15, 15, 15, 15};
+  const fr a2 = sqr(a);
+  const fr t3 = mul(a, a2), t5 = mul(t3, a2), t7 = mul(t5, a2), t9 = mul(t7, a2), t11 = mul(t9, a2),
+           t13 = mul(t11, a2), t15 = mul(t13, a2);
+  fr r = t3;
+  for (int s = 0; s < 49; s++) {
+    for (int q = 0; q < SQ[s]; q++) r = sqr(r);
+    const int v = WV[s];
+    fr t;  // masked OR of the eight entries (a select chain on the structs is lowered to a scratch array)
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      t.v[k] = (a.v[k] & (0u - (uint32_t)(v == 1))) | (t3.v[k] & (0u - (uint32_t)(v == 3))) |
+               (t5.v[k] & (0u - (uint32_t)(v == 5))) | (t7.v[k] & (0u - (uint32_t)(v == 7))) |
+               (t9.v[k] & (0u - (uint32_t)(v == 9))) | (t11.v[k] & (0u - (uint32_t)(v == 11))) |
+               (t13.v[k] & (0u - (uint32_t)(v == 13))) | (t15.v[k] & (0u - (uint32_t)(v == 15)));
+    r = mul(r, t);
+  }
+  return r;
+}
+
 // Batch inversion (Montgomery's trick) over n values in a caller-provided array.
 // x[i] := x[i]^-1 (0 stays 0); scratch must hold n elements.
 template <typename Acc>

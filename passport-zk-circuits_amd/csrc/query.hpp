@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
   }
   fr others, total;
   fr_group_others<64>(acc, others, total);
-  fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
+  fr inv = fr_mul(fr_inv_sw<true>(total), others);  // = 1 / acc (4 waves per SIMD: the throughput product)
 #pragma unroll
   for (int j = 3; j >= 0; j--) {
     const int i = lane + 64 * j;

@@ -581,7 +581,7 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
   }
   fr others, total;
   fr_group_others<BJJ_SEGS>(acc, others, total);
-  fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
+  fr inv = fr_mul(fr_inv_sw(total), others);  // = 1 / acc
   fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
   for (int qi = NQ - 1; qi >= 0; qi--) {
     fr e = elem(qi);
@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
   }
   fr others, total;
   fr_group_others<G>(acc, others, total);
-  fr inv = fr_mul(fr_inv(total), others);  // = 1 / acc
+  fr inv = fr_mul(fr_inv_sw(total), others);  // = 1 / acc
 #pragma unroll
   for (int k = NL - 1; k >= 0; k--) {
     fr r = fr_zero();
@@ -741,7 +741,7 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
   // isEqual(root_0, root): inverse of root - root_0
   fr rin = fr_to_mont(load_fr(row + 32ull * R.in_root));
   fr dlt = fr_sub(rin, roots[0]);
-  core[3 * SMT_LEVELS + 1] = fr_inv(dlt);
+  core[3 * SMT_LEVELS + 1] = fr_inv_sw(dlt);
   // smtVerifier.isVerified === 1 where the circuit asserts it (identityStateVerifier.circom:46; the register
   // circuit leaves it commented out, passportVerificationBuilder.circom:240)
   if (R.smt_check && !fr_is_zero(dlt)) set_status(status ? status + w : nullptr, ST_ISV_ROOT);

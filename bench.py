@@ -137,31 +137,50 @@ class GpuEngine:
         from pzkwit import native, inputs as I
         self.torch, self.dev = torch, dev
         self.layout = "O0 (all signals)"
-        if workload.startswith("register"):
-            params = I.instance_params(args.sig_eff)
+        if workload.startswith("register") or workload.startswith("query"):
+            if workload.startswith("register"):
+                circuit, size_arg, params = native.PZK_CIRCUIT_REGISTER, 0, I.instance_params(args.sig_eff)
+                n_in = I.PassportGen.shared(SIG_SEED[args.sig_eff], 64, args.sig_eff).n_inputs
+                shape = {1: "register_canonical", 20: "register_sig20"}.get(args.sig_eff)
+            else:
+                circuit, size_arg, params = native.PZK_CIRCUIT_QUERY, 80, {"doc": 1 if workload == "query-td1" else 0}
+                n_in = native.layout_info(params, circuit, size_arg).n_inputs
+                shape = "query" if workload == "query" else None
+            n_o0 = native.layout_info(params, circuit, size_arg).witness_size
             sym = None
             if getattr(args, "sym", None):
                 from pzkwit import symmap
                 if args.sym.startswith("synthetic"):
                     frac = int(args.sym.split(":")[1]) if ":" in args.sym else 4
-                    n_in = I.PassportGen.shared(SIG_SEED[args.sig_eff], 64, args.sig_eff).n_inputs
-                    keep = symmap.synthetic_keep(native.layout_witness_size(params), 1 + 4 + n_in, fraction=frac)
+                    keep = symmap.synthetic_keep(n_o0, 1 + 4 + n_in, fraction=frac)
                     sym = symmap.sym_text(keep)
                     self.layout = ("synthetic .sym map: outputs + inputs + 1/%d of the O0 signals (hash subset; NOT "
                                    "circom's O2, which cannot be built here)" % frac)
+                elif args.sym in ("o1shape", "o2shape"):
+                    level = int(args.sym[1])
+                    if shape is None:
+                        raise SystemExit("--sym %s: no committed shape map for this workload (tools/gen_shape_maps.py)"
+                                         % args.sym)
+                    wit = symmap.load_shape(shape, level)
+                    sym = symmap.sym_text_wit(wit)
+                    self.layout = ("circom --O%d-shaped .sym map (data/shape/%s_o%d.npz: circom's documented "
+                                   "simplification applied to the restated constraints, %d of %d signals; which "
+                                   "signals circom itself keeps is parity unpinned)"
+                                   % (level, shape, level, int(wit.max()), n_o0 - 1))
                 else:
                     sym = open(args.sym).read()
                     self.layout = ".sym map %s" % os.path.basename(args.sym)
-            self.inst = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params, sym=sym)
+            self.inst = native.Instance(circuit, size_arg, params, sym=sym)
             if sym is not None:
                 inv = symmap.parse_sym(sym)
                 if (np.diff(inv) <= 0).any() or os.environ.get("PZK_SYM_GATHER"):  # two O0 staging chunks of <= 1024 witnesses
-                    self.o0_staging_bytes = 2 * 1024 * 32 * native.layout_witness_size(params)
+                    self.o0_staging_bytes = 2 * 1024 * 32 * n_o0
                     self.layout += "; staging + gather (non-monotone map)"
                 else:
                     self.layout += "; emitted directly (monotone map, mapsink.hpp)"
-        elif workload.startswith("query"):
-            self.inst = native.Instance(native.PZK_CIRCUIT_QUERY, 80, {"doc": 1} if workload == "query-td1" else None)
+            if workload.startswith("query"):
+                self.layout += ("; BabyPbk (identityStateVerifier.circom:19, undefined in the snapshot) substituted by "
+                                "the reference's BabyjubjubBase8Multiplication (DESIGN.md §11)")
         else:
             self.inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
         self.W, self.NIN = self.inst.witness_size, self.inst.n_inputs
@@ -313,7 +332,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slot) size")
     ap.add_argument("--slots", type=int, default=1, help="output slots (ring) per GPU")
-    ap.add_argument("--sym", default=None, help="signal -> witness map: a circom .sym file, or synthetic[:N]")
+    ap.add_argument("--sym", default=None, help="signal -> witness map: a circom .sym file, o1shape / o2shape (the "
+                    "committed circom-shaped maps), or synthetic[:N]")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
@@ -561,34 +581,89 @@ def _mixed_host_rows(sigs, lo, hi, n_in_max, workers):
     return out
 
 
-def bench_mixed(args):
-    """Config 5: a mixed-flow batch (40 % RSA-2048, 30 % RSA-4096, 30 % ECDSA secp256r1, seed 5),
-    --batch witnesses per GPU on average, sharded across ranks by .wtns bytes (pzkwit.mixed). As in
-    run_rank: rank 0 makes every rank's input rows and scatters them over the process group; status and
-    public signals are all-gathered after the timed region. On a rank, each flow has its own instance and
-    its own output slot, so the flows' pipelined calls overlap (no synchronisation between instances)."""
+class MixedGpuEngine:
+    """Config 5's measured path on one rank: one libpzkwit instance per flow, each with its own output slot, so
+    the flows' pipelined calls overlap (no synchronisation between instances inside a step)."""
+
+    def __init__(self, flows, groups, dev):
+        import torch
+        from pzkwit import native
+        self.torch, self.dev, self.groups = torch, dev, groups
+        self.inst = {sg: native.Instance(native.PZK_CIRCUIT_REGISTER, 0, flows[sg]) for sg in groups}
+        self.n_inputs = {sg: i.n_inputs for sg, i in self.inst.items()}
+        self.witness_size = {sg: i.witness_size for sg, i in self.inst.items()}
+
+    def setup(self, d_in, first, n_local):
+        """d_in: {flow: its compact input rows [n, n_inputs * 32] on the device}; first: {flow: row of its first
+        witness in the rank's status vector}."""
+        torch = self.torch
+        self.d_in, self.first = d_in, first
+        # one output slot per flow, sized so the slots and the instances' scratch fit beside each other
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        scratch = {1: 1 << 20, 2: 2 << 20, 20: 10 << 20}  # per-witness core scratch of one set
+        budget = int(free * 0.85) // max(1, len(self.groups))
+        self.sub = {sg: max(1, min(len(self.groups[sg]), budget // (32 * self.witness_size[sg] + 3 * scratch[sg])))
+                    for sg in self.groups}
+        self.d_out = {sg: torch.empty(self.sub[sg] * 32 * self.witness_size[sg], dtype=torch.uint8, device=self.dev)
+                      for sg in self.groups}
+        self.d_st = torch.zeros(n_local, dtype=torch.int32, device=self.dev)
+        torch.cuda.synchronize(self.dev)  # the library's streams do not wait for torch's stream
+
+    def _run(self, st, collect=None):
+        for sg, idx in self.groups.items():
+            W, NIN = self.witness_size[sg], self.n_inputs[sg]
+            for a in range(0, len(idx), self.sub[sg]):
+                n = min(self.sub[sg], len(idx) - a)
+                self.inst[sg].witness_batch_device(self.d_in[sg].data_ptr() + a * NIN * 32, n, self.d_out[sg].data_ptr(),
+                                                   32 * W, st.data_ptr() + 4 * (self.first[sg] + a))
+                if collect:
+                    self.inst[sg].sync()
+                    collect(sg, a, n, self.d_out[sg].view(self.sub[sg], W, 32)[:n])
+
+    def step(self):
+        self._run(self.d_st)
+
+    def sync(self):
+        for i in self.inst.values():
+            i.sync()
+        self.torch.cuda.synchronize(self.dev)
+
+    def statuses(self):
+        return self.d_st
+
+    def public_pass(self, n_pub):
+        """Untimed: status + public signals (witness[1 .. n_pub]) of every witness of the shard."""
+        torch = self.torch
+        st = torch.zeros_like(self.d_st)
+        pub = torch.zeros((st.shape[0], n_pub, 32), dtype=torch.uint8, device=self.dev)
+
+        def collect(sg, a, n, rows):
+            pub[self.first[sg] + a: self.first[sg] + a + n] = rows[:, 1: 1 + n_pub]
+        self._run(st, collect)
+        torch.cuda.synchronize(self.dev)
+        return st, pub
+
+
+def run_mixed_rank(args, rank, world, local, dist, engine_cls=MixedGpuEngine, device="cuda", rows_fn=None):
+    """One rank of config 5 (also driven by tests/test_host.py over gloo with a stub engine and stub rows).
+
+    Every rank derives the same plan (_mixed_plan: flows, costs, cost-balanced contiguous shards). Rank 0 makes
+    every shard's input rows (grouped per flow, zero-padded to the widest flow) and scatters shard r to rank r;
+    each rank cuts its flows' compact rows back out, runs W + K steps, and status + public signals are
+    all-gathered after the timed region (rank-major; within a rank grouped per flow). Returns the JSON record."""
     import torch
     from pzkwit import native, dist as D
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    dev = torch.device(device, local) if device == "cuda" else torch.device(device)
+    rows_fn = rows_fn or _mixed_host_rows
     per_gpu = args.batch or 4096
     total = per_gpu * world
     sigs, flows, costs, shards = _mixed_plan(per_gpu, world)
     lo, hi = shards[rank]
     groups = _mixed_groups(sigs, lo, hi)
-    inst = {sg: native.Instance(native.PZK_CIRCUIT_REGISTER, 0, flows[sg]) for sg in groups}
+    engine = engine_cls(flows, groups, dev)
     n_in_max = max(native.layout_inputs(flows[sg]) for sg, _ in MIX)
     row_bytes = n_in_max * 32
     rows_max = max(h - l for l, h in shards)
-    # inputs: rank 0 makes every shard (grouped per flow, padded rows), scatters shard r to rank r
     t0 = time.time()
     recv = torch.zeros(rows_max * row_bytes, dtype=torch.uint8, device=dev)
     if rank == 0:
@@ -596,7 +671,7 @@ def bench_mixed(args):
         parts = []
         for r, (a, b) in enumerate(shards):
             h = np.zeros((rows_max, n_in_max, 32), dtype=np.uint8)
-            h[: b - a] = _mixed_host_rows(sigs, a, b, n_in_max, workers)
+            h[: b - a] = rows_fn(sigs, a, b, n_in_max, workers)
             parts.append(torch.from_numpy(h.reshape(-1)))
         log("mixed inputs: %d x %d rows generated on rank 0 in %.1fs" % (world, rows_max, time.time() - t0))
         if dist is None:
@@ -612,62 +687,29 @@ def bench_mixed(args):
     d_in, first = {}, {}
     pos = 0
     for sg, idx in groups.items():  # per flow: compact rows of its own width
-        d_in[sg] = view[pos: pos + len(idx), : 32 * inst[sg].n_inputs].contiguous()
+        d_in[sg] = view[pos: pos + len(idx), : 32 * engine.n_inputs[sg]].contiguous()
         first[sg] = pos
         pos += len(idx)
     del recv, view
-    # one output slot per flow, sized so the slots and the instances' scratch fit beside each other
-    free, _ = torch.cuda.mem_get_info(dev)
-    scratch = {1: 1 << 20, 2: 2 << 20, 20: 10 << 20}  # per-witness core scratch of one set
-    budget = int(free * 0.85) // max(1, len(groups))
-    sub = {sg: max(1, min(len(groups[sg]), budget // (32 * inst[sg].witness_size + 3 * scratch[sg]))) for sg in groups}
-    d_out = {sg: torch.empty(sub[sg] * 32 * inst[sg].witness_size, dtype=torch.uint8, device=dev) for sg in groups}
-    d_st = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
-    log("mixed rank %d: flows %s, sub-batches %s, slots %.1f GB" % (
-        rank, {k: len(v) for k, v in groups.items()}, sub, sum(t.numel() for t in d_out.values()) / 1e9))
-    torch.cuda.synchronize(dev)  # the library's streams do not wait for torch's stream
-
-    def step():
-        for sg, idx in groups.items():
-            W, NIN = inst[sg].witness_size, inst[sg].n_inputs
-            for a in range(0, len(idx), sub[sg]):
-                n = min(sub[sg], len(idx) - a)
-                inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n, d_out[sg].data_ptr(), 32 * W,
-                                              d_st.data_ptr() + 4 * (first[sg] + a))
-
-    def sync():
-        for i in inst.values():
-            i.sync()
-        torch.cuda.synchronize(dev)
-
+    engine.setup(d_in, first, hi - lo)
+    log("mixed rank %d: flows %s, sub-batches %s" % (rank, {k: len(v) for k, v in groups.items()},
+                                                       getattr(engine, "sub", None)))
     for _ in range(args.warmup):
-        step()
-    sync()
+        engine.step()
+    engine.sync()
     if dist:
         dist.barrier()
-    sync()
+    engine.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    sync()
+        engine.step()
+    engine.sync()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    bad = int((d_st != 0).sum().item())  # lanes failing in the last timed step
-    # untimed: status + public signals (witness[1 .. 5]) of every witness of the shard, for the gather
+    bad = int((engine.statuses() != 0).sum().item())  # lanes failing in the last timed step
     n_pub = 5
-    pub = torch.zeros((hi - lo, n_pub, 32), dtype=torch.uint8, device=dev)
-    st = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
-    for sg, idx in groups.items():
-        W, NIN = inst[sg].witness_size, inst[sg].n_inputs
-        out = d_out[sg].view(sub[sg], W, 32)
-        for a in range(0, len(idx), sub[sg]):
-            n = min(sub[sg], len(idx) - a)
-            inst[sg].witness_batch_device(d_in[sg].data_ptr() + a * NIN * 32, n, d_out[sg].data_ptr(), 32 * W,
-                                          st.data_ptr() + 4 * (first[sg] + a))
-            inst[sg].sync()
-            pub[first[sg] + a: first[sg] + a + n] = out[:n, 1: 1 + n_pub]
-    torch.cuda.synchronize(dev)
+    st, pub = engine.public_pass(n_pub)
     my_bytes = sum(costs[lo:hi])
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -683,17 +725,33 @@ def bench_mixed(args):
                 "order": "rank-major; within a rank grouped per flow (SIG 1, 2, 20), global order inside a group"}
     value = total * args.steps / dt
     job_gbs = sum(costs) * args.steps / dt / 1e9
-    out = {
+    return {
         "metric": "mixed-flow registerIdentityBuilder witnesses/sec (config 5: RSA-2048/RSA-4096/ECDSA-P256)",
         "value": round(value, 2), "unit": "witnesses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": "mixed flows %s, %d per GPU, cost-sharded" % (dict(MIX), per_gpu),
                    "flows": {str(k): len(v) for k, v in groups.items()}, "rank0_bytes": my_bytes,
-                   "sub_batches": {str(k): v for k, v in sub.items()}, "invalid_lanes": bad,
+                   "sub_batches": {str(k): v for k, v in (getattr(engine, "sub", None) or {}).items()},
+                   "invalid_lanes": bad,
                    "inputs": "rank 0 generates every shard and scatters it (process group)", "gathered": gathered},
         "job_hbm": {"achieved": round(job_gbs, 1), "unit": "GB/s", "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
     }
+
+
+def bench_mixed(args):
+    """Config 5: a mixed-flow batch (40 % RSA-2048, 30 % RSA-4096, 30 % ECDSA secp256r1, seed 5),
+    --batch witnesses per GPU on average, sharded across ranks by .wtns bytes (pzkwit.mixed)."""
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    out = run_mixed_rank(args, rank, world, local, dist)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

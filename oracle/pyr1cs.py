@@ -120,3 +120,61 @@ def check_query(wit, td1=False):
     r = Report()
     rc = lib().ck_query(int(td1), w.ctypes.data, w.shape[0], ctypes.byref(r))
     return rc, r.as_dict()
+
+
+class CkStruct(ctypes.Structure):
+    _fields_ = [("n_cons", ctypes.c_uint64), ("n_sup", ctypes.c_uint64), ("cls", ctypes.POINTER(ctypes.c_uint8)),
+                ("off", ctypes.POINTER(ctypes.c_uint64)), ("sup", ctypes.POINTER(ctypes.c_uint32))]
+
+
+CIRCUITS = {"register": 0, "query": 1, "sha256": 2, "poseidon": 3}
+QUAD, LIN, COPY, CONST = 0, 1, 2, 3
+
+
+def _shape_lib():
+    L = lib()
+    if not getattr(L, "_shape_ready", False):
+        L.ck_structure.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                                   ctypes.POINTER(CkStruct)]
+        L.ck_struct_free.argtypes = [ctypes.POINTER(CkStruct)]
+        L.ck_shape_map.argtypes = [ctypes.POINTER(CkStruct), ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_void_p]
+        L.ck_shape_map.restype = ctypes.c_int64
+        L._shape_ready = True
+    return L
+
+
+def structure(circuit, n, arg=0, seed=0x5EED, **params):
+    """The restated circuit's constraint structure (oracle/r1cs_shape.inc.c): a dict with per-constraint class
+    `cls` (QUAD / LIN / COPY / CONST), support offsets `off` and signals `sup`, plus `_handle` for shape_map."""
+    import numpy as np
+    L = _shape_lib()
+    _load_poseidon()
+    p = CkParams(**params) if params else None
+    st = CkStruct()
+    rc = L.ck_structure(CIRCUITS[circuit], int(arg), ctypes.byref(p) if p is not None else None, int(n), seed,
+                        ctypes.byref(st))
+    if rc:
+        raise RuntimeError("ck_structure(%s): %d" % (circuit, rc))
+    nc, ns = st.n_cons, st.n_sup
+    out = {"n_cons": nc,
+           "cls": np.ctypeslib.as_array(st.cls, (nc,)).copy(),
+           "off": np.ctypeslib.as_array(st.off, (nc + 1,)).copy(),
+           "sup": np.ctypeslib.as_array(st.sup, (max(ns, 1),))[:ns].copy(),
+           "_handle": st}
+    return out
+
+
+def shape_map(struct, n, n_protect, level):
+    """-> (wit, witness_size): wit[s] = witness index of O0 signal s, -1 = removed (level 1: --O1-shaped, 2:
+    --O2-shaped)."""
+    import numpy as np
+    wit = np.zeros(n, dtype=np.int32)
+    m = _shape_lib().ck_shape_map(ctypes.byref(struct["_handle"]), n, n_protect, level, wit.ctypes.data)
+    if m < 0:
+        raise RuntimeError("ck_shape_map: %d" % m)
+    return wit, int(m)
+
+
+def free_structure(struct):
+    _shape_lib().ck_struct_free(ctypes.byref(struct["_handle"]))

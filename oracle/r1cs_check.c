@@ -37,13 +37,26 @@ typedef struct {
   int oob;                  /* a signal index past the witness: allocation mismatch */
 } ck_t;
 
+/* structure trace (r1cs_shape.inc.c): while TR is set, every constraint also records the signals it reads and its
+ * residual lhs - rhs */
+typedef struct {
+  uint32_t *sig; uint64_t n_sig, cap_sig;  /* signals read, constraint after constraint */
+  uint64_t *off; fr_t *res; uint64_t n_cons, cap_cons, cap_res;  /* per constraint: end of its reads, residual */
+  int nomem;
+} ck_tr_t;
+static ck_tr_t *TR = NULL;
+static void tr_read(size_t i);
+static void tr_cons(fr_t residual);
+
 /* signal read: marks coverage */
 static inline fr_t S(ck_t *c, size_t i) {
   if (i >= c->n) { c->oob = 1; return fr_zero(); }
   c->cov[i] = 1;
+  if (TR) tr_read(i);
   return c->w[i];
 }
 static void req(ck_t *c, fr_t lhs, fr_t rhs, const char *tmpl, int line, size_t at) {
+  if (TR) tr_cons(fr_sub(lhs, rhs));
   if (!fr_eq(lhs, rhs)) {
     if (!c->n_bad) { c->first_bad = (int64_t)c->n_cons; c->first_tmpl = tmpl; c->first_line = line; c->first_at = at; }
     c->n_bad++;
@@ -2530,3 +2543,5 @@ int ck_query(int td1, const uint8_t *wit, size_t nw, ck_report *r) {
   req(&c, S(&c, 0), KC(1), "witness[0] = 1", 0, 0);
   return ck_end(&c, walked, r);
 }
+
+#include "r1cs_shape.inc.c"

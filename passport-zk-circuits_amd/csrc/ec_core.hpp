@@ -923,12 +923,14 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
   const uint4* src = reinterpret_cast<const uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
   for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
   __syncthreads();
-  const uint32_t* prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
-  const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
+  // mapped: the kept elements' descriptors, stored consecutively from their mapped index (desc_run)
+  const DescRun dr = desc_run<MM>(L, wtns, stride, w, wk, R.off + wk.start, L.ec_prog + L.ec_prog_off[type] + wk.start);
+  const uint32_t* prog = dr.prog;
+  const OutRow out = dr.out;
   // ECT_U descriptors per batch, loaded before the batch's stores (a global load issued after a store waits for it:
   // gfx9 vmcnt counts both, in order); with prefetch the next batch's descriptors are loaded ahead of this batch's
   // stores (PZK_ECT_PREFETCH, PZK_ECT_U: tuning knobs). Two lanes per element, 1 KiB per wave store.
-  const uint32_t tot = 2 * wk.count, step = ECT_U * blockDim.x;
+  const uint32_t tot = 2 * dr.count, step = ECT_U * blockDim.x;
   uint32_t d[ECT_U], dn[ECT_U];
   auto load = [&](uint32_t base, uint32_t* dd) {
 #pragma unroll
@@ -945,7 +947,7 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
-      store_half<MM>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
+      store_half<MAP_O0>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
     if (!prefetch && base + step < tot) load(base + step, dn);
   }

@@ -110,8 +110,10 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
     // lane (emit_run stages through LDS for the emitters whose elements are expensive).
     // SHA_U descriptors are loaded before the SHA_U stores that use them (a global load issued
     // after a store waits for it: gfx9 vmcnt counts both)
-    const uint32_t* prog = L.sha_prog + wk.start;
-    const uint32_t tot = 2 * wk.count;
+    // Mapped: the kept elements' descriptors (desc_run), stored consecutively from their mapped index.
+    const DescRun dr = desc_run<MM>(L, wtns, stride, w, wk, R.off + wk.start, L.sha_prog + wk.start);
+    const uint32_t* prog = dr.prog;
+    const uint32_t tot = 2 * dr.count;
     for (uint32_t base = threadIdx.x; base < tot; base += SHA_U * blockDim.x) {
       uint32_t d[SHA_U];
 #pragma unroll
@@ -123,7 +125,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_sha(DevLayout L, const Wo
       for (int k = 0; k < SHA_U; k++) {
         const uint32_t h = base + k * blockDim.x;
         const uint64_t v = (h & 1) ? 0 : sha_desc_apply(d[k], wt[d[k] & 2047]);
-        store_half<MM>(out, h, make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), h < tot);
+        store_half<MAP_O0>(dr.out, h, make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u), h < tot);
       }
     }
   } else {  // RK_SHA_OWN: H_0..H_B (H_m = Hin of block m, H_B = Hout)

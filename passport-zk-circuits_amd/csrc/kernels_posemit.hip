@@ -37,8 +37,14 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
   // the block's descriptors go to LDS first: a global load inside the store loop would wait for
   // every store in flight (gfx9 vmcnt counts stores too)
+  // (mapped: the kept elements' image indices, from the instance's compacted program, desc_run)
   __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
-  for (uint32_t i = threadIdx.x; i < wk.count; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
+  const DescRun dr0 = desc_run<MM>(L, wtns, stride, 0, wk, R.off + wk.start, nullptr);
+  const uint32_t cnt = dr0.count;
+  if (MM == MAP_DIRECT)
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = (uint16_t)dr0.prog[i];
+  else
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
   const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
   for (uint32_t w = w0; w < w1; w++) {
     if (w != w0) __syncthreads();  // every lane has read the previous witness's image
@@ -47,13 +53,11 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
     PZK_POS_ACC(0, t0);
     PZK_POS_CLK(t1);
     // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
-    const OutRow out = out_row(L, wtns, stride, w, R.off + wk.start);
+    const OutRow out{wtns + (size_t)w * stride, dr0.out.g, KeepMap{nullptr, nullptr}};
     const uint4* im = reinterpret_cast<const uint4*>(img);
-    const uint32_t tot = 2 * wk.count;
-    for (uint32_t h0 = threadIdx.x & ~63u; h0 < tot; h0 += blockDim.x) {  // wave-uniform loop: store_half's map window
-      const uint32_t h = h0 + (threadIdx.x & 63);
-      store_half<MM>(out, h, h < tot ? im[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u), h < tot);
-    }
+    const uint32_t tot = 2 * cnt;
+    for (uint32_t h = threadIdx.x; h < tot; h += blockDim.x)
+      store_half<MAP_O0>(out, h, im[2u * prog[h >> 1] + (h & 1)], true);
     PZK_POS_ACC(1, t1);
   }
 }

@@ -285,6 +285,7 @@ struct DevLayout {
   const uint32_t* ec_tab_off;       // entry offset of table op t inside a witness's tables
   uint32_t ec_tab_entries;          // table entries per witness
   KeepMap keep;                     // direct emission into a .sym-mapped witness (mapsink.hpp)
+  const uint32_t* mprog;            // mapped: kept descriptors of the SHA / Poseidon / EC table work items, at Work.pad
 };
 
 }  // namespace pzk

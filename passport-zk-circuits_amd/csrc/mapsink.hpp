@@ -85,11 +85,50 @@ __device__ __forceinline__ void store_half(const OutRow& o, uint32_t h, const ui
   if (valid && map_keep(m, e)) reinterpret_cast<uint4*>(o.row)[2ull * map_rank(m, e) + (h & 1)] = v;
 }
 
-// for (q < count) out[q] = f(q), wave-contiguous (fr.hpp emit_run); mapped: the kept elements of a wave
-// are compacted through the LDS stage and stored as one contiguous run of the mapped row. A wave with no
-// kept element skips its evaluation; otherwise f runs on every valid lane as in the O0 path (element
-// functions may scan across the wave's lanes, regemit.hpp bmneq_tmpr)
-template <int MM = MAP_ANY, typename F>
+// kept signals below O0 index g (wave-uniform g): the mapped row index of the first kept element at or after g
+__device__ __forceinline__ uint32_t map_rank_at(const KeepMap& M, uint64_t g) {
+  const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 6));
+  const uint64_t w = ((cu64_t*)M.bits)[i];
+  return ((cu32_t*)M.rank)[i] + (uint32_t)__popcll(w & ((1ull << (g & 63)) - 1));
+}
+
+// Block-wide (every thread calls it; it ends with __syncthreads): the kept elements among the run's O0 elements
+// [a, a + n) (n > 0), ascending, as list[k] = payload(q) with q their offset from a; returns how many. Kept element
+// k goes to mapped row index map_rank_at(o.g + a) + k. Each wave takes whole bitmap words (scalar loads: the
+// address is wave-uniform), a lane per bit, and places its kept bit by the word's rank + the set bits below it.
+template <typename T, typename P>
+__device__ __forceinline__ uint32_t kept_collect(const OutRow& o, uint32_t a, uint32_t n, T* list, P payload) {
+  const uint64_t lo = o.g + a, hi = lo + n;
+  const uint32_t r0 = map_rank_at(o.map, lo), nk = map_rank_at(o.map, hi) - r0;
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t i0 = (uint32_t)(lo >> 6), i1 = (uint32_t)((hi - 1) >> 6);
+  for (uint32_t i = i0 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); i <= i1; i += nw) {
+    const uint32_t iu = __builtin_amdgcn_readfirstlane(i);
+    const uint64_t word = ((cu64_t*)o.map.bits)[iu];
+    const uint32_t rk = ((cu32_t*)o.map.rank)[iu];
+    const uint64_t e = ((uint64_t)iu << 6) + lane;
+    if (((word >> lane) & 1) && e >= lo && e < hi)
+      list[rk + (uint32_t)__popcll(word & ((1ull << lane) - 1)) - r0] = payload((uint32_t)(e - lo));
+  }
+  __syncthreads();
+  return nk;
+}
+
+// the kept-offset list of mapped emit_run segments (one LDS array per kernel, whichever element functions it runs)
+constexpr uint32_t MAP_SEG = 2048;
+__device__ __forceinline__ uint16_t* map_seg_list() {
+  __shared__ uint16_t klist[MAP_SEG];
+  return klist;
+}
+
+// for (q < count) out[q] = f(q), wave-contiguous (fr.hpp emit_run).
+// Mapped (block-wide: every thread of the workgroup calls it): the run is taken in segments of MAP_SEG O0
+// elements; per segment the kept offsets are collected into LDS (kept_collect) and the waves evaluate f on the
+// KEPT elements only, 64 per wave instruction, stored contiguously at the segment's mapped index (the kept
+// elements of a run are consecutive in a monotone map). LANE_INDEP = false: f scans across the wave's lanes
+// (regemit.hpp bmneq_tmpr needs 64 consecutive q per wave), so every element of a wave with a kept one is
+// evaluated in O0 order and the kept ones are compacted through the stage.
+template <int MM = MAP_ANY, bool LANE_INDEP = true, typename F>
 __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4* stage_block, F f) {
   if (MM == MAP_O0 || (MM == MAP_ANY && !o.map.bits)) {
     emit_run(o.row + 32ull * o.g, count, stage_block, f);
@@ -97,25 +136,59 @@ __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4*
   }
   const uint32_t lane = threadIdx.x & 63;
   uint4* stage = stage_block + (threadIdx.x >> 6) * 128;
-  for (uint32_t q0 = threadIdx.x - lane; q0 < count; q0 += blockDim.x) {
-    const uint32_t q = q0 + lane;
-    const MapWin m = map_win(o.map, o.g + q0);
-    const bool keep = q < count && map_keep(m, o.g + q);
-    const uint64_t mask = __ballot(keep);
-    if (mask == 0) continue;  // wave-uniform
-    const El e = q < count ? f(q) : el_zero();
-    const uint32_t pos = (uint32_t)__popcll(mask & ((1ull << lane) - 1)), nk = (uint32_t)__popcll(mask);
-    if (keep) {
-      stage[2 * pos] = e.lo;
-      stage[2 * pos + 1] = e.hi;
+  if constexpr (LANE_INDEP) {
+    uint16_t* klist = map_seg_list();
+    for (uint32_t a = 0; a < count; a += MAP_SEG) {
+      const uint32_t n = min(MAP_SEG, count - a);
+      const uint32_t r0 = map_rank_at(o.map, o.g + a);
+      const uint32_t nk = kept_collect(o, a, n, klist, [](uint32_t q) { return (uint16_t)q; });
+      uint8_t* dst = o.row + 32ull * r0;
+      for (uint32_t k0 = threadIdx.x - lane; k0 < nk; k0 += blockDim.x) {
+        const uint32_t k = k0 + lane;
+        const El e = k < nk ? f(a + klist[k]) : el_zero();
+        wave_store(dst + 32ull * k0, e, nk - k0 < 64 ? nk - k0 : 64, stage);
+      }
+      __syncthreads();  // klist is rewritten by the next segment
     }
-    wave_sync();
-    const uint4 a = stage[lane], b = stage[64 + lane];
-    uint4* d = reinterpret_cast<uint4*>(o.row + 32ull * map_rank(m, o.g + q0));
-    if (lane < 2 * nk) d[lane] = a;
-    if (64 + lane < 2 * nk) d[64 + lane] = b;
-    wave_sync();
+  } else {
+    for (uint32_t q0 = threadIdx.x - lane; q0 < count; q0 += blockDim.x) {
+      const uint32_t q = q0 + lane;
+      const MapWin m = map_win(o.map, o.g + q0);
+      const bool keep = q < count && map_keep(m, o.g + q);
+      const uint64_t mask = __ballot(keep);
+      if (mask == 0) continue;  // wave-uniform
+      const El e = q < count ? f(q) : el_zero();
+      const uint32_t pos = (uint32_t)__popcll(mask & ((1ull << lane) - 1)), nk = (uint32_t)__popcll(mask);
+      if (keep) {
+        stage[2 * pos] = e.lo;
+        stage[2 * pos + 1] = e.hi;
+      }
+      wave_sync();
+      const uint4 a = stage[lane], b = stage[64 + lane];
+      uint4* d = reinterpret_cast<uint4*>(o.row + 32ull * map_rank(m, o.g + q0));
+      if (lane < 2 * nk) d[lane] = a;
+      if (64 + lane < 2 * nk) d[64 + lane] = b;
+      wave_sync();
+    }
   }
+}
+
+// A descriptor-driven emitter's work item (k_emit_sha block programs, k_emit_pos, k_emit_ect): O0, its
+// descriptors are prog[0 .. count) and it stores at O0 index g; mapped, the instance's compacted program
+// (DevLayout.mprog, built by pzk_instance_create_mapped) holds the kept elements' descriptors at Work.pad, and
+// they go to consecutive mapped indices from rank(g). Either way the store loop is the O0 loop.
+struct DescRun {
+  const uint32_t* prog;  // mapped: L.mprog + Work.pad
+  uint32_t count;        // elements to store
+  OutRow out;            // identity store: row + 32 * (out.g + k)
+};
+template <int MM>
+__device__ __forceinline__ DescRun desc_run(const DevLayout& L, uint8_t* wtns, size_t stride, uint32_t w, const Work& wk,
+                                            uint64_t g, const uint32_t* o0_prog) {
+  uint8_t* row = wtns + (size_t)w * stride;
+  if (MM == MAP_O0 || (MM == MAP_ANY && !L.keep.bits)) return DescRun{o0_prog, wk.count, OutRow{row, g, KeepMap{nullptr, nullptr}}};
+  const uint32_t r0 = map_rank_at(L.keep, g), r1 = map_rank_at(L.keep, g + wk.count);
+  return DescRun{L.mprog + wk.pad, r1 - r0, OutRow{row, r0, KeepMap{nullptr, nullptr}}};
 }
 
 }  // namespace pzk

@@ -736,7 +736,9 @@ __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, u
     constexpr MMStarts S = mm_starts(K);
     constexpr uint32_t a = S.v[SEC], n = S.v[SEC + 1] - S.v[SEC];
     PZK_MM_CLK(t0);
-    emit_run<MM>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    // tmpResult rows (and BigMultNonEqualOverflow's, K != 32) are segmented scans across the wave (bmneq_tmpr)
+    constexpr bool INDEP = !(SEC == MM_TMPR || (SEC == MM_KARA && (K & (K - 1)) != 0));
+    emit_run<MM, INDEP>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
     PZK_MM_ACC(SEC, t0);
     mm_sections<K, SEC + 1, MM>(C, out, stage);
   }

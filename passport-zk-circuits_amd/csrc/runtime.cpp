@@ -138,7 +138,7 @@ struct pzk_instance {
   // side streams of the register pipeline (signature core; SHA emitters; other emitters, s_emit
   // below): four streams in all, one per hardware queue (GPU_MAX_HW_QUEUES = 4)
   hipStream_t s_rsa = nullptr, s_sha = nullptr;
-  hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_entry = nullptr;
+  hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_entry = nullptr, ev_dep = nullptr;
   // device copies of the layout
   Region* d_regions = nullptr;
   Work* d_work[E_COUNT] = {};
@@ -176,6 +176,7 @@ struct pzk_instance {
   // (mapsink.hpp): keep bitmap over the O0 indices + the kept count below every 64-signal boundary
   uint64_t* d_keep_bits = nullptr;
   uint32_t* d_keep_rank = nullptr;
+  uint32_t* d_mprog = nullptr;  // the kept elements' descriptors of the descriptor-driven work items (Work.pad)
   // any other map: O0 chunks into staging slots, then k_wtns_gather
   uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
   std::vector<uint32_t> kept;     // mapped instances: the kept O0 indices, sorted (pzk_phase_info's bytes)
@@ -226,6 +227,7 @@ struct pzk_instance {
     L.ec_tab_off = d_ec_tab_off;
     L.ec_tab_entries = lay.ec_tab_entries;
     L.keep = KeepMap{d_keep_bits, d_keep_rank};
+    L.mprog = d_mprog;
     return L;
   }
 };
@@ -336,14 +338,14 @@ static void free_all(pzk_instance* I) {
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
                   I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small, I->d_map,
-                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank};
+                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank, I->d_mprog};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
   for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail})
     if (s) (void)hipStreamDestroy(s);
-  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_pos, I->ev_tab})
+  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : I->ev_done)
     for (hipEvent_t e : set)
@@ -454,7 +456,7 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess;
-  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_pos, &I->ev_tab})
+  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t& e : I->ev_gather) {
     ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -550,6 +552,32 @@ int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t
     for (uint32_t g : inv) bits[g >> 6] |= 1ull << (g & 63);
     for (size_t i = 1; i < nw; i++) rank[i] = rank[i - 1] + (uint32_t)__builtin_popcountll(bits[i - 1]);
     ok = upload(&I->d_keep_bits, bits) == 0 && upload(&I->d_keep_rank, rank) == 0;
+    // descriptor-driven emitters (SHA-256 blocks, Poseidon blocks, EC table blocks): each work item's kept
+    // descriptors, compacted in O0 order, at Work.pad of the item (mapsink.hpp desc_run), so those emitters run
+    // their O0 store loop over the kept elements only
+    std::vector<uint32_t> mprog;
+    const Layout& lay = I->lay;
+    auto kept = [&](uint64_t g) { return (bits[g >> 6] >> (g & 63)) & 1; };
+    for (int e : {E_SHA, E_SHAD, E_POS, E_ECT}) {
+      std::vector<Work> wl = lay.work[e];
+      for (Work& wk : wl) {
+        const Region& R = lay.regions[wk.region];
+        const uint32_t* src = nullptr;
+        const uint16_t* src16 = nullptr;
+        if (R.kind == RK_SHA_BLOCK) src = lay.sha_prog.data() + wk.start;
+        else if (R.kind == RK_POSEIDON) src16 = lay.pos_prog.data() + lay.pos_prog_off[lay.pos[R.a[0]].n + 1] + wk.start;
+        else if (R.kind == RK_ECT) src = lay.ec_prog.data() + lay.ec_prog_off[R.a[1]] + wk.start;
+        else continue;
+        wk.pad = (uint32_t)mprog.size();
+        for (uint32_t q = 0; q < wk.count; q++)
+          if (kept(R.off + wk.start + q)) mprog.push_back(src ? src[q] : src16[q]);
+      }
+      if (I->d_work[e]) { (void)hipFree(I->d_work[e]); I->d_work[e] = nullptr; }
+      ok = ok && upload(&I->d_work[e], wl) == 0;
+      I->lay.work[e] = wl;
+    }
+    if (mprog.empty()) mprog.push_back(0);
+    ok = ok && upload(&I->d_mprog, mprog) == 0;
   } else {
     ok = upload(&I->d_map, inv) == 0;
   }
@@ -575,6 +603,7 @@ int pzk_layout_query(const pzk_params* params, pzk_info* info, uint32_t* n_regio
   info->n_outputs = L.n_outputs;
   info->n_public_inputs = L.n_public;
   info->n_input_groups = (uint32_t)L.inputs.size();
+  info->pipeline_depth = NSETS;
   if (n_regions) *n_regions = (uint32_t)L.regions.size();
   return 0;
 }
@@ -682,8 +711,12 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
 // emitters). Streams are not joined at the end of a call: call k + 1's cores start while call k's
 // emitters still run. Before touching set k % NSETS again, call k + NSETS waits for the end of call k
 // on all four streams (ev_done). With a caller stream the call is joined into it at exit (serialised).
+// dep: an instance stream whose work so far the call must follow (the input upload of pzk_witness_batch_host,
+// the staging-slot waits of batch_mapped). Every stream of the call descends from its chain stream st (the
+// other streams wait for events recorded on st), so st waiting for dep orders the whole call after it — also
+// when a QueryIdentity call's chain runs on s_rsa or s_tail instead of the main stream.
 static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
-                        int32_t* d_status, const pzk_exec* exec) {
+                        int32_t* d_status, const pzk_exec* exec, hipStream_t dep = nullptr) {
   const int set = (int)(I->calls % NSETS);
   Scratch& S = I->scr[set];
   int rc = ensure_scratch(I, S, batch);
@@ -706,6 +739,10 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   if (user) {
     HIPCHK(hipEventRecord(I->ev_entry, user));
     HIPCHK(hipStreamWaitEvent(st, I->ev_entry, 0));
+  }
+  if (dep && dep != st) {
+    HIPCHK(hipEventRecord(I->ev_dep, dep));
+    HIPCHK(hipStreamWaitEvent(st, I->ev_dep, 0));
   }
   const uint32_t B = (uint32_t)batch;
   const Layout& lay = I->lay;
@@ -898,9 +935,11 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   return 0;
 }
 
-// With a signal map: chunks of MAP_CHUNK witnesses, each through the O0 pipeline into d_o0[slot]
-// (slot = the chunk's scratch set, so chunk k + 2, which waits for ev_done of set k, never overwrites a
-// slot chunk k's gather still reads), then k_wtns_gather into the caller's rows on the main stream.
+// With a non-monotone signal map: chunks of MAP_CHUNK witnesses, each through the O0 pipeline into d_o0[slot]
+// (slot = chunk index & 1), then k_wtns_gather into the caller's rows on the main stream. The only guard of a
+// slot is ev_gather[slot] (the gather two chunks back that read it): the main stream waits for it, and the
+// chunk's call waits for the main stream (batch_locked's dep), whichever stream its chain runs on. The caller's
+// stream is joined the same way (its inputs may still be in flight there).
 static constexpr size_t MAP_CHUNK = 1024, MAP_CHUNK_MIN = 64;  // witnesses per O0 chunk (halved while it does not fit)
 static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
                         int32_t* d_status, const pzk_exec* exec) {
@@ -934,9 +973,9 @@ static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     const int set = (int)(I->calls % NSETS), slot = (int)((lo / chunk) & 1);
     HIPCHK(hipStreamWaitEvent(I->stream, I->ev_gather[slot], 0));  // the gather two chunks back read this slot
     int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[slot], o0_stride,
-                          d_status ? d_status + lo : nullptr, &ex);
+                          d_status ? d_status + lo : nullptr, &ex, I->stream);
     if (rc) return rc;
-    for (int i = 1; i < 5; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
+    for (int i = 0; i < 5; i++) HIPCHK(hipStreamWaitEvent(I->stream, I->ev_done[set][i], 0));
     HIPCHK(launch_wtns_gather(I->d_o0[slot], o0_stride, I->d_map, I->out_size, d_wtns + stride * lo, stride, (uint32_t)n,
                               I->stream));
     HIPCHK(hipEventRecord(I->ev_done[set][0], I->stream));
@@ -1001,8 +1040,9 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
   hipStream_t st = I->stream;
   HIPCHK(hipMemcpyAsync(I->d_in, h_inputs, in_bytes, hipMemcpyHostToDevice, st));
   pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
+  // the upload is on the main stream: batch_mapped orders every chunk after it, batch_locked via dep
   rc = I->d_map ? batch_mapped(I, I->d_in, batch, I->d_out, 32ull * I->out_size, I->d_status, &ex)
-                : batch_locked(I, I->d_in, batch, I->d_out, 32ull * I->out_size, I->d_status, &ex);
+                : batch_locked(I, I->d_in, batch, I->d_out, 32ull * I->out_size, I->d_status, &ex, st);
   if (rc) return rc;
   if ((rc = sync_all(I))) return rc;
   HIPCHK(hipMemcpy(h_wtns, I->d_out, out_bytes, hipMemcpyDeviceToHost));

@@ -112,9 +112,9 @@ def lib():
     return _lib
 
 
-def layout_info(params, circuit=None):
-    """pzk_info of a RegisterIdentityBuilder instance, from the host layout (no device)."""
-    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit)
+def layout_info(params, circuit=None, size_arg=0):
+    """pzk_info of an instance (default: RegisterIdentityBuilder), from the host layout (no device)."""
+    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit, size_arg=size_arg)
     for k, v in param_fields(params).items():
         setattr(p, k, v)
     info = PzkInfo()
@@ -132,9 +132,9 @@ def layout_inputs(params, circuit=None):
     return int(layout_info(params, circuit).n_inputs)
 
 
-def sym_check(params, sym, circuit=None):
+def sym_check(params, sym, circuit=None, size_arg=0):
     """Validate a .sym text against an instance's O0 numbering (host only) -> mapped witness size."""
-    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit)
+    p = PzkParams(circuit=PZK_CIRCUIT_REGISTER if circuit is None else circuit, size_arg=size_arg)
     for k, v in param_fields(params).items():
         setattr(p, k, v)
     b = sym.encode() if isinstance(sym, str) else sym

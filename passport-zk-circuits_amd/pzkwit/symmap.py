@@ -50,3 +50,39 @@ def synthetic_keep(o0_size, n_prefix, fraction=4, salt=0x5A):
     keep = (h % np.uint64(fraction)) == 0
     keep[:n_prefix] = True
     return keep
+
+
+# ---- circom-shaped maps (approximate --O1 / --O2; tools/gen_shape_maps.py, oracle/r1cs_shape.inc.c)
+import os  # noqa: E402
+
+SHAPE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "shape")
+
+
+def shape_path(name, level):
+    return os.path.join(SHAPE_DIR, "%s_o%d.npz" % (name, level))
+
+
+def save_shape(path, wit):
+    """wit: witness index per O0 signal (-1 = removed), stored as differences (the map is mostly a ramp)."""
+    d = np.diff(np.asarray(wit, dtype=np.int64), prepend=0).astype(np.int32)
+    np.savez_compressed(path, dwit=d)
+
+
+def load_shape(name, level):
+    """-> wit (int32 per O0 signal): the --O<level>-shaped map of a committed instance. The maps follow circom's
+    documented simplification rules applied to the restated constraints; which signals circom itself keeps is
+    parity unpinned."""
+    with np.load(shape_path(name, level)) as z:
+        return np.cumsum(z["dwit"].astype(np.int64)).astype(np.int32)
+
+
+def sym_text_wit(wit, names=None):
+    """circom .sym text of a witness-index array (signal 0, the constant, is not listed)."""
+    wit = np.asarray(wit)
+    s = np.arange(1, wit.shape[0])
+    if names is None:
+        lines = np.char.add(np.char.add(np.char.add(s.astype(str), ","), wit[1:].astype(str)), ",0,s")
+        lines = np.char.add(lines, s.astype(str))
+    else:
+        lines = ["%d,%d,0,%s" % (i, wit[i], names[i]) for i in s]
+    return "\n".join(lines) + "\n"

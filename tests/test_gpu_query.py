@@ -93,3 +93,54 @@ def test_query_witness_calculator_json(oracle):
     rc, ref = oracle.query_witness(Q.pack(inp))
     assert rc == 0 and len(w) == ref.shape[0]
     assert all(w[i] == int.from_bytes(ref[i].tobytes(), "little") for i in range(len(w)))
+
+
+def _nonmonotone_query_map(n_o0, n_in):
+    """A query .sym map that keeps a third of the signals and swaps two kept witness indices, so the instance
+    takes the staging + gather path (runtime.cpp batch_mapped)."""
+    from pzkwit import symmap
+    lines = symmap.sym_text(symmap.synthetic_keep(n_o0, 1 + 9 + n_in, fraction=3)).splitlines()
+    kept = [i for i, ln in enumerate(lines) if int(ln.split(",")[1]) > 20]
+    a, b = kept[7], kept[len(kept) // 2]
+    la, lb = lines[a].split(","), lines[b].split(",")
+    la[1], lb[1] = lb[1], la[1]
+    lines[a], lines[b] = ",".join(la), ",".join(lb)
+    txt = "\n".join(lines) + "\n"
+    inv = symmap.parse_sym(txt)
+    assert (np.diff(inv[1:]) < 0).any()
+    return txt, inv
+
+
+def test_query_gathered_map_over_three_chunks_and_stream(inst):
+    """QueryIdentity calls rotate their chain over three streams (runtime.cpp batch_locked); a gathered map runs a
+    batch as chunks of 1024 witnesses through two O0 staging slots. 2200 witnesses = three chunks, so chunk 3
+    reuses chunk 1's slot while chunk 2's chain runs on another stream: every row must equal the O0 witness at the
+    map's indices, through witness_batch_host and through witness_stream (inputs uploaded on the stream's own
+    stream)."""
+    rng = SplitMix64(0x3C3)
+    uniq = np.stack([Q.pack(Q.make_query(rng, depth=[0, 79, 40, None][k % 4])[0]) for k in range(40)])
+    w0, s0 = inst.witness_batch_host(uniq)
+    assert (s0 == 0).all()
+    txt, inv = _nonmonotone_query_map(inst.witness_size, inst.n_inputs)
+    mp = native.Instance(native.PZK_CIRCUIT_QUERY, 80, sym=txt)
+    assert mp.witness_size == inv.shape[0]
+    n = 2200
+    rows = np.concatenate([uniq] * (n // 40))
+    want = w0[:, inv]
+    wm, sm = mp.witness_batch_host(rows)
+    assert (sm == 0).all()
+    for i in range(0, n, 97):
+        assert (wm[i] == want[i % 40]).all(), i
+    assert all((wm[i] == want[i % 40]).all() for i in range(n - 40, n))
+    del wm
+    seen = []
+
+    def sink(first, w, st):
+        assert (st == 0).all()
+        for k in range(0, w.shape[0], 61):
+            assert (w[k] == want[(first + k) % 40]).all(), first + k
+        assert (w[-1] == want[(first + w.shape[0] - 1) % 40]).all()
+        seen.append((first, w.shape[0]))
+
+    mp.witness_stream(rows, sink, chunk=n)
+    assert seen == [(0, n)]

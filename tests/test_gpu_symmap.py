@@ -119,3 +119,37 @@ def test_keep_all_map_is_o0_and_nonmonotone_map_gathers():
     assert (np.diff(inv[1:]) < 0).any()
     _, _, wm2, sm2 = _host_pair(params, txt, rows)
     assert (sm2 == 0).all() and (wm2 == w0[:, inv]).all()
+
+
+@pytest.mark.parametrize("name,level", [("register_canonical", 1), ("register_canonical", 2), ("register_sig20", 2),
+                                        ("query", 1), ("query", 2)])
+def test_shape_maps_equal_o0_subset(name, level):
+    """The circom-shaped maps (approximate --O1 / --O2, data/shape/, tools/gen_shape_maps.py): every emitter writes
+    only the kept elements (mapsink.hpp kept_collect / desc_run) and the mapped rows equal the O0 rows at the map's
+    indices, element for element, with merged signals read through their class's first signal."""
+    wit = symmap.load_shape(name, level)
+    txt = symmap.sym_text_wit(wit)
+    inv = symmap.parse_sym(txt)
+    if name == "query":
+        from pzkwit import query as Q
+        from pzkwit.field import SplitMix64
+        rng = SplitMix64(0x5A + level)
+        rows = np.stack([Q.pack(Q.make_query(rng, depth=d)[0]) for d in (0, 79, 40, None, 5)])
+        o0 = native.Instance(native.PZK_CIRCUIT_QUERY, 80)
+        mp = native.Instance(native.PZK_CIRCUIT_QUERY, 80, sym=txt)
+    else:
+        params = I.CANONICAL if name == "register_canonical" else I.instance_params(20)
+        g = I.PassportGen(seed=0x90 + level, n_keys=1, params=params, workers=1)
+        rows = np.stack([I.pack_register_inputs(g.passport_at(i, smt_depth=3 * i), params) for i in range(3)])
+        o0 = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params)
+        mp = native.Instance(native.PZK_CIRCUIT_REGISTER, 0, params, sym=txt)
+    assert mp.witness_size == inv.shape[0] == wit.max() + 1
+    w0, s0 = o0.witness_batch_host(rows)
+    wm, sm = mp.witness_batch_host(rows)
+    assert (s0 == 0).all() and (sm == s0).all()
+    for b in range(rows.shape[0]):
+        bad = np.nonzero((wm[b] != w0[b][inv]).any(axis=1))[0]
+        assert bad.size == 0, "%s O%d row %d: %d mapped elements differ (first k=%d, O0 %d)" % (
+            name, level, b, bad.size, bad[0], inv[bad[0]])
+        merged = np.flatnonzero(wit >= 0)
+        assert (w0[b][merged] == wm[b][wit[merged]]).all()  # merged signals carry their class's value

@@ -167,7 +167,7 @@ class _StubEngine:
 
     def __init__(self, args, workload, dev):
         import torch
-        nin = 842 if workload == "query" else 3072
+        nin = {"query": 842, "register": 5778}.get(workload, 3072)
         self.torch, self.NIN, self.W, self.n_pub, self.inst = torch, nin, nin + 300, 4, _StubInst()
         self.layout = "stub"
 
@@ -194,7 +194,8 @@ def _bench_rank(rank, world, port, q, workload="sha256"):
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    args = argparse.Namespace(workload=workload, batch=6, sub=None, slots=1, steps=2, warmup=1, sig_eff=0, no_cpu=True,
+    args = argparse.Namespace(workload=workload, batch=6, sub=None, slots=1, steps=2, warmup=1,
+                              sig_eff=1 if workload == "register" else 0, no_cpu=True,
                               no_host=True,
                               gpus=world)
     r = bench.run_rank(args, rank, world, 0, dist, engine_cls=_StubEngine, device="cpu")
@@ -203,11 +204,12 @@ def _bench_rank(rank, world, port, q, workload="sha256"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("workload", ["sha256", "query"])
+@pytest.mark.parametrize("workload", ["sha256", "query", "register"])
 def test_bench_two_ranks_gloo_scatter_gather(workload):
     """bench.run_rank over a 2-rank gloo group with the GPU path stubbed: rank 0 generates the job's
     inputs and scatters the shards, the ranks' statuses and public rows are gathered in global order,
-    and the record reports n_gpus = 2. Also for the QueryIdentity workload (its rows)."""
+    and the record reports n_gpus = 2. Also for the QueryIdentity and the config-3
+    RegisterIdentityBuilder workloads (their rows)."""
     import hashlib
     import socket
     import torch.multiprocessing as mp
@@ -230,6 +232,9 @@ def test_bench_two_ranks_gloo_scatter_gather(workload):
     if workload == "query":
         from pzkwit import query as Q
         rows = Q.batch_rows(12, seed=0x9, distinct=64)
+    elif workload == "register":
+        import bench
+        rows = bench.make_register_inputs(12, 0, seed=bench.SIG_SEED[1], sig=1, workers=2)
     else:
         _, rows = I.sha256_config2_batch(12, seed=2, blocks=6)
     assert g["witnesses"] == 12
@@ -259,3 +264,131 @@ def test_sym_map_validation():
                      ("%d,1,0,a\n" % n_o0, "outside"), ("x,1,0,a\n", "expected"), ("1,-1,0,a\n", "no signal")]:
         with pytest.raises(native.PzkError, match=msg):
             native.sym_check(I.CANONICAL, bad)
+
+
+# ---- config 5 (mixed flows) over two ranks: bench.run_mixed_rank with a stub engine and stub rows
+def _mixed_row(gi, sg, n_in):
+    """stub input row of global witness gi of flow sg: element k = (gi, sg, k) in its first bytes"""
+    r = np.zeros((n_in, 32), dtype=np.uint8)
+    k = np.arange(n_in)
+    r[:, 0] = (gi * 7 + k) & 0xFF
+    r[:, 1] = sg
+    r[:, 2] = k & 0xFF
+    r[:, 3] = k >> 8
+    r[:, 4] = gi & 0xFF
+    return r
+
+
+def _mixed_stub_rows(sigs, lo, hi, n_in_max, workers):
+    """bench._mixed_host_rows' layout (grouped per flow in MIX order, rows padded to n_in_max) with stub rows"""
+    import bench
+    from pzkwit import native
+    out = np.zeros((hi - lo, n_in_max, 32), dtype=np.uint8)
+    pos = 0
+    for sg, idx in bench._mixed_groups(sigs, lo, hi).items():
+        n_in = native.layout_inputs(dict(I.CANONICAL, sig=sg))
+        for gi in idx:
+            out[pos, :n_in] = _mixed_row(gi, sg, n_in)
+            pos += 1
+    return out
+
+
+def _mixed_digest(row_bytes):
+    import hashlib
+    return np.frombuffer(hashlib.sha256(row_bytes).digest(), dtype=np.uint8)
+
+
+class _MixedStubEngine:
+    """bench.MixedGpuEngine's interface on the CPU. Status = element 0's byte 0 & 1 of the flow's compact row;
+    public signals = elements 1..4 of the compact row and a digest of the WHOLE compact row (so a wrong per-flow
+    width in the rank's cut shows)."""
+
+    def __init__(self, flows, groups, dev):
+        import torch
+        from pzkwit import native
+        self.torch, self.groups = torch, groups
+        self.n_inputs = {sg: native.layout_inputs(flows[sg]) for sg in groups}
+
+    def setup(self, d_in, first, n_local):
+        self.d_in, self.first = d_in, first
+        self.d_st = self.torch.zeros(n_local, dtype=self.torch.int32)
+
+    def step(self):
+        for sg in self.groups:
+            rows = self.d_in[sg].view(-1, self.n_inputs[sg], 32)
+            self.d_st[self.first[sg]: self.first[sg] + rows.shape[0]] = (rows[:, 0, 0] & 1).to(self.torch.int32)
+
+    def sync(self):
+        pass
+
+    def statuses(self):
+        return self.d_st
+
+    def public_pass(self, n_pub):
+        torch = self.torch
+        pub = torch.zeros((self.d_st.shape[0], n_pub, 32), dtype=torch.uint8)
+        for sg in self.groups:
+            rows = self.d_in[sg].view(-1, self.n_inputs[sg], 32)
+            f = self.first[sg]
+            pub[f: f + rows.shape[0], :4] = rows[:, 1:5]
+            for k in range(rows.shape[0]):
+                pub[f + k, 4] = torch.from_numpy(_mixed_digest(rows[k].numpy().tobytes()).copy())
+        return self.d_st.clone(), pub
+
+
+def _mixed_rank(rank, world, port, q):
+    import argparse
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = argparse.Namespace(workload="mixed", batch=10, steps=2, warmup=1, gpus=world)
+    out = bench.run_mixed_rank(args, rank, world, 0, dist, engine_cls=_MixedStubEngine, device="cpu",
+                               rows_fn=_mixed_stub_rows)
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_mixed_bench_two_ranks_gloo():
+    """Config 5's multi-rank path (bench.run_mixed_rank) over a 2-rank gloo group with the GPU path stubbed: the
+    per-flow grouped scatter from rank 0, each rank's cut back to compact rows of its flows' own widths, and the
+    all-gather of statuses and public rows in rank-major, per-flow grouped order."""
+    import hashlib
+    import socket
+    import torch.multiprocessing as mp
+    import bench
+    from pzkwit import native
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if repo not in sys.path:
+        sys.path.insert(0, repo)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mixed_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = q.get(timeout=180)
+    for p in ps:
+        p.join(60)
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    # expected gather: rank-major, within a rank per flow (MIX order), global order inside a flow
+    sigs, flows, costs, shards = bench._mixed_plan(10, 2)
+    st, pub = [], []
+    for lo, hi in shards:
+        for sg, idx in bench._mixed_groups(sigs, lo, hi).items():
+            n_in = native.layout_inputs(flows[sg])
+            for gi in idx:
+                r = _mixed_row(gi, sg, n_in)
+                st.append(int(r[0, 0]) & 1)
+                p = np.zeros((5, 32), dtype=np.uint8)
+                p[:4] = r[1:5]
+                p[4] = _mixed_digest(r.tobytes())
+                pub.append(p)
+    g = out["config"]["gathered"]
+    assert g["witnesses"] == 20 and g["status_nonzero"] == sum(st)
+    assert g["public_sha256"] == hashlib.sha256(np.stack(pub).tobytes()).hexdigest()[:16]
+    assert out["config"]["invalid_lanes"] == sum(st)  # both ranks' last timed step
+    assert set(out["config"]["flows"]) <= {"1", "2", "20"}

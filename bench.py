@@ -24,6 +24,9 @@ sys.path.insert(0, os.path.join(REPO, "passport-zk-circuits_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md: a wave
+# issues each VALU instruction over 2 cycles), 2.4 GHz max clock -> G wave-instructions/s
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2
 
 
 def log(*a):
@@ -418,6 +421,22 @@ def report(args, r, world):
     # whole-job algorithmic bytes: inputs read once + .wtns header and elements written once
     job_bytes = 32 * NIN + 76 + 32 * W
     job_gbs = value * job_bytes / 1e9
+    # whole-job VALU roofline: wave-level VALU instructions per witness (SQ_INSTS_VALU summed over the job's kernels,
+    # from the committed PMC pass of this workload) x witnesses/s against the chip's VALU issue rate
+    valu = None
+    for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
+        if not r["engine"].layout.startswith("O0"):
+            break
+        tj = json.load(open(tf))
+        if tj.get("workload") == workload and tj.get("valu_insts_per_witness"):
+            ipw = tj["valu_insts_per_witness"]
+            ach = ipw * value / 1e9
+            top = sorted(((v.get("valu_insts_per_witness", 0), k) for k, v in tj["kernels"].items()), reverse=True)[:3]
+            valu = {"bound": "valu", "insts_per_witness": ipw, "achieved": round(ach, 1), "peak": VALU_PEAK_GIPS,
+                    "unit": "G wave-instr/s", "frac": round(ach / (VALU_PEAK_GIPS * world), 4),
+                    "top_kernels": {k: v for v, k in top}, "source": os.path.relpath(tf, REPO),
+                    "note": "issue-rate bound (1 wave64 VALU instruction / 2 cycles / SIMD at 2.4 GHz); 64-bit "
+                            "integer multiply-adds take more than one issue slot, so the attainable fraction is < 1"}
     phases = {p: {"ms_per_launch": round(tm[p][0] / max(tm[p][1], 1), 4), "launches": tm[p][1],
                   "kernel": info[p][0], "alg_bytes_per_witness": info[p][1]} for p in tm if tm[p][1]}
     out = {
@@ -434,7 +453,8 @@ def report(args, r, world):
         "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "bytes_per_launch": int(bytes_per_launch),
-                     "avg_launch_ms": round(avg_ms, 4)},
+                     "avg_launch_ms": round(avg_ms, 4), "valu": valu,
+                     "job_bound": ("valu" if valu and valu["frac"] > job_gbs / (HBM_PEAK_GBS * world) else "hbm")},
         "job_hbm": {"alg_bytes_per_witness": job_bytes, "achieved": round(job_gbs, 1), "unit": "GB/s",
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
         "phases": phases,

@@ -42,7 +42,8 @@ enum {
  * verbatim, plus the circuit family and its size argument for the standalone circuits. */
 typedef struct pzk_params {
   int32_t circuit;            /* PZK_CIRCUIT_* */
-  int32_t size_arg;           /* n for POSEIDON, blocks for SHA256 / SHA1 / SHA384 / SHA512; ignored for REGISTER */
+  int32_t size_arg;           /* n for POSEIDON, blocks for SHA256 / SHA1 / SHA384 / SHA512, idTreeDepth (80) for
+                                 QUERY; ignored for REGISTER */
   int32_t signature_type;     /* SIGNATURE_TYPE (signatureVerification.circom:9-127): 1 = RSA-2048 PKCS#1 v1.5
                                  SHA-256 e = 65537, 2 = RSA-4096, 3 = RSA-2048 SHA-1, 4 = RSA-3072 SHA-1
                                  e = 37187; 10-12 = RSA-2048 PSS SHA-256 (10: e = 3; 12: salt 64), 13 = RSA-2048

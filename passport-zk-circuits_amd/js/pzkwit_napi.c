@@ -16,6 +16,17 @@
  *        inputs: Buffer of batch x nInputs x 32 B (LE normal form); runs pzk_witness_batch_host
  *        on a libuv worker thread (napi_create_async_work), so the event loop stays free.
  *
+ *   witnessBatchWtns(handle, inputs, batch) -> Promise<{ wtns: Buffer, status: Int32Array }>: the same batch as
+ *        ONE Buffer of batch .wtns images back to back (76-byte header + witness each), so a caller takes
+ *        per-input .wtns as views (subarray) instead of copies; rows arrive through pzk_witness_stream (pinned
+ *        chunks, device->host copy beside compute) and are copied once into their image.
+ *   witnessStream(handle, inputs, batch, chunk, onChunk) -> Promise<void>: pzk_witness_stream, the streamed
+ *        form of gen-witness.sh:25's one-.wtns-per-input loop. onChunk(first, rows, status) runs on the JS
+ *        thread for each chunk in order: rows is a Buffer over the library's PINNED chunk slot (n x witnessSize
+ *        x 32 B, no copy), valid only until onChunk returns or the promise it returns settles — the slot is then
+ *        reused; status is an Int32Array copy. A truthy result (or promise value) or a throw stops the stream and
+ *        rejects the call (a throw with its own error). Host memory stays at two chunks whatever the batch.
+ *
  *   passportParse({ dg1, dg15, sod })       -> { params, name, refAaShift, ... } (pzk_passport_parse)
  *   passportInputs(params, passports, identity, threads)
  *                                           -> Promise<{ rows: Buffer, status: Int32Array }>: the bulk SOD
@@ -28,7 +39,9 @@
  * N-API version 4 features only (Node >= 10.16 / 12.x).
  */
 #define NAPI_VERSION 4
+#define _POSIX_C_SOURCE 200809L
 #include <node_api.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -287,6 +300,261 @@ static napi_value js_witness_batch(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+
+/* ---------------------------------------------------------------- streamed delivery (pzk_witness_stream) */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref inputs_ref;
+  napi_ref error_ref;           /* the exception onChunk threw, to reject with */
+  napi_threadsafe_function tsfn;
+  pzk_instance* inst;
+  const uint8_t* inputs;
+  size_t batch, chunk;
+  /* the chunk being handed over (set on the worker thread, read on the JS thread) */
+  size_t first, n, stride;
+  const uint8_t* rows;
+  const int32_t* status;
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  int handed, sink_rc;
+  /* witnessBatchWtns: the sink copies rows into batch .wtns images instead of calling JS */
+  uint8_t* images;
+  int32_t* img_status;
+  size_t img_bytes;
+  uint8_t header[76];
+  int rc;
+  char err[512];
+} stream_job;
+
+static void stream_release(stream_job* j, int rc) {
+  pthread_mutex_lock(&j->mu);
+  j->sink_rc = rc;
+  j->handed = 1;
+  pthread_cond_signal(&j->cv);
+  pthread_mutex_unlock(&j->mu);
+}
+
+static stream_job* cb_job(napi_env env, napi_callback_info info, napi_value* arg) {
+  size_t argc = 1;
+  void* data = NULL;
+  if (napi_get_cb_info(env, info, &argc, arg, NULL, &data) != napi_ok) return NULL;
+  if (argc < 1) napi_get_undefined(env, arg);
+  return (stream_job*)data;
+}
+
+static int truthy(napi_env env, napi_value v) {
+  napi_value b;
+  bool r = false;
+  if (napi_coerce_to_bool(env, v, &b) != napi_ok || napi_get_value_bool(env, b, &r) != napi_ok) return 1;
+  return r ? 1 : 0;
+}
+
+/* the promise onChunk returned settled */
+static napi_value chunk_fulfilled(napi_env env, napi_callback_info info) {
+  napi_value v;
+  stream_job* j = cb_job(env, info, &v);
+  if (j) stream_release(j, truthy(env, v));
+  return NULL;
+}
+static napi_value chunk_rejected(napi_env env, napi_callback_info info) {
+  napi_value v;
+  stream_job* j = cb_job(env, info, &v);
+  if (j) {
+    if (!j->error_ref) napi_create_reference(env, v, 1, &j->error_ref);
+    stream_release(j, 1);
+  }
+  return NULL;
+}
+
+static void noop_finalize(napi_env env, void* data, void* hint) { (void)env; (void)data; (void)hint; }
+
+/* JS thread: onChunk(first, rows, status) for the chunk the worker is blocked on */
+static void stream_call_js(napi_env env, napi_value js_cb, void* context, void* data) {
+  stream_job* j = (stream_job*)data;
+  (void)context;
+  if (!env) { stream_release(j, 1); return; }  /* the environment is shutting down */
+  napi_value argv[3], undef, ret, sab;
+  void* st_copy = NULL;
+  int ok = napi_create_double(env, (double)j->first, &argv[0]) == napi_ok &&
+           napi_create_external_buffer(env, j->n * j->stride, (void*)j->rows, noop_finalize, NULL, &argv[1]) == napi_ok &&
+           napi_create_arraybuffer(env, j->n * sizeof(int32_t), &st_copy, &sab) == napi_ok;
+  if (ok) {
+    memcpy(st_copy, j->status, j->n * sizeof(int32_t));
+    ok = napi_create_typedarray(env, napi_int32_array, j->n, sab, 0, &argv[2]) == napi_ok &&
+         napi_get_undefined(env, &undef) == napi_ok;
+  }
+  if (!ok) { stream_release(j, 1); return; }
+  if (napi_call_function(env, undef, js_cb, 3, argv, &ret) != napi_ok) {
+    napi_value exc;
+    if (napi_get_and_clear_last_exception(env, &exc) == napi_ok && !j->error_ref)
+      napi_create_reference(env, exc, 1, &j->error_ref);
+    stream_release(j, 1);
+    return;
+  }
+  /* a thenable: wait for it to settle (e.g. an fs.promises write of the chunk's .wtns files) */
+  napi_valuetype t;
+  bool has_then = false;
+  napi_value then_fn;
+  if (napi_typeof(env, ret, &t) == napi_ok && t == napi_object &&
+      napi_has_named_property(env, ret, "then", &has_then) == napi_ok && has_then &&
+      napi_get_named_property(env, ret, "then", &then_fn) == napi_ok) {
+    napi_value fns[2];
+    if (napi_create_function(env, "fulfilled", NAPI_AUTO_LENGTH, chunk_fulfilled, j, &fns[0]) == napi_ok &&
+        napi_create_function(env, "rejected", NAPI_AUTO_LENGTH, chunk_rejected, j, &fns[1]) == napi_ok &&
+        napi_call_function(env, ret, then_fn, 2, fns, NULL) == napi_ok)
+      return;
+    stream_release(j, 1);
+    return;
+  }
+  stream_release(j, truthy(env, ret));
+}
+
+/* worker thread (inside pzk_witness_stream): hand the chunk to JS and wait until it is done with the rows */
+static int stream_sink(void* user, size_t first, size_t n, const uint8_t* rows, size_t stride, const int32_t* status) {
+  stream_job* j = (stream_job*)user;
+  if (j->images) {  /* witnessBatchWtns: one copy into the chunk's .wtns images */
+    const size_t img = 76 + stride;
+    for (size_t i = 0; i < n; i++) {
+      memcpy(j->images + (first + i) * img, j->header, 76);
+      memcpy(j->images + (first + i) * img + 76, rows + i * stride, stride);
+    }
+    memcpy(j->img_status + first, status, n * sizeof(int32_t));
+    return 0;
+  }
+  pthread_mutex_lock(&j->mu);
+  j->first = first; j->n = n; j->rows = rows; j->stride = stride; j->status = status; j->handed = 0;
+  pthread_mutex_unlock(&j->mu);
+  if (napi_call_threadsafe_function(j->tsfn, j, napi_tsfn_blocking) != napi_ok) return 1;
+  pthread_mutex_lock(&j->mu);
+  while (!j->handed) pthread_cond_wait(&j->cv, &j->mu);
+  const int rc = j->sink_rc;
+  pthread_mutex_unlock(&j->mu);
+  return rc;
+}
+
+static void stream_execute(napi_env env, void* data) {
+  (void)env;
+  stream_job* j = (stream_job*)data;
+  j->rc = pzk_witness_stream(j->inst, j->inputs, j->batch, j->chunk, stream_sink, j, NULL);
+  if (j->rc) snprintf(j->err, sizeof j->err, "pzk_witness_stream: %s", pzk_last_error());
+}
+
+static void stream_complete(napi_env env, napi_status st, void* data) {
+  stream_job* j = (stream_job*)data;
+  napi_value err_msg, err, result;
+  napi_delete_reference(env, j->inputs_ref);
+  if (j->tsfn) napi_release_threadsafe_function(j->tsfn, napi_tsfn_release);
+  if (st != napi_ok || j->rc != 0) {
+    if (j->error_ref && napi_get_reference_value(env, j->error_ref, &err) == napi_ok && err) {
+      napi_reject_deferred(env, j->deferred, err);
+    } else {
+      napi_create_string_utf8(env, j->rc ? j->err : "pzkwit: async work cancelled", NAPI_AUTO_LENGTH, &err_msg);
+      napi_create_error(env, NULL, err_msg, &err);
+      napi_reject_deferred(env, j->deferred, err);
+    }
+    free(j->images);
+    free(j->img_status);
+  } else if (j->images) {
+    napi_value wbuf, sab, sarr;
+    napi_create_object(env, &result);
+    napi_create_external_buffer(env, j->img_bytes, j->images, free_cb, NULL, &wbuf);
+    napi_create_external_arraybuffer(env, j->img_status, j->batch * sizeof(int32_t), free_cb, NULL, &sab);
+    napi_create_typedarray(env, napi_int32_array, j->batch, sab, 0, &sarr);
+    napi_set_named_property(env, result, "wtns", wbuf);
+    napi_set_named_property(env, result, "status", sarr);
+    napi_resolve_deferred(env, j->deferred, result);
+  } else {
+    napi_get_undefined(env, &result);
+    napi_resolve_deferred(env, j->deferred, result);
+  }
+  if (j->error_ref) napi_delete_reference(env, j->error_ref);
+  pthread_mutex_destroy(&j->mu);
+  pthread_cond_destroy(&j->cv);
+  napi_delete_async_work(env, j->work);
+  free(j);
+}
+
+/* shared argument handling of witnessStream / witnessBatchWtns: (handle, inputs, batch, ...) */
+static stream_job* stream_job_new(napi_env env, napi_value* argv, pzk_info* pi) {
+  pzk_instance* inst = get_instance(env, argv[0]);
+  if (!inst) return NULL;
+  void* in_data = NULL;
+  size_t in_len = 0;
+  if (napi_get_buffer_info(env, argv[1], &in_data, &in_len) != napi_ok) {
+    napi_throw_type_error(env, NULL, "inputs must be a Buffer");
+    return NULL;
+  }
+  uint32_t batch = 0;
+  if (napi_get_value_uint32(env, argv[2], &batch) != napi_ok) { napi_throw_type_error(env, NULL, "batch"); return NULL; }
+  if (pzk_instance_info(inst, pi) != 0) { throw_pzk(env, "pzk_instance_info"); return NULL; }
+  if ((uint64_t)in_len != (uint64_t)batch * pi->n_inputs * 32) {
+    napi_throw_range_error(env, NULL, "inputs length != batch * nInputs * 32");
+    return NULL;
+  }
+  stream_job* j = (stream_job*)calloc(1, sizeof(stream_job));
+  if (!j) { napi_throw_error(env, NULL, "pzkwit: host allocation failed"); return NULL; }
+  j->inst = inst;
+  j->inputs = (const uint8_t*)in_data;
+  j->batch = batch;
+  pthread_mutex_init(&j->mu, NULL);
+  pthread_cond_init(&j->cv, NULL);
+  if (napi_create_reference(env, argv[1], 1, &j->inputs_ref) != napi_ok) {
+    free(j);
+    napi_throw_error(env, NULL, "pzkwit: reference");
+    return NULL;
+  }
+  return j;
+}
+
+static napi_value stream_start(napi_env env, stream_job* j, const char* what) {
+  napi_value promise, name;
+  CHECK(napi_create_promise(env, &j->deferred, &promise));
+  CHECK(napi_create_string_utf8(env, what, NAPI_AUTO_LENGTH, &name));
+  CHECK(napi_create_async_work(env, NULL, name, stream_execute, stream_complete, j, &j->work));
+  CHECK(napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+static napi_value js_witness_stream(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5], name;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 5) { napi_throw_type_error(env, NULL, "witnessStream(handle, inputs, batch, chunk, onChunk)"); return NULL; }
+  napi_valuetype t;
+  CHECK(napi_typeof(env, argv[4], &t));
+  if (t != napi_function) { napi_throw_type_error(env, NULL, "onChunk must be a function"); return NULL; }
+  uint32_t chunk = 0;
+  CHECK(napi_get_value_uint32(env, argv[3], &chunk));
+  pzk_info pi;
+  stream_job* j = stream_job_new(env, argv, &pi);
+  if (!j) return NULL;
+  j->chunk = chunk;
+  CHECK(napi_create_string_utf8(env, "pzkwit.witnessStream", NAPI_AUTO_LENGTH, &name));
+  CHECK(napi_create_threadsafe_function(env, argv[4], NULL, name, 0, 1, NULL, NULL, NULL, stream_call_js, &j->tsfn));
+  return stream_start(env, j, "pzkwit.witnessStream");
+}
+
+static napi_value js_witness_batch_wtns(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) { napi_throw_type_error(env, NULL, "witnessBatchWtns(handle, inputs, batch)"); return NULL; }
+  pzk_info pi;
+  stream_job* j = stream_job_new(env, argv, &pi);
+  if (!j) return NULL;
+  j->img_bytes = j->batch * (76 + (size_t)pi.witness_size * 32);
+  j->images = (uint8_t*)malloc(j->img_bytes ? j->img_bytes : 1);
+  j->img_status = (int32_t*)calloc(j->batch ? j->batch : 1, sizeof(int32_t));
+  if (!j->images || !j->img_status || pzk_wtns_header(j->inst, j->header) != 0) {
+    napi_delete_reference(env, j->inputs_ref);
+    free(j->images); free(j->img_status); free(j);
+    napi_throw_error(env, NULL, "pzkwit: host allocation failed");
+    return NULL;
+  }
+  return stream_start(env, j, "pzkwit.witnessBatchWtns");
+}
+
 /* ---------------------------------------------------------------- SOD preprocessor (pzkpassport.h) */
 static napi_value params_object(napi_env env, const pzk_params* p) {
   napi_value o, v;
@@ -478,6 +746,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"instanceInfo", NULL, js_instance_info, NULL, NULL, NULL, napi_enumerable, NULL},
       {"wtnsHeader", NULL, js_wtns_header, NULL, NULL, NULL, napi_enumerable, NULL},
       {"witnessBatch", NULL, js_witness_batch, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"witnessBatchWtns", NULL, js_witness_batch_wtns, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"witnessStream", NULL, js_witness_stream, NULL, NULL, NULL, napi_enumerable, NULL},
       {"passportParse", NULL, js_passport_parse, NULL, NULL, NULL, napi_enumerable, NULL},
       {"passportInputs", NULL, js_passport_inputs, NULL, NULL, NULL, napi_enumerable, NULL},
   };

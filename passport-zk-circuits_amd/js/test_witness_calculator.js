@@ -2,10 +2,12 @@
 //   node test_witness_calculator.js cpu [PP.json ROWS.bin]   addon loads, marshalling + error texts; with
 //        PP.json ({ params, passports: [{dg1, dg15, sod} base64], names }) the bulk preprocessor binding:
 //        passportParse names and passportInputs rows == ROWS.bin (the C-ABI's rows, via Python)
-//   node test_witness_calculator.js gpu IN.json OUT.wtns [EXTRA.json]
+//   node test_witness_calculator.js gpu IN.json OUT.wtns [EXTRA.json [OUTDIR]]
 //        Poseidon KAT, then the register witness of IN.json written as .wtns; with EXTRA.json
-//        ({ inputs: [3 passports' JSON], sym: ".sym text" }) concurrent calls on different passports and a
-//        .sym-mapped instance
+//        ({ inputs: [3 passports' JSON], sym: ".sym text" }) concurrent calls on different passports, a
+//        .sym-mapped instance, and the streamed forms: 64 witnesses in chunks of 16 checked against the serial
+//        results with the process's resident memory bounded by two chunks, an async sink, a sink that stops the
+//        stream, and (OUTDIR) writeWTNSFiles of [IN, 3 passports] as OUTDIR/w<i>.wtns
 "use strict";
 const assert = require("assert");
 const fs = require("fs");
@@ -109,10 +111,55 @@ async function gpu(inPath, outPath, extraPath) {
       if (Buffer.compare(mw.subarray(76 + 32 * k, 108 + 32 * k), o0.subarray(76 + 32 * inv[k], 108 + 32 * inv[k])) !== 0)
         throw new Error(`mapped element ${k} (signal ${inv[k]}) differs`);
   }
+  if (extraPath) {
+    const extra = JSON.parse(fs.readFileSync(extraPath, "utf8"));
+    const three = extra.inputs;
+    const ser = [];
+    for (const x of three) ser.push(Buffer.from(await rc.calculateWTNSBin(x, true)));
+    const rowBytes = rc.witnessSize * 32, chunk = 16, n = 64;
+    // streamed, 64 witnesses (the three passports tiled) in chunks of 16: every witness equals its passport's
+    // serial .wtns, in order, and the resident set grows by about two chunks of rows (the library's pinned
+    // slots), not by the 64 witnesses a batch call would hold
+    const inputs64 = Array.from({ length: n }, (_, i) => three[i % 3]);
+    global.gc && global.gc();
+    const rss0 = process.memoryUsage().rss;
+    let peak = rss0, next = 0;
+    await rc.calculateWTNSBinStream(inputs64, (i, header, witness, st) => {
+      assert.strictEqual(i, next++);
+      assert.strictEqual(st, 0);
+      assert.ok(Buffer.compare(Buffer.from(header), ser[i % 3].subarray(0, 76)) === 0, `header ${i}`);
+      assert.ok(Buffer.compare(witness, ser[i % 3].subarray(76)) === 0, `streamed witness ${i}`);
+      peak = Math.max(peak, process.memoryUsage().rss);
+    }, true, chunk);
+    assert.strictEqual(next, n);
+    const grew = peak - rss0, bound = 2.5 * chunk * rowBytes + 512e6;
+    assert.ok(grew < bound && grew < n * rowBytes, `resident set grew ${grew} B (bound ${bound})`);
+    // an async sink: the library waits for each chunk's promise before reusing its pinned slot
+    let seen = 0;
+    await rc.calculateWTNSBinStream(inputs64.slice(0, 8), async (i, header, witness) => {
+      await new Promise((r) => setTimeout(r, 1));
+      assert.ok(Buffer.compare(witness, ser[i % 3].subarray(76)) === 0, `async sink ${i}`);
+      seen++;
+    }, true, 3);
+    assert.strictEqual(seen, 8);
+    // a throwing sink stops the stream and rejects with its own error
+    await assert.rejects(rc.calculateWTNSBinStream(inputs64.slice(0, 6), (i) => {
+      if (i === 3) throw new Error("stop at 3");
+    }, true, 2), /stop at 3/);
+    // the instance still works after a stopped stream
+    const again = Buffer.from(await rc.calculateWTNSBin(three[0], true));
+    assert.ok(Buffer.compare(again, ser[0]) === 0);
+    if (outDir) {
+      const path = require("path");
+      const cnt = await rc.writeWTNSFiles([input].concat(three), (i) => path.join(outDir, `w${i}.wtns`), true, 2);
+      assert.strictEqual(cnt, 4);
+    }
+    console.log(`js stream ok (64 witnesses, resident +${(grew / 1e9).toFixed(2)} GB for chunks of ${chunk})`);
+  }
   console.log(`js gpu ok (witnessSize ${rc.witnessSize}, ${Date.now() - t0} ms)`);
 }
 
-const ppPath = mode === "cpu" ? process.argv[3] : null, rowsPath = process.argv[4];
+const ppPath = mode === "cpu" ? process.argv[3] : null, rowsPath = process.argv[4], outDir = process.argv[6];
 (mode === "cpu" ? cpu() : gpu(process.argv[3], process.argv[4], process.argv[5])).catch((e) => {
   console.error(e);
   process.exit(1);

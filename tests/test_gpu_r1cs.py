@@ -56,10 +56,11 @@ def test_sha512_device_witnesses(out_bits, blocks):
 
 @pytest.mark.parametrize("sig,depths", [(1, [0, 1, 2, 40, 79, 0, 5, 17]), (2, [0, 9, 33]), (3, [0, 4]), (4, [2]),
                                         (10, [0, 3]), (11, [0, 6]), (12, [1]), (13, [0, 3]), (14, [0]), (20, [0, 2]),
-                                        (21, [1])])
+                                        (21, [1]), (24, [0]), (25, [2])])
 def test_config3_4_register_device_witnesses(sig, depths):
     """Config 3 (canonical, SMT root of the one-leaf tree) and config 4 (depth-k SMT paths), the
-    RSA-4096 flow of config 5 and the SHA-1 / RSA-3072 / RSA-PSS instances: every device witness
+    RSA-4096 flow of config 5, the SHA-1 / RSA-3072 / RSA-PSS instances and the ECDSA curves (P-256,
+    brainpoolP256r1, secp224r1, brainpoolP384r1): every device witness
     satisfies all of its constraints (2.25 M for the canonical instance)."""
     params = I.instance_params(sig)
     g = I.PassportGen(seed=0x40 + sig, n_keys=2, params=params, workers=1)

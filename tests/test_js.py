@@ -56,11 +56,15 @@ def test_js_register_wtns_matches_oracle(oracle, tmp_path):
     n_o0 = native.layout_witness_size(I.CANONICAL)
     keep = symmap.synthetic_keep(n_o0, 1 + 4 + 5778, fraction=4)
     merged = symmap.synthetic_keep(n_o0, 0, fraction=5, salt=0x33)
-    extra.write_text(json.dumps({"inputs": [I.passport_json(gen.passport_at(k, smt_depth=d)) for k, d in ((8, 3), (9, 0), (10, 7))],
+    three = [gen.passport_at(k, smt_depth=d) for k, d in ((8, 3), (9, 0), (10, 7))]
+    extra.write_text(json.dumps({"inputs": [I.passport_json(p) for p in three],
                                  "sym": symmap.sym_text(keep, merged=merged)}))
-    r = subprocess.run(["node", "test_witness_calculator.js", "gpu", str(inp), str(out), str(extra)], cwd=JS,
-                       capture_output=True, text=True, timeout=600)
+    outdir = tmp_path / "wtns"
+    outdir.mkdir()
+    r = subprocess.run(["node", "--expose-gc", "test_witness_calculator.js", "gpu", str(inp), str(out), str(extra),
+                        str(outdir)], cwd=JS, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "js stream ok" in r.stdout, r.stdout
     data = out.read_bytes()
     prm = oracle.register_params(**I.CANONICAL)
     rc, ref = oracle.register_witness(prm, I.pack_register_inputs(pp))
@@ -68,3 +72,8 @@ def test_js_register_wtns_matches_oracle(oracle, tmp_path):
     assert data[:4] == b"wtns" and len(data) == 76 + ref.size
     got = np.frombuffer(data[76:], dtype=np.uint8).reshape(ref.shape)
     assert (got == ref).all()
+    # writeWTNSFiles (streamed, one .wtns per input as gen-witness.sh:25): each file == header + oracle witness
+    for i, p in enumerate([pp] + three):
+        f = (outdir / ("w%d.wtns" % i)).read_bytes()
+        rc, ref = oracle.register_witness(prm, I.pack_register_inputs(p))
+        assert rc == 0 and f[:76] == data[:76] and f[76:] == ref.tobytes(), i

@@ -62,15 +62,29 @@ def traffic_json(prefix, batch, out_path, workload=None):
     # every batch launches k_load_values exactly once
     n_batches = len({r["Dispatch_Id"] for r in csv.DictReader(open(prefix + "_wr/run_counter_collection.csv"))
                      if "k_load_values" in r["Kernel_Name"]})
+    # the instruction-mix pass (SQ_INSTS_VALU: wave-level VALU instructions) for the VALU roofline
+    sq_path = prefix + "_sq/run_counter_collection.csv"
+    sq, n_sq = {}, 0
+    if os.path.exists(sq_path):
+        sq = sums(sq_path)
+        n_sq = len({r["Dispatch_Id"] for r in csv.DictReader(open(sq_path)) if "k_load_values" in r["Kernel_Name"]})
     res = {}
-    for k in sorted(set(rd) | set(wr)):
+    valu_total = 0.0
+    for k in sorted(set(rd) | set(wr) | set(sq)):
         if not k.startswith("k_"):
             continue
         f = 2 * rd.get(k, {}).get("FETCH_SIZE", 0) * 1024 / n_batches
         w = wr.get(k, {}).get("WRITE_SIZE", 0) * 1024 / n_batches
         res[k] = {"fetch_bytes_per_witness": round(f / batch), "write_bytes_per_witness": round(w / batch),
                   "traffic_bytes_per_witness": round((f + w) / batch)}
-    json.dump({"source": prefix, "batch": batch, "workload": workload, "kernels": res}, open(out_path, "w"), indent=1)
+        if n_sq:
+            v = sq.get(k, {}).get("SQ_INSTS_VALU", 0) / n_sq / batch
+            res[k]["valu_insts_per_witness"] = round(v, 1)
+            valu_total += v
+    out = {"source": prefix, "batch": batch, "workload": workload, "kernels": res}
+    if n_sq:
+        out["valu_insts_per_witness"] = round(valu_total, 1)
+    json.dump(out, open(out_path, "w"), indent=1)
 
 
 if __name__ == "__main__":

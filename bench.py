@@ -35,23 +35,34 @@ def log(*a):
 
 
 # ----------------------------------------------------------------------------- inputs
+def smt_depth_of(spec, i):
+    """SMT proof depth of passport i: spec "0" (the default: a one-leaf registration tree, every level below the
+    insertion level hashes Poseidon(0, 0)) or "A-B" (uniform over A..B by a hash of i, e.g. 20-30 for a tree of
+    about a million identities, 40-79 for config 4's deep proofs)."""
+    if "-" not in str(spec):
+        return int(spec)
+    a, b = (int(x) for x in str(spec).split("-"))
+    return a + ((i * 0x9E3779B1) >> 7) % (b - a + 1)
+
+
 def _gen_slice(args):
-    seed, lo, hi, n_keys, sig = args
+    seed, lo, hi, n_keys, sig = args[:5]
+    depth = args[5] if len(args) > 5 else "0"
     from pzkwit import inputs as I
     g = I.PassportGen.shared(seed, n_keys, sig)
     out = np.zeros((hi - lo, g.n_inputs, 32), dtype=np.uint8)
     for k, i in enumerate(range(lo, hi)):
-        I.pack_register_inputs(g.passport_at(i), g.params, out=out[k])
+        I.pack_register_inputs(g.passport_at(i, smt_depth=smt_depth_of(depth, i)), g.params, out=out[k])
     return lo, out
 
 
-def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1):
+def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1, smt_depth="0"):
     """Passports first .. first + batch - 1 of the synthetic stream, packed."""
     from pzkwit import inputs as I
     workers = workers or max(1, min(16, os.cpu_count() or 1))
     keys = I.PassportGen.shared(seed, n_keys, sig).keys  # keys generated once (parallel inside), handed to workers
     step = (batch + workers * 4 - 1) // (workers * 4)
-    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig) for lo in range(0, batch, step)]
+    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig, smt_depth) for lo in range(0, batch, step)]
     n_in = I.PassportGen.shared(seed, n_keys, sig).n_inputs
     buf = np.zeros((batch, n_in, 32), dtype=np.uint8)
     if workers == 1:
@@ -250,7 +261,7 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
         workers = max(1, min(CPU_SHARE * world, os.cpu_count() or 1))
         if register:
             host = make_register_inputs(batch * world, 0, seed=SIG_SEED[args.sig_eff], sig=args.sig_eff,
-                                        workers=workers)
+                                        workers=workers, smt_depth=getattr(args, "smt_depth", "0"))
         elif args.workload.startswith("query"):
             from pzkwit import query as Q
             host = Q.batch_rows(batch * world, seed=0x9, distinct=64, td1=args.workload == "query-td1")
@@ -337,6 +348,8 @@ def main():
     ap.add_argument("--slots", type=int, default=1, help="output slots (ring) per GPU")
     ap.add_argument("--sym", default=None, help="signal -> witness map: a circom .sym file, o1shape / o2shape (the "
                     "committed circom-shaped maps), or synthetic[:N]")
+    ap.add_argument("--smt-depth", default="0", help="register workloads: SMT proof depth of the synthetic "
+                    "passports, N or A-B (uniform); default 0 (a one-leaf registration tree)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
@@ -449,6 +462,7 @@ def report(args, r, world):
                              "ring of output slots that the next sub-batches overwrite (a 4096 batch of 72 MB "
                              "witnesses exceeds one GPU's HBM); host delivery is not in the timed region",
                    "witness_elements": W, "witness_bytes": 32 * W, "layout": r["engine"].layout,
+                   "smt_depth": getattr(args, "smt_depth", "0") if args.workload.startswith("register") else None,
                    "parallelism": "shard%d" % world, "invalid_lanes": r["bad"], "gathered": r["gathered"]},
         "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

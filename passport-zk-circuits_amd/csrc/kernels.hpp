@@ -61,6 +61,9 @@ hipError_t launch_emit_ect(const DevLayout& L, const Work* work, uint32_t n_work
                            hipStream_t st);
 hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K, const Bufs& B,
                            uint32_t batch, int t, hipStream_t st);
+// the zero-input Poseidon images and hashes of t = 2..6 (poseidon.hpp pos_zimg_off), once per instance;
+// scratch: 2 + 512 Fr of device memory; sequential launches on st
+hipError_t launch_pos_zero_img(const PosConsts& K, fr* scratch, fr* zimg, hipStream_t st);
 hipError_t launch_emit_mm(const DevLayout& L, const Work* work, uint32_t n_work, const Bufs& B, uint32_t batch,
                           hipStream_t st);
 hipError_t launch_emit(int emitter, const DevLayout& L, const Work* work, uint32_t n_work, const PosConsts& K,

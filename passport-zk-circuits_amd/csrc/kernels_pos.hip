@@ -35,6 +35,10 @@ __global__ void __launch_bounds__(256) k_pos_core(PosConsts K, const PosTask* ta
     int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
     if (task.smt_level < jl) return;  // whole group: same witness
   }
+  if (pos_inputs_zero(task, vs, w)) {  // whole group: the constant zero-input hash (k_pos_core1)
+    if (j == 0) vs.at(task.out_slot, w) = K.Zhash(T);
+    return;
+  }
   pos_core_group<T, G>(K, task, vs, w, pos_core + (size_t)w * core_elems, j);
 }
 

@@ -27,6 +27,11 @@ __global__ void __launch_bounds__(64) k_pos_core1(PosConsts K, const PosTask* ta
     int jl = (int)reinterpret_cast<const uint32_t*>(smt_core + (size_t)w * smt_core_fr + 3 * SMT_LEVELS)[0];
     if (task.smt_level < jl) return;
   }
+  // zero inputs: the hash is the constant one, and the emitter copies the constant image instead of reading a core
+  if (pos_inputs_zero(task, vs, w)) {
+    vs.at(task.out_slot, w) = K.Zhash(T);
+    return;
+  }
   const PosLineSink out{pos_core + (size_t)w * core_elems + task.core_off, lines + threadIdx.x};
   pos_core_lane<T>(K, task, vs, w, out);
 }

@@ -49,7 +49,15 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   for (uint32_t w = w0; w < w1; w++) {
     if (w != w0) __syncthreads();  // every lane has read the previous witness's image
     PZK_POS_CLK(t0);
-    pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+    if (pos_inputs_zero(task, vs, w)) {
+      // zero inputs (the SMT levels below the insertion level): the constant image (no core was written for it)
+      const uint4* z = reinterpret_cast<const uint4*>(K.Zimg(T));
+      uint4* d = reinterpret_cast<uint4*>(img);
+      for (uint32_t i = threadIdx.x; i < 2u * I.size; i += blockDim.x) d[i] = z[i];
+      __syncthreads();
+    } else {
+      pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+    }
     PZK_POS_ACC(0, t0);
     PZK_POS_CLK(t1);
     // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
@@ -60,6 +68,40 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
       store_half<MAP_O0>(out, h, im[2u * prog[h >> 1] + (h & 1)], true);
     PZK_POS_ACC(1, t1);
   }
+}
+
+// The zero-input block of width T (setup, once per instance): the permutation of zeros on one lane, then its image.
+// scratch: 2 + 512 Fr (a one-witness value store: slot 0 = every input, slot 1 = the hash; the core's states)
+template <int T>
+__global__ void __launch_bounds__(256) k_pos_zero_img(PosConsts K, fr* scratch, fr* zimg) {
+  constexpr PosImg I(T);
+  __shared__ fr img[I.size];
+  __shared__ fr lines[4 * 64];
+  PosTask task{};
+  task.n = T - 1;
+  task.out_slot = 1;
+  task.smt_level = -1;
+  const ValueStore vs{scratch, 1};
+  fr* core = scratch + 4;  // 128-byte aligned (PosLineSink writes whole lines)
+  if (threadIdx.x == 0) {
+    scratch[0] = fr_zero();
+    pos_core_lane<T>(K, task, vs, 0, PosLineSink{core, lines});
+  }
+  __threadfence();
+  __syncthreads();
+  pos_img_fill<T>(img, K, core, vs, task, 0);
+  fr* out = zimg + pos_zimg_off(T);
+  for (int i = threadIdx.x; i < I.size; i += blockDim.x) out[i] = img[i];
+  if (threadIdx.x == 0) out[I.size] = vs.at(1, 0);
+}
+
+hipError_t launch_pos_zero_img(const PosConsts& K, fr* scratch, fr* zimg, hipStream_t st) {
+  hipLaunchKernelGGL(k_pos_zero_img<2>, dim3(1), dim3(256), 0, st, K, scratch, zimg);
+  hipLaunchKernelGGL(k_pos_zero_img<3>, dim3(1), dim3(256), 0, st, K, scratch, zimg);
+  hipLaunchKernelGGL(k_pos_zero_img<4>, dim3(1), dim3(256), 0, st, K, scratch, zimg);
+  hipLaunchKernelGGL(k_pos_zero_img<5>, dim3(1), dim3(256), 0, st, K, scratch, zimg);
+  hipLaunchKernelGGL(k_pos_zero_img<6>, dim3(1), dim3(256), 0, st, K, scratch, zimg);
+  return hipGetLastError();
 }
 
 // witnesses per workgroup (A/B: PZK_POS_WPB, default 1)

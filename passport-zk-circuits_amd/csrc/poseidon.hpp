@@ -16,11 +16,24 @@
 
 namespace pzk {
 
+// PoseidonHash(n) of all-zero inputs is one constant block per width (the SMT levels below a proof's insertion
+// level hash Switcher(0, 0), merkleTree/SMTVerifier.circom:104-106): per t, its image in pos_img_fill's layout
+// (normal form) followed by the hash (Montgomery), computed once per instance (k_pos_zero_img)
+__host__ __device__ constexpr uint32_t pos_zimg_off(int t) {
+  uint32_t o = 0;
+  for (int u = 2; u < t; u++) o += (uint32_t)PosImg(u).size + 1;
+  return o;
+}
+constexpr uint32_t POS_ZIMG_TOTAL = pos_zimg_off(POS_MAX_T + 1);
+
 struct PosConsts {
   const fr* base;   // Montgomery-form constants
   const fr* nbase;  // the same constants in normal form
   PosParamIndex ix;
   const fr* sbase;  // partial-round products S[i] * C[5t + r] (Montgomery) at S's indices (k_pos_sc, runtime.cpp)
+  const fr* zimg;   // zero-input images and hashes (pos_zimg_off)
+  __device__ __forceinline__ const fr* Zimg(int t) const { return zimg + pos_zimg_off(t); }
+  __device__ __forceinline__ const fr& Zhash(int t) const { return zimg[pos_zimg_off(t) + PosImg(t).size]; }
   __device__ __forceinline__ const fr& SC(int t, int i) const { return sbase[ix.s_off[t] + i]; }
   __device__ __forceinline__ const fr& Cn(int t, int i) const { return nbase[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& C(int t, int i) const { return base[ix.c_off[t] + i]; }
@@ -38,6 +51,17 @@ struct ValueStore {
   uint32_t batch;
   __device__ __forceinline__ fr& at(int slot, uint32_t w) const { return v[(size_t)slot * batch + w]; }
 };
+
+// every input of the task is 0 (Montgomery 0 = 0): the permutation is the constant zero-input one (PosConsts.Zimg)
+__device__ __forceinline__ bool pos_inputs_zero(const PosTask& task, const ValueStore& vs, uint32_t w) {
+  uint32_t acc = 0;
+  for (int k = 0; k < task.n; k++) {
+    const fr& v = vs.at(task.in_slot[k], w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v.v[i];
+  }
+  return acc == 0;
+}
 
 // Round-state sink of pos_core_lane. Each lane's core slice starts on a 128-byte line (the builder aligns
 // task.core_off and the per-witness core to 4 Fr); element k is parked in the lane's 4-element line in LDS

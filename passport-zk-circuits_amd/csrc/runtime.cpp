@@ -158,6 +158,10 @@ struct pzk_instance {
   fr* d_inv_small = nullptr;
   PosParamIndex pix{};
   int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
+  fr* d_pos_zimg = nullptr;  // zero-input Poseidon images + hashes (poseidon.hpp pos_zimg_off)
+  PosConsts pos_consts() const {
+    return PosConsts{d_pos_consts, d_pos_consts + pos_consts_n, pix, d_pos_consts + 2 * pos_consts_n, d_pos_zimg};
+  }
   // per-batch scratch, grown on demand; two sets, alternating per call, so that call k + 1's
   // cores can run while call k's emitters still read set k % 2
   Scratch scr[NSETS];
@@ -167,7 +171,7 @@ struct pzk_instance {
   hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
   hipStream_t s_tail = nullptr;  // the small tail emitters (PZK_TAIL=own), so the next call's SHA emitter never queues behind them
-  hipEvent_t ev_pos = nullptr, ev_tab = nullptr;
+  hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
   // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
   // --O0 witness of a chunk into d_o0[slot]; k_wtns_gather compacts it into the caller's rows
@@ -305,7 +309,13 @@ static int load_poseidon(pzk_instance* I) {
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_pos_sc, dim3(POS_MAX_T - 1), dim3(64), 0, 0, I->d_pos_consts, I->d_pos_consts + 2 * n, I->pix);
   HIPCHK(hipGetLastError());
+  // the zero-input blocks (every PoseidonHash of zeros, e.g. the SMT levels below a proof's insertion level)
+  fr* scratch = nullptr;
+  HIPCHK(hipMalloc(&I->d_pos_zimg, sizeof(fr) * POS_ZIMG_TOTAL));
+  HIPCHK(hipMalloc(&scratch, sizeof(fr) * (4 + 512)));
+  HIPCHK(launch_pos_zero_img(I->pos_consts(), scratch, I->d_pos_zimg, nullptr));
   HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipFree(scratch));
   return 0;
 }
 
@@ -338,14 +348,15 @@ static void free_all(pzk_instance* I) {
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
                   I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small, I->d_map,
-                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank, I->d_mprog};
+                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank, I->d_mprog, I->d_pos_zimg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
   for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail})
     if (s) (void)hipStreamDestroy(s);
-  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab})
+  for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab,
+                       I->ev_smt, I->ev_chain})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : I->ev_done)
     for (hipEvent_t e : set)
@@ -456,7 +467,8 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess;
-  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab})
+  for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
+                        &I->ev_smt, &I->ev_chain})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t& e : I->ev_gather) {
     ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -748,7 +760,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   const Layout& lay = I->lay;
   DevLayout L = I->dev_layout();
   ValueStore vs{S.d_values, B};
-  PosConsts K{I->d_pos_consts, I->d_pos_consts + I->pos_consts_n, I->pix, I->d_pos_consts + 2 * I->pos_consts_n};
+  const PosConsts K = I->pos_consts();
   Bufs bufs{d_inputs, S.d_sha_core, S.d_rsa_core, S.d_pos_core, S.d_bjj_core, S.d_smt_core, vs, d_wtns, stride,
             d_status, S.d_ec_core, S.d_ec_inv, S.d_ec_tab, I->d_inv_small, S.d_derived};
   Timing* T = nullptr;
@@ -891,9 +903,27 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st));
       HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(2, 3, S.d_smt_order))) return rc; }
-    { PhaseScope ps(T, slot, PH_SMT, st);
+    // The SMT chain (one dependent Poseidon permutation per proof level above the insertion level: ~0.5-1 ms per
+    // level per call, so 25+ ms for the proof depths of a real registration tree) runs on its own stream (the fifth,
+    // otherwise idle in register calls), so the next call's SHA core / prep / Poseidon / BabyJubJub chain does not
+    // queue behind it; only the emitters that read its output (the SMT level images, the small SMT regions) wait.
+    static const char* tail_env = getenv("PZK_TAIL");
+    static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0
+                                 : !strcmp(tail_env, "rsa") ? 3 : !strcmp(tail_env, "own") ? 4 : 2;
+    // PZK_SMT (A/B): main = the chain on the main stream (rounds 1-3); own = on the fifth stream, the tail emitters
+    // placed by PZK_TAIL; tail (default) = on the fifth stream with the tail emitters behind it there, so the SHA
+    // emitter stream never waits for a long chain
+    static const char* smt_env = getenv("PZK_SMT");
+    static const int smt_mode = !smt_env ? 2 : !strcmp(smt_env, "main") ? 0 : !strcmp(smt_env, "own") ? 1 : 2;
+    hipStream_t s_smt = (serial || tail_mode == 4 || smt_mode == 0) ? st : I->s_tail;
+    if (s_smt != st) {
+      HIPCHK(hipEventRecord(I->ev_smt, st));
+      HIPCHK(hipStreamWaitEvent(s_smt, I->ev_smt, 0));
+    }
+    { PhaseScope ps(T, slot, PH_SMT, s_smt);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              st)); }
+                              s_smt)); }
+    HIPCHK(hipEventRecord(I->ev_chain, s_smt));
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
     HIPCHK(hipEventRecord(I->ev_bjj, st));
@@ -903,17 +933,17 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // behind the signature emitters and the small regions / flow / checks behind the SHA emitters
     // (default, "split": 70.7k vs 68.3k / 69.0k witnesses/s for all-on-sha / all-on-emit; "rsa", the tail on
     // the RSA stream, equals split; tuning switch PZK_TAIL=sha|emit|split|rsa, profiles/README.md)
-    static const char* tail_env = getenv("PZK_TAIL");
-    static const int tail_mode = !tail_env ? 2 : !strcmp(tail_env, "emit") ? 1 : !strcmp(tail_env, "sha") ? 0
-                                 : !strcmp(tail_env, "rsa") ? 3 : !strcmp(tail_env, "own") ? 4 : 2;
     hipStream_t s_tail = tail_mode == 1 ? s_emit : tail_mode == 3 ? s_rsa : tail_mode == 4 ? s_own : s_sha,
                 s_pos = tail_mode == 0 ? s_sha : s_emit, s_bjj = tail_mode == 4 ? s_own : s_sha;
+    if (s_smt != st && smt_mode == 2) s_tail = s_smt;
     HIPCHK(hipStreamWaitEvent(s_bjj, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_bjj))) return rc;
     HIPCHK(hipStreamWaitEvent(s_pos, I->ev_pos, 0));
+    if (s_smt != st && s_pos != s_smt) HIPCHK(hipStreamWaitEvent(s_pos, I->ev_chain, 0));  // SMT level images
     if ((rc = emit(E_POS, s_pos))) return rc;
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_pos, 0));
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_rsa, 0));
+    if (s_smt != st && s_tail != s_smt) HIPCHK(hipStreamWaitEvent(s_tail, I->ev_chain, 0));  // SMT regions, status
     if ((rc = emit(E_GEN, s_tail))) return rc;
     if ((rc = emit(E_FLOW, s_tail))) return rc;
     if (!lay.is_ecdsa) {

@@ -45,25 +45,40 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = (uint16_t)dr0.prog[i];
   else
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
+  __syncthreads();
+  const uint32_t tot = 2 * cnt;
   const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
   for (uint32_t w = w0; w < w1; w++) {
-    if (w != w0) __syncthreads();  // every lane has read the previous witness's image
-    PZK_POS_CLK(t0);
     if (pos_inputs_zero(task, vs, w)) {
-      // zero inputs (the SMT levels below the insertion level): the constant image (no core was written for it)
+      // zero inputs (the SMT levels below the insertion level): the block is the constant zero-input one; its
+      // elements are gathered straight from the image in global memory (L2-resident, 5 widths x <= 41 KB), U
+      // halves per lane loaded ahead of their stores (no core was written for this witness)
+      constexpr int U = 8;
       const uint4* z = reinterpret_cast<const uint4*>(K.Zimg(T));
-      uint4* d = reinterpret_cast<uint4*>(img);
-      for (uint32_t i = threadIdx.x; i < 2u * I.size; i += blockDim.x) d[i] = z[i];
-      __syncthreads();
-    } else {
-      pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+      uint4* dst = reinterpret_cast<uint4*>(wtns + (size_t)w * stride) + 2 * dr0.out.g;
+      for (uint32_t h0 = threadIdx.x; h0 < tot; h0 += U * blockDim.x) {
+        uint4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+          const uint32_t h = h0 + k * blockDim.x;
+          v[k] = h < tot ? z[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+          const uint32_t h = h0 + k * blockDim.x;
+          if (h < tot) dst[h] = v[k];
+        }
+      }
+      continue;
     }
+    __syncthreads();  // every lane has read the previous witness's image
+    PZK_POS_CLK(t0);
+    pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
     PZK_POS_ACC(0, t0);
     PZK_POS_CLK(t1);
     // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
     const OutRow out{wtns + (size_t)w * stride, dr0.out.g, KeepMap{nullptr, nullptr}};
     const uint4* im = reinterpret_cast<const uint4*>(img);
-    const uint32_t tot = 2 * cnt;
     for (uint32_t h = threadIdx.x; h < tot; h += blockDim.x)
       store_half<MAP_O0>(out, h, im[2u * prog[h >> 1] + (h & 1)], true);
     PZK_POS_ACC(1, t1);

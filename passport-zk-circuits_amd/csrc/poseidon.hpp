@@ -135,6 +135,32 @@ __device__ __forceinline__ void pos_core_lane(const PosConsts& K, const PosTask&
   vs.at(task.out_slot, w) = h;
 }
 
+// The constants of one width T staged in LDS, with PosConsts' accessors (t fixed): k_smt_chain reads them every
+// round of every level, and from LDS those reads never wait for the round-state stores in flight (a global load
+// issued after a store waits for it: gfx9 vmcnt counts both).
+template <int T>
+struct PosConstsLds {
+  static constexpr int RP = pos_rp(T), NC = RP + 8 * T, NM = T * T, NS = (2 * T - 1) * RP;
+  static constexpr int SIZE = NC + 2 * NM + 2 * NS;  // C | M | P | S | S * C
+  const fr* c;
+  __device__ __forceinline__ const fr& C(int, int i) const { return c[i]; }
+  __device__ __forceinline__ const fr& M(int, int i, int j) const { return c[NC + i * T + j]; }
+  __device__ __forceinline__ const fr& Pm(int, int i, int j) const { return c[NC + NM + i * T + j]; }
+  __device__ __forceinline__ const fr& S(int, int i) const { return c[NC + 2 * NM + i]; }
+  __device__ __forceinline__ const fr& SC(int, int i) const { return c[NC + 2 * NM + NS + i]; }
+  // every thread of the workgroup; the caller syncs before use
+  __device__ static void stage(fr* lds, const PosConsts& K) {
+    for (int i = threadIdx.x; i < SIZE; i += blockDim.x) {
+      const fr* src = i < NC ? K.base + K.ix.c_off[T] + i
+                    : i < NC + NM ? K.base + K.ix.m_off[T] + (i - NC)
+                    : i < NC + 2 * NM ? K.base + K.ix.p_off[T] + (i - NC - NM)
+                    : i < NC + 2 * NM + NS ? K.base + K.ix.s_off[T] + (i - NC - 2 * NM)
+                                           : K.sbase + K.ix.s_off[T] + (i - NC - 2 * NM - NS);
+      lds[i] = *src;
+    }
+  }
+};
+
 // Cooperative permutation: G lanes per (witness, task), lane j < t holds state element j; returns
 // the hash to every lane of the group
 // (G = 4 for t <= 4, 8 otherwise; the lanes j >= t carry zeros). A full round is one S-box per
@@ -143,17 +169,16 @@ __device__ __forceinline__ void pos_core_lane(const PosConsts& K, const PosTask&
 // X0..X3, Y0..Y_RP, Z1..Z3), written by the owning lanes. ~3.5x shorter dependency chain than
 // one lane per permutation and ~70 VGPRs instead of 256, so the kernel can be placed next to
 // the emitters.
-template <int T, int G>
-__device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
-                                               fr* core /* this witness's Poseidon core */, int j) {
+// The cooperative permutation itself: lane j < t enters with its input (lane 0: 0), the round states go to out
+// (this task's core slice), every lane of the group gets the hash (Montgomery).
+template <int T, int G, class KC>
+__device__ __forceinline__ fr pos_perm_group(const KC& K, fr st, fr* out, int j) {
   constexpr int t = T;
   const int RP = pos_nrp(t);
   const bool act = j < t;
   const int jj = act ? j : 0;
-  fr* out = core + task.core_off;
-  fr st = fr_zero();
-  if (act && j > 0) st = vs.at(task.in_slot[j - 1], w);
   if (act) st = fr_add(st, K.C(t, j));
+  else st = fr_zero();
   const int lane = threadIdx.x & 63, gb = lane & ~(G - 1);
   auto mix = [&](const fr& x, bool use_p) -> fr {  // sum_k Mat[k][j] * x_k
     fr acc = fr_zero();
@@ -220,7 +245,15 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
     st = mix(a, false);
   }
   if (act) out[o + j] = st;  // Z3
-  fr h = group_sum(act ? fr_mul(K.M(t, jj, 0), pow5(st)) : fr_zero());
+  return group_sum(act ? fr_mul(K.M(t, jj, 0), pow5(st)) : fr_zero());  // every lane of the group: the hash
+}
+
+template <int T, int G>
+__device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
+                                               fr* core /* this witness's Poseidon core */, int j) {
+  fr in = fr_zero();
+  if (j > 0 && j < T) in = vs.at(task.in_slot[j - 1], w);
+  const fr h = pos_perm_group<T, G>(K, in, core + task.core_off, j);
   if (j == 0) vs.at(task.out_slot, w) = h;
   return h;  // every lane of the group holds the hash (Montgomery)
 }

@@ -698,37 +698,58 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 #endif
 
 // sequential part: levels j-1 .. 0, then all roots and the isEqual inverse. SMT_CHAIN_LANES lanes per
-// witness run each level hash as a cooperative permutation (pos_core_group: lane k < 3 holds state
-// element k); every lane writes the level's two hash inputs itself, so the permutation's input loads
-// read the lane's own stores, and the hash comes back to every lane of the group by its butterfly.
+// witness run each level hash as a cooperative permutation (pos_perm_group: lane k < 3 holds state
+// element k) whose hash comes back to every lane of the group by its butterfly. Everything the level loop
+// reads is staged in LDS first — the width-3 constants, the group's siblings (Montgomery) and left/right bits,
+// the level tasks' core offsets — so the loop issues no global load: a global load issued after the round-state
+// stores would wait for them (gfx9 vmcnt counts both), one store latency per round of every level.
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
                                                  ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order,
                                                  int32_t* status, uint32_t batch) {
   core_priority();
-  constexpr int G = SMT_CHAIN_LANES;
+  constexpr int G = SMT_CHAIN_LANES, NG = 64 / G;
   static_assert(G == 4 && 64 % G == 0, "PoseidonHash(2) groups are 4 lanes (t = 3)");
+  using KL = PosConstsLds<3>;
+  __shared__ fr kc[KL::SIZE];
+  __shared__ fr sibs[NG][SMT_LEVELS];
+  __shared__ uint8_t lrs[NG][SMT_LEVELS];
+  __shared__ int32_t lv_core[SMT_LEVELS];
+  KL::stage(kc, K);
+  for (int i = threadIdx.x; i < SMT_LEVELS; i += blockDim.x) lv_core[i] = L.pos[level_task[i]].core_off;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = tid / G;
-  const int jl = (int)(tid % G);
-  if (g >= batch) return;  // whole lane groups only
-  const uint32_t w = order ? order[g] : g;  // k_smt_order: lane groups by proof depth, deepest first
+  const int jl = (int)(tid % G), gi = (int)(threadIdx.x / G);
+  const bool live = g < batch;  // whole lane groups only; every thread takes part in the barrier
+  const uint32_t w = live ? (order ? order[g] : g) : 0;  // k_smt_order: lane groups by proof depth, deepest first
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;
   const uint32_t* flags = reinterpret_cast<const uint32_t*>(core + 2 * SMT_LEVELS);
-  const int j = (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0];
+  const int j = live ? (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0] : 0;
+  const int top = j < SMT_LEVELS ? j : SMT_LEVELS;
+  for (int i = jl; i < top; i += G) {
+    sibs[gi][i] = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
+    lrs[gi][i] = (uint8_t)((flags[i] >> 4) & 1);
+  }
+  __syncthreads();
+  if (!live) return;
+  const KL Kl{kc};
   const fr leaf = vs.at(R.v_leaf, w);
   fr child = leaf;  // root_j = leaf
   fr* pcore = pos_core + (size_t)w * L.pos_core_elems;
-  for (int i = (j < SMT_LEVELS ? j : SMT_LEVELS) - 1; i >= 0; i--) {
-    const fr sib = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
-    const int lr = (flags[i] >> 4) & 1;
-    vs.at(R.v_smt_lr + 2 * i, w) = lr ? sib : child;
-    vs.at(R.v_smt_lr + 2 * i + 1, w) = lr ? child : sib;
-    child = pos_core_group<3, G>(K, L.pos[level_task[i]], vs, w, pcore, jl);  // root_i = H_i (st_top = 1 below j)
+  for (int i = top - 1; i >= 0; i--) {
+    const fr sib = sibs[gi][i];
+    const bool lr = lrs[gi][i] != 0;
+    const fr lv = lr ? sib : child, rv = lr ? child : sib;  // Switcher (SMTVerifier.circom): the level's L / R
+    if (jl == 0) {
+      vs.at(R.v_smt_lr + 2 * i, w) = lv;
+      vs.at(R.v_smt_lr + 2 * i + 1, w) = rv;
+    }
+    child = pos_perm_group<3, G>(Kl, jl == 1 ? lv : jl == 2 ? rv : fr_zero(), pcore + lv_core[i], jl);
+    if (jl == 0) vs.at(R.v_smt_h + i, w) = child;  // root_i = H_i (st_top = 1 below j)
   }
-  if (jl != 0) return;  // lane 0 wrote every level hash this kernel made (pos_core_group's out_slot store)
+  if (jl != 0) return;  // lane 0 wrote every level hash this kernel made
   // roots of every level: root_i = st_top_i * H_i + st_inew_i * leaf (SMTVerifier.circom:104-106)
   fr* roots = core + SMT_LEVELS;
   for (int i = 0; i < SMT_LEVELS; i++) {

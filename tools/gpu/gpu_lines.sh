@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU: optional parity tests, then bench lines.
-# usage: TESTS="<pytest -k expr>|all|none" SMOKE=1 tools/gpu/gpu_lines.sh TAG "name:bench args" ["name:bench args" ...]
+# usage: TESTS="<pytest -k expr>|all|none" SMOKE=1 tools/gpu/gpu_lines.sh TAG "name:[VAR=v ...|]bench args" ...
+# (a spec may start with environment assignments for that line, separated from the bench args by '|')
 # Each line runs `python bench.py <args>` under its own timeout into gpurun_out/TAG/bench_<name>.json and prints
 # value / job HBM / per-phase ms; the script stops at the first failure.
 set -o pipefail
@@ -23,9 +24,10 @@ if [ -n "$SMOKE" ]; then
   tail -1 $O/smoke.log
 fi
 for spec in "$@"; do
-  name=${spec%%:*}; args=${spec#*:}
+  name=${spec%%:*}; args=${spec#*:}; envs=""
+  if [[ "$args" == *"|"* ]]; then envs=${args%%|*}; args=${args#*|}; fi
   f=$O/bench_$name.json
-  timeout -k 10 600 python -u bench.py $args > $f 2> $O/bench_$name.err || { tail -20 $O/bench_$name.err; exit 1; }
+  env $envs timeout -k 10 600 python -u bench.py $args > $f 2> $O/bench_$name.err || { tail -20 $O/bench_$name.err; exit 1; }
   python3 - "$f" "$name" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))

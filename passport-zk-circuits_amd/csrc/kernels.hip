@@ -2,6 +2,7 @@
 // here; the host runtime in runtime.cpp launches them through the launch_* wrappers).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "poseidon.hpp"
 #include "regcore.hpp"
@@ -380,8 +381,9 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
                             hipStream_t st) {
-  hipLaunchKernelGGL(k_smt_chain, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64), dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core,
-                     smt_core, order, status, vs.batch);
+  static const bool call = getenv("PZK_CHAIN_MUL") && !strcmp(getenv("PZK_CHAIN_MUL"), "call");
+  hipLaunchKernelGGL(call ? k_smt_chain<FrMulCall> : k_smt_chain<FrMulInline>, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
+                     dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core, smt_core, order, status, vs.batch);
   return hipGetLastError();
 }
 

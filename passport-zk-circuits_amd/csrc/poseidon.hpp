@@ -169,9 +169,25 @@ struct PosConstsLds {
 // X0..X3, Y0..Y_RP, Z1..Z3), written by the owning lanes. ~3.5x shorter dependency chain than
 // one lane per permutation and ~70 VGPRs instead of 256, so the kernel can be placed next to
 // the emitters.
+// Product policies of the cooperative permutation: inline (the Poseidon cores) or out of line (k_smt_chain: one
+// copy of each product in the level loop, whose code then stays in the instruction cache it shares with the
+// emitter kernels on the same CUs)
+struct FrMulInline {
+  __device__ static __forceinline__ fr mul(const fr& a, const fr& b) { return fr_mul(a, b); }
+  __device__ static __forceinline__ fr sqr(const fr& a) { return fr_sqr(a); }
+};
+__device__ __attribute__((noinline)) static fr fr_mul_ool(fr a, fr b) { return fr_mul(a, b); }
+__device__ __attribute__((noinline)) static fr fr_sqr_ool(fr a) { return fr_sqr(a); }
+struct FrMulCall {
+  __device__ static __forceinline__ fr mul(const fr& a, const fr& b) { return fr_mul_ool(a, b); }
+  __device__ static __forceinline__ fr sqr(const fr& a) { return fr_sqr_ool(a); }
+};
+template <class PM>
+__device__ __forceinline__ fr pow5p(const fr& x) { fr x2 = PM::sqr(x), x4 = PM::sqr(x2); return PM::mul(x4, x); }
+
 // The cooperative permutation itself: lane j < t enters with its input (lane 0: 0), the round states go to out
 // (this task's core slice), every lane of the group gets the hash (Montgomery).
-template <int T, int G, class KC>
+template <int T, int G, class KC, class PM = FrMulInline>
 __device__ __forceinline__ fr pos_perm_group(const KC& K, fr st, fr* out, int j) {
   constexpr int t = T;
   const int RP = pos_nrp(t);
@@ -185,7 +201,7 @@ __device__ __forceinline__ fr pos_perm_group(const KC& K, fr st, fr* out, int j)
 #pragma unroll
     for (int k = 0; k < t; k++) {
       fr xk = fr_shfl(x, gb + k, 64);
-      acc = fr_add(acc, fr_mul(use_p ? K.Pm(t, k, jj) : K.M(t, k, jj), xk));
+      acc = fr_add(acc, PM::mul(use_p ? K.Pm(t, k, jj) : K.M(t, k, jj), xk));
     }
     return act ? acc : fr_zero();
   };
@@ -199,53 +215,55 @@ __device__ __forceinline__ fr pos_perm_group(const KC& K, fr st, fr* out, int j)
     }
     return v;
   };
+  // One loop over the 7 full rounds with the partial rounds in front of full round 4, none unrolled: each round
+  // body exists once in the code (two full-round copies made k_smt_chain's level loop ~9,000 instructions, more
+  // than the instruction cache holds beside the emitters' code).
   int o = 0;
-  for (int r = 0; r < 4; r++) {  // full rounds 0..3 (round 3 mixes with P)
-    if (act) out[o + j] = st;
-    o += t;
-    fr a = act ? fr_add(pow5(st), K.C(t, (r + 1) * t + jj)) : fr_zero();
-    st = mix(a, r == 3);
-  }
-  for (int r = 0; r < RP; r++) {  // partial rounds
-    if (act) out[o + j] = st;
-    o += t;
-    const int sb = (2 * t - 1) * r;
-    if constexpr (G > T) {
-      // 3 product times per round, with the group's spare lane t: s0 = x^5 + C with x = st_0, and
-      //   lane 0:   st_0' = S[0] s0 + sum_k S[k] st_k      (S[0] s0 = x^3 (S[0] x^2) + S[0] C)
-      //   lane k:   st_k' = st_k + S'[k] s0                (S'[k] s0 = x^3 (S'[k] x^2) + S'[k] C)
-      // A: lane 0 x^2, lanes k their terms S[k] st_k | B: lane 0 x^3, lanes k S'[k] x^2, lane t S[0] x^2 |
-      // C: every lane x^3 times its B product. The S * C constants come precomputed (K.SC).
-      const fr a = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
-      const fr x2 = fr_shfl(a, gb, 64);
-      const fr b = fr_mul(j == 0 ? st : act ? K.S(t, sb + t + jj - 1) : K.S(t, sb), x2);
-      const fr x3 = fr_shfl(b, gb, 64), s0x2 = fr_shfl(b, gb + t, 64);
-      const fr c = fr_mul(x3, j == 0 ? s0x2 : b);
-      const fr sum = group_sum(j == 0 ? fr_add(c, K.SC(t, sb)) : act ? a : fr_zero());
-      if (j == 0) st = sum;
-      else if (act) st = fr_add(st, fr_add(c, K.SC(t, sb + t + jj - 1)));
-    } else {
-      // 4 product times (no spare lane: t = 4 on 4 lanes): one product on every lane: lane 0 squares its state
-      // (the S-box's first step), lanes 1..t-1 take their sparse-matrix terms S[k] * st_k
-      const fr p = fr_mul(j == 0 ? st : K.S(t, sb + jj), st);
-      fr s0 = fr_zero();
-      if (j == 0) s0 = fr_add(fr_mul(fr_sqr(p), st), K.C(t, 5 * t + r));
-      s0 = fr_shfl(s0, gb, 64);
-      // one product on every lane: lane 0's term S[0] * s0, the others' updates s0 * S'[k]
-      const fr q = fr_mul(j == 0 ? K.S(t, sb) : K.S(t, sb + t + jj - 1), s0);
-      const fr sum = group_sum(j == 0 ? q : act ? p : fr_zero());
-      if (j == 0) st = sum;
-      else if (act) st = fr_add(st, q);
+#pragma unroll 1
+  for (int f = 0; f < 7; f++) {
+    if (f == 4) {
+#pragma unroll 1
+      for (int r = 0; r < RP; r++) {  // partial rounds
+        if (act) out[o + j] = st;
+        o += t;
+        const int sb = (2 * t - 1) * r;
+        if constexpr (G > T) {
+          // 3 product times per round, with the group's spare lane t: s0 = x^5 + C with x = st_0, and
+          //   lane 0:   st_0' = S[0] s0 + sum_k S[k] st_k      (S[0] s0 = x^3 (S[0] x^2) + S[0] C)
+          //   lane k:   st_k' = st_k + S'[k] s0                (S'[k] s0 = x^3 (S'[k] x^2) + S'[k] C)
+          // A: lane 0 x^2, lanes k their terms S[k] st_k | B: lane 0 x^3, lanes k S'[k] x^2, lane t S[0] x^2 |
+          // C: every lane x^3 times its B product. The S * C constants come precomputed (K.SC).
+          const fr a = PM::mul(j == 0 ? st : K.S(t, sb + jj), st);
+          const fr x2 = fr_shfl(a, gb, 64);
+          const fr b = PM::mul(j == 0 ? st : act ? K.S(t, sb + t + jj - 1) : K.S(t, sb), x2);
+          const fr x3 = fr_shfl(b, gb, 64), s0x2 = fr_shfl(b, gb + t, 64);
+          const fr c = PM::mul(x3, j == 0 ? s0x2 : b);
+          const fr sum = group_sum(j == 0 ? fr_add(c, K.SC(t, sb)) : act ? a : fr_zero());
+          if (j == 0) st = sum;
+          else if (act) st = fr_add(st, fr_add(c, K.SC(t, sb + t + jj - 1)));
+        } else {
+          // 4 product times (no spare lane: t = 4 on 4 lanes): one product on every lane: lane 0 squares its state
+          // (the S-box's first step), lanes 1..t-1 take their sparse-matrix terms S[k] * st_k
+          const fr p = PM::mul(j == 0 ? st : K.S(t, sb + jj), st);
+          fr s0 = fr_zero();
+          if (j == 0) s0 = fr_add(PM::mul(PM::sqr(p), st), K.C(t, 5 * t + r));
+          s0 = fr_shfl(s0, gb, 64);
+          // one product on every lane: lane 0's term S[0] * s0, the others' updates s0 * S'[k]
+          const fr q = PM::mul(j == 0 ? K.S(t, sb) : K.S(t, sb + t + jj - 1), s0);
+          const fr sum = group_sum(j == 0 ? q : act ? p : fr_zero());
+          if (j == 0) st = sum;
+          else if (act) st = fr_add(st, q);
+        }
+      }
     }
-  }
-  for (int r = 0; r < 3; r++) {  // full rounds 4..6
-    if (act) out[o + j] = st;
+    if (act) out[o + j] = st;  // full round f (round 3 mixes with P)
     o += t;
-    fr a = act ? fr_add(pow5(st), K.C(t, 5 * t + RP + r * t + jj)) : fr_zero();
-    st = mix(a, false);
+    const int c0 = f < 4 ? (f + 1) * t : 5 * t + RP + (f - 4) * t;
+    fr a = act ? fr_add(pow5p<PM>(st), K.C(t, c0 + jj)) : fr_zero();
+    st = mix(a, f == 3);
   }
   if (act) out[o + j] = st;  // Z3
-  return group_sum(act ? fr_mul(K.M(t, jj, 0), pow5(st)) : fr_zero());  // every lane of the group: the hash
+  return group_sum(act ? PM::mul(K.M(t, jj, 0), pow5p<PM>(st)) : fr_zero());  // every lane of the group: the hash
 }
 
 template <int T, int G>

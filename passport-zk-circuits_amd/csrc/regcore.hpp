@@ -703,7 +703,9 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 // reads is staged in LDS first — the width-3 constants, the group's siblings (Montgomery) and left/right bits,
 // the level tasks' core offsets — so the loop issues no global load: a global load issued after the round-state
 // stores would wait for them (gfx9 vmcnt counts both), one store latency per round of every level.
+// PM: the product policy (PZK_CHAIN_MUL=inline|call, A/B; poseidon.hpp FrMulInline / FrMulCall)
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
+template <class PM>
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,
                                                  ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order,
                                                  int32_t* status, uint32_t batch) {
@@ -746,7 +748,7 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
       vs.at(R.v_smt_lr + 2 * i, w) = lv;
       vs.at(R.v_smt_lr + 2 * i + 1, w) = rv;
     }
-    child = pos_perm_group<3, G>(Kl, jl == 1 ? lv : jl == 2 ? rv : fr_zero(), pcore + lv_core[i], jl);
+    child = pos_perm_group<3, G, KL, PM>(Kl, jl == 1 ? lv : jl == 2 ? rv : fr_zero(), pcore + lv_core[i], jl);
     if (jl == 0) vs.at(R.v_smt_h + i, w) = child;  // root_i = H_i (st_top = 1 below j)
   }
   if (jl != 0) return;  // lane 0 wrote every level hash this kernel made

@@ -48,8 +48,11 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   __syncthreads();
   const uint32_t tot = 2 * cnt;
   const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
+  // which of the workgroup's witnesses have zero inputs: tested before any store (wpb <= 64)
+  uint64_t zmask = 0;
+  for (uint32_t w = w0; w < w1; w++) zmask |= (uint64_t)pos_inputs_zero(task, vs, w) << (w - w0);
   for (uint32_t w = w0; w < w1; w++) {
-    if (pos_inputs_zero(task, vs, w)) {
+    if ((zmask >> (w - w0)) & 1) {
       // zero inputs (the SMT levels below the insertion level): the block is the constant zero-input one; its
       // elements are gathered straight from the image in global memory (L2-resident, 5 widths x <= 41 KB), U
       // halves per lane loaded ahead of their stores (no core was written for this witness)

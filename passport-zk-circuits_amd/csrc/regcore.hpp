@@ -354,10 +354,17 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
     const int k = e / K, i = e - k * K;
     return reinterpret_cast<uint8_t*>(core + (size_t)k * MMW + 4 * K + 1 + 4 * i);
   };
+  // the run's exclusive prefix products stay in LDS ([element of the run][lane]): parked in the core's inverse
+  // slots they cost a write and a read of 32 B per IsEqual, and each read waited for the run's stores
+  // (up to 20 multiplications: 65537, 3, 37187; a longer PowerMod schedule parks them in the slots as before)
+  constexpr int PER_MAX = (20 * K + 63) / 64;
+  __shared__ fr pre_run[PER_MAX * 64];
+  const bool in_lds = PER <= PER_MAX;  // block-uniform
   fr acc = fr_mont_one();
   for (int e = e0; e < e1; e++) {
     fr d = diff(e);
-    store_fr(slot(e), acc);  // exclusive prefix within the run
+    if (in_lds) pre_run[(e - e0) * 64 + lane] = acc;  // exclusive prefix within the run
+    else store_fr(slot(e), acc);
     if (!fr_is_zero(d)) acc = fr_mul(acc, d);
   }
   // exclusive prefix / suffix products of the run products across the wave (log-step scans)
@@ -375,7 +382,7 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
   for (int e = e1 - 1; e >= e0; e--) {
     fr d = diff(e);
     fr r = fr_zero();
-    if (!fr_is_zero(d)) { r = fr_mul(inv, load_fr(slot(e))); inv = fr_mul(inv, d); }
+    if (!fr_is_zero(d)) { r = fr_mul(inv, in_lds ? pre_run[(e - e0) * 64 + lane] : load_fr(slot(e))); inv = fr_mul(inv, d); }
     store_fr(slot(e), fr_from_mont(r));
   }
 }

@@ -181,6 +181,7 @@ struct pzk_instance {
   uint64_t* d_keep_bits = nullptr;
   uint32_t* d_keep_rank = nullptr;
   uint32_t* d_mprog = nullptr;  // the kept elements' descriptors of the descriptor-driven work items (Work.pad)
+  uint32_t ect_split = ~0u;     // ECDSA: EC table work items [0, ect_split) on the signature stream, the rest on s_sha
   // any other map: O0 chunks into staging slots, then k_wtns_gather
   uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
   std::vector<uint32_t> kept;     // mapped instances: the kept O0 indices, sorted (pzk_phase_info's bytes)
@@ -482,6 +483,17 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
     }
   if (!ok) { free_all(I); delete I; return fail(PZK_E_HIP, "hipStreamCreate/hipEventCreate failed"); }
   I->out_size = I->lay.wit_size;
+  if (I->lay.is_ecdsa) {  // PZK_ECT_SPLIT: the share of the EC table elements emitted on the SHA emitter stream
+    static const double frac = getenv("PZK_ECT_SPLIT") ? atof(getenv("PZK_ECT_SPLIT")) : 0.0;
+    const std::vector<Work>& wl = I->lay.work[E_ECT];
+    uint64_t tot = 0, acc = 0;
+    for (const Work& w : wl) tot += w.count;
+    I->ect_split = (uint32_t)wl.size();
+    for (uint32_t i = 0; i < wl.size() && frac > 0; i++) {
+      if ((double)acc >= (1.0 - frac) * (double)tot) { I->ect_split = i; break; }
+      acc += wl[i].count;
+    }
+  }
   *out = I;
   return 0;
 }
@@ -758,6 +770,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   }
   const uint32_t B = (uint32_t)batch;
   const Layout& lay = I->lay;
+  const uint32_t ect_split = I->ect_split;
   DevLayout L = I->dev_layout();
   ValueStore vs{S.d_values, B};
   const PosConsts K = I->pos_consts();
@@ -781,8 +794,15 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     return 0;
   };
-  auto emit = [&](int e, hipStream_t s) -> int {
+  // one emitter's work items [a, b) (default: all) on stream s
+  auto emit = [&](int e, hipStream_t s, uint32_t a = 0, uint32_t b = ~0u) -> int {
+    b = std::min<uint32_t>(b, (uint32_t)lay.work[e].size());
+    if (a >= b && e != E_POS) return 0;
     PhaseScope ps(lay.work[e].empty() ? nullptr : T, slot, EMIT_PHASE[e], s);
+    if (e != E_POS && (a != 0 || b != lay.work[e].size())) {
+      HIPCHK(launch_emit(e, L, I->d_work[e] + a, b - a, K, bufs, B, lay.max_t, s));
+      return 0;
+    }
     if (e == E_POS) {
       for (const auto& g : lay.pos_emit_groups)
         HIPCHK(launch_emit(e, L, I->d_work[e] + g[1], g[2], K, bufs, B, (int)g[0], s));
@@ -895,7 +915,9 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if (lay.is_ecdsa) {
       if ((rc = emit(E_ECR, s_sig))) return rc;  // the generator multiplication's selection tables (EC core only)
       HIPCHK(hipStreamWaitEvent(s_sig, I->ev_tab, 0));
-      if ((rc = emit(E_ECT, s_sig))) return rc;
+      // the EC table blocks are ~60 % of an ECDSA witness: the first part on the signature stream, the rest on the
+      // SHA emitter stream after this call's SHA emitters (PZK_ECT_SPLIT: the share of the elements there)
+      if ((rc = emit(E_ECT, s_sig, 0, ect_split))) return rc;
     }
     // main chain
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_prep(L, d_inputs, S.d_sha_core, vs, d_status, st)); }
@@ -952,6 +974,10 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     if ((rc = emit(E_BITS, s_tail))) return rc;
     if ((rc = emit(E_GENR, s_tail))) return rc;
+    if (lay.is_ecdsa && ect_split < lay.work[E_ECT].size()) {
+      HIPCHK(hipStreamWaitEvent(s_sha, I->ev_tab, 0));
+      if ((rc = emit(E_ECT, s_sha, ect_split))) return rc;
+    }
   }
   hipStream_t streams[5] = {st, s_rsa, s_sha, s_emit, s_own};
   for (int i = 0; i < 5; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));

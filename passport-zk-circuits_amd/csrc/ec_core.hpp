@@ -911,8 +911,14 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
 // workgroup size: a big table (P-224 51 KB, brainpoolP384r1 39 KB of LDS) caps the workgroups per CU at 3-4, so
 // those curves run 8 waves per workgroup to keep ~24-32 waves per CU in flight
 constexpr int ECT_NT = EC_TABLE_MAX[EC_CV] > 1024 ? 512 : 256;
+#ifndef PZK_ECT_WPE  // A/B builds (tools/gpu): minimum waves per SIMD the register allocation must allow
+#define PZK_ECT_WPE 1
+#endif
+#ifndef PZK_ECT_DIAG  // A/B builds only: 1 = no table load, 2 = no table lookup (wrong output; timing probes)
+#define PZK_ECT_DIAG 0
+#endif
 template <int MM, int ECT_U>  // store mode (mapsink.hpp), descriptors per batch
-__global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
+__global__ void __launch_bounds__(ECT_NT) __attribute__((amdgpu_waves_per_eu(PZK_ECT_WPE))) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
                                                   size_t stride, int prefetch) {
   __shared__ uint4 tab[2 * EC_TABLE_MAX[EC_CV]];
   const Work wk = work[blockIdx.x];
@@ -921,8 +927,6 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
   const int t = R.a[0], type = R.a[1];
   const uint32_t n = L.ec_tab_n[type];
   const uint4* src = reinterpret_cast<const uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
-  for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
-  __syncthreads();
   // mapped: the kept elements' descriptors, stored consecutively from their mapped index (desc_run)
   const DescRun dr = desc_run<MM>(L, wtns, stride, w, wk, R.off + wk.start, L.ec_prog + L.ec_prog_off[type] + wk.start);
   const uint32_t* prog = dr.prog;
@@ -939,7 +943,31 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
       dd[k] = h < tot ? prog[h >> 1] : 0u;
     }
   };
+  // the first descriptor batch is in flight with the table's loads (one load latency per workgroup, not two)
   load(threadIdx.x, dn);
+  // the table: all of a thread's loads issued before its LDS writes (a load / write loop waits out one load latency
+  // per iteration)
+#ifdef PZK_ECT_SERIAL_LOAD  // A/B builds: the round-3 load / write loop
+  if (PZK_ECT_DIAG != 1)
+    for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
+  if (false) {
+#else
+  if (PZK_ECT_DIAG != 1) {
+#endif
+    constexpr int TL = (2 * EC_TABLE_MAX[EC_CV] + ECT_NT - 1) / ECT_NT;
+    uint4 tv[TL];
+#pragma unroll
+    for (int k = 0; k < TL; k++) {
+      const uint32_t i = threadIdx.x + k * ECT_NT;
+      tv[k] = src[i < 2 * n ? i : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < TL; k++) {
+      const uint32_t i = threadIdx.x + k * ECT_NT;
+      if (i < 2 * n) tab[i] = tv[k];
+    }
+  }
+  __syncthreads();
   for (uint32_t base = threadIdx.x; base < tot; base += step) {
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) d[k] = dn[k];
@@ -947,7 +975,8 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
 #pragma unroll
     for (int k = 0; k < ECT_U; k++) {
       const uint32_t h = base + k * blockDim.x;
-      store_half<MAP_O0>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
+      const uint4 v = PZK_ECT_DIAG == 2 ? make_uint4(d[k], h, 0u, 0u) : ect_value(tab, d[k], h & 1);
+      store_half<MAP_O0>(out, h, h < tot ? v : make_uint4(0u, 0u, 0u, 0u), h < tot);
     }
     if (!prefetch && base + step < tot) load(base + step, dn);
   }

@@ -363,12 +363,25 @@ hipError_t launch_bjj_table(fr* table, hipStream_t st) {
 
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st) {
-  // PZK_BJJ_SEGS (8 / 16 / 32): lanes per witness, for tuning runs (runtime.cpp validates the value)
-  static const int segs = getenv("PZK_BJJ_SEGS") ? atoi(getenv("PZK_BJJ_SEGS")) : BJJ_SEGS_DEFAULT;
+  // scratch given: the round-3 kernel with its global scratch array (QueryIdentity's default, bjj_uses_scratch);
+  // PZK_BJJ_SEGS: lanes per witness (scratch 8 / 16 / 32, recompute 16 / 32 / 64), for tuning runs (runtime.cpp
+  // validates it)
+  static const int env_segs = getenv("PZK_BJJ_SEGS") ? atoi(getenv("PZK_BJJ_SEGS")) : 0;
+  const int segs = env_segs ? env_segs : scratch ? BJJ_SEGS_DEFAULT : BJJ_RC_SEGS_DEFAULT;
   const uint32_t lanes = vs.batch * segs;
-  auto kern = segs == 8 ? k_bjj_core<8> : segs == 32 ? k_bjj_core<32> : k_bjj_core<16>;
-  hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
+  if (scratch) {
+    auto kern = segs == 8 ? k_bjj_core<8> : segs == 32 ? k_bjj_core<32> : k_bjj_core<16>;
+    hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
+  } else {
+    auto kern = segs == 16 ? k_bjj_core_rc<16> : segs == 32 ? k_bjj_core_rc<32> : k_bjj_core_rc<64>;
+    hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, vs.batch);
+  }
   return hipGetLastError();
+}
+
+bool bjj_uses_scratch(bool chain_critical) {
+  const char* v = getenv("PZK_BJJ");
+  return v ? !strcmp(v, "scratch") : chain_critical;
 }
 
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,

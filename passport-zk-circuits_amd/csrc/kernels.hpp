@@ -39,6 +39,10 @@ hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* 
 hipError_t launch_bjj_table(fr* table, hipStream_t st);
 hipError_t launch_wtns_gather(const uint8_t* o0, size_t o0_stride, const uint32_t* map, uint64_t out_size, uint8_t* out,
                               size_t out_stride, uint32_t batch, hipStream_t st);
+// whether the BabyJubJub core runs the round-3 kernel with its global scratch array (launch_bjj_core: when it is
+// given one): by default where the core is on a latency-critical chain (QueryIdentity), else the recompute kernel
+// with no scratch; PZK_BJJ=scratch|rc overrides (A/B switch)
+bool bjj_uses_scratch(bool chain_critical);
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st);
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,

@@ -473,12 +473,29 @@ constexpr uint32_t BJJ_INV_B8X[8] = {0x7bc45854u, 0x42cd5135u, 0x5936d873u, 0x5d
                                      0x40d1c783u, 0x40e2c828u, 0xcaabb2bdu, 0x0b1a7dddu};
 constexpr uint64_t BJJ_A = 168700, BJJ_D = 168696;
 
+// the same constants in Montgomery form (R = 2^256), as literals: a kernel that sets them from these keeps no
+// registers for them (the compiler rematerialises literal moves)
+constexpr uint32_t BJJ_M_A[8] = {0xfff261e0u, 0x95accf61u, 0x9df7d378u, 0x24780d65u,
+                                 0x7e906ae8u, 0xe0ac11b0u, 0x16d3def3u, 0x0f35db22u};
+constexpr uint32_t BJJ_M_D[8] = {0xaff261f5u, 0x2735f484u, 0x9a2e0f63u, 0x70ba1b57u,
+                                 0x1e2caa8cu, 0xff41c9a9u, 0x8fe6025fu, 0x07704a8eu};
+constexpr uint32_t BJJ_M_B8X[8] = {0x1a89fa86u, 0x0a8fc7bcu, 0xe9e48627u, 0xa7d9d786u,
+                                   0x65bea369u, 0xee6158b4u, 0x2f874519u, 0x14a0ff6du};
+constexpr uint32_t BJJ_M_B8Y[8] = {0x0d0201aau, 0xb83342d2u, 0xcdcfeac7u, 0x2ffef2f7u,
+                                   0x25a6e625u, 0xbfa79a94u, 0xc3a44b70u, 0x0dfb859du};
+constexpr uint32_t BJJ_M_B8TD[8] = {0x0f1b2ee0u, 0x10c75c99u, 0xc23309edu, 0x83d5e20cu,
+                                    0xe93991cfu, 0x3fc6be6bu, 0xb5195112u, 0x03a44577u};
+
 struct BjjConsts {
   fr A, D, B8x, B8y, B8t_d;  // Montgomery
   __device__ __forceinline__ void init() {
     A = fr_to_mont(fr_u64(BJJ_A)); D = fr_to_mont(fr_u64(BJJ_D));
     B8x = fr_to_mont(fr_const(BJJ_B8X)); B8y = fr_to_mont(fr_const(BJJ_B8Y));
     B8t_d = fr_mul(fr_mul(D, B8x), B8y);
+  }
+  __device__ __forceinline__ void init_literal() {
+    A = fr_const(BJJ_M_A); D = fr_const(BJJ_M_D);
+    B8x = fr_const(BJJ_M_B8X); B8y = fr_const(BJJ_M_B8Y); B8t_d = fr_const(BJJ_M_B8TD);
   }
 };
 
@@ -514,6 +531,38 @@ __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
 #endif
 
 
+// segment start of the ladder below: A_{i0-1} = p * Base8, p = sk >> (254 - i0) (an i0-bit prefix), summed from the
+// fixed-base table (8-bit windows; the top window of a prefix may be partial)
+__device__ __forceinline__ void bjj_seg_start(const fr& sk, int i0, const fr* table, const BjjConsts& C, bool& have,
+                                              ExtPt& A) {
+  have = false;
+  A = ExtPt{fr_zero(), fr_zero(), fr_zero(), fr_zero()};
+  for (int wi = 0; 8 * wi < i0; wi++) {
+    uint32_t v = 0;
+    for (int b = 0; b < 8 && 8 * wi + b < i0; b++) v |= fr_bit(sk, 254 - i0 + 8 * wi + b) << b;
+    if (!v) continue;
+    const fr* e = table + 3 * (size_t)(wi * 256 + v);
+    if (!have) { A = ExtPt{e[0], e[1], fr_mont_one(), fr_mul(e[0], e[1])}; have = true; }
+    else A = bjj_add_affine(A, e[0], e[1], e[2], C.A);
+  }
+}
+// ladder step i (curve.circom:156-168): D_i = 2 A_{i-1} when A_{i-1} exists (the (0,0) sentinel otherwise: D = 0),
+// A_i = D_i + Base8 when bit 253 - i of sk is set, else D_i
+__device__ __forceinline__ void bjj_step(const fr& sk, int i, const BjjConsts& C, bool& have, ExtPt& A, bool& haveD,
+                                         ExtPt& D) {
+  const uint32_t bit = fr_bit(sk, 253 - i);
+  haveD = i > 0 && have;
+  D = haveD ? bjj_dbl(A, C.A) : ExtPt{fr_zero(), fr_zero(), fr_zero(), fr_zero()};
+  if (bit) {
+    if (haveD) A = bjj_add_affine(D, C.B8x, C.B8y, C.B8t_d, C.A);
+    else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = fr_mul(C.B8x, C.B8y); }
+    have = true;
+  } else {
+    if (haveD) A = D;
+    have = haveD;
+  }
+}
+
 // BabyjubjubBase8Multiplication (babyjubjub/curve.circom:143-171): MSB-first double-and-add over
 // the 254 bits of sk with the (0,0) sentinel for "no point yet". The ladder is cut into BJJ_SEGS
 // segments of BJJ_SEG_LEN steps, one lane each (BJJ_SEGS adjacent lanes = one witness): a segment
@@ -541,35 +590,16 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
   const int i0 = seg * BJJ_SEG_LEN, i1 = i0 + BJJ_SEG_LEN < NS ? i0 + BJJ_SEG_LEN : NS, ns = i1 - i0;
   auto S = [&](int e) -> fr& { return scratch[(size_t)e * nlanes + tid]; };
   const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
-  auto sk_bit = [&](int k) -> uint32_t { return fr_bit(sk, k); };  // bit k of sk
-  // segment start: A_{i0-1} = p * Base8, p = sk >> (254 - i0) (an i0-bit prefix)
-  bool have = false;
+  bool have;
   ExtPt A;
-  for (int wi = 0; 8 * wi < i0; wi++) {
-    uint32_t v = 0;
-    for (int b = 0; b < 8 && 8 * wi + b < i0; b++) v |= sk_bit(254 - i0 + 8 * wi + b) << b;
-    if (!v) continue;
-    const fr* e = table + 3 * (size_t)(wi * 256 + v);
-    if (!have) { A = ExtPt{e[0], e[1], fr_mont_one(), fr_mul(e[0], e[1])}; have = true; }
-    else A = bjj_add_affine(A, e[0], e[1], e[2], C.A);
-  }
+  bjj_seg_start(sk, i0, table, C, have, A);
   // projective coords of D_i (local elems 0..3ns) and A_i (3ns..6ns): [X, Y, Z] per step
   for (int j = 0; j < ns; j++) {
-    const int i = i0 + j;
-    const uint32_t bit = sk_bit(253 - i);
     ExtPt D;
-    bool haveD = false;
-    if (i > 0 && have) { D = bjj_dbl(A, C.A); haveD = true; }
+    bool haveD;
+    bjj_step(sk, i0 + j, C, have, A, haveD, D);
     if (haveD) { S(3 * j) = D.X; S(3 * j + 1) = D.Y; S(3 * j + 2) = D.Z; }
     else { S(3 * j) = fr_zero(); S(3 * j + 1) = fr_zero(); S(3 * j + 2) = fr_zero(); }
-    if (bit) {
-      if (haveD) A = bjj_add_affine(D, C.B8x, C.B8y, C.B8t_d, C.A);
-      else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = fr_mul(C.B8x, C.B8y); }
-      have = true;
-    } else {
-      if (haveD) A = D;
-      have = haveD;
-    }
     const int o = 3 * BJJ_SEG_LEN + 3 * j;
     if (have) { S(o) = A.X; S(o + 1) = A.Y; S(o + 2) = A.Z; }
     else { S(o) = fr_zero(); S(o + 1) = fr_zero(); S(o + 2) = fr_zero(); }
@@ -603,6 +633,85 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
   if (i1 == NS) {
     vs.at(L.reg.v_bjj, w) = out[5 * (NS - 1) + 2];
     vs.at(L.reg.v_bjj + 1, w) = out[5 * (NS - 1) + 3];
+  }
+}
+
+// The same ladder and outputs without the scratch array (k_bjj_core keeps 74 KB of points and prefix products per
+// witness in global memory, 6x its algorithmic traffic): the forward pass keeps only the step prefix products (LDS,
+// SL per lane) and two checkpoints of the ladder state (registers: the segment start and the state before step CK);
+// the backward pass recomputes step j's D and A from the nearer checkpoint (SL = 4: 2 + 1 + 2 + 1 extra steps).
+// Same per-lane segments as k_bjj_core, SEGS lanes per witness.
+#ifndef PZK_BJJ_RC_WPE  // waves per SIMD the register allocation must allow (A/B builds)
+#define PZK_BJJ_RC_WPE 2
+#endif
+template <int BJJ_SEGS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PZK_BJJ_RC_WPE))) k_bjj_core_rc(DevLayout L, ValueStore vs, const fr* table, fr* bjj_core,
+                                                   uint32_t batch) {
+  constexpr int SL = BJJ_SCRATCH_STEPS / BJJ_SEGS, CK = SL / 2;
+  static_assert(64 % BJJ_SEGS == 0 && SL * BJJ_SEGS >= BJJ_STEPS && SL >= 2, "segments must cover the ladder");
+  __shared__ fr pre[SL][64];  // prefix product before step j, per lane
+  core_priority();
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = tid / BJJ_SEGS;
+  const int seg = (int)(tid % BJJ_SEGS);
+  if (w >= batch) return;  // whole lane groups only (64 % BJJ_SEGS == 0)
+  BjjConsts C;
+  C.init_literal();
+  const int NS = BJJ_STEPS;
+  const int i0 = seg * SL, i1 = i0 + SL < NS ? i0 + SL : NS, ns = i1 - i0;
+  const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
+  bool have0, have1;
+  ExtPt A0, A1;
+  bjj_seg_start(sk, i0, table, C, have0, A0);
+  have1 = have0;
+  A1 = A0;
+  // forward: the ladder, prefix products of the inverted elements (Z(D_i), Z(A_i), X(D_i); zeros skipped)
+  fr acc = fr_mont_one();
+  {
+    bool have = have0;
+    ExtPt A = A0;
+    for (int j = 0; j < ns; j++) {
+      if (j == CK) { have1 = have; A1 = A; }
+      bool haveD;
+      ExtPt D;
+      bjj_step(sk, i0 + j, C, have, A, haveD, D);
+      pre[j][threadIdx.x] = acc;
+      const fr e1 = have ? A.Z : fr_zero();
+      if (!fr_is_zero(D.Z)) acc = fr_mul(acc, D.Z);
+      if (!fr_is_zero(e1)) acc = fr_mul(acc, e1);
+      if (!fr_is_zero(D.X)) acc = fr_mul(acc, D.X);
+    }
+  }
+  fr others, total;
+  fr_group_others<BJJ_SEGS>(acc, others, total);
+  fr inv = fr_mul(fr_inv_sw(total), others);  // = 1 / acc
+  fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
+  fr last_x = fr_zero(), last_y = fr_zero();
+  for (int j = ns - 1; j >= 0; j--) {
+    const int jb = j >= CK ? CK : 0;
+    bool have = j >= CK ? have1 : have0, haveD = false;
+    ExtPt A = j >= CK ? A1 : A0, D;
+    for (int k = jb; k <= j; k++) bjj_step(sk, i0 + k, C, have, A, haveD, D);
+    const fr e0 = D.Z, e1 = have ? A.Z : fr_zero(), e2 = D.X;
+    const fr q0 = pre[j][threadIdx.x];
+    const fr q1 = fr_is_zero(e0) ? q0 : fr_mul(q0, e0);
+    const fr q2 = fr_is_zero(e1) ? q1 : fr_mul(q1, e1);
+    fr r0 = fr_zero(), r1 = fr_zero(), r2 = fr_zero();
+    if (!fr_is_zero(e2)) { r2 = fr_mul(inv, q2); inv = fr_mul(inv, e2); }
+    if (!fr_is_zero(e1)) { r1 = fr_mul(inv, q1); inv = fr_mul(inv, e1); }
+    if (!fr_is_zero(e0)) { r0 = fr_mul(inv, q0); inv = fr_mul(inv, e0); }
+    fr* o = out + 5 * (i0 + j);  // Dx, Dy, Ax, Ay, inv(Dx)
+    const fr ax = fr_mul(A.X, r1), ay = fr_mul(A.Y, r1);
+    o[0] = fr_mul(D.X, r0);
+    o[1] = fr_mul(D.Y, r0);
+    o[2] = ax;
+    o[3] = ay;
+    o[4] = fr_mul(D.Z, r2);  // 1/x = Z / X
+    if (j == ns - 1) { last_x = ax; last_y = ay; }
+  }
+  if (i1 == NS) {
+    vs.at(L.reg.v_bjj, w) = last_x;
+    vs.at(L.reg.v_bjj + 1, w) = last_y;
   }
 }
 

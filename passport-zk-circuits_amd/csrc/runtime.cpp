@@ -409,8 +409,13 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   }
   if (const char* u = getenv("PZK_BJJ_SEGS")) {  // tuning switch of k_bjj_core (kernels.hip)
     int v = atoi(u);
-    if (v != 8 && v != 16 && v != 32) return fail(PZK_E_ARG, std::string("PZK_BJJ_SEGS=") + u + ": valid values are 8, 16, 32");
+    const bool sc = bjj_uses_scratch(params->circuit == PZK_CIRCUIT_QUERY);
+    if (sc ? (v != 8 && v != 16 && v != 32) : (v != 16 && v != 32 && v != 64))
+      return fail(PZK_E_ARG, std::string("PZK_BJJ_SEGS=") + u +
+                                 (sc ? ": valid values are 8, 16, 32 (PZK_BJJ=scratch)" : ": valid values are 16, 32, 64"));
   }
+  if (const char* u = getenv("PZK_BJJ"))
+    if (strcmp(u, "scratch") && strcmp(u, "rc")) return fail(PZK_E_ARG, std::string("PZK_BJJ=") + u + ": valid values are rc, scratch");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(PZK_E_NODEVICE, "no HIP device visible: pzkwit has no CPU fallback");
@@ -707,7 +712,7 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
       {(void**)&S.d_rsa_core, 8ull * L.rsa_core_words * batch},
       {(void**)&S.d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
       {(void**)&S.d_bjj_core, 32ull * L.bjj_core_fr * batch},
-      {(void**)&S.d_bjj_scratch, (L.is_register || L.is_query) ? 32ull * BJJ_SCRATCH_FR * batch : 0},
+      {(void**)&S.d_bjj_scratch, (L.is_register || L.is_query) && bjj_uses_scratch(L.is_query) ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&S.d_smt_core, 32ull * L.smt_core_fr * batch},
       {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].core_words * batch : 0},
       {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].jac_words * batch : 0},

@@ -62,6 +62,25 @@ def test_no_device_fails_loudly():
         native.Instance(native.PZK_CIRCUIT_POSEIDON, 2)
 
 
+@pytest.mark.parametrize("env,msg", [
+    ({"PZK_BJJ": "bogus"}, "PZK_BJJ=bogus: valid values are rc, scratch"),
+    ({"PZK_BJJ_SEGS": "8"}, "PZK_BJJ_SEGS=8: valid values are 16, 32, 64"),
+    ({"PZK_BJJ": "scratch", "PZK_BJJ_SEGS": "64"}, "PZK_BJJ_SEGS=64: valid values are 8, 16, 32"),
+    ({"PZK_SHA_U": "7"}, "PZK_SHA_U=7: valid values are 8, 16, 32"),
+])
+def test_tuning_switches_validated(env, msg):
+    """The tuning switches are checked before any device call (runtime.cpp pzk_instance_create): a bad value is an
+    argument error on any host, GPU or not. Run in a child: the library reads the switches once per process."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from pzkwit import native\n"
+            "try:\n    native.Instance(native.PZK_CIRCUIT_POSEIDON, 2)\nexcept native.PzkError as e:\n    print(e)\n"
+            % os.path.dirname(os.path.dirname(native.__file__)))
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                         timeout=120)
+    assert msg in out.stdout, out.stdout + out.stderr
+
+
 PARAM_SETS = [
     I.CANONICAL,
     dict(I.CANONICAL, doc=1),                      # TD1 chunking (190-bit dg1 chunks)

@@ -911,30 +911,38 @@ __device__ __forceinline__ uint4 ect_value(const uint4* tab, uint32_t d, uint32_
 // workgroup size: a big table (P-224 51 KB, brainpoolP384r1 39 KB of LDS) caps the workgroups per CU at 3-4, so
 // those curves run 8 waves per workgroup to keep ~24-32 waves per CU in flight
 constexpr int ECT_NT = EC_TABLE_MAX[EC_CV] > 1024 ? 512 : 256;
-#ifndef PZK_ECT_WPE  // A/B builds (tools/gpu): minimum waves per SIMD the register allocation must allow
-#define PZK_ECT_WPE 1
-#endif
-#ifndef PZK_ECT_DIAG  // A/B builds only: 1 = no table load, 2 = no table lookup (wrong output; timing probes)
-#define PZK_ECT_DIAG 0
-#endif
+// Work item x a run of WPB witnesses (PZK_ECT_WPB): the next witness's table is loaded into registers while this
+// one's elements are stored, so a workgroup waits out one table load (an HBM round trip, 13 % of the kernel as one
+// load per workgroup: profiles/r4_ectab) per WPB witnesses. The descriptor program is the same for all of them.
 template <int MM, int ECT_U>  // store mode (mapsink.hpp), descriptors per batch
-__global__ void __launch_bounds__(ECT_NT) __attribute__((amdgpu_waves_per_eu(PZK_ECT_WPE))) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
-                                                  size_t stride, int prefetch) {
+__global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* work, const uint8_t* ec_tab, uint8_t* wtns,
+                                                  size_t stride, int prefetch, uint32_t wpb, uint32_t batch) {
   __shared__ uint4 tab[2 * EC_TABLE_MAX[EC_CV]];
+  constexpr int TL = (2 * EC_TABLE_MAX[EC_CV] + ECT_NT - 1) / ECT_NT;  // table uint4 per thread
   const Work wk = work[blockIdx.x];
-  const uint32_t w = blockIdx.y;
+  const uint32_t wb = blockIdx.y * wpb, we = wb + wpb < batch ? wb + wpb : batch;
   const Region R = L.regions[wk.region];
   const int t = R.a[0], type = R.a[1];
-  const uint32_t n = L.ec_tab_n[type];
-  const uint4* src = reinterpret_cast<const uint4*>(ec_tab + 32ull * ((size_t)w * L.ec_tab_entries + L.ec_tab_off[t]));
+  const uint32_t n2 = 2 * L.ec_tab_n[type];
+  // native 4-vectors: a uint4 (HIP_vector_type) copy lowers to memcpy, which keeps tv[] in scratch
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* tab0 = reinterpret_cast<const u32x4*>(ec_tab + 32ull * L.ec_tab_off[t]);
+  u32x4* tabv = reinterpret_cast<u32x4*>(tab);
+  const size_t tab_stride = 2ull * L.ec_tab_entries;  // uint4 per witness
+  uint32_t ti[TL];  // this thread's table elements (clamped: every load is issued, before any use)
+#pragma unroll
+  for (int k = 0; k < TL; k++) ti[k] = threadIdx.x + k * ECT_NT < n2 ? threadIdx.x + k * ECT_NT : 0u;
+  u32x4 tv[TL];
   // mapped: the kept elements' descriptors, stored consecutively from their mapped index (desc_run)
-  const DescRun dr = desc_run<MM>(L, wtns, stride, w, wk, R.off + wk.start, L.ec_prog + L.ec_prog_off[type] + wk.start);
-  const uint32_t* prog = dr.prog;
-  const OutRow out = dr.out;
+  const uint64_t g = R.off + wk.start;
+  const uint32_t* o0_prog = L.ec_prog + L.ec_prog_off[type] + wk.start;
+  const DescRun dr0 = desc_run<MM>(L, wtns, stride, wb, wk, g, o0_prog);
+  const uint32_t* prog = dr0.prog;
   // ECT_U descriptors per batch, loaded before the batch's stores (a global load issued after a store waits for it:
-  // gfx9 vmcnt counts both, in order); with prefetch the next batch's descriptors are loaded ahead of this batch's
-  // stores (PZK_ECT_PREFETCH, PZK_ECT_U: tuning knobs). Two lanes per element, 1 KiB per wave store.
-  const uint32_t tot = 2 * dr.count, step = ECT_U * blockDim.x;
+  // gfx9 vmcnt counts both, in order); with prefetch the next batch's descriptors (the next witness's first batch
+  // at the end of a witness) are loaded ahead of this batch's stores (PZK_ECT_PREFETCH, PZK_ECT_U: tuning knobs).
+  // Two lanes per element, 1 KiB per wave store.
+  const uint32_t tot = 2 * dr0.count, step = ECT_U * blockDim.x;
   uint32_t d[ECT_U], dn[ECT_U];
   auto load = [&](uint32_t base, uint32_t* dd) {
 #pragma unroll
@@ -943,42 +951,32 @@ __global__ void __launch_bounds__(ECT_NT) __attribute__((amdgpu_waves_per_eu(PZK
       dd[k] = h < tot ? prog[h >> 1] : 0u;
     }
   };
-  // the first descriptor batch is in flight with the table's loads (one load latency per workgroup, not two)
-  load(threadIdx.x, dn);
-  // the table: all of a thread's loads issued before its LDS writes (a load / write loop waits out one load latency
-  // per iteration)
-#ifdef PZK_ECT_SERIAL_LOAD  // A/B builds: the round-3 load / write loop
-  if (PZK_ECT_DIAG != 1)
-    for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) tab[i] = src[i];
-  if (false) {
-#else
-  if (PZK_ECT_DIAG != 1) {
-#endif
-    constexpr int TL = (2 * EC_TABLE_MAX[EC_CV] + ECT_NT - 1) / ECT_NT;
-    uint4 tv[TL];
+  load(threadIdx.x, dn);  // in flight with the first table's loads
 #pragma unroll
-    for (int k = 0; k < TL; k++) {
-      const uint32_t i = threadIdx.x + k * ECT_NT;
-      tv[k] = src[i < 2 * n ? i : 0];
+  for (int k = 0; k < TL; k++) tv[k] = tab0[wb * tab_stride + ti[k]];
+  for (uint32_t w = wb; w < we; w++) {
+    if (w > wb) __syncthreads();  // the previous witness's lookups are done
+#pragma unroll
+    for (int k = 0; k < TL; k++) tabv[ti[k]] = tv[k];  // clamped elements rewrite element 0 with its own value
+    __syncthreads();
+    const bool more_w = w + 1 < we;
+    const size_t nt = (more_w ? w + 1 : w) * tab_stride;  // the next witness's table behind this one's stores
+#pragma unroll
+    for (int k = 0; k < TL; k++) tv[k] = tab0[nt + ti[k]];
+    const OutRow out = desc_run<MM>(L, wtns, stride, w, wk, g, o0_prog).out;
+    for (uint32_t base = threadIdx.x; base < tot; base += step) {
+#pragma unroll
+      for (int k = 0; k < ECT_U; k++) d[k] = dn[k];
+      const bool more = base + step < tot || more_w;
+      const uint32_t nbase = base + step < tot ? base + step : threadIdx.x;
+      if (prefetch && more) load(nbase, dn);
+#pragma unroll
+      for (int k = 0; k < ECT_U; k++) {
+        const uint32_t h = base + k * blockDim.x;
+        store_half<MAP_O0>(out, h, h < tot ? ect_value(tab, d[k], h & 1) : make_uint4(0u, 0u, 0u, 0u), h < tot);
+      }
+      if (!prefetch && more) load(nbase, dn);
     }
-#pragma unroll
-    for (int k = 0; k < TL; k++) {
-      const uint32_t i = threadIdx.x + k * ECT_NT;
-      if (i < 2 * n) tab[i] = tv[k];
-    }
-  }
-  __syncthreads();
-  for (uint32_t base = threadIdx.x; base < tot; base += step) {
-#pragma unroll
-    for (int k = 0; k < ECT_U; k++) d[k] = dn[k];
-    if (prefetch && base + step < tot) load(base + step, dn);
-#pragma unroll
-    for (int k = 0; k < ECT_U; k++) {
-      const uint32_t h = base + k * blockDim.x;
-      const uint4 v = PZK_ECT_DIAG == 2 ? make_uint4(d[k], h, 0u, 0u) : ect_value(tab, d[k], h & 1);
-      store_half<MAP_O0>(out, h, h < tot ? v : make_uint4(0u, 0u, 0u, 0u), h < tot);
-    }
-    if (!prefetch && base + step < tot) load(base + step, dn);
   }
 }
 

@@ -52,7 +52,11 @@ hipError_t launch_emit_ect_cv(const DevLayout& L, const Work* work, uint32_t n_w
   static const int u = getenv("PZK_ECT_U") ? atoi(getenv("PZK_ECT_U")) : 16;  // isolated P-256: 8 / 16 / 32 = 22.6 / 21.7 / 41.0 ms
   auto kern = L.keep.bits ? k_emit_ect<MAP_DIRECT, 16>
               : u == 16 ? k_emit_ect<MAP_O0, 16> : u == 32 ? k_emit_ect<MAP_O0, 32> : k_emit_ect<MAP_O0, 8>;
-  hipLaunchKernelGGL(kern, dim3(n_work, batch), dim3(ECT_NT), 0, st, L, work, B.ec_tab, B.wtns, B.stride, prefetch);
+  // witnesses per workgroup (A/B switch PZK_ECT_WPB; the next witness's table loads behind this one's stores)
+  static const uint32_t wpb = getenv("PZK_ECT_WPB") ? (uint32_t)atoi(getenv("PZK_ECT_WPB")) : 4u;
+  if (wpb < 1 || wpb > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3(n_work, (batch + wpb - 1) / wpb), dim3(ECT_NT), 0, st, L, work, B.ec_tab, B.wtns,
+                     B.stride, prefetch, wpb, batch);
   return hipGetLastError();
 }
 

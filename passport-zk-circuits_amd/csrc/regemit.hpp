@@ -396,9 +396,9 @@ struct MMCore {
   const uint64_t *x, *y, *q, *r, *n, *inv, *cr;  // LDS
   const uint64_t *cxy, *cqn;                      // LDS: column sums of x*y (2K-1) and q*n (2K), 3 words each
   bool kara;                                      // x*y by KaratsubaOverflow (K = 2^m), else schoolbook
-  const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32; else null)
+  const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32 / 64; else null)
   const uint8_t* kt_hi;
-  const uint64_t* ko;                             // LDS node outputs of Karatsuba levels 1..KO_LEVELS (K = 32; else null)
+  const uint64_t* ko;                             // LDS node outputs of the upper Karatsuba levels (K = 32 / 64; else null)
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
 };
 __device__ __forceinline__ U192 u192_at(const uint64_t* a, int i) { U192 r; r.a0 = a[3 * i]; r.a1 = a[3 * i + 1]; r.a2 = a[3 * i + 2]; return r; }
@@ -415,11 +415,6 @@ __device__ __forceinline__ U192 u192_shfl_up(const U192& v, unsigned d) {
   return r;
 }
 
-// value of Karatsuba node input j under offset mask O: sum of limbs a[j + o], o in O (<= 2^70)
-__device__ __forceinline__ void kara_in(const uint64_t* a, uint64_t O, int j, uint64_t& lo, uint64_t& hi) {
-  lo = 0; hi = 0;
-  while (O) { int o = __builtin_ctzll(O); O &= O - 1; uint64_t v = a[j + o]; lo += v; hi += lo < v; }
-}
 // U192 += (alo + ahi 2^64) * (blo + bhi 2^64), ahi, bhi < 2^8
 __device__ __forceinline__ void mac2(U192& acc, uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi) {
   acc.mac(alo, blo);
@@ -433,62 +428,6 @@ __device__ __forceinline__ W256 u192w(const U192& a) {
   r.v[4] = (uint32_t)a.a2; r.v[5] = (uint32_t)(a.a2 >> 32);
   return r;
 }
-// KaratsubaOverflow(N) block size S(N) = 4N + 3 S(N/2), S(1) = 4 (closed table, no recursion)
-__host__ __device__ inline uint32_t kara_size(int N) {
-  switch (N) {
-    case 1: return 4; case 2: return 20; case 4: return 76; case 8: return 260; case 16: return 844;
-    case 32: return 2660; case 64: return 8236; default: return 0;
-  }
-}
-
-// Karatsuba subtree signal (bigIntHelpers.circom:11-53). A node's out[] is the convolution of
-// its inputs: at the root that is the x*y column sums (LDS); below it, products of the node's
-// input values from the table (K = 32) or sums over the node's limb offsets (K = 64).
-__device__ __forceinline__ W256 kara_sig(const MMCore& C, int N, uint32_t s) {
-  uint64_t O = 1;  // offsets set (bit o = offset o)
-  int lvl = 0, m = 0, p3 = 1, base = 0;  // level, node index in level, 3^lvl, table start of the level
-  for (;;) {
-    const int tb = C.kt_lo && lvl > 0 ? base + m * 2 * N : -1;  // this node's table slice
-    if (s < (uint32_t)(2 * N)) {
-      if (s == (uint32_t)(2 * N - 1)) return w_zero();  // top coefficient (K(1).out[1] never assigned)
-      if (lvl == 0) return u192w(u192_at(C.cxy, (int)s));
-      U192 acc;
-      int lo = s < (uint32_t)N ? 0 : (int)s - N + 1, hi = s < (uint32_t)N ? (int)s : N - 1;
-      for (int u = lo; u <= hi; u++) {
-        uint64_t al, ah, bl, bh;
-        if (tb >= 0) {
-          al = C.kt_lo[tb + u]; ah = C.kt_hi[tb + u];
-          bl = C.kt_lo[tb + N + (int)s - u]; bh = C.kt_hi[tb + N + (int)s - u];
-        } else {
-          kara_in(C.x, O, u, al, ah);
-          kara_in(C.y, O, (int)s - u, bl, bh);
-        }
-        mac2(acc, al, ah, bl, bh);
-      }
-      return u192w(acc);
-    }
-    if (s < (uint32_t)(4 * N)) {
-      const int k = (int)s - 2 * N;  // in1[0..N) then in2[0..N)
-      uint64_t lo, hi;
-      if (tb >= 0) { lo = C.kt_lo[tb + k]; hi = C.kt_hi[tb + k]; }
-      else kara_in(k < N ? C.x : C.y, O, k < N ? k : k - N, lo, hi);
-      W256 r = w_zero(); r.v[0] = (uint32_t)lo; r.v[1] = (uint32_t)(lo >> 32); r.v[2] = (uint32_t)hi;
-      return r;
-    }
-    s -= 4 * N;
-    int h = N / 2;
-    const uint32_t cs = kara_size(h), c = s >= cs ? (s >= 2 * cs ? 2u : 1u) : 0u;  // child 0, 1, 2
-    s -= c * cs;
-    if (c == 1) O <<= h;
-    else if (c == 2) O |= O << h;
-    if (lvl > 0) base += p3 * 2 * N;
-    p3 *= 3;
-    m = 3 * m + (int)c;
-    lvl++;
-    N = h;
-  }
-}
-
 // signed 256-bit (two's complement in W256) -> normal-form field element
 __device__ __forceinline__ W256 w_signed_to_fr(const W256& a) {
   if (!(a.v[7] >> 31)) return a;
@@ -545,8 +484,7 @@ __device__ __forceinline__ W256 mm_sig(const MMCore& C, uint32_t d) {
     case MM_XYN: { int g = s / K, i = s - g * K; return w_u64(g == 0 ? C.x[i] : g == 1 ? C.y[i] : C.n[i]); }
     case MM_MOUT: return u192w(u192_at(C.cxy, (int)s));                // mult.out = x*y columns
     case MM_MCOPY: return w_u64(s < (uint32_t)K ? C.x[s] : C.y[s - K]);
-    case MM_KARA: {
-      if (C.kara) return kara_sig(C, K, s);
+    case MM_KARA: {  // K = 32 / 64 (KaratsubaOverflow) go to kara_el32 / kara_el64 (mm_el)
       // BigMultNonEqualOverflow(K, K) of x, y: out[2K-1] | in1[K], in2[K] | tmpMults[K][K] | tmpResult[2K-1][K]
       uint32_t e = s;
       if (e < (uint32_t)(2 * K - 1)) return u192w(u192_at(C.cxy, (int)e));
@@ -639,8 +577,8 @@ __device__ __forceinline__ El el_num2bits(uint64_t lo, uint64_t hi, uint32_t L, 
 // KaratsubaOverflow(32) signal from tables (K = KT_K): the node is found by a fixed five-step descent over the
 // compile-time subtree sizes (no size switch, no loop), its inputs are Karatsuba table entries and the outputs of
 // levels 1..KO_LEVELS come precomputed from LDS (ko, filled once per workgroup by k_emit_mm), so only the two
-// deepest levels (<= 2 products per signal) are multiplied here. kara_sig walked the tree and formed each output
-// as a convolution of up to 16 products per lane, the dominant VALU cost of the K = 32 emitter.
+// deepest levels (<= 2 products per signal) are multiplied here (round 2 walked the tree per signal and formed each
+// output as a convolution of up to 16 products per lane, the dominant VALU cost of the K = 32 emitter).
 constexpr int KO_LEVELS = 3, KO_VALUES = 456;  // 3 x 32 + 9 x 16 + 27 x 8 node outputs (2N per node)
 __device__ __forceinline__ int kt_level_base(int l) {  // first table entry of level l >= 1 (2N entries per node)
   return l == 1 ? 0 : l == 2 ? 96 : l == 3 ? 240 : l == 4 ? 456 : 780;
@@ -678,6 +616,81 @@ __device__ __forceinline__ El kara_el32(const MMCore& C, const uint64_t* ko, uin
   return el_w(u192w(acc));
 }
 
+// KaratsubaOverflow(64) signal (K = 64, RSA-4096), the K = 32 scheme one level deeper. LDS holds the in1/in2
+// values of levels 1..K64_TL (K64_TL_VALUES, filled once per workgroup) and the node outputs of levels
+// 1..K64_OL (ko). Deeper nodes' inputs (levels 5, 6: N = 2, 1) are sums of at most 4 level-4 entries, found by
+// walking up the tree as offset masks (a child takes its parent's low half, high half, or their sum), so the
+// table fits beside the block's core (3 workgroups per CU); output signals of levels 3..6 multiply <= 8 / 4 / 2 / 1
+// pairs of such values. The round-2 walker this replaces summed limbs of x and y for every input and every
+// product (91 k VALU instructions per wave).
+constexpr int K64_TL = 4, K64_OL = 2;
+__host__ __device__ constexpr int kt_base64(int l) {  // first table entry of level l >= 1 (2N entries per node)
+  return l <= 1 ? 0 : l == 2 ? 192 : l == 3 ? 480 : l == 4 ? 912 : 1560;
+}
+constexpr int K64_TL_VALUES = kt_base64(K64_TL + 1), K64_OL_VALUES = kt_base64(K64_OL + 1);  // 1560, 480
+__device__ __forceinline__ El kara_el64(const MMCore& C, const uint64_t* ko, uint32_t s) {
+  constexpr uint32_t SZ[7] = {mm_kara_size(64), mm_kara_size(32), mm_kara_size(16), mm_kara_size(8),
+                              mm_kara_size(4), mm_kara_size(2), mm_kara_size(1)};
+  int lvl = 0, m = 0;
+  uint32_t p = s;
+#pragma unroll
+  for (int L = 0; L < 6; L++) {  // node at level L has 4 N_L own signals, then its 3 child subtrees of SZ[L + 1]
+    const uint32_t own = 4u * (64u >> L);
+    if (lvl == L && p >= own) {
+      p -= own;
+      const uint32_t c = (p >= SZ[L + 1] ? 1u : 0u) + (p >= 2 * SZ[L + 1] ? 1u : 0u);
+      p -= c * SZ[L + 1];
+      m = 3 * m + (int)c;
+      lvl = L + 1;
+    }
+  }
+  const int N = 64 >> lvl;
+  // input value k of in1 (op 0) or in2 (op 1) of node (lvl, m), lvl >= 1
+  auto val = [&](int op, int k, uint64_t& lo, uint64_t& hi) {
+    if (lvl <= K64_TL) {
+      const int i = kt_base64(lvl) + m * 2 * N + op * N + k;
+      lo = C.kt_lo[i]; hi = C.kt_hi[i];
+      return;
+    }
+    uint32_t O = 1u << k;  // offsets into the level-K64_TL ancestor's N = 4 values
+    int a = m, n = N;
+    for (int l = lvl; l > K64_TL; l--) {
+      const int c = a % 3;
+      a /= 3;
+      O = c == 0 ? O : c == 1 ? O << n : (O | (O << n));
+      n *= 2;
+    }
+    const int tb = kt_base64(K64_TL) + a * 2 * n + op * n;
+    lo = 0; hi = 0;
+    while (O) {
+      const int j = __builtin_ctz(O);
+      O &= O - 1;
+      const uint64_t v = C.kt_lo[tb + j];
+      lo += v;
+      hi += C.kt_hi[tb + j] + (lo < v ? 1u : 0u);
+    }
+  };
+  if (p >= 2u * N) {  // in1[N] | in2[N]
+    const int k = (int)p - 2 * N;
+    if (lvl == 0) return el_u64(k < N ? C.x[k] : C.y[k - N]);
+    uint64_t lo, hi;
+    val(k >= N ? 1 : 0, k >= N ? k - N : k, lo, hi);
+    return el_u128(lo, hi);
+  }
+  if (p == 2u * N - 1) return el_zero();  // top coefficient (K(1).out[1] never assigned)
+  if (lvl == 0) return el_w(u192w(u192_at(C.cxy, (int)p)));
+  if (lvl <= K64_OL) return el_w(u192w(u192_at(ko, kt_base64(lvl) + m * 2 * N + (int)p)));
+  const int lo_u = (int)p < N ? 0 : (int)p - N + 1, hi_u = (int)p < N ? (int)p : N - 1;
+  U192 acc;
+  for (int u = lo_u; u <= hi_u; u++) {
+    uint64_t al, ah, bl, bh;
+    val(0, u, al, ah);
+    val(1, (int)p - u, bl, bh);
+    mac2(acc, al, ah, bl, bh);
+  }
+  return el_w(u192w(acc));
+}
+
 template <int K, int SEC>
 __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
   if constexpr (SEC == MM_MODCHK) {  // Num2Bits(64)(mod_i): out[64] | in | sum[64]
@@ -707,6 +720,11 @@ __device__ __forceinline__ El mm_el(const MMCore& C, uint32_t s) {
     return el_num2bits(lo, hi, RL, t);
   } else if constexpr (SEC == MM_KARA && K == KT_K) {
     return kara_el32(C, C.ko, s);
+  } else if constexpr (SEC == MM_KARA && K == 64) {
+    return kara_el64(C, C.ko, s);
+  } else if constexpr (SEC == MM_KARA) {
+    static_assert((K & (K - 1)) != 0, "KaratsubaOverflow sizes have their own table path");
+    return el_w(mm_sig(C, ((uint32_t)SEC << 24) | s));
   } else if constexpr (SEC == MM_Q) {
     return el_u64(C.q[s]);
   } else if constexpr (SEC == MM_R) {
@@ -773,12 +791,12 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   __syncthreads();
   // Karatsuba input table (K = 32), level by level: a child's operand is the parent's low half,
   // high half, or their sum
-  constexpr int KTN = K == KT_K ? KT_VALUES : 1;
+  constexpr int KTN = K == KT_K ? KT_VALUES : K == 64 ? K64_TL_VALUES : 1;
   __shared__ uint64_t kt_lo[KTN];
   __shared__ uint8_t kt_hi[KTN];
-  if (K == KT_K) {
+  if (K == KT_K || K == 64) {
     int base = 0, pbase = 0, nodes = 3;
-    for (int l = 1; l <= KT_LEVELS; l++) {
+    for (int l = 1; l <= (K == KT_K ? KT_LEVELS : K64_TL); l++) {
       const int N = K >> l, cnt = nodes * 2 * N;
       for (int r = threadIdx.x; r < cnt; r += blockDim.x) {
         const int m = r / (2 * N), k = r - m * 2 * N, op = k >= N, u = k - op * N, p = m / 3, c = m - 3 * p;
@@ -805,12 +823,13 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   }
   // outputs of the Karatsuba nodes of levels 1..KO_LEVELS (K = 32): out[s] = sum_u in1[u] in2[s - u] over the
   // node's table inputs, once per workgroup (kara_el32 reads them)
-  constexpr int KON = K == KT_K ? 3 * KO_VALUES : 1;
+  constexpr int KON = K == KT_K ? 3 * KO_VALUES : K == 64 ? 3 * K64_OL_VALUES : 1;
   __shared__ uint64_t ko[KON];
-  if (K == KT_K) {
-    for (int r = threadIdx.x; r < KO_VALUES; r += blockDim.x) {
-      const int l = r < 96 ? 1 : r < 240 ? 2 : 3, N = K >> l, rr = r - kt_level_base(l), m = rr / (2 * N);
-      const int p = rr - m * 2 * N, tb = kt_level_base(l) + m * 2 * N;
+  if (K == KT_K || K == 64) {
+    for (int r = threadIdx.x; r < (K == KT_K ? KO_VALUES : K64_OL_VALUES); r += blockDim.x) {
+      const int l = K == KT_K ? (r < 96 ? 1 : r < 240 ? 2 : 3) : (r < kt_base64(2) ? 1 : 2), N = K >> l;
+      const int lb = K == KT_K ? kt_level_base(l) : kt_base64(l), rr = r - lb, m = rr / (2 * N);
+      const int p = rr - m * 2 * N, tb = lb + m * 2 * N;
       U192 acc;
       if (p < 2 * N - 1)
         for (int u = p < N ? 0 : p - N + 1; u <= (p < N ? p : N - 1); u++)
@@ -820,8 +839,8 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
     __syncthreads();
   }
   MMCore C{K, lds, lds + K, lds + 2 * K, lds + 3 * K + 1, lds + MM_CORE_WORDS(K), lds + 4 * K + 1, lds + 8 * K + 1,
-           cxy, cqn, (K & (K - 1)) == 0, K == KT_K ? kt_lo : nullptr, K == KT_K ? kt_hi : nullptr,
-           K == KT_K ? ko : nullptr};
+           cxy, cqn, (K & (K - 1)) == 0, K == KT_K || K == 64 ? kt_lo : nullptr, K == KT_K || K == 64 ? kt_hi : nullptr,
+           K == KT_K || K == 64 ? ko : nullptr};
   const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   PZK_MM_ACC(MM_SECTIONS, tp);  // prologue: core loads, column sums, Karatsuba input table

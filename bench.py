@@ -648,16 +648,30 @@ class MixedGpuEngine:
         self.d_st = torch.zeros(n_local, dtype=torch.int32, device=self.dev)
         torch.cuda.synchronize(self.dev)  # the library's streams do not wait for torch's stream
 
+    def _calls(self):
+        """(flow, first row) of every call of a step: flow by flow (PZK_MIX_ORDER=flow) or round robin over the flows
+        (default), so each flow's calls are spread over the step instead of one flow's calls all queued first"""
+        if os.environ.get("PZK_MIX_ORDER", "rr") == "flow":
+            return [(sg, a) for sg, idx in self.groups.items() for a in range(0, len(idx), self.sub[sg])]
+        # the flow with the largest witnesses (ECDSA: the longest core chain per call) first in every round
+        order = sorted(self.groups, key=lambda sg: -self.witness_size[sg])
+        per = {sg: list(range(0, len(self.groups[sg]), self.sub[sg])) for sg in order}
+        out, k = [], 0
+        while any(k < len(aa) for aa in per.values()):
+            out += [(sg, aa[k]) for sg, aa in per.items() if k < len(aa)]
+            k += 1
+        return out
+
     def _run(self, st, collect=None):
-        for sg, idx in self.groups.items():
+        for sg, a in self._calls():
+            idx = self.groups[sg]
             W, NIN = self.witness_size[sg], self.n_inputs[sg]
-            for a in range(0, len(idx), self.sub[sg]):
-                n = min(self.sub[sg], len(idx) - a)
-                self.inst[sg].witness_batch_device(self.d_in[sg].data_ptr() + a * NIN * 32, n, self.d_out[sg].data_ptr(),
-                                                   32 * W, st.data_ptr() + 4 * (self.first[sg] + a))
-                if collect:
-                    self.inst[sg].sync()
-                    collect(sg, a, n, self.d_out[sg].view(self.sub[sg], W, 32)[:n])
+            n = min(self.sub[sg], len(idx) - a)
+            self.inst[sg].witness_batch_device(self.d_in[sg].data_ptr() + a * NIN * 32, n, self.d_out[sg].data_ptr(),
+                                               32 * W, st.data_ptr() + 4 * (self.first[sg] + a))
+            if collect:
+                self.inst[sg].sync()
+                collect(sg, a, n, self.d_out[sg].view(self.sub[sg], W, 32)[:n])
 
     def step(self):
         self._run(self.d_st)

@@ -771,8 +771,27 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   const Region R = L.regions[wk.region];
   const uint64_t* mc = B.rsa_core + (size_t)w * L.rsa_core_words + (size_t)R.a[0] * MM_CORE_WORDS(K);
   const uint8_t* row = B.inputs + 32ull * (uint64_t)w * L.n_inputs;
+#ifdef PZK_MM_SERIAL_LOAD  // A/B builds: the round-3 load / write loops
   for (int i = threadIdx.x; i < MM_CORE_WORDS(K); i += blockDim.x) lds[i] = mc[i];
   for (int i = threadIdx.x; i < K; i += blockDim.x) lds[MM_CORE_WORDS(K) + i] = in_u64(row + 32ull * (R.a[1] + i));
+#else
+  // every load issued before any LDS write: a load / write loop waits out one HBM round trip per iteration, and
+  // under the emitters' store stream that is several microseconds each (MM_CORE_WORDS(32) = 381: two per thread)
+  constexpr int MM_NT = 256, CW = MM_CORE_WORDS(K), CL = (CW + MM_NT - 1) / MM_NT;
+  uint64_t cv[CL];
+#pragma unroll
+  for (int k = 0; k < CL; k++) {
+    const int i = threadIdx.x + k * MM_NT;
+    cv[k] = mc[i < CW ? i : 0];
+  }
+  const uint64_t xin = in_u64(row + 32ull * (R.a[1] + (threadIdx.x < K ? threadIdx.x : 0)));
+#pragma unroll
+  for (int k = 0; k < CL; k++) {
+    const int i = threadIdx.x + k * MM_NT;
+    if (i < CW) lds[i] = cv[k];
+  }
+  if (threadIdx.x < K) lds[CW + threadIdx.x] = xin;
+#endif
   __syncthreads();
   // column sums of x*y (2K-1) and q*n (2K), one thread per column
   uint64_t* cxy = lds + MM_CORE_WORDS(K) + K;

@@ -167,12 +167,12 @@ struct pzk_instance {
   Scratch scr[NSETS];
   uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
   // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit, tail, chain2)
-  static constexpr int NSTREAMS = 6;
+  static constexpr int NSTREAMS = 7;
   hipEvent_t ev_done[NSETS][NSTREAMS] = {};
   hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
   hipStream_t s_tail = nullptr;  // the small tail emitters (PZK_TAIL=own), so the next call's SHA emitter never queues behind them
-  hipStream_t s_chain2 = nullptr;  // register calls: the second SMT chain stream (PZK_SMT_CHAINS=2)
+  hipStream_t s_chain2 = nullptr, s_chain3 = nullptr;  // register calls: further SMT chain streams (PZK_SMT_CHAINS)
   uint64_t chain_rr = 0;           // register calls: SMT chain stream rotation
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
@@ -357,7 +357,7 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3})
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab,
                        I->ev_smt, I->ev_chain})
@@ -391,7 +391,7 @@ struct DeviceGuard {
 
 // wait until every stream of the instance has drained (all calls issued so far are complete)
 static int sync_all(pzk_instance* I) {
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
@@ -476,7 +476,8 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_lo) == hipSuccess;
+       hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+       hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
                         &I->ev_smt, &I->ev_chain})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -946,11 +947,12 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // tail = on the fifth stream with the tail emitters behind it there (76.8k / 47.3k)
     static const char* smt_env = getenv("PZK_SMT");
     static const int smt_mode = !smt_env ? 1 : !strcmp(smt_env, "main") ? 0 : !strcmp(smt_env, "tail") ? 2 : 1;
-    // PZK_SMT_CHAINS=2 (A/B): consecutive calls' chains alternate between the fifth and a sixth stream, so two
-    // chains run side by side (QueryIdentity's rotation, §11)
-    static const int smt_chains = getenv("PZK_SMT_CHAINS") ? atoi(getenv("PZK_SMT_CHAINS")) : 2;  // r4_ect: 64.8k vs 52.3k (depth 40-79)
-    hipStream_t s_smt = (serial || tail_mode == 4 || smt_mode == 0) ? st
-                        : (smt_chains >= 2 && (I->chain_rr++ & 1)) ? I->s_chain2 : I->s_tail;
+    // PZK_SMT_CHAINS=1..3 (A/B): consecutive calls' chains rotate over that many streams, so that many chains run
+    // side by side (QueryIdentity's rotation, §11); r4_ect: 64.8k (2) vs 52.3k (1) at depth 40-79
+    static const int smt_chains = getenv("PZK_SMT_CHAINS") ? atoi(getenv("PZK_SMT_CHAINS")) : 2;
+    const hipStream_t chain_streams[3] = {I->s_tail, I->s_chain2, I->s_chain3};
+    const int n_chain = smt_chains < 1 ? 1 : smt_chains > 3 ? 3 : smt_chains;
+    hipStream_t s_smt = (serial || tail_mode == 4 || smt_mode == 0) ? st : chain_streams[I->chain_rr++ % n_chain];
     if (s_smt != st) {
       HIPCHK(hipEventRecord(I->ev_smt, st));
       HIPCHK(hipStreamWaitEvent(s_smt, I->ev_smt, 0));
@@ -992,7 +994,8 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
       if ((rc = emit(E_ECT, s_sha, ect_split))) return rc;
     }
   }
-  hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, serial ? st : I->s_chain2};
+  hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, serial ? st : I->s_chain2,
+                                                 serial ? st : I->s_chain3};
   for (int i = 0; i < pzk_instance::NSTREAMS; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));

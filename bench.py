@@ -355,11 +355,12 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
     ap.add_argument("--host-sample", type=int, default=None, help="witnesses streamed for host_delivered")
     args = ap.parse_args()
-    if args.workload == "mixed":
-        # one instance per flow, six streams each: with HIP's default 4 hardware queues the flows' streams share
-        # queues and serialise behind each other (40.9k -> 43.2k witnesses/s at 16, profiles/r4_hwq/); set before any
-        # HIP call, inherited by the ranks launch_ranks starts
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    if args.workload == "mixed" and os.environ.get("PZK_MIX_HWQ", "16") != "keep":
+        # one instance per flow, seven streams each: with 4 hardware queues (HIP's default, and what the GPU boxes'
+        # environment sets) the flows' streams share queues and serialise behind each other (40.9k -> 43.2k
+        # witnesses/s at 16, profiles/r4_hwq/); set before any HIP call, inherited by the ranks launch_ranks starts
+        # (PZK_MIX_HWQ=keep leaves the environment's value)
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PZK_MIX_HWQ", "16")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)  # before torch / any GPU call
     args.sig_eff = (args.sig or WL_SIG[args.workload]) if args.workload.startswith("register") else 0
@@ -787,6 +788,7 @@ def run_mixed_rank(args, rank, world, local, dist, engine_cls=MixedGpuEngine, de
                    "flows": {str(k): len(v) for k, v in groups.items()}, "rank0_bytes": my_bytes,
                    "sub_batches": {str(k): v for k, v in (getattr(engine, "sub", None) or {}).items()},
                    "invalid_lanes": bad, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                   "call_order": os.environ.get("PZK_MIX_ORDER", "rr"),
                    "inputs": "rank 0 generates every shard and scatters it (process group)", "gathered": gathered},
         "job_hbm": {"achieved": round(job_gbs, 1), "unit": "GB/s", "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
     }

@@ -476,8 +476,11 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_lo) == hipSuccess;
+       hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_lo) == hipSuccess;
+  // the third chain stream only when asked for (PZK_SMT_CHAINS=3): with several instances in a process every stream
+  // competes for the process's hardware queues
+  if (ok && getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
+    ok = hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
                         &I->ev_smt, &I->ev_chain})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -951,7 +954,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // side by side (QueryIdentity's rotation, §11); r4_ect: 64.8k (2) vs 52.3k (1) at depth 40-79
     static const int smt_chains = getenv("PZK_SMT_CHAINS") ? atoi(getenv("PZK_SMT_CHAINS")) : 2;
     const hipStream_t chain_streams[3] = {I->s_tail, I->s_chain2, I->s_chain3};
-    const int n_chain = smt_chains < 1 ? 1 : smt_chains > 3 ? 3 : smt_chains;
+    const int n_chain = smt_chains < 1 ? 1 : smt_chains >= 3 && I->s_chain3 ? 3 : smt_chains >= 2 ? 2 : 1;
     hipStream_t s_smt = (serial || tail_mode == 4 || smt_mode == 0) ? st : chain_streams[I->chain_rr++ % n_chain];
     if (s_smt != st) {
       HIPCHK(hipEventRecord(I->ev_smt, st));
@@ -995,7 +998,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
   }
   hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, serial ? st : I->s_chain2,
-                                                 serial ? st : I->s_chain3};
+                                                 serial ? st : I->s_chain3 ? I->s_chain3 : I->s_chain2};
   for (int i = 0; i < pzk_instance::NSTREAMS; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));

@@ -394,8 +394,11 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
                             hipStream_t st) {
-  static const bool call = getenv("PZK_CHAIN_MUL") && !strcmp(getenv("PZK_CHAIN_MUL"), "call");
-  hipLaunchKernelGGL(call ? k_smt_chain<FrMulCall> : k_smt_chain<FrMulInline>, dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
+  // PZK_CHAIN_MUL=inline (CIOS, default) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch
+  static const char* pm = getenv("PZK_CHAIN_MUL");
+  static const int mode = !pm ? 0 : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
+  hipLaunchKernelGGL(mode == 1 ? k_smt_chain<FrMulCall> : mode == 2 ? k_smt_chain<FrMulFips> : k_smt_chain<FrMulInline>,
+                     dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
                      dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core, smt_core, order, status, vs.batch);
   return hipGetLastError();
 }

@@ -182,6 +182,11 @@ struct FrMulCall {
   __device__ static __forceinline__ fr mul(const fr& a, const fr& b) { return fr_mul_ool(a, b); }
   __device__ static __forceinline__ fr sqr(const fr& a) { return fr_sqr_ool(a); }
 };
+// FIPS products (fr.hpp fr_mul_fast: the throughput product, 1,200 vs 1,560 cycles per wave64 product)
+struct FrMulFips {
+  __device__ static __forceinline__ fr mul(const fr& a, const fr& b) { return fr_mul_fast(a, b); }
+  __device__ static __forceinline__ fr sqr(const fr& a) { return fr_mul_fast(a, a); }
+};
 template <class PM>
 __device__ __forceinline__ fr pow5p(const fr& x) { fr x2 = PM::sqr(x), x4 = PM::sqr(x2); return PM::mul(x4, x); }
 

@@ -819,7 +819,7 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 // reads is staged in LDS first — the width-3 constants, the group's siblings (Montgomery) and left/right bits,
 // the level tasks' core offsets — so the loop issues no global load: a global load issued after the round-state
 // stores would wait for them (gfx9 vmcnt counts both), one store latency per round of every level.
-// PM: the product policy (PZK_CHAIN_MUL=inline|call, A/B; poseidon.hpp FrMulInline / FrMulCall)
+// PM: the product policy (PZK_CHAIN_MUL=inline|call|fips, A/B; poseidon.hpp FrMulInline / FrMulCall / FrMulFips)
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 template <class PM>
 __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, const int32_t* level_task, const uint8_t* inputs,

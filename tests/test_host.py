@@ -392,3 +392,27 @@ def test_mixed_bench_two_ranks_gloo():
     assert g["public_sha256"] == hashlib.sha256(np.stack(pub).tobytes()).hexdigest()[:16]
     assert out["config"]["invalid_lanes"] == sum(st)  # both ranks' last timed step
     assert set(out["config"]["flows"]) <= {"1", "2", "20"}
+
+
+def test_mixed_engine_call_order(monkeypatch):
+    """MixedGpuEngine issues a step's calls round robin over the flows, the flow with the largest witnesses first in
+    every round (PZK_MIX_ORDER=flow: flow by flow); either way every row of every flow is covered exactly once."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    class E:
+        pass
+    e = E()
+    e.groups = {1: list(range(1658)), 2: list(range(1246)), 20: list(range(1192))}
+    e.sub = {1: 1156, 2: 898, 20: 420}
+    e.witness_size = {1: 2251704, 2: 2828764, 20: 5488453}
+    monkeypatch.delenv("PZK_MIX_ORDER", raising=False)
+    rr = bench.MixedGpuEngine._calls(e)
+    assert rr == [(20, 0), (2, 0), (1, 0), (20, 420), (2, 898), (1, 1156), (20, 840)]
+    monkeypatch.setenv("PZK_MIX_ORDER", "flow")
+    fl = bench.MixedGpuEngine._calls(e)
+    assert fl == [(1, 0), (1, 1156), (2, 0), (2, 898), (20, 0), (20, 420), (20, 840)]
+    for calls in (rr, fl):
+        for sg, idx in e.groups.items():
+            covered = sorted(r for g, a in calls if g == sg for r in range(a, min(a + e.sub[sg], len(idx))))
+            assert covered == idx

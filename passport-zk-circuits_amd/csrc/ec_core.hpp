@@ -960,11 +960,9 @@ __global__ void __launch_bounds__(ECT_NT) k_emit_ect(DevLayout L, const Work* wo
     for (int k = 0; k < TL; k++) tabv[ti[k]] = tv[k];  // clamped elements rewrite element 0 with its own value
     __syncthreads();
     const bool more_w = w + 1 < we;
-    if (more_w) {  // the next witness's table, behind this one's stores
-      const size_t nt = (size_t)(w + 1) * tab_stride;
+    const size_t nt = (more_w ? w + 1 : w) * tab_stride;  // the next witness's table behind this one's stores
 #pragma unroll
-      for (int k = 0; k < TL; k++) tv[k] = tab0[nt + ti[k]];
-    }
+    for (int k = 0; k < TL; k++) tv[k] = tab0[nt + ti[k]];
     const OutRow out = desc_run<MM>(L, wtns, stride, w, wk, g, o0_prog).out;
     for (uint32_t base = threadIdx.x; base < tot; base += step) {
 #pragma unroll

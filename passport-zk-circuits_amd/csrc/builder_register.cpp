@@ -86,17 +86,20 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   const int aa_hs = p.aa_signature_algo == 23 ? 192 : 248;
   // signature / pubkey input length: 2 x CHUNK_NUMBER for ECDSA (registerIdentityBuilder.circom:124-135)
   const int K = ecdsa ? 2 * EC_GEO[cv].nl : p.signature_type == 2 ? 64 : (p.signature_type == 14 || p.signature_type == 4) ? 48 : 32;
-  const int ecB = p.ec_block_number, d15B = p.dg15_block_number, ecLen = HBS * ecB, d15Len = HBS * d15B;
+  const int ecB = p.ec_block_number, d15B = p.dg15_block_number;
   const bool aa = p.aa_signature_algo != 0;
   if (ecB < 1 || ecB > 16 || d15B < 0 || d15B > 16 || (aa && d15B < 1)) { why = "block numbers out of range"; return false; }
+  const int ecLen = HBS * ecB, d15Len = HBS * d15B;
   if (HBS != DBS && d15B) {
     why = "dg15 block sizes differ: registerIdentityBuilder.circom:151 assigns dg15[DG15_BLOCK_NUMBER * HASH_BLOCK_SIZE] to "
           "RegisterIdentity's dg15[DG15_SIZE * DG_HASH_BLOCK_SIZE] (identity.circom:22)";
     return false;
   }
-  const int dg15shift = aa ? p.dg15_shift : DG;
-  if (p.dg1_shift < 0 || p.dg1_shift + DG > ecLen || dg15shift < 24 || dg15shift + DG > ecLen ||
-      p.ec_shift < 0 || p.ec_shift + HT > 1024 || (aa && p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len)) {
+  // (64-bit sums: the shifts are caller-supplied int32)
+  const int64_t dg15shift = aa ? p.dg15_shift : DG;
+  if (p.dg1_shift < 0 || (int64_t)p.dg1_shift + DG > ecLen || dg15shift < 24 || dg15shift + DG > ecLen ||
+      p.ec_shift < 0 || (int64_t)p.ec_shift + HT > 1024 ||
+      (aa && (p.aa_shift < 0 || (int64_t)p.aa_shift + (aa_ec ? 2 * aa_f : 1024) > d15Len))) {
     why = "shift parameters address bits outside the inputs";
     return false;
   }
@@ -199,7 +202,7 @@ bool build_register(const pzk_params& p, Layout& L, std::string& why) {
   sha_blocks(J_SA, IN_SA, 1024 / HBS);
   // PassportVerificationFlow(ecLen, DG, EHT, DG1_SHIFT, DG15_ACTUAL_SHIFT, EC_SHIFT, AA): 3 DG + 8 IsEqual
   b.region(RK_FLOW, 1 + 2 * DG + ecLen + EHT + 1024 + (3 * DG + 8) * (1 + SZ_ISEQUAL),
-           {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, dg15shift, p.ec_shift, p.aa_signature_algo});
+           {J_DG1, J_DG15, J_EC, J_SA, IN_EC, IN_SA, p.dg1_shift, (int32_t)dg15shift, p.ec_shift, p.aa_signature_algo});
   L.bjj_core_fr = BJJ_CORE_FR;
   L.smt_core_fr = SMT_CORE_FR;
   if (ecdsa) {

@@ -16,6 +16,7 @@
 #include "ec_common.hpp"
 #include "poseidon.hpp"
 #include "query_layout.hpp"
+#include "host_api.hpp"
 
 using namespace pzk;
 
@@ -126,8 +127,16 @@ struct Scratch {
   }
 };
 
-// scratch sets (pipeline depth): call k uses set k % NSETS and waits for call k - NSETS
-static constexpr int NSETS = 3;
+// PZK_POST=0 (A/B): the register call's chain-dependent emission stays behind the chain on the emitter streams
+// (rounds 1-4) instead of on its own post-chain stream
+static bool post_chain_split() {
+  static const bool v = !(getenv("PZK_POST") && atoi(getenv("PZK_POST")) == 0);
+  return v;
+}
+
+// scratch sets (pipeline depth): call k uses set k % nsets and waits for call k - nsets (nsets = 3, or
+// PZK_NSETS = 2..4 for A/B)
+static constexpr int NSETS = PIPELINE_SETS_MAX;  // capacity
 
 struct pzk_instance {
   pzk_params params;
@@ -166,13 +175,17 @@ struct pzk_instance {
   // cores can run while call k's emitters still read set k % 2
   Scratch scr[NSETS];
   uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
+  int nsets = 3;       // scratch sets in use (pipeline depth)
   // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit, tail, chain2)
-  static constexpr int NSTREAMS = 7;
+  static constexpr int NSTREAMS = 8;
   hipEvent_t ev_done[NSETS][NSTREAMS] = {};
   hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
   hipStream_t s_tail = nullptr;  // the small tail emitters (PZK_TAIL=own), so the next call's SHA emitter never queues behind them
   hipStream_t s_chain2 = nullptr, s_chain3 = nullptr;  // register calls: further SMT chain streams (PZK_SMT_CHAINS)
+  // register calls: the emission that reads the SMT chain's output (the SMT level Poseidon blocks, the SMT regions),
+  // one stream for every call so that a later call's writes of those regions follow an earlier call's
+  hipStream_t s_post = nullptr;
   uint64_t chain_rr = 0;           // register calls: SMT chain stream rotation
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
@@ -357,7 +370,7 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post})
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab,
                        I->ev_smt, I->ev_chain})
@@ -391,7 +404,7 @@ struct DeviceGuard {
 
 // wait until every stream of the instance has drained (all calls issued so far are complete)
 static int sync_all(pzk_instance* I) {
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
@@ -401,7 +414,7 @@ extern "C" {
 const char* pzk_last_error(void) { return g_err.c_str(); }
 const char* pzk_version(void) { return "pzkwit 0.2.0 (gfx950)"; }
 
-int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
+static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out) {
   if (!params || !out) return fail(PZK_E_ARG, "null argument");
   if (const char* u = getenv("PZK_SHA_U")) {  // tuning switch of the SHA emitter (kernels.hip)
     int v = atoi(u);
@@ -421,6 +434,7 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
     return fail(PZK_E_NODEVICE, "no HIP device visible: pzkwit has no CPU fallback");
   pzk_instance* I = new pzk_instance();
   I->params = *params;
+  I->nsets = nsets_env();
   std::string why;
   if (!build_layout(*params, I->lay, why)) { delete I; return fail(PZK_E_PARAMS, why); }
   HIPCHK(hipGetDevice(&I->device));
@@ -481,6 +495,8 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   // competes for the process's hardware queues
   if (ok && getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
     ok = hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_lo) == hipSuccess;
+  if (ok && I->lay.is_register && post_chain_split())
+    ok = hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
                         &I->ev_smt, &I->ev_chain})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -511,64 +527,7 @@ int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
   return 0;
 }
 
-// circom .sym text ("signal_idx,witness_idx,component_idx,name" per line; witness_idx -1 = eliminated)
-// -> inv[k] = O0 index of output witness element k (inv[0] = 0, the constant 1). Signal indices are the
-// --O0 numbering (1 .. o0_size - 1); witness indices must cover 1 .. max, each by one or
-// more signals (several signals on one index: the lowest signal index is emitted).
-static bool parse_sym(const char* text, size_t len, uint64_t o0_size, std::vector<uint32_t>& inv, std::string& why) {
-  std::vector<int64_t> w_of;  // witness index -> signal index
-  size_t i = 0;
-  uint64_t line = 0;
-  auto num = [&](int64_t& v) -> bool {
-    bool neg = false, any = false;
-    v = 0;
-    if (i < len && text[i] == '-') { neg = true; i++; }
-    while (i < len && text[i] >= '0' && text[i] <= '9') { v = v * 10 + (text[i] - '0'); i++; any = true; if (v > (1ll << 40)) return false; }
-    if (neg) v = -v;
-    return any;
-  };
-  while (i < len) {
-    line++;
-    if (text[i] == '\n' || text[i] == '\r') { i++; continue; }
-    int64_t sig, wit, comp;
-    if (!num(sig) || i >= len || text[i++] != ',' || !num(wit) || i >= len || text[i++] != ',' || !num(comp)) {
-      why = "sym line " + std::to_string(line) + ": expected signal_idx,witness_idx,component_idx,name";
-      return false;
-    }
-    while (i < len && text[i] != '\n') i++;
-    if (sig < 1 || (uint64_t)sig >= o0_size) {
-      why = "sym line " + std::to_string(line) + ": signal index " + std::to_string(sig) + " outside 1.." +
-            std::to_string(o0_size - 1);
-      return false;
-    }
-    if (wit == -1) continue;
-    if (wit < 1) { why = "sym line " + std::to_string(line) + ": bad witness index"; return false; }
-    if ((uint64_t)wit >= w_of.size()) w_of.resize(wit + 1, -1);
-    // circom's simplification can merge equal signals onto one witness index (snarkjs loadSymbols joins
-    // their names with '|'): they carry one value, so the lowest signal index stands for all of them
-    if (w_of[wit] == -1 || sig < w_of[wit]) w_of[wit] = sig;
-  }
-  if (w_of.size() < 2) { why = "sym: no signal is kept"; return false; }
-  inv.assign(w_of.size(), 0);
-  for (size_t k = 1; k < w_of.size(); k++) {
-    if (w_of[k] < 0) { why = "sym: witness index " + std::to_string(k) + " is not assigned"; return false; }
-    inv[k] = (uint32_t)w_of[k];
-  }
-  return true;
-}
-
-int pzk_sym_check(const pzk_params* params, const char* sym, size_t sym_len, uint64_t* witness_size) {
-  if (!params || !sym) return fail(PZK_E_ARG, "null argument");
-  Layout L;
-  std::string why;
-  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
-  std::vector<uint32_t> inv;
-  if (!parse_sym(sym, sym_len, L.wit_size, inv, why)) return fail(PZK_E_ARG, why);
-  if (witness_size) *witness_size = inv.size();
-  return 0;
-}
-
-int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t sym_len, pzk_instance** out) {
+static int pzk_instance_create_mapped_impl(const pzk_params* params, const char* sym, size_t sym_len, pzk_instance** out) {
   if (!params || !out) return fail(PZK_E_ARG, "null argument");
   if (!sym) return pzk_instance_create(params, out);
   pzk_instance* I = nullptr;
@@ -577,44 +536,19 @@ int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t
   std::vector<uint32_t> inv;
   std::string why;
   if (!parse_sym(sym, sym_len, I->lay.wit_size, inv, why)) { pzk_instance_destroy(I); return fail(PZK_E_ARG, why); }
-  bool monotone = true;
-  for (size_t k = 1; k < inv.size() && monotone; k++) monotone = inv[k] > inv[k - 1];
+  MapProgram mp;
   static const bool force_gather = getenv("PZK_SYM_GATHER") != nullptr;  // A/B: the staging + gather path
+  map_program(I->lay, inv, force_gather, mp);
   bool ok;
-  if (monotone && !force_gather) {
-    // direct emission: keep bitmap (+ 2 zero words past the end: a wave's window reads words i, i + 1)
-    const size_t nw = I->lay.wit_size / 64 + 3;
-    std::vector<uint64_t> bits(nw, 0);
-    std::vector<uint32_t> rank(nw, 0);
-    for (uint32_t g : inv) bits[g >> 6] |= 1ull << (g & 63);
-    for (size_t i = 1; i < nw; i++) rank[i] = rank[i - 1] + (uint32_t)__builtin_popcountll(bits[i - 1]);
-    ok = upload(&I->d_keep_bits, bits) == 0 && upload(&I->d_keep_rank, rank) == 0;
-    // descriptor-driven emitters (SHA-256 blocks, Poseidon blocks, EC table blocks): each work item's kept
-    // descriptors, compacted in O0 order, at Work.pad of the item (mapsink.hpp desc_run), so those emitters run
-    // their O0 store loop over the kept elements only
-    std::vector<uint32_t> mprog;
-    const Layout& lay = I->lay;
-    auto kept = [&](uint64_t g) { return (bits[g >> 6] >> (g & 63)) & 1; };
+  if (mp.direct) {
+    // direct emission (mapsink.hpp): keep bitmap + ranks, and the descriptor-driven work items' kept descriptors
+    ok = upload(&I->d_keep_bits, mp.bits) == 0 && upload(&I->d_keep_rank, mp.rank) == 0;
     for (int e : {E_SHA, E_SHAD, E_POS, E_ECT}) {
-      std::vector<Work> wl = lay.work[e];
-      for (Work& wk : wl) {
-        const Region& R = lay.regions[wk.region];
-        const uint32_t* src = nullptr;
-        const uint16_t* src16 = nullptr;
-        if (R.kind == RK_SHA_BLOCK) src = lay.sha_prog.data() + wk.start;
-        else if (R.kind == RK_POSEIDON) src16 = lay.pos_prog.data() + lay.pos_prog_off[lay.pos[R.a[0]].n + 1] + wk.start;
-        else if (R.kind == RK_ECT) src = lay.ec_prog.data() + lay.ec_prog_off[R.a[1]] + wk.start;
-        else continue;
-        wk.pad = (uint32_t)mprog.size();
-        for (uint32_t q = 0; q < wk.count; q++)
-          if (kept(R.off + wk.start + q)) mprog.push_back(src ? src[q] : src16[q]);
-      }
       if (I->d_work[e]) { (void)hipFree(I->d_work[e]); I->d_work[e] = nullptr; }
-      ok = ok && upload(&I->d_work[e], wl) == 0;
-      I->lay.work[e] = wl;
+      ok = ok && upload(&I->d_work[e], mp.work[e]) == 0;
+      I->lay.work[e] = mp.work[e];
     }
-    if (mprog.empty()) mprog.push_back(0);
-    ok = ok && upload(&I->d_mprog, mprog) == 0;
+    ok = ok && upload(&I->d_mprog, mp.mprog) == 0;
   } else {
     ok = upload(&I->d_map, inv) == 0;
   }
@@ -629,35 +563,7 @@ int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t
   return 0;
 }
 
-int pzk_layout_query(const pzk_params* params, pzk_info* info, uint32_t* n_regions) {
-  if (!params || !info) return fail(PZK_E_ARG, "null argument");
-  Layout L;
-  std::string why;
-  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
-  memset(info, 0, sizeof *info);
-  info->witness_size = L.wit_size;
-  info->n_inputs = L.n_inputs;
-  info->n_outputs = L.n_outputs;
-  info->n_public_inputs = L.n_public;
-  info->n_input_groups = (uint32_t)L.inputs.size();
-  info->pipeline_depth = NSETS;
-  if (n_regions) *n_regions = (uint32_t)L.regions.size();
-  return 0;
-}
-
-int pzk_layout_region(const pzk_params* params, uint32_t i, uint64_t* off, uint32_t* len, uint32_t* kind) {
-  if (!params) return fail(PZK_E_ARG, "null argument");
-  Layout L;
-  std::string why;
-  if (!build_layout(*params, L, why)) return fail(PZK_E_PARAMS, why);
-  if (i >= L.regions.size()) return fail(PZK_E_ARG, "region index out of range");
-  if (off) *off = L.regions[i].off;
-  if (len) *len = L.regions[i].len;
-  if (kind) *kind = L.regions[i].kind;
-  return 0;
-}
-
-void pzk_instance_destroy(pzk_instance* inst) {
+static void pzk_instance_destroy_impl(pzk_instance* inst) {
   if (!inst) return;
   {
     // calls are asynchronous across the instance's streams: wait for a concurrent caller to leave and
@@ -670,7 +576,7 @@ void pzk_instance_destroy(pzk_instance* inst) {
   delete inst;
 }
 
-int pzk_instance_info(const pzk_instance* I, pzk_info* info) {
+static int pzk_instance_info_impl(const pzk_instance* I, pzk_info* info) {
   if (!I || !info) return fail(PZK_E_ARG, "null argument");
   memset(info, 0, sizeof *info);
   info->witness_size = I->out_size;
@@ -678,11 +584,11 @@ int pzk_instance_info(const pzk_instance* I, pzk_info* info) {
   info->n_outputs = I->lay.n_outputs;
   info->n_public_inputs = I->lay.n_public;
   info->n_input_groups = (uint32_t)I->lay.inputs.size();
-  info->pipeline_depth = NSETS;
+  info->pipeline_depth = I->nsets;
   return 0;
 }
 
-int pzk_instance_input(const pzk_instance* I, uint32_t i, const char** name, uint64_t* offset, uint64_t* length) {
+static int pzk_instance_input_impl(const pzk_instance* I, uint32_t i, const char** name, uint64_t* offset, uint64_t* length) {
   if (!I || i >= I->lay.inputs.size()) return fail(PZK_E_ARG, "input index out of range");
   if (name) *name = I->lay.inputs[i].name.c_str();
   if (offset) *offset = I->lay.inputs[i].offset;
@@ -690,7 +596,7 @@ int pzk_instance_input(const pzk_instance* I, uint32_t i, const char** name, uin
   return 0;
 }
 
-int pzk_wtns_header(const pzk_instance* I, uint8_t h[76]) {
+static int pzk_wtns_header_impl(const pzk_instance* I, uint8_t h[76]) {
   if (!I || !h) return fail(PZK_E_ARG, "null argument");
   static const uint8_t prime[32] = {0x01, 0x00, 0x00, 0xf0, 0x93, 0xf5, 0xe1, 0x43, 0x91, 0x70, 0xb9,
                                     0x79, 0x48, 0xe8, 0x33, 0x28, 0x5d, 0x58, 0x81, 0x81, 0xb6, 0x45,
@@ -743,10 +649,10 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
 
 // One call, with the instance lock held and the device set.
 //
-// Pipelining: call k uses scratch set k % NSETS and four instance streams — main (the
+// Pipelining: call k uses scratch set k % nsets and four instance streams — main (the
 // Poseidon/SMT/BabyJubJub chain), rsa (the signature core), sha (the SHA emitters) and emit (the other
 // emitters). Streams are not joined at the end of a call: call k + 1's cores start while call k's
-// emitters still run. Before touching set k % NSETS again, call k + NSETS waits for the end of call k
+// emitters still run. Before touching set k % nsets again, call k + nsets waits for the end of call k
 // on all four streams (ev_done). With a caller stream the call is joined into it at exit (serialised).
 // dep: an instance stream whose work so far the call must follow (the input upload of pzk_witness_batch_host,
 // the staging-slot waits of batch_mapped). Every stream of the call descends from its chain stream st (the
@@ -754,7 +660,7 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
 // when a QueryIdentity call's chain runs on s_rsa or s_tail instead of the main stream.
 static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
                         int32_t* d_status, const pzk_exec* exec, hipStream_t dep = nullptr) {
-  const int set = (int)(I->calls % NSETS);
+  const int set = (int)(I->calls % I->nsets);
   Scratch& S = I->scr[set];
   int rc = ensure_scratch(I, S, batch);
   if (rc) return rc;
@@ -769,7 +675,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   static const int qry_chains = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 3;
   hipStream_t st = I->stream;
   if (I->lay.is_query && !serial && qry_chains > 1) {
-    const int c = qry_chains >= 3 ? set : set & 1;  // NSETS = 3 calls in flight
+    const int c = qry_chains >= 3 ? set % 3 : set & 1;  // nsets (3) calls in flight
     st = c == 0 ? I->stream : c == 1 ? I->s_rsa : I->s_tail;
   }
   for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(st, e, 0));
@@ -809,16 +715,23 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   };
   // one emitter's work items [a, b) (default: all) on stream s
   auto emit = [&](int e, hipStream_t s, uint32_t a = 0, uint32_t b = ~0u) -> int {
-    b = std::min<uint32_t>(b, (uint32_t)lay.work[e].size());
-    if (a >= b && e != E_POS) return 0;
+    if (e == E_POS) {
+      b = std::min<uint32_t>(b, (uint32_t)lay.pos_emit_groups.size());
+      if (a >= b) return 0;
+    } else {
+      b = std::min<uint32_t>(b, (uint32_t)lay.work[e].size());
+      if (a >= b) return 0;
+    }
     PhaseScope ps(lay.work[e].empty() ? nullptr : T, slot, EMIT_PHASE[e], s);
-    if (e != E_POS && (a != 0 || b != lay.work[e].size())) {
+    if (e != E_POS && (a != 0 || b != lay.work[e].size())) {  // a part of the work list
       HIPCHK(launch_emit(e, L, I->d_work[e] + a, b - a, K, bufs, B, lay.max_t, s));
       return 0;
     }
-    if (e == E_POS) {
-      for (const auto& g : lay.pos_emit_groups)
+    if (e == E_POS) {  // E_POS: [a, b) are pos_emit_groups
+      for (uint32_t gi = a; gi < std::min<uint32_t>(b, (uint32_t)lay.pos_emit_groups.size()); gi++) {
+        const auto& g = lay.pos_emit_groups[gi];
         HIPCHK(launch_emit(e, L, I->d_work[e] + g[1], g[2], K, bufs, B, (int)g[0], s));
+      }
     } else {
       HIPCHK(launch_emit(e, L, I->d_work[e], (uint32_t)lay.work[e].size(), K, bufs, B, lay.max_t, s));
     }
@@ -978,13 +891,27 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if (s_smt != st && smt_mode == 2) s_tail = s_smt;
     HIPCHK(hipStreamWaitEvent(s_bjj, I->ev_bjj, 0));
     if ((rc = emit(E_BJJ, s_bjj))) return rc;
+    // The emission that reads the chain's output — the SMT level Poseidon blocks (pos_emit_groups from
+    // pos_chain_group) and the SMT regions of E_GEN (work items from gen_chain_work) — goes to the post-chain stream
+    // (s_post, one for all calls, so a later call's writes of those regions follow an earlier call's). The emitter
+    // streams then never wait for the chain: with proofs of depth 1-79 (config 4) the chain of a 2048-witness call
+    // takes 35-48 ms beside the emitters, longer than the call period, and every emitter queued behind a wait for it
+    // idled (PZK_POST=0: the rounds 1-4 placement, everything behind the chain)
+    const bool post = I->s_post && !serial && s_smt != st;
+    const uint32_t pos_split = post ? lay.pos_chain_group : ~0u, gen_split = post ? lay.gen_chain_work : ~0u;
     HIPCHK(hipStreamWaitEvent(s_pos, I->ev_pos, 0));
-    if (s_smt != st && s_pos != s_smt) HIPCHK(hipStreamWaitEvent(s_pos, I->ev_chain, 0));  // SMT level images
-    if ((rc = emit(E_POS, s_pos))) return rc;
+    if (!post && s_smt != st && s_pos != s_smt) HIPCHK(hipStreamWaitEvent(s_pos, I->ev_chain, 0));  // SMT level images
+    if ((rc = emit(E_POS, s_pos, 0, pos_split))) return rc;
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_pos, 0));
     HIPCHK(hipStreamWaitEvent(s_tail, I->ev_rsa, 0));
-    if (s_smt != st && s_tail != s_smt) HIPCHK(hipStreamWaitEvent(s_tail, I->ev_chain, 0));  // SMT regions, status
-    if ((rc = emit(E_GEN, s_tail))) return rc;
+    if (!post && s_smt != st && s_tail != s_smt) HIPCHK(hipStreamWaitEvent(s_tail, I->ev_chain, 0));  // SMT regions
+    if ((rc = emit(E_GEN, s_tail, 0, gen_split))) return rc;
+    if (post) {
+      HIPCHK(hipStreamWaitEvent(I->s_post, I->ev_pos, 0));
+      HIPCHK(hipStreamWaitEvent(I->s_post, I->ev_chain, 0));
+      if ((rc = emit(E_POS, I->s_post, pos_split))) return rc;
+      if ((rc = emit(E_GEN, I->s_post, gen_split))) return rc;
+    }
     if ((rc = emit(E_FLOW, s_tail))) return rc;
     if (!lay.is_ecdsa) {
       PhaseScope ps(T, slot, PH_PREP, s_tail);
@@ -998,7 +925,8 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
   }
   hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, serial ? st : I->s_chain2,
-                                                 serial ? st : I->s_chain3 ? I->s_chain3 : I->s_chain2};
+                                                 serial ? st : I->s_chain3 ? I->s_chain3 : I->s_chain2,
+                                                 serial || !I->s_post ? st : I->s_post};
   for (int i = 0; i < pzk_instance::NSTREAMS; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));
@@ -1045,7 +973,7 @@ static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   pzk_exec ex{I->device, exec ? (exec->flags & PZK_EXEC_TIMING) : 0, nullptr};
   for (size_t lo = 0; lo < batch; lo += chunk) {
     const size_t n = std::min(chunk, batch - lo);
-    const int set = (int)(I->calls % NSETS), slot = (int)((lo / chunk) & 1);
+    const int set = (int)(I->calls % I->nsets), slot = (int)((lo / chunk) & 1);
     HIPCHK(hipStreamWaitEvent(I->stream, I->ev_gather[slot], 0));  // the gather two chunks back read this slot
     int rc = batch_locked(I, d_inputs + 32ull * I->lay.n_inputs * lo, n, I->d_o0[slot], o0_stride,
                           d_status ? d_status + lo : nullptr, &ex, I->stream);
@@ -1066,7 +994,7 @@ static int batch_mapped(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   return 0;
 }
 
-int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
+static int pzk_witness_batch_impl(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
                       int32_t* d_status, const pzk_exec* exec) {
   if (!I || !d_inputs || !d_wtns) return fail(PZK_E_ARG, "null argument");
   if (batch == 0) return 0;
@@ -1081,7 +1009,7 @@ int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, ui
   return batch_locked(I, d_inputs, batch, d_wtns, stride, d_status, exec);  // O0, or a monotone map emitted directly
 }
 
-int pzk_instance_sync(pzk_instance* I) {
+static int pzk_instance_sync_impl(pzk_instance* I) {
   if (!I) return fail(PZK_E_ARG, "null argument");
   std::lock_guard<std::mutex> lock(I->mu);
   DeviceGuard dg(I->device);
@@ -1089,7 +1017,7 @@ int pzk_instance_sync(pzk_instance* I) {
   return sync_all(I);
 }
 
-int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
+static int pzk_witness_batch_host_impl(pzk_instance* I, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
                            int32_t* h_status, const pzk_exec* exec) {
   if (!I || !h_inputs || !h_wtns) return fail(PZK_E_ARG, "null argument");
   if (batch == 0) return 0;
@@ -1130,7 +1058,7 @@ int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batc
 // calling thread hands chunk c - 1's pinned rows to the sink meanwhile. Chunk c + 2 reuses slot c % 2:
 // its upload waits for the device->host copy of chunk c (ev_d2h), and its copy down is issued only after
 // the sink of chunk c has returned.
-int pzk_witness_stream(pzk_instance* I, const uint8_t* h_inputs, size_t batch, size_t chunk, pzk_sink_fn sink,
+static int pzk_witness_stream_impl(pzk_instance* I, const uint8_t* h_inputs, size_t batch, size_t chunk, pzk_sink_fn sink,
                        void* user, const pzk_exec* exec) {
   if (!I || !h_inputs || !sink) return fail(PZK_E_ARG, "null argument");
   if (batch == 0) return 0;
@@ -1195,7 +1123,7 @@ int pzk_witness_stream(pzk_instance* I, const uint8_t* h_inputs, size_t batch, s
   return deliver(n_chunks - 1);
 }
 
-int pzk_timing(pzk_instance* I, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset) {
+static int pzk_timing_impl(pzk_instance* I, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset) {
   if (!I || !count) return fail(PZK_E_ARG, "null argument");
   for (int s = 0; s < Timing::RING; s++) I->timing.collect(s);
   uint32_t n = std::min<uint32_t>(*count, PH_COUNT);
@@ -1212,7 +1140,7 @@ int pzk_timing(pzk_instance* I, const char** names, double* ms, uint64_t* launch
   return 0;
 }
 
-int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, const char** kernel,
+static int pzk_phase_info_impl(const pzk_instance* I, uint32_t phase, const char** name, const char** kernel,
                    uint64_t* bytes_per_witness) {
   if (!I || phase >= PH_COUNT) return fail(PZK_E_ARG, "bad phase");
   if (name) *name = PHASE_NAMES[phase];
@@ -1268,6 +1196,60 @@ int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, con
     *bytes_per_witness = b;
   }
   return 0;
+}
+
+
+// ------------------------------------------------------------------ C-ABI entry points (guarded)
+int pzk_instance_create(const pzk_params* params, pzk_instance** out) {
+  return guarded([&] { return pzk_instance_create_impl(params, out); });
+}
+
+int pzk_instance_create_mapped(const pzk_params* params, const char* sym, size_t sym_len, pzk_instance** out) {
+  return guarded([&] { return pzk_instance_create_mapped_impl(params, sym, sym_len, out); });
+}
+
+void pzk_instance_destroy(pzk_instance* inst) {
+  (void)guarded([&] { pzk_instance_destroy_impl(inst); return 0; });
+}
+
+int pzk_instance_info(const pzk_instance* I, pzk_info* info) {
+  return guarded([&] { return pzk_instance_info_impl(I, info); });
+}
+
+int pzk_instance_input(const pzk_instance* I, uint32_t i, const char** name, uint64_t* offset, uint64_t* length) {
+  return guarded([&] { return pzk_instance_input_impl(I, i, name, offset, length); });
+}
+
+int pzk_wtns_header(const pzk_instance* I, uint8_t h[76]) {
+  return guarded([&] { return pzk_wtns_header_impl(I, h); });
+}
+
+int pzk_witness_batch(pzk_instance* I, const uint8_t* d_inputs, size_t batch, uint8_t* d_wtns, size_t stride,
+                      int32_t* d_status, const pzk_exec* exec) {
+  return guarded([&] { return pzk_witness_batch_impl(I, d_inputs, batch, d_wtns, stride, d_status, exec); });
+}
+
+int pzk_instance_sync(pzk_instance* I) {
+  return guarded([&] { return pzk_instance_sync_impl(I); });
+}
+
+int pzk_witness_batch_host(pzk_instance* I, const uint8_t* h_inputs, size_t batch, uint8_t* h_wtns,
+                           int32_t* h_status, const pzk_exec* exec) {
+  return guarded([&] { return pzk_witness_batch_host_impl(I, h_inputs, batch, h_wtns, h_status, exec); });
+}
+
+int pzk_witness_stream(pzk_instance* I, const uint8_t* h_inputs, size_t batch, size_t chunk, pzk_sink_fn sink,
+                       void* user, const pzk_exec* exec) {
+  return guarded([&] { return pzk_witness_stream_impl(I, h_inputs, batch, chunk, sink, user, exec); });
+}
+
+int pzk_timing(pzk_instance* I, const char** names, double* ms, uint64_t* launches, uint32_t* count, int reset) {
+  return guarded([&] { return pzk_timing_impl(I, names, ms, launches, count, reset); });
+}
+
+int pzk_phase_info(const pzk_instance* I, uint32_t phase, const char** name, const char** kernel,
+                   uint64_t* bytes_per_witness) {
+  return guarded([&] { return pzk_phase_info_impl(I, phase, name, kernel, bytes_per_witness); });
 }
 
 }  // extern "C"

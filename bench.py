@@ -48,21 +48,24 @@ def smt_depth_of(spec, i):
 def _gen_slice(args):
     seed, lo, hi, n_keys, sig = args[:5]
     depth = args[5] if len(args) > 5 else "0"
+    root = args[6] if len(args) > 6 else False
     from pzkwit import inputs as I
     g = I.PassportGen.shared(seed, n_keys, sig)
     out = np.zeros((hi - lo, g.n_inputs, 32), dtype=np.uint8)
     for k, i in enumerate(range(lo, hi)):
-        I.pack_register_inputs(g.passport_at(i, smt_depth=smt_depth_of(depth, i)), g.params, out=out[k])
+        I.pack_register_inputs(g.passport_at(i, smt_depth=smt_depth_of(depth, i), smt_root=root), g.params, out=out[k])
     return lo, out
 
 
-def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1, smt_depth="0"):
-    """Passports first .. first + batch - 1 of the synthetic stream, packed."""
+def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1, smt_depth="0", smt_root=False):
+    """Passports first .. first + batch - 1 of the synthetic stream, packed. smt_root: with deep
+    proofs, slaveMerkleRoot = the proof's root (Python Poseidon; config 4) instead of 0."""
     from pzkwit import inputs as I
     workers = workers or max(1, min(16, os.cpu_count() or 1))
     keys = I.PassportGen.shared(seed, n_keys, sig).keys  # keys generated once (parallel inside), handed to workers
     step = (batch + workers * 4 - 1) // (workers * 4)
-    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig, smt_depth) for lo in range(0, batch, step)]
+    jobs = [(seed, first + lo, first + min(batch, lo + step), n_keys, sig, smt_depth, smt_root)
+            for lo in range(0, batch, step)]
     n_in = I.PassportGen.shared(seed, n_keys, sig).n_inputs
     buf = np.zeros((batch, n_in, 32), dtype=np.uint8)
     if workers == 1:
@@ -77,9 +80,50 @@ def make_register_inputs(batch, first, seed=3, n_keys=64, workers=None, sig=1, s
 
 # ----------------------------------------------------------------------------- CPU baseline
 # workload -> SIGNATURE_TYPE of the RegisterIdentityBuilder instance, and its input seed
-WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21}
+WL_SIG = {"register": 1, "register-ecdsa": 20, "register-pss": 11, "register-brainpool": 21, "config4": 1}
 SIG_SEED = {1: 3, 2: 4, 3: 11, 4: 12, 10: 6, 11: 7, 12: 8, 13: 13, 14: 10, 20: 5, 21: 9, 24: 14, 25: 15}
 CPU_SHARE = 16  # host CPUs a one-GPU job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
+# the canonical instance, seed 0x4, SMT proofs of depth uniform in 1..79 (non-zero siblings
+# below the depth, zeros above), slaveMerkleRoot = the proof's root
+CONFIG4 = {"seed": 4, "smt_depth": "1-79"}
+CONFIG4_WORKLOAD = ("RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports, SMT proofs of depth "
+                    "1-79 (config 4, seed 0x4)")
+# PoseidonHash(2) of the KATs (0,0), (1,2), (p-1,p-1) and 1,000 pairs from SplitMix64 seed 0x1
+POSEIDON_BATCH = 1 << 20
+
+
+def register_like(workload):
+    return workload.startswith("register") or workload == "config4"
+
+
+def workload_seed(args):
+    return CONFIG4["seed"] if args.workload == "config4" else SIG_SEED[args.sig_eff]
+
+
+def workload_depth(args):
+    depth = getattr(args, "smt_depth", "0")
+    if args.workload == "config4" and depth == "0":
+        return CONFIG4["smt_depth"]
+    return depth
+
+
+def poseidon_config1_pairs():
+    """Config 1's 1,003 input pairs (the order of tools/gen_poseidon_kats.js)."""
+    from pzkwit import field
+    pairs = [(0, 0), (1, 2), (field.P - 1, field.P - 1)]
+    rng = field.SplitMix64(1)
+    pairs += [(rng.fr(), rng.fr()) for _ in range(1000)]
+    return pairs
+
+
+def poseidon_rows(n):
+    """n input rows of PoseidonHash(2): config 1's pairs, repeated. -> (n, 2, 32) uint8"""
+    pairs = poseidon_config1_pairs()
+    uniq = np.zeros((len(pairs), 2, 32), dtype=np.uint8)
+    for i, (a, b) in enumerate(pairs):
+        uniq[i, 0] = np.frombuffer(a.to_bytes(32, "little"), dtype=np.uint8)
+        uniq[i, 1] = np.frombuffer(b.to_bytes(32, "little"), dtype=np.uint8)
+    return uniq[np.arange(n) % len(pairs)]
 
 
 def _cpu_work(args):
@@ -93,6 +137,10 @@ def _cpu_work(args):
         w = np.zeros((nw, 32), dtype=np.uint8)
         for r in rows:
             pyoracle.register_witness(prm, r, out=w)
+    elif kind == "poseidon":
+        for r in rows:
+            rc, _ = pyoracle.poseidon_witness([int.from_bytes(bytes(e), "little") for e in r])
+            assert rc == 0
     elif kind.startswith("query"):
         td1 = kind == "query-td1"
         w = np.zeros((pyoracle.query_sizes(td1)[1], 32), dtype=np.uint8)
@@ -151,10 +199,11 @@ class GpuEngine:
         from pzkwit import native, inputs as I
         self.torch, self.dev = torch, dev
         self.layout = "O0 (all signals)"
-        if workload.startswith("register") or workload.startswith("query"):
-            if workload.startswith("register"):
+        self.layout_key = args.sym if getattr(args, "sym", None) else "O0"  # PMC pass lookup (pmc_pass)
+        if register_like(workload) or workload.startswith("query"):
+            if register_like(workload):
                 circuit, size_arg, params = native.PZK_CIRCUIT_REGISTER, 0, I.instance_params(args.sig_eff)
-                n_in = I.PassportGen.shared(SIG_SEED[args.sig_eff], 64, args.sig_eff).n_inputs
+                n_in = I.PassportGen.shared(workload_seed(args), 64, args.sig_eff).n_inputs
                 shape = {1: "register_canonical", 20: "register_sig20"}.get(args.sig_eff)
             else:
                 circuit, size_arg, params = native.PZK_CIRCUIT_QUERY, 80, {"doc": 1 if workload == "query-td1" else 0}
@@ -195,6 +244,8 @@ class GpuEngine:
             if workload.startswith("query"):
                 self.layout += ("; BabyPbk (identityStateVerifier.circom:19, undefined in the snapshot) substituted by "
                                 "the reference's BabyjubjubBase8Multiplication (DESIGN.md §11)")
+        elif workload == "poseidon":
+            self.inst = native.Instance(native.PZK_CIRCUIT_POSEIDON, 2)
         else:
             self.inst = native.Instance(native.PZK_CIRCUIT_SHA256, 6)
         self.W, self.NIN = self.inst.witness_size, self.inst.n_inputs
@@ -240,42 +291,99 @@ class GpuEngine:
         return st, pub
 
 
+def host_rows(args, workload, n, world):
+    """Rank 0: the whole job's input rows of a workload on the host. -> (n, NIN, 32) uint8"""
+    from pzkwit import inputs as I
+    workers = max(1, min(CPU_SHARE * world, os.cpu_count() or 1))
+    if workload == "config4":
+        return make_register_inputs(n, 0, seed=CONFIG4["seed"], sig=1, workers=workers, smt_depth=CONFIG4["smt_depth"],
+                                    smt_root=True)
+    if register_like(workload):
+        return make_register_inputs(n, 0, seed=workload_seed(args), sig=args.sig_eff, workers=workers,
+                                    smt_depth=workload_depth(args), smt_root=args.workload == "config4")
+    if workload.startswith("query"):
+        from pzkwit import query as Q
+        return Q.batch_rows(n, seed=0x9, distinct=64, td1=workload == "query-td1")
+    if workload == "poseidon":
+        return poseidon_rows(n)
+    _, host = I.sha256_config2_batch(n, seed=2, blocks=6)
+    return host
+
+
+def scatter_rows(d_in, full, dist, dev):
+    """Shard r of the job's rows (rank 0's host tensor [world, shard bytes]) into rank r's device buffer."""
+    if dist is None:
+        d_in.copy_(full[0])
+    else:
+        parts = list(full.to(dev).unbind(0)) if full is not None else None
+        dist.scatter(d_in, parts, src=0)
+        del parts
+
+
+def timed_steps(engine, args, dist):
+    """W untimed warmup steps, then exactly K timed steps between barriers + device synchronisation.
+    -> (seconds, lanes failing in the timed steps)"""
+    for _ in range(args.warmup):
+        engine.step(0, False)
+    engine.sync()
+    if hasattr(engine.inst, "timing"):
+        engine.inst.timing(reset=True)
+    if dist:
+        dist.barrier()
+    engine.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        engine.step(k, True)
+    engine.sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    bad = int((engine.statuses(args.steps) != 0).sum().item())
+    return dt, bad
+
+
+def reduce_run(dist, dev, dt, bad):
+    """max of the timed seconds and sum of the failing lanes over ranks"""
+    if not dist:
+        return dt, bad
+    import torch
+    tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    bt = torch.tensor([bad], device=dev, dtype=torch.int64)
+    dist.all_reduce(bt)
+    return float(tt.item()), int(bt.item())
+
+
+def wants_config4(args):
+    """The default register line also measures config 4 on the same instance, reported beside the
+    headline config-3 value (`config4` key)."""
+    return (args.workload == "register" and args.sig_eff == 1 and getattr(args, "smt_depth", "0") == "0"
+            and not getattr(args, "sym", None) and not getattr(args, "no_config4", False))
+
+
 def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"):
     """One rank of the bench (also driven by tests/test_host.py over gloo with a stub engine).
 
     Rank 0 generates the whole job's inputs on the host, ranks receive their contiguous shard from
     it over the process group (RCCL point-to-point scatter on GPUs), run W + K steps, and the
-    per-lane status + public signals are all-gathered after the timed region. Returns the JSON
-    record on rank 0."""
+    per-lane status + public signals are all-gathered after the timed region. The default register line then
+    runs config 4's inputs through the same instance the same way. Returns the record for rank 0's report."""
     import torch
-    from pzkwit import dist as D, inputs as I
+    from pzkwit import dist as D
     dev = torch.device(device, local) if device == "cuda" else torch.device(device)
-    register = args.workload.startswith("register")
-    batch = args.batch or (4096 if register or args.workload.startswith("query") else 1024)
+    register = register_like(args.workload)
+    batch = args.batch or (4096 if register or args.workload.startswith("query")
+                           else POSEIDON_BATCH if args.workload == "poseidon" else 1024)
     engine = engine_cls(args, args.workload, dev)
     NIN, W = engine.NIN, engine.W
     # inputs: rank 0 makes all world x batch rows, scatters shard r to rank r
     t0 = time.time()
     full = None
     if rank == 0:
-        workers = max(1, min(CPU_SHARE * world, os.cpu_count() or 1))
-        if register:
-            host = make_register_inputs(batch * world, 0, seed=SIG_SEED[args.sig_eff], sig=args.sig_eff,
-                                        workers=workers, smt_depth=getattr(args, "smt_depth", "0"))
-        elif args.workload.startswith("query"):
-            from pzkwit import query as Q
-            host = Q.batch_rows(batch * world, seed=0x9, distinct=64, td1=args.workload == "query-td1")
-        else:
-            _, host = I.sha256_config2_batch(batch * world, seed=2, blocks=6)
-        full = torch.from_numpy(host.reshape(world, -1))
+        full = torch.from_numpy(host_rows(args, args.workload, batch * world, world).reshape(world, -1))
         log("inputs: %d x %d rows generated on rank 0 in %.1fs" % (world, batch, time.time() - t0))
     d_in = torch.empty(batch * NIN * 32, dtype=torch.uint8, device=dev)
-    if dist is None:
-        d_in.copy_(full[0])
-    else:
-        parts = list(full.to(dev).unbind(0)) if rank == 0 else None
-        dist.scatter(d_in, parts, src=0)
-        del parts
+    scatter_rows(d_in, full, dist, dev)
     del full
 
     stride = 32 * W
@@ -302,37 +410,31 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
         W, stride / 1e6, batch, sub, slots, slots * sub * stride / 1e9))
     engine.setup(d_in, batch, sub, slots, args.steps)
 
-    for _ in range(args.warmup):
-        engine.step(0, False)
-    engine.sync()
-    if hasattr(engine.inst, "timing"):
-        engine.inst.timing(reset=True)
-    if dist:
-        dist.barrier()
-    engine.sync()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        engine.step(k, True)
-    engine.sync()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    bad = int((engine.statuses(args.steps) != 0).sum().item())  # lanes failing in the TIMED steps
+    dt, bad = timed_steps(engine, args, dist)
+    timing = engine.inst.timing() if hasattr(engine.inst, "timing") else None
     st, pub = engine.public_pass()
+    dt, bad = reduce_run(dist, dev, dt, bad)
     if dist:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        bt = torch.tensor([bad], device=dev, dtype=torch.int64)
-        dist.all_reduce(bt)
-        bad = int(bt.item())
         st, pub = D.gather_results(dist, st, pub, device=dev)
     import hashlib
     gathered = {"witnesses": int(st.shape[0]), "status_nonzero": int((st != 0).sum().item()),
                 "public_signals": int(pub.shape[1]),
                 "public_sha256": hashlib.sha256(pub.cpu().numpy().tobytes()).hexdigest()[:16]}
+    c4 = None
+    if wants_config4(args):
+        t0 = time.time()
+        full = None
+        if rank == 0:
+            full = torch.from_numpy(host_rows(args, "config4", batch * world, world).reshape(world, -1))
+            log("config 4 inputs: %d x %d rows generated on rank 0 in %.1fs" % (world, batch, time.time() - t0))
+        scatter_rows(d_in, full, dist, dev)
+        del full
+        engine.sync()
+        d4, b4 = reduce_run(dist, dev, *timed_steps(engine, args, dist))
+        t4 = engine.inst.timing() if hasattr(engine.inst, "timing") else None
+        c4 = dict(dt=d4, bad=b4, timing=t4)
     return dict(dt=dt, bad=bad, batch=batch, sub=sub, slots=slots, W=W, NIN=NIN, engine=engine,
-                gathered=gathered)
+                gathered=gathered, timing=timing, config4=c4)
 
 
 # ----------------------------------------------------------------------------- main
@@ -341,7 +443,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "sha256", "mixed", "query", "query-td1"], default="register")
+    ap.add_argument("--workload", choices=["register", "register-ecdsa", "register-pss", "register-brainpool", "config4",
+                                           "sha256", "poseidon", "mixed", "query", "query-td1"], default="register")
     ap.add_argument("--sig", type=int, default=None, help="SIGNATURE_TYPE of a register workload (overrides --workload's)")
     ap.add_argument("--batch", type=int, default=None, help="witnesses per GPU per step")
     ap.add_argument("--sub", type=int, default=None, help="sub-batch (output slot) size")
@@ -350,6 +453,8 @@ def main():
                     "committed circom-shaped maps), or synthetic[:N]")
     ap.add_argument("--smt-depth", default="0", help="register workloads: SMT proof depth of the synthetic "
                     "passports, N or A-B (uniform); default 0 (a one-leaf registration tree)")
+    ap.add_argument("--no-config4", action="store_true", help="default register line: skip the embedded config-4 "
+                    "measurement")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
@@ -360,10 +465,18 @@ def main():
         # environment sets) the flows' streams share queues and serialise behind each other (40.9k -> 43.2k
         # witnesses/s at 16, profiles/r4_hwq/); set before any HIP call, inherited by the ranks launch_ranks starts
         # (PZK_MIX_HWQ=keep leaves the environment's value)
-        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PZK_MIX_HWQ", "16")
+        hwq = os.environ.get("PZK_MIX_HWQ", "16")
+        if not hwq.isdigit() or not 1 <= int(hwq) <= 32:
+            raise SystemExit("PZK_MIX_HWQ=%s: expected an integer 1..32 (hardware queues per process) or 'keep'" % hwq)
+        if os.environ.get("GPU_MAX_HW_QUEUES") != hwq:
+            log("mixed workload: GPU_MAX_HW_QUEUES %s -> %s (PZK_MIX_HWQ; 'keep' leaves it)"
+                % (os.environ.get("GPU_MAX_HW_QUEUES", "unset"), hwq))
+        os.environ["GPU_MAX_HW_QUEUES"] = hwq
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus)  # before torch / any GPU call
-    args.sig_eff = (args.sig or WL_SIG[args.workload]) if args.workload.startswith("register") else 0
+    args.sig_eff = (args.sig or WL_SIG[args.workload]) if register_like(args.workload) else 0
+    if args.workload == "config4" and args.sig not in (None, 1):
+        raise SystemExit("--workload config4 is SIGNATURE_TYPE 1 (SURVEY.md §8d)")
     if args.workload == "mixed":
         return bench_mixed(args)
 
@@ -385,9 +498,12 @@ def main():
         dist.destroy_process_group()
 
 
-def report(args, r, world):
+def workload_name(args):
+    """(metric, config.workload) of the line"""
     from pzkwit import inputs as I
     sig = args.sig_eff
+    if args.workload == "config4":
+        return "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline", CONFIG4_WORKLOAD
     if args.workload.startswith("register"):
         metric = "registerIdentityBuilder witnesses/sec, batch=4096, 1 & 8 MI355X; % HBM roofline"
         workload = "RegisterIdentityBuilder(1,256,3,4,600,248,1,1496,3,256) synthetic passports (config 3)"
@@ -406,18 +522,62 @@ def report(args, r, world):
             workload = "RegisterIdentityBuilder(%d,%d,%d,%d,%d,%d,%d,%d,%d,%d) synthetic passports" % tuple(
                 q[k] for k in ("sig", "dg_hash", "doc", "ec_blocks", "ec_shift", "dg1_shift", "aa", "dg15_shift",
                                "dg15_blocks", "aa_shift"))
-    elif args.workload.startswith("query"):
+        if getattr(args, "smt_depth", "0") != "0":
+            workload = workload.replace(" (config 3)", "") + ", SMT proofs of depth %s" % args.smt_depth
+        return metric, workload
+    if args.workload.startswith("query"):
         td1 = args.workload == "query-td1"
-        metric = "QueryIdentity%s(80) witnesses/sec, batch=4096 (SURVEY.md row f4)" % ("TD1" if td1 else "")
-        workload = "QueryIdentity%s(80) synthetic queries (64 distinct, SMT proofs of depth 0-79)" % ("TD1" if td1 else "")
-    else:
-        metric = "Sha256HashChunks(6) witnesses/sec, batch=1024 (config 2)"
-        workload = "Sha256HashChunks(6) synthetic 312-375 B messages (config 2)"
+        return ("QueryIdentity%s(80) witnesses/sec, batch=4096 (SURVEY.md row f4)" % ("TD1" if td1 else ""),
+                "QueryIdentity%s(80) synthetic queries (64 distinct, SMT proofs of depth 0-79)" % ("TD1" if td1 else ""))
+    if args.workload == "poseidon":
+        return ("PoseidonHash(2) witnesses/sec (config 1)",
+                "PoseidonHash(2) of config 1's 1,003 input pairs (KATs (0,0), (1,2), (p-1,p-1) + 1,000 SplitMix64 "
+                "seed 0x1 pairs), repeated to the batch")
+    return ("Sha256HashChunks(6) witnesses/sec, batch=1024 (config 2)",
+            "Sha256HashChunks(6) synthetic 312-375 B messages (config 2)")
+
+
+def pmc_pass(workload, layout_key):
+    """The committed PMC pass of a workload + layout (profiles/pmc_*/traffic.json, tools/pmc_summary.py): the last
+    one in name order, or None"""
+    found = None
+    for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
+        tj = json.load(open(tf))
+        if tj.get("workload") == workload and tj.get("layout_key", "O0") == layout_key:
+            found = (tf, tj)
+    return found
+
+
+def valu_roofline(tj, tf, value, world):
+    """whole-job VALU roofline: wave-level VALU instructions per witness (SQ_INSTS_VALU summed over the job's
+    kernels, from the committed PMC pass of this workload) x witnesses/s against the chip's VALU issue rate"""
+    if not tj or not tj.get("valu_insts_per_witness"):
+        return None
+    ipw = tj["valu_insts_per_witness"]
+    ach = ipw * value / 1e9
+    top = sorted(((v.get("valu_insts_per_witness", 0), k) for k, v in tj["kernels"].items()), reverse=True)[:3]
+    return {"bound": "valu", "insts_per_witness": ipw, "achieved": round(ach, 1), "peak": VALU_PEAK_GIPS,
+            "unit": "G wave-instr/s", "frac": round(ach / (VALU_PEAK_GIPS * world), 4),
+            "top_kernels": {k: v for v, k in top}, "source": os.path.relpath(tf, REPO),
+            "note": "issue-rate bound (1 wave64 VALU instruction / 2 cycles / SIMD at 2.4 GHz); 64-bit "
+                    "integer multiply-adds take more than one issue slot, so the attainable fraction is < 1"}
+
+
+def phase_table(tm, info):
+    return {p: {"ms_per_launch": round(tm[p][0] / max(tm[p][1], 1), 4), "launches": tm[p][1],
+                "kernel": info[p][0], "alg_bytes_per_witness": info[p][1]} for p in tm if tm[p][1]}
+
+
+def report(args, r, world):
+    from pzkwit import inputs as I
+    sig = args.sig_eff
+    metric, workload = workload_name(args)
     dt, batch, sub, W, NIN, inst = r["dt"], r["batch"], r["sub"], r["W"], r["NIN"], r["engine"].inst
     value = batch * world * args.steps / dt
+    layout_key = getattr(r["engine"], "layout_key", "O0")
 
     # roofline of the dominant kernel (HIP events on the launch stream, inside the timed region)
-    tm = inst.timing()
+    tm = r.get("timing") or inst.timing()
     info = {n: (k, b) for n, k, b in inst.phase_info()}
     # the dominant kernel = the one carrying the most algorithmic bytes (k_emit_sha: ~75 % of the witness)
     dom = max((p for p in tm if tm[p][1] > 0), key=lambda p: info[p][1])
@@ -426,49 +586,33 @@ def report(args, r, world):
     # launches cover ragged sub-batches: bytes per launch = bytes of all timed witnesses / launches
     bytes_per_launch = info[dom][1] * batch * args.steps / launches
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
+    # PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per witness, tools/pmc_summary.py) from the committed pass of the
+    # workload and layout this line measures; none -> null
     traffic, traffic_src = None, None
-    # PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per witness, tools/pmc_summary.py) committed under
-    # profiles/pmc_*/traffic.json for the workload this line measures; none -> null
-    for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
-        if not r["engine"].layout.startswith("O0"):
-            break  # the committed PMC passes measured the O0 layout
-        tj = json.load(open(tf))
+    pm = pmc_pass(workload, layout_key)
+    tf, tj = pm if pm else (None, None)
+    if tj:
         ks = [tj["kernels"].get(k) for k in info[dom][0].split("+")]
-        if tj.get("workload") == workload and all(ks):
+        if all(ks):
             traffic = sum(k["traffic_bytes_per_witness"] for k in ks) * batch * args.steps / launches
             traffic_src = os.path.relpath(tf, REPO)
     # whole-job algorithmic bytes: inputs read once + .wtns header and elements written once
     job_bytes = 32 * NIN + 76 + 32 * W
     job_gbs = value * job_bytes / 1e9
-    # whole-job VALU roofline: wave-level VALU instructions per witness (SQ_INSTS_VALU summed over the job's kernels,
-    # from the committed PMC pass of this workload) x witnesses/s against the chip's VALU issue rate
-    valu = None
-    for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*", "traffic.json"))):
-        if not r["engine"].layout.startswith("O0"):
-            break
-        tj = json.load(open(tf))
-        if tj.get("workload") == workload and tj.get("valu_insts_per_witness"):
-            ipw = tj["valu_insts_per_witness"]
-            ach = ipw * value / 1e9
-            top = sorted(((v.get("valu_insts_per_witness", 0), k) for k, v in tj["kernels"].items()), reverse=True)[:3]
-            valu = {"bound": "valu", "insts_per_witness": ipw, "achieved": round(ach, 1), "peak": VALU_PEAK_GIPS,
-                    "unit": "G wave-instr/s", "frac": round(ach / (VALU_PEAK_GIPS * world), 4),
-                    "top_kernels": {k: v for v, k in top}, "source": os.path.relpath(tf, REPO),
-                    "note": "issue-rate bound (1 wave64 VALU instruction / 2 cycles / SIMD at 2.4 GHz); 64-bit "
-                            "integer multiply-adds take more than one issue slot, so the attainable fraction is < 1"}
-    phases = {p: {"ms_per_launch": round(tm[p][0] / max(tm[p][1], 1), 4), "launches": tm[p][1],
-                  "kernel": info[p][0], "alg_bytes_per_witness": info[p][1]} for p in tm if tm[p][1]}
+    valu = valu_roofline(tj, tf, value, world)
     out = {
         "metric": metric, "value": round(value, 2), "unit": "witnesses/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bn254_fr (u32 limbs)",
         "data": "synthetic",
         "config": {"workload": workload, "batch_per_gpu": batch, "sub_batch": sub, "output_slots": r["slots"],
                    "output": "device-resident generation: each sub-batch's .wtns rows are written to HBM into a "
                              "ring of output slots that the next sub-batches overwrite (a 4096 batch of 72 MB "
                              "witnesses exceeds one GPU's HBM); host delivery is not in the timed region",
                    "witness_elements": W, "witness_bytes": 32 * W, "layout": r["engine"].layout,
-                   "smt_depth": getattr(args, "smt_depth", "0") if args.workload.startswith("register") else None,
+                   "layout_key": layout_key,
+                   "smt_depth": workload_depth(args) if register_like(args.workload) else None,
                    "parallelism": "shard%d" % world, "invalid_lanes": r["bad"], "gathered": r["gathered"]},
         "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -477,23 +621,43 @@ def report(args, r, world):
                      "job_bound": ("valu" if valu and valu["frac"] > job_gbs / (HBM_PEAK_GBS * world) else "hbm")},
         "job_hbm": {"alg_bytes_per_witness": job_bytes, "achieved": round(job_gbs, 1), "unit": "GB/s",
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},
-        "phases": phases,
+        "phases": phase_table(tm, info),
     }
-    if world == 1 and not args.no_host and args.workload.startswith("register"):
+    c4 = r.get("config4")
+    if c4:
+        v4 = batch * world * args.steps / c4["dt"]
+        g4 = v4 * job_bytes / 1e9
+        pm4 = pmc_pass(CONFIG4_WORKLOAD, "O0")
+        out["config4"] = {
+            "what": "SURVEY.md §8d config 4 on the same instance and sub-batching, measured after the headline line "
+                    "(W warmup + K timed steps of its own inputs; the driver's 8-GPU run shards it 8 x %d)" % batch,
+            "workload": CONFIG4_WORKLOAD, "value": round(v4, 2), "unit": "witnesses/s", "n_gpus": world,
+            "ms_per_step": round(c4["dt"] / args.steps * 1e3, 3), "smt_depth": CONFIG4["smt_depth"],
+            "seed": "0x%x" % CONFIG4["seed"], "slave_merkle_root": "the proof's root (Python Poseidon)",
+            "invalid_lanes": c4["bad"],
+            "job_hbm": {"achieved": round(g4, 1), "unit": "GB/s", "frac": round(g4 / (HBM_PEAK_GBS * world), 4)},
+            "valu": valu_roofline(pm4[1], pm4[0], v4, world) if pm4 else None,
+            "phases": phase_table(c4["timing"], info) if c4.get("timing") else None}
+    if world == 1 and not args.no_host and register_like(args.workload):
         out["host_delivered"] = host_delivered(args, r["engine"].inst, sig)
-    if world == 1 and not args.no_cpu and args.workload.startswith("register") and sig in (1, 3, 10, 11, 12, 20, 21, 24, 25):
+    if world == 1 and not args.no_cpu and register_like(args.workload) and sig in (1, 3, 10, 11, 12, 20, 21, 24, 25):
         out["input_side"] = input_side(sig)
     if world == 1 and not args.no_cpu:  # CPU baseline: N = 1 only (bounded sample)
         procs = max(1, min(CPU_SHARE, os.cpu_count() or 1))
-        if args.workload.startswith("register"):
+        if register_like(args.workload):
             ns = args.cpu_sample or (48 if sig >= 20 else 96 if sig == 11 else 128) * procs
-            rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=SIG_SEED[sig], sig=sig)
+            rows = make_register_inputs(ns, 10 ** 6, workers=procs, seed=workload_seed(args), sig=sig,
+                                        smt_depth=workload_depth(args))
             kind = "register:%d" % sig
         elif args.workload.startswith("query"):
             from pzkwit import query as Q
             ns = args.cpu_sample or 64 * procs
             rows = Q.batch_rows(ns, seed=99, distinct=64, td1=args.workload == "query-td1")
             kind = args.workload
+        elif args.workload == "poseidon":
+            ns = args.cpu_sample or 1003 * 4 * procs
+            rows = poseidon_rows(ns)
+            kind = "poseidon"
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)
@@ -505,15 +669,27 @@ def report(args, r, world):
             affinity = len(os.sched_getaffinity(0))
         except AttributeError:
             affinity = os.cpu_count()
+        nproc = os.cpu_count() or 1
         out["cpu_baseline"] = {
             "value": round(v, 2), "unit": "witnesses/s", "cores": procs, "kind": "port",
             "sample": "%d witnesses of the same workload on %d processes (%.1fs wall); the C oracle "
                       "(oracle/witness_oracle.c, a test-grade restatement; the reference's WASM calculator "
                       "cannot be built or run here)" % (ns, procs, cdt),
             "value_1thread": round(v1, 2), "sample_1thread": "%d witnesses, 1 process (%.1fs)" % (n1, cdt1),
-            "host_cpus": os.cpu_count(), "host_cpus_affinity": affinity,
-            "cores_note": "%d = the host CPU share of a one-GPU job on the GPU box (its OMP_NUM_THREADS); "
-                          "the box's nproc counts the whole machine" % CPU_SHARE}
+            "host_cpus": nproc, "host_cpus_affinity": affinity,
+            # all host cores: one witness per process, no shared state, so the rate scales with
+            # processes (16 processes give 14.9-15.2x the 1-thread rate in rounds 1-4); the box allows a one-GPU job
+            # 16 busy CPUs, so the nproc-wide figure is the 16-process rate scaled, not a run on every core
+            "value_nproc_scaled": round(v * nproc / procs, 2),
+            "cores_note": "cores = %d, the host CPU share of a one-GPU job on the GPU box (its OMP_NUM_THREADS); "
+                          "value_nproc_scaled = value x %d / %d (the box's nproc), an extrapolation: the pool does "
+                          "not allow a one-GPU job to occupy every host core" % (CPU_SHARE, nproc, procs)}
+        if args.workload == "poseidon":
+            jf = os.path.join(REPO, "profiles", "r5_config1", "poseidon_js.json")
+            if os.path.exists(jf):
+                js = json.load(open(jf))
+                out["cpu_baseline"]["reference_js"] = {
+                    k: js.get(k) for k in ("value", "unit", "cores", "sample", "node", "measured_on")}
     return out
 
 

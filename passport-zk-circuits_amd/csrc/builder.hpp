@@ -33,6 +33,10 @@ struct Layout {
   std::vector<uint16_t> pos_prog;    // Poseidon block programs, t = 2..6 (pos_prog.hpp)
   uint32_t pos_prog_off[POS_MAX_T + 1] = {};
   std::vector<std::array<uint32_t, 3>> pos_emit_groups;  // (t, first work, works) of work[E_POS]
+  // emission that reads the SMT chain's output (k_smt_chain): the SMT level Poseidon blocks are the groups
+  // [pos_chain_group, end) of pos_emit_groups, the SMT regions of E_GEN the work items [gen_chain_work, end); the
+  // rest of both emitters can run before the chain ends (register runtime: the post-chain stream)
+  uint32_t pos_chain_group = 0, gen_chain_work = 0;
   std::vector<ShaJob> sha;
   uint32_t sha_core_words = 0;
   std::vector<PosTask> pos;            // sorted by level, then t

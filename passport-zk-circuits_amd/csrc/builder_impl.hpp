@@ -182,32 +182,55 @@ struct Builder {
       L.work[e].swap(keep);
       L.work[ed].swap(later);
     }
-    // Poseidon emission: one launch per width t, each with the LDS its image needs
+    // Poseidon emission: one launch per width t, each with the LDS its image needs; the SMT level blocks (their core
+    // state comes from the SMT chain) last, in groups of their own
     {
       auto t_of = [&](const Work& w) { return L.pos[L.regions[w.region].a[0]].n + 1; };
+      auto chain_of = [&](const Work& w) { return L.pos[L.regions[w.region].a[0]].smt_level >= 0 ? 1 : 0; };
       std::vector<Work>& pw = L.work[E_POS];
-      std::stable_sort(pw.begin(), pw.end(), [&](const Work& x, const Work& y) { return t_of(x) < t_of(y); });
+      std::stable_sort(pw.begin(), pw.end(), [&](const Work& x, const Work& y) {
+        return chain_of(x) != chain_of(y) ? chain_of(x) < chain_of(y) : t_of(x) < t_of(y);
+      });
       L.pos_emit_groups.clear();
+      L.pos_chain_group = ~0u;
       for (uint32_t i = 0; i < pw.size(); i++) {
         uint32_t t = (uint32_t)t_of(pw[i]);
-        if (L.pos_emit_groups.empty() || L.pos_emit_groups.back()[0] != t) L.pos_emit_groups.push_back({t, i, 0});
+        const bool ch = chain_of(pw[i]) != 0;
+        if (ch && L.pos_chain_group == ~0u) {
+          L.pos_chain_group = (uint32_t)L.pos_emit_groups.size();
+          L.pos_emit_groups.push_back({t, i, 0});
+        } else if (L.pos_emit_groups.empty() || L.pos_emit_groups.back()[0] != t) {
+          L.pos_emit_groups.push_back({t, i, 0});
+        }
         L.pos_emit_groups.back()[2]++;
       }
+      if (L.pos_chain_group == ~0u) L.pos_chain_group = (uint32_t)L.pos_emit_groups.size();
     }
-    // packed emitters: consecutive regions (witness order) share work items of <= GEN_PACK signals
+    // packed emitters: consecutive regions (witness order) share work items of <= GEN_PACK signals; E_GEN's regions
+    // that read the SMT chain's output come after all others, from work item gen_chain_work on
+    auto smt_chain_region = [](uint32_t kind) {
+      return kind == RK_SMT_OWN || kind == RK_SMTHASH || kind == RK_SMT_LEVEL || kind == RK_SWITCHER ||
+             kind == RK_ISEQ_ROOT;
+    };
     for (int e = 0; e < E_COUNT; e++) {
       if (!emitter_packed(e)) continue;
       Work cur_w{0, 0, 0, 0};
       auto flush = [&]() { if (cur_w.count) L.work[e].push_back(cur_w); cur_w = Work{(uint32_t)L.gen_pieces.size(), 0, 0, 0}; };
       flush();
-      for (uint32_t ri = 0; ri < L.regions.size(); ri++) {
-        const Region& r = L.regions[ri];
-        if (emitter_of(r.kind) != e) continue;
-        for (uint32_t s = 0; s < r.len;) {
-          if (cur_w.count == GEN_PACK || cur_w.pad == GEN_MAX_PIECES) flush();
-          uint32_t take = std::min(r.len - s, GEN_PACK - cur_w.count);
-          L.gen_pieces.push_back(GenPiece{ri, s, cur_w.count, 0});
-          cur_w.count += take; cur_w.pad++; s += take;
+      for (int pass = 0; pass < (e == E_GEN ? 2 : 1); pass++) {
+        if (pass == 1) {
+          flush();
+          L.gen_chain_work = (uint32_t)L.work[e].size();
+        }
+        for (uint32_t ri = 0; ri < L.regions.size(); ri++) {
+          const Region& r = L.regions[ri];
+          if (emitter_of(r.kind) != e || (e == E_GEN && smt_chain_region(r.kind) != (pass == 1))) continue;
+          for (uint32_t s = 0; s < r.len;) {
+            if (cur_w.count == GEN_PACK || cur_w.pad == GEN_MAX_PIECES) flush();
+            uint32_t take = std::min(r.len - s, GEN_PACK - cur_w.count);
+            L.gen_pieces.push_back(GenPiece{ri, s, cur_w.count, 0});
+            cur_w.count += take; cur_w.pad++; s += take;
+          }
         }
       }
       flush();

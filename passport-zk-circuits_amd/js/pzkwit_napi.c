@@ -22,9 +22,10 @@
  *        chunks, device->host copy beside compute) and are copied once into their image.
  *   witnessStream(handle, inputs, batch, chunk, onChunk) -> Promise<void>: pzk_witness_stream, the streamed
  *        form of gen-witness.sh:25's one-.wtns-per-input loop. onChunk(first, rows, status) runs on the JS
- *        thread for each chunk in order: rows is a Buffer over the library's PINNED chunk slot (n x witnessSize
- *        x 32 B, no copy), valid only until onChunk returns or the promise it returns settles — the slot is then
- *        reused; status is an Int32Array copy. A truthy result (or promise value) or a throw stops the stream and
+ *        thread for each chunk in order: rows is an ArrayBuffer over the library's PINNED chunk slot (n x
+ *        witnessSize x 32 B, no copy), valid until onChunk returns or the promise it returns settles: it is then
+ *        DETACHED (every view of it reads as empty) before the slot is reused — a JS-owned copy where the runtime
+ *        refuses external buffers; status is an Int32Array copy. A truthy result (or promise value) or a throw stops the stream and
  *        rejects the call (a throw with its own error). Host memory stays at two chunks whatever the batch.
  *
  *   passportParse({ dg1, dg15, sod })       -> { params, name, refAaShift, ... } (pzk_passport_parse)
@@ -36,9 +37,10 @@
  *        n x 82 x 32 B (slaveMerkleRoot, skIdentity, 80 branches) or null.
  *
  * Errors: a failing pzk_* call throws (or rejects with) an Error carrying pzk_last_error().
- * N-API version 4 features only (Node >= 10.16 / 12.x).
+ * N-API version 7 (Node >= 12.19 / 14.x): napi_detach_arraybuffer invalidates a streamed chunk's view when the
+ * chunk is done with.
  */
-#define NAPI_VERSION 4
+#define NAPI_VERSION 7
 #define _POSIX_C_SOURCE 200809L
 #include <node_api.h>
 #include <pthread.h>
@@ -315,6 +317,8 @@ typedef struct {
   size_t first, n, stride;
   const uint8_t* rows;
   const int32_t* status;
+  napi_ref rows_ref;            /* the ArrayBuffer over the pinned chunk handed to onChunk (JS thread only) */
+  int rows_external;            /* 1: it views the library's pinned slot (detached when the chunk is done) */
   pthread_mutex_t mu;
   pthread_cond_t cv;
   int handed, sink_rc;
@@ -350,11 +354,26 @@ static int truthy(napi_env env, napi_value v) {
   return r ? 1 : 0;
 }
 
+/* JS thread: onChunk is done with the chunk (returned, threw, or its promise settled). The pinned slot its rows
+ * live in is reused two chunks later and freed with the instance, so the ArrayBuffer over it is detached first:
+ * any view of it a callback kept (an un-awaited write, a stored subarray) then reads as empty instead of reading
+ * recycled or freed memory. A copied chunk (rows_external = 0) stays valid and is left to the GC. */
+static void chunk_done(napi_env env, stream_job* j, int rc) {
+  if (j->rows_ref) {
+    napi_value ab;
+    if (j->rows_external && napi_get_reference_value(env, j->rows_ref, &ab) == napi_ok && ab)
+      napi_detach_arraybuffer(env, ab);
+    napi_delete_reference(env, j->rows_ref);
+    j->rows_ref = NULL;
+  }
+  stream_release(j, rc);
+}
+
 /* the promise onChunk returned settled */
 static napi_value chunk_fulfilled(napi_env env, napi_callback_info info) {
   napi_value v;
   stream_job* j = cb_job(env, info, &v);
-  if (j) stream_release(j, truthy(env, v));
+  if (j) chunk_done(env, j, truthy(env, v));
   return NULL;
 }
 static napi_value chunk_rejected(napi_env env, napi_callback_info info) {
@@ -362,34 +381,46 @@ static napi_value chunk_rejected(napi_env env, napi_callback_info info) {
   stream_job* j = cb_job(env, info, &v);
   if (j) {
     if (!j->error_ref) napi_create_reference(env, v, 1, &j->error_ref);
-    stream_release(j, 1);
+    chunk_done(env, j, 1);
   }
   return NULL;
 }
 
 static void noop_finalize(napi_env env, void* data, void* hint) { (void)env; (void)data; (void)hint; }
 
+/* the chunk's rows as an ArrayBuffer: external over the pinned slot (zero copy, detached in chunk_done), or —
+ * where the runtime refuses external buffers (V8 sandbox) — a JS-owned copy */
+static int chunk_arraybuffer(napi_env env, stream_job* j, napi_value* ab) {
+  const size_t bytes = j->n * j->stride;
+  j->rows_external = napi_create_external_arraybuffer(env, (void*)j->rows, bytes, noop_finalize, NULL, ab) == napi_ok;
+  if (!j->rows_external) {
+    void* copy = NULL;
+    if (napi_create_arraybuffer(env, bytes, &copy, ab) != napi_ok) return 0;
+    memcpy(copy, j->rows, bytes);
+  }
+  return napi_create_reference(env, *ab, 1, &j->rows_ref) == napi_ok;
+}
+
 /* JS thread: onChunk(first, rows, status) for the chunk the worker is blocked on */
 static void stream_call_js(napi_env env, napi_value js_cb, void* context, void* data) {
   stream_job* j = (stream_job*)data;
   (void)context;
-  if (!env) { stream_release(j, 1); return; }  /* the environment is shutting down */
+  if (!env) { stream_release(j, 1); return; }  /* the environment is shutting down: nothing was handed to JS */
   napi_value argv[3], undef, ret, sab;
   void* st_copy = NULL;
-  int ok = napi_create_double(env, (double)j->first, &argv[0]) == napi_ok &&
-           napi_create_external_buffer(env, j->n * j->stride, (void*)j->rows, noop_finalize, NULL, &argv[1]) == napi_ok &&
+  int ok = napi_create_double(env, (double)j->first, &argv[0]) == napi_ok && chunk_arraybuffer(env, j, &argv[1]) &&
            napi_create_arraybuffer(env, j->n * sizeof(int32_t), &st_copy, &sab) == napi_ok;
   if (ok) {
     memcpy(st_copy, j->status, j->n * sizeof(int32_t));
     ok = napi_create_typedarray(env, napi_int32_array, j->n, sab, 0, &argv[2]) == napi_ok &&
          napi_get_undefined(env, &undef) == napi_ok;
   }
-  if (!ok) { stream_release(j, 1); return; }
+  if (!ok) { chunk_done(env, j, 1); return; }
   if (napi_call_function(env, undef, js_cb, 3, argv, &ret) != napi_ok) {
     napi_value exc;
     if (napi_get_and_clear_last_exception(env, &exc) == napi_ok && !j->error_ref)
       napi_create_reference(env, exc, 1, &j->error_ref);
-    stream_release(j, 1);
+    chunk_done(env, j, 1);
     return;
   }
   /* a thenable: wait for it to settle (e.g. an fs.promises write of the chunk's .wtns files) */
@@ -404,10 +435,10 @@ static void stream_call_js(napi_env env, napi_value js_cb, void* context, void* 
         napi_create_function(env, "rejected", NAPI_AUTO_LENGTH, chunk_rejected, j, &fns[1]) == napi_ok &&
         napi_call_function(env, ret, then_fn, 2, fns, NULL) == napi_ok)
       return;
-    stream_release(j, 1);
+    chunk_done(env, j, 1);
     return;
   }
-  stream_release(j, truthy(env, ret));
+  chunk_done(env, j, truthy(env, ret));
 }
 
 /* worker thread (inside pzk_witness_stream): hand the chunk to JS and wait until it is done with the rows */

@@ -146,6 +146,23 @@ async function gpu(inPath, outPath, extraPath) {
     await assert.rejects(rc.calculateWTNSBinStream(inputs64.slice(0, 6), (i) => {
       if (i === 3) throw new Error("stop at 3");
     }, true, 2), /stop at 3/);
+    // a view kept past its callback is detached when the chunk is done (reads as empty, never as a recycled slot)
+    const kept = [];
+    await rc.calculateWTNSBinStream(inputs64.slice(0, 4), (i, header, witness) => { kept.push(witness); }, true, 2);
+    assert.ok(kept.length === 4 && kept.every((w) => w.length === 0), `kept views: ${kept.map((w) => w.length)}`);
+    // a call into the same calculator from inside onWitness rejects instead of deadlocking on the instance
+    let reentrant = null;
+    await rc.calculateWTNSBinStream(inputs64.slice(0, 2), async () => {
+      try { await rc.calculateWTNSBin(three[0], true); } catch (e) { reentrant = e; }
+    }, true, 2);
+    assert.ok(reentrant && /streaming/.test(reentrant.message), `re-entrant call: ${reentrant}`);
+    // a failing lane with sanityCheck rejects before any onWitness of its chunk runs
+    const bad = JSON.parse(JSON.stringify(three[0]));
+    bad.dg1[10] = bad.dg1[10] === "1" ? "0" : "1";  // dg1 hash != the EC field -> flow check (code 7)
+    let called = 0;
+    await assert.rejects(rc.calculateWTNSBinStream([three[1], bad], async () => { called++; }, true, 2),
+                         /Assert Failed/);
+    assert.strictEqual(called, 0);
     // the instance still works after a stopped stream
     const again = Buffer.from(await rc.calculateWTNSBin(three[0], true));
     assert.ok(Buffer.compare(again, ser[0]) === 0);

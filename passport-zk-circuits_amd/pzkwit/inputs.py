@@ -414,12 +414,12 @@ class PassportGen:
         bs = hash_block(sig_hash_type(pr["sig"]))
         return 1 + pr["ec_blocks"] * bs + 1024 + pr["dg15_blocks"] * bs + 1024 + 2 * K + 80 + 1
 
-    def passport_at(self, i, smt_depth=0):
+    def passport_at(self, i, smt_depth=0, smt_root=False):
         """Passport i from its own stream (independent of generation order)."""
         saved = self.rng
         self.rng = SplitMix64((self.seed << 40) ^ (0x50415353 + i))
         try:
-            return self.passport(i, smt_depth)
+            return self.passport(i, smt_depth, smt_root)
         finally:
             self.rng = saved
 
@@ -436,8 +436,10 @@ class PassportGen:
             self._pkhash[key.n] = h
         return h
 
-    def passport(self, i, smt_depth=0):
-        """Returns dict of raw fields for passport i (bytes + ints)."""
+    def passport(self, i, smt_depth=0, smt_root=False):
+        """Returns dict of raw fields for passport i (bytes + ints). smt_depth k > 0: siblings[0..k-1] uniform
+        non-zero Fr; the root is then computed (smt_root=True, Python Poseidon, ~0.6 ms
+        per level) or left 0 (the circuit does not enforce it: passportVerificationBuilder.circom:240)."""
         pr = self.params
         rng = self.rng
         key = self.keys[i % len(self.keys)]
@@ -484,7 +486,10 @@ class PassportGen:
                 while v == 0:
                     v = rng.fr()
                 siblings[k] = v
-            root = None  # computed by the caller (config 4); not enforced by the circuit
+            root = None  # not enforced by the circuit
+            if smt_root:
+                from .query import smt_root as _root
+                root = _root(pkh, pkh, siblings)  # SMTVerifier.circom:109-176 with key = value = pubkeyHash
         else:
             root = int(root_hex, 16)
         return dict(dg1=dg1, dg15=dg15, ec=ec, sa=sa, sig=sig, n=key.n, sk=sk, root=root,

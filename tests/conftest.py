@@ -6,6 +6,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "passport-zk-circuits_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(1, REPO)  # bench.py (its input generators)
 
 
 def pytest_configure(config):

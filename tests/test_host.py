@@ -241,6 +241,14 @@ def test_bench_two_ranks_gloo_scatter_gather(workload):
     assert g["status_nonzero"] == int((rows[:, 0, 0] != 0).sum())
     assert g["public_sha256"] == hashlib.sha256(rows[:, :4].tobytes()).hexdigest()[:16]
     assert out["config"]["invalid_lanes"] == 2 * int((rows[:, 0, 0] != 0).sum())
+    if workload == "register":
+        # the default register line also runs config 4's inputs (seed 0x4, proofs of depth 1-79) through the ranks
+        c4 = out["config4"]
+        rows4 = bench.make_register_inputs(12, 0, seed=4, sig=1, workers=2, smt_depth="1-79", smt_root=True)
+        assert c4["n_gpus"] == 2 and c4["value"] > 0 and c4["smt_depth"] == "1-79"
+        assert c4["invalid_lanes"] == 2 * int((rows4[:, 0, 0] != 0).sum())
+    else:
+        assert "config4" not in out
 
 
 def test_sym_map_validation():

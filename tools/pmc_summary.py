@@ -1,7 +1,8 @@
 """Per-kernel PMC summary (last dispatch of each kernel) from rocprofv3 counter_collection CSVs.
 
 usage: pmc_summary.py DIR_PREFIX   (reads DIR_PREFIX_sq, _rd, _wr)
-       pmc_summary.py DIR_PREFIX --json BATCH OUT.json [WORKLOAD]   (WORKLOAD: bench.py's config.workload)
+       pmc_summary.py DIR_PREFIX --json BATCH OUT.json [WORKLOAD [LAYOUT_KEY]]   (bench.py's config.workload and
+       config.layout_key: "O0", or the --sym argument of a mapped line)
 FETCH_SIZE is doubled (gfx950 reports half the bytes of wide streaming reads; MI355X_MICROARCH.md
 HBM section); FETCH_SIZE / WRITE_SIZE are in KB."""
 import csv
@@ -45,7 +46,7 @@ def main(prefix):
               f"{(rgb + wgb) / ms if ms else 0:10.1f}")
 
 
-def traffic_json(prefix, batch, out_path, workload=None):
+def traffic_json(prefix, batch, out_path, workload=None, layout_key="O0"):
     """Per-kernel HBM traffic per witness (FETCH_SIZE x 2 + WRITE_SIZE, bytes) for bench.py's
     roofline.traffic; batch = witnesses per launch of the profiled run."""
     import json
@@ -81,7 +82,7 @@ def traffic_json(prefix, batch, out_path, workload=None):
             v = sq.get(k, {}).get("SQ_INSTS_VALU", 0) / n_sq / batch
             res[k]["valu_insts_per_witness"] = round(v, 1)
             valu_total += v
-    out = {"source": prefix, "batch": batch, "workload": workload, "kernels": res}
+    out = {"source": prefix, "batch": batch, "workload": workload, "layout_key": layout_key, "kernels": res}
     if n_sq:
         out["valu_insts_per_witness"] = round(valu_total, 1)
     json.dump(out, open(out_path, "w"), indent=1)
@@ -89,6 +90,7 @@ def traffic_json(prefix, batch, out_path, workload=None):
 
 if __name__ == "__main__":
     if len(sys.argv) > 3 and sys.argv[2] == "--json":
-        traffic_json(sys.argv[1], int(sys.argv[3]), sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None)
+        traffic_json(sys.argv[1], int(sys.argv[3]), sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None,
+                     sys.argv[6] if len(sys.argv) > 6 else "O0")
     else:
         main(sys.argv[1])

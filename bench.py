@@ -461,7 +461,7 @@ def main():
     ap.add_argument("--host-sample", type=int, default=None, help="witnesses streamed for host_delivered")
     args = ap.parse_args()
     if args.workload == "mixed" and os.environ.get("PZK_MIX_HWQ", "16") != "keep":
-        # one instance per flow, seven streams each: with 4 hardware queues (HIP's default, and what the GPU boxes'
+        # one instance per flow, seven streams each (four high, three low priority): with 4 hardware queues per priority (HIP's default, and what the GPU boxes'
         # environment sets) the flows' streams share queues and serialise behind each other (40.9k -> 43.2k
         # witnesses/s at 16, profiles/r4_hwq/); set before any HIP call, inherited by the ranks launch_ranks starts
         # (PZK_MIX_HWQ=keep leaves the environment's value)

@@ -363,7 +363,7 @@ hipError_t launch_bjj_table(fr* table, hipStream_t st) {
 
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st) {
-  // scratch given: the round-3 kernel with its global scratch array (QueryIdentity's default, bjj_uses_scratch);
+  // scratch given: the round-3 kernel with its global scratch array (the default, bjj_uses_scratch);
   // PZK_BJJ_SEGS: lanes per witness (scratch 8 / 16 / 32, recompute 16 / 32 / 64), for tuning runs (runtime.cpp
   // validates it)
   static const int env_segs = getenv("PZK_BJJ_SEGS") ? atoi(getenv("PZK_BJJ_SEGS")) : 0;
@@ -380,8 +380,9 @@ hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, f
 }
 
 bool bjj_uses_scratch(bool chain_critical) {
+  (void)chain_critical;
   const char* v = getenv("PZK_BJJ");
-  return v ? !strcmp(v, "scratch") : chain_critical;
+  return v ? !strcmp(v, "scratch") : true;
 }
 
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
@@ -393,10 +394,12 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
-                            hipStream_t st) {
-  // PZK_CHAIN_MUL=inline (CIOS, default) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch
+                            bool query, hipStream_t st) {
+  // PZK_CHAIN_MUL=inline (CIOS) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch. Default: CIOS for
+  // QueryIdentity (196.5k vs 201.7k witnesses/s with FIPS), FIPS for the register circuit (config 4 +2.1 %,
+  // profiles/r5d, r5e)
   static const char* pm = getenv("PZK_CHAIN_MUL");
-  static const int mode = !pm ? 0 : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
+  const int mode = !pm ? (query ? 0 : 2) : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
   hipLaunchKernelGGL(mode == 1 ? k_smt_chain<FrMulCall> : mode == 2 ? k_smt_chain<FrMulFips> : k_smt_chain<FrMulInline>,
                      dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
                      dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core, smt_core, order, status, vs.batch);

@@ -39,17 +39,20 @@ hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* 
 hipError_t launch_bjj_table(fr* table, hipStream_t st);
 hipError_t launch_wtns_gather(const uint8_t* o0, size_t o0_stride, const uint32_t* map, uint64_t out_size, uint8_t* out,
                               size_t out_stride, uint32_t batch, hipStream_t st);
-// whether the BabyJubJub core runs the round-3 kernel with its global scratch array (launch_bjj_core: when it is
-// given one): by default where the core is on a latency-critical chain (QueryIdentity), else the recompute kernel
-// with no scratch; PZK_BJJ=scratch|rc overrides (A/B switch)
+// whether the BabyJubJub core runs the kernel with its global scratch array (launch_bjj_core: when it is given one):
+// by default yes — QueryIdentity (the core is on its latency-critical chain) and, since round 5, the register
+// circuit too (k_bjj_core_rc recomputes the ladder instead, 1.35x instead of 6x its bytes but twice the VALU:
+// configs 3 / 4 / O2-shaped +1.0 / +0.7 / +5.7 % with the scratch kernel, profiles/r5e); PZK_BJJ=scratch|rc (A/B)
 bool bjj_uses_scratch(bool chain_critical);
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st);
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st);
+// query: QueryIdentity's chain (default product: CIOS, the shorter dependent chain) vs the register circuit's
+// (FIPS: half the VALU instructions, and the register chain is off every emitter's path)
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
-                            hipStream_t st);
+                            bool query, hipStream_t st);
 // witnesses ordered by SMT insertion level (the chain's length), deepest first, for k_smt_chain's lane groups
 hipError_t launch_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order, uint32_t batch, hipStream_t st);
 // QueryIdentity prep (query.hpp): DG1 fields, dg1 chunks, citizenship inverses, the query checks

@@ -213,8 +213,8 @@ constexpr int MM_CORE_WORDS(int K) { return 12 * K - 3; }  // x[K] y[K] q[K+1] r
 constexpr int BJJ_STEPS = 254;
 constexpr int BJJ_EMIT_STEPS = 32;                           // ladder steps per k_emit_bjj work item
 constexpr int BJJ_SCRATCH_STEPS = 256;                       // k_bjj_core: SEGS lanes per witness x 256 / SEGS steps
-constexpr int BJJ_SEGS_DEFAULT = 32;
-constexpr int BJJ_RC_SEGS_DEFAULT = 64;                     // k_bjj_core_rc (recompute, no scratch): lanes per witness                        // A/B 8 / 16 / 32: 2.00 / 1.47 / 1.22 ms per 2048 witnesses
+constexpr int BJJ_SEGS_DEFAULT = 32;                        // k_bjj_core lanes per witness; A/B 8 / 16 / 32: 2.00 / 1.47 / 1.22 ms per 2048 witnesses
+constexpr int BJJ_RC_SEGS_DEFAULT = 64;                     // k_bjj_core_rc (recompute, no scratch): lanes per witness
 constexpr int BJJ_TABLE_WINDOWS = 32;                        // fixed-base table: 32 windows x 256 x (x, y, t2d)
 constexpr int BJJ_SCRATCH_FR = 9 * BJJ_SCRATCH_STEPS;        // per witness, for any segment count
 constexpr int BJJ_CORE_FR = 5 * BJJ_STEPS;                  // per step: Dx, Dy, Ax, Ay, inv(Dx)   (Montgomery)

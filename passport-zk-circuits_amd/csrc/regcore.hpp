@@ -383,8 +383,16 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
     fr d = diff(e);
     fr r = fr_zero();
     if (!fr_is_zero(d)) { r = fr_mul(inv, in_lds ? pre_run[(e - e0) * 64 + lane] : load_fr(slot(e))); inv = fr_mul(inv, d); }
-    store_fr(slot(e), fr_from_mont(r));
+    r = fr_from_mont(r);
+    if (in_lds) pre_run[(e - e0) * 64 + lane] = r;  // the lane's own entry: read above, in this iteration
+    else store_fr(slot(e), r);
   }
+  if (!in_lds) return;
+  // written out in element order, 64 consecutive 32-byte inverse slots per store instruction: lane l's run is
+  // elements [l PER, (l + 1) PER), so storing from the loop above put 64 partial lines of 64 different slots in
+  // flight per iteration, and L2 wrote most lines twice (2.0x the inverse bytes, pmc_r4c3)
+  __syncthreads();  // the LDS writes above (other lanes' runs) before the reads below
+  for (int e = lane; e < NE; e += 64) store_fr(slot(e), pre_run[(e % PER) * 64 + e / PER]);
 }
 
 // ============================================================================ RSA EM checks
@@ -815,10 +823,12 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
 
 // sequential part: levels j-1 .. 0, then all roots and the isEqual inverse. SMT_CHAIN_LANES lanes per
 // witness run each level hash as a cooperative permutation (pos_perm_group: lane k < 3 holds state
-// element k) whose hash comes back to every lane of the group by its butterfly. Everything the level loop
-// reads is staged in LDS first — the width-3 constants, the group's siblings (Montgomery) and left/right bits,
-// the level tasks' core offsets — so the loop issues no global load: a global load issued after the round-state
-// stores would wait for them (gfx9 vmcnt counts both), one store latency per round of every level.
+// element k) whose hash comes back to every lane of the group by its butterfly. What the rounds read is staged in
+// LDS first — the width-3 constants, the group's left/right bits, the level tasks' core offsets — so no round
+// issues a global load (one issued after the round-state stores would wait for them: gfx9 vmcnt counts both).
+// The siblings are the one global read: level i - 1's is loaded when level i starts and converted when level i
+// ends, one wait per level (round 5: staging all 80 per lane group took 40 KB of the 63 KB of LDS a chain
+// workgroup held beside the emitters on every CU it ran on).
 // PM: the product policy (PZK_CHAIN_MUL=inline|call|fips, A/B; poseidon.hpp FrMulInline / FrMulCall / FrMulFips)
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 template <class PM>
@@ -830,7 +840,6 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
   static_assert(G == 4 && 64 % G == 0, "PoseidonHash(2) groups are 4 lanes (t = 3)");
   using KL = PosConstsLds<3>;
   __shared__ fr kc[KL::SIZE];
-  __shared__ fr sibs[NG][SMT_LEVELS];
   __shared__ uint8_t lrs[NG][SMT_LEVELS];
   __shared__ int32_t lv_core[SMT_LEVELS];
   KL::stage(kc, K);
@@ -846,18 +855,17 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
   const uint32_t* flags = reinterpret_cast<const uint32_t*>(core + 2 * SMT_LEVELS);
   const int j = live ? (int)reinterpret_cast<const uint32_t*>(core + 3 * SMT_LEVELS)[0] : 0;
   const int top = j < SMT_LEVELS ? j : SMT_LEVELS;
-  for (int i = jl; i < top; i += G) {
-    sibs[gi][i] = fr_to_mont(load_fr(row + 32ull * (R.in_br + i)));
-    lrs[gi][i] = (uint8_t)((flags[i] >> 4) & 1);
-  }
+  for (int i = jl; i < top; i += G) lrs[gi][i] = (uint8_t)((flags[i] >> 4) & 1);
   __syncthreads();
   if (!live) return;
   const KL Kl{kc};
   const fr leaf = vs.at(R.v_leaf, w);
   fr child = leaf;  // root_j = leaf
   fr* pcore = pos_core + (size_t)w * L.pos_core_elems;
+  const uint8_t* sib_row = row + 32ull * R.in_br;
+  fr sib = top > 0 ? fr_to_mont(load_fr(sib_row + 32ull * (top - 1))) : fr_zero();
   for (int i = top - 1; i >= 0; i--) {
-    const fr sib = sibs[gi][i];
+    const fr sib_next_raw = i > 0 ? load_fr(sib_row + 32ull * (i - 1)) : fr_zero();  // before this level's stores
     const bool lr = lrs[gi][i] != 0;
     const fr lv = lr ? sib : child, rv = lr ? child : sib;  // Switcher (SMTVerifier.circom): the level's L / R
     if (jl == 0) {
@@ -866,6 +874,7 @@ __global__ void __launch_bounds__(64) k_smt_chain(DevLayout L, PosConsts K, cons
     }
     child = pos_perm_group<3, G, KL, PM>(Kl, jl == 1 ? lv : jl == 2 ? rv : fr_zero(), pcore + lv_core[i], jl);
     if (jl == 0) vs.at(R.v_smt_h + i, w) = child;  // root_i = H_i (st_top = 1 below j)
+    sib = fr_to_mont(sib_next_raw);
   }
   if (jl != 0) return;  // lane 0 wrote every level hash this kernel made
   // roots of every level: root_i = st_top_i * H_i + st_inew_i * leaf (SMTVerifier.circom:104-106)

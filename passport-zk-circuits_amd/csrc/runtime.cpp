@@ -144,8 +144,10 @@ struct pzk_instance {
   Layout lay;
   int device = 0;
   hipStream_t stream = nullptr;
-  // side streams of the register pipeline (signature core; SHA emitters; other emitters, s_emit
-  // below): four streams in all, one per hardware queue (GPU_MAX_HW_QUEUES = 4)
+  // side streams of the register pipeline (signature core; SHA emitters; other emitters, s_emit below). A register
+  // instance has seven: main, s_rsa and the SMT chain streams s_tail / s_chain2 at high priority, s_sha, s_emit and
+  // s_post at low priority (eight with PZK_SMT_CHAINS=3); HIP gives each priority GPU_MAX_HW_QUEUES (4) hardware
+  // queues, so no two of them share one (pzk_instance_create)
   hipStream_t s_rsa = nullptr, s_sha = nullptr;
   hipEvent_t ev_load = nullptr, ev_sha = nullptr, ev_rsa = nullptr, ev_bjj = nullptr, ev_entry = nullptr, ev_dep = nullptr;
   // device copies of the layout
@@ -487,14 +489,23 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess;
+  // The SMT chain streams (s_tail, s_chain2; QueryIdentity's third chain is s_tail) are high priority as well
+  // (PZK_CHAIN_PRIO=lo: the rounds 1-4 placement). Besides dispatch order this sets the hardware queues: HIP gives
+  // each stream priority a pool of GPU_MAX_HW_QUEUES (4 by default) queues and lets streams share one beyond that,
+  // and a shared queue executes its streams' packets in submission order, so a stream waiting for the chain stalls
+  // the other stream on its queue. High: main, rsa, s_tail, s_chain2; low: s_sha, s_emit, s_post — no two streams of
+  // an instance share a queue at the default queue count (profiles/r5b, r5c).
+  static const bool chain_lo = getenv("PZK_CHAIN_PRIO") && !strcmp(getenv("PZK_CHAIN_PRIO"), "lo");
+  const int prio_chain = chain_lo ? prio_lo : prio_hi;
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_lo) == hipSuccess;
+       hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_chain) == hipSuccess;
+  if (ok && I->lay.is_register)  // the register circuit's second SMT chain stream
+    ok = hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_chain) == hipSuccess;
   // the third chain stream only when asked for (PZK_SMT_CHAINS=3): with several instances in a process every stream
   // competes for the process's hardware queues
   if (ok && getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
-    ok = hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_lo) == hipSuccess;
+    ok = hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_chain) == hipSuccess;
   if (ok && I->lay.is_register && post_chain_split())
     ok = hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, prio_lo) == hipSuccess;
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
@@ -759,7 +770,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6, S.d_smt_order))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              st)); }
+                              true, st)); }
     HIPCHK(hipEventRecord(I->ev_pos, st));
     // PZK_QRY_EMIT1=1: every emitter on one stream (with 3 chain streams that is 4 streams in use = the
     // hardware queues a process gets by default)
@@ -875,7 +886,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     { PhaseScope ps(T, slot, PH_SMT, s_smt);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              s_smt)); }
+                              false, s_smt)); }
     HIPCHK(hipEventRecord(I->ev_chain, s_smt));
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }
@@ -924,9 +935,9 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
       if ((rc = emit(E_ECT, s_sha, ect_split))) return rc;
     }
   }
-  hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, serial ? st : I->s_chain2,
-                                                 serial ? st : I->s_chain3 ? I->s_chain3 : I->s_chain2,
-                                                 serial || !I->s_post ? st : I->s_post};
+  auto or_st = [&](hipStream_t s) { return serial || !s ? st : s; };  // streams an instance does not have: st
+  hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, or_st(I->s_chain2),
+                                                 or_st(I->s_chain3), or_st(I->s_post)};
   for (int i = 0; i < pzk_instance::NSTREAMS; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));
@@ -1171,6 +1182,10 @@ static int pzk_phase_info_impl(const pzk_instance* I, uint32_t phase, const char
       if (r.kind == RK_INCOPY) b += 32ull * r.len;
       if (r.kind == RK_POSEIDON) b += 32ull * pos_core_len(r.a[1] + 1);
       if (r.kind == RK_MODMUL) b += 8ull * MM_CORE_WORDS(L.reg.K);
+      if (r.kind == RK_FLOW) {  // the encapsulated content and signed attributes bits it copies (and compares)
+        const ShaJob& je = L.sha[r.a[2]];
+        b += 32ull * ((je.algo >= 3 ? 1024 : 512) * (uint64_t)je.blocks + 1024);
+      }
     }
     if (phase == PH_SHA_CORE)
       for (const ShaJob& j : L.sha)
@@ -1190,7 +1205,8 @@ static int pzk_phase_info_impl(const pzk_instance* I, uint32_t phase, const char
            32ull * (9 + 4 + 1 + 240);                   // chunks, citizenship index and its 240 IsEqual inverses
     if (phase == PH_SMT && (L.is_register || L.is_query))  // siblings, root and key read; SMT core and the
       b += 32ull * (SMT_LEVELS + 2) + 32ull * SMT_CORE_FR + 32ull * 2 * SMT_LEVELS;  // level hash inputs written
-    if (phase == PH_RSA_CORE) b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K;
+    if (phase == PH_RSA_CORE)  // core written + signature and modulus read; k_rsa_inv reads every remainder and the
+      b += 8ull * L.rsa_core_words + 32ull * 2 * L.reg.K + 8ull * L.reg.n_modmul * L.reg.K + 32ull * L.reg.K;  // modulus
     if (phase == PH_BJJ_CORE) b += 32ull * L.bjj_core_fr;
     if (phase == PH_LOAD) b += 64ull * L.loads.size();
     *bytes_per_witness = b;

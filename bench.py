@@ -405,6 +405,7 @@ def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"
         sub = (batch + parts_n - 1) // parts_n
     else:
         sub = batch
+    sub = min(sub, 32768)  # pzk_witness_batch takes <= 65535 witnesses per call (its grids' y dimension)
     slots = min(slots, (batch + sub - 1) // sub)
     log("witness_size=%d (%.1f MB), batch=%d, sub-batch=%d, %d output slots %.1f GB" % (
         W, stride / 1e6, batch, sub, slots, slots * sub * stride / 1e9))
@@ -600,6 +601,15 @@ def report(args, r, world):
     job_bytes = 32 * NIN + 76 + 32 * W
     job_gbs = value * job_bytes / 1e9
     valu = valu_roofline(tj, tf, value, world)
+    # the same kernel alone (the PMC pass serialises dispatches): its bytes over its standalone time, for the share of
+    # the concurrent schedule's HBM the other emitters take while it runs
+    standalone = None
+    if tj and all(tj["kernels"].get(k, {}).get("standalone_ms_per_batch") for k in info[dom][0].split("+")):
+        sms = sum(tj["kernels"][k]["standalone_ms_per_batch"] for k in info[dom][0].split("+"))
+        sb = info[dom][1] * tj["batch"]
+        standalone = {"ms_per_launch": sms, "witnesses_per_launch": tj["batch"],
+                      "achieved": round(sb / (sms / 1e3) / 1e9, 1), "frac": round(sb / (sms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "source": os.path.relpath(tf, REPO)}
     out = {
         "metric": metric, "value": round(value, 2), "unit": "witnesses/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -617,7 +627,7 @@ def report(args, r, world):
         "roofline": {"bound": "hbm", "kernel": info[dom][0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "bytes_per_launch": int(bytes_per_launch),
-                     "avg_launch_ms": round(avg_ms, 4), "valu": valu,
+                     "avg_launch_ms": round(avg_ms, 4), "standalone": standalone, "valu": valu,
                      "job_bound": ("valu" if valu and valu["frac"] > job_gbs / (HBM_PEAK_GBS * world) else "hbm")},
         "job_hbm": {"alg_bytes_per_witness": job_bytes, "achieved": round(job_gbs, 1), "unit": "GB/s",
                     "frac": round(job_gbs / (HBM_PEAK_GBS * world), 4)},

@@ -127,6 +127,12 @@ struct Scratch {
   }
 };
 
+// QueryIdentity: chain streams its calls rotate over (PZK_QRY_CHAINS = 1..4, default 3)
+static int qry_chain_streams() {
+  static const int v = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 3;
+  return v < 1 ? 1 : v > 4 ? 4 : v;
+}
+
 // PZK_POST=0 (A/B): the register call's chain-dependent emission stays behind the chain on the emitter streams
 // (rounds 1-4) instead of on its own post-chain stream
 static bool post_chain_split() {
@@ -500,7 +506,7 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_chain) == hipSuccess;
-  if (ok && I->lay.is_register)  // the register circuit's second SMT chain stream
+  if (ok && (I->lay.is_register || (I->lay.is_query && qry_chain_streams() >= 4)))  // a second / fourth chain stream
     ok = hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_chain) == hipSuccess;
   // the third chain stream only when asked for (PZK_SMT_CHAINS=3): with several instances in a process every stream
   // competes for the process's hardware queues
@@ -681,13 +687,13 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   static const bool serial = getenv("PZK_SERIAL") != nullptr;
   // QueryIdentity: the whole per-call chain (prep .. SMT chain) is one latency-bound dependency chain whose
   // length is the SMT proof depth (k_smt_chain: 0.5 ms per level for 4096 witnesses, one wave per CU), so
-  // consecutive calls rotate over PZK_QRY_CHAINS (1 / 2 / 3) chain streams — the two high-priority streams,
-  // then the fifth stream — and their chains run side by side
-  static const int qry_chains = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 3;
+  // consecutive calls rotate over qry_chain_streams() (1 / 2 / 3 / 4) chain streams — main, s_rsa, s_tail,
+  // s_chain2, all high priority — and their chains run side by side
+  const int qry_chains = qry_chain_streams();
   hipStream_t st = I->stream;
   if (I->lay.is_query && !serial && qry_chains > 1) {
-    const int c = qry_chains >= 3 ? set % 3 : set & 1;  // nsets (3) calls in flight
-    st = c == 0 ? I->stream : c == 1 ? I->s_rsa : I->s_tail;
+    const int c = (int)((I->calls - 1) % (uint64_t)qry_chains);
+    st = c == 0 ? I->stream : c == 1 ? I->s_rsa : c == 2 ? I->s_tail : I->s_chain2;
   }
   for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(st, e, 0));
   if (user) {
@@ -783,12 +789,18 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if ((rc = emit(E_QRY, s_sha))) return rc;
     if ((rc = emit(E_BITS, s_sha))) return rc;  // Num2Bits(254) of the tree position reads level 3
   } else if (!lay.is_register) {
+    // standalone circuits (PoseidonHash(n), the SHA hashers): the core on the main stream, the emitters on the emit
+    // stream behind it, so call k's emitters run beside call k + 1's core (config 1: PoseidonHash(2))
     { PhaseScope ps(T, slot, PH_SHA_CORE, st);
       HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, 0, L.n_sha, S.d_sha_core, d_status, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }
+    if (s_emit != st) {
+      HIPCHK(hipEventRecord(I->ev_pos, st));
+      HIPCHK(hipStreamWaitEvent(s_emit, I->ev_pos, 0));
+    }
     for (int e = 0; e < E_COUNT; e++)
-      if ((rc = emit(e, st))) return rc;
-    s_rsa = s_sha = s_emit = s_own = st;
+      if ((rc = emit(e, s_emit))) return rc;
+    s_rsa = s_sha = s_own = st;
   } else {
     // Four streams. The dependency chains get the high-priority streams: the
     // signature core (rsa) depends only on the inputs; the Poseidon/SMT/BabyJubJub chain (main)

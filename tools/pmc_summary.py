@@ -50,14 +50,25 @@ def traffic_json(prefix, batch, out_path, workload=None, layout_key="O0"):
     """Per-kernel HBM traffic per witness (FETCH_SIZE x 2 + WRITE_SIZE, bytes) for bench.py's
     roofline.traffic; batch = witnesses per launch of the profiled run."""
     import json
+    def bare(r):  # bare kernel name: no return type, template arguments or namespaces (pzk::ec_c1::k_...)
+        return r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+
     def sums(path):
         tot, calls = defaultdict(lambda: defaultdict(float)), defaultdict(int)
         for r in csv.DictReader(open(path)):
-            # bare kernel name: no return type, template arguments or namespaces (pzk::ec_c1::k_...)
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+            k = bare(r)
             tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
             calls[(k, r["Dispatch_Id"])] = 1
         return tot
+
+    def durations(path):  # kernel -> summed dispatch duration (ms); the counter passes serialise dispatches
+        dur = {}
+        for r in csv.DictReader(open(path)):
+            dur[(bare(r), r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        out = defaultdict(float)
+        for (k, _), v in dur.items():
+            out[k] += v
+        return out
     rd = sums(prefix + "_rd/run_counter_collection.csv")
     wr = sums(prefix + "_wr/run_counter_collection.csv")
     # every batch launches k_load_values exactly once
@@ -69,6 +80,7 @@ def traffic_json(prefix, batch, out_path, workload=None, layout_key="O0"):
     if os.path.exists(sq_path):
         sq = sums(sq_path)
         n_sq = len({r["Dispatch_Id"] for r in csv.DictReader(open(sq_path)) if "k_load_values" in r["Kernel_Name"]})
+    ms = durations(prefix + "_wr/run_counter_collection.csv")
     res = {}
     valu_total = 0.0
     for k in sorted(set(rd) | set(wr) | set(sq)):
@@ -77,7 +89,8 @@ def traffic_json(prefix, batch, out_path, workload=None, layout_key="O0"):
         f = 2 * rd.get(k, {}).get("FETCH_SIZE", 0) * 1024 / n_batches
         w = wr.get(k, {}).get("WRITE_SIZE", 0) * 1024 / n_batches
         res[k] = {"fetch_bytes_per_witness": round(f / batch), "write_bytes_per_witness": round(w / batch),
-                  "traffic_bytes_per_witness": round((f + w) / batch)}
+                  "traffic_bytes_per_witness": round((f + w) / batch),
+                  "standalone_ms_per_batch": round(ms.get(k, 0.0) / n_batches, 4)}
         if n_sq:
             v = sq.get(k, {}).get("SQ_INSTS_VALU", 0) / n_sq / batch
             res[k]["valu_insts_per_witness"] = round(v, 1)

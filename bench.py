@@ -665,16 +665,17 @@ def report(args, r, world):
             rows = Q.batch_rows(ns, seed=99, distinct=64, td1=args.workload == "query-td1")
             kind = args.workload
         elif args.workload == "poseidon":
-            ns = args.cpu_sample or 1003 * 4 * procs
+            ns = args.cpu_sample or 1003 * 100 * procs  # ~10 s at the oracle's ~11k witnesses/s per process
             rows = poseidon_rows(ns)
             kind = "poseidon"
         else:
             ns = args.cpu_sample or 64 * procs
             _, rows = I.sha256_config2_batch(ns, seed=99, blocks=6)
             kind = args.workload
-        v, cdt = cpu_baseline(kind, list(rows), procs)
+        rows = np.asarray(rows)  # slices of one array go to the worker processes (not a list of small arrays)
+        v, cdt = cpu_baseline(kind, rows, procs)
         n1 = max(2, ns // (4 * procs))
-        v1, cdt1 = cpu_baseline_1thread(kind, list(rows[:n1]))
+        v1, cdt1 = cpu_baseline_1thread(kind, rows[:n1])
         try:
             affinity = len(os.sched_getaffinity(0))
         except AttributeError:

@@ -8,9 +8,9 @@
 
 namespace pzk {
 
-int nsets_env() {
+int nsets_env(bool query) {
   const char* e = getenv("PZK_NSETS");
-  const int v = e ? atoi(e) : 3;
+  const int v = e ? atoi(e) : query ? 6 : 3;
   return v < 2 ? 2 : v > PIPELINE_SETS_MAX ? PIPELINE_SETS_MAX : v;
 }
 
@@ -78,9 +78,34 @@ void map_program(const Layout& lay, const std::vector<uint32_t>& inv, bool force
   for (uint32_t g : inv) out.bits[g >> 6] |= 1ull << (g & 63);
   for (size_t i = 1; i < nw; i++) out.rank[i] = out.rank[i - 1] + (uint32_t)__builtin_popcountll(out.bits[i - 1]);
   auto kept = [&](uint64_t g) { return (out.bits[g >> 6] >> (g & 63)) & 1; };
+  auto kept_in = [&](uint64_t a, uint64_t n) {
+    uint64_t c = 0;
+    for (uint64_t g = a; g < a + n; g++) c += kept(g);
+    return c;
+  };
   for (int e : {E_SHA, E_SHAD, E_POS, E_ECT}) {
     std::vector<Work>& wl = out.work[e];
     wl = lay.work[e];
+    if (e == E_SHA || e == E_SHAD) {
+      // SHA block chunks hold EMIT_CHUNK O0 signals; with a map keeping a fifth of them a workgroup would build its
+      // word table for ~800 stores. Consecutive chunks of a block merge until they hold EMIT_CHUNK kept signals
+      // (the O2-shaped line: 188k -> 200k witnesses/s at 16,384-signal chunks, profiles/r5i)
+      std::vector<Work> merged;
+      uint64_t kept_cur = 0;
+      for (const Work& wk : wl) {
+        const uint64_t k = kept_in(lay.regions[wk.region].off + wk.start, wk.count);
+        Work* last = merged.empty() ? nullptr : &merged.back();
+        if (last && last->region == wk.region && lay.regions[wk.region].kind == RK_SHA_BLOCK &&
+            last->start + last->count == wk.start && kept_cur + k <= EMIT_CHUNK) {
+          last->count += wk.count;
+          kept_cur += k;
+        } else {
+          merged.push_back(wk);
+          kept_cur = k;
+        }
+      }
+      wl.swap(merged);
+    }
     for (Work& wk : wl) {
       const Region& R = lay.regions[wk.region];
       const uint32_t* src = nullptr;
@@ -125,7 +150,7 @@ static int layout_query_impl(const pzk_params* params, pzk_info* info, uint32_t*
   info->n_outputs = L.n_outputs;
   info->n_public_inputs = L.n_public;
   info->n_input_groups = (uint32_t)L.inputs.size();
-  info->pipeline_depth = nsets_env();
+  info->pipeline_depth = nsets_env(params->circuit == PZK_CIRCUIT_QUERY);
   if (n_regions) *n_regions = (uint32_t)L.regions.size();
   return 0;
 }

@@ -15,8 +15,11 @@ namespace pzk {
 
 int api_fail(int code, const std::string& msg);  // sets pzk_last_error(), returns code (runtime.cpp)
 
-constexpr int PIPELINE_SETS_MAX = 4;  // scratch sets an instance can rotate over
-int nsets_env();                      // PZK_NSETS (A/B), default 3
+constexpr int PIPELINE_SETS_MAX = 6;  // scratch sets an instance can rotate over
+// scratch sets = calls in flight: PZK_NSETS (A/B), else 6 for QueryIdentity (its calls are one long chain each:
+// 196.7k -> 229.3k -> 238.1k witnesses/s with four chain streams and three / four / six sets, profiles/r5h, r5i),
+// 3 for the others
+int nsets_env(bool query = false);
 
 // circom .sym text -> inv[k] = O0 index of output witness element k (inv[0] = 0)
 bool parse_sym(const char* text, size_t len, uint64_t o0_size, std::vector<uint32_t>& inv, std::string& why);

@@ -127,9 +127,9 @@ struct Scratch {
   }
 };
 
-// QueryIdentity: chain streams its calls rotate over (PZK_QRY_CHAINS = 1..4, default 3)
+// QueryIdentity: chain streams its calls rotate over (PZK_QRY_CHAINS = 1..4, default 4: the high-priority pool)
 static int qry_chain_streams() {
-  static const int v = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 3;
+  static const int v = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 4;
   return v < 1 ? 1 : v > 4 ? 4 : v;
 }
 
@@ -141,7 +141,7 @@ static bool post_chain_split() {
 }
 
 // scratch sets (pipeline depth): call k uses set k % nsets and waits for call k - nsets (nsets = 3, or
-// PZK_NSETS = 2..4 for A/B)
+// PZK_NSETS = 2..6 for A/B; nsets_env)
 static constexpr int NSETS = PIPELINE_SETS_MAX;  // capacity
 
 struct pzk_instance {
@@ -442,7 +442,7 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
     return fail(PZK_E_NODEVICE, "no HIP device visible: pzkwit has no CPU fallback");
   pzk_instance* I = new pzk_instance();
   I->params = *params;
-  I->nsets = nsets_env();
+  I->nsets = nsets_env(params->circuit == PZK_CIRCUIT_QUERY);
   std::string why;
   if (!build_layout(*params, I->lay, why)) { delete I; return fail(PZK_E_PARAMS, why); }
   HIPCHK(hipGetDevice(&I->device));

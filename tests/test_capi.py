@@ -64,8 +64,8 @@ def test_no_device_fails_loudly():
 
 @pytest.mark.parametrize("env,msg", [
     ({"PZK_BJJ": "bogus"}, "PZK_BJJ=bogus: valid values are rc, scratch"),
-    ({"PZK_BJJ_SEGS": "8"}, "PZK_BJJ_SEGS=8: valid values are 16, 32, 64"),
-    ({"PZK_BJJ": "scratch", "PZK_BJJ_SEGS": "64"}, "PZK_BJJ_SEGS=64: valid values are 8, 16, 32"),
+    ({"PZK_BJJ": "rc", "PZK_BJJ_SEGS": "8"}, "PZK_BJJ_SEGS=8: valid values are 16, 32, 64"),
+    ({"PZK_BJJ_SEGS": "64"}, "PZK_BJJ_SEGS=64: valid values are 8, 16, 32"),  # the scratch core is the default
     ({"PZK_SHA_U": "7"}, "PZK_SHA_U=7: valid values are 8, 16, 32"),
 ])
 def test_tuning_switches_validated(env, msg):

@@ -395,11 +395,12 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
                             bool query, hipStream_t st) {
-  // PZK_CHAIN_MUL=inline (CIOS) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch. Default: CIOS for
-  // QueryIdentity (196.5k vs 201.7k witnesses/s with FIPS), FIPS for the register circuit (config 4 +2.1 %,
-  // profiles/r5d, r5e)
+  // PZK_CHAIN_MUL=inline (CIOS) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch. Default FIPS: half the
+  // chain's VALU instructions; config 4 +2.1 % (profiles/r5e), QueryIdentity +2.2 % once six calls are in flight
+  // (245.1k -> 250.6k witnesses/s, profiles/r5m; with three, where the chain's latency showed, CIOS was 2.6 % ahead)
+  (void)query;
   static const char* pm = getenv("PZK_CHAIN_MUL");
-  const int mode = !pm ? (query ? 0 : 2) : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
+  const int mode = !pm ? 2 : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
   hipLaunchKernelGGL(mode == 1 ? k_smt_chain<FrMulCall> : mode == 2 ? k_smt_chain<FrMulFips> : k_smt_chain<FrMulInline>,
                      dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
                      dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core, smt_core, order, status, vs.batch);

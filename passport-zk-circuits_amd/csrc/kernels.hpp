@@ -48,8 +48,7 @@ hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, f
                            hipStream_t st);
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st);
-// query: QueryIdentity's chain (default product: CIOS, the shorter dependent chain) vs the register circuit's
-// (FIPS: half the VALU instructions, and the register chain is off every emitter's path)
+// query: QueryIdentity's chain or the register circuit's (both default to FIPS products, PZK_CHAIN_MUL overrides)
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
                             bool query, hipStream_t st);

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -135,10 +136,12 @@ static int qry_chain_streams() {
 
 // PZK_POST=0 (A/B): the register call's chain-dependent emission stays behind the chain on the emitter streams
 // (rounds 1-4) instead of on its own post-chain stream
-static bool post_chain_split() {
-  static const bool v = !(getenv("PZK_POST") && atoi(getenv("PZK_POST")) == 0);
-  return v;
+static bool post_chain_split(bool shared) {
+  const char* e = getenv("PZK_POST");
+  return e ? atoi(e) != 0 : !shared;
 }
+// live register instances in the process (pzk_instance_create / destroy): the stream set of a new instance
+static std::atomic<int> g_register_instances{0};
 
 // scratch sets (pipeline depth): call k uses set k % nsets and waits for call k - nsets (nsets = 3, or
 // PZK_NSETS = 2..6 for A/B; nsets_env)
@@ -184,6 +187,7 @@ struct pzk_instance {
   Scratch scr[NSETS];
   uint64_t calls = 0;  // pzk_witness_batch calls so far (selects the scratch set)
   int nsets = 3;       // scratch sets in use (pipeline depth)
+  int prio_lo = 0, prio_hi = 0;  // the device's stream priority range
   // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit, tail, chain2)
   static constexpr int NSTREAMS = 8;
   hipEvent_t ev_done[NSETS][NSTREAMS] = {};
@@ -495,25 +499,17 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   bool ok = hipStreamCreateWithPriority(&I->stream, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess;
-  // The SMT chain streams (s_tail, s_chain2; QueryIdentity's third chain is s_tail) are high priority as well
-  // (PZK_CHAIN_PRIO=lo: the rounds 1-4 placement). Besides dispatch order this sets the hardware queues: HIP gives
-  // each stream priority a pool of GPU_MAX_HW_QUEUES (4 by default) queues and lets streams share one beyond that,
-  // and a shared queue executes its streams' packets in submission order, so a stream waiting for the chain stalls
-  // the other stream on its queue. High: main, rsa, s_tail, s_chain2; low: s_sha, s_emit, s_post — no two streams of
-  // an instance share a queue at the default queue count (profiles/r5b, r5c).
-  static const bool chain_lo = getenv("PZK_CHAIN_PRIO") && !strcmp(getenv("PZK_CHAIN_PRIO"), "lo");
-  const int prio_chain = chain_lo ? prio_lo : prio_hi;
+  I->prio_lo = prio_lo;
+  I->prio_hi = prio_hi;
   ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess &&
-       hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_chain) == hipSuccess;
-  if (ok && (I->lay.is_register || (I->lay.is_query && qry_chain_streams() >= 4)))  // a second / fourth chain stream
-    ok = hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_chain) == hipSuccess;
-  // the third chain stream only when asked for (PZK_SMT_CHAINS=3): with several instances in a process every stream
-  // competes for the process's hardware queues
-  if (ok && getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
-    ok = hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_chain) == hipSuccess;
-  if (ok && I->lay.is_register && post_chain_split())
-    ok = hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, prio_lo) == hipSuccess;
+       hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
+  // the chain streams: QueryIdentity's now (its third / fourth chain, high priority); the register circuit's at its
+  // first call (ensure_chain_streams), when it is known whether other register instances share the process
+  if (ok && !I->lay.is_register) {
+    ok = hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    if (ok && I->lay.is_query && qry_chain_streams() >= 4)
+      ok = hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_hi) == hipSuccess;
+  }
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
                         &I->ev_smt, &I->ev_chain})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -540,6 +536,7 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
       acc += wl[i].count;
     }
   }
+  if (I->lay.is_register) g_register_instances++;
   *out = I;
   return 0;
 }
@@ -582,6 +579,7 @@ static int pzk_instance_create_mapped_impl(const pzk_params* params, const char*
 
 static void pzk_instance_destroy_impl(pzk_instance* inst) {
   if (!inst) return;
+  if (inst->lay.is_register) g_register_instances--;
   {
     // calls are asynchronous across the instance's streams: wait for a concurrent caller to leave and
     // for every call in flight to drain, on the instance's device, before anything is freed
@@ -664,6 +662,31 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
   return 0;
 }
 
+// A register instance's chain and post-chain streams, created at its first call. The SMT chain streams (s_tail,
+// s_chain2) are high priority: besides dispatch order this sets the hardware queues — HIP gives each stream priority
+// a pool of GPU_MAX_HW_QUEUES (4 by default) queues and lets streams share one beyond that, and a shared queue runs
+// its streams' packets in submission order, so a stream waiting for the chain stalls the other. One instance: high
+// main, rsa, s_tail, s_chain2; low s_sha, s_emit, s_post — nothing shared (config 4 58.3k -> 71.4k witnesses/s,
+// profiles/r5c). Several register instances in one process (config 5: one per flow) are another matter: with every
+// instance's full set config 5 ran 8.5k witnesses/s, with low-priority chain streams and post-chain streams 31.9k,
+// with neither 48.2k — and with the first instance's full set beside the others' rounds 1-4 sets, 4.9k
+// (profiles/r5j-r5l). So an instance whose first call finds other register instances alive takes the rounds 1-4
+// set (low-priority chain streams, no post-chain stream). PZK_CHAIN_PRIO=hi|lo and PZK_POST=0|1 force either.
+static int ensure_chain_streams(pzk_instance* I) {
+  if (!I->lay.is_register || I->s_tail) return 0;
+  const bool shared = g_register_instances.load() > 1;
+  const char* cp_env = getenv("PZK_CHAIN_PRIO");
+  const bool chain_lo = cp_env ? !strcmp(cp_env, "lo") : shared;
+  const int prio_chain = chain_lo ? I->prio_lo : I->prio_hi;
+  HIPCHK(hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_chain));
+  HIPCHK(hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_chain));
+  // the third chain stream only when asked for (PZK_SMT_CHAINS=3)
+  if (getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
+    HIPCHK(hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_chain));
+  if (post_chain_split(shared)) HIPCHK(hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, I->prio_lo));
+  return 0;
+}
+
 // One call, with the instance lock held and the device set.
 //
 // Pipelining: call k uses scratch set k % nsets and four instance streams — main (the
@@ -679,7 +702,9 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
                         int32_t* d_status, const pzk_exec* exec, hipStream_t dep = nullptr) {
   const int set = (int)(I->calls % I->nsets);
   Scratch& S = I->scr[set];
-  int rc = ensure_scratch(I, S, batch);
+  int rc = ensure_chain_streams(I);
+  if (rc) return rc;
+  rc = ensure_scratch(I, S, batch);
   if (rc) return rc;
   I->calls++;
   hipStream_t user = (exec && exec->stream) ? (hipStream_t)exec->stream : nullptr;
@@ -789,8 +814,13 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     if ((rc = emit(E_QRY, s_sha))) return rc;
     if ((rc = emit(E_BITS, s_sha))) return rc;  // Num2Bits(254) of the tree position reads level 3
   } else if (!lay.is_register) {
-    // standalone circuits (PoseidonHash(n), the SHA hashers): the core on the main stream, the emitters on the emit
-    // stream behind it, so call k's emitters run beside call k + 1's core (config 1: PoseidonHash(2))
+    // standalone circuits: the core on the main stream; PoseidonHash(n)'s emitters on the emit stream behind it, so
+    // call k's emitters run beside call k + 1's core (config 1 27.2M -> 28.7M witnesses/s); the SHA hashers' stay on
+    // the main stream (config 2 200k serial vs 175k overlapped: the SHA core took 4x longer beside the emitter,
+    // profiles/r5j). PZK_OVERLAP=0|1 forces one (A/B).
+    static const char* ov_env = getenv("PZK_OVERLAP");
+    const bool overlap = ov_env ? atoi(ov_env) != 0 : L.n_sha == 0;
+    if (!overlap) s_emit = st;
     { PhaseScope ps(T, slot, PH_SHA_CORE, st);
       HIPCHK(launch_sha_core(L, d_inputs, S.d_derived, 0, L.n_sha, S.d_sha_core, d_status, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(0, 1 << 20))) return rc; }

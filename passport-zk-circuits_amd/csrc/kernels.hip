@@ -275,7 +275,8 @@ __device__ __forceinline__ void emit_gen_body(const DevLayout& L, const Work* wo
     }
 }
 
-__global__ void __launch_bounds__(EMIT_THREADS) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
+// (at most 96 VGPRs: five workgroups per CU instead of four at 112; LDS allows nine)
+__global__ void __launch_bounds__(EMIT_THREADS, 5) k_emit_gen(DevLayout L, const Work* work, Bufs B) {
   emit_gen_body<false>(L, work, B);
 }
 // QueryIdentity's small regions (query.hpp): the same packed emitter with its own element function, so

@@ -27,9 +27,10 @@ static __device__ unsigned long long g_pos_prof[2];
 // stores of witness k are still in flight while the image of witness k + 1 is computed, so one workgroup
 // overlaps its own compute with its store drain; the block's descriptors are loaded once per WPB witnesses.
 template <int T, int MM>
-__global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
+// (t <= 3: at most 96 VGPRs, so five workgroups fit on a CU as their LDS allows; wider blocks are LDS-bound at <= 4)
+__global__ void __launch_bounds__(EMIT_THREADS, T <= 3 ? 5 : 1) k_emit_pos(DevLayout L, const Work* work, PosConsts K, ValueStore vs,
                                                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch,
-                                                          uint32_t wpb) {
+                                                          uint32_t wpb, bool kept_fill) {
   constexpr PosImg I(T);
   __shared__ fr img[I.size];
   const Work wk = work[blockIdx.x];
@@ -41,30 +42,47 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
   __shared__ uint16_t prog[pos_hash_size_c(T - 1)];
   const DescRun dr0 = desc_run<MM>(L, wtns, stride, 0, wk, R.off + wk.start, nullptr);
   const uint32_t cnt = dr0.count;
-  if (MM == MAP_DIRECT)
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = (uint16_t)dr0.prog[i];
-  else
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
-  __syncthreads();
-  const uint32_t tot = 2 * cnt;
   const uint32_t w0 = blockIdx.y * wpb, w1 = min(batch, w0 + wpb);
   // which of the workgroup's witnesses have zero inputs: tested before any store (wpb <= 64)
   uint64_t zmask = 0;
   for (uint32_t w = w0; w < w1; w++) zmask |= (uint64_t)pos_inputs_zero(task, vs, w) << (w - w0);
+  // (an O0 workgroup whose witnesses are all zero blocks copies zero rows and needs no program)
+  // mapped: the image parts the kept signals read (pos_img_need), so the fill skips the rest (the O2-shaped map keeps
+  // the S-box powers of a block: no GetSum row, no partial-round state)
+  __shared__ uint32_t need_s;
+  if (MM == MAP_DIRECT && kept_fill) {
+    if (threadIdx.x == 0) need_s = 0;
+    __syncthreads();
+    uint32_t need = 0;
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const uint32_t d = dr0.prog[i];
+      prog[i] = (uint16_t)d;
+      need |= pos_img_need<T>(d);
+    }
+    if (need) atomicOr(&need_s, need);
+  } else if (MM == MAP_DIRECT) {
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = (uint16_t)dr0.prog[i];
+  } else if (zmask != (w1 - w0 == 64 ? ~0ull : (1ull << (w1 - w0)) - 1)) {
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) prog[i] = L.pos_prog[L.pos_prog_off[T] + wk.start + i];
+  }
+  __syncthreads();
+  const uint32_t need = MM == MAP_DIRECT && kept_fill ? need_s : (uint32_t)PI_ALL;
+  const uint32_t tot = 2 * cnt;
   for (uint32_t w = w0; w < w1; w++) {
     if ((zmask >> (w - w0)) & 1) {
-      // zero inputs (the SMT levels below the insertion level): the block is the constant zero-input one; its
-      // elements are gathered straight from the image in global memory (L2-resident, 5 widths x <= 41 KB), U
-      // halves per lane loaded ahead of their stores (no core was written for this witness)
+      // zero inputs (the SMT levels below the insertion level): the block is the constant zero-input one (no core
+      // was written for this witness), read from global memory (L2-resident): O0, a straight copy of the block's
+      // zero row (K.Zrow); mapped, the kept elements gathered from the zero image through the compacted program.
+      // U halves per lane loaded ahead of their stores.
       constexpr int U = 8;
-      const uint4* z = reinterpret_cast<const uint4*>(K.Zimg(T));
       uint4* dst = reinterpret_cast<uint4*>(wtns + (size_t)w * stride) + 2 * dr0.out.g;
+      const uint4* z = reinterpret_cast<const uint4*>(MM == MAP_O0 ? K.Zrow(T) + wk.start : K.Zimg(T));
       for (uint32_t h0 = threadIdx.x; h0 < tot; h0 += U * blockDim.x) {
         uint4 v[U];
 #pragma unroll
         for (int k = 0; k < U; k++) {
           const uint32_t h = h0 + k * blockDim.x;
-          v[k] = h < tot ? z[2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u);
+          v[k] = h < tot ? z[MM == MAP_O0 ? h : 2u * prog[h >> 1] + (h & 1)] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
         for (int k = 0; k < U; k++) {
@@ -76,7 +94,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) k_emit_pos(DevLayout L, const Wo
     }
     __syncthreads();  // every lane has read the previous witness's image
     PZK_POS_CLK(t0);
-    pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w);
+    pos_img_fill<T>(img, K, pos_core + (size_t)w * L.pos_core_elems + task.core_off, vs, task, w, need);
     PZK_POS_ACC(0, t0);
     PZK_POS_CLK(t1);
     // two lanes per element (16 B each, 1 KiB contiguous per wave store), each copying its half
@@ -144,10 +162,11 @@ hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work
 #endif
   if (n_work == 0) return hipSuccess;
   const uint32_t wpb = pos_wpb();
+  static const bool kept_fill = getenv("PZK_POS_FULL") == nullptr;  // A/B: mapped blocks fill the whole image
   dim3 g(n_work, (batch + wpb - 1) / wpb), blk(EMIT_THREADS);
 #define PZK_POS_LAUNCH(T_)                                                                                              \
   hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<T_, MAP_DIRECT> : k_emit_pos<T_, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, \
-                     B.pos_core, B.wtns, B.stride, batch, wpb)
+                     B.pos_core, B.wtns, B.stride, batch, wpb, kept_fill)
   switch (t) {
     case 2: PZK_POS_LAUNCH(2); break;
     case 3: PZK_POS_LAUNCH(3); break;

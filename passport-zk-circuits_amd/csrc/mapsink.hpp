@@ -114,8 +114,11 @@ __device__ __forceinline__ uint32_t kept_collect(const OutRow& o, uint32_t a, ui
   return nk;
 }
 
-// the kept-offset list of mapped emit_run segments (one LDS array per kernel, whichever element functions it runs)
-constexpr uint32_t MAP_SEG = 2048;
+// the kept-offset list of mapped emit_run segments (one LDS array per kernel, whichever element functions it runs).
+// 26 bitmap words, sized for occupancy: with 2,048 the mapped k_emit_mm<32> took 40,984 B of LDS (24 B over a
+// quarter of the CU's 160 KiB: three workgroups per CU instead of four) and the mapped k_emit_sha 21,152 B (seven
+// instead of the eight its registers allow)
+constexpr uint32_t MAP_SEG = 1664;
 __device__ __forceinline__ uint16_t* map_seg_list() {
   __shared__ uint16_t klist[MAP_SEG];
   return klist;

@@ -25,6 +25,14 @@ __host__ __device__ constexpr uint32_t pos_zimg_off(int t) {
   return o;
 }
 constexpr uint32_t POS_ZIMG_TOTAL = pos_zimg_off(POS_MAX_T + 1);
+// ... followed by the zero-input blocks themselves in the O0 signal order (the image permuted by the width's block
+// program, pos_prog.hpp; built on the host at instance creation): a zero block of an O0 layout is a plain copy
+__host__ __device__ constexpr uint32_t pos_zrow_off(int t) {
+  uint32_t o = POS_ZIMG_TOTAL;
+  for (int u = 2; u < t; u++) o += pos_hash_size_c(u - 1);
+  return o;
+}
+constexpr uint32_t POS_ZBUF_TOTAL = pos_zrow_off(POS_MAX_T + 1);
 
 struct PosConsts {
   const fr* base;   // Montgomery-form constants
@@ -34,6 +42,7 @@ struct PosConsts {
   const fr* zimg;   // zero-input images and hashes (pos_zimg_off)
   __device__ __forceinline__ const fr* Zimg(int t) const { return zimg + pos_zimg_off(t); }
   __device__ __forceinline__ const fr& Zhash(int t) const { return zimg[pos_zimg_off(t) + PosImg(t).size]; }
+  __device__ __forceinline__ const fr* Zrow(int t) const { return zimg + pos_zrow_off(t); }
   __device__ __forceinline__ const fr& SC(int t, int i) const { return sbase[ix.s_off[t] + i]; }
   __device__ __forceinline__ const fr& Cn(int t, int i) const { return nbase[ix.c_off[t] + i]; }
   __device__ __forceinline__ const fr& C(int t, int i) const { return base[ix.c_off[t] + i]; }
@@ -294,9 +303,34 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
 // previous fill gave each lane one S-box chain OR one conversion in a branchy loop: waves holding both ran both, and
 // the 81 S-box chains of t = 3 occupied two waves for 4 product times while the others idled: 14.5 product-times
 // of wave work per block against 10.5 here.)
+// Image parts a block's stored signals may need beyond the S-box powers x^2, x^4, x^5 and the Ark outputs, which are
+// always filled: a mapped block (a .sym layout) fills only those its kept signals read (pos_img_need)
+enum : uint32_t {
+  PI_X = 1,     // S-box inputs x (full rounds; partial rounds' state 0)
+  PI_ST = 2,    // the other partial-round states and Y_RP
+  PI_MIX = 4,   // the GetSum rows: products, prefix sums (full mix, mixLast, partial mix)
+  PI_MISC = 8,  // hash inputs / output, the zero
+  PI_ALL = 15
+};
+template <int T>
+__device__ __forceinline__ uint32_t pos_img_need(uint32_t d) {  // the image part descriptor d reads
+  constexpr PosImg I(T);
+  if ((int)d < I.p2) return PI_X;
+  if ((int)d < I.fs) return 0;
+  if ((int)d < I.pin) return PI_MIX;
+  if ((int)d < I.pp2) {
+    const int k = (int)d - I.pin, r = k / T;
+    return (r < I.rp && k - r * T == 0) ? PI_X : PI_ST;
+  }
+  if ((int)d < I.ps) return 0;
+  if ((int)d < I.inp) return PI_MIX;
+  if ((int)d < I.pr) return PI_MISC;
+  return PI_MIX;
+}
+
 template <int T>
 __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const fr* core, const ValueStore& vs,
-                                             const PosTask& task, uint32_t w) {
+                                             const PosTask& task, uint32_t w, uint32_t need = PI_ALL) {
   constexpr int t = T;
   constexpr PosImg I(T);
   constexpr int RP = I.rp;
@@ -334,8 +368,9 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
   int ci = 0, din = 0, d2 = 0, d4 = 0, d5 = 0, dark = -1, cidx = 0;
   if (chain) sbox(tid, ci, din, d2, d4, d5, dark, cidx);
   fr xm = chain ? core[ci] : fr_zero(), x2m = xm, x2 = xm, x4 = xm;
+  const bool mix = need & PI_MIX;
   // step 1 (product): x^2 R = sqr(x R) | independent products [0, A1)
-  for (int q = tid; q < NS + A1; q += nt) {
+  for (int q = tid; q < NS + (mix ? A1 : 0); q += nt) {
     fr x = xm, y = xm;
     int e1 = -1, e2 = -1;
     if (q >= NS) aprod(q - NS, x, y, e1, e2);
@@ -343,12 +378,15 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (q < NS) x2m = r;
     else { img[e1] = r; img[e2] = r; }
   }
-  // step 2 (conversion): x^2 | S-box inputs, partial-round states, hash inputs / output, zero
-  for (int q = tid; q < NS + NF; q += nt) {
+  // step 2 (conversion): x^2 | S-box inputs, partial-round states, hash inputs / output, zero (the parts asked for)
+  const bool nx = need & PI_X, nst = need & PI_ST, nmisc = need & PI_MISC;
+  for (int q = tid; q < NS + (nx ? NS : 0) + (nst ? NC : 0) + (nmisc ? NF - NS - NC : 0); q += nt) {
     fr x = x2m;
     int e = q < NS ? d2 : -1;
     if (q >= NS) {
-      const int f = q - NS;
+      int f = q - NS;
+      if (!nx) f += NS;
+      if (f >= NS && !nst) f += NC;
       if (f < NS) {  // S-box input x
         int c_, i_, a_, b_, g_, h_, k_;
         sbox(f, c_, i_, a_, b_, g_, h_, k_);
@@ -372,7 +410,7 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (e >= 0) img[e] = r;
   }
   // step 3 (product): x^4 = (x^2 R) x^2 | independent products [A1, A1 + A3)
-  for (int q = tid; q < NS + A3; q += nt) {
+  for (int q = tid; q < NS + (mix ? A3 : 0); q += nt) {
     fr x = x2m, y = x2;
     int e1 = d4, e2 = -1;
     if (q >= NS) aprod(A1 + q - NS, x, y, e1, e2);
@@ -382,7 +420,7 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (e2 >= 0) img[e2] = r;
   }
   // step 4 (product): x^5 = x^4 (x R), Ark output | independent products [A1 + A3, NA)
-  for (int q = tid; q < NS + A4; q += nt) {
+  for (int q = tid; q < NS + (mix ? A4 : 0); q += nt) {
     fr x = x4, y = xm;
     int e1 = d5, e2 = -1;
     if (q >= NS) aprod(A1 + A3 + q - NS, x, y, e1, e2);
@@ -392,6 +430,7 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (q < NS && dark >= 0) img[dark] = fr_add(r, K.Cn(t, cidx));
   }
   __syncthreads();
+  if (!mix) return;
   // step 5 (product): the GetSum terms of an S-box output (full mix f, output i: Mat_f[k][i] * ark[f][k]; mixLast:
   // M[k][0] * x5[7][k]; partial r, k = 0: S[(2t-1) r] * (S-box output + Ark))
   constexpr int NFR = 7 * t;

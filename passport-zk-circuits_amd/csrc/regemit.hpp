@@ -866,6 +866,8 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never
   // straddles the start of a wave (K = 32: two rows per wave; K = 64: one)
+  // (mapped blocks with the sections merged into as few runs as the scan sections allow, one kept-list collection
+  // per 1,664 signals instead of one per section, measured 4 % slower on the O2-shaped line: profiles/r5p)
   mm_sections<K, 0, MM>(C, out, stage);
 }
 

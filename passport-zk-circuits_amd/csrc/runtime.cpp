@@ -189,7 +189,7 @@ struct pzk_instance {
   int nsets = 3;       // scratch sets in use (pipeline depth)
   int prio_lo = 0, prio_hi = 0;  // the device's stream priority range
   // ev_done[s][i]: end of the last call that used scratch set s, on stream i (main, rsa, sha, emit, tail, chain2)
-  static constexpr int NSTREAMS = 8;
+  static constexpr int NSTREAMS = 10;  // ev_done slots (the streams list at the end of batch_locked)
   hipEvent_t ev_done[NSETS][NSTREAMS] = {};
   hipEvent_t ev_gather[2] = {};  // end of the last gather out of d_o0[slot]
   hipStream_t s_emit = nullptr;
@@ -198,6 +198,13 @@ struct pzk_instance {
   // register calls: the emission that reads the SMT chain's output (the SMT level Poseidon blocks, the SMT regions),
   // one stream for every call so that a later call's writes of those regions follow an earlier call's
   hipStream_t s_post = nullptr;
+  // register calls, PZK_SIGEMIT=own (A/B): the signature emitters (k_emit_mm) on a stream of their own, so the next
+  // call's RSA core never queues behind them (PZK_MM_PRIO=hi|lo, default lo)
+  hipStream_t s_mm = nullptr;
+  // register calls with two SHA emitter streams (ensure_chain_streams): odd calls put the SHA emitters and the emission
+  // behind them (the s_sha role) on s_sha2, so consecutive calls' SHA emitters do not queue behind each other on one
+  // hardware queue (the O2-shaped line: that queue ran 90 % of the period and paced the pipeline, profiles/r5g)
+  hipStream_t s_sha2 = nullptr;
   uint64_t chain_rr = 0;           // register calls: SMT chain stream rotation
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
@@ -340,11 +347,28 @@ static int load_poseidon(pzk_instance* I) {
   HIPCHK(hipGetLastError());
   // the zero-input blocks (every PoseidonHash of zeros, e.g. the SMT levels below a proof's insertion level)
   fr* scratch = nullptr;
-  HIPCHK(hipMalloc(&I->d_pos_zimg, sizeof(fr) * POS_ZIMG_TOTAL));
+  HIPCHK(hipMalloc(&I->d_pos_zimg, sizeof(fr) * POS_ZBUF_TOTAL));
   HIPCHK(hipMalloc(&scratch, sizeof(fr) * (4 + 512)));
   HIPCHK(launch_pos_zero_img(I->pos_consts(), scratch, I->d_pos_zimg, nullptr));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipFree(scratch));
+  // the zero-input blocks in O0 signal order (PosConsts::Zrow): image element pos_prog[i] at row position i
+  const std::vector<uint16_t>& prog = I->lay.pos_prog;
+  if (!prog.empty()) {
+    std::vector<fr> buf(POS_ZBUF_TOTAL);
+    HIPCHK(hipMemcpy(buf.data(), I->d_pos_zimg, sizeof(fr) * POS_ZIMG_TOTAL, hipMemcpyDeviceToHost));
+    for (int t = 2; t <= POS_MAX_T; t++) {
+      const uint32_t n = pos_hash_size_c(t - 1), img = (uint32_t)PosImg(t).size;
+      if (I->lay.pos_prog_off[t] + n > prog.size()) return fail(PZK_E_DATA, "internal: Poseidon block program size");
+      for (uint32_t i = 0; i < n; i++) {
+        const uint16_t d = prog[I->lay.pos_prog_off[t] + i];
+        if (d >= img) return fail(PZK_E_DATA, "internal: Poseidon block descriptor out of the image");
+        buf[pos_zrow_off(t) + i] = buf[pos_zimg_off(t) + d];
+      }
+    }
+    HIPCHK(hipMemcpy(I->d_pos_zimg + POS_ZIMG_TOTAL, buf.data() + POS_ZIMG_TOTAL,
+                     sizeof(fr) * (POS_ZBUF_TOTAL - POS_ZIMG_TOTAL), hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -382,7 +406,8 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post, I->s_mm,
+                        I->s_sha2})
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab,
                        I->ev_smt, I->ev_chain})
@@ -416,7 +441,8 @@ struct DeviceGuard {
 
 // wait until every stream of the instance has drained (all calls issued so far are complete)
 static int sync_all(pzk_instance* I) {
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post})
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post, I->s_mm,
+                        I->s_sha2})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
@@ -501,7 +527,10 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
             hipStreamCreateWithPriority(&I->s_rsa, hipStreamNonBlocking, prio_hi) == hipSuccess;
   I->prio_lo = prio_lo;
   I->prio_hi = prio_hi;
-  ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+  // (PZK_SHA_PRIO=hi, A/B: the SHA emitter stream at high priority — give the process GPU_MAX_HW_QUEUES >= 5 then,
+  // or it shares a hardware queue with a chain stream)
+  static const bool sha_hi = getenv("PZK_SHA_PRIO") && !strcmp(getenv("PZK_SHA_PRIO"), "hi");
+  ok = ok && hipStreamCreateWithPriority(&I->s_sha, hipStreamNonBlocking, sha_hi ? prio_hi : prio_lo) == hipSuccess &&
        hipStreamCreateWithPriority(&I->s_emit, hipStreamNonBlocking, prio_lo) == hipSuccess;
   // the chain streams: QueryIdentity's now (its third / fourth chain, high priority); the register circuit's at its
   // first call (ensure_chain_streams), when it is known whether other register instances share the process
@@ -684,6 +713,19 @@ static int ensure_chain_streams(pzk_instance* I) {
   if (getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
     HIPCHK(hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_chain));
   if (post_chain_split(shared)) HIPCHK(hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, I->prio_lo));
+  static const char* se_env = getenv("PZK_SIGEMIT");
+  if (se_env && !strcmp(se_env, "own") && !shared && !I->lay.is_ecdsa) {
+    static const char* mp_env = getenv("PZK_MM_PRIO");
+    const bool hi = mp_env && !strcmp(mp_env, "hi");
+    HIPCHK(hipStreamCreateWithPriority(&I->s_mm, hipStreamNonBlocking, hi ? I->prio_hi : I->prio_lo));
+  }
+  // two SHA emitter streams: default for mapped layouts keeping at most half of the signals (O2-shaped 206.9k ->
+  // 218.5k witnesses/s; O1-shaped, 56 % kept, 130.8k -> 130.2k: profiles/r5q); the O0 layout keeps one (+1 % with
+  // two, but each k_emit_sha launch then runs beside the other call's and takes twice as long: its roofline line
+  // would read 0.35 for the same HBM work, profiles/r5p). PZK_SHA_STREAMS=1|2 forces either.
+  const char* ss_env = getenv("PZK_SHA_STREAMS");
+  const bool sha2 = ss_env ? atoi(ss_env) >= 2 : I->d_keep_bits != nullptr && 2 * I->out_size <= I->lay.wit_size;
+  if (sha2 && !shared) HIPCHK(hipStreamCreateWithPriority(&I->s_sha2, hipStreamNonBlocking, I->prio_lo));
   return 0;
 }
 
@@ -779,7 +821,8 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     return 0;
   };
-  hipStream_t s_rsa = serial ? st : I->s_rsa, s_sha = serial ? st : I->s_sha, s_emit = serial ? st : I->s_emit,
+  hipStream_t s_rsa = serial ? st : I->s_rsa, s_emit = serial ? st : I->s_emit,
+              s_sha = serial ? st : I->s_sha2 && lay.is_register && (I->calls & 1) ? I->s_sha2 : I->s_sha,
               s_own = serial ? st : I->s_tail;
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);
@@ -886,7 +929,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // behind this call's EC table emitter. Tuning switch PZK_SIGEMIT=rsa|emit forces one placement.
     static const char* se_env = getenv("PZK_SIGEMIT");
     const bool sig_on_rsa = se_env ? strcmp(se_env, "emit") != 0 : !lay.is_ecdsa;
-    hipStream_t s_sig = sig_on_rsa ? s_rsa : s_emit;
+    hipStream_t s_sig = I->s_mm && !serial ? I->s_mm : sig_on_rsa ? s_rsa : s_emit;
     HIPCHK(hipStreamWaitEvent(s_sig, I->ev_rsa, 0));
     if ((rc = emit(E_MM, s_sig))) return rc;
     if ((rc = emit(E_SHAD, s_sig))) return rc;
@@ -979,7 +1022,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
   }
   auto or_st = [&](hipStream_t s) { return serial || !s ? st : s; };  // streams an instance does not have: st
   hipStream_t streams[pzk_instance::NSTREAMS] = {st, s_rsa, s_sha, s_emit, s_own, or_st(I->s_chain2),
-                                                 or_st(I->s_chain3), or_st(I->s_post)};
+                                                 or_st(I->s_chain3), or_st(I->s_post), or_st(I->s_mm), st};  // (s_sha2: in slot 2 when used)
   for (int i = 0; i < pzk_instance::NSTREAMS; i++) HIPCHK(hipEventRecord(I->ev_done[set][i], streams[i]));
   if (user) {
     for (hipEvent_t e : I->ev_done[set]) HIPCHK(hipStreamWaitEvent(user, e, 0));

@@ -379,27 +379,44 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // All 64 lanes of the wave call this; lane l holds element l of the wave's run starting at
-// wave_out; only the first nvalid elements are stored. stage: 128 uint4 of LDS per wave.
+// wave_out; only the first nvalid elements are stored. stage: SW uint4 of LDS per wave — 128, or 64 (half the LDS,
+// the two 1 KiB stores staged one after the other: for kernels whose LDS bounds their workgroups per CU)
+template <int SW = 128>
 __device__ __forceinline__ void wave_store(uint8_t* wave_out, const El& e, uint32_t nvalid, uint4* stage) {
   const uint32_t lane = threadIdx.x & 63;
-  stage[2 * lane] = e.lo;
-  stage[2 * lane + 1] = e.hi;
-  wave_sync();
-  const uint4 a = stage[lane], b = stage[64 + lane];
   uint4* d = reinterpret_cast<uint4*>(wave_out);
-  if (lane < 2 * nvalid) d[lane] = a;
-  if (64 + lane < 2 * nvalid) d[64 + lane] = b;
-  wave_sync();
+  if constexpr (SW == 128) {
+    stage[2 * lane] = e.lo;
+    stage[2 * lane + 1] = e.hi;
+    wave_sync();
+    const uint4 a = stage[lane], b = stage[64 + lane];
+    if (lane < 2 * nvalid) d[lane] = a;
+    if (64 + lane < 2 * nvalid) d[64 + lane] = b;
+    wave_sync();
+  } else {
+    static_assert(SW == 64, "stage: 128 or 64 uint4 per wave");
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      if ((lane >> 5) == h) {
+        stage[2 * (lane & 31)] = e.lo;
+        stage[2 * (lane & 31) + 1] = e.hi;
+      }
+      wave_sync();
+      const uint4 a = stage[lane];
+      if (64 * h + lane < 2 * nvalid) d[64 * h + lane] = a;
+      wave_sync();
+    }
+  }
 }
 // for (q < count) out[q] = f(q), wave-contiguous; f(q) is evaluated only for q < count
-template <typename F>
+template <int SW = 128, typename F>
 __device__ __forceinline__ void emit_run(uint8_t* out, uint32_t count, uint4* stage_block, F f) {
   const uint32_t lane = threadIdx.x & 63;
-  uint4* stage = stage_block + (threadIdx.x >> 6) * 128;
+  uint4* stage = stage_block + (threadIdx.x >> 6) * SW;
   for (uint32_t q0 = threadIdx.x - lane; q0 < count; q0 += blockDim.x) {
     const uint32_t q = q0 + lane;
     const El e = q < count ? f(q) : el_zero();
-    wave_store(out + 32ull * q0, e, count - q0 < 64 ? count - q0 : 64, stage);
+    wave_store<SW>(out + 32ull * q0, e, count - q0 < 64 ? count - q0 : 64, stage);
   }
 }
 

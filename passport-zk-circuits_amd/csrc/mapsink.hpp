@@ -131,14 +131,14 @@ __device__ __forceinline__ uint16_t* map_seg_list() {
 // elements of a run are consecutive in a monotone map). LANE_INDEP = false: f scans across the wave's lanes
 // (regemit.hpp bmneq_tmpr needs 64 consecutive q per wave), so every element of a wave with a kept one is
 // evaluated in O0 order and the kept ones are compacted through the stage.
-template <int MM = MAP_ANY, bool LANE_INDEP = true, typename F>
+template <int MM = MAP_ANY, bool LANE_INDEP = true, int SW = 128, typename F>
 __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4* stage_block, F f) {
   if (MM == MAP_O0 || (MM == MAP_ANY && !o.map.bits)) {
-    emit_run(o.row + 32ull * o.g, count, stage_block, f);
+    emit_run<SW>(o.row + 32ull * o.g, count, stage_block, f);
     return;
   }
   const uint32_t lane = threadIdx.x & 63;
-  uint4* stage = stage_block + (threadIdx.x >> 6) * 128;
+  uint4* stage = stage_block + (threadIdx.x >> 6) * SW;
   if constexpr (LANE_INDEP) {
     uint16_t* klist = map_seg_list();
     for (uint32_t a = 0; a < count; a += MAP_SEG) {
@@ -149,7 +149,7 @@ __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4*
       for (uint32_t k0 = threadIdx.x - lane; k0 < nk; k0 += blockDim.x) {
         const uint32_t k = k0 + lane;
         const El e = k < nk ? f(a + klist[k]) : el_zero();
-        wave_store(dst + 32ull * k0, e, nk - k0 < 64 ? nk - k0 : 64, stage);
+        wave_store<SW>(dst + 32ull * k0, e, nk - k0 < 64 ? nk - k0 : 64, stage);
       }
       __syncthreads();  // klist is rewritten by the next segment
     }
@@ -162,16 +162,30 @@ __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4*
       if (mask == 0) continue;  // wave-uniform
       const El e = q < count ? f(q) : el_zero();
       const uint32_t pos = (uint32_t)__popcll(mask & ((1ull << lane) - 1)), nk = (uint32_t)__popcll(mask);
-      if (keep) {
-        stage[2 * pos] = e.lo;
-        stage[2 * pos + 1] = e.hi;
-      }
-      wave_sync();
-      const uint4 a = stage[lane], b = stage[64 + lane];
       uint4* d = reinterpret_cast<uint4*>(o.row + 32ull * map_rank(m, o.g + q0));
-      if (lane < 2 * nk) d[lane] = a;
-      if (64 + lane < 2 * nk) d[64 + lane] = b;
-      wave_sync();
+      if constexpr (SW == 128) {
+        if (keep) {
+          stage[2 * pos] = e.lo;
+          stage[2 * pos + 1] = e.hi;
+        }
+        wave_sync();
+        const uint4 a = stage[lane], b = stage[64 + lane];
+        if (lane < 2 * nk) d[lane] = a;
+        if (64 + lane < 2 * nk) d[64 + lane] = b;
+        wave_sync();
+      } else {
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {  // kept elements 32 h .. 32 h + 31
+          if (keep && (pos >> 5) == h) {
+            stage[2 * (pos & 31)] = e.lo;
+            stage[2 * (pos & 31) + 1] = e.hi;
+          }
+          wave_sync();
+          const uint4 a = stage[lane];
+          if (64 * h + lane < 2 * nk) d[64 * h + lane] = a;
+          wave_sync();
+        }
+      }
     }
   }
 }

@@ -398,10 +398,21 @@ struct MMCore {
   bool kara;                                      // x*y by KaratsubaOverflow (K = 2^m), else schoolbook
   const uint64_t* kt_lo;                          // LDS Karatsuba input table (K = 32 / 64; else null)
   const uint8_t* kt_hi;
-  const uint64_t* ko;                             // LDS node outputs of the upper Karatsuba levels (K = 32 / 64; else null)
+  const uint32_t* ko;                             // LDS node outputs of the upper Karatsuba levels, 5 words each (ko5_at;
+                                                  // K = 32 / 64; else null)
   __device__ __forceinline__ uint64_t X(int i) const { return i < K ? x[i] : 0; }
 };
 __device__ __forceinline__ U192 u192_at(const uint64_t* a, int i) { U192 r; r.a0 = a[3 * i]; r.a1 = a[3 * i + 1]; r.a2 = a[3 * i + 2]; return r; }
+// a Karatsuba node output (< 2^139) in 5 LDS words: 20 instead of 24 bytes per value, so the mapped / O0 k_emit_mm<32>
+// fits five workgroups per CU
+__device__ __forceinline__ U192 ko5_at(const uint32_t* a, int i) {
+  const uint32_t* p = a + 5 * i;
+  U192 r;
+  r.a0 = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
+  r.a1 = (uint64_t)p[2] | ((uint64_t)p[3] << 32);
+  r.a2 = p[4];
+  return r;
+}
 __device__ __forceinline__ void u192_addto(U192& a, const U192& b) {
   uint64_t s0 = a.a0 + b.a0; uint64_t c = s0 < b.a0;
   uint64_t s1 = a.a1 + b.a1; uint64_t c1 = s1 < b.a1; uint64_t s1b = s1 + c; c1 += s1b < s1;
@@ -583,7 +594,7 @@ constexpr int KO_LEVELS = 3, KO_VALUES = 456;  // 3 x 32 + 9 x 16 + 27 x 8 node 
 __device__ __forceinline__ int kt_level_base(int l) {  // first table entry of level l >= 1 (2N entries per node)
   return l == 1 ? 0 : l == 2 ? 96 : l == 3 ? 240 : l == 4 ? 456 : 780;
 }
-__device__ __forceinline__ El kara_el32(const MMCore& C, const uint64_t* ko, uint32_t s) {
+__device__ __forceinline__ El kara_el32(const MMCore& C, const uint32_t* ko, uint32_t s) {
   constexpr uint32_t SZ[6] = {mm_kara_size(32), mm_kara_size(16), mm_kara_size(8), mm_kara_size(4), mm_kara_size(2),
                               mm_kara_size(1)};
   int lvl = 0, m = 0;
@@ -608,7 +619,7 @@ __device__ __forceinline__ El kara_el32(const MMCore& C, const uint64_t* ko, uin
   }
   if (p == 2u * N - 1) return el_zero();  // top coefficient (K(1).out[1] never assigned)
   if (lvl == 0) return el_w(u192w(u192_at(C.cxy, (int)p)));
-  if (lvl <= KO_LEVELS) return el_w(u192w(u192_at(ko, kt_level_base(lvl) + m * 2 * N + (int)p)));
+  if (lvl <= KO_LEVELS) return el_w(u192w(ko5_at(ko, kt_level_base(lvl) + m * 2 * N + (int)p)));
   const int tb = kt_level_base(lvl) + m * 2 * N, lo = (int)p < N ? 0 : (int)p - N + 1, hi = (int)p < N ? (int)p : N - 1;
   U192 acc;
   for (int u = lo; u <= hi; u++)  // <= 2 terms (N <= 2)
@@ -628,7 +639,7 @@ __host__ __device__ constexpr int kt_base64(int l) {  // first table entry of le
   return l <= 1 ? 0 : l == 2 ? 192 : l == 3 ? 480 : l == 4 ? 912 : 1560;
 }
 constexpr int K64_TL_VALUES = kt_base64(K64_TL + 1), K64_OL_VALUES = kt_base64(K64_OL + 1);  // 1560, 480
-__device__ __forceinline__ El kara_el64(const MMCore& C, const uint64_t* ko, uint32_t s) {
+__device__ __forceinline__ El kara_el64(const MMCore& C, const uint32_t* ko, uint32_t s) {
   constexpr uint32_t SZ[7] = {mm_kara_size(64), mm_kara_size(32), mm_kara_size(16), mm_kara_size(8),
                               mm_kara_size(4), mm_kara_size(2), mm_kara_size(1)};
   int lvl = 0, m = 0;
@@ -679,7 +690,7 @@ __device__ __forceinline__ El kara_el64(const MMCore& C, const uint64_t* ko, uin
   }
   if (p == 2u * N - 1) return el_zero();  // top coefficient (K(1).out[1] never assigned)
   if (lvl == 0) return el_w(u192w(u192_at(C.cxy, (int)p)));
-  if (lvl <= K64_OL) return el_w(u192w(u192_at(ko, kt_base64(lvl) + m * 2 * N + (int)p)));
+  if (lvl <= K64_OL) return el_w(u192w(ko5_at(ko, kt_base64(lvl) + m * 2 * N + (int)p)));
   const int lo_u = (int)p < N ? 0 : (int)p - N + 1, hi_u = (int)p < N ? (int)p : N - 1;
   U192 acc;
   for (int u = lo_u; u <= hi_u; u++) {
@@ -748,6 +759,9 @@ static __device__ unsigned long long g_mm_prof[MM_SECTIONS + 2];
 #define PZK_MM_ACC(i, t0)
 #endif
 
+// the BigMultModP emitter's store stage: 64 uint4 per wave (wave_store's two-round form), which with the 5-word node
+// outputs brings k_emit_mm<32> to 31 KB of LDS: five workgroups per CU instead of four
+constexpr int MM_STAGE = 64;
 template <int K, int SEC, int MM>
 __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, uint4* stage) {
   if constexpr (SEC < (int)MM_SECTIONS) {
@@ -756,7 +770,7 @@ __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, u
     PZK_MM_CLK(t0);
     // tmpResult rows (and BigMultNonEqualOverflow's, K != 32) are segmented scans across the wave (bmneq_tmpr)
     constexpr bool INDEP = !(SEC == MM_TMPR || (SEC == MM_KARA && (K & (K - 1)) != 0));
-    emit_run<MM, INDEP>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    emit_run<MM, INDEP, MM_STAGE>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
     PZK_MM_ACC(SEC, t0);
     mm_sections<K, SEC + 1, MM>(C, out, stage);
   }
@@ -843,7 +857,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
   // outputs of the Karatsuba nodes of levels 1..KO_LEVELS (K = 32): out[s] = sum_u in1[u] in2[s - u] over the
   // node's table inputs, once per workgroup (kara_el32 reads them)
   constexpr int KON = K == KT_K ? 3 * KO_VALUES : K == 64 ? 3 * K64_OL_VALUES : 1;
-  __shared__ uint64_t ko[KON];
+  __shared__ uint32_t ko[(KON + 2) / 3 * 5];
   if (K == KT_K || K == 64) {
     for (int r = threadIdx.x; r < (K == KT_K ? KO_VALUES : K64_OL_VALUES); r += blockDim.x) {
       const int l = K == KT_K ? (r < 96 ? 1 : r < 240 ? 2 : 3) : (r < kt_base64(2) ? 1 : 2), N = K >> l;
@@ -853,7 +867,9 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
       if (p < 2 * N - 1)
         for (int u = p < N ? 0 : p - N + 1; u <= (p < N ? p : N - 1); u++)
           mac2(acc, kt_lo[tb + u], kt_hi[tb + u], kt_lo[tb + N + p - u], kt_hi[tb + N + p - u]);
-      ko[3 * r] = acc.a0; ko[3 * r + 1] = acc.a1; ko[3 * r + 2] = acc.a2;
+      uint32_t* o = ko + 5 * r;
+      o[0] = (uint32_t)acc.a0; o[1] = (uint32_t)(acc.a0 >> 32); o[2] = (uint32_t)acc.a1; o[3] = (uint32_t)(acc.a1 >> 32);
+      o[4] = (uint32_t)acc.a2;
     }
     __syncthreads();
   }
@@ -861,7 +877,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
            cxy, cqn, (K & (K - 1)) == 0, K == KT_K || K == 64 ? kt_lo : nullptr, K == KT_K || K == 64 ? kt_hi : nullptr,
            K == KT_K || K == 64 ? ko : nullptr};
   const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
-  __shared__ uint4 stage[2 * 256];
+  __shared__ uint4 stage[MM_STAGE * 4];
   PZK_MM_ACC(MM_SECTIONS, tp);  // prologue: core loads, column sums, Karatsuba input table
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never

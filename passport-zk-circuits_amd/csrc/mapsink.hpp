@@ -119,8 +119,9 @@ __device__ __forceinline__ uint32_t kept_collect(const OutRow& o, uint32_t a, ui
 // quarter of the CU's 160 KiB: three workgroups per CU instead of four) and the mapped k_emit_sha 21,152 B (seven
 // instead of the eight its registers allow)
 constexpr uint32_t MAP_SEG = 1664;
+template <uint32_t SEG = MAP_SEG>
 __device__ __forceinline__ uint16_t* map_seg_list() {
-  __shared__ uint16_t klist[MAP_SEG];
+  __shared__ uint16_t klist[SEG];
   return klist;
 }
 
@@ -131,7 +132,7 @@ __device__ __forceinline__ uint16_t* map_seg_list() {
 // elements of a run are consecutive in a monotone map). LANE_INDEP = false: f scans across the wave's lanes
 // (regemit.hpp bmneq_tmpr needs 64 consecutive q per wave), so every element of a wave with a kept one is
 // evaluated in O0 order and the kept ones are compacted through the stage.
-template <int MM = MAP_ANY, bool LANE_INDEP = true, int SW = 128, typename F>
+template <int MM = MAP_ANY, bool LANE_INDEP = true, int SW = 128, uint32_t SEG = MAP_SEG, typename F>
 __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4* stage_block, F f) {
   if (MM == MAP_O0 || (MM == MAP_ANY && !o.map.bits)) {
     emit_run<SW>(o.row + 32ull * o.g, count, stage_block, f);
@@ -140,9 +141,9 @@ __device__ __forceinline__ void emit_run(const OutRow& o, uint32_t count, uint4*
   const uint32_t lane = threadIdx.x & 63;
   uint4* stage = stage_block + (threadIdx.x >> 6) * SW;
   if constexpr (LANE_INDEP) {
-    uint16_t* klist = map_seg_list();
-    for (uint32_t a = 0; a < count; a += MAP_SEG) {
-      const uint32_t n = min(MAP_SEG, count - a);
+    uint16_t* klist = map_seg_list<SEG>();
+    for (uint32_t a = 0; a < count; a += SEG) {
+      const uint32_t n = min(SEG, count - a);
       const uint32_t r0 = map_rank_at(o.map, o.g + a);
       const uint32_t nk = kept_collect(o, a, n, klist, [](uint32_t q) { return (uint16_t)q; });
       uint8_t* dst = o.row + 32ull * r0;

@@ -762,6 +762,8 @@ static __device__ unsigned long long g_mm_prof[MM_SECTIONS + 2];
 // the BigMultModP emitter's store stage: 64 uint4 per wave (wave_store's two-round form), which with the 5-word node
 // outputs brings k_emit_mm<32> to 31 KB of LDS: five workgroups per CU instead of four
 constexpr int MM_STAGE = 64;
+// and its mapped kept-list segments: 896 signals (14 bitmap words), so the mapped k_emit_mm<32> also fits five per CU
+constexpr uint32_t MM_SEG = 896;
 template <int K, int SEC, int MM>
 __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, uint4* stage) {
   if constexpr (SEC < (int)MM_SECTIONS) {
@@ -770,7 +772,7 @@ __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, u
     PZK_MM_CLK(t0);
     // tmpResult rows (and BigMultNonEqualOverflow's, K != 32) are segmented scans across the wave (bmneq_tmpr)
     constexpr bool INDEP = !(SEC == MM_TMPR || (SEC == MM_KARA && (K & (K - 1)) != 0));
-    emit_run<MM, INDEP, MM_STAGE>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
+    emit_run<MM, INDEP, MM_STAGE, MM_SEG>(out.at(a), n, stage, [=](uint32_t q) { return mm_el<K, SEC>(C, q); });
     PZK_MM_ACC(SEC, t0);
     mm_sections<K, SEC + 1, MM>(C, out, stage);
   }
@@ -899,7 +901,8 @@ __device__ __forceinline__ uint32_t bjj_step_of(uint32_t s) { return s < 46 ? 0 
 __device__ __forceinline__ uint32_t bjj_sig_of(uint32_t i) { return i == 0 ? 0 : 46 + 60 * (i - 1); }
 
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
-__global__ void __launch_bounds__(256) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
+// (at most 80 VGPRs: six workgroups per CU, as its LDS allows, instead of five at 88)
+__global__ void __launch_bounds__(256, 6) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
   __shared__ fr rec[(BJJ_EMIT_STEPS + 1) * BR_N];
   __shared__ uint32_t bits[BJJ_EMIT_STEPS + 1];
   const Work wk = work[blockIdx.x];

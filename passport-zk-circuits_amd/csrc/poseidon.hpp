@@ -378,27 +378,34 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     if (q < NS) x2m = r;
     else { img[e1] = r; img[e2] = r; }
   }
-  // step 2 (conversion): x^2 | S-box inputs, partial-round states, hash inputs / output, zero (the parts asked for)
+  // step 2 (conversion): x^2 | S-box inputs, partial-round states, hash inputs / output, zero (the parts asked for).
+  // With the GetSum rows built, an S-box input other than layers 0 and 4 is the previous mix's output — its row's
+  // last prefix sum — and is copied from there at the end (a copy instead of a conversion: 77 of t = 3's 81)
   const bool nx = need & PI_X, nst = need & PI_ST, nmisc = need & PI_MISC;
-  for (int q = tid; q < NS + (nx ? NS : 0) + (nst ? NC : 0) + (nmisc ? NF - NS - NC : 0); q += nt) {
+  const int NXC = nx ? (mix ? 2 * t : NS) : 0;
+  for (int q = tid; q < NS + NXC + (nst ? NC : 0) + (nmisc ? NF - NS - NC : 0); q += nt) {
     fr x = x2m;
     int e = q < NS ? d2 : -1;
     if (q >= NS) {
       int f = q - NS;
-      if (!nx) f += NS;
-      if (f >= NS && !nst) f += NC;
-      if (f < NS) {  // S-box input x
+      if (f < NXC) {  // S-box input x (mix: layers 0 and 4 only)
         int c_, i_, a_, b_, g_, h_, k_;
-        sbox(f, c_, i_, a_, b_, g_, h_, k_);
+        sbox(mix ? (f < t ? f : 3 * t + f) : f, c_, i_, a_, b_, g_, h_, k_);
         x = core[c_]; e = i_;
-      } else if (f < NS + NC) {
-        const int c = f - NS;
+        f = -1;
+      } else {
+        f -= NXC;
+        if (!nst) f += NC;
+      }
+      if (f < 0) {
+      } else if (f < NC) {
+        const int c = f;
         int r, i;
         if (c < RP * (t - 1)) { r = c / (t - 1); i = 1 + (c - r * (t - 1)); }
         else { r = RP; i = c - RP * (t - 1); }
         x = core[4 * t + r * t + i]; e = I.pin + r * t + i;
       } else {
-        const int k = f - NS - NC;
+        const int k = f - NC;
         x = fr_zero();
         if (k < task.n) { x = vs.at(task.in_slot[k], w); e = I.inp + k; }
         else if (k == 5) { x = vs.at(task.out_slot, w); e = I.hash; }
@@ -467,6 +474,23 @@ __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const 
     fr acc = img[base];
 #pragma unroll
     for (int k = 1; k < t; k++) { acc = fr_add(acc, img[base + k]); img[base + k] = acc; }
+  }
+  __syncthreads();
+  if (!nx) return;
+  // the S-box inputs of full layers 1-3, 5-7 (the mix after layer f - 1, full row (f - 1, j)) and of the partial
+  // rounds (round 0: the P mix after layer 3, full row (3, 0); round r: the partial mix of round r - 1)
+  for (int q = tid; q < NS; q += nt) {
+    int src = -1, dst;
+    if (q < 8 * t) {
+      const int f = q / t, j = q - f * t;
+      if (f != 0 && f != 4) src = I.fs + ((f - 1) * t + j) * t + t - 1;
+      dst = I.in + q;
+    } else {
+      const int r = q - 8 * t;
+      src = r == 0 ? I.fs + (3 * t) * t + t - 1 : I.ps + (r - 1) * t + t - 1;
+      dst = I.pin + r * t;
+    }
+    if (src >= 0) img[dst] = img[src];
   }
   __syncthreads();
 }

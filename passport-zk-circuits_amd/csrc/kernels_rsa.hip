@@ -79,9 +79,15 @@ hipError_t launch_emit_mm(const DevLayout& L, const Work* work, uint32_t n_work,
   }
 #endif
   if (n_work == 0) return hipSuccess;
-  dim3 g(n_work, batch), blk(EMIT_THREADS);
   const bool m = L.keep.bits != nullptr;  // store mode (mapsink.hpp)
-  auto kern = L.reg.K == 32 ? (m ? k_emit_mm<32, MAP_DIRECT> : k_emit_mm<32, MAP_O0>)
+  // O0 K = 32: eight waves per workgroup (35 KB of LDS, three per CU by registers: 24 waves instead of 5 x 4 = 20, the
+  // prologue's column sums and tables on twice the threads): config 3 +1.0 % on one box, k_emit_sha's share of
+  // the chip up with it (profiles/r5z). PZK_MM_THREADS=256 restores four waves.
+  static const bool wide = !getenv("PZK_MM_THREADS") || atoi(getenv("PZK_MM_THREADS")) != 256;
+  const bool w512 = wide && !m && L.reg.K == 32;
+  dim3 g(n_work, batch), blk(w512 ? 512 : EMIT_THREADS);
+  auto kern = w512 ? k_emit_mm<32, MAP_O0, 512>
+            : L.reg.K == 32 ? (m ? k_emit_mm<32, MAP_DIRECT> : k_emit_mm<32, MAP_O0>)
             : L.reg.K == 48 ? (m ? k_emit_mm<48, MAP_DIRECT> : k_emit_mm<48, MAP_O0>)
                             : (m ? k_emit_mm<64, MAP_DIRECT> : k_emit_mm<64, MAP_O0>);
   hipLaunchKernelGGL(kern, g, blk, 0, st, L, work, B);

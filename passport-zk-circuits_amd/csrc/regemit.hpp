@@ -778,8 +778,8 @@ __device__ __forceinline__ void mm_sections(const MMCore C, const OutRow& out, u
   }
 }
 
-template <int K, int MM>
-__global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
+template <int K, int MM, int NT = 256>
+__global__ void __launch_bounds__(NT) k_emit_mm(DevLayout L, const Work* work, Bufs B) {
   __shared__ uint64_t lds[MM_CORE_WORDS(K) + K + 3 * (4 * K - 1)];
   PZK_MM_CLK(tp);
   const Work wk = work[blockIdx.x];
@@ -793,7 +793,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
 #else
   // every load issued before any LDS write: a load / write loop waits out one HBM round trip per iteration, and
   // under the emitters' store stream that is several microseconds each (MM_CORE_WORDS(32) = 381: two per thread)
-  constexpr int MM_NT = 256, CW = MM_CORE_WORDS(K), CL = (CW + MM_NT - 1) / MM_NT;
+  constexpr int MM_NT = NT, CW = MM_CORE_WORDS(K), CL = (CW + MM_NT - 1) / MM_NT;
   uint64_t cv[CL];
 #pragma unroll
   for (int k = 0; k < CL; k++) {
@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(256) k_emit_mm(DevLayout L, const Work* work, 
            cxy, cqn, (K & (K - 1)) == 0, K == KT_K || K == 64 ? kt_lo : nullptr, K == KT_K || K == 64 ? kt_hi : nullptr,
            K == KT_K || K == 64 ? ko : nullptr};
   const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
-  __shared__ uint4 stage[MM_STAGE * 4];
+  __shared__ uint4 stage[MM_STAGE * (NT / 64)];
   PZK_MM_ACC(MM_SECTIONS, tp);  // prologue: core loads, column sums, Karatsuba input table
   // section by section, each with its own specialised element function (mm_el<K, SEC>): every
   // wave works inside one section, and each section starts wave-aligned, so a tmpResult row never

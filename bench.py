@@ -726,11 +726,37 @@ def host_delivered(args, inst, sig, n=None):
     dt = time.perf_counter() - t0
     assert seen["n"] == n, seen
     row_bytes = 32 * inst.witness_size
+    link = d2h_link_gbs()
+    gbs = n * row_bytes / dt / 1e9
     return {"what": "pzk_witness_stream: inputs from host memory, witnesses into pinned host memory (device->host "
                     "copy of chunk c beside the compute of chunk c + 1), every row handed to a host sink",
             "value": round(n / dt, 2), "unit": "witnesses/s", "witnesses": n, "seconds": round(dt, 3),
-            "row_bytes": row_bytes, "gb_per_s": round(n * row_bytes / dt / 1e9, 2),
+            "row_bytes": row_bytes, "layout": "mapped (%s)" % args.sym if args.sym else "O0",
+            "gb_per_s": round(gbs, 2),
+            "link": {"what": "the host link the rows cross: PCIe 5.0 x16 device->host, 64 GB/s per direction "
+                             "theoretical; measured = one 4 GiB device->pinned-host copy on this box",
+                     "theoretical_gbs": 64.0, "measured_gbs": link,
+                     "frac_of_measured": round(gbs / link, 3) if link else None},
             "sink_checks": {"rows": seen["n"], "status_nonzero": seen["bad"], "witness0_is_one": seen["one"]}}
+
+
+def d2h_link_gbs(nbytes=4 << 30):
+    """Device -> pinned host copy rate of one large buffer (the ceiling host delivery is measured against)."""
+    import torch
+    try:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        dst.copy_(src, non_blocking=True)  # warm
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        del src, dst
+        return round(nbytes / dt / 1e9, 2)
+    except RuntimeError:
+        return None
 
 
 def input_side(sig, distinct=128, n=8192):

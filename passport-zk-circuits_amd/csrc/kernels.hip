@@ -6,6 +6,7 @@
 
 #include "poseidon.hpp"
 #include "regcore.hpp"
+#include "smt_chain4.hpp"
 #include "pss.hpp"
 #include "regemit.hpp"
 #include "sha.hpp"
@@ -380,8 +381,7 @@ hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, f
   return hipGetLastError();
 }
 
-bool bjj_uses_scratch(bool chain_critical) {
-  (void)chain_critical;
+bool bjj_uses_scratch() {
   const char* v = getenv("PZK_BJJ");
   return v ? !strcmp(v, "scratch") : true;
 }
@@ -395,16 +395,26 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
-                            bool query, hipStream_t st) {
-  // PZK_CHAIN_MUL=inline (CIOS) | call (CIOS out of line) | fips (fr_mul_fast): A/B switch. Default FIPS: half the
-  // chain's VALU instructions; config 4 +2.1 % (profiles/r5e), QueryIdentity +2.2 % once six calls are in flight
-  // (245.1k -> 250.6k witnesses/s, profiles/r5m; with three, where the chain's latency showed, CIOS was 2.6 % ahead)
-  (void)query;
+                            hipStream_t st) {
+  // PZK_CHAIN=lane (A/B): the round-5 chain, one cooperative permutation on 4 lanes per witness with one-lane
+  // products (PZK_CHAIN_MUL=inline | call | fips picks its product); default: k_smt_chain4, 16 lanes per witness on
+  // quad-spread products (smt_chain4.hpp)
+  static const char* ch = getenv("PZK_CHAIN");
+  if (!ch || strcmp(ch, "lane") != 0) {
+    hipLaunchKernelGGL(k_smt_chain4, dim3((vs.batch * 16 + 255) / 256), dim3(256), 0, st, L, K, level_task, inputs, vs,
+                       pos_core, smt_core, order, status, vs.batch);
+    return hipGetLastError();
+  }
   static const char* pm = getenv("PZK_CHAIN_MUL");
   const int mode = !pm ? 2 : !strcmp(pm, "call") ? 1 : !strcmp(pm, "fips") ? 2 : 0;
   hipLaunchKernelGGL(mode == 1 ? k_smt_chain<FrMulCall> : mode == 2 ? k_smt_chain<FrMulFips> : k_smt_chain<FrMulInline>,
                      dim3((vs.batch * SMT_CHAIN_LANES + 63) / 64),
                      dim3(64), 0, st, L, K, level_task, inputs, vs, pos_core, smt_core, order, status, vs.batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_qc_build(const PosConsts& K, fr* qc, hipStream_t st) {
+  hipLaunchKernelGGL(k_qc_build, dim3(1), dim3(256), 0, st, K, qc);
   return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ hipError_t launch_wtns_gather(const uint8_t* o0, size_t o0_stride, const uint32_
 // by default yes — QueryIdentity (the core is on its latency-critical chain) and, since round 5, the register
 // circuit too (k_bjj_core_rc recomputes the ladder instead, 1.35x instead of 6x its bytes but twice the VALU:
 // configs 3 / 4 / O2-shaped +1.0 / +0.7 / +5.7 % with the scratch kernel, profiles/r5e); PZK_BJJ=scratch|rc (A/B)
-bool bjj_uses_scratch(bool chain_critical);
+bool bjj_uses_scratch();
 hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, fr* bjj_core, fr* scratch,
                            hipStream_t st);
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
@@ -51,7 +51,9 @@ hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore
 // query: QueryIdentity's chain or the register circuit's (both default to FIPS products, PZK_CHAIN_MUL overrides)
 hipError_t launch_smt_chain(const DevLayout& L, const PosConsts& K, const int32_t* level_task, const uint8_t* inputs,
                             ValueStore vs, fr* pos_core, fr* smt_core, const uint32_t* order, int32_t* status,
-                            bool query, hipStream_t st);
+                            hipStream_t st);
+// the quad SMT chain's constant table (smt_chain4.hpp), once per instance
+hipError_t launch_qc_build(const PosConsts& K, fr* qc, hipStream_t st);
 // witnesses ordered by SMT insertion level (the chain's length), deepest first, for k_smt_chain's lane groups
 hipError_t launch_smt_order(const fr* smt_core, uint32_t smt_core_fr, uint32_t* order, uint32_t batch, hipStream_t st);
 // QueryIdentity prep (query.hpp): DG1 fields, dg1 chunks, citizenship inverses, the query checks

@@ -222,6 +222,16 @@ constexpr int SMT_LEVELS = 80;
 constexpr int SMT_CHAIN_LANES = 4;                          // k_smt_chain: lanes per witness (one PoseidonHash(2) group)
 constexpr int SMT_PREP_LANES = 8;                           // k_smt_prep: lanes per witness (10 levels each)
 constexpr int SMT_CORE_FR = 3 * SMT_LEVELS + 2;             // inv(sibling), root, flags per level; j; inv(root-root0)
+// the quad SMT chain's constant table (smt_chain4.hpp k_qc_build; Montgomery-form Fr entries, width 3)
+constexpr int QC_RP = 57;                    // partial rounds of width 3 (pos_rp(3))
+constexpr int QC_INIT = 0;                   // [C0, C1, C2, 0]: per quad, the initial Ark constants
+constexpr int QC_FULL = 4;                   // 8 records of 16: full rounds 0..6, then the hash; per quad 4 entries
+constexpr int QC_PART = QC_FULL + 8 * 16;    // 57 records of 10 (QC_P_*)
+constexpr int QC_R2 = QC_PART + QC_RP * 10;  // R^2 mod p (normal form -> Montgomery)
+constexpr int QC_SIZE = QC_R2 + 1;
+// a partial-round record: the step-2 multipliers (quad 0 S0, quad 1 S'1, quad 2 S'2), the step-3 row constants S1,
+// S2, the constant terms K0, K1, K2, the Montgomery one and a zero
+enum { QC_P_S0 = 0, QC_P_SP1, QC_P_SP2, QC_P_S1, QC_P_S2, QC_P_K0, QC_P_K1, QC_P_K2, QC_P_ONE, QC_P_ZERO };
 
 constexpr int POS_MAX_T = 6;
 __host__ __device__ inline int pos_nrp(int t) {

@@ -40,6 +40,7 @@ struct PosConsts {
   PosParamIndex ix;
   const fr* sbase;  // partial-round products S[i] * C[5t + r] (Montgomery) at S's indices (k_pos_sc, runtime.cpp)
   const fr* zimg;   // zero-input images and hashes (pos_zimg_off)
+  const fr* qc;     // the quad SMT chain's constant table (smt_chain4.hpp, QC_SIZE entries)
   __device__ __forceinline__ const fr* Zimg(int t) const { return zimg + pos_zimg_off(t); }
   __device__ __forceinline__ const fr& Zhash(int t) const { return zimg[pos_zimg_off(t) + PosImg(t).size]; }
   __device__ __forceinline__ const fr* Zrow(int t) const { return zimg + pos_zrow_off(t); }

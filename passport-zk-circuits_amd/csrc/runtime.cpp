@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -140,8 +141,19 @@ static bool post_chain_split(bool shared) {
   const char* e = getenv("PZK_POST");
   return e ? atoi(e) != 0 : !shared;
 }
-// live register instances in the process (pzk_instance_create / destroy): the stream set of a new instance
-static std::atomic<int> g_register_instances{0};
+// live register instances per device (pzk_instance_create / destroy): an instance's stream set depends on whether
+// it shares its device with other register instances (ensure_chain_streams)
+static std::mutex g_reg_mu;
+static std::map<int, int> g_register_instances;
+static void register_count_add(int device, int d) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_register_instances[device] += d;
+}
+static int register_count(int device) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_register_instances.find(device);
+  return it == g_register_instances.end() ? 0 : it->second;
+}
 
 // scratch sets (pipeline depth): call k uses set k % nsets and waits for call k - nsets (nsets = 3, or
 // PZK_NSETS = 2..6 for A/B; nsets_env)
@@ -179,8 +191,9 @@ struct pzk_instance {
   PosParamIndex pix{};
   int pos_consts_n = 0;  // constants per copy (Montgomery copy first, then normal form)
   fr* d_pos_zimg = nullptr;  // zero-input Poseidon images + hashes (poseidon.hpp pos_zimg_off)
+  fr* d_qc = nullptr;        // the quad SMT chain's constants (smt_chain4.hpp)
   PosConsts pos_consts() const {
-    return PosConsts{d_pos_consts, d_pos_consts + pos_consts_n, pix, d_pos_consts + 2 * pos_consts_n, d_pos_zimg};
+    return PosConsts{d_pos_consts, d_pos_consts + pos_consts_n, pix, d_pos_consts + 2 * pos_consts_n, d_pos_zimg, d_qc};
   }
   // per-batch scratch, grown on demand; two sets, alternating per call, so that call k + 1's
   // cores can run while call k's emitters still read set k % 2
@@ -206,6 +219,7 @@ struct pzk_instance {
   // hardware queue (the O2-shaped line: that queue ran 90 % of the period and paced the pipeline, profiles/r5g)
   hipStream_t s_sha2 = nullptr;
   uint64_t chain_rr = 0;           // register calls: SMT chain stream rotation
+  bool chain_set_shared = false;   // the chain stream set (s_tail ..) was made for a device shared with other register instances
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
   // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
@@ -350,6 +364,9 @@ static int load_poseidon(pzk_instance* I) {
   HIPCHK(hipMalloc(&I->d_pos_zimg, sizeof(fr) * POS_ZBUF_TOTAL));
   HIPCHK(hipMalloc(&scratch, sizeof(fr) * (4 + 512)));
   HIPCHK(launch_pos_zero_img(I->pos_consts(), scratch, I->d_pos_zimg, nullptr));
+  // the quad SMT chain's constant table (width 3)
+  HIPCHK(hipMalloc(&I->d_qc, sizeof(fr) * QC_SIZE));
+  HIPCHK(launch_qc_build(I->pos_consts(), I->d_qc, nullptr));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipFree(scratch));
   // the zero-input blocks in O0 signal order (PosConsts::Zrow): image element pos_prog[i] at row position i
@@ -401,7 +418,7 @@ static void free_all(pzk_instance* I) {
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
                   I->d_pos_consts, I->d_bjj_table, I->d_in, I->d_out, I->d_status, I->d_ec_gpow, I->d_ec_prog,
                   I->d_ec_tab_off, I->d_ec_ops[0], I->d_ec_ops[1], I->d_ec_ops[2], I->d_inv_small, I->d_map,
-                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank, I->d_mprog, I->d_pos_zimg};
+                  I->d_o0[0], I->d_o0[1], I->d_keep_bits, I->d_keep_rank, I->d_mprog, I->d_pos_zimg, I->d_qc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
@@ -460,7 +477,7 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
   }
   if (const char* u = getenv("PZK_BJJ_SEGS")) {  // tuning switch of k_bjj_core (kernels.hip)
     int v = atoi(u);
-    const bool sc = bjj_uses_scratch(params->circuit == PZK_CIRCUIT_QUERY);
+    const bool sc = bjj_uses_scratch();
     if (sc ? (v != 8 && v != 16 && v != 32) : (v != 16 && v != 32 && v != 64))
       return fail(PZK_E_ARG, std::string("PZK_BJJ_SEGS=") + u +
                                  (sc ? ": valid values are 8, 16, 32 (PZK_BJJ=scratch)" : ": valid values are 16, 32, 64"));
@@ -565,7 +582,7 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
       acc += wl[i].count;
     }
   }
-  if (I->lay.is_register) g_register_instances++;
+  if (I->lay.is_register) register_count_add(I->device, 1);
   *out = I;
   return 0;
 }
@@ -608,7 +625,7 @@ static int pzk_instance_create_mapped_impl(const pzk_params* params, const char*
 
 static void pzk_instance_destroy_impl(pzk_instance* inst) {
   if (!inst) return;
-  if (inst->lay.is_register) g_register_instances--;
+  if (inst->lay.is_register) register_count_add(inst->device, -1);
   {
     // calls are asynchronous across the instance's streams: wait for a concurrent caller to leave and
     // for every call in flight to drain, on the instance's device, before anything is freed
@@ -666,7 +683,7 @@ static int ensure_scratch(pzk_instance* I, Scratch& S, size_t batch) {
       {(void**)&S.d_rsa_core, 8ull * L.rsa_core_words * batch},
       {(void**)&S.d_rsa_colsum, L.is_register ? 8ull * 3 * 2 * L.reg.K * batch : 0},
       {(void**)&S.d_bjj_core, 32ull * L.bjj_core_fr * batch},
-      {(void**)&S.d_bjj_scratch, (L.is_register || L.is_query) && bjj_uses_scratch(L.is_query) ? 32ull * BJJ_SCRATCH_FR * batch : 0},
+      {(void**)&S.d_bjj_scratch, (L.is_register || L.is_query) && bjj_uses_scratch() ? 32ull * BJJ_SCRATCH_FR * batch : 0},
       {(void**)&S.d_smt_core, 32ull * L.smt_core_fr * batch},
       {(void**)&S.d_ec_core, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].core_words * batch : 0},
       {(void**)&S.d_ec_jac, L.is_ecdsa ? 8ull * EC_GEO[L.reg.ec_curve].jac_words * batch : 0},
@@ -699,25 +716,40 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
 // profiles/r5c). Several register instances in one process (config 5: one per flow) are another matter: with every
 // instance's full set config 5 ran 8.5k witnesses/s, with low-priority chain streams and post-chain streams 31.9k,
 // with neither 48.2k — and with the first instance's full set beside the others' rounds 1-4 sets, 4.9k
-// (profiles/r5j-r5l). So an instance whose first call finds other register instances alive takes the rounds 1-4
-// set (low-priority chain streams, no post-chain stream). PZK_CHAIN_PRIO=hi|lo and PZK_POST=0|1 force either.
+// (profiles/r5j-r5l). So an instance that shares its device with other register instances takes the rounds 1-4 set
+// (low-priority chain streams, no post-chain stream). The count is per device and is re-checked at every call: an
+// instance whose set no longer matches (another instance appeared on its device, or went away) drains its streams
+// and rebuilds the set, so the order in which a caller creates and first runs its instances does not matter.
+// PZK_CHAIN_PRIO=hi|lo and PZK_POST=0|1 force either. The streams are created into locals and assigned only once all
+// exist: a failure leaves the instance without a set (retried at the next call), never with half of one.
 static int ensure_chain_streams(pzk_instance* I) {
-  if (!I->lay.is_register || I->s_tail) return 0;
-  const bool shared = g_register_instances.load() > 1;
+  if (!I->lay.is_register) return 0;
+  const bool shared = register_count(I->device) > 1;
+  if (I->s_tail && I->chain_set_shared == shared) return 0;
+  if (I->s_tail) {  // the set no longer fits: drain every call in flight, then replace it
+    int rc = sync_all(I);
+    if (rc) return rc;
+    for (hipStream_t* s : {&I->s_tail, &I->s_chain2, &I->s_chain3, &I->s_post, &I->s_mm, &I->s_sha2})
+      if (*s) { (void)hipStreamDestroy(*s); *s = nullptr; }
+  }
+  hipStream_t made[6] = {};  // s_tail, s_chain2, s_chain3, s_post, s_mm, s_sha2
+  auto create = [&](int k, int prio) -> bool {
+    if (hipStreamCreateWithPriority(&made[k], hipStreamNonBlocking, prio) == hipSuccess) return true;
+    made[k] = nullptr;
+    return false;
+  };
   const char* cp_env = getenv("PZK_CHAIN_PRIO");
   const bool chain_lo = cp_env ? !strcmp(cp_env, "lo") : shared;
   const int prio_chain = chain_lo ? I->prio_lo : I->prio_hi;
-  HIPCHK(hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_chain));
-  HIPCHK(hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_chain));
+  bool ok = create(0, prio_chain) && create(1, prio_chain);
   // the third chain stream only when asked for (PZK_SMT_CHAINS=3)
-  if (getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3)
-    HIPCHK(hipStreamCreateWithPriority(&I->s_chain3, hipStreamNonBlocking, prio_chain));
-  if (post_chain_split(shared)) HIPCHK(hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, I->prio_lo));
+  if (ok && getenv("PZK_SMT_CHAINS") && atoi(getenv("PZK_SMT_CHAINS")) >= 3) ok = create(2, prio_chain);
+  if (ok && post_chain_split(shared)) ok = create(3, I->prio_lo);
   static const char* se_env = getenv("PZK_SIGEMIT");
-  if (se_env && !strcmp(se_env, "own") && !shared && !I->lay.is_ecdsa) {
+  if (ok && se_env && !strcmp(se_env, "own") && !shared && !I->lay.is_ecdsa) {
     static const char* mp_env = getenv("PZK_MM_PRIO");
     const bool hi = mp_env && !strcmp(mp_env, "hi");
-    HIPCHK(hipStreamCreateWithPriority(&I->s_mm, hipStreamNonBlocking, hi ? I->prio_hi : I->prio_lo));
+    ok = create(4, hi ? I->prio_hi : I->prio_lo);
   }
   // two SHA emitter streams: default for mapped layouts keeping at most half of the signals (O2-shaped 206.9k ->
   // 218.5k witnesses/s; O1-shaped, 56 % kept, 130.8k -> 130.2k: profiles/r5q); the O0 layout keeps one (+1 % with
@@ -725,7 +757,19 @@ static int ensure_chain_streams(pzk_instance* I) {
   // would read 0.35 for the same HBM work, profiles/r5p). PZK_SHA_STREAMS=1|2 forces either.
   const char* ss_env = getenv("PZK_SHA_STREAMS");
   const bool sha2 = ss_env ? atoi(ss_env) >= 2 : I->d_keep_bits != nullptr && 2 * I->out_size <= I->lay.wit_size;
-  if (sha2 && !shared) HIPCHK(hipStreamCreateWithPriority(&I->s_sha2, hipStreamNonBlocking, I->prio_lo));
+  if (ok && sha2 && !shared) ok = create(5, I->prio_lo);
+  if (!ok) {
+    for (hipStream_t s : made)
+      if (s) (void)hipStreamDestroy(s);
+    return fail(PZK_E_HIP, "hipStreamCreateWithPriority failed (the instance's chain streams)");
+  }
+  I->s_tail = made[0];
+  I->s_chain2 = made[1];
+  I->s_chain3 = made[2];
+  I->s_post = made[3];
+  I->s_mm = made[4];
+  I->s_sha2 = made[5];
+  I->chain_set_shared = shared;
   return 0;
 }
 
@@ -844,7 +888,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6, S.d_smt_order))) return rc; }
     { PhaseScope ps(T, slot, PH_SMT, st);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              true, st)); }
+                              st)); }
     HIPCHK(hipEventRecord(I->ev_pos, st));
     // PZK_QRY_EMIT1=1: every emitter on one stream (with 3 chain streams that is 4 streams in use = the
     // hardware queues a process gets by default)
@@ -971,7 +1015,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     }
     { PhaseScope ps(T, slot, PH_SMT, s_smt);
       HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              false, s_smt)); }
+                              s_smt)); }
     HIPCHK(hipEventRecord(I->ev_chain, s_smt));
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }

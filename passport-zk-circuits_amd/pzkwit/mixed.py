@@ -52,7 +52,9 @@ def shard_by_cost(costs, world, rank):
 
 class MixedBatch:
     """Runs a list of (params, input_row) items, grouped per instance. `instances` are created on
-    first use and reused across calls."""
+    first use and reused across calls; a call creates every instance its items need before it runs
+    any of them, so the library sees the whole set of register instances sharing the device when it
+    picks their stream sets (runtime.cpp ensure_chain_streams)."""
 
     def __init__(self):
         self.instances = {}
@@ -71,6 +73,8 @@ class MixedBatch:
             groups.setdefault(params_key(prm), (prm, []))[1].append(i)
         wits = [None] * len(items)
         status = np.zeros(len(items), dtype=np.int32)
+        for prm, _ in groups.values():
+            self.instance(prm)
         for prm, idx in groups.values():
             inst = self.instance(prm)
             rows = np.stack([items[i][1] for i in idx])

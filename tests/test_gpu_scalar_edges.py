@@ -1,6 +1,6 @@
 """GPU: the register path at the scalar edges of tests/test_scalar_edges.py — skIdentity in {0, 1, 2, 2^248,
 2^251 + x, 2^253 + x, p - 2, p - 1} and a pubkey hash >= 2^253 as the SMT key — element for element against the
-oracle through both BabyJubJub cores (k_bjj_core_rc, the register default, and the scratch kernel, PZK_BJJ=scratch),
+oracle through both BabyJubJub cores (the scratch kernel k_bjj_core, the default, and k_bjj_core_rc, PZK_BJJ=rc),
 and config 4's proofs (depths 1-79, slaveMerkleRoot = the proof's root): the device's SMT chain sets
 isVerified = 1 on every lane (identity.circom:112-120, babyjubjub/curve.circom:143-171, aliascheck.circom:7-14,
 SMTVerifier.circom:109-176)."""

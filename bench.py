@@ -356,9 +356,10 @@ def reduce_run(dist, dev, dt, bad):
 
 def wants_config4(args):
     """The default register line also measures config 4 on the same instance, reported beside the
-    headline config-3 value (`config4` key)."""
+    headline config-3 value (`config4` key); with --sym on the mapped instance (the prover-facing layout with real
+    SMT proofs)."""
     return (args.workload == "register" and args.sig_eff == 1 and getattr(args, "smt_depth", "0") == "0"
-            and not getattr(args, "sym", None) and not getattr(args, "no_config4", False))
+            and not getattr(args, "no_config4", False))
 
 
 def run_rank(args, rank, world, local, dist, engine_cls=GpuEngine, device="cuda"):
@@ -637,7 +638,7 @@ def report(args, r, world):
     if c4:
         v4 = batch * world * args.steps / c4["dt"]
         g4 = v4 * job_bytes / 1e9
-        pm4 = pmc_pass(CONFIG4_WORKLOAD, "O0")
+        pm4 = pmc_pass(CONFIG4_WORKLOAD, layout_key)
         out["config4"] = {
             "what": "SURVEY.md §8d config 4 on the same instance and sub-batching, measured after the headline line "
                     "(W warmup + K timed steps of its own inputs; the driver's 8-GPU run shards it 8 x %d)" % batch,

@@ -182,23 +182,72 @@ __device__ __forceinline__ fq fq_mul64(const fq& a, const fq& b, const QLane& c)
 // iteration adds the rows' a_j * b and m * p into them (fr_mac: one v_mad_u64_u32 + one carry add per product);
 // the frame then shifts one word: E <- O + (E >> 32), O <- the next lane's E word 0 (quad lane 0's is zero).
 // Result < (K + sum_r |a_r| |b_r| + R p) / R; the caller keeps it below 2^256.
-template <int NR, class A, int J = 0>
-__device__ __forceinline__ void fq_dot_rows(A& aw, const fq* b, uint64_t& e, uint32_t& et, uint64_t& o, uint32_t& ot) {
+// The rows' products of one iteration: 2 NR v_mad_u64_u32 into the two columns, each with its own SGPR carry-out
+// pair, then the 2 NR carry adds into the columns' top words. A VALU write of an SGPR needs two wait states before a
+// VALU reads it as a carry-in; with the adds after all the products that spacing is there without s_nop for NR >= 2
+// (NR = 1 pads one). Every register a later DPP reads (E's low word) is written at least two instructions before
+// the block ends.
+template <int NR>
+__device__ __forceinline__ void fq_rows_mac(const uint32_t* a, const fq* b, uint64_t& e, uint32_t& et, uint64_t& o,
+                                            uint32_t& ot) {
+  static_assert(NR == 1 || NR == 2 || NR == 3, "rows");
+  uint64_t c0, c1, c2, c3, c4, c5;
+  if constexpr (NR == 1) {
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %6, %8, %1\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %2, %4, 0, %2, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, 0, %3, %5"
+        : "+v"(e), "+v"(o), "+v"(et), "+v"(ot), "=&s"(c0), "=&s"(c1)
+        : "v"(a[0]), "v"(b[0].lo), "v"(b[0].hi));
+  } else if constexpr (NR == 2) {
+    asm("v_mad_u64_u32 %0, %4, %8, %10, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %8, %11, %1\n\t"
+        "v_mad_u64_u32 %0, %6, %9, %12, %0\n\t"
+        "v_mad_u64_u32 %1, %7, %9, %13, %1\n\t"
+        "v_addc_co_u32_e64 %2, %4, 0, %2, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, 0, %3, %5\n\t"
+        "v_addc_co_u32_e64 %2, %6, 0, %2, %6\n\t"
+        "v_addc_co_u32_e64 %3, %7, 0, %3, %7"
+        : "+v"(e), "+v"(o), "+v"(et), "+v"(ot), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+        : "v"(a[0]), "v"(a[1]), "v"(b[0].lo), "v"(b[0].hi), "v"(b[1].lo), "v"(b[1].hi));
+  } else {
+    asm("v_mad_u64_u32 %0, %4, %10, %13, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %10, %14, %1\n\t"
+        "v_mad_u64_u32 %0, %6, %11, %15, %0\n\t"
+        "v_mad_u64_u32 %1, %7, %11, %16, %1\n\t"
+        "v_mad_u64_u32 %0, %8, %12, %17, %0\n\t"
+        "v_mad_u64_u32 %1, %9, %12, %18, %1\n\t"
+        "v_addc_co_u32_e64 %2, %4, 0, %2, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, 0, %3, %5\n\t"
+        "v_addc_co_u32_e64 %2, %6, 0, %2, %6\n\t"
+        "v_addc_co_u32_e64 %3, %7, 0, %3, %7\n\t"
+        "v_addc_co_u32_e64 %2, %8, 0, %2, %8\n\t"
+        "v_addc_co_u32_e64 %3, %9, 0, %3, %9"
+        : "+v"(e), "+v"(o), "+v"(et), "+v"(ot), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3), "=&s"(c4), "=&s"(c5)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(b[0].lo), "v"(b[0].hi), "v"(b[1].lo), "v"(b[1].hi), "v"(b[2].lo),
+          "v"(b[2].hi));
+  }
+  (void)c2; (void)c3; (void)c4; (void)c5;
+}
+template <int NR, class A, int J>
+__device__ __forceinline__ void fq_dot_a(A& aw, uint32_t* a) {
   if constexpr (NR > 0) {
-    const uint32_t a = aw(NR - 1, std::integral_constant<int, J>{});
-    fr_mac(e, et, a, b[NR - 1].lo);
-    fr_mac(o, ot, a, b[NR - 1].hi);
-    fq_dot_rows<NR - 1, A, J>(aw, b, e, et, o, ot);
+    a[NR - 1] = aw(NR - 1, std::integral_constant<int, J>{});
+    fq_dot_a<NR - 1, A, J>(aw, a);
   }
 }
 template <int NR, class A, int J = 0>
 __device__ __forceinline__ void fq_dot_iter(A& aw, const fq* b, const QLane& c, uint64_t& e, uint32_t& et, uint64_t& o,
                                             uint32_t& ot) {
   if constexpr (J < 8) {
-    fq_dot_rows<NR, A, J>(aw, b, e, et, o, ot);
+    uint32_t a[NR];
+    fq_dot_a<NR, A, J>(aw, a);
+    fq_rows_mac<NR>(a, b, e, et, o, ot);
     const uint32_t m = qbcast<0>((uint32_t)e) * PINV;
-    fr_mac(e, et, m, c.p0);
-    fr_mac(o, ot, m, c.p1);
+    const uint32_t mm[1] = {m};
+    const fq pp[1] = {fq{c.p0, c.p1}};
+    fq_rows_mac<1>(mm, pp, e, et, o, ot);
     // shift one word: the odd column becomes the even one (plus the even column's carry), the next lane's even word
     // becomes this lane's odd column
     const uint32_t nx = qnext((uint32_t)e);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU (round 4): selected -m gpu tests (or all with ALL=1), smoke(), the default bench line.
-# usage: tools/gpu/gpu_r4_check.sh TAG [pytest -k expression]
+# usage: tools/gpu/gpu_check.sh TAG [pytest -k expression]
 set -o pipefail
 TAG=${1:-r4}
 O=gpurun_out/$TAG

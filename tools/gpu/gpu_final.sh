@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 end: the whole -m gpu suite, smoke(), the driver's default bench command, rocprofv3 --kernel-trace --stats
+# Round end: the whole -m gpu suite, smoke(), the driver's default bench command, rocprofv3 --kernel-trace --stats
 # of the same bench command (without the CPU legs), then the other lines.
-# usage: tools/gpu/gpu_r5_final.sh TAG
+# usage: tools/gpu/gpu_final.sh TAG
 set -o pipefail
-TAG=${1:-r5_final}
+TAG=${1:-final}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # (SQ_*), HBM read bytes (FETCH_SIZE), HBM write bytes (WRITE_SIZE), one counter group per run, then
 # tools/pmc_summary.py: per-kernel table + traffic.json (traffic and VALU instructions per witness, keyed by the
 # bench line's config.workload).
-# usage: tools/gpu/gpu_pmc_r4.sh TAG BATCH "bench args"
+# usage: tools/gpu/gpu_pmc_line.sh TAG BATCH "bench args"
 set -o pipefail
 TAG=$1; B=$2; EXTRA=$3
 O=gpurun_out/$TAG

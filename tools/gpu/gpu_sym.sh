@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU (round 4): mapped-layout parity tests, then the config-3 line O0 / --O2-shaped / --O1-shaped / synthetic map.
-# usage: tools/gpu/gpu_r4_sym.sh TAG [pytest -k expression]
+# usage: tools/gpu/gpu_sym.sh TAG [pytest -k expression]
 set -o pipefail
 TAG=${1:-r4_sym}
 O=gpurun_out/$TAG

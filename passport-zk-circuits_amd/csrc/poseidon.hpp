@@ -329,6 +329,9 @@ __device__ __forceinline__ uint32_t pos_img_need(uint32_t d) {  // the image par
   return PI_MIX;
 }
 
+// core: the permutation's round states in Montgomery form, canonical (k_pos_core, k_pos_core1) or below 2.2p
+// (k_smt_chain4): every core value read here goes through fr_mul_fast or fr_from_mont_fast, whose results are
+// canonical for such inputs.
 template <int T>
 __device__ __forceinline__ void pos_img_fill(fr* img, const PosConsts& K, const fr* core, const ValueStore& vs,
                                              const PosTask& task, uint32_t w, uint32_t need = PI_ALL) {

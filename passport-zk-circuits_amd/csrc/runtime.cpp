@@ -134,6 +134,15 @@ static int qry_chain_streams() {
   static const int v = getenv("PZK_QRY_CHAINS") ? atoi(getenv("PZK_QRY_CHAINS")) : 4;
   return v < 1 ? 1 : v > 4 ? 4 : v;
 }
+// QueryIdentity: emitter stream pairs its calls alternate over (PZK_QRY_EMIT = 1 | 2, default 2). With one pair the
+// two emitter streams paced the line: with the quad SMT chain the Poseidon emitter stream ran 81 % and the other
+// emitter stream 73 % of the timed region while the chain streams ran 48-67 % (profiles/r6d). Calls in flight never
+// share output rows (pzkwit.h: a reused d_wtns needs a call index >= k + pipeline_depth), so consecutive calls'
+// emitters need no ordering between them.
+static int qry_emit_pairs() {
+  static const int v = getenv("PZK_QRY_EMIT") ? atoi(getenv("PZK_QRY_EMIT")) : 2;
+  return v < 2 ? 1 : 2;
+}
 
 // PZK_POST=0 (A/B): the register call's chain-dependent emission stays behind the chain on the emitter streams
 // (rounds 1-4) instead of on its own post-chain stream
@@ -555,6 +564,11 @@ static int pzk_instance_create_impl(const pzk_params* params, pzk_instance** out
     ok = hipStreamCreateWithPriority(&I->s_tail, hipStreamNonBlocking, prio_hi) == hipSuccess;
     if (ok && I->lay.is_query && qry_chain_streams() >= 4)
       ok = hipStreamCreateWithPriority(&I->s_chain2, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    // QueryIdentity: a second pair of emitter streams for odd calls (qry_emit_pairs): the low-priority pool's other
+    // two hardware queues
+    if (ok && I->lay.is_query && qry_emit_pairs() >= 2)
+      ok = hipStreamCreateWithPriority(&I->s_sha2, hipStreamNonBlocking, prio_lo) == hipSuccess &&
+           hipStreamCreateWithPriority(&I->s_post, hipStreamNonBlocking, prio_lo) == hipSuccess;
   }
   for (hipEvent_t* e : {&I->ev_load, &I->ev_sha, &I->ev_rsa, &I->ev_bjj, &I->ev_entry, &I->ev_dep, &I->ev_pos, &I->ev_tab,
                         &I->ev_smt, &I->ev_chain})
@@ -875,7 +889,11 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     // QueryIdentity(80) (query.hpp): one chain on the call's chain stream — prep, the BabyJubJub key, Poseidon levels
     // 0-3 (sk hashes, nullifier, dg1 commitment, pk / position / value hashes), the SMT prep (needs the tree
     // position), levels 4-5 (the new-leaf hash and the level hashes above the insertion level), the SMT chain;
-    // then the emitters on the two emitter streams
+    // then the emitters on the two emitter streams (odd calls: the second emitter pair, qry_emit_pairs)
+    if (!serial && I->s_sha2 && I->s_post && (I->calls & 1)) {
+      s_sha = I->s_sha2;
+      s_emit = I->s_post;
+    }
     { PhaseScope ps(T, slot, PH_PREP, st); HIPCHK(launch_qry_prep(L, d_inputs, vs, d_status, st)); }
     { PhaseScope ps(T, slot, PH_BJJ_CORE, st);
       HIPCHK(launch_bjj_core(L, vs, I->d_bjj_table, S.d_bjj_core, S.d_bjj_scratch, st)); }

@@ -16,8 +16,8 @@
 //                  stk' = x^3 (x) (S'k x^2) + stk (x) 1 + S'k C            (x^2 = st0 (x) st0, x^3 = x^2 (x) st0)
 // ((x) is the Montgomery product; the constant terms enter as K = c * R mod p, so K * R^-1 = c.) With canonical
 // constants every state stays below 2.2p (products of inputs < 2.2p are < 2.0p + the K term; R / p > 5.28), so the
-// 256-bit digits never overflow. What leaves the kernel (the round states of the Poseidon core, the level hashes,
-// Switcher outputs) is canonicalised first (two conditional subtractions).
+// 256-bit digits never overflow. The level hashes and Switcher outputs leave the kernel canonicalised (two conditional
+// subtractions); the round states of the Poseidon core leave as they are (< 2.2p, see pos2_perm_quad).
 //
 // The constant table (QC_*, Montgomery form, built once per instance by k_qc_build from the reference's constants
 // poseidonConstants.circom, as PosConsts holds them) is staged in LDS per workgroup; every lane reads its own 8-byte
@@ -101,9 +101,12 @@ __device__ __forceinline__ fq fq_load(const void* src, int q) {
 __device__ __forceinline__ fq pos2_perm_quad(const fr* qc, fq in, fr* out, int quad, const QLane& c) {
   fq st = fq_add_raw(in, qc_digit(qc, QC_INIT + quad, c.q));  // < 2p
   int o = 0;
+  // the round states leave as they are, below 2.2p, not canonicalised: their only reader, the Poseidon image fill
+  // (pos_img_fill), takes every core value through a FIPS product or a Montgomery -> normal conversion, and both give
+  // the canonical result for inputs below 2.2p (fr_mul_fast: < (2.2p * 2.2p + R p) / R < 2p before its final
+  // subtraction; fr_from_mont_fast: < p + 1)
   auto store = [&](const fq& v) {
-    const fq cv = fq_canon2(v, c);
-    if (quad < 3) fq_store(out + o + quad, cv, c.q);
+    if (quad < 3) fq_store(out + o + quad, v, c.q);
     o += 3;
   };
   // full round f (f = 7: the hash): x5 = st^5 per quad, then the lazy mix over the three quads' x5

@@ -39,14 +39,15 @@ def _calls(torch, insts, rows, n_calls, per_call):
     dev = torch.device("cuda:0")
     d_in = torch.from_numpy(rows).to(dev)
     NIN = rows.shape[1]
+    bufs = [(torch.empty((per_call, insts[k % len(insts)].witness_size, 32), dtype=torch.uint8, device=dev),
+             torch.full((per_call,), -1, dtype=torch.int32, device=dev)) for k in range(n_calls)]
     done = []
-    torch.cuda.synchronize()  # the library's streams do not wait for torch's stream
+    torch.cuda.synchronize()  # the library's streams do not wait for torch's stream (the buffers' fills)
     for k in range(n_calls):
         inst = insts[k % len(insts)]
         W = inst.witness_size
         lo = (k * per_call) % rows.shape[0]
-        out = torch.empty((per_call, W, 32), dtype=torch.uint8, device=dev)
-        st = torch.full((per_call,), -1, dtype=torch.int32, device=dev)
+        out, st = bufs[k]
         inst.witness_batch_device(d_in.data_ptr() + lo * NIN * 32, per_call, out.data_ptr(), 32 * W, st.data_ptr())
         done.append((inst, lo, out, st))
     for inst in insts:

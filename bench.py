@@ -462,12 +462,12 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the host_delivered (streamed) measurement")
     ap.add_argument("--host-sample", type=int, default=None, help="witnesses streamed for host_delivered")
     args = ap.parse_args()
-    if args.workload == "mixed" and os.environ.get("PZK_MIX_HWQ", "16") != "keep":
-        # one instance per flow, seven streams each (four high, three low priority): with 4 hardware queues per priority (HIP's default, and what the GPU boxes'
-        # environment sets) the flows' streams share queues and serialise behind each other (40.9k -> 43.2k
-        # witnesses/s at 16, profiles/r4_hwq/); set before any HIP call, inherited by the ranks launch_ranks starts
-        # (PZK_MIX_HWQ=keep leaves the environment's value)
-        hwq = os.environ.get("PZK_MIX_HWQ", "16")
+    if args.workload == "mixed" and os.environ.get("PZK_MIX_HWQ", "keep") != "keep":
+        # PZK_MIX_HWQ=N (A/B): GPU_MAX_HW_QUEUES for the mixed line, set before any HIP call and inherited by the ranks
+        # launch_ranks starts. Default: the environment's value (the boxes' 4). Round 4 needed 16 (40.9k -> 43.2k
+        # witnesses/s, profiles/r4_hwq/); since the instances sharing a device take the reduced stream set
+        # (runtime.cpp ensure_chain_streams) the line holds at 4: 46.9k (profiles/r6i/)
+        hwq = os.environ.get("PZK_MIX_HWQ")
         if not hwq.isdigit() or not 1 <= int(hwq) <= 32:
             raise SystemExit("PZK_MIX_HWQ=%s: expected an integer 1..32 (hardware queues per process) or 'keep'" % hwq)
         if os.environ.get("GPU_MAX_HW_QUEUES") != hwq:

@@ -229,6 +229,11 @@ struct pzk_instance {
   hipStream_t s_sha2 = nullptr;
   uint64_t chain_rr = 0;           // register calls: SMT chain stream rotation
   bool chain_set_shared = false;   // the chain stream set (s_tail ..) was made for a device shared with other register instances
+  // register instances sharing a device run on that device's one stream set (ensure_chain_streams): the instance's
+  // own main / rsa / sha / emit streams wait here meanwhile
+  bool on_pool = false;
+  hipStream_t own[4] = {};
+  bool sha2_on = false;            // odd calls' SHA emission on s_sha2 (mapped layouts keeping <= 1/2 of the signals)
   hipEvent_t ev_pos = nullptr, ev_tab = nullptr, ev_smt = nullptr, ev_chain = nullptr;
   std::mutex mu;  // one in-flight call per instance (pzkwit.h): concurrent callers are serialised
   // optional signal -> witness map (circom .sym, pzk_instance_create_mapped): the emitters write the
@@ -422,6 +427,59 @@ static void free_stream_bufs(pzk_instance* I) {
   I->st_cap = 0;
 }
 
+// The device's register stream set (PZK_SHARED_STREAMS=0: one set per instance, the round-5 scheme): main, rsa, the two
+// SMT chain streams at high priority; sha, emit, post, sha2 at low priority — GPU_MAX_HW_QUEUES (4) hardware queues per
+// priority, so the set shares no queue whatever number of register instances run on the device.
+struct PoolSet {
+  hipStream_t s[8] = {};
+  int refs = 0;
+};
+static std::map<int, PoolSet> g_pools;  // per device, under g_reg_mu
+static bool shared_streams_on() {  // PZK_SHARED_STREAMS=1 (A/B; default off, see ensure_chain_streams)
+  static const bool v = getenv("PZK_SHARED_STREAMS") && atoi(getenv("PZK_SHARED_STREAMS")) != 0;
+  return v;
+}
+static void pool_release(int device) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  PoolSet& P = g_pools[device];
+  if (--P.refs > 0) return;
+  for (hipStream_t& st : P.s)
+    if (st) { (void)hipStreamDestroy(st); st = nullptr; }
+}
+static bool pool_acquire(int device, int prio_lo, int prio_hi, hipStream_t* out) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  PoolSet& P = g_pools[device];
+  if (P.refs == 0) {
+    for (int k = 0; k < 8; k++)
+      if (hipStreamCreateWithPriority(&P.s[k], hipStreamNonBlocking, k < 4 ? prio_hi : prio_lo) != hipSuccess) {
+        for (hipStream_t& st : P.s)
+          if (st) { (void)hipStreamDestroy(st); st = nullptr; }
+        return false;
+      }
+  }
+  P.refs++;
+  for (int k = 0; k < 8; k++) out[k] = P.s[k];
+  return true;
+}
+// leave the device's stream set: the instance's own main / rsa / sha / emit streams come back
+static void pool_leave(pzk_instance* I) {
+  if (!I->on_pool) return;
+  I->stream = I->own[0];
+  I->s_rsa = I->own[1];
+  I->s_sha = I->own[2];
+  I->s_emit = I->own[3];
+  for (hipStream_t& o : I->own) o = nullptr;
+  I->s_tail = I->s_chain2 = I->s_chain3 = I->s_post = I->s_mm = I->s_sha2 = nullptr;
+  I->on_pool = false;
+  pool_release(I->device);
+}
+static void release_streams(pzk_instance* I) {
+  pool_leave(I);
+  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post, I->s_mm,
+                        I->s_sha2})
+    if (s) (void)hipStreamDestroy(s);
+}
+
 static void free_all(pzk_instance* I) {
   free_scratch(I);
   void* ptrs[] = {I->d_regions, I->d_gen_pieces, I->d_sha_prog, I->d_pos_prog, I->d_sha, I->d_pos, I->d_loads, I->d_level_task,
@@ -432,9 +490,7 @@ static void free_all(pzk_instance* I) {
     if (p) (void)hipFree(p);
   for (auto* p : I->d_work)
     if (p) (void)hipFree(p);
-  for (hipStream_t s : {I->stream, I->s_rsa, I->s_sha, I->s_emit, I->s_tail, I->s_chain2, I->s_chain3, I->s_post, I->s_mm,
-                        I->s_sha2})
-    if (s) (void)hipStreamDestroy(s);
+  release_streams(I);
   for (hipEvent_t e : {I->ev_load, I->ev_sha, I->ev_rsa, I->ev_bjj, I->ev_entry, I->ev_dep, I->ev_pos, I->ev_tab,
                        I->ev_smt, I->ev_chain})
     if (e) (void)hipEventDestroy(e);
@@ -722,29 +778,63 @@ static int check_exec_device(const pzk_instance* I, const pzk_exec* exec) {
   return 0;
 }
 
-// A register instance's chain and post-chain streams, created at its first call. The SMT chain streams (s_tail,
-// s_chain2) are high priority: besides dispatch order this sets the hardware queues — HIP gives each stream priority
-// a pool of GPU_MAX_HW_QUEUES (4 by default) queues and lets streams share one beyond that, and a shared queue runs
-// its streams' packets in submission order, so a stream waiting for the chain stalls the other. One instance: high
-// main, rsa, s_tail, s_chain2; low s_sha, s_emit, s_post — nothing shared (config 4 58.3k -> 71.4k witnesses/s,
-// profiles/r5c). Several register instances in one process (config 5: one per flow) are another matter: with every
-// instance's full set config 5 ran 8.5k witnesses/s, with low-priority chain streams and post-chain streams 31.9k,
-// with neither 48.2k — and with the first instance's full set beside the others' rounds 1-4 sets, 4.9k
-// (profiles/r5j-r5l). So an instance that shares its device with other register instances takes the rounds 1-4 set
-// (low-priority chain streams, no post-chain stream). The count is per device and is re-checked at every call: an
-// instance whose set no longer matches (another instance appeared on its device, or went away) drains its streams
-// and rebuilds the set, so the order in which a caller creates and first runs its instances does not matter.
-// PZK_CHAIN_PRIO=hi|lo and PZK_POST=0|1 force either. The streams are created into locals and assigned only once all
-// exist: a failure leaves the instance without a set (retried at the next call), never with half of one.
+// A register instance's chain and post-chain streams, chosen at every call. The SMT chain streams (s_tail, s_chain2)
+// are high priority: besides dispatch order this sets the hardware queues — HIP gives each stream priority a pool of
+// GPU_MAX_HW_QUEUES (4 by default) queues and lets streams share one beyond that, and a shared queue runs its streams'
+// packets in submission order, so a stream waiting for the chain stalls the other. One instance: high main, rsa,
+// s_tail, s_chain2; low s_sha, s_emit, s_post (+ s_sha2 for sparse maps) — nothing shared (config 4 58.3k -> 71.4k
+// witnesses/s, profiles/r5c). Several register instances on one device (config 5: one per flow) with a set each
+// overflow the queues (round 5: with every instance's full set config 5 ran 8.5k witnesses/s, with low-priority chain
+// streams and no post-chain streams 48.2k, but only at GPU_MAX_HW_QUEUES=16 — ~41k at the default 4, profiles/r4_hwq,
+// r5j-r5l). So an instance that shares its device with other register instances takes the reduced set (low-priority
+// chain streams, no post-chain stream): config 5 46.9k witnesses/s at the default 4 queues (profiles/r6i). One set for
+// all instances of a device (PZK_SHARED_STREAMS=1: the device pool, PoolSet — their calls queue into the same eight
+// streams in submission order, which fit the default queues) measured 43.2k there: a flow's long chain (the ECDSA core
+// on s_rsa) then blocks the next flow's cores. The count is per device and is re-checked at every call: an instance
+// whose set no longer matches (another instance appeared on its device, or went away) drains its streams and
+// rebuilds, so the order in which a caller creates and first runs its instances does not matter. PZK_CHAIN_PRIO=hi|lo
+// and PZK_POST=0|1 force the reduced set's choices.
+// Own sets are created into locals and assigned only once all exist: a failure leaves the instance without a set
+// (retried at the next call), never with half of one.
 static int ensure_chain_streams(pzk_instance* I) {
   if (!I->lay.is_register) return 0;
   const bool shared = register_count(I->device) > 1;
-  if (I->s_tail && I->chain_set_shared == shared) return 0;
-  if (I->s_tail) {  // the set no longer fits: drain every call in flight, then replace it
+  const bool pool = shared && shared_streams_on();
+  // odd calls' SHA emission on a second stream: default for mapped layouts keeping at most half of the signals
+  // (O2-shaped 206.9k -> 218.5k witnesses/s; O1-shaped, 56 % kept, 130.8k -> 130.2k: profiles/r5q); the O0 layout
+  // keeps one (+1 % with two, but each k_emit_sha launch then runs beside the other call's and takes twice as long:
+  // its roofline line would read 0.35 for the same HBM work, profiles/r5p). PZK_SHA_STREAMS=1|2 forces either.
+  const char* ss_env = getenv("PZK_SHA_STREAMS");
+  I->sha2_on = ss_env ? atoi(ss_env) >= 2 : I->d_keep_bits != nullptr && 2 * I->out_size <= I->lay.wit_size;
+  if (pool ? I->on_pool : (I->s_tail && !I->on_pool && I->chain_set_shared == shared)) return 0;
+  if (I->s_tail || I->on_pool) {  // the set no longer fits: drain every call in flight, then replace it
     int rc = sync_all(I);
     if (rc) return rc;
-    for (hipStream_t* s : {&I->s_tail, &I->s_chain2, &I->s_chain3, &I->s_post, &I->s_mm, &I->s_sha2})
-      if (*s) { (void)hipStreamDestroy(*s); *s = nullptr; }
+    if (I->on_pool) {
+      pool_leave(I);
+    } else {
+      for (hipStream_t* s : {&I->s_tail, &I->s_chain2, &I->s_chain3, &I->s_post, &I->s_mm, &I->s_sha2})
+        if (*s) { (void)hipStreamDestroy(*s); *s = nullptr; }
+    }
+  }
+  if (pool) {  // the device's one set: every register instance on it queues into the same eight streams
+    hipStream_t p[8];
+    if (!pool_acquire(I->device, I->prio_lo, I->prio_hi, p))
+      return fail(PZK_E_HIP, "hipStreamCreateWithPriority failed (the device's register stream set)");
+    I->own[0] = I->stream;
+    I->own[1] = I->s_rsa;
+    I->own[2] = I->s_sha;
+    I->own[3] = I->s_emit;
+    I->stream = p[0];
+    I->s_rsa = p[1];
+    I->s_tail = p[2];
+    I->s_chain2 = p[3];
+    I->s_sha = p[4];
+    I->s_emit = p[5];
+    I->s_post = p[6];
+    I->s_sha2 = p[7];
+    I->on_pool = true;
+    return 0;
   }
   hipStream_t made[6] = {};  // s_tail, s_chain2, s_chain3, s_post, s_mm, s_sha2
   auto create = [&](int k, int prio) -> bool {
@@ -765,13 +855,7 @@ static int ensure_chain_streams(pzk_instance* I) {
     const bool hi = mp_env && !strcmp(mp_env, "hi");
     ok = create(4, hi ? I->prio_hi : I->prio_lo);
   }
-  // two SHA emitter streams: default for mapped layouts keeping at most half of the signals (O2-shaped 206.9k ->
-  // 218.5k witnesses/s; O1-shaped, 56 % kept, 130.8k -> 130.2k: profiles/r5q); the O0 layout keeps one (+1 % with
-  // two, but each k_emit_sha launch then runs beside the other call's and takes twice as long: its roofline line
-  // would read 0.35 for the same HBM work, profiles/r5p). PZK_SHA_STREAMS=1|2 forces either.
-  const char* ss_env = getenv("PZK_SHA_STREAMS");
-  const bool sha2 = ss_env ? atoi(ss_env) >= 2 : I->d_keep_bits != nullptr && 2 * I->out_size <= I->lay.wit_size;
-  if (ok && sha2 && !shared) ok = create(5, I->prio_lo);
+  if (ok && I->sha2_on && !shared) ok = create(5, I->prio_lo);
   if (!ok) {
     for (hipStream_t s : made)
       if (s) (void)hipStreamDestroy(s);
@@ -880,7 +964,7 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     return 0;
   };
   hipStream_t s_rsa = serial ? st : I->s_rsa, s_emit = serial ? st : I->s_emit,
-              s_sha = serial ? st : I->s_sha2 && lay.is_register && (I->calls & 1) ? I->s_sha2 : I->s_sha,
+              s_sha = serial ? st : I->s_sha2 && I->sha2_on && lay.is_register && (I->calls & 1) ? I->s_sha2 : I->s_sha,
               s_own = serial ? st : I->s_tail;
   if (d_status) HIPCHK(hipMemsetAsync(d_status, 0, sizeof(int32_t) * batch, st));
   { PhaseScope ps(T, slot, PH_LOAD, st);

@@ -5,6 +5,7 @@
 
 #include "../../include/pzkwit.h"
 #include "host_api.hpp"
+#include "pos_prog.hpp"
 
 namespace pzk {
 
@@ -78,6 +79,7 @@ void map_program(const Layout& lay, const std::vector<uint32_t>& inv, bool force
   for (uint32_t g : inv) out.bits[g >> 6] |= 1ull << (g & 63);
   for (size_t i = 1; i < nw; i++) out.rank[i] = out.rank[i - 1] + (uint32_t)__builtin_popcountll(out.bits[i - 1]);
   auto kept = [&](uint64_t g) { return (out.bits[g >> 6] >> (g & 63)) & 1; };
+  bool mix_t[POS_MAX_T + 1] = {};
   auto kept_in = [&](uint64_t a, uint64_t n) {
     uint64_t c = 0;
     for (uint64_t g = a; g < a + n; g++) c += kept(g);
@@ -116,9 +118,14 @@ void map_program(const Layout& lay, const std::vector<uint32_t>& inv, bool force
       else continue;
       wk.pad = (uint32_t)out.mprog.size();
       for (uint32_t q = 0; q < wk.count; q++)
-        if (kept(R.off + wk.start + q)) out.mprog.push_back(src ? src[q] : src16[q]);
+        if (kept(R.off + wk.start + q)) {
+          out.mprog.push_back(src ? src[q] : src16[q]);
+          if (src16) mix_t[lay.pos[R.a[0]].n + 1] |= (pos_img_need_t(lay.pos[R.a[0]].n + 1, src16[q]) & PI_MIX) != 0;
+        }
     }
   }
+  for (int t = 2; t <= POS_MAX_T; t++)
+    if (!mix_t[t]) out.pos_nomix |= 1u << t;
   if (out.mprog.empty()) out.mprog.push_back(0);
 }
 

@@ -34,6 +34,7 @@ struct MapProgram {
   std::vector<uint64_t> bits;
   std::vector<uint32_t> rank, mprog;
   std::vector<Work> work[E_COUNT];  // the work lists of E_SHA, E_SHAD, E_POS, E_ECT with Work.pad set
+  uint32_t pos_nomix = 0;           // bit t: no kept signal of a width-t Poseidon block reads a GetSum row (pos_prog.hpp)
 };
 void map_program(const Layout& lay, const std::vector<uint32_t>& inv, bool force_gather, MapProgram& out);
 

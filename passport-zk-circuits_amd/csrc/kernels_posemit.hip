@@ -32,7 +32,10 @@ __global__ void __launch_bounds__(EMIT_THREADS, T <= 3 ? 5 : 1) k_emit_pos(DevLa
                                                           const fr* pos_core, uint8_t* wtns, size_t stride, uint32_t batch,
                                                           uint32_t wpb, bool kept_fill) {
   constexpr PosImg I(T);
-  __shared__ fr img[I.size];
+  // the image: dynamic LDS of I.size elements, or I.fs when no block of the launch keeps a GetSum signal (mapped
+  // layouts, DevLayout.pos_nomix: the image parts from fs on are never filled or read then)
+  extern __shared__ uint4 pos_img_lds[];
+  fr* img = reinterpret_cast<fr*>(pos_img_lds);
   const Work wk = work[blockIdx.x];
   const Region R = L.regions[wk.region];
   const PosTask& task = L.pos[R.a[0]];  // global: in_slot is indexed at run time
@@ -164,9 +167,23 @@ hipError_t launch_emit_pos(const DevLayout& L, const Work* work, uint32_t n_work
   const uint32_t wpb = pos_wpb();
   static const bool kept_fill = getenv("PZK_POS_FULL") == nullptr;  // A/B: mapped blocks fill the whole image
   dim3 g(n_work, (batch + wpb - 1) / wpb), blk(EMIT_THREADS);
+  // LDS image size (k_emit_pos): the part before the GetSum rows when the launch's blocks keep none of them. The
+  // width-6 image is 63 KB, and beside the other emitters' workgroups (k_emit_sha 20 KB, k_emit_mm 32 KB, ... packed
+  // onto every CU) such a workgroup waited for a CU with that much LDS free: k_emit_pos<6> ran 40x its standalone
+  // time in the concurrent schedule and its stream paced the O2-shaped line (profiles/r6k)
+  const bool small = L.keep.bits && kept_fill && ((L.pos_nomix >> t) & 1u);
+  const size_t lds = 32ull * (small ? (size_t)PosImg(t).fs : (size_t)PosImg(t).size);
 #define PZK_POS_LAUNCH(T_)                                                                                              \
-  hipLaunchKernelGGL((L.keep.bits ? k_emit_pos<T_, MAP_DIRECT> : k_emit_pos<T_, MAP_O0>), g, blk, 0, st, L, work, K, B.vs, \
-                     B.pos_core, B.wtns, B.stride, batch, wpb, kept_fill)
+  {                                                                                                                    \
+    auto kern = L.keep.bits ? k_emit_pos<T_, MAP_DIRECT> : k_emit_pos<T_, MAP_O0>;                                     \
+    static bool attr[2] = {false, false};                                                                              \
+    if (!attr[L.keep.bits ? 1 : 0]) {                                                                                  \
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                         \
+                                32 * PosImg(T_).size);                                                                 \
+      attr[L.keep.bits ? 1 : 0] = true;                                                                                \
+    }                                                                                                                  \
+    hipLaunchKernelGGL(kern, g, blk, lds, st, L, work, K, B.vs, B.pos_core, B.wtns, B.stride, batch, wpb, kept_fill);   \
+  }
   switch (t) {
     case 2: PZK_POS_LAUNCH(2); break;
     case 3: PZK_POS_LAUNCH(3); break;

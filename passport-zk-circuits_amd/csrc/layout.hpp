@@ -297,6 +297,7 @@ struct DevLayout {
   uint32_t ec_tab_entries;          // table entries per witness
   KeepMap keep;                     // direct emission into a .sym-mapped witness (mapsink.hpp)
   const uint32_t* mprog;            // mapped: kept descriptors of the SHA / Poseidon / EC table work items, at Work.pad
+  uint32_t pos_nomix;               // mapped: bit t set when no width-t block keeps a GetSum signal (k_emit_pos LDS size)
 };
 
 }  // namespace pzk

@@ -306,28 +306,8 @@ __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& 
 // of wave work per block against 10.5 here.)
 // Image parts a block's stored signals may need beyond the S-box powers x^2, x^4, x^5 and the Ark outputs, which are
 // always filled: a mapped block (a .sym layout) fills only those its kept signals read (pos_img_need)
-enum : uint32_t {
-  PI_X = 1,     // S-box inputs x (full rounds; partial rounds' state 0)
-  PI_ST = 2,    // the other partial-round states and Y_RP
-  PI_MIX = 4,   // the GetSum rows: products, prefix sums (full mix, mixLast, partial mix)
-  PI_MISC = 8,  // hash inputs / output, the zero
-  PI_ALL = 15
-};
 template <int T>
-__device__ __forceinline__ uint32_t pos_img_need(uint32_t d) {  // the image part descriptor d reads
-  constexpr PosImg I(T);
-  if ((int)d < I.p2) return PI_X;
-  if ((int)d < I.fs) return 0;
-  if ((int)d < I.pin) return PI_MIX;
-  if ((int)d < I.pp2) {
-    const int k = (int)d - I.pin, r = k / T;
-    return (r < I.rp && k - r * T == 0) ? PI_X : PI_ST;
-  }
-  if ((int)d < I.ps) return 0;
-  if ((int)d < I.inp) return PI_MIX;
-  if ((int)d < I.pr) return PI_MISC;
-  return PI_MIX;
-}
+__device__ __forceinline__ uint32_t pos_img_need(uint32_t d) { return pos_img_need_t(T, d); }
 
 // core: the permutation's round states in Montgomery form, canonical (k_pos_core, k_pos_core1) or below 2.2p
 // (k_smt_chain4): every core value read here goes through fr_mul_fast or fr_from_mont_fast, whose results are

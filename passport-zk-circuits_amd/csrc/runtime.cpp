@@ -244,6 +244,7 @@ struct pzk_instance {
   uint64_t* d_keep_bits = nullptr;
   uint32_t* d_keep_rank = nullptr;
   uint32_t* d_mprog = nullptr;  // the kept elements' descriptors of the descriptor-driven work items (Work.pad)
+  uint32_t pos_nomix = 0;       // DevLayout.pos_nomix (mapped instances)
   uint32_t ect_split = ~0u;     // ECDSA: EC table work items [0, ect_split) on the signature stream, the rest on s_sha
   // any other map: O0 chunks into staging slots, then k_wtns_gather
   uint32_t* d_map = nullptr;      // out_size entries: O0 index of output element k
@@ -296,6 +297,7 @@ struct pzk_instance {
     L.ec_tab_entries = lay.ec_tab_entries;
     L.keep = KeepMap{d_keep_bits, d_keep_rank};
     L.mprog = d_mprog;
+    L.pos_nomix = pos_nomix;
     return L;
   }
 };
@@ -679,6 +681,7 @@ static int pzk_instance_create_mapped_impl(const pzk_params* params, const char*
       I->lay.work[e] = mp.work[e];
     }
     ok = ok && upload(&I->d_mprog, mp.mprog) == 0;
+    I->pos_nomix = mp.pos_nomix;
   } else {
     ok = upload(&I->d_map, inv) == 0;
   }

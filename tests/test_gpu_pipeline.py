@@ -1,9 +1,9 @@
 """GPU: the scheduling paths of calls left in flight (runtime.cpp batch_locked / ensure_chain_streams), each
 against the CPU oracle rather than against another run of the same code:
 
-* two register instances on one device, both created before the first call, so both take the shared stream set
-  (low-priority SMT chain streams, no post-chain stream); calls alternate between them without synchronising,
-  then one instance is destroyed and the other's next calls rebuild its stream set (the full, unshared one);
+* two register instances on one device, so both take the reduced stream set (low-priority SMT chain streams, no
+  post-chain stream); calls alternate between them without synchronising, then one instance is destroyed and the
+  other's next calls drain and rebuild its stream set (the full one);
 * an O2-shaped mapped instance (a monotone .sym keeping a quarter of the signals: odd calls' SHA emission on the
   second SHA stream) with back-to-back unsynchronised calls;
 * QueryIdentity(80) with more calls in flight than it has scratch sets' worth of chain streams (six sets over four

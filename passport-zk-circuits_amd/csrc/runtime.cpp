@@ -991,20 +991,35 @@ static int batch_locked(pzk_instance* I, const uint8_t* d_inputs, size_t batch, 
     { PhaseScope ps(T, slot, PH_SMT, st); HIPCHK(launch_smt_prep(L, d_inputs, vs, S.d_smt_core, d_status, st));
       HIPCHK(launch_smt_order(S.d_smt_core, L.smt_core_fr, S.d_smt_order, B, st)); }
     { PhaseScope ps(T, slot, PH_POS_CORE, st); if ((rc = pos_levels(4, 6, S.d_smt_order))) return rc; }
-    { PhaseScope ps(T, slot, PH_SMT, st);
-      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
-                              st)); }
-    HIPCHK(hipEventRecord(I->ev_pos, st));
     // PZK_QRY_EMIT1=1: every emitter on one stream (with 3 chain streams that is 4 streams in use = the
     // hardware queues a process gets by default)
     static const bool emit1 = getenv("PZK_QRY_EMIT1") != nullptr;
     hipStream_t s_pe = emit1 ? s_sha : s_emit;
-    HIPCHK(hipStreamWaitEvent(s_pe, I->ev_pos, 0));
-    if ((rc = emit(E_POS, s_pe))) return rc;
-    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_pos, 0));
-    if ((rc = emit(E_GEN, s_sha))) return rc;
-    if ((rc = emit(E_QRY, s_sha))) return rc;
-    if ((rc = emit(E_BITS, s_sha))) return rc;  // Num2Bits(254) of the tree position reads level 3
+    // PZK_QRY_SPLIT=0|1 (A/B): what does not read the SMT chain — the Poseidon blocks before pos_chain_group, E_GEN's
+    // regions before gen_chain_work, the query checks and the bit decompositions — is emitted before the chain, the
+    // rest after it, as the register circuit's post-chain split does
+    static const bool split = [] { const char* e = getenv("PZK_QRY_SPLIT"); return e ? atoi(e) != 0 : true; }();
+    if (split) {
+      HIPCHK(hipEventRecord(I->ev_pos, st));
+      HIPCHK(hipStreamWaitEvent(s_pe, I->ev_pos, 0));
+      if ((rc = emit(E_POS, s_pe, 0, lay.pos_chain_group))) return rc;
+      HIPCHK(hipStreamWaitEvent(s_sha, I->ev_pos, 0));
+      if ((rc = emit(E_QRY, s_sha))) return rc;
+      if ((rc = emit(E_BITS, s_sha))) return rc;  // Num2Bits(254) of the tree position reads level 3
+      if ((rc = emit(E_GEN, s_sha, 0, lay.gen_chain_work))) return rc;
+    }
+    { PhaseScope ps(T, slot, PH_SMT, st);
+      HIPCHK(launch_smt_chain(L, K, I->d_level_task, d_inputs, vs, S.d_pos_core, S.d_smt_core, S.d_smt_order, d_status,
+                              st)); }
+    HIPCHK(hipEventRecord(I->ev_chain, st));
+    HIPCHK(hipStreamWaitEvent(s_pe, I->ev_chain, 0));
+    if ((rc = emit(E_POS, s_pe, split ? lay.pos_chain_group : 0))) return rc;
+    HIPCHK(hipStreamWaitEvent(s_sha, I->ev_chain, 0));
+    if ((rc = emit(E_GEN, s_sha, split ? lay.gen_chain_work : 0))) return rc;
+    if (!split) {
+      if ((rc = emit(E_QRY, s_sha))) return rc;
+      if ((rc = emit(E_BITS, s_sha))) return rc;
+    }
   } else if (!lay.is_register) {
     // standalone circuits: the core on the main stream; PoseidonHash(n)'s emitters on the emit stream behind it, so
     // call k's emitters run beside call k + 1's core (config 1 27.2M -> 28.7M witnesses/s); the SHA hashers' stay on

@@ -27,6 +27,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md: a wave
 # issues each VALU instruction over 2 cycles), 2.4 GHz max clock -> G wave-instructions/s
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2
+# Measured chip-wide issue rates (tools/fieldbench/issuebench.hip, profiles/r6p/issuebench.txt; 8 waves per SIMD,
+# independent chains): v_add_u32 975 G wave-instr/s; v_mad_u64_u32 515, v_lshl_add_u64 518, v_add_co_u32 541,
+# v_mul_lo_u32 549, v_mul_hi_u32 570, DPP moves 584. The field arithmetic is mostly of the second kind.
+VALU_RATE_SIMPLE_GIPS = 975.0
+VALU_RATE_INT64_GIPS = 515.0
+VALU_RATE_CARRY_GIPS = 541.0
 
 
 def log(*a):
@@ -558,11 +564,26 @@ def valu_roofline(tj, tf, value, world):
     ipw = tj["valu_insts_per_witness"]
     ach = ipw * value / 1e9
     top = sorted(((v.get("valu_insts_per_witness", 0), k) for k, v in tj["kernels"].items()), reverse=True)[:3]
-    return {"bound": "valu", "insts_per_witness": ipw, "achieved": round(ach, 1), "peak": VALU_PEAK_GIPS,
-            "unit": "G wave-instr/s", "frac": round(ach / (VALU_PEAK_GIPS * world), 4),
-            "top_kernels": {k: v for v, k in top}, "source": os.path.relpath(tf, REPO),
-            "note": "issue-rate bound (1 wave64 VALU instruction / 2 cycles / SIMD at 2.4 GHz); 64-bit "
-                    "integer multiply-adds take more than one issue slot, so the attainable fraction is < 1"}
+    res = {"bound": "valu", "insts_per_witness": ipw, "achieved": round(ach, 1), "peak": VALU_PEAK_GIPS,
+           "unit": "G wave-instr/s", "frac": round(ach / (VALU_PEAK_GIPS * world), 4),
+           "top_kernels": {k: v for v, k in top}, "source": os.path.relpath(tf, REPO),
+           "note": "issue-rate bound (1 wave64 VALU instruction / 2 cycles / SIMD at 2.4 GHz); 64-bit "
+                   "integer multiply-adds take more than one issue slot, so the attainable fraction is < 1"}
+    # the instruction classes of the same workload (tools/pmc_valu.py: SQ_INSTS_VALU_INT64 beside SQ_INSTS_VALU), priced
+    # at the measured issue rates: INT64 at v_mad_u64_u32's, the rest between v_add_u32's (lo) and a carry add's (hi)
+    vf = os.path.join(os.path.dirname(tf), "valu.json")
+    if os.path.exists(vf):
+        vj = json.load(open(vf))
+        i64 = sum(k.get("int64_per_witness", 0) for k in vj["kernels"].values())
+        rest = max(vj["valu_insts_per_witness"] - i64, 0.0)
+        busy = lambda r: value / world * (i64 / (VALU_RATE_INT64_GIPS * 1e9) + rest / (r * 1e9))
+        res["measured_issue"] = {"int64_per_witness": round(i64, 1), "other_per_witness": round(rest, 1),
+                                 "frac_lo": round(busy(VALU_RATE_SIMPLE_GIPS), 4),
+                                 "frac_hi": round(busy(VALU_RATE_CARRY_GIPS), 4),
+                                 "rates_gips": {"int64": VALU_RATE_INT64_GIPS, "simple": VALU_RATE_SIMPLE_GIPS,
+                                                "carry": VALU_RATE_CARRY_GIPS},
+                                 "source": os.path.relpath(vf, REPO)}
+    return res
 
 
 def phase_table(tm, info):

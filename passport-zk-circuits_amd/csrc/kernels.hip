@@ -346,7 +346,8 @@ hipError_t launch_prep(const DevLayout& L, const uint8_t* inputs, const uint32_t
 }
 
 hipError_t launch_qry_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, int32_t* status, hipStream_t st) {
-  hipLaunchKernelGGL(k_qry_prep, dim3(vs.batch), dim3(64), 0, st, L, inputs, vs, status);
+  hipLaunchKernelGGL(k_qry_prep, dim3((vs.batch + QP_WAVES - 1) / QP_WAVES), dim3(64 * QP_WAVES), 0, st, L, inputs, vs,
+                     status);
   return hipGetLastError();
 }
 

@@ -292,21 +292,28 @@ __device__ __forceinline__ El query_small(const DevLayout& L, const Bufs& B, con
 }
 
 // ============================================================================ k_qry_prep
-// wave = witness. DG1DataExtractor fields and the dg1 commitment chunks (Bits2Num over input bits, 64 per
-// ballot as in k_prep), the citizenship's list index and the 240 IsEqual inverses (one batched inversion across
-// the wave), and the checks of the query templates: ForceEqualIfEnabled (19), DateDecoder re-encoding (20),
-// CitizenshipCheck (21, 22), LessThan(8) ranges of the date comparisons (1), input range (64).
+// wave = witness, QP_WAVES witnesses per workgroup. DG1DataExtractor fields and the dg1 commitment chunks (Bits2Num
+// over input bits, 64 per ballot as in k_prep), the citizenship's list index and the 240 IsEqual inverses (one batched
+// inversion across the wave, whose single field inversion is shared by the workgroup's witnesses: wave 0 inverts
+// the QP_WAVES wave totals at once — a wave inverting its own total spent ~75 % of the kernel's VALU on it), and the
+// checks of the query templates: ForceEqualIfEnabled (19), DateDecoder re-encoding (20), CitizenshipCheck (21, 22),
+// LessThan(8) ranges of the date comparisons (1), input range (64).
+constexpr int QP_WAVES = 8;
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
-__global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, int32_t* status) {
+__global__ void __launch_bounds__(64 * QP_WAVES) k_qry_prep(DevLayout L, const uint8_t* inputs, ValueStore vs,
+                                                            int32_t* status) {
   core_priority();
-  const uint32_t w = blockIdx.x;
-  if (w >= vs.batch) return;  // whole wave
-  const int lane = threadIdx.x;
+  __shared__ fr s_tot[QP_WAVES];
+  const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const uint32_t w0 = blockIdx.x * QP_WAVES + (uint32_t)wv;
+  const bool live = w0 < vs.batch;  // a wave past the batch takes part in the barriers only
+  const uint32_t w = live ? w0 : vs.batch - 1;
   const RegInfo& R = L.reg;
   const QView Q = q_view(L, inputs, w);
   const bool td1 = R.q_td1 != 0;
   bool bad = false;
-  if (lane == 0) vs.at(R.v_one, w) = fr_mont_one();
+  const bool wr = live && lane == 0;  // a wave past the batch stores nothing
+  if (wr) vs.at(R.v_one, w) = fr_mont_one();
   uint64_t f64[9];
 #pragma unroll
   for (int k = 0; k < 9; k++) {
@@ -314,12 +321,12 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
     const int Lk = td1 ? Q1_DGX_L[k] : Q_DGX_L[k], Sk = td1 ? Q1_DGX_SHIFT[k] : Q_DGX_SHIFT[k];
     const fr v = wave_bits_fr(Q.row, QI_DG1 + Sk, Lk, -1, bad);
     f64[k] = (uint64_t)v.v[0] | ((uint64_t)v.v[1] << 32);
-    if (lane == 0) vs.at(R.q_dgf + k, w) = fr_to_mont(v);
+    if (wr) vs.at(R.q_dgf + k, w) = fr_to_mont(v);
   }
   const int CH = q_chunk(td1);
   for (int i = 0; i < 4; i++) {  // dg1Chunking[i] = Bits2Num(186 | 190), in[j] = dg1[CH i + j] (queryIdentity.circom:192-198)
     const fr v = wave_bits_fr(Q.row, QI_DG1 + CH * i, CH, +1, bad);
-    if (lane == 0) vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
+    if (wr) vs.at(R.v_dg1 + i, w) = fr_to_mont(v);
   }
   // CitizenshipCheck: index of the citizenship in COUNTRY_ARR and 1 / (citizenship - COUNTRY_ARR[i])
   const uint64_t cit = f64[q_f_cit(td1)];
@@ -339,7 +346,19 @@ __global__ void __launch_bounds__(64) k_qry_prep(DevLayout L, const uint8_t* inp
   }
   fr others, total;
   fr_group_others<64>(acc, others, total);
-  fr inv = fr_mul(fr_inv_sw<true>(total), others);  // = 1 / acc (4 waves per SIMD: the throughput product)
+  // the workgroup's totals inverted together: lane k of wave 0 holds wave k's total (a lane past QP_WAVES one)
+  if (lane == 0) s_tot[wv] = live ? total : fr_mont_one();
+  __syncthreads();
+  if (wv == 0) {
+    const fr t = lane < QP_WAVES ? s_tot[lane] : fr_mont_one();
+    fr t_others, t_all;
+    fr_group_others<QP_WAVES>(t, t_others, t_all);
+    const fr t_inv = fr_mul(fr_inv_sw<true>(t_all), t_others);  // = 1 / total of wave `lane`
+    if (lane < QP_WAVES) s_tot[lane] = t_inv;  // (read above, by this wave only)
+  }
+  __syncthreads();
+  if (!live) return;
+  fr inv = fr_mul(s_tot[wv], others);  // = 1 / acc
 #pragma unroll
   for (int j = 3; j >= 0; j--) {
     const int i = lane + 64 * j;

@@ -374,7 +374,11 @@ hipError_t launch_bjj_core(const DevLayout& L, ValueStore vs, const fr* table, f
   const uint32_t lanes = vs.batch * segs;
   if (scratch) {
     auto kern = segs == 8 ? k_bjj_core<8> : segs == 32 ? k_bjj_core<32> : k_bjj_core<16>;
-    hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, scratch, vs.batch);
+    const uint32_t wg = 64 * BJJ_WG_WAVES;
+    // PZK_BJJ_PAIRED=0 (A/B): every lane sums its own segment start (bjj_seg_start) instead of the balanced pairs
+    static const bool paired = !getenv("PZK_BJJ_PAIRED") || atoi(getenv("PZK_BJJ_PAIRED")) != 0;
+    hipLaunchKernelGGL(kern, dim3((lanes + wg - 1) / wg), dim3(wg), 0, st, L, vs, table, bjj_core, scratch, vs.batch,
+                       paired);
   } else {
     auto kern = segs == 16 ? k_bjj_core_rc<16> : segs == 32 ? k_bjj_core_rc<32> : k_bjj_core_rc<64>;
     hipLaunchKernelGGL(kern, dim3((lanes + 63) / 64), dim3(64), 0, st, L, vs, table, bjj_core, vs.batch);

@@ -50,15 +50,18 @@ hipError_t launch_rsa_core(const DevLayout& L, const uint8_t* inputs, uint64_t* 
   const bool lane = rsa_core_lane() && colsum;
   if (L.reg.K == 48) {  // RSA-3072 (SIGNATURE_TYPE 14): cooperative core only
     HIP_TRY((launch_rsa_core2<48, 16>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<48>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
+    hipLaunchKernelGGL(k_rsa_inv<48>, dim3((batch + RI_WAVES - 1) / RI_WAVES), dim3(64 * RI_WAVES), 0, st, L, inputs,
+                       rsa_core, batch);
   } else if (L.reg.K == 32) {
     HIP_TRY((lane ? launch_rsa_lane<32, 64>(L, inputs, rsa_core, colsum, status, batch, st)
                   : launch_rsa_core2<32, 8>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<32>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
+    hipLaunchKernelGGL(k_rsa_inv<32>, dim3((batch + RI_WAVES - 1) / RI_WAVES), dim3(64 * RI_WAVES), 0, st, L, inputs,
+                       rsa_core, batch);
   } else {
     HIP_TRY((lane ? launch_rsa_lane<64, 32>(L, inputs, rsa_core, colsum, status, batch, st)
                   : launch_rsa_core2<64, 16>(L, inputs, rsa_core, status, batch, st)));
-    hipLaunchKernelGGL(k_rsa_inv<64>, dim3(batch), dim3(64), 0, st, L, inputs, rsa_core, batch);
+    hipLaunchKernelGGL(k_rsa_inv<64>, dim3((batch + RI_WAVES - 1) / RI_WAVES), dim3(64 * RI_WAVES), 0, st, L, inputs,
+                       rsa_core, batch);
   }
   return hipGetLastError();
 }

@@ -331,41 +331,69 @@ __global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inp
 // IsEqual inverses of (r_i - n_i) for every limb of every BigMultModP (BigLessEqThan,
 // bigIntComparators.circom:50-75; IsZero.inv = 1/in or 0, comparators.circom:17): one wave per
 // witness, one batched inversion over the 17 x K differences. Lane l takes a contiguous run of
-// elements; the run products are combined across the wave with shuffles, so the single Fr
-// inversion is shared by the 64 lanes. Output: normal form, in each BigMultModP's inv slots.
+// elements; the run products are combined across the wave with shuffles, and the wave totals of the workgroup's
+// RI_WAVES witnesses are inverted together by wave 0 (one Fr inversion per wave was ~85 % of the kernel's VALU).
+// Output: normal form, in each BigMultModP's inv slots.
+constexpr int RI_WAVES = 8;
+// f(integral_constant<int, J>) for J = J0 .. N - 1, unrolled by construction (register arrays indexed by J stay in
+// registers; a #pragma unroll of the same loop leaves them in scratch once the body is large)
+template <int J, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (J < N) {
+    f(std::integral_constant<int, J>{});
+    static_for<J + 1, N>(f);
+  }
+}
 template <int K>
-__global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core, uint32_t batch) {
+__global__ void __launch_bounds__(64 * RI_WAVES) k_rsa_inv(DevLayout L, const uint8_t* inputs, uint64_t* rsa_core,
+                                                           uint32_t batch) {
   core_priority();
-  const uint32_t w = blockIdx.x;
-  if (w >= batch) return;
-  const int lane = threadIdx.x;
-  const int NE = L.reg.n_modmul * K, PER = (NE + 63) / 64;
+  // the run's exclusive prefix products stay in registers ([element of the run]): parked in the core's inverse
+  // slots they cost a write and a read of 32 B per IsEqual, and each read waited for the run's stores
+  // (up to 20 multiplications: 65537, 3, 37187; a longer PowerMod schedule parks them in the slots as before)
+  // (up to 12 per lane, RSA-2048 / 3072: 20 multiplications; RSA-4096 and a longer PowerMod schedule park them in the
+  // slots)
+  constexpr int PER_MAX = (20 * K + 63) / 64 < 12 ? (20 * K + 63) / 64 : 12;
+  __shared__ fr s_tot[RI_WAVES];
+  __shared__ fr s_out[RI_WAVES][64];  // element-order staging of the stores
+  const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const uint32_t w0 = blockIdx.x * RI_WAVES + (uint32_t)wv;
+  const bool live = w0 < batch;  // a wave past the batch takes part in the barriers only, and stores nothing
+  const uint32_t w = live ? w0 : batch - 1;
+  // (the layout's fields as locals: a lambda below that reached the by-value kernel argument put a copy of it in scratch)
+  const int NE = L.reg.n_modmul * K, PER = (NE + 63) / 64, in_pk = (int)L.reg.in_pk;
   constexpr int MMW = MM_CORE_WORDS(K);
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   uint64_t* core = rsa_core + (size_t)w * L.rsa_core_words;
-  const int e0 = lane * PER, e1 = e0 + PER < NE ? e0 + PER : NE;
-  auto diff = [&](int e) -> fr {  // (r_i - n_i) in Montgomery form
+  const int e0 = lane * PER, e1 = !live ? e0 : e0 + PER < NE ? e0 + PER : NE;
+  auto diff = [=](int e) -> fr {  // (r_i - n_i) in Montgomery form
     const int k = e / K, i = e - k * K;
-    const uint64_t a = core[(size_t)k * MMW + 3 * K + 1 + i], b = in_u64(row + 32ull * (L.reg.in_pk + i));
+    const uint64_t a = core[(size_t)k * MMW + 3 * K + 1 + i], b = in_u64(row + 32ull * (in_pk + i));
     fr d = a >= b ? fr_u64(a - b) : fr_sub(fr_zero(), fr_u64(b - a));
     return fr_to_mont(d);
   };
-  auto slot = [&](int e) -> uint8_t* {
+  auto slot = [=](int e) -> uint8_t* {
     const int k = e / K, i = e - k * K;
     return reinterpret_cast<uint8_t*>(core + (size_t)k * MMW + 4 * K + 1 + 4 * i);
   };
-  // the run's exclusive prefix products stay in LDS ([element of the run][lane]): parked in the core's inverse
-  // slots they cost a write and a read of 32 B per IsEqual, and each read waited for the run's stores
-  // (up to 20 multiplications: 65537, 3, 37187; a longer PowerMod schedule parks them in the slots as before)
-  constexpr int PER_MAX = (20 * K + 63) / 64;
-  __shared__ fr pre_run[PER_MAX * 64];
-  const bool in_lds = PER <= PER_MAX;  // block-uniform
+  const bool in_reg = PER <= PER_MAX;  // grid-uniform
+  fr pr[PER_MAX];
   fr acc = fr_mont_one();
-  for (int e = e0; e < e1; e++) {
-    fr d = diff(e);
-    if (in_lds) pre_run[(e - e0) * 64 + lane] = acc;  // exclusive prefix within the run
-    else store_fr(slot(e), acc);
-    if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+  if (in_reg) {
+    static_for<0, PER_MAX>([&](auto J) __attribute__((always_inline)) {
+      const int e = e0 + J();
+      if (e < e1) {
+        const fr d = diff(e);
+        pr[J()] = acc;  // exclusive prefix within the run
+        if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+      }
+    });
+  } else {
+    for (int e = e0; e < e1; e++) {
+      const fr d = diff(e);
+      store_fr(slot(e), acc);
+      if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+    }
   }
   // exclusive prefix / suffix products of the run products across the wave (log-step scans)
   fr incl = acc, sincl = acc;
@@ -377,22 +405,51 @@ __global__ void __launch_bounds__(64) k_rsa_inv(DevLayout L, const uint8_t* inpu
   fr pre = fr_shfl_up(incl, 1), suf = fr_shfl_down(sincl, 1);
   if (lane == 0) pre = fr_mont_one();
   if (lane == 63) suf = fr_mont_one();
-  const fr total = fr_shfl(incl, 63, 64);
-  fr inv = fr_mul(fr_mul(fr_inv(total), pre), suf);  // = 1 / (this run's product)
-  for (int e = e1 - 1; e >= e0; e--) {
-    fr d = diff(e);
-    fr r = fr_zero();
-    if (!fr_is_zero(d)) { r = fr_mul(inv, in_lds ? pre_run[(e - e0) * 64 + lane] : load_fr(slot(e))); inv = fr_mul(inv, d); }
-    r = fr_from_mont(r);
-    if (in_lds) pre_run[(e - e0) * 64 + lane] = r;  // the lane's own entry: read above, in this iteration
-    else store_fr(slot(e), r);
+  // the workgroup's wave totals inverted together (lane k of wave 0: wave k's total; a dead wave's is 1)
+  if (lane == 63) s_tot[wv] = incl;
+  __syncthreads();
+  if (wv == 0) {
+    const fr t = lane < RI_WAVES ? s_tot[lane] : fr_mont_one();
+    fr t_others, t_all;
+    fr_group_others<RI_WAVES>(t, t_others, t_all);
+    const fr t_inv = fr_mul(fr_inv(t_all), t_others);  // = 1 / total of wave `lane`
+    if (lane < RI_WAVES) s_tot[lane] = t_inv;  // (read above, by this wave only)
   }
-  if (!in_lds) return;
+  __syncthreads();
+  fr inv = fr_mul(fr_mul(s_tot[wv], pre), suf);  // = 1 / (this run's product)
+  if (!in_reg) {
+    if (!live) return;
+    for (int e = e1 - 1; e >= e0; e--) {
+      const fr d = diff(e);
+      fr r = fr_zero();
+      if (!fr_is_zero(d)) { r = fr_mul(inv, load_fr(slot(e))); inv = fr_mul(inv, d); }
+      store_fr(slot(e), fr_from_mont(r));
+    }
+    return;
+  }
+  static_for<0, PER_MAX>([&](auto J) __attribute__((always_inline)) {
+    constexpr int j = PER_MAX - 1 - J();
+    const int e = e0 + j;
+    if (e < e1) {
+      const fr d = diff(e);
+      fr r = fr_zero();
+      if (!fr_is_zero(d)) { r = fr_mul(inv, pr[j]); inv = fr_mul(inv, d); }
+      pr[j] = fr_from_mont(r);
+    }
+  });
   // written out in element order, 64 consecutive 32-byte inverse slots per store instruction: lane l's run is
   // elements [l PER, (l + 1) PER), so storing from the loop above put 64 partial lines of 64 different slots in
   // flight per iteration, and L2 wrote most lines twice (2.0x the inverse bytes, pmc_r4c3)
-  __syncthreads();  // the LDS writes above (other lanes' runs) before the reads below
-  for (int e = lane; e < NE; e += 64) store_fr(slot(e), pre_run[(e % PER) * 64 + e / PER]);
+  for (int t = 0; t < (NE + 63) / 64; t++) {  // (the same step count in every wave: NE is the instance's)
+    static_for<0, PER_MAX>([&](auto J) __attribute__((always_inline)) {
+      const int e = e0 + J();
+      if (e < e1 && (e >> 6) == t) s_out[wv][e & 63] = pr[J()];
+    });
+    __syncthreads();
+    const int e = 64 * t + lane;
+    if (live && e < NE) store_fr(slot(e), s_out[wv][lane]);
+    __syncthreads();
+  }
 }
 
 // ============================================================================ RSA EM checks
@@ -554,6 +611,46 @@ __device__ __forceinline__ void bjj_seg_start(const fr& sk, int i0, const fr* ta
     else A = bjj_add_affine(A, e[0], e[1], e[2], C.A);
   }
 }
+// The same start points with the table additions of each lane pair (seg, SEGS - 1 - seg) balanced: prefix lengths grow
+// with seg, so the lane with the shorter prefix also sums the top windows of its partner's and hands that partial sum
+// over (a wave shuffle and one general addition): a lane's additions go from up to SEGS - 1 windows (SEGS = 32: 31)
+// to about half. The sums start from the identity (0 : 1 : 1 : 0) — the addition law is complete on BabyJubJub
+// (a a square, d not) — so Z differs from bjj_seg_start's but the affine point and `have` do not.
+template <int SEGS, int SEG_LEN>
+__device__ __forceinline__ void bjj_seg_start_paired(const fr& sk, int seg, const fr* table, const BjjConsts& C,
+                                                     bool& have, ExtPt& A) {
+  static_assert(SEGS % 2 == 0 && SEG_LEN % 8 == 0, "lane pairs of whole windows");
+  constexpr int NWIN = SEG_LEN / 8;  // windows per segment of prefix
+  const int p = SEGS - 1 - seg;
+  const bool helper = seg < p;
+  const int n_own = NWIN * seg, n_p = NWIN * p, n_lo = helper ? n_own : n_p;
+  const int half = (n_own + n_p + 1) / 2, h = half - n_lo;  // h: the longer prefix's windows the helper sums
+  const int own_end = helper ? n_own : n_own - h;
+  const ExtPt id{fr_zero(), fr_mont_one(), fr_mont_one(), fr_zero()};
+  ExtPt Ao = id, Ah = id;
+  bool ho = false, hh = false;
+  for (int k = 0; k < half; k++) {
+    const bool mine = k < own_end;
+    if (!mine && !(helper && k - own_end < h)) continue;
+    const int i0x = SEG_LEN * (mine ? seg : p), wi = mine ? k : n_p - h + (k - own_end);
+    uint32_t v = 0;
+    for (int b = 0; b < 8; b++) v |= fr_bit(sk, 254 - i0x + 8 * wi + b) << b;
+    if (!v) continue;
+    const fr* e = table + 3 * (size_t)(wi * 256 + v);
+    const ExtPt cur = bjj_add_affine(mine ? Ao : Ah, e[0], e[1], e[2], C.A);
+    if (mine) { Ao = cur; ho = true; }
+    else { Ah = cur; hh = true; }
+  }
+  auto xo = [](const fr& a) { fr r; for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl_xor((int)a.v[k], SEGS - 1, 64); return r; };
+  const ExtPt got{xo(Ah.X), xo(Ah.Y), xo(Ah.Z), xo(Ah.T)};
+  const bool gh = __shfl_xor((int)hh, SEGS - 1, 64) != 0;
+  if (!helper && gh) {
+    Ao = ho ? bjj_add(Ao, got, C) : got;
+    ho = true;
+  }
+  have = ho;
+  A = Ao;
+}
 // ladder step i (curve.circom:156-168): D_i = 2 A_{i-1} when A_{i-1} exists (the (0,0) sentinel otherwise: D = 0),
 // A_i = D_i + Base8 when bit 253 - i of sk is set, else D_i
 __device__ __forceinline__ void bjj_step(const fr& sk, int i, const BjjConsts& C, bool& have, ExtPt& A, bool& haveD,
@@ -576,42 +673,33 @@ __device__ __forceinline__ void bjj_step(const fr& sk, int i, const BjjConsts& C
 // segments of BJJ_SEG_LEN steps, one lane each (BJJ_SEGS adjacent lanes = one witness): a segment
 // starts from A_{i0-1} = (sk >> (254 - i0)) * Base8, summed from the fixed-base table, so the
 // segments run in parallel. The affine outputs need 1/Z of every point (and 1/x of every D):
-// one batched inversion per witness, whose single Fr inversion is shared by the 8 lanes
-// through wave shuffles.
+// one batched inversion per witness across its lanes (wave shuffles), and one Fr inversion per workgroup: wave 0
+// inverts the BJJ_WG_WAVES * 64 / BJJ_SEGS witness totals at once (a Fr inversion per witness group was ~40 % of
+// the kernel's VALU).
 // scratch: SoA [elem][lane], 9 * SEG_LEN elements per lane (X,Y,Z of D and A, 3 prefixes).
 // SEGS (8 / 16 / 32 lanes per witness, SEG_LEN = 256 / SEGS steps each) trades the segment-start
 // table sums (up to i0 / 8 affine additions) against ladder length and occupancy.
+constexpr int BJJ_WG_WAVES = 4;
 template <int BJJ_SEGS>
-__global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, const fr* table, fr* bjj_core,
-                                                fr* scratch, uint32_t batch) {
-  constexpr int BJJ_SEG_LEN = BJJ_SCRATCH_STEPS / BJJ_SEGS;
+__global__ void __launch_bounds__(64 * BJJ_WG_WAVES) k_bjj_core(DevLayout L, ValueStore vs, const fr* table,
+                                                               fr* bjj_core, fr* scratch, uint32_t batch,
+                                                               bool paired) {
+  constexpr int BJJ_SEG_LEN = BJJ_SCRATCH_STEPS / BJJ_SEGS, NW = 64 * BJJ_WG_WAVES / BJJ_SEGS;
   static_assert(64 % BJJ_SEGS == 0 && BJJ_SEG_LEN * BJJ_SEGS >= BJJ_STEPS, "segments must cover the ladder");
+  static_assert(NW <= 64 && (NW & (NW - 1)) == 0, "the workgroup's witness totals: one per lane of wave 0");
+  __shared__ fr s_tot[NW];
   core_priority();
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nlanes = batch * BJJ_SEGS;
   const uint32_t w = tid / BJJ_SEGS;
   const int seg = (int)(tid % BJJ_SEGS);
-  if (w >= batch) return;  // whole lane groups only (64 % BJJ_SEGS == 0)
+  if (blockIdx.x * (uint32_t)NW >= batch) return;  // whole workgroups only (no lane of it is live)
+  const bool live = w < batch;  // a lane group past the batch takes part in the workgroup's barriers only
   BjjConsts C;
   C.init();
   const int NS = BJJ_STEPS;
   const int i0 = seg * BJJ_SEG_LEN, i1 = i0 + BJJ_SEG_LEN < NS ? i0 + BJJ_SEG_LEN : NS, ns = i1 - i0;
   auto S = [&](int e) -> fr& { return scratch[(size_t)e * nlanes + tid]; };
-  const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
-  bool have;
-  ExtPt A;
-  bjj_seg_start(sk, i0, table, C, have, A);
-  // projective coords of D_i (local elems 0..3ns) and A_i (3ns..6ns): [X, Y, Z] per step
-  for (int j = 0; j < ns; j++) {
-    ExtPt D;
-    bool haveD;
-    bjj_step(sk, i0 + j, C, have, A, haveD, D);
-    if (haveD) { S(3 * j) = D.X; S(3 * j + 1) = D.Y; S(3 * j + 2) = D.Z; }
-    else { S(3 * j) = fr_zero(); S(3 * j + 1) = fr_zero(); S(3 * j + 2) = fr_zero(); }
-    const int o = 3 * BJJ_SEG_LEN + 3 * j;
-    if (have) { S(o) = A.X; S(o + 1) = A.Y; S(o + 2) = A.Z; }
-    else { S(o) = fr_zero(); S(o + 1) = fr_zero(); S(o + 2) = fr_zero(); }
-  }
   // batched inversion of Z(D_i), Z(A_i), X(D_i) over the segment, then across the BJJ_SEGS lanes
   auto elem = [&](int qi) -> fr {
     int j = qi / 3, kind = qi - 3 * j;
@@ -619,14 +707,45 @@ __global__ void __launch_bounds__(64) k_bjj_core(DevLayout L, ValueStore vs, con
   };
   const int NQ = 3 * ns, PRE = 6 * BJJ_SEG_LEN;
   fr acc = fr_mont_one();
-  for (int qi = 0; qi < NQ; qi++) {
-    fr e = elem(qi);
-    S(PRE + qi) = acc;
-    if (!fr_is_zero(e)) acc = fr_mul(acc, e);
+  if (live) {
+    const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
+    bool have;
+    ExtPt A;
+    if (paired) bjj_seg_start_paired<BJJ_SEGS, BJJ_SEG_LEN>(sk, seg, table, C, have, A);
+    else bjj_seg_start(sk, i0, table, C, have, A);
+    // projective coords of D_i (local elems 0..3ns) and A_i (3ns..6ns): [X, Y, Z] per step
+    for (int j = 0; j < ns; j++) {
+      ExtPt D;
+      bool haveD;
+      bjj_step(sk, i0 + j, C, have, A, haveD, D);
+      if (haveD) { S(3 * j) = D.X; S(3 * j + 1) = D.Y; S(3 * j + 2) = D.Z; }
+      else { S(3 * j) = fr_zero(); S(3 * j + 1) = fr_zero(); S(3 * j + 2) = fr_zero(); }
+      const int o = 3 * BJJ_SEG_LEN + 3 * j;
+      if (have) { S(o) = A.X; S(o + 1) = A.Y; S(o + 2) = A.Z; }
+      else { S(o) = fr_zero(); S(o + 1) = fr_zero(); S(o + 2) = fr_zero(); }
+    }
+    for (int qi = 0; qi < NQ; qi++) {
+      fr e = elem(qi);
+      S(PRE + qi) = acc;
+      if (!fr_is_zero(e)) acc = fr_mul(acc, e);
+    }
   }
   fr others, total;
   fr_group_others<BJJ_SEGS>(acc, others, total);
-  fr inv = fr_mul(fr_inv_sw(total), others);  // = 1 / acc
+  // the workgroup's witness totals inverted together (lane k of wave 0: witness group k; a dead group's total is 1)
+  const int g = (int)(threadIdx.x / BJJ_SEGS);
+  if (seg == 0) s_tot[g] = total;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const fr t = threadIdx.x < NW ? s_tot[threadIdx.x] : fr_mont_one();
+    fr t_others, t_all;
+    fr_group_others<NW>(t, t_others, t_all);
+    const fr t_inv = fr_mul(fr_inv_sw(t_all), t_others);  // = 1 / total of group threadIdx.x
+    if (threadIdx.x < NW) s_tot[threadIdx.x] = t_inv;  // (read above, by this wave only)
+  }
+  __syncthreads();
+  if (!live) return;
+  fr inv = fr_mul(s_tot[g], others);  // = 1 / acc
   fr* out = bjj_core + (size_t)w * L.bjj_core_fr;
   for (int qi = NQ - 1; qi >= 0; qi--) {
     fr e = elem(qi);

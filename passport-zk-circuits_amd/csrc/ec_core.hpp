@@ -848,13 +848,8 @@ __global__ void __launch_bounds__(64) k_ec_link(DevLayout L, const uint8_t* inpu
   }
 }
 
-// Phase 4, lane = (witness, j): IsEqual inverses (genmult dummy tests, scalarMult isZeroResult /
-// isZeroAddition) of the differences in[1] - in[0]; 0 -> 0 (comparators.circom:17)
-__global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_inv, uint32_t batch) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t w = gid / ECG.n_inv;
-  const int j = (int)(gid % ECG.n_inv);
-  if (w >= batch) return;
+// the difference k_ec_inv inverts for (witness w, inverse j), normal form
+__device__ __forceinline__ fr ec_inv_diff(const uint64_t* ec_core, uint32_t w, int j) {
   const uint64_t* C = ec_core + (size_t)w * ECG.core_words;
   const uint64_t dx = EC_D[0];
   fr d;
@@ -868,8 +863,27 @@ __global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_i
   } else {
     d = fr_diff_u64(dx, C[ECG.c_sm_ap + P2 * (j - ECG.i_sm_za + 1)]);
   }
-  ec_inv[(size_t)w * ECG.n_inv + j] = fr_is_zero(d) ? d : fr_from_mont_fast(fr_inv<true>(fr_mul_fast(d, fr_const(R2_))));
+  return d;
 }
+
+// Phase 4, lane = (witness, j): IsEqual inverses (genmult dummy tests, scalarMult isZeroResult /
+// isZeroAddition) of the differences in[1] - in[0]; 0 -> 0 (comparators.circom:17). One batched inversion per wave
+// (the wave's non-zero differences multiplied across it with shuffles, one Fr inversion shared by the 64 lanes;
+// a Fr inversion per lane was 131k VALU per wave, pmc_r4e2).
+__global__ void __launch_bounds__(64) k_ec_inv(const uint64_t* ec_core, fr* ec_inv, uint32_t batch) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = gid / ECG.n_inv;
+  const int j = (int)(gid % ECG.n_inv);
+  const bool live = w < batch;  // a lane past the batch multiplies 1 into the wave's product and stores nothing
+  fr d = fr_zero();
+  if (live) d = ec_inv_diff(ec_core, w, j);
+  const fr a = fr_is_zero(d) ? fr_mont_one() : fr_mul_fast(d, fr_const(R2_));
+  fr others, total;
+  fr_group_others<64>(a, others, total);
+  const fr r = fr_mul_fast(fr_inv<true>(total), others);  // = 1 / a
+  if (live) ec_inv[(size_t)w * ECG.n_inv + j] = fr_is_zero(d) ? d : fr_from_mont_fast(r);
+}
+
 
 // ============================================================ k_ec_table: lane per (witness, op)
 template <int TYPE>

@@ -890,12 +890,15 @@ __global__ void __launch_bounds__(NT) k_emit_mm(DevLayout L, const Work* work, B
 }
 
 // ------------------------------------------------------------------ BabyJubJub steps
-// Two stages. (1) Per ladder step, the twelve distinct field values its 60 signals are drawn
-// from (coordinates, the adder's/doubler's products, the IsZero inverse) are computed once, in
-// normal form, into an LDS record: one thread per (step, value). (2) Every signal is then a
-// select from the record (plus at most one subtraction, which needs no Montgomery form).
+// Two stages. (1) Per ladder step, the fourteen distinct field values its 60 signals are drawn
+// from (coordinates, the adder's/doubler's products, the IsZero inverse, -x1 and -y1) are computed once, in
+// normal form, into an LDS record: one thread per (step, value); five constants follow the records. (2) Every
+// signal is then one read of the record array at an index chosen by integer selects (the choice depends on the
+// step's bit and on x1 = 0: selecting 8-word values per signal instead took ~680 VALU per wave and element).
 // Work items are step-aligned (BJJ_EMIT_STEPS steps each, builder_impl.hpp).
-enum BjjRec { BR_X1, BR_Y1, BR_OX, BR_OY, BR_INV, BR_X1Y2, BR_Y1X2, BR_DELTA, BR_TAU, BR_XYD, BR_DELTAD, BR_TAUD, BR_N };
+enum BjjRec { BR_X1, BR_Y1, BR_OX, BR_OY, BR_INV, BR_X1Y2, BR_Y1X2, BR_DELTA, BR_TAU, BR_XYD, BR_DELTAD, BR_TAUD,
+              BR_NX1, BR_NY1, BR_N };
+enum BjjConst { BC_ZERO, BC_ONE, BC_B8X, BC_B8Y, BC_INVB8X, BC_N };
 
 __device__ __forceinline__ uint32_t bjj_step_of(uint32_t s) { return s < 46 ? 0 : 1 + (s - 46) / 60; }
 __device__ __forceinline__ uint32_t bjj_sig_of(uint32_t i) { return i == 0 ? 0 : 46 + 60 * (i - 1); }
@@ -903,8 +906,9 @@ __device__ __forceinline__ uint32_t bjj_sig_of(uint32_t i) { return i == 0 ? 0 :
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
 // (at most 80 VGPRs: six workgroups per CU, as its LDS allows, instead of five at 88)
 __global__ void __launch_bounds__(256, 6) k_emit_bjj(DevLayout L, const Work* work, Bufs B) {
-  __shared__ fr rec[(BJJ_EMIT_STEPS + 1) * BR_N];
-  __shared__ uint32_t bits[BJJ_EMIT_STEPS + 1];
+  constexpr int CB = (BJJ_EMIT_STEPS + 1) * BR_N;  // the constants' base in rec
+  __shared__ fr rec[CB + BC_N];
+  __shared__ uint32_t bits[BJJ_EMIT_STEPS + 1], zx1[BJJ_EMIT_STEPS + 1];
   const Work wk = work[blockIdx.x];
   const uint32_t w = blockIdx.y;
   const Region R = L.regions[wk.region];
@@ -919,15 +923,20 @@ __global__ void __launch_bounds__(256, 6) k_emit_bjj(DevLayout L, const Work* wo
       int i = base + j;
       bits[j] = fr_bit(sk, 253 - i);
     }
+    if (threadIdx.x < BC_N) {
+      const int c = (int)threadIdx.x;
+      rec[CB + c] = c == BC_ZERO ? fr_zero() : c == BC_ONE ? fr_u64(1) : c == BC_B8X ? fr_const(BJJ_B8X)
+                  : c == BC_B8Y ? fr_const(BJJ_B8Y) : fr_const(BJJ_INV_B8X);
+    }
   }
   __syncthreads();
   // value-major item order: the lanes of a wave compute the same record value for consecutive
-  // steps (one or two branches of the switch per wave instead of all twelve)
+  // steps (one or two branches of the switch per wave instead of all fourteen)
   for (int q = threadIdx.x; q < nrec * BR_N; q += blockDim.x) {
     const int v = q / nrec, j = q - v * nrec, i = base + j;
     const fr* P = core + 5 * i;
     fr r;
-    if (v >= BR_XYD) {  // doubler of step i (doublers[i-1]) over A_{i-1}
+    if (v == BR_XYD || v == BR_DELTAD || v == BR_TAUD) {  // doubler of step i (doublers[i-1]) over A_{i-1}
       if (i == 0) r = fr_zero();
       else {
         fr xp = P[-3], yp = P[-2];  // core + 5(i-1) + 2, + 3
@@ -943,8 +952,10 @@ __global__ void __launch_bounds__(256, 6) k_emit_bjj(DevLayout L, const Work* wo
       fr x1 = i == 0 ? fr_zero() : P[0], y1 = i == 0 ? fr_zero() : P[1];
       fr x2 = bit ? fr_to_mont(fr_const(BJJ_B8X)) : fr_zero(), y2 = bit ? fr_to_mont(fr_const(BJJ_B8Y)) : fr_zero();
       switch (v) {
-        case BR_X1: r = x1; break;
+        case BR_X1: r = x1; zx1[j] = fr_is_zero(x1); break;
         case BR_Y1: r = y1; break;
+        case BR_NX1: r = fr_sub(fr_zero(), x1); break;
+        case BR_NY1: r = fr_sub(fr_zero(), y1); break;
         case BR_INV: r = i == 0 ? fr_zero() : P[4]; break;
         case BR_X1Y2: r = fr_mul_fast(x1, y2); break;
         case BR_Y1X2: r = fr_mul_fast(y1, x2); break;
@@ -955,67 +966,49 @@ __global__ void __launch_bounds__(256, 6) k_emit_bjj(DevLayout L, const Work* wo
     rec[j * BR_N + v] = fr_from_mont_fast(r);
   }
   __syncthreads();
-  const fr B8x = fr_const(BJJ_B8X), B8y = fr_const(BJJ_B8Y), one = fr_u64(1);
   const OutRow out = out_row(L, B.wtns, B.stride, w, R.off + wk.start);
   __shared__ uint4 stage[2 * 256];
   emit_run(out, wk.count, stage, [&](uint32_t q) -> El {
     const uint32_t s = wk.start + q, i = bjj_step_of(s), t = s - bjj_sig_of(i);
     const int j = (int)i - base;
-    const fr* rc = rec + j * BR_N;
-    fr res;
+    const int rc = j * BR_N, rp = rc - BR_N;
+    constexpr int ZERO = CB + BC_ZERO, ONE = CB + BC_ONE;
+    int idx;
     if (t >= 46) {  // doublers[i-1]: out[2] = D_i | in[2] = A_{i-1} | adder out, in1, in2, beta, gamma, delta, tau
-      const fr* rp = rc - BR_N;
-      uint32_t u = t - 46;
-      if (u < 2) res = rc[BR_X1 + u];
-      else if (u < 4) res = rp[BR_OX + u - 2];
-      else if (u < 6) res = rc[BR_X1 + u - 4];
-      else if (u < 10) res = rp[BR_OX + (u & 1)];
-      else if (u < 12) res = rc[BR_XYD];
-      else res = rc[u == 12 ? BR_DELTAD : BR_TAUD];
+      const uint32_t u = t - 46;
+      idx = u < 2 ? rc + BR_X1 + (int)u : u < 4 ? rp + BR_OX + (int)u - 2 : u < 6 ? rc + BR_X1 + (int)u - 4
+          : u < 10 ? rp + BR_OX + (int)(u & 1) : u < 12 ? rc + BR_XYD : rc + (u == 12 ? BR_DELTAD : BR_TAUD);
     } else {
-      const bool bit = bits[j];
-      const fr x1 = rc[BR_X1], y1 = rc[BR_Y1];
-      const fr x2 = bit ? B8x : fr_zero(), y2 = bit ? B8y : fr_zero();
-      const bool z1 = fr_is_zero(x1), z2 = !bit;
-      const fr rawx = (!z1 && !z2) ? rc[BR_OX] : fr_zero(), rawy = (!z1 && !z2) ? rc[BR_OY] : fr_zero();
-      if (t < 2) res = rc[BR_OX + t];
-      else if (t < 4) res = t == 2 ? x1 : y1;
-      else if (t < 6) res = t == 4 ? x2 : y2;
-      else if (t < 9) res = t == 6 ? (z1 ? one : fr_zero()) : t == 7 ? x1 : rc[BR_INV];
-      else if (t < 12) res = t == 9 ? (z2 ? one : fr_zero()) : t == 10 ? x2 : (bit ? fr_const(BJJ_INV_B8X) : fr_zero());
+      const bool bit = bits[j] != 0, z1 = zx1[j] != 0, z2 = !bit;
+      const int x1 = rc + BR_X1, y1 = rc + BR_Y1, x2 = bit ? CB + BC_B8X : ZERO, y2 = bit ? CB + BC_B8Y : ZERO;
+      const int rawx = (!z1 && !z2) ? rc + BR_OX : ZERO, rawy = (!z1 && !z2) ? rc + BR_OY : ZERO;
+      if (t < 2) idx = rc + BR_OX + (int)t;
+      else if (t < 4) idx = t == 2 ? x1 : y1;
+      else if (t < 6) idx = t == 4 ? x2 : y2;
+      else if (t < 9) idx = t == 6 ? (z1 ? ONE : ZERO) : t == 7 ? x1 : rc + BR_INV;
+      else if (t < 12) idx = t == 9 ? (z2 ? ONE : ZERO) : t == 10 ? x2 : (bit ? CB + BC_INVB8X : ZERO);
       else if (t < 22) {  // adder: out[2] | in1[2], in2[2] | beta, gamma, delta, tau
-        uint32_t u = t - 12;
-        if (u < 2) res = u == 0 ? rawx : rawy;
-        else if (u < 4) res = u == 2 ? x1 : y1;
-        else if (u < 6) res = u == 4 ? x2 : y2;
-        else res = rc[BR_X1Y2 + (u - 6)];
+        const uint32_t u = t - 12;
+        idx = u < 2 ? (u == 0 ? rawx : rawy) : u < 4 ? (u == 2 ? x1 : y1) : u < 6 ? (u == 4 ? x2 : y2)
+            : rc + BR_X1Y2 + (int)(u - 6);
       } else {  // switchers L0, R0, L1, R1: out[2] | bool, in[2] | aux
-        uint32_t u = t - 22, sw = u / 6, k = u % 6;
+        const uint32_t u = t - 22, sw = u / 6, k = u % 6;
         const bool cy = (sw >> 1) != 0;
-        const fr raw = cy ? rawy : rawx, in1c = cy ? y1 : x1, in2c = cy ? y2 : x2;
-        const fr l0 = z2 ? in1c : raw, l1 = z2 ? raw : in1c;
+        const int raw = cy ? rawy : rawx, in1c = cy ? y1 : x1, in2c = cy ? y2 : x2;
+        const int l0 = z2 ? in1c : raw, l1 = z2 ? raw : in1c;
         if ((sw & 1) == 0) {
-          switch (k) {
-            case 0: res = l0; break;
-            case 1: res = l1; break;
-            case 2: res = z2 ? one : fr_zero(); break;
-            case 3: res = raw; break;
-            case 4: res = in1c; break;
-            default: res = z2 ? fr_sub(in1c, raw) : fr_zero(); break;
-          }
+          // aux = z2 ? in1c - raw : 0, and raw = 0 when z2
+          idx = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? (z2 ? ONE : ZERO) : k == 3 ? raw : k == 4 ? in1c
+              : (z2 ? in1c : ZERO);
         } else {
-          switch (k) {
-            case 0: res = z1 ? in2c : l0; break;
-            case 1: res = z1 ? l0 : in2c; break;
-            case 2: res = z1 ? one : fr_zero(); break;
-            case 3: res = l0; break;
-            case 4: res = in2c; break;
-            default: res = z1 ? fr_sub(in2c, l0) : fr_zero(); break;
-          }
+          // aux = z1 ? in2c - l0 : 0; with z1, raw = 0, so l0 = (z2 ? in1c : 0) and in2c = (z2 ? 0 : in2c)
+          const int aux = !z1 ? ZERO : z2 ? rc + (cy ? BR_NY1 : BR_NX1) : in2c;
+          idx = k == 0 ? (z1 ? in2c : l0) : k == 1 ? (z1 ? l0 : in2c) : k == 2 ? (z1 ? ONE : ZERO) : k == 3 ? l0
+              : k == 4 ? in2c : aux;
         }
       }
     }
-    return el_fr(res);
+    return el_fr(rec[idx]);
   });
 }
 #endif

@@ -281,12 +281,20 @@ __device__ __forceinline__ fr pos_perm_group(const KC& K, fr st, fr* out, int j)
   return group_sum(act ? PM::mul(K.M(t, jj, 0), pow5p<PM>(st)) : fr_zero());  // every lane of the group: the hash
 }
 
+// The product of the narrow-level Poseidon cores and the BabyJubJub core (round 6): FIPS, the throughput product —
+// the lines those cores sit on are VALU-bound; -DPZK_CORE_CIOS builds the latency product (A/B).
+#ifdef PZK_CORE_CIOS
+using CoreMul = FrMulInline;
+#else
+using CoreMul = FrMulFips;
+#endif
+
 template <int T, int G>
 __device__ __forceinline__ fr pos_core_group(const PosConsts& K, const PosTask& task, const ValueStore& vs, uint32_t w,
                                                fr* core /* this witness's Poseidon core */, int j) {
   fr in = fr_zero();
   if (j > 0 && j < T) in = vs.at(task.in_slot[j - 1], w);
-  const fr h = pos_perm_group<T, G>(K, in, core + task.core_off, j);
+  const fr h = pos_perm_group<T, G, PosConsts, CoreMul>(K, in, core + task.core_off, j);
   if (j == 0) vs.at(task.out_slot, w) = h;
   return h;  // every lane of the group holds the hash (Montgomery)
 }

@@ -512,21 +512,23 @@ __global__ void __launch_bounds__(64) k_rsa_check(DevLayout L, const uint8_t* in
 // twisted Edwards a x^2 + y^2 = 1 + d x^2 y^2, a = 168700, d = 168696 (babyjubjub/curve.circom:62-70)
 struct ExtPt { fr X, Y, Z, T; };
 
+template <class PM = FrMulInline>
 __device__ __forceinline__ ExtPt bjj_dbl(const ExtPt& P, const fr& A) {  // dbl-2008-hwcd
-  fr a = fr_sqr(P.X), b = fr_sqr(P.Y), c = fr_sqr(P.Z);
+  fr a = PM::sqr(P.X), b = PM::sqr(P.Y), c = PM::sqr(P.Z);
   c = fr_add(c, c);
-  fr d = fr_mul(A, a);
+  fr d = PM::mul(A, a);
   fr xy = fr_add(P.X, P.Y);
-  fr e = fr_sub(fr_sub(fr_sqr(xy), a), b);
+  fr e = fr_sub(fr_sub(PM::sqr(xy), a), b);
   fr g = fr_add(d, b), f = fr_sub(g, c), h = fr_sub(d, b);
-  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+  return ExtPt{PM::mul(e, f), PM::mul(g, h), PM::mul(f, g), PM::mul(e, h)};
 }
+template <class PM = FrMulInline>
 __device__ __forceinline__ ExtPt bjj_add_affine(const ExtPt& P, const fr& x2, const fr& y2, const fr& t2d, const fr& A) {
   // add-2008-hwcd with Z2 = 1, t2d = d * x2 * y2
-  fr a = fr_mul(P.X, x2), b = fr_mul(P.Y, y2), c = fr_mul(P.T, t2d), d = P.Z;
-  fr e = fr_sub(fr_sub(fr_mul(fr_add(P.X, P.Y), fr_add(x2, y2)), a), b);
-  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, fr_mul(A, a));
-  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+  fr a = PM::mul(P.X, x2), b = PM::mul(P.Y, y2), c = PM::mul(P.T, t2d), d = P.Z;
+  fr e = fr_sub(fr_sub(PM::mul(fr_add(P.X, P.Y), fr_add(x2, y2)), a), b);
+  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, PM::mul(A, a));
+  return ExtPt{PM::mul(e, f), PM::mul(g, h), PM::mul(f, g), PM::mul(e, h)};
 }
 
 // Base8 (babyjubjub/get.circom:9-10), normal form; 1/Base8.x (IsZero of adders' in2)
@@ -566,11 +568,12 @@ struct BjjConsts {
 
 // Fixed-base table for the segment start points: T[w][v] = v * 2^(8w) * Base8, w < 32, v < 256,
 // affine (x, y) and t2d = d*x*y, Montgomery form. Built once per instance (k_bjj_table).
+template <class PM = FrMulInline>
 __device__ __forceinline__ ExtPt bjj_add(const ExtPt& P, const ExtPt& Q, const BjjConsts& C) {  // add-2008-hwcd
-  fr a = fr_mul(P.X, Q.X), b = fr_mul(P.Y, Q.Y), c = fr_mul(fr_mul(P.T, C.D), Q.T), d = fr_mul(P.Z, Q.Z);
-  fr e = fr_sub(fr_sub(fr_mul(fr_add(P.X, P.Y), fr_add(Q.X, Q.Y)), a), b);
-  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, fr_mul(C.A, a));
-  return ExtPt{fr_mul(e, f), fr_mul(g, h), fr_mul(f, g), fr_mul(e, h)};
+  fr a = PM::mul(P.X, Q.X), b = PM::mul(P.Y, Q.Y), c = PM::mul(PM::mul(P.T, C.D), Q.T), d = PM::mul(P.Z, Q.Z);
+  fr e = fr_sub(fr_sub(PM::mul(fr_add(P.X, P.Y), fr_add(Q.X, Q.Y)), a), b);
+  fr f = fr_sub(d, c), g = fr_add(d, c), h = fr_sub(b, PM::mul(C.A, a));
+  return ExtPt{PM::mul(e, f), PM::mul(g, h), PM::mul(f, g), PM::mul(e, h)};
 }
 
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
@@ -598,6 +601,7 @@ __global__ void __launch_bounds__(256) k_bjj_table(fr* table) {
 
 // segment start of the ladder below: A_{i0-1} = p * Base8, p = sk >> (254 - i0) (an i0-bit prefix), summed from the
 // fixed-base table (8-bit windows; the top window of a prefix may be partial)
+template <class PM = FrMulInline>
 __device__ __forceinline__ void bjj_seg_start(const fr& sk, int i0, const fr* table, const BjjConsts& C, bool& have,
                                               ExtPt& A) {
   have = false;
@@ -607,8 +611,8 @@ __device__ __forceinline__ void bjj_seg_start(const fr& sk, int i0, const fr* ta
     for (int b = 0; b < 8 && 8 * wi + b < i0; b++) v |= fr_bit(sk, 254 - i0 + 8 * wi + b) << b;
     if (!v) continue;
     const fr* e = table + 3 * (size_t)(wi * 256 + v);
-    if (!have) { A = ExtPt{e[0], e[1], fr_mont_one(), fr_mul(e[0], e[1])}; have = true; }
-    else A = bjj_add_affine(A, e[0], e[1], e[2], C.A);
+    if (!have) { A = ExtPt{e[0], e[1], fr_mont_one(), PM::mul(e[0], e[1])}; have = true; }
+    else A = bjj_add_affine<PM>(A, e[0], e[1], e[2], C.A);
   }
 }
 // The same start points with the table additions of each lane pair (seg, SEGS - 1 - seg) balanced: prefix lengths grow
@@ -616,7 +620,7 @@ __device__ __forceinline__ void bjj_seg_start(const fr& sk, int i0, const fr* ta
 // over (a wave shuffle and one general addition): a lane's additions go from up to SEGS - 1 windows (SEGS = 32: 31)
 // to about half. The sums start from the identity (0 : 1 : 1 : 0) — the addition law is complete on BabyJubJub
 // (a a square, d not) — so Z differs from bjj_seg_start's but the affine point and `have` do not.
-template <int SEGS, int SEG_LEN>
+template <int SEGS, int SEG_LEN, class PM = FrMulInline>
 __device__ __forceinline__ void bjj_seg_start_paired(const fr& sk, int seg, const fr* table, const BjjConsts& C,
                                                      bool& have, ExtPt& A) {
   static_assert(SEGS % 2 == 0 && SEG_LEN % 8 == 0, "lane pairs of whole windows");
@@ -637,7 +641,7 @@ __device__ __forceinline__ void bjj_seg_start_paired(const fr& sk, int seg, cons
     for (int b = 0; b < 8; b++) v |= fr_bit(sk, 254 - i0x + 8 * wi + b) << b;
     if (!v) continue;
     const fr* e = table + 3 * (size_t)(wi * 256 + v);
-    const ExtPt cur = bjj_add_affine(mine ? Ao : Ah, e[0], e[1], e[2], C.A);
+    const ExtPt cur = bjj_add_affine<PM>(mine ? Ao : Ah, e[0], e[1], e[2], C.A);
     if (mine) { Ao = cur; ho = true; }
     else { Ah = cur; hh = true; }
   }
@@ -645,7 +649,7 @@ __device__ __forceinline__ void bjj_seg_start_paired(const fr& sk, int seg, cons
   const ExtPt got{xo(Ah.X), xo(Ah.Y), xo(Ah.Z), xo(Ah.T)};
   const bool gh = __shfl_xor((int)hh, SEGS - 1, 64) != 0;
   if (!helper && gh) {
-    Ao = ho ? bjj_add(Ao, got, C) : got;
+    Ao = ho ? bjj_add<PM>(Ao, got, C) : got;
     ho = true;
   }
   have = ho;
@@ -653,14 +657,15 @@ __device__ __forceinline__ void bjj_seg_start_paired(const fr& sk, int seg, cons
 }
 // ladder step i (curve.circom:156-168): D_i = 2 A_{i-1} when A_{i-1} exists (the (0,0) sentinel otherwise: D = 0),
 // A_i = D_i + Base8 when bit 253 - i of sk is set, else D_i
+template <class PM = FrMulInline>
 __device__ __forceinline__ void bjj_step(const fr& sk, int i, const BjjConsts& C, bool& have, ExtPt& A, bool& haveD,
                                          ExtPt& D) {
   const uint32_t bit = fr_bit(sk, 253 - i);
   haveD = i > 0 && have;
-  D = haveD ? bjj_dbl(A, C.A) : ExtPt{fr_zero(), fr_zero(), fr_zero(), fr_zero()};
+  D = haveD ? bjj_dbl<PM>(A, C.A) : ExtPt{fr_zero(), fr_zero(), fr_zero(), fr_zero()};
   if (bit) {
-    if (haveD) A = bjj_add_affine(D, C.B8x, C.B8y, C.B8t_d, C.A);
-    else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = fr_mul(C.B8x, C.B8y); }
+    if (haveD) A = bjj_add_affine<PM>(D, C.B8x, C.B8y, C.B8t_d, C.A);
+    else { A.X = C.B8x; A.Y = C.B8y; A.Z = fr_mont_one(); A.T = PM::mul(C.B8x, C.B8y); }
     have = true;
   } else {
     if (haveD) A = D;
@@ -711,13 +716,13 @@ __global__ void __launch_bounds__(64 * BJJ_WG_WAVES) k_bjj_core(DevLayout L, Val
     const fr sk = fr_from_mont(vs.at(L.reg.v_sk, w));
     bool have;
     ExtPt A;
-    if (paired) bjj_seg_start_paired<BJJ_SEGS, BJJ_SEG_LEN>(sk, seg, table, C, have, A);
-    else bjj_seg_start(sk, i0, table, C, have, A);
+    if (paired) bjj_seg_start_paired<BJJ_SEGS, BJJ_SEG_LEN, CoreMul>(sk, seg, table, C, have, A);
+    else bjj_seg_start<CoreMul>(sk, i0, table, C, have, A);
     // projective coords of D_i (local elems 0..3ns) and A_i (3ns..6ns): [X, Y, Z] per step
     for (int j = 0; j < ns; j++) {
       ExtPt D;
       bool haveD;
-      bjj_step(sk, i0 + j, C, have, A, haveD, D);
+      bjj_step<CoreMul>(sk, i0 + j, C, have, A, haveD, D);
       if (haveD) { S(3 * j) = D.X; S(3 * j + 1) = D.Y; S(3 * j + 2) = D.Z; }
       else { S(3 * j) = fr_zero(); S(3 * j + 1) = fr_zero(); S(3 * j + 2) = fr_zero(); }
       const int o = 3 * BJJ_SEG_LEN + 3 * j;
@@ -727,7 +732,7 @@ __global__ void __launch_bounds__(64 * BJJ_WG_WAVES) k_bjj_core(DevLayout L, Val
     for (int qi = 0; qi < NQ; qi++) {
       fr e = elem(qi);
       S(PRE + qi) = acc;
-      if (!fr_is_zero(e)) acc = fr_mul(acc, e);
+      if (!fr_is_zero(e)) acc = CoreMul::mul(acc, e);
     }
   }
   fr others, total;
@@ -750,12 +755,12 @@ __global__ void __launch_bounds__(64 * BJJ_WG_WAVES) k_bjj_core(DevLayout L, Val
   for (int qi = NQ - 1; qi >= 0; qi--) {
     fr e = elem(qi);
     fr r = fr_zero();
-    if (!fr_is_zero(e)) { r = fr_mul(inv, S(PRE + qi)); inv = fr_mul(inv, e); }
+    if (!fr_is_zero(e)) { r = CoreMul::mul(inv, S(PRE + qi)); inv = CoreMul::mul(inv, e); }
     const int j = qi / 3, kind = qi - 3 * j;
     fr* o = out + 5 * (i0 + j);  // Dx, Dy, Ax, Ay, inv(Dx)
-    if (kind == 0) { o[0] = fr_mul(S(3 * j), r); o[1] = fr_mul(S(3 * j + 1), r); }
-    else if (kind == 1) { o[2] = fr_mul(S(3 * BJJ_SEG_LEN + 3 * j), r); o[3] = fr_mul(S(3 * BJJ_SEG_LEN + 3 * j + 1), r); }
-    else { o[4] = fr_mul(S(3 * j + 2), r); }  // 1/x = Z / X
+    if (kind == 0) { o[0] = CoreMul::mul(S(3 * j), r); o[1] = CoreMul::mul(S(3 * j + 1), r); }
+    else if (kind == 1) { o[2] = CoreMul::mul(S(3 * BJJ_SEG_LEN + 3 * j), r); o[3] = CoreMul::mul(S(3 * BJJ_SEG_LEN + 3 * j + 1), r); }
+    else { o[4] = CoreMul::mul(S(3 * j + 2), r); }  // 1/x = Z / X
   }
   if (i1 == NS) {
     vs.at(L.reg.v_bjj, w) = out[5 * (NS - 1) + 2];

@@ -393,8 +393,9 @@ bool bjj_uses_scratch() {
 
 hipError_t launch_smt_prep(const DevLayout& L, const uint8_t* inputs, ValueStore vs, fr* smt_core, int32_t* status,
                            hipStream_t st) {
-  hipLaunchKernelGGL(k_smt_prep, dim3((vs.batch * SMT_PREP_LANES + 63) / 64), dim3(64), 0, st, L, inputs, vs, smt_core, status,
-                     vs.batch);
+  const uint32_t wg = 64 * SMT_PREP_WAVES;
+  hipLaunchKernelGGL(k_smt_prep, dim3((vs.batch * SMT_PREP_LANES + wg - 1) / wg), dim3(wg), 0, st, L, inputs, vs, smt_core,
+                     status, vs.batch);
   return hipGetLastError();
 }
 

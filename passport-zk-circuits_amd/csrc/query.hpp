@@ -332,18 +332,28 @@ __global__ void __launch_bounds__(64 * QP_WAVES) k_qry_prep(DevLayout L, const u
   const uint64_t cit = f64[q_f_cit(td1)];
   int first = 240;
   fr d[4], pre[4];
-  fr acc = fr_mont_one();
+  // (run before and after the workgroup's inversion: arrays kept across its barriers went to scratch)
+  auto forward = [&]() {
+    fr a = fr_mont_one();
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = lane + 64 * j;
+      const bool has = i < 240;
+      const uint32_t ci = has ? Q_COUNTRY[i] : 0u;
+      d[j] = has ? fr_to_mont(fr_sdiff(cit, ci)) : fr_zero();
+      pre[j] = a;
+      if (!fr_is_zero(d[j])) a = fr_mul(a, d[j]);
+    }
+    return a;
+  };
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int i = lane + 64 * j;
     const bool has = i < 240;
-    const uint32_t ci = has ? Q_COUNTRY[i] : 0u;
-    const uint64_t m = __ballot(has && ci == cit);
+    const uint64_t m = __ballot(has && (has ? Q_COUNTRY[i] : 0u) == cit);
     if (m && first == 240) first = 64 * j + __builtin_ctzll(m);
-    d[j] = has ? fr_to_mont(fr_sdiff(cit, ci)) : fr_zero();
-    pre[j] = acc;
-    if (!fr_is_zero(d[j])) acc = fr_mul(acc, d[j]);
   }
+  const fr acc = forward();
   fr others, total;
   fr_group_others<64>(acc, others, total);
   // the workgroup's totals inverted together: lane k of wave 0 holds wave k's total (a lane past QP_WAVES one)
@@ -359,6 +369,7 @@ __global__ void __launch_bounds__(64 * QP_WAVES) k_qry_prep(DevLayout L, const u
   __syncthreads();
   if (!live) return;
   fr inv = fr_mul(s_tot[wv], others);  // = 1 / acc
+  forward();
 #pragma unroll
   for (int j = 3; j >= 0; j--) {
     const int i = lane + 64 * j;

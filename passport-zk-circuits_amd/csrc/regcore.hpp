@@ -385,22 +385,22 @@ __global__ void __launch_bounds__(64 * RI_WAVES) k_rsa_inv(DevLayout L, const ui
       if (e < e1) {
         const fr d = diff(e);
         pr[J()] = acc;  // exclusive prefix within the run
-        if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+        if (!fr_is_zero(d)) acc = fr_mul_fast(acc, d);
       }
     });
   } else {
     for (int e = e0; e < e1; e++) {
       const fr d = diff(e);
       store_fr(slot(e), acc);
-      if (!fr_is_zero(d)) acc = fr_mul(acc, d);
+      if (!fr_is_zero(d)) acc = fr_mul_fast(acc, d);
     }
   }
   // exclusive prefix / suffix products of the run products across the wave (log-step scans)
   fr incl = acc, sincl = acc;
   for (int d = 1; d < 64; d <<= 1) {
     fr a = fr_shfl_up(incl, d), b = fr_shfl_down(sincl, d);
-    if (lane >= d) incl = fr_mul(incl, a);
-    if (lane + d < 64) sincl = fr_mul(sincl, b);
+    if (lane >= d) incl = fr_mul_fast(incl, a);
+    if (lane + d < 64) sincl = fr_mul_fast(sincl, b);
   }
   fr pre = fr_shfl_up(incl, 1), suf = fr_shfl_down(sincl, 1);
   if (lane == 0) pre = fr_mont_one();
@@ -412,17 +412,17 @@ __global__ void __launch_bounds__(64 * RI_WAVES) k_rsa_inv(DevLayout L, const ui
     const fr t = lane < RI_WAVES ? s_tot[lane] : fr_mont_one();
     fr t_others, t_all;
     fr_group_others<RI_WAVES>(t, t_others, t_all);
-    const fr t_inv = fr_mul(fr_inv(t_all), t_others);  // = 1 / total of wave `lane`
+    const fr t_inv = fr_mul_fast(fr_inv<true>(t_all), t_others);  // = 1 / total of wave `lane`
     if (lane < RI_WAVES) s_tot[lane] = t_inv;  // (read above, by this wave only)
   }
   __syncthreads();
-  fr inv = fr_mul(fr_mul(s_tot[wv], pre), suf);  // = 1 / (this run's product)
+  fr inv = fr_mul_fast(fr_mul_fast(s_tot[wv], pre), suf);  // = 1 / (this run's product)
   if (!in_reg) {
     if (!live) return;
     for (int e = e1 - 1; e >= e0; e--) {
       const fr d = diff(e);
       fr r = fr_zero();
-      if (!fr_is_zero(d)) { r = fr_mul(inv, load_fr(slot(e))); inv = fr_mul(inv, d); }
+      if (!fr_is_zero(d)) { r = fr_mul_fast(inv, load_fr(slot(e))); inv = fr_mul_fast(inv, d); }
       store_fr(slot(e), fr_from_mont(r));
     }
     return;
@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(64 * RI_WAVES) k_rsa_inv(DevLayout L, const ui
     if (e < e1) {
       const fr d = diff(e);
       fr r = fr_zero();
-      if (!fr_is_zero(d)) { r = fr_mul(inv, pr[j]); inv = fr_mul(inv, d); }
+      if (!fr_is_zero(d)) { r = fr_mul_fast(inv, pr[j]); inv = fr_mul_fast(inv, d); }
       pr[j] = fr_from_mont(r);
     }
   });
@@ -854,17 +854,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PZK_BJJ
 // are one batched inversion per witness (segment prefix products per lane, the segment totals
 // combined by shuffles, one Fr inversion shared by the group, as in k_bjj_core); the SMTLevIns /
 // SMTVerifierSM chains are integer recurrences over the 80 isZero bits, which every lane of the
-// group rebuilds from the gathered bit mask and writes for its own levels.
+// group rebuilds from the gathered bit mask and writes for its own levels. The workgroup's SMT_PREP_WAVES * 64 / G
+// witness totals are inverted together by wave 0 (round 6), with FIPS products.
+constexpr int SMT_PREP_WAVES = 4;
 #ifndef PZK_TEMPLATE_KERNELS_ONLY  // defined once, in kernels.hip
-__global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs, fr* smt_core,
-                                                int32_t* status, uint32_t batch) {
+__global__ void __launch_bounds__(64 * SMT_PREP_WAVES) k_smt_prep(DevLayout L, const uint8_t* inputs, ValueStore vs,
+                                                                 fr* smt_core, int32_t* status, uint32_t batch) {
   core_priority();
-  constexpr int G = SMT_PREP_LANES, NL = SMT_LEVELS / SMT_PREP_LANES;
+  constexpr int G = SMT_PREP_LANES, NL = SMT_LEVELS / SMT_PREP_LANES, NW = 64 * SMT_PREP_WAVES / SMT_PREP_LANES;
   static_assert(SMT_LEVELS % SMT_PREP_LANES == 0 && 64 % SMT_PREP_LANES == 0 && NL <= 32, "level split");
+  static_assert(NW <= 64 && (NW & (NW - 1)) == 0, "the workgroup's witness totals: one per lane of wave 0");
+  __shared__ fr s_tot[NW];
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t w = tid / G;
+  const uint32_t w0 = tid / G;
   const int seg = (int)(tid % G), i0 = seg * NL;
-  if (w >= batch) return;  // whole lane groups only
+  const bool live = w0 < batch;  // a lane group past the batch takes part in the barriers only, and stores nothing
+  const uint32_t w = live ? w0 : batch - 1;
   const RegInfo& R = L.reg;
   const uint8_t* row = inputs + 32ull * (uint64_t)w * L.n_inputs;
   fr* core = smt_core + (size_t)w * L.smt_core_fr;
@@ -873,23 +878,43 @@ __global__ void __launch_bounds__(64) k_smt_prep(DevLayout L, const uint8_t* inp
   // inverses of the siblings (SMTLevIns isZero, SMTVerifier.circom:47-50), batched
   fr sm[NL];
   uint32_t zmask = 0;  // bit k: sibling i0 + k is zero
-  fr acc = fr_mont_one();
+  // (the forward pass runs twice, before and after the workgroup's inversion: arrays kept across its barriers and its
+  // register-hungry inversion went to scratch)
+  auto forward = [&](bool park) {  // park: the exclusive prefixes go to the inverse slots (read back below)
+    fr a = fr_mont_one();
 #pragma unroll
-  for (int k = 0; k < NL; k++) {
-    const fr sn = load_fr(row + 32ull * (R.in_br + i0 + k));
-    const bool z = fr_is_zero(sn);
-    zmask |= (uint32_t)z << k;
-    sm[k] = fr_to_mont(sn);
-    core[i0 + k] = acc;
-    if (!z) acc = fr_mul(acc, sm[k]);
-  }
+    for (int k = 0; k < NL; k++) {
+      const fr sn = load_fr(row + 32ull * (R.in_br + i0 + k));
+      const bool z = fr_is_zero(sn);
+      zmask |= (uint32_t)z << k;
+      sm[k] = fr_to_mont(sn);
+      if (park) core[i0 + k] = a;
+      if (!z) a = fr_mul_fast(a, sm[k]);
+    }
+    return a;
+  };
+  const fr acc = live ? forward(false) : fr_mont_one();
   fr others, total;
   fr_group_others<G>(acc, others, total);
-  fr inv = fr_mul(fr_inv_sw(total), others);  // = 1 / acc
+  const int g = (int)(threadIdx.x / G);
+  if (seg == 0) s_tot[g] = total;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const fr t = threadIdx.x < NW ? s_tot[threadIdx.x] : fr_mont_one();
+    fr t_others, t_all;
+    fr_group_others<NW>(t, t_others, t_all);
+    const fr t_inv = fr_mul_fast(fr_inv_sw<true>(t_all), t_others);  // = 1 / total of group threadIdx.x
+    if (threadIdx.x < NW) s_tot[threadIdx.x] = t_inv;  // (read above, by this wave only)
+  }
+  __syncthreads();
+  if (!live) return;
+  fr inv = fr_mul_fast(s_tot[g], others);  // = 1 / acc
+  zmask = 0;
+  forward(true);
 #pragma unroll
   for (int k = NL - 1; k >= 0; k--) {
     fr r = fr_zero();
-    if (!((zmask >> k) & 1)) { r = fr_mul(inv, core[i0 + k]); inv = fr_mul(inv, sm[k]); }
+    if (!((zmask >> k) & 1)) { r = fr_mul_fast(inv, core[i0 + k]); inv = fr_mul_fast(inv, sm[k]); }
     core[i0 + k] = fr_from_mont(r);
   }
   // the group's isZero bits, levels 0..79

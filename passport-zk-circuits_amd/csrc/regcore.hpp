@@ -334,7 +334,10 @@ __global__ void __launch_bounds__(NL) k_rsa_core(DevLayout L, const uint8_t* inp
 // elements; the run products are combined across the wave with shuffles, and the wave totals of the workgroup's
 // RI_WAVES witnesses are inverted together by wave 0 (one Fr inversion per wave was ~85 % of the kernel's VALU).
 // Output: normal form, in each BigMultModP's inv slots.
-constexpr int RI_WAVES = 8;
+#ifndef PZK_RI_WAVES  // witnesses (waves) per k_rsa_inv workgroup (A/B builds)
+#define PZK_RI_WAVES 8
+#endif
+constexpr int RI_WAVES = PZK_RI_WAVES;
 // f(integral_constant<int, J>) for J = J0 .. N - 1, unrolled by construction (register arrays indexed by J stay in
 // registers; a #pragma unroll of the same loop leaves them in scratch once the body is large)
 template <int J, int N, class F>
